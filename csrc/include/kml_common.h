@@ -1,0 +1,58 @@
+// kml_common.h — shared device/host helpers for the kubeml_amd HIP kernels.
+//
+// Target: gfx950 (MI355X, CDNA4) only.  Wave64 everywhere; bf16 is handled as raw
+// 16-bit payloads (ushort) with explicit round-to-nearest-even conversion so that
+// every kernel controls its own vector widths (16 B per lane on the hot loads).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KML_API extern "C" __attribute__((visibility("default")))
+
+#define KML_WAVE 64
+
+typedef unsigned short bf16_t;  // raw bf16 bits
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 MFMA accumulator
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+// round-to-nearest-even; NaN stays NaN (quiet bit forced)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float lo_bf(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// grid sizing for streaming kernels: cap at 256 CUs x 8 blocks, grid-stride the rest
+static inline unsigned kml_stream_grid(long long n_items, int block) {
+  long long g = (n_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+#define KML_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -1,0 +1,293 @@
+// bn.hip — BatchNorm2d (NHWC, bf16 activations, fp32 statistics) for gfx950.
+//
+// Training forward is split as   conv(+stats epilogue)  ->  bn_apply
+// so the per-channel sum / sum-of-squares come for free from the producing GEMM
+// (conv_igemm.hip).  kml_bn_stats exists for inputs that were not produced by our
+// conv (user models).  bn_apply fuses: normalisation, affine, optional residual
+// add and optional ReLU, plus the running-stat update (momentum, unbiased var) and
+// the saved mean / inv-std used by backward.
+//
+// Backward is two streaming passes:
+//   bn_bwd_reduce : dz = dy * [y > 0] (if ReLU);  dbeta += sum dz,  dgamma += sum dz*xhat
+//                   (accumulated straight into the flat fp32 gradient buffer)
+//   bn_bwd_apply  : dx = gamma*rstd*(dz - (dbeta + xhat*dgamma)/M), and optionally
+//                   dres = dz (gradient of the residual branch).
+// All loads are 16 B per lane (8 channels), C % 8 == 0.
+//
+// Reference parity: torch.nn.BatchNorm2d semantics (momentum 0.1, eps 1e-5, biased
+// batch variance for normalisation, unbiased for the running estimate), which the
+// reference gets from cuDNN through torchvision resnet34 (function_resnet34.py:101).
+#include "kml_common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack_bf2(f[0], f[1]); v.y = pack_bf2(f[2], f[3]);
+  v.z = pack_bf2(f[4], f[5]); v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+// column sums over an [M][C] bf16 matrix: out[0..C) += sum x, out[C..2C) += sum x^2
+// Each thread owns one 8-channel chunk; threads sharing a chunk are reduced in LDS.
+__global__ __launch_bounds__(TPB) void k_bn_stats(const bf16_t* __restrict__ x, float* __restrict__ stats,
+                                                  long long M, int C) {
+  const int CH = C / 8;                 // chunks per row
+  const int rows_per_iter = TPB / CH;   // CH <= 256 assumed (C <= 2048)
+  const int tid = threadIdx.x;
+  const int chunk = tid % CH, rsub = tid / CH;
+  float s1[8] = {0}, s2[8] = {0};
+  if (rsub < rows_per_iter) {
+    for (long long r = (long long)blockIdx.x * rows_per_iter + rsub; r < M;
+         r += (long long)gridDim.x * rows_per_iter) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + r * C + chunk * 8), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s1[i] += f[i]; s2[i] += f[i] * f[i]; }
+    }
+  }
+  __shared__ float red[TPB][17];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
+  __syncthreads();
+  if (tid < CH) {
+    float a1[8] = {0}, a2[8] = {0};
+    for (int rr = 0; rr < rows_per_iter; ++rr) {
+      const int t = rr * CH + tid;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a1[i] += red[t][i]; a2[i] += red[t][8 + i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(stats + tid * 8 + i, a1[i]);
+      atomicAdd(stats + C + tid * 8 + i, a2[i]);
+    }
+  }
+}
+
+// y = act((x - mean) * rstd * gamma + beta [+ res])
+// mode 0: training (stats = [sum, sumsq] over M rows); mode 1: eval (running stats)
+__global__ __launch_bounds__(TPB) void k_bn_apply(
+    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
+    float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C]
+  float* scale = sh;
+  float* shift = sh + C;
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    float mean, var;
+    if (mode == 0) {
+      mean = stats[c] / (float)M;
+      var = fmaxf(stats[C + c] / (float)M - mean * mean, 0.f);
+    } else {
+      mean = run_mean[c];
+      var = run_var[c];
+    }
+    const float rstd = rsqrtf(var + eps);
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    scale[c] = g * rstd;
+    shift[c] = bb - mean * g * rstd;
+    if (mode == 0 && blockIdx.x == 0) {
+      if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
+      if (run_mean) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+      }
+    }
+  }
+  __syncthreads();
+  const long long n8 = M * C / 8;
+  const int CH = C / 8;
+  for (long long i = blockIdx.x * (long long)TPB + threadIdx.x; i < n8; i += (long long)gridDim.x * TPB) {
+    const int c0 = (int)(i % CH) * 8;
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+    float r[8];
+    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = f[k] * scale[c0 + k] + shift[c0 + k];
+      if (res) v += r[k];
+      if (relu) v = fmaxf(v, 0.f);
+      f[k] = v;
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+// dz = dy * [y>0];  dbeta += sum dz;  dgamma += sum dz * (x - mean) * rstd
+__global__ __launch_bounds__(TPB) void k_bn_bwd_reduce(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, long long M, int C) {
+  const int CH = C / 8;
+  const int rows_per_iter = TPB / CH;
+  const int tid = threadIdx.x;
+  const int chunk = tid % CH, rsub = tid / CH;
+  float sd[8] = {0}, sx[8] = {0}, mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mu[i] = mean[chunk * 8 + i]; rs[i] = rstd[chunk * 8 + i]; }
+  if (rsub < rows_per_iter) {
+    for (long long r = (long long)blockIdx.x * rows_per_iter + rsub; r < M;
+         r += (long long)gridDim.x * rows_per_iter) {
+      const long long off = r * C + chunk * 8;
+      float d[8], xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + off), d);
+      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+      if (y) {
+        float yv[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sd[i] += d[i]; sx[i] += d[i] * (xv[i] - mu[i]) * rs[i]; }
+    }
+  }
+  __shared__ float red[TPB][17];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = sd[i]; red[tid][8 + i] = sx[i]; }
+  __syncthreads();
+  if (tid < CH) {
+    float a1[8] = {0}, a2[8] = {0};
+    for (int rr = 0; rr < rows_per_iter; ++rr) {
+      const int t = rr * CH + tid;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a1[i] += red[t][i]; a2[i] += red[t][8 + i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      atomicAdd(dbeta + tid * 8 + i, a1[i]);
+      atomicAdd(dgamma + tid * 8 + i, a2[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_bn_bwd_apply(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ dgamma, const float* __restrict__ dbeta, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dres, long long M, int C) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // a[C], b[C], mu[C], rs[C]
+  float* ka = sh;          // gamma*rstd
+  float* kb = sh + C;      // dbeta/M
+  float* kc = sh + 2 * C;  // dgamma/M
+  float* mu = sh + 3 * C;
+  float* rs = sh + 4 * C;
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    const float g = gamma ? gamma[c] : 1.f;
+    ka[c] = g * rstd[c];
+    kb[c] = dbeta[c] * invM;
+    kc[c] = dgamma[c] * invM;
+    mu[c] = mean[c];
+    rs[c] = rstd[c];
+  }
+  __syncthreads();
+  const long long n8 = M * C / 8;
+  const int CH = C / 8;
+  for (long long i = blockIdx.x * (long long)TPB + threadIdx.x; i < n8; i += (long long)gridDim.x * TPB) {
+    const int c0 = (int)(i % CH) * 8;
+    float d[8], xv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    if (y) {
+      float yv[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+    }
+    if (dres) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float xh = (xv[k] - mu[c]) * rs[c];
+      o[k] = ka[c] * (d[k] - kb[c] - xh * kc[c]);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
+// relu backward alone: dx = dy * [y > 0]  (bf16, x8)
+__global__ void k_relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                           bf16_t* __restrict__ dx, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float d[8], yv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+    reinterpret_cast<uint4*>(dx)[i] = pack8(d);
+  }
+}
+
+__global__ void k_relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+unsigned rows_grid(long long M, int C) {
+  const int rpi = TPB / (C / 8);
+  long long g = (M + rpi * 8 - 1) / (rpi * 8);  // >= 8 rows per thread
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+KML_API int kml_bn_stats(const bf16_t* x, float* stats, long long M, int C, hipStream_t s) {
+  if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_stats, dim3(rows_grid(M, C)), dim3(TPB), 0, s, x, stats, M, C);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_bn_apply(const bf16_t* x, const float* stats, const float* gamma, const float* beta,
+                         const bf16_t* res, bf16_t* y, float* save_mean, float* save_rstd, float* run_mean,
+                         float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
+                         hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 2 * C * sizeof(float), s,
+                     x, stats, gamma, beta, res, y, save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum,
+                     relu, mode);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
+                       const float* gamma, float* dgamma, float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C,
+                       hipStream_t s) {
+  if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(rows_grid(M, C)), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta,
+                     M, C);
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 5 * C * sizeof(float), s,
+                     dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx, dres, M, C);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_relu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_relu_fwd, dim3(kml_stream_grid(n / 8, 256)), dim3(256), 0, s, x, y, n / 8);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long long n, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_relu_bwd, dim3(kml_stream_grid(n / 8, 256)), dim3(256), 0, s, dy, y, dx, n / 8);
+  KML_LAUNCH_CHECK();
+}

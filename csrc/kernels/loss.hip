@@ -1,0 +1,126 @@
+// loss.hip — softmax cross-entropy (mean reduction) for gfx950.
+//
+// forward : one wave64 per row.  Online max/sum-exp over the row (bf16 or fp32
+//           logits, 16 B loads), writes the row's log-sum-exp, loss and whether the
+//           argmax equals the label (the reference's validation "correct" count,
+//           function_resnet34.py:86-89).  Rows whose label == ignore_index contribute 0.
+// reduce  : one block folds per-row results into [mean loss, correct, valid].
+// backward: dlogits = grad_out * (softmax - onehot) / valid, recomputed from the saved
+//           log-sum-exp (no [B, C] probability tensor is kept).
+#include "kml_common.h"
+
+namespace {
+
+template <typename T> __device__ __forceinline__ float ldf(const T* p);
+template <> __device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <> __device__ __forceinline__ float ldf<float>(const float* p) { return *p; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_ce_fwd(const T* __restrict__ logits, const long long* __restrict__ labels,
+                                                float* __restrict__ lse, float* __restrict__ rowloss,
+                                                float* __restrict__ rowcorrect, int B, int C, long long ignore) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const T* x = logits + (long long)row * C;
+  float m = -INFINITY, s = 0.f;
+  int amax = 0;
+  float vmax = -INFINITY;
+  for (int c = lane; c < C; c += 64) {
+    const float v = ldf<T>(x + c);
+    if (v > vmax) { vmax = v; amax = c; }
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+    else s += __expf(v - m);
+  }
+  // combine (m, s) across the wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, mo);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+    m = mn;
+    const float vo = __shfl_xor(vmax, o, 64);
+    const int ao = __shfl_xor(amax, o, 64);
+    if (vo > vmax || (vo == vmax && ao < amax)) { vmax = vo; amax = ao; }
+  }
+  if (lane == 0) {
+    const long long y = labels[row];
+    const float l = m + __logf(s);
+    lse[row] = l;
+    if (y == ignore || y < 0 || y >= C) { rowloss[row] = 0.f; rowcorrect[row] = -1.f; }
+    else { rowloss[row] = l - ldf<T>(x + y); rowcorrect[row] = (amax == (int)y) ? 1.f : 0.f; }
+  }
+}
+
+// out[0] = sum loss / valid, out[1] = correct count, out[2] = valid rows
+__global__ __launch_bounds__(1024) void k_ce_reduce(const float* __restrict__ rowloss,
+                                                    const float* __restrict__ rowcorrect, float* __restrict__ out,
+                                                    int B) {
+  float l = 0.f, c = 0.f, v = 0.f;
+  for (int i = threadIdx.x; i < B; i += 1024) {
+    const float rc = rowcorrect[i];
+    if (rc >= 0.f) { l += rowloss[i]; c += rc; v += 1.f; }
+  }
+  l = wave_sum(l); c = wave_sum(c); v = wave_sum(v);
+  __shared__ float sh[3][16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][w] = l; sh[1][w] = c; sh[2][w] = v; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float L = 0, Cc = 0, V = 0;
+    for (int i = 0; i < 16; ++i) { L += sh[0][i]; Cc += sh[1][i]; V += sh[2][i]; }
+    out[0] = V > 0 ? L / V : 0.f;
+    out[1] = Cc;
+    out[2] = V;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
+                                                const float* __restrict__ lse, const float* __restrict__ red,
+                                                const float* __restrict__ grad_out, T* __restrict__ dlogits, int B,
+                                                int C, long long ignore) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const long long y = labels[row];
+  const bool skip = (y == ignore || y < 0 || y >= C);
+  const float valid = red[2];
+  const float g = (grad_out ? *grad_out : 1.f) / fmaxf(valid, 1.f);
+  const float l = lse[row];
+  const T* x = logits + (long long)row * C;
+  T* d = dlogits + (long long)row * C;
+  for (int c = lane; c < C; c += 64) {
+    float v = skip ? 0.f : (__expf(ldf<T>(x + c) - l) - (c == y ? 1.f : 0.f)) * g;
+    if constexpr (sizeof(T) == 2) d[c] = f2bf(v); else d[c] = v;
+  }
+}
+
+}  // namespace
+
+// dtype: 0 = bf16 logits, 1 = fp32 logits.  ws = [3*B] fp32 workspace (lse, rowloss, rowcorrect)
+KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, float* out3, int B, int C,
+                       long long ignore, int dtype, hipStream_t s) {
+  dim3 g((B + 3) / 4);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_ce_fwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, ws + B, ws + 2 * B,
+                       B, C, ignore);
+  else
+    hipLaunchKernelGGL(k_ce_fwd<float>, g, dim3(256), 0, s, (const float*)logits, labels, ws, ws + B, ws + 2 * B, B,
+                       C, ignore);
+  hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, s, ws + B, ws + 2 * B, out3, B);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
+                       const float* grad_out, void* dlogits, int B, int C, long long ignore, int dtype,
+                       hipStream_t s) {
+  dim3 g((B + 3) / 4);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_ce_bwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, out3, grad_out,
+                       (bf16_t*)dlogits, B, C, ignore);
+  else
+    hipLaunchKernelGGL(k_ce_bwd<float>, g, dim3(256), 0, s, (const float*)logits, labels, ws, out3, grad_out,
+                       (float*)dlogits, B, C, ignore);
+  KML_LAUNCH_CHECK();
+}

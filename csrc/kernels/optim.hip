@@ -1,0 +1,185 @@
+// optim.hip — fused multi-tensor optimizers over the flat parameter buffer (gfx950).
+//
+// All trainable parameters of a model live in ONE fp32 master buffer, their
+// gradients in ONE fp32 buffer (the same buffer RCCL all-reduces) and their bf16
+// compute copies in ONE shadow buffer.  Each optimizer step is therefore a single
+// streaming launch over ~N floats: read w, g (+ state), write w, state and the bf16
+// shadow the next forward consumes.  The data-parallel 1/world average is folded in
+// as grad_scale, so the all-reduce needs no separate scaling pass.
+//
+// Learning rate and step count are read from device memory, so a hipGraph-captured
+// training step follows an LR schedule / Adam bias correction without re-capture.
+//
+// Semantics follow torch.optim.SGD (momentum, dampening, nesterov, weight_decay) and
+// torch.optim.Adam / AdamW (L2 vs decoupled decay), which is what the reference's user
+// code configures (function_lenet.py:77-79, function_resnet34.py:62, function_vgg11.py:54).
+// Optimizer-state reset at every K-AVG round (reference network.py:121-128) is a
+// hipMemsetAsync of the state buffers (kml_memset).
+#include "kml_common.h"
+
+namespace {
+
+__global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
+                      bf16_t* __restrict__ shadow, const float* __restrict__ lr_ptr, float lr_host, float wd,
+                      float momentum, float dampening, int nesterov, int first, float grad_scale, long long n) {
+  const float lr = lr_ptr ? *lr_ptr : lr_host;
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 W = reinterpret_cast<float4*>(w)[i];
+    const float4 G = reinterpret_cast<const float4*>(g)[i];
+    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w};
+    float mv[4] = {0, 0, 0, 0};
+    if (mom && momentum != 0.f) {
+      const float4 Mv = reinterpret_cast<float4*>(mom)[i];
+      mv[0] = Mv.x; mv[1] = Mv.y; mv[2] = Mv.z; mv[3] = Mv.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float d = gv[k] * grad_scale + wd * wv[k];
+      if (mom && momentum != 0.f) {
+        mv[k] = first ? d : momentum * mv[k] + (1.f - dampening) * d;
+        d = nesterov ? d + momentum * mv[k] : mv[k];
+      }
+      wv[k] -= lr * d;
+    }
+    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    if (mom && momentum != 0.f) reinterpret_cast<float4*>(mom)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    if (shadow) {
+      uint2 s;
+      s.x = pack_bf2(wv[0], wv[1]);
+      s.y = pack_bf2(wv[2], wv[3]);
+      reinterpret_cast<uint2*>(shadow)[i] = s;
+    }
+  }
+  // scalar tail
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float d = g[i] * grad_scale + wd * w[i];
+    if (mom && momentum != 0.f) {
+      mom[i] = first ? d : momentum * mom[i] + (1.f - dampening) * d;
+      d = nesterov ? d + momentum * mom[i] : mom[i];
+    }
+    w[i] -= lr * d;
+    if (shadow) shadow[i] = f2bf(w[i]);
+  }
+}
+
+__global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, bf16_t* __restrict__ shadow, const float* __restrict__ lr_ptr,
+                       const float* __restrict__ step_ptr, float lr_host, float step_host, float b1, float b2,
+                       float eps, float wd, int decoupled, float grad_scale, long long n) {
+  const float lr = lr_ptr ? *lr_ptr : lr_host;
+  const float t = step_ptr ? *step_ptr : step_host;
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const float step_size = lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 W = reinterpret_cast<float4*>(w)[i];
+    const float4 G = reinterpret_cast<const float4*>(g)[i];
+    float4 M = reinterpret_cast<float4*>(m)[i];
+    float4 V = reinterpret_cast<float4*>(v)[i];
+    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w};
+    float mv[4] = {M.x, M.y, M.z, M.w}, vv[4] = {V.x, V.y, V.z, V.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gg = gv[k] * grad_scale;
+      if (decoupled) wv[k] *= (1.f - lr * wd);
+      else gg += wd * wv[k];
+      mv[k] = b1 * mv[k] + (1.f - b1) * gg;
+      vv[k] = b2 * vv[k] + (1.f - b2) * gg * gg;
+      const float denom = sqrtf(vv[k]) * rbc2 + eps;
+      wv[k] -= step_size * mv[k] / denom;
+    }
+    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+    reinterpret_cast<float4*>(m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    reinterpret_cast<float4*>(v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (shadow) {
+      uint2 s;
+      s.x = pack_bf2(wv[0], wv[1]);
+      s.y = pack_bf2(wv[2], wv[3]);
+      reinterpret_cast<uint2*>(shadow)[i] = s;
+    }
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gg = g[i] * grad_scale;
+    float wi = w[i];
+    if (decoupled) wi *= (1.f - lr * wd);
+    else gg += wd * wi;
+    m[i] = b1 * m[i] + (1.f - b1) * gg;
+    v[i] = b2 * v[i] + (1.f - b2) * gg * gg;
+    wi -= step_size * m[i] / (sqrtf(v[i]) * rbc2 + eps);
+    w[i] = wi;
+    if (shadow) shadow[i] = f2bf(wi);
+  }
+}
+
+__global__ void k_inc(float* p, float by) { if (threadIdx.x == 0 && blockIdx.x == 0) *p += by; }
+
+// sum of squares of an fp32 vector into out[0] (atomic; out zeroed by caller)
+__global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ x, float* __restrict__ out, long long n) {
+  float s = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    s += x[i] * x[i];
+  s = wave_sum(s);
+  __shared__ float sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+// x *= min(1, max_norm / (sqrt(sumsq) + 1e-6))  — global-norm clipping, scale on device
+__global__ void k_clip_scale(float* __restrict__ x, const float* __restrict__ sumsq, float max_norm, long long n) {
+  const float nrm = sqrtf(*sumsq);
+  const float c = fminf(1.f, max_norm / (nrm + 1e-6f));
+  if (c >= 1.f) return;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] *= c;
+}
+
+// p *= 1 / max(*count, 1)    (K-AVG divisor computed on device by the count all-reduce)
+__global__ void k_scale_inv_dev(float* __restrict__ p, const float* __restrict__ count, long long n) {
+  const float inv = 1.f / fmaxf(*count, 1.f);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] *= inv;
+}
+
+}  // namespace
+
+KML_API int kml_memset(void* p, int value, long long bytes, hipStream_t s) {
+  return (int)hipMemsetAsync(p, value, (size_t)bytes, s);
+}
+
+KML_API int kml_sgd(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr, float lr, float wd,
+                    float momentum, float dampening, int nesterov, int first, float grad_scale, long long n,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_sgd, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, w, g, mom, shadow, lr_ptr, lr,
+                     wd, momentum, dampening, nesterov, first, grad_scale, n);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_adam(float* w, const float* g, float* m, float* v, bf16_t* shadow, const float* lr_ptr,
+                     const float* step_ptr, float lr, float step, float b1, float b2, float eps, float wd,
+                     int decoupled, float grad_scale, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, w, g, m, v, shadow, lr_ptr,
+                     step_ptr, lr, step, b1, b2, eps, wd, decoupled, grad_scale, n);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_increment(float* p, float by, hipStream_t s) {
+  hipLaunchKernelGGL(k_inc, dim3(1), dim3(64), 0, s, p, by);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_clip_grad_norm(float* g, float* ws1, float max_norm, long long n, hipStream_t s) {
+  hipMemsetAsync(ws1, 0, sizeof(float), s);
+  hipLaunchKernelGGL(k_sumsq, dim3(kml_stream_grid(n, 256 * 4)), dim3(256), 0, s, g, ws1, n);
+  hipLaunchKernelGGL(k_clip_scale, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, g, ws1, max_norm, n);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_scale_inv_dev(float* p, const float* count, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_inv_dev, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, p, count, n);
+  KML_LAUNCH_CHECK();
+}

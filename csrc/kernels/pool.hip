@@ -1,0 +1,164 @@
+// pool.hip — pooling for NHWC bf16 on gfx950.
+//
+//   maxpool fwd : one thread per (output pixel, 8-channel chunk); writes the window
+//                 argmax (uint8, row-major tap index) for backward.
+//   maxpool bwd : gather formulation (each input element sums the output gradients of
+//                 the windows that selected it) — no atomics, no zero-fill pass.
+//   global avgpool fwd/bwd (AdaptiveAvgPool2d(1)).
+// Reference parity: nn.MaxPool2d(3,2,1) of the ResNet stem / nn.MaxPool2d(2) of LeNet
+// (function_lenet.py:25-31), AdaptiveAvgPool2d((1,1)) of torchvision resnet.
+#include "kml_common.h"
+
+namespace {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack_bf2(f[0], f[1]); v.y = pack_bf2(f[2], f[3]);
+  v.z = pack_bf2(f[4], f[5]); v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+struct PoolGeom { int B, H, W, C, OH, OW, k, s, p; };
+
+__global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                              unsigned char* __restrict__ idx, PoolGeom g) {
+  const int CH = g.C / 8;
+  const long long total = (long long)g.B * g.OH * g.OW * CH;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % CH);
+    long long pix = t / CH;
+    const int ow = (int)(pix % g.OW); pix /= g.OW;
+    const int oh = (int)(pix % g.OH); const int b = (int)(pix / g.OH);
+    float best[8]; int bi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bi[i] = 0; }
+    for (int r = 0; r < g.k; ++r) {
+      const int ih = oh * g.s - g.p + r;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int q = 0; q < g.k; ++q) {
+        const int iw = ow * g.s - g.p + q;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + ((long long)(b * g.H + ih) * g.W + iw) * g.C + ch * 8), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (f[i] > best[i] || (f[i] != f[i])) { best[i] = f[i]; bi[i] = r * g.k + q; }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[t] = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    reinterpret_cast<uint2*>(idx)[t] = packed;
+  }
+}
+
+__global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char* __restrict__ idx,
+                              bf16_t* __restrict__ dx, PoolGeom g) {
+  const int CH = g.C / 8;
+  const long long total = (long long)g.B * g.H * g.W * CH;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % CH);
+    long long pix = t / CH;
+    const int iw = (int)(pix % g.W); pix /= g.W;
+    const int ih = (int)(pix % g.H); const int b = (int)(pix / g.H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // outputs whose window contains ih: oh*s - p <= ih <= oh*s - p + k - 1
+    const int oh_lo = max(0, (ih + g.p - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (ih + g.p) / g.s);
+    const int ow_lo = max(0, (iw + g.p - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (iw + g.p) / g.s);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int r = ih - (oh * g.s - g.p);
+      if (r < 0 || r >= g.k) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int q = iw - (ow * g.s - g.p);
+        if (q < 0 || q >= g.k) continue;
+        const long long o = ((long long)(b * g.OH + oh) * g.OW + ow) * CH + ch;
+        const uint2 pk = reinterpret_cast<const uint2*>(idx)[o];
+        float d[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+        const int tap = r * g.k + q;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned w = i < 4 ? pk.x : pk.y;
+          if ((int)((w >> (8 * (i & 3))) & 0xff) == tap) acc[i] += d[i];
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[t] = pack8(acc);
+  }
+}
+
+// global average pool: x [B][HW][C] -> y [B][C]; one thread per (b, chunk)
+__global__ void k_gavg_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B, int HW, int C) {
+  const int CH = C / 8;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * CH) return;
+  const int b = t / CH, ch = t % CH;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int p = 0; p < HW; ++p) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + ((long long)b * HW + p) * C + ch * 8), f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += f[i];
+  }
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] *= inv;
+  reinterpret_cast<uint4*>(y)[t] = pack8(acc);
+}
+
+__global__ void k_gavg_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int B, int HW, int C) {
+  const int CH = C / 8;
+  const long long total = (long long)B * HW * CH;
+  const float inv = 1.f / HW;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+       t += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % CH);
+    const long long b = t / CH / HW;
+    float d[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[b * CH + ch], d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] *= inv;
+    reinterpret_cast<uint4*>(dx)[t] = pack8(d);
+  }
+}
+
+}  // namespace
+
+KML_API int kml_maxpool_fwd(const bf16_t* x, bf16_t* y, unsigned char* idx, int B, int H, int W, int C, int k,
+                            int s, int p, hipStream_t st) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  PoolGeom g{B, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
+  long long total = (long long)B * g.OH * g.OW * (C / 8);
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, x, y, idx, g);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_maxpool_bwd(const bf16_t* dy, const unsigned char* idx, bf16_t* dx, int B, int H, int W, int C,
+                            int k, int s, int p, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  PoolGeom g{B, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
+  long long total = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, idx, dx, g);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_gavgpool_fwd(const bf16_t* x, bf16_t* y, int B, int HW, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int n = B * (C / 8);
+  hipLaunchKernelGGL(k_gavg_fwd, dim3((n + 255) / 256), dim3(256), 0, st, x, y, B, HW, C);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_gavgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int HW, int C, hipStream_t st) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  long long total = (long long)B * HW * (C / 8);
+  hipLaunchKernelGGL(k_gavg_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, dx, B, HW, C);
+  KML_LAUNCH_CHECK();
+}

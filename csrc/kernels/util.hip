@@ -1,0 +1,144 @@
+// util.hip — small utility kernels: version probe, fill, scale, cast, axpby.
+#include "kml_common.h"
+
+KML_API int kml_abi_version() { return 1; }
+
+__global__ void k_fill_f32(float* __restrict__ p, float v, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+KML_API int kml_fill_f32(float* p, float v, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill_f32, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, p, v, n);
+  KML_LAUNCH_CHECK();
+}
+
+// x *= a  (fp32, vectorised by 4 when aligned)
+__global__ void k_scale_f32(float* __restrict__ p, float a, long long n) {
+  long long n4 = n >> 2;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = p4[i];
+    v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+    p4[i] = v;
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+    p[i] *= a;
+}
+
+KML_API int kml_scale_f32(float* p, float a, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_f32, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, p, a, n);
+  KML_LAUNCH_CHECK();
+}
+
+__global__ void k_f32_to_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, long long n) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = f2bf(x[i]);
+}
+__global__ void k_bf16_to_f32(const bf16_t* __restrict__ x, float* __restrict__ y, long long n) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = bf2f(x[i]);
+}
+
+KML_API int kml_f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_f32_to_bf16, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, x, y, n);
+  KML_LAUNCH_CHECK();
+}
+KML_API int kml_bf16_to_f32(const bf16_t* x, float* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_bf16_to_f32, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, x, y, n);
+  KML_LAUNCH_CHECK();
+}
+
+// y = a*x + b*y over bf16 NHWC tensors (used for residual-gradient sums), vectorised x8
+__global__ void k_add_bf16(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                           bf16_t* __restrict__ y, long long n8) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    uint4 va = reinterpret_cast<const uint4*>(a)[i];
+    uint4 vb = reinterpret_cast<const uint4*>(b)[i];
+    uint4 o;
+    o.x = pack_bf2(lo_bf(va.x) + lo_bf(vb.x), hi_bf(va.x) + hi_bf(vb.x));
+    o.y = pack_bf2(lo_bf(va.y) + lo_bf(vb.y), hi_bf(va.y) + hi_bf(vb.y));
+    o.z = pack_bf2(lo_bf(va.z) + lo_bf(vb.z), hi_bf(va.z) + hi_bf(vb.z));
+    o.w = pack_bf2(lo_bf(va.w) + lo_bf(vb.w), hi_bf(va.w) + hi_bf(vb.w));
+    reinterpret_cast<uint4*>(y)[i] = o;
+  }
+}
+
+KML_API int kml_add_bf16(const bf16_t* a, const bf16_t* b, bf16_t* y, long long n, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  long long n8 = n / 8;
+  hipLaunchKernelGGL(k_add_bf16, dim3(kml_stream_grid(n8, 256)), dim3(256), 0, s, a, b, y, n8);
+  KML_LAUNCH_CHECK();
+}
+
+// out[c] += sum_m x[m][c]   (bf16 [M][C] -> fp32, any C; used for Linear / conv bias grads)
+__global__ __launch_bounds__(256) void k_colsum_bf16(const bf16_t* __restrict__ x, float* __restrict__ out,
+                                                     long long M, int C, int rows_per_block) {
+  const long long r0 = (long long)blockIdx.y * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+    float s = 0.f;
+    for (long long r = r0; r < r1; ++r) s += bf2f(x[r * C + c]);
+    atomicAdd(out + c, s);
+  }
+}
+
+KML_API int kml_colsum_bf16(const bf16_t* x, float* out, long long M, int C, hipStream_t s) {
+  int rpb = 64;
+  long long gy = (M + rpb - 1) / rpb;
+  if (gy > 65535) { rpb = (int)((M + 65534) / 65535); gy = (M + rpb - 1) / rpb; }
+  dim3 grid((C + 255) / 256, (unsigned)gy);
+  hipLaunchKernelGGL(k_colsum_bf16, grid, dim3(256), 0, s, x, out, M, C, rpb);
+  KML_LAUNCH_CHECK();
+}
+
+__global__ void k_add_i64(long long* __restrict__ p, long long v, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] += v;
+}
+
+KML_API int kml_add_i64(long long* p, long long v, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_i64, dim3((n + 255) / 256), dim3(256), 0, s, p, v, n);
+  KML_LAUNCH_CHECK();
+}
+
+// zero-pad the channel dim: x [P][C] -> y [P][CP] (bf16), CP >= C
+__global__ void k_pad_channels(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long P, int C, int CP) {
+  long long total = P * CP;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long p = i / CP;
+    int c = (int)(i - p * CP);
+    y[i] = c < C ? x[p * C + c] : (bf16_t)0;
+  }
+}
+
+KML_API int kml_pad_channels(const bf16_t* x, bf16_t* y, long long P, int C, int CP, hipStream_t s) {
+  hipLaunchKernelGGL(k_pad_channels, dim3(kml_stream_grid(P * CP, 256)), dim3(256), 0, s, x, y, P, C, CP);
+  KML_LAUNCH_CHECK();
+}
+
+// NCHW fp32 -> NHWC bf16 with channel padding (input adapter for user tensors)
+__global__ void k_nchw_to_nhwc_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int B, int C, int HW,
+                                    int CP) {
+  long long total = (long long)B * HW * CP;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % CP);
+    long long t = i / CP;
+    int p = (int)(t % HW);
+    int b = (int)(t / HW);
+    y[i] = c < C ? f2bf(x[((long long)b * C + c) * HW + p]) : (bf16_t)0;
+  }
+}
+
+KML_API int kml_nchw_to_nhwc_bf16(const float* x, bf16_t* y, int B, int C, int HW, int CP, hipStream_t s) {
+  long long total = (long long)B * HW * CP;
+  hipLaunchKernelGGL(k_nchw_to_nhwc_bf16, dim3(kml_stream_grid(total, 256)), dim3(256), 0, s, x, y, B, C, HW, CP);
+  KML_LAUNCH_CHECK();
+}

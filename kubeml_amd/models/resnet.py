@@ -1,0 +1,287 @@
+"""ResNet family on the MI355X-native layers (torchvision-compatible names/shapes).
+
+``resnet34()`` is the reference's headline workload: torchvision ``resnet34()`` with
+the ImageNet stem (7x7/2 conv + 3x3/2 max-pool) and the 1000-class head, trained on
+32x32 CIFAR-10 images (ml/experiments/kubeml/function_resnet34.py:101).  With that
+stem the spatial size is 16 -> 8 -> 8 -> 4 -> 2 -> 1, so layer4 runs at 1x1 and the
+implicit-GEMM kernels collapse its 3x3 convolutions to their centre tap.
+
+GPU training runs every residual block as ONE autograd node (:class:`BlockFn`):
+conv(+BN-stats) -> BN(+residual)+ReLU forward, fused BN-backward / split-K wgrad /
+dgrad(+residual-gradient) backward.  ``state_dict()`` is key-for-key and
+shape-for-shape torchvision's, so reference checkpoints load unchanged.
+Also: ``resnet50`` (Bottleneck, north-star config 3) and CIFAR ResNet-20/32/44/56
+(option-A shortcut, reference ml/experiments/kubeml/resnet32.py:44-146).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as tnn
+import torch.nn.functional as F
+
+from ..nn import modules as M
+from ..nn.fused import BlockFn, ConvBNUnit, StatsArena, block_params
+
+
+def _gpu_train(x):
+    return x.is_cuda and torch.is_grad_enabled()
+
+
+class BasicBlock(tnn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = M.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = M.BatchNorm2d(planes)
+        self.relu = M.ReLU(inplace=True)
+        self.conv2 = M.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = M.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+        plan = [(self.conv1, self.bn1, True, "main")]
+        if downsample is not None:
+            plan.append((downsample[0], downsample[1], False, "short"))
+        plan.append((self.conv2, self.bn2, True, "last"))
+        self._kml_plan = plan
+
+    def forward(self, x):
+        if x.is_cuda:
+            if _gpu_train(x) and self.training:
+                return BlockFn.apply(x, self, *block_params(self))
+            return _block_eval(self, x)
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), relu=True, residual=idt)
+
+
+class Bottleneck(tnn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = M.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = M.BatchNorm2d(planes)
+        self.conv2 = M.Conv2d(planes, planes, 3, stride, 1, bias=False)
+        self.bn2 = M.BatchNorm2d(planes)
+        self.conv3 = M.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = M.BatchNorm2d(planes * 4)
+        self.relu = M.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+        plan = [(self.conv1, self.bn1, True, "main"), (self.conv2, self.bn2, True, "main")]
+        if downsample is not None:
+            plan.append((downsample[0], downsample[1], False, "short"))
+        plan.append((self.conv3, self.bn3, True, "last"))
+        self._kml_plan = plan
+
+    def forward(self, x):
+        if x.is_cuda:
+            if _gpu_train(x) and self.training:
+                return BlockFn.apply(x, self, *block_params(self))
+            return _block_eval(self, x)
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
+        return self.bn3(self.conv3(out), relu=True, residual=idt)
+
+
+def _block_eval(block, x):
+    """Inference / no-grad forward (running or batch statistics, no saved tensors)."""
+    training = block.training
+    short = None
+    h = x
+    for conv, bn, relu, role in block._kml_plan:
+        if role == "short":
+            short, _ = ConvBNUnit.forward(x, conv, bn, relu, None, training)
+        elif role == "last":
+            h, _ = ConvBNUnit.forward(h, conv, bn, relu, short if short is not None else x, training)
+        else:
+            h, _ = ConvBNUnit.forward(h, conv, bn, relu, None, training)
+    return h
+
+
+class _Stem(tnn.Module):
+    """Holds nothing; ResNet.forward drives conv1/bn1/maxpool (names stay top-level)."""
+
+
+class ResNet(tnn.Module):
+    def __init__(self, block, layers, num_classes=1000, in_channels=3):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = M.Conv2d(in_channels, 64, 7, 2, 3, bias=False)
+        self.bn1 = M.BatchNorm2d(64)
+        self.relu = M.ReLU(inplace=True)
+        self.maxpool = M.MaxPool2d(3, 2, 1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], 2)
+        self.layer3 = self._make_layer(block, 256, layers[2], 2)
+        self.layer4 = self._make_layer(block, 512, layers[3], 2)
+        self.avgpool = M.AdaptiveAvgPool2d((1, 1))
+        self.fc = M.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, M.Conv2d):
+                tnn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, M.BatchNorm2d):
+                tnn.init.constant_(m.weight, 1)
+                tnn.init.constant_(m.bias, 0)
+        self._arena = StatsArena([m for m in self.modules() if isinstance(m, M.BatchNorm2d)])
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = tnn.Sequential(M.Conv2d(self.inplanes, planes * block.expansion, 1, stride, bias=False),
+                                        M.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
+        return tnn.Sequential(*layers)
+
+    def forward(self, x):
+        """x: NHWC bf16 (channels padded to 8) on GPU, or NCHW float (converted)."""
+        if x.dim() == 4 and (x.shape[-1] not in (self.conv1.in_channels, self.conv1.cin_pad)
+                             or x.dtype != torch.bfloat16 and x.is_cuda):
+            x = M.to_nhwc(x, self.conv1.cin_pad)
+        if x.is_cuda:
+            if self.training:
+                from ..ops import kernels as K
+                self._arena.begin(x.device)
+                self._bump_counters()
+            x = self._stem_gpu(x)
+        else:
+            x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.avgpool(x)
+        return self.fc(x)
+
+    def _bump_counters(self):
+        # num_batches_tracked of every BN: one tiny kernel each is avoided by keeping
+        # the counters in one int64 arena (allocated on first use)
+        arena = getattr(self, "_nbt_arena", None)
+        bns = self._arena.bns
+        if arena is None or arena.device != bns[0].running_mean.device:
+            dev = bns[0].running_mean.device
+            arena = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+            for i, bn in enumerate(bns):
+                arena[i] = bn.num_batches_tracked.to(dev)
+                bn.num_batches_tracked = arena[i]
+            self._nbt_arena = arena
+        from ..ops import kernels as K
+        K.add_i64_(arena)
+
+    def _stem_gpu(self, x):
+        if torch.is_grad_enabled() and self.training:
+            return _StemFn.apply(x, self, self.conv1.weight, self.bn1.weight, self.bn1.bias)
+        y, _ = ConvBNUnit.forward(x, self.conv1, self.bn1, True, None, self.training)
+        from ..ops import kernels as K
+        y, _ = K.maxpool_fwd(y, 3, 2, 1)
+        return y
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, net, *params):
+        from ..ops import kernels as K
+        y, s = ConvBNUnit.forward(x, net.conv1, net.bn1, True, None, True)
+        p, idx = K.maxpool_fwd(y, 3, 2, 1)
+        ctx.net, ctx.s, ctx.idx, ctx.yshape = net, s, idx, y.shape
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        from ..ops import kernels as K
+        net = ctx.net
+        dy = K.maxpool_bwd(dp.contiguous(), ctx.idx, ctx.yshape, 3, 2, 1)
+        dx, _ = ConvBNUnit.backward(dy, ctx.s, net.conv1, net.bn1, False, ctx.needs_input_grad[0])
+        ctx.s = ctx.idx = None
+        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+def resnet18(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, **kw)
+
+
+def resnet34(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet50(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, **kw)
+
+
+# ---------------------------------------------------------------------------------------
+# CIFAR ResNet (He et al. 2016, option-A identity shortcut) — reference resnet32.py
+# ---------------------------------------------------------------------------------------
+
+class _LambdaShortcut(tnn.Module):
+    """Option A: stride-2 subsample + zero-pad channels (parameter-free)."""
+
+    def __init__(self, planes):
+        super().__init__()
+        self.pad = planes // 4
+
+    def forward(self, x):  # NHWC
+        y = x[:, ::2, ::2, :]
+        return F.pad(y, (self.pad, self.pad)).contiguous()
+
+
+class CifarBasicBlock(tnn.Module):
+    def __init__(self, in_planes, planes, stride=1):
+        super().__init__()
+        self.conv1 = M.Conv2d(in_planes, planes, 3, stride, 1, bias=False)
+        self.bn1 = M.BatchNorm2d(planes)
+        self.conv2 = M.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = M.BatchNorm2d(planes)
+        self.shortcut = _LambdaShortcut(planes) if (stride != 1 or in_planes != planes) else None
+
+    def forward(self, x):
+        idt = x if self.shortcut is None else self.shortcut(x)
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), relu=True, residual=idt)
+
+
+class CifarResNet(tnn.Module):
+    def __init__(self, num_blocks, num_classes=10):
+        super().__init__()
+        self.in_planes = 16
+        self.conv1 = M.Conv2d(3, 16, 3, 1, 1, bias=False)
+        self.bn1 = M.BatchNorm2d(16)
+        self.layer1 = self._make(16, num_blocks, 1)
+        self.layer2 = self._make(32, num_blocks, 2)
+        self.layer3 = self._make(64, num_blocks, 2)
+        self.linear = M.Linear(64, num_classes)
+        for m in self.modules():
+            if isinstance(m, (M.Conv2d, M.Linear)):
+                tnn.init.kaiming_normal_(m.weight)
+
+    def _make(self, planes, n, stride):
+        layers = []
+        for s in [stride] + [1] * (n - 1):
+            layers.append(CifarBasicBlock(self.in_planes, planes, s))
+            self.in_planes = planes
+        return tnn.Sequential(*layers)
+
+    def forward(self, x):
+        if x.dim() == 4 and x.shape[1] == 3 and x.shape[-1] != 3:
+            x = M.to_nhwc(x, self.conv1.cin_pad)
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.layer3(self.layer2(self.layer1(out)))
+        B, H, W, C = out.shape
+        out = out.reshape(B, H * W, C).float().mean(1) if not out.is_cuda else M.AdaptiveAvgPool2d()(out)
+        return self.linear(out)
+
+
+def resnet20(num_classes=10):
+    return CifarResNet(3, num_classes)
+
+
+def resnet32(num_classes=10):
+    return CifarResNet(5, num_classes)
+
+
+def resnet44(num_classes=10):
+    return CifarResNet(7, num_classes)
+
+
+def resnet56(num_classes=10):
+    return CifarResNet(9, num_classes)

@@ -1,0 +1,180 @@
+"""Flat parameter space: one fp32 master / fp32 grad / bf16 shadow buffer per model.
+
+Why flat (MI355X-first): the optimizer step, the gradient all-reduce over RCCL and
+the K-AVG model average are then each ONE launch / ONE collective over a contiguous
+buffer sized for HBM, instead of ~200 per-tensor launches.  This is the
+equivalent of the reference's reference-model store (ml/pkg/model/model.go:14-53,
+one gorgonia tensor per layer merged on the CPU), re-homed to HBM.
+
+Layout rules
+------------
+* Every parameter owns a *storage region* whose shape is chosen by its module
+  (conv weights: KRSC ``[Cout, KH, KW, Cin_pad]`` so the MFMA kernels read them
+  directly) and is exposed to PyTorch as a strided *view* with the usual torch
+  shape (``[Cout, Cin, KH, KW]``).  ``state_dict()`` therefore carries exactly the
+  torchvision names and shapes, and torch optimizers / ``load_state_dict`` keep
+  working.
+* ``p.grad`` is bound to the matching view of the grad buffer; our backward kernels
+  accumulate into it (``+=``), which is torch's ``.grad`` accumulation semantics.
+* ``p._kml_shadow`` is the bf16 copy in storage layout that the forward kernels
+  consume; it is refreshed by the fused optimizers, or lazily when ``p._version``
+  moved (a foreign optimizer or ``load_state_dict`` wrote the master).
+* Regions are packed in REVERSE registration order so that backward (which runs
+  from the last layer to the first) fills the grad buffer front-to-back: a prefix
+  of the buffer is final as soon as the corresponding layers are done, which is
+  what the bucketed, backward-overlapped all-reduce exploits.
+* Regions are 64-element aligned (256 B) so every region starts on a cache line.
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable, List, Optional
+
+import torch
+
+ALIGN = 64
+
+
+def _storage_spec(p: torch.nn.Parameter):
+    shape = getattr(p, "_kml_storage_shape", None)
+    view = getattr(p, "_kml_view", None)
+    if shape is None:
+        return tuple(p.shape), (lambda s: s)
+    return tuple(shape), view
+
+
+class FlatParamSpace:
+    """Owns the flat buffers for a list of parameters (all on one device)."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], device=None, reverse: bool = True,
+                 with_shadow: Optional[bool] = None):
+        params = [p for p in params if p.requires_grad]
+        seen = set()
+        uniq = []
+        for p in params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        self.params: List[torch.nn.Parameter] = list(reversed(uniq)) if reverse else uniq
+        if device is None:
+            device = self.params[0].device if self.params else torch.device("cpu")
+        self.device = torch.device(device)
+        if with_shadow is None:
+            with_shadow = self.device.type == "cuda"
+        self.offsets = []
+        off = 0
+        specs = []
+        for p in self.params:
+            shape, view = _storage_spec(p)
+            n = 1
+            for d in shape:
+                n *= d
+            specs.append((shape, view, n))
+            self.offsets.append((off, n))
+            off += -(-n // ALIGN) * ALIGN
+        self.numel = max(off, ALIGN)
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.shadow = (torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
+                       if with_shadow else None)
+        with torch.no_grad():
+            for p, (shape, view, n), (o, _) in zip(self.params, specs, self.offsets):
+                st = self.master[o:o + n].view(shape)
+                pv = view(st)
+                pv.copy_(p.data.to(self.device))
+                p.data = pv
+                gst = self.grad[o:o + n].view(shape)
+                p.grad = view(gst)
+                p._kml_grad = p.grad
+                p._kml_grad_storage = gst
+                p._kml_master_storage = st
+                if self.shadow is not None:
+                    p._kml_shadow = self.shadow[o:o + n].view(shape)
+                p._kml_flat = self
+        self.refresh_shadow()
+
+    # ------------------------------------------------------------------ utilities
+    def refresh_shadow(self):
+        """bf16 shadow := master (after init, load_state_dict, K-AVG averaging)."""
+        if self.shadow is None:
+            return
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+            K.f32_to_bf16(self.master, self.shadow)
+        else:
+            self.shadow.copy_(self.master)
+        for p in self.params:
+            p._kml_shadow_version = p._version
+
+    def rebind_grads(self):
+        for p in self.params:
+            p.grad = p._kml_grad
+
+    def zero_grad(self):
+        if self.device.type == "cuda":
+            from ..ops import kernels as K
+            K.memset_(self.grad)
+        else:
+            self.grad.zero_()
+        self.rebind_grads()
+
+    def buckets(self, bucket_bytes: int):
+        """Contiguous [start, end) element ranges of the grad buffer, ~bucket_bytes each,
+        cut on parameter boundaries, in backward-completion order."""
+        out = []
+        cap = max(ALIGN, bucket_bytes // 4)
+        start = 0
+        cur_end = 0
+        members = []
+        for idx, (o, n) in enumerate(self.offsets):
+            end = o + (-(-n // ALIGN) * ALIGN)
+            members.append(idx)
+            cur_end = end
+            if cur_end - start >= cap:
+                out.append((start, cur_end, members))
+                start, members = cur_end, []
+        if members:
+            out.append((start, self.numel, members))
+        return out
+
+    def state_vector(self) -> torch.Tensor:
+        return self.master
+
+
+def flatten_module(module: torch.nn.Module, device=None) -> FlatParamSpace:
+    """Move all trainable parameters of ``module`` into one FlatParamSpace."""
+    space = FlatParamSpace(list(module.parameters()), device=device)
+    module._kml_flat = space
+    return space
+
+
+def ensure_param_ready(p: torch.nn.Parameter):
+    """Standalone (non-flattened) GPU parameter: give it grad/shadow storage once."""
+    if getattr(p, "_kml_flat", None) is not None:
+        return
+    FlatParamSpace([p], device=p.device)
+
+
+def shadow_of(p: torch.nn.Parameter) -> torch.Tensor:
+    """bf16 storage-layout copy of p, refreshed if the master changed under us."""
+    ensure_param_ready(p)
+    if getattr(p, "_kml_shadow_version", None) != p._version:
+        from ..ops import kernels as K
+        st = p._kml_master_storage
+        K.f32_to_bf16(st.contiguous(), p._kml_shadow)
+        p._kml_shadow_version = p._version
+    return p._kml_shadow
+
+
+def grad_storage_of(p: torch.nn.Parameter) -> torch.Tensor:
+    """fp32 storage-layout grad region of p (zeroed and re-bound if p.grad was reset)."""
+    ensure_param_ready(p)
+    if p.grad is None:
+        p._kml_grad_storage.zero_()
+        p.grad = p._kml_grad
+    return p._kml_grad_storage
+
+
+def master_of(p: torch.nn.Parameter) -> torch.Tensor:
+    """fp32 storage-layout master region of p (contiguous; what the kernels read)."""
+    ensure_param_ready(p)
+    return p._kml_master_storage

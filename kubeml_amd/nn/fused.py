@@ -1,0 +1,172 @@
+"""Fused conv -> BatchNorm -> (+residual) -> ReLU units and block-level autograd.
+
+A ``ConvBNUnit`` is the basic building block of the CNN workloads (ResNet-34/50,
+VGG-16-BN).  Its training forward is two kernels:
+
+    conv_igemm (FWD, epilogue accumulates per-channel sum/sumsq)  ->  bn_apply(+res, ReLU)
+
+and its backward three:
+
+    bn_bwd (reduce + apply, ReLU mask, residual-gradient copy)  ->  conv WGRAD (split-K,
+    into the flat fp32 grad buffer)  ->  conv DGRAD (epilogue adds the other branch's
+    input gradient, so residual merges cost no separate add kernel).
+
+Whole residual blocks are single autograd nodes (``BlockFn``) so PyTorch's autograd
+never inserts its own gradient-accumulation kernels between our launches: the
+entire step runs on the HIP kernels and captures cleanly into one hipGraph.
+
+BN statistics buffers come from one per-forward arena that the model zeroes with a
+single ``hipMemsetAsync`` (see :func:`StatsArena`).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+from torch.autograd import Function
+
+from .flat import grad_storage_of, master_of, shadow_of
+
+
+class StatsArena:
+    """One zeroed fp32 buffer per forward holding [sum, sumsq] for every BN of a model."""
+
+    def __init__(self, bns):
+        self.bns = list(bns)
+        off = 0
+        for bn in self.bns:
+            bn._kml_stats_off = off
+            off += 2 * bn.num_features
+        self.numel = max(off, 1)
+
+    def begin(self, device):
+        from ..ops import kernels as K
+        buf = torch.empty(self.numel, dtype=torch.float32, device=device)
+        K.memset_(buf)
+        for bn in self.bns:
+            o = bn._kml_stats_off
+            bn._kml_stats = buf[o:o + 2 * bn.num_features]
+        self.counters = [bn.num_batches_tracked for bn in self.bns]
+        return buf
+
+
+def _stats_for(bn, device):
+    st = getattr(bn, "_kml_stats", None)
+    if st is None or st.device != device:
+        from ..ops import kernels as K
+        st = torch.empty(2 * bn.num_features, dtype=torch.float32, device=device)
+        K.memset_(st)
+    bn._kml_stats = None  # single use
+    return st
+
+
+class ConvBNUnit:
+    """Stateless executor for (conv module, bn module, relu)."""
+
+    @staticmethod
+    def forward(x, conv, bn, relu: bool, res: Optional[torch.Tensor], training: bool):
+        from ..ops import kernels as K
+        w = shadow_of(conv.weight)
+        kh, kw = conv.kernel_size
+        gamma, beta = master_of(bn.weight), master_of(bn.bias)
+        if training:
+            stats = _stats_for(bn, x.device)
+            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats)
+            C = c.shape[-1]
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            rstd = torch.empty_like(mean)
+            y = K.bn_apply(c, stats, gamma, beta, res=res, save_mean=mean, save_rstd=rstd,
+                           run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
+                           momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu)
+            return y, (x, c, y if relu else None, mean, rstd)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding)
+        y = K.bn_apply(c, None, gamma, beta, res=res, run_mean=bn.running_mean, run_var=bn.running_var,
+                       eps=bn.eps, relu=relu, training=False)
+        return y, None
+
+    @staticmethod
+    def backward(dy, saved, conv, bn, want_dres: bool, need_dx: bool, addend=None):
+        from ..ops import kernels as K
+        x, c, y, mean, rstd = saved
+        dres = torch.empty_like(dy) if want_dres else None
+        dc = K.bn_bwd(dy, y, c, mean, rstd, master_of(bn.weight), grad_storage_of(bn.weight),
+                      grad_storage_of(bn.bias), dres=dres)
+        kh, kw = conv.kernel_size
+        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding)
+        dx = None
+        if need_dx:
+            dx = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
+                              addend=addend)
+        return dx, dres
+
+
+class BlockFn(Function):
+    """Autograd node for a residual block described by a ``plan`` of units.
+
+    plan: list of (conv, bn, relu, role) in forward order where role is one of
+      "main"   — unit on the main branch fed by the previous main output
+      "short"  — projection shortcut fed by the block input
+      "last"   — final main unit; its BN adds the shortcut (identity or "short")
+    """
+
+    @staticmethod
+    def forward(ctx, x, block, *params):
+        training = True
+        saved = []
+        h = x
+        short = None
+        for conv, bn, relu, role in block._kml_plan:
+            if role == "short":
+                short, s = ConvBNUnit.forward(x, conv, bn, relu, None, training)
+                saved.append(s)
+            elif role == "last":
+                res = short if short is not None else x
+                h, s = ConvBNUnit.forward(h, conv, bn, relu, res, training)
+                saved.append(s)
+            else:
+                h, s = ConvBNUnit.forward(h, conv, bn, relu, None, training)
+                saved.append(s)
+        ctx.block = block
+        ctx.saved = saved
+        return h
+
+    @staticmethod
+    def backward(ctx, dout):
+        block = ctx.block
+        plan = block._kml_plan
+        saved = ctx.saved
+        dout = dout.contiguous()
+        need_x = ctx.needs_input_grad[0]
+        # walk main units backwards; the last unit also yields the shortcut gradient dz
+        main = [(i, u) for i, u in enumerate(plan) if u[3] != "short"]
+        short = [(i, u) for i, u in enumerate(plan) if u[3] == "short"]
+        g = dout
+        dres = None
+        for k in range(len(main) - 1, -1, -1):
+            i, (conv, bn, relu, role) = main[k]
+            is_last = role == "last"
+            is_first = k == 0
+            addend = None
+            if is_first:
+                # shortcut gradient joins here: identity -> dres, projection -> its dgrad
+                if short:
+                    j, (sc, sb, sr, _) = short[0]
+                    addend, _ = ConvBNUnit.backward(dres, saved[j], sc, sb, False, need_x)
+                else:
+                    addend = dres
+            dx, dz = ConvBNUnit.backward(g, saved[i], conv, bn, want_dres=is_last,
+                                         need_dx=(not is_first) or need_x, addend=addend if is_first else None)
+            if is_last:
+                dres = dz
+                if is_first and short:  # single-unit main branch (not used by ResNets)
+                    pass
+            g = dx
+        ctx.saved = None
+        return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+def block_params(block) -> List[torch.nn.Parameter]:
+    ps = []
+    for conv, bn, _, _ in block._kml_plan:
+        ps += [conv.weight, bn.weight, bn.bias]
+    return ps

@@ -1,0 +1,423 @@
+"""MI355X-native layers (NHWC bf16 activations, HIP kernels, flat fp32 parameters).
+
+Activation convention: 4-d activations are NHWC.  On an MI355X they are bf16 with
+the channel dimension padded to a multiple of 8 (16-byte vectors); on the CPU the
+same modules run in fp32 through the stock PyTorch reference ops so the whole
+framework (SDK, K-AVG, elastic resize, CLI) is testable without a GPU.
+
+Parameters keep torch's shapes and ``state_dict`` names (``weight`` ``[Cout, Cin,
+KH, KW]``, ``bias``, BN ``running_mean`` …) but are views into storage laid out for
+the kernels (see :mod:`kubeml_amd.nn.flat`).  Gradients are accumulated by the HIP
+kernels directly into ``p.grad`` storage (``+=``), matching torch's semantics.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as tnn
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from .flat import grad_storage_of, master_of, shadow_of
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def _round8(c):
+    return -(-c // 8) * 8
+
+
+def _on_gpu(x):
+    return x.is_cuda
+
+
+# ======================================================================================
+# Conv2d
+# ======================================================================================
+
+class _ConvFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod):
+        from ..ops import kernels as K
+        w = shadow_of(weight)
+        y = K.conv_fwd(x, w, mod.kernel_size[0], mod.kernel_size[1], mod.stride, mod.padding,
+                       bias=None if bias is None else master_of(bias))
+        ctx.mod = mod
+        ctx.x = x
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        mod = ctx.mod
+        dy = dy.contiguous()
+        K.conv_wgrad(ctx.x, dy, grad_storage_of(mod.weight), mod.kernel_size[0], mod.kernel_size[1],
+                     mod.stride, mod.padding)
+        if ctx.has_bias:
+            K.colsum_(dy.view(-1, dy.shape[-1]), grad_storage_of(mod.bias))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv_dgrad(dy, shadow_of(mod.weight), ctx.x.shape, mod.kernel_size[0],
+                              mod.kernel_size[1], mod.stride, mod.padding)
+        ctx.x = None
+        return dx, None, None, None
+
+
+class Conv2d(tnn.Module):
+    """NHWC convolution on MFMA implicit-GEMM kernels (groups=1, dilation=1)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.kernel_size = _pair(kernel_size)
+        self.stride = _pair(stride)
+        self.padding = _pair(padding)
+        self.cin_pad = _round8(in_channels)
+        kh, kw = self.kernel_size
+        self.weight = tnn.Parameter(torch.empty(out_channels, in_channels, kh, kw))
+        self.bias = tnn.Parameter(torch.empty(out_channels)) if bias else None
+        cin, cp = in_channels, self.cin_pad
+        self.weight._kml_storage_shape = (out_channels, kh, kw, cp)
+        self.weight._kml_view = (lambda st: st[..., :cin].permute(0, 3, 1, 2)) if cp != cin else \
+            (lambda st: st.permute(0, 3, 1, 2))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        tnn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            fan_in = self.in_channels * self.kernel_size[0] * self.kernel_size[1]
+            b = 1 / math.sqrt(fan_in)
+            tnn.init.uniform_(self.bias, -b, b)
+
+    def extra_repr(self):
+        return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
+                f"stride={self.stride}, padding={self.padding}, bias={self.bias is not None}, layout=NHWC")
+
+    def forward(self, x):
+        if not _on_gpu(x):
+            y = F.conv2d(x.permute(0, 3, 1, 2), self.weight, self.bias, self.stride, self.padding)
+            return y.permute(0, 2, 3, 1)
+        if x.shape[-1] != self.cin_pad:
+            from ..ops import kernels as K
+            x = K.pad_channels(x.contiguous(), self.cin_pad)
+        return _ConvFn.apply(x.contiguous(), self.weight, self.bias, self)
+
+
+# ======================================================================================
+# Linear (a 1x1 convolution over a 1x1 image on the same MFMA kernels)
+# ======================================================================================
+
+class _LinearFn(Function):
+    @staticmethod
+    def forward(ctx, x2, weight, bias, mod, relu):
+        from ..ops import kernels as K
+        op, ip = mod.out_pad, mod.in_pad
+        w = shadow_of(weight).view(op, 1, 1, ip)
+        B = x2.shape[0]
+        bias_st = None if bias is None else master_of(bias)
+        y = K.conv_fwd(x2.view(B, 1, 1, ip), w, 1, 1, (1, 1), (0, 0), bias=bias_st, relu=relu).view(B, op)
+        ctx.mod, ctx.x, ctx.has_bias, ctx.relu = mod, x2, bias is not None, relu
+        ctx.y = y if relu else None
+        if op != mod.out_features:
+            y = y[:, :mod.out_features].contiguous()
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        mod = ctx.mod
+        op, ip = mod.out_pad, mod.in_pad
+        B = dy.shape[0]
+        dy = dy.contiguous()
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        if op != mod.out_features:
+            dy = K.pad_channels(dy, op)
+        if ctx.relu:
+            dy = K.relu_bwd(dy, ctx.y)
+        dy4 = dy.view(B, 1, 1, op)
+        K.conv_wgrad(ctx.x.view(B, 1, 1, ip), dy4, grad_storage_of(mod.weight).view(op, 1, 1, ip),
+                     1, 1, (1, 1), (0, 0))
+        if ctx.has_bias:
+            K.colsum_(dy, grad_storage_of(mod.bias))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w = shadow_of(mod.weight).view(op, 1, 1, ip)
+            dx = K.conv_dgrad(dy4, w, (B, 1, 1, ip), 1, 1, (1, 1), (0, 0)).view(B, ip)
+        ctx.x = ctx.y = None
+        return dx, None, None, None, None
+
+
+class Linear(tnn.Module):
+    def __init__(self, in_features, out_features, bias=True, fused_relu=False):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.in_pad = _round8(in_features)
+        self.out_pad = _round8(out_features)
+        self.fused_relu = fused_relu
+        self.weight = tnn.Parameter(torch.empty(out_features, in_features))
+        self.bias = tnn.Parameter(torch.empty(out_features)) if bias else None
+        # storage padded to 16-byte rows/columns for the MFMA kernels (pad entries stay 0)
+        inf, outf = in_features, out_features
+        self.weight._kml_storage_shape = (self.out_pad, self.in_pad)
+        self.weight._kml_view = lambda st: st[:outf, :inf]
+        if self.bias is not None:
+            self.bias._kml_storage_shape = (self.out_pad,)
+            self.bias._kml_view = lambda st: st[:outf]
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        tnn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            b = 1 / math.sqrt(self.in_features)
+            tnn.init.uniform_(self.bias, -b, b)
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
+
+    def forward(self, x):
+        if not _on_gpu(x):
+            y = F.linear(x, self.weight, self.bias)
+            return F.relu(y) if self.fused_relu else y
+        if x.dim() != 2:
+            x = x.reshape(x.shape[0], -1)
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        if x.shape[1] != self.in_pad:
+            from ..ops import kernels as K
+            x = K.pad_channels(x.contiguous(), self.in_pad)
+        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, self.fused_relu)
+
+
+# ======================================================================================
+# BatchNorm2d (+ fused ReLU / residual)
+# ======================================================================================
+
+class _BNFn(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, mod, relu, res):
+        from ..ops import kernels as K
+        C = x.shape[-1]
+        stats = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        K.memset_(stats)
+        K.bn_stats(x.view(-1, C), stats)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        y = K.bn_apply(x, stats, master_of(weight), master_of(bias), res=res, save_mean=mean, save_rstd=rstd,
+                       run_mean=mod.running_mean if mod.track_running_stats else None,
+                       run_var=mod.running_var if mod.track_running_stats else None,
+                       eps=mod.eps, momentum=mod.momentum if mod.momentum is not None else 0.1, relu=relu)
+        ctx.mod, ctx.x, ctx.y, ctx.mean, ctx.rstd, ctx.relu, ctx.has_res = mod, x, y, mean, rstd, relu, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        mod = ctx.mod
+        dy = dy.contiguous()
+        dres = torch.empty_like(dy) if ctx.has_res else None
+        dx = K.bn_bwd(dy, ctx.y if ctx.relu else None, ctx.x, ctx.mean, ctx.rstd, master_of(mod.weight),
+                      grad_storage_of(mod.weight), grad_storage_of(mod.bias), dres=dres)
+        ctx.x = ctx.y = None
+        return dx, None, None, None, None, dres
+
+
+class BatchNorm2d(tnn.BatchNorm2d):
+    """torch.nn.BatchNorm2d semantics and state_dict, NHWC input, HIP kernels on GPU."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats)
+        if not affine:
+            raise NotImplementedError("affine=False is not supported by the fused kernels")
+
+    def forward(self, x, relu=False, residual=None):
+        if not _on_gpu(x):
+            y = F.batch_norm(x.permute(0, 3, 1, 2), self.running_mean, self.running_var, self.weight, self.bias,
+                             self.training or not self.track_running_stats, self.momentum or 0.1, self.eps)
+            y = y.permute(0, 2, 3, 1)
+            if self.training and self.track_running_stats:
+                self.num_batches_tracked.add_(1)
+            if residual is not None:
+                y = y + residual
+            return F.relu(y) if relu else y
+        x = x.contiguous()
+        if self.training or not self.track_running_stats:
+            if self.track_running_stats:
+                from ..ops import kernels as K
+                K.add_i64_(self.num_batches_tracked)
+            return _BNFn.apply(x, self.weight, self.bias, self, relu, residual)
+        from ..ops import kernels as K
+        return K.bn_apply(x, None, master_of(self.weight), master_of(self.bias), res=residual,
+                          run_mean=self.running_mean, run_var=self.running_var, eps=self.eps, relu=relu,
+                          training=False)
+
+
+# ======================================================================================
+# activations / pooling / shape
+# ======================================================================================
+
+class _ReLUFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        from ..ops import kernels as K
+        y = K.relu_fwd(x)
+        ctx.y = y
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        dx = K.relu_bwd(dy.contiguous(), ctx.y)
+        ctx.y = None
+        return dx
+
+
+class ReLU(tnn.Module):
+    def __init__(self, inplace=False):
+        super().__init__()
+
+    def forward(self, x):
+        if not _on_gpu(x) or x.numel() % 8 or x.dtype != torch.bfloat16:
+            return F.relu(x)
+        return _ReLUFn.apply(x.contiguous())
+
+
+class _MaxPoolFn(Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        from ..ops import kernels as K
+        y, idx = K.maxpool_fwd(x, k, s, p)
+        ctx.idx, ctx.shape, ctx.kp = idx, x.shape, (k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        k, s, p = ctx.kp
+        dx = K.maxpool_bwd(dy.contiguous(), ctx.idx, ctx.shape, k, s, p)
+        ctx.idx = None
+        return dx, None, None, None
+
+
+class MaxPool2d(tnn.Module):
+    def __init__(self, kernel_size, stride=None, padding=0):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.stride = stride if stride is not None else kernel_size
+        self.padding = padding
+
+    def extra_repr(self):
+        return f"kernel_size={self.kernel_size}, stride={self.stride}, padding={self.padding}"
+
+    def forward(self, x):
+        if not _on_gpu(x):
+            return F.max_pool2d(x.permute(0, 3, 1, 2), self.kernel_size, self.stride, self.padding).permute(0, 2, 3, 1)
+        return _MaxPoolFn.apply(x.contiguous(), self.kernel_size, self.stride, self.padding)
+
+
+class _GAvgFn(Function):
+    @staticmethod
+    def forward(ctx, x):
+        from ..ops import kernels as K
+        ctx.shape = x.shape
+        return K.gavgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        return K.gavgpool_bwd(dy.contiguous(), ctx.shape)
+
+
+class AdaptiveAvgPool2d(tnn.Module):
+    """Only output_size=1 (global average); returns [B, C]."""
+
+    def __init__(self, output_size=(1, 1)):
+        super().__init__()
+        if _pair(output_size) != (1, 1):
+            raise NotImplementedError("only global average pooling is supported")
+
+    def forward(self, x):
+        B, H, W, C = x.shape
+        if not _on_gpu(x):
+            return x.mean((1, 2))
+        if H * W == 1:
+            return x.reshape(B, C)  # 1x1 spatial (ResNet on 32x32 input): pooling is the identity
+        return _GAvgFn.apply(x.contiguous())
+
+
+class Flatten(tnn.Module):
+    def forward(self, x):
+        if x.dim() == 4:  # NHWC -> match torch's NCHW flatten order
+            if _on_gpu(x) and x.shape[1] * x.shape[2] == 1:
+                return x.reshape(x.shape[0], -1)
+            return x.permute(0, 3, 1, 2).reshape(x.shape[0], -1)
+        return x.reshape(x.shape[0], -1)
+
+
+def to_nhwc(x, cin_pad=None):
+    """User NCHW input -> the layers' activation layout for its device."""
+    if x.dim() != 4:
+        return x
+    if x.is_cuda:
+        from ..ops import kernels as K
+        if x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and x.is_contiguous():
+            return x  # already NHWC bf16
+        return K.nchw_to_nhwc_bf16(x, cin_pad)
+    y = x.permute(0, 2, 3, 1)
+    return y if y.is_floating_point() else y.float()
+
+
+# ======================================================================================
+# loss
+# ======================================================================================
+
+class _CEFn(Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        from ..ops import kernels as K
+        out3, ws, lab = K.ce_fwd(logits, labels, ignore_index)
+        ctx.save = (logits, lab, ws, out3, ignore_index)
+        ctx.out3 = out3
+        return out3[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..ops import kernels as K
+        logits, lab, ws, out3, ig = ctx.save
+        d = K.ce_bwd(logits, lab, ws, out3, grad_out=g.reshape(1).float().contiguous(), ignore_index=ig)
+        ctx.save = None
+        return d, None, None
+
+
+def cross_entropy(logits, labels, ignore_index=-100, return_correct=False):
+    """Mean softmax cross-entropy (fused HIP kernel on GPU).  With return_correct the
+    device-side argmax==label count of the same pass is returned as well."""
+    if not logits.is_cuda:
+        loss = F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
+        if return_correct:
+            valid = labels != ignore_index
+            return loss, (logits.argmax(1) == labels)[valid].sum().float()
+        return loss
+    if return_correct:
+        from ..ops import kernels as K
+        if torch.is_grad_enabled() and logits.requires_grad:
+            loss = _CEFn.apply(logits.contiguous(), labels, ignore_index)
+            return loss, loss.grad_fn.out3[1]  # grad_fn is the Function ctx; same fused pass
+        out3, _, _ = K.ce_fwd(logits.contiguous(), labels, ignore_index)
+        return out3[0], out3[1]
+    return _CEFn.apply(logits.contiguous(), labels, ignore_index)
+
+
+class CrossEntropyLoss(tnn.Module):
+    def __init__(self, ignore_index=-100):
+        super().__init__()
+        self.ignore_index = ignore_index
+
+    def forward(self, logits, labels):
+        return cross_entropy(logits, labels, self.ignore_index)

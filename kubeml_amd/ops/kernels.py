@@ -1,0 +1,399 @@
+"""Thin, checked launchers for the HIP kernels in ``csrc/kernels``.
+
+Every function here takes torch tensors that already live on an MI355X, validates
+shape / dtype / contiguity on the host (a wrong shape must never reach a kernel),
+allocates outputs from PyTorch's caching allocator and launches on PyTorch's
+current stream — so the calls compose with ``torch.cuda.graph`` capture.
+
+Tensor conventions
+------------------
+* activations: bf16, NHWC contiguous, C % 8 == 0
+* conv weights: bf16 KRSC ``[Cout, KH, KW, Cin]`` contiguous (the bf16 shadow)
+* weight gradients: fp32 KRSC, accumulated (``+=``) into the caller's buffer
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from .._native import HIP
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _s() -> int:
+    return _native.stream_ptr()
+
+
+def _p(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t, dtype, name, ndim=None):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name}: expected {ndim}-d tensor, got shape {tuple(t.shape)}")
+
+
+# --------------------------------------------------------------------------------------
+# convolution (implicit GEMM, MFMA)
+# --------------------------------------------------------------------------------------
+
+_TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32)]
+_TUNED: dict = {}  # (mode, M, N, K) -> (bm, bn, splits); filled by tools/tune_conv.py tables
+
+
+def out_hw(H, W, KH, KW, sh, sw, ph, pw):
+    return (H + 2 * ph - KH) // sh + 1, (W + 2 * pw - KW) // sw + 1
+
+
+def tap_window(H, W, KH, KW, sh, sw, ph, pw):
+    """Taps [r0,r1)x[s0,s1) that touch the image for some output pixel (mirrors the C++)."""
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+
+    def axis(I, O, K, st, p):
+        ok = [t for t in range(K) if any(0 <= o * st - p + t < I for o in range(O))]
+        return (ok[0], ok[-1] + 1) if ok else (0, 0)
+    r0, r1 = axis(H, OH, KH, sh, ph)
+    s0, s1 = axis(W, OW, KW, sw, pw)
+    return r0, r1, s0, s1
+
+
+def _pick_tile(M, N, target=240):
+    best = None
+    for bm, bn in _TILES:
+        if bm > max(32, -(-M // 32) * 32) or bn > max(32, -(-N // 32) * 32):
+            continue
+        blocks = -(-M // bm) * -(-N // bn)
+        if blocks >= target:
+            return bm, bn
+        best = (bm, bn)
+    return best or (32, 32)
+
+
+def plan_conv(mode, M, N, Kd):
+    key = (mode, M, N, Kd)
+    if key in _TUNED:
+        return _TUNED[key]
+    if mode == "wgrad":
+        bm, bn = _pick_tile(M, N, target=10**9)  # smallest tile; parallelism comes from split-K
+        for cand in [(64, 64), (64, 32), (32, 64), (32, 32)]:
+            if cand[0] <= max(32, -(-M // 32) * 32) and cand[1] <= max(32, -(-N // 32) * 32):
+                bm, bn = cand
+                break
+        tiles = -(-M // bm) * -(-N // bn)
+        splits = max(1, min(-(-512 // tiles), Kd // 256))
+        return bm, bn, splits
+    bm, bn = _pick_tile(M, N)
+    return bm, bn, 1
+
+
+def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None):
+    """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats += )."""
+    _chk(x, BF16, "x", 4)
+    _chk(w, BF16, "w", 4)
+    B, H, W, C = x.shape
+    K = w.shape[0]
+    if tuple(w.shape[1:]) != (KH, KW, C):
+        raise ValueError(f"weight shape {tuple(w.shape)} does not match KH={KH} KW={KW} Cin={C}")
+    if C % 8:
+        raise ValueError("Cin must be a multiple of 8 (pad channels)")
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    if out is None:
+        out = torch.empty((B, OH, OW, K), dtype=BF16, device=x.device)
+    if bias is not None:
+        _chk(bias, F32, "bias")
+    if stats is not None:
+        _chk(stats, F32, "stats")
+        assert stats.numel() >= 2 * K
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    bm, bn, _ = plan_conv("fwd", B * OH * OW, K, (r1 - r0) * (s1 - s0) * C)
+    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i s",
+             _p(x), _p(w), _p(out), _p(bias), _p(stats), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
+             int(relu), bm, bn, _s())
+    return out
+
+
+def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None):
+    """dx = conv input gradient (+ addend, the fused residual-gradient sum)."""
+    _chk(dy, BF16, "dy", 4)
+    _chk(w, BF16, "w", 4)
+    B, H, W, C = in_shape
+    K = w.shape[0]
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    if tuple(dy.shape) != (B, OH, OW, K):
+        raise ValueError(f"dy shape {tuple(dy.shape)} != {(B, OH, OW, K)}")
+    if K % 8 or C % 8:
+        raise ValueError("channels must be multiples of 8")
+    if out is None:
+        out = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    if addend is not None:
+        _chk(addend, BF16, "addend")
+        assert addend.shape == out.shape
+    bm, bn, _ = plan_conv("dgrad", B * H * W, C, (r1 - r0) * (s1 - s0) * K)
+    HIP.call("kml_conv_dgrad", "p p p p i i i i i i i i i i i i i s",
+             _p(dy), _p(w), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, _s())
+    return out
+
+
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad):
+    """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient."""
+    _chk(x, BF16, "x", 4)
+    _chk(dy, BF16, "dy", 4)
+    _chk(dw, F32, "dw", 4)
+    B, H, W, C = x.shape
+    K = dy.shape[3]
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    if tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
+        raise ValueError("wgrad shape mismatch")
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    bm, bn, splits = plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW)
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i s",
+             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, splits, 1, _s())
+    return dw
+
+
+# --------------------------------------------------------------------------------------
+# batch norm / relu / elementwise
+# --------------------------------------------------------------------------------------
+
+def bn_stats(x2d, stats):
+    _chk(x2d, BF16, "x")
+    M, C = x2d.numel() // x2d.shape[-1], x2d.shape[-1]
+    HIP.call("kml_bn_stats", "p p l i s", _p(x2d), _p(stats), M, C, _s())
+
+
+def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=None, run_mean=None,
+             run_var=None, eps=1e-5, momentum=0.1, relu=False, training=True):
+    _chk(x, BF16, "x")
+    C = x.shape[-1]
+    M = x.numel() // C
+    if y is None:
+        y = torch.empty_like(x)
+    if res is not None:
+        _chk(res, BF16, "res")
+        if res.shape != x.shape:
+            raise ValueError("residual shape mismatch")
+    HIP.call("kml_bn_apply", "p p p p p p p p p p l i f f i i s",
+             _p(x), _p(stats), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
+             _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu),
+             0 if training else 1, _s())
+    return y
+
+
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
+    """dgamma/dbeta (+=) and dx; y given => ReLU mask applied; dres (optional) receives dz."""
+    _chk(dy, BF16, "dy")
+    _chk(x, BF16, "x")
+    C = x.shape[-1]
+    M = x.numel() // C
+    if dx is None:
+        dx = torch.empty_like(x)
+    HIP.call("kml_bn_bwd", "p p p p p p p p p p l i s",
+             _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
+             _p(dres), M, C, _s())
+    return dx
+
+
+def relu_fwd(x):
+    y = torch.empty_like(x)
+    HIP.call("kml_relu_fwd", "p p l s", _p(x), _p(y), x.numel(), _s())
+    return y
+
+
+def relu_bwd(dy, y):
+    dx = torch.empty_like(dy)
+    HIP.call("kml_relu_bwd", "p p p l s", _p(dy), _p(y), _p(dx), dy.numel(), _s())
+    return dx
+
+
+def add_bf16(a, b, out=None):
+    out = torch.empty_like(a) if out is None else out
+    HIP.call("kml_add_bf16", "p p p l s", _p(a), _p(b), _p(out), a.numel(), _s())
+    return out
+
+
+def memset_(t, value=0):
+    HIP.call("kml_memset", "p i l s", _p(t), int(value), t.numel() * t.element_size(), _s())
+    return t
+
+
+def f32_to_bf16(x, out=None):
+    out = torch.empty(x.shape, dtype=BF16, device=x.device) if out is None else out
+    HIP.call("kml_f32_to_bf16", "p p l s", _p(x), _p(out), x.numel(), _s())
+    return out
+
+
+def scale_(x, a):
+    HIP.call("kml_scale_f32", "p f l s", _p(x), float(a), x.numel(), _s())
+    return x
+
+
+# --------------------------------------------------------------------------------------
+# pooling
+# --------------------------------------------------------------------------------------
+
+def maxpool_fwd(x, k, s, p):
+    _chk(x, BF16, "x", 4)
+    B, H, W, C = x.shape
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    y = torch.empty((B, OH, OW, C), dtype=BF16, device=x.device)
+    idx = torch.empty((B, OH, OW, C), dtype=torch.uint8, device=x.device)
+    HIP.call("kml_maxpool_fwd", "p p p i i i i i i i s", _p(x), _p(y), _p(idx), B, H, W, C, k, s, p, _s())
+    return y, idx
+
+
+def maxpool_bwd(dy, idx, in_shape, k, s, p):
+    B, H, W, C = in_shape
+    dx = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    HIP.call("kml_maxpool_bwd", "p p p i i i i i i i s", _p(dy), _p(idx), _p(dx), B, H, W, C, k, s, p, _s())
+    return dx
+
+
+def gavgpool_fwd(x):
+    B, H, W, C = x.shape
+    y = torch.empty((B, C), dtype=BF16, device=x.device)
+    HIP.call("kml_gavgpool_fwd", "p p i i i s", _p(x), _p(y), B, H * W, C, _s())
+    return y
+
+
+def gavgpool_bwd(dy, in_shape):
+    B, H, W, C = in_shape
+    dx = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    HIP.call("kml_gavgpool_bwd", "p p i i i s", _p(dy), _p(dx), B, H * W, C, _s())
+    return dx
+
+
+# --------------------------------------------------------------------------------------
+# loss
+# --------------------------------------------------------------------------------------
+
+def ce_fwd(logits, labels, ignore_index=-100):
+    """Returns (out3, ws): out3 = [mean loss, correct, valid] fp32 on device."""
+    if logits.dim() != 2:
+        raise ValueError("logits must be [B, C]")
+    if not logits.is_contiguous():
+        logits = logits.contiguous()
+    dt = {BF16: 0, F32: 1}[logits.dtype]
+    B, C = logits.shape
+    labels = labels.to(torch.int64).contiguous()
+    ws = torch.empty(3 * B, dtype=F32, device=logits.device)
+    out3 = torch.empty(3, dtype=F32, device=logits.device)
+    HIP.call("kml_ce_fwd", "p p p p i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), B, C,
+             int(ignore_index), dt, _s())
+    return out3, ws, labels
+
+
+def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100):
+    dt = {BF16: 0, F32: 1}[logits.dtype]
+    B, C = logits.shape
+    d = torch.empty_like(logits)
+    HIP.call("kml_ce_bwd", "p p p p p p i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
+             _p(d), B, C, int(ignore_index), dt, _s())
+    return d
+
+
+# --------------------------------------------------------------------------------------
+# optimizers
+# --------------------------------------------------------------------------------------
+
+def sgd_(w, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=False, first=False,
+         grad_scale=1.0, lr_dev=None):
+    n = w.numel()
+    HIP.call("kml_sgd", "p p p p p f f f f i i f l s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
+             float(lr), float(wd), float(momentum), float(dampening), int(nesterov), int(first),
+             float(grad_scale), n, _s())
+
+
+def adam_(w, g, m, v, shadow, lr, step, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, decoupled=False,
+          grad_scale=1.0, lr_dev=None, step_dev=None):
+    n = w.numel()
+    HIP.call("kml_adam", "p p p p p p p f f f f f f i f l s", _p(w), _p(g), _p(m), _p(v), _p(shadow),
+             _p(lr_dev), _p(step_dev), float(lr), float(step), float(b1), float(b2), float(eps), float(wd),
+             int(decoupled), float(grad_scale), n, _s())
+
+
+def increment_(t, by=1.0):
+    HIP.call("kml_increment", "p f s", _p(t), float(by), _s())
+
+
+def clip_grad_norm_(g, ws1, max_norm):
+    HIP.call("kml_clip_grad_norm", "p p f l s", _p(g), _p(ws1), float(max_norm), g.numel(), _s())
+
+
+def scale_inv_dev_(x, count):
+    HIP.call("kml_scale_inv_dev", "p p l s", _p(x), _p(count), x.numel(), _s())
+
+
+# --------------------------------------------------------------------------------------
+# data
+# --------------------------------------------------------------------------------------
+
+def augment(src_u8, labels_src, ctr, B, out=None, labels_out=None, CP=8, pad=4, flip=True, train=True,
+            mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
+    """src_u8 [N,H,W,C] uint8 on device -> [B,H,W,CP] bf16 normalised batch starting at ctr[2]."""
+    N, H, W, C = src_u8.shape
+    if out is None:
+        out = torch.empty((B, H, W, CP), dtype=BF16, device=src_u8.device)
+    if labels_out is None:
+        labels_out = torch.empty((B,), dtype=torch.int64, device=src_u8.device)
+    mean_a = (torch.tensor(list(mean) + [0.0] * (4 - len(mean)), dtype=F32))
+    std_a = (torch.tensor(list(std) + [1.0] * (4 - len(std)), dtype=F32))
+    HIP.call("kml_augment", "p p p p p i i i i i i i i i p p s", _p(src_u8), _p(labels_src), _p(out),
+             _p(labels_out), _p(ctr), N, H, W, C, CP, B, pad, int(flip), int(train),
+             mean_a.data_ptr(), std_a.data_ptr(), _s())
+    return out, labels_out
+
+
+# --------------------------------------------------------------------------------------
+# layout / misc
+# --------------------------------------------------------------------------------------
+
+def colsum_(x2d, out):
+    """out (fp32, [C]) += column sums of bf16 [M, C]."""
+    _chk(x2d, BF16, "x")
+    C = x2d.shape[-1]
+    HIP.call("kml_colsum_bf16", "p p l i s", _p(x2d), _p(out), x2d.numel() // C, C, _s())
+    return out
+
+
+def add_i64_(t, v=1):
+    HIP.call("kml_add_i64", "p l i s", _p(t), int(v), t.numel(), _s())
+
+
+def pad_channels(x, CP):
+    _chk(x, BF16, "x")
+    C = x.shape[-1]
+    y = torch.empty(x.shape[:-1] + (CP,), dtype=BF16, device=x.device)
+    HIP.call("kml_pad_channels", "p p l i i s", _p(x), _p(y), x.numel() // C, C, CP, _s())
+    return y
+
+
+def nchw_to_nhwc_bf16(x, CP=None):
+    """User NCHW fp32 tensor -> NHWC bf16 with channels padded to a multiple of 8."""
+    x = x.float().contiguous()
+    B, C, H, W = x.shape
+    CP = CP or -(-C // 8) * 8
+    y = torch.empty((B, H, W, CP), dtype=BF16, device=x.device)
+    HIP.call("kml_nchw_to_nhwc_bf16", "p p i i i i s", _p(x), _p(y), B, C, H * W, CP, _s())
+    return y
+
+
+def advance_counter_(ctr, batch, n):
+    """ctr = [seed, step, start]: step += 1, start = (start + batch) mod n (device-side)."""
+    HIP.call("kml_advance_counter", "p f f s", _p(ctr), float(batch), float(n), _s())

@@ -1,0 +1,249 @@
+"""Fused optimizers over the flat parameter space (one HIP launch per step).
+
+``SGD`` / ``Adam`` / ``AdamW`` accept the same arguments as their ``torch.optim``
+counterparts.  When the parameters live in :class:`~kubeml_amd.nn.flat.FlatParamSpace`
+buffers (the GPU path) the step is one ``kml_sgd`` / ``kml_adam`` launch per space
+that also refreshes the bf16 shadow copy; otherwise (CPU) it defers to the stock
+torch implementation so CPU-only plumbing tests share the exact same semantics.
+
+The learning rate lives in a device scalar (``lr_tensor``) so a graph-captured step
+follows LR changes (``set_lr``) without re-capture, and Adam's step counter is a
+device scalar incremented inside the captured region.
+
+``reset_state()`` implements the reference's per-round optimizer reset under K-step
+averaging (python/kubeml/kubeml/network.py:121-128): a memset of the state buffers.
+
+``from_torch(opt)`` converts a user's ``torch.optim.SGD/Adam/AdamW`` (what
+``KubeModel.configure_optimizers`` returns in reference code) into the fused one
+with identical hyper-parameters.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+
+__all__ = ["SGD", "Adam", "AdamW", "from_torch", "FusedOptimizer"]
+
+
+def _spaces(params):
+    """Group params by their flat space (None for params without one)."""
+    groups: Dict[int, tuple] = {}
+    loose = []
+    for p in params:
+        sp = getattr(p, "_kml_flat", None)
+        if sp is None:
+            loose.append(p)
+        else:
+            groups.setdefault(id(sp), (sp, []))[1].append(p)
+    return [g for g in groups.values()], loose
+
+
+class FusedOptimizer(torch.optim.Optimizer):
+    kind = "base"
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self._state_bufs: Dict[int, Dict[str, torch.Tensor]] = {}
+        self._lr_dev: Dict[torch.device, torch.Tensor] = {}
+        self._grad_scale = 1.0
+        self._first = True
+        self._step_dev: Dict[torch.device, torch.Tensor] = {}
+        self._step_host = 0
+
+    # --- device scalars -------------------------------------------------------------
+    def lr_tensor(self, device):
+        t = self._lr_dev.get(device)
+        if t is None:
+            t = torch.full((1,), float(self.param_groups[0]["lr"]), dtype=torch.float32, device=device)
+            self._lr_dev[device] = t
+        return t
+
+    def set_lr(self, lr: float):
+        for g in self.param_groups:
+            g["lr"] = lr
+        for t in self._lr_dev.values():
+            t.fill_(float(lr))
+
+    def set_grad_scale(self, s: float):
+        """Folded into the step: the DP all-reduce SUMs, the optimizer averages."""
+        self._grad_scale = float(s)
+
+    def _flat_groups(self):
+        ps = [p for g in self.param_groups for p in g["params"]]
+        return _spaces(ps)
+
+    def zero_grad(self, set_to_none: bool = False):
+        spaces, loose = self._flat_groups()
+        for sp, _ in spaces:
+            sp.zero_grad()
+        for p in loose:
+            if p.grad is not None:
+                if set_to_none:
+                    p.grad = None
+                else:
+                    p.grad.zero_()
+
+    def reset_state(self):
+        """Zero every optimizer state buffer (K-AVG round boundary)."""
+        from ..ops import kernels as K
+        for bufs in self._state_bufs.values():
+            for t in bufs.values():
+                if t.is_cuda:
+                    K.memset_(t)
+                else:
+                    t.zero_()
+        self.state.clear()
+        self._first = True
+        self._step_host = 0
+        for t in self._step_dev.values():
+            t.zero_()
+
+    def _bufs(self, sp, names):
+        key = id(sp)
+        d = self._state_bufs.get(key)
+        if d is None:
+            d = {n: torch.zeros(sp.numel, dtype=torch.float32, device=sp.device) for n in names}
+            self._state_bufs[key] = d
+        return d
+
+
+class SGD(FusedOptimizer):
+    kind = "sgd"
+
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
+                                      weight_decay=weight_decay, nesterov=nesterov))
+        if len(self.param_groups) > 1:
+            raise ValueError("fused SGD supports a single param group")
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        spaces, loose = self._flat_groups()
+        for sp, members in spaces:
+            if sp.device.type != "cuda":
+                loose += members
+                continue
+            from ..ops import kernels as K
+            mom = self._bufs(sp, ["momentum"])["momentum"] if g["momentum"] != 0 else None
+            K.sgd_(sp.master, sp.grad, mom, sp.shadow, g["lr"], wd=g["weight_decay"], momentum=g["momentum"],
+                   dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
+                   grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device))
+        if loose:
+            _torch_sgd(loose, g, self.state, self._grad_scale)
+        self._first = False
+        return loss
+
+
+def _torch_sgd(params, g, state, grad_scale):
+    for p in params:
+        if p.grad is None:
+            continue
+        d = p.grad * grad_scale if grad_scale != 1.0 else p.grad
+        if g["weight_decay"]:
+            d = d.add(p, alpha=g["weight_decay"])
+        if g["momentum"]:
+            st = state.setdefault(p, {})
+            buf = st.get("momentum_buffer")
+            if buf is None:
+                buf = d.clone().detach()
+                st["momentum_buffer"] = buf
+            else:
+                buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+            d = d.add(buf, alpha=g["momentum"]) if g["nesterov"] else buf
+        p.add_(d, alpha=-g["lr"])
+
+
+class Adam(FusedOptimizer):
+    kind = "adam"
+    decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        if len(self.param_groups) > 1:
+            raise ValueError("fused Adam supports a single param group")
+
+    def step_tensor(self, device):
+        t = self._step_dev.get(device)
+        if t is None:
+            t = torch.zeros(1, dtype=torch.float32, device=device)
+            self._step_dev[device] = t
+        return t
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        spaces, loose = self._flat_groups()
+        self._step_host += 1
+        for sp, members in spaces:
+            if sp.device.type != "cuda":
+                loose += members
+                continue
+            from ..ops import kernels as K
+            st = self._step_dev_inc(sp.device)
+            bufs = self._bufs(sp, ["exp_avg", "exp_avg_sq"])
+            K.adam_(sp.master, sp.grad, bufs["exp_avg"], bufs["exp_avg_sq"], sp.shadow, g["lr"], 0.0, b1, b2,
+                    g["eps"], g["weight_decay"], self.decoupled, self._grad_scale,
+                    lr_dev=self.lr_tensor(sp.device), step_dev=st)
+        if loose:
+            _torch_adam(loose, g, self.state, self._grad_scale, self.decoupled)
+        return loss
+
+    def _step_dev_inc(self, device):
+        from ..ops import kernels as K
+        t = self.step_tensor(device)
+        K.increment_(t, 1.0)
+        return t
+
+
+class AdamW(Adam):
+    kind = "adamw"
+    decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, lr, betas, eps, weight_decay)
+
+
+def _torch_adam(params, g, state, grad_scale, decoupled):
+    b1, b2 = g["betas"]
+    for p in params:
+        if p.grad is None:
+            continue
+        st = state.setdefault(p, {})
+        if not st:
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros_like(p)
+            st["exp_avg_sq"] = torch.zeros_like(p)
+        st["step"] += 1
+        t = st["step"]
+        gr = p.grad * grad_scale
+        if decoupled:
+            p.mul_(1 - g["lr"] * g["weight_decay"])
+        elif g["weight_decay"]:
+            gr = gr.add(p, alpha=g["weight_decay"])
+        st["exp_avg"].mul_(b1).add_(gr, alpha=1 - b1)
+        st["exp_avg_sq"].mul_(b2).addcmul_(gr, gr, value=1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        denom = (st["exp_avg_sq"].sqrt() / (bc2 ** 0.5)).add_(g["eps"])
+        p.addcdiv_(st["exp_avg"], denom, value=-g["lr"] / bc1)
+
+
+def from_torch(opt: torch.optim.Optimizer) -> FusedOptimizer:
+    """Fused equivalent of a stock torch optimizer (same params and hyper-parameters)."""
+    if isinstance(opt, FusedOptimizer):
+        return opt
+    params = [p for g in opt.param_groups for p in g["params"]]
+    g = opt.param_groups[0]
+    if isinstance(opt, torch.optim.AdamW):
+        return AdamW(params, lr=g["lr"], betas=g["betas"], eps=g["eps"], weight_decay=g["weight_decay"])
+    if isinstance(opt, torch.optim.Adam):
+        return Adam(params, lr=g["lr"], betas=g["betas"], eps=g["eps"], weight_decay=g["weight_decay"])
+    if isinstance(opt, torch.optim.SGD):
+        return SGD(params, lr=g["lr"], momentum=g["momentum"], dampening=g["dampening"],
+                   weight_decay=g["weight_decay"], nesterov=g["nesterov"])
+    raise TypeError(f"no fused equivalent for {type(opt).__name__}")

@@ -1,0 +1,195 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference of the same op.
+
+Inputs are rounded to bf16 first, so the reference sees exactly the values the
+kernel sees; tolerances cover fp32 accumulation-order differences and the final
+bf16 rounding of outputs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _rel(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CONV_CASES = [
+    # B, H, W, Cin, Cout, k, stride, pad
+    (4, 32, 32, 8, 64, 7, 2, 3),     # ResNet stem (Cin padded 3->8)
+    (8, 8, 8, 64, 64, 3, 1, 1),      # layer1
+    (8, 8, 8, 64, 128, 3, 2, 1),     # layer2.0.conv1
+    (8, 8, 8, 64, 128, 1, 2, 0),     # layer2 downsample
+    (8, 4, 4, 128, 128, 3, 1, 1),
+    (8, 2, 2, 256, 512, 3, 2, 1),    # layer4.0.conv1 (2x2 -> 1x1)
+    (16, 1, 1, 512, 512, 3, 1, 1),   # layer4 (centre tap only)
+    (3, 5, 7, 16, 24, 3, 1, 1),      # ragged
+    (33, 1, 1, 512, 1000, 1, 1, 0),  # Linear as 1x1 conv (N not multiple of 32)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    from kubeml_amd.ops import kernels as K
+    B, H, W, Ci, Co, k, s, p = case
+    torch.manual_seed(0)
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * (1.0 / (k * k * Ci) ** 0.5))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=s, padding=p)
+    stats = torch.zeros(2 * Co, device=dev)
+    y = K.conv_fwd(x, w, k, k, (s, s), (p, p), stats=stats)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    yf = yr.detach().permute(0, 2, 3, 1).reshape(-1, Co)
+    assert torch.allclose(stats[:Co], yf.sum(0), rtol=2e-2, atol=1e-1 * (yf.shape[0] ** 0.5))
+    assert _rel(stats[Co:], (yf * yf).sum(0)) < 2e-2
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    dx = K.conv_dgrad(dyn, w, x.shape, k, k, (s, s), (p, p))
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    dw = torch.zeros(Co, k, k, Ci, device=dev)
+    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p))
+    assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < 1e-2
+
+
+def test_conv_fwd_bias_relu():
+    from kubeml_amd.ops import kernels as K
+    x = _bf(torch.randn(8, 6, 6, 16, device=dev))
+    w = _bf(torch.randn(32, 3, 3, 16, device=dev) * 0.1)
+    b = torch.randn(32, device=dev)
+    y = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), bias=b, relu=True)
+    yr = F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1))
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+
+
+@pytest.mark.parametrize("C,M,relu,res", [(64, 4096, True, False), (128, 1000, True, True), (512, 64, False, True)])
+def test_bn_train_fwd_bwd(C, M, relu, res):
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(1)
+    x = _bf(torch.randn(M, C, device=dev) * 2 + 0.5)
+    r = _bf(torch.randn(M, C, device=dev)) if res else None
+    g = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    rm = torch.zeros(C, device=dev)
+    rv = torch.ones(C, device=dev)
+    stats = torch.zeros(2 * C, device=dev)
+    K.bn_stats(x, stats)
+    mean = torch.empty(C, device=dev)
+    rstd = torch.empty(C, device=dev)
+    y = K.bn_apply(x, stats, g, b, res=r, save_mean=mean, save_rstd=rstd, run_mean=rm, run_var=rv, relu=relu)
+    # reference
+    xr = x.float().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    rmr = torch.zeros(C, device=dev)
+    rvr = torch.ones(C, device=dev)
+    yr = F.batch_norm(xr, rmr, rvr, gr, br, training=True, momentum=0.1, eps=1e-5)
+    if res:
+        yr = yr + r.float()
+    if relu:
+        yr = F.relu(yr)
+    assert _rel(y, yr) < 1e-2
+    assert torch.allclose(rm, rmr, atol=1e-3) and torch.allclose(rv, rvr, rtol=1e-2, atol=1e-3)
+    dy = _bf(torch.randn(M, C, device=dev))
+    yr.backward(dy.float())
+    dg = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    dres = torch.empty_like(x) if res else None
+    dx = K.bn_bwd(dy, y if relu else None, x, mean, rstd, g, dg, db, dres=dres)
+    assert _rel(dx, xr.grad) < 2e-2
+    assert _rel(dg, gr.grad) < 1e-2
+    assert _rel(db, br.grad) < 1e-2
+
+
+def test_maxpool_and_gavg():
+    from kubeml_amd.ops import kernels as K
+    x = _bf(torch.randn(4, 16, 16, 64, device=dev))
+    y, idx = K.maxpool_fwd(x, 3, 2, 1)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.permute(0, 3, 1, 2).float(), yr)
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dx = K.maxpool_bwd(dy.permute(0, 2, 3, 1).contiguous(), idx, x.shape, 3, 2, 1)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    g = K.gavgpool_fwd(x)
+    assert _rel(g, x.float().mean((1, 2))) < 1e-2
+    gd = K.gavgpool_bwd(_bf(torch.ones(4, 64, device=dev)), x.shape)
+    assert torch.allclose(gd.float(), torch.full_like(gd.float(), 1 / 256))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy(dtype):
+    from kubeml_amd.ops import kernels as K
+    logits = (torch.randn(37, 1000, device=dev) * 3).to(dtype)
+    labels = torch.randint(0, 1000, (37,), device=dev)
+    labels[3] = -100
+    out3, ws, lab = K.ce_fwd(logits, labels)
+    lr = logits.float().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, ignore_index=-100)
+    assert abs(out3[0].item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    valid = labels != -100
+    correct = (lr.argmax(1) == labels)[valid].sum().item()
+    assert int(out3[1].item()) == correct and int(out3[2].item()) == int(valid.sum())
+    ref.backward()
+    go = torch.tensor([2.0], device=dev)
+    d = K.ce_bwd(logits, lab, ws, out3, grad_out=go)
+    assert _rel(d, 2 * lr.grad) < 1e-2
+
+
+def test_sgd_adam():
+    from kubeml_amd.ops import kernels as K
+    n = 10007
+    w = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    mom = torch.zeros(n, device=dev)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    wr = w.clone().requires_grad_(False)
+    opt = torch.optim.SGD([torch.nn.Parameter(wr)], lr=0.1, momentum=0.9, weight_decay=1e-4)
+    p = opt.param_groups[0]["params"][0]
+    for it in range(3):
+        p.grad = g.clone()
+        opt.step()
+        K.sgd_(w, g, mom, sh, 0.1, wd=1e-4, momentum=0.9, first=(it == 0))
+    assert torch.allclose(w, p.data, atol=1e-5)
+    assert torch.allclose(sh.float(), w, rtol=1e-2, atol=1e-2)
+    # adamw
+    w2 = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    p2 = torch.nn.Parameter(w2.clone())
+    opt2 = torch.optim.AdamW([p2], lr=1e-3, weight_decay=0.01)
+    for it in range(3):
+        p2.grad = g.clone()
+        opt2.step()
+        K.adam_(w2, g, m, v, None, 1e-3, it + 1, wd=0.01, decoupled=True)
+    assert torch.allclose(w2, p2.data, atol=1e-5)
+
+
+def test_augment():
+    from kubeml_amd.ops import kernels as K
+    N = 50
+    src = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, 10, (N,), device=dev)
+    ctr = torch.tensor([7.0, 3.0, 40.0], device=dev)
+    out, lo = K.augment(src, lab, ctr, 16, train=False)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=dev)
+    std = torch.tensor([0.229, 0.224, 0.225], device=dev)
+    idx = (torch.arange(16, device=dev) + 40) % N
+    ref = (src[idx].float() / 255 - mean) / std
+    assert _rel(out[..., :3], ref) < 1e-2
+    assert (out[..., 3:] == 0).all()
+    assert torch.equal(lo, lab[idx])
+    out2, _ = K.augment(src, lab, ctr, 16, train=True)
+    assert out2.shape == (16, 32, 32, 8)
