@@ -3,65 +3,95 @@
 // One kernel family covers the three convolution GEMMs of training (and Linear
 // layers, which are 1x1 convolutions over a 1x1 image):
 //
-//   FWD   : Y[m=(b,oh,ow)][n=cout]    = sum_k  im2col(X)[m][k=(tap,cin)] * W[n][k]
-//   DGRAD : dX[m=(b,ih,iw)][n=cin]    = sum_k  dY[(b,oh,ow)][cout] * W[cout][tap][cin]   k=(tap,cout)
-//   WGRAD : dW[m=cout][n=(tap,cin)]  += sum_k  dY[k=pixel][cout]  * im2col(X)[k][n]      (split-K, fp32 atomics)
+//   FWD   : Y[m=(b,oh,ow)][n=cout]   = sum_k im2col(X)[m][k=(tap,cin)] * W[n][k]
+//   DGRAD : dX[m=(b,ih,iw)][n=cin]   = sum_k dY[(b,oh,ow)][cout] * W[cout][tap][cin],  k=(tap,cout)
+//   WGRAD : dW[m=cout][n=(tap,cin)] += sum_k dY[k=pixel][cout] * im2col(X)[k][n]
 //
 // Layouts: activations NHWC bf16 (C % 8 == 0), weights KRSC bf16 ([Cout][KH][KW][Cin]),
-// weight gradients KRSC fp32 (written straight into the flat fp32 gradient buffer the
-// all-reduce and the fused optimizer consume).
+// weight gradients KRSC fp32 — written straight into the flat fp32 gradient buffer that
+// RCCL all-reduces and the fused optimizer consumes.
 //
-// Tiling (CDNA4): 256 threads = 4 wave64 in a 2x2 grid, each wave owns a
-// (BM/2)x(BN/2) sub-tile built from v_mfma_f32_16x16x32_bf16 fragments; BK = 32.
-// Operands are staged global->registers->LDS (16 B per lane) with a two-buffer LDS
-// ring and one barrier per K-step.  An operand whose K axis is contiguous in memory
-// lives in LDS as [row][k] and is read with ds_read_b128; an operand whose K axis is
-// strided (dgrad weights, both wgrad operands) lives as [k][row] in its natural memory
-// order and is read with the gfx950 transposing read ds_read_b64_tr_b16, so no
-// transpose pass or transposed weight copy is ever materialised.
-//
-// Only the convolution taps that can touch the image for SOME output pixel
-// ([r0,r1) x [s0,s1), computed on the host) are enumerated: on ResNet-34's layer4
-// (1x1 spatial at 32x32 input) a 3x3 conv degenerates to its centre tap and the
-// GEMM K shrinks 9x.
-//
-// Epilogue options (FWD): fp32 bias, ReLU, and per-channel BatchNorm statistics
-// (sum, sum of squares) accumulated from the fp32 accumulators with wave
-// reductions + one atomic per (wave, channel) — this removes BN's stats pass.
+// CDNA4 mapping
+// -------------
+// * 256 threads = 4 wave64 in a 2x2 grid; each wave owns a (BM/2)x(BN/2) sub-tile of
+//   v_mfma_f32_16x16x32_bf16 fragments; BK = 32 or 64 (1 or 2 MFMA k-substeps).
+// * Software pipeline, prefetch distance 2: two register stages hold K-tiles t+1 and
+//   t+2 in flight while the MFMAs consume tile t from a two-buffer LDS ring (one
+//   barrier per K-step).  Every global load is unconditional — out-of-range chunks
+//   (conv padding, ragged edges, split-K tails) are redirected to a zero page instead
+//   of being branched around — so hipcc emits counted vmcnt waits rather than the
+//   vmcnt(0)-per-load it generates for branch-guarded loads (CDNA guide §5, trap (c)),
+//   and the loop body is a straight line.
+// * Index math is hoisted: per-thread pixel/row state is computed once; when a K-tile
+//   stays inside one filter tap (Cin % BK == 0, every ResNet layer but the stem) the tap
+//   is block-uniform scalar math; remaining divisions use host-precomputed
+//   multiply-shift magic numbers.
+// * An operand whose K axis is contiguous in memory lives in LDS as [row][k] (+16 B pad,
+//   conflict-free ds_read_b128); an operand whose K axis is strided (dgrad weights, both
+//   wgrad operands) lives as [k][row] in its natural order and is read with the gfx950
+//   transposing ds_read_b64_tr_b16 — no transpose pass, no transposed weight copy.
+// * Only taps touching the image for SOME output pixel are enumerated ([r0,r1)x[s0,s1),
+//   host-computed): ResNet-34's layer4 (1x1 spatial at 32x32 input) runs its 3x3
+//   convolutions as centre-tap GEMMs, 9x less K.
+// * Split-K for latency-bound small-M layers.  FWD/DGRAD: each split writes its fp32
+//   partial tile to a slab (fragment order, coalesced float4), releases at agent scope,
+//   takes a ticket; the last arriver acquires, sums the slabs in split order
+//   (deterministic) and runs the epilogue; tickets are reset by the last arriver
+//   (graph-replay safe, no memset per call).  WGRAD: fp32 atomics into the
+//   zeroed-per-step gradient buffer.
+// * Epilogues: FWD bias / ReLU / per-channel BatchNorm sum+sumsq from the fp32 values
+//   (BN needs no statistics pass); DGRAD adds an optional bf16 addend (the other
+//   branch of a residual block) so gradient merges need no add kernel.
 //
 // Reference parity: the reference runs these convolutions through cuDNN inside the
 // user's torch module (ml/experiments/kubeml/function_resnet34.py:72-76).
 #include "kml_common.h"
 
+#include <type_traits>
+
 namespace {
 
-constexpr int BK = 32;
-constexpr int PADK = 8;   // K-contiguous LDS rows: 40 bf16 = 80 B (conflict-free b128 reads)
-constexpr int PADR = 8;   // K-strided LDS rows: R+8 bf16
+constexpr int PADK = 8;  // K-contiguous LDS rows: BK+8 bf16
+constexpr int PADR = 8;  // K-strided LDS rows: R+8 bf16
 
 enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
 
+// n / d for 0 <= n < 2^31 via multiply-shift (host computes m, s)
+struct FastDiv {
+  unsigned m;
+  int s;
+  int d;
+};
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)(((unsigned long long)(unsigned)n * f.m) >> f.s);
+}
+
 struct ConvArgs {
-  const bf16_t* x;    // input activations NHWC (FWD, WGRAD)
-  const bf16_t* w;    // weights KRSC (FWD, DGRAD)
-  const bf16_t* dy;   // output grads NHWC (DGRAD, WGRAD)
-  bf16_t* out;        // Y (FWD) or dX (DGRAD)
-  float* dw;          // fp32 weight grads KRSC (WGRAD)
-  float* stats;       // [2][Cout] BN sum / sumsq (FWD, optional)
-  const float* bias;  // [Cout] (FWD, optional)
-  const bf16_t* addend; // [M][N] added to the DGRAD output (fused residual-gradient sum)
-  int B, H, W, C;     // input geometry (C = Cin)
-  int OH, OW, K;      // output geometry (K = Cout)
+  const bf16_t* x;       // input activations NHWC (FWD, WGRAD)
+  const bf16_t* w;       // weights KRSC (FWD, DGRAD)
+  const bf16_t* dy;      // output grads NHWC (DGRAD, WGRAD)
+  const bf16_t* zp;      // 16-byte zero page (target of out-of-range loads)
+  bf16_t* out;           // Y (FWD) or dX (DGRAD)
+  float* dw;             // fp32 weight grads KRSC (WGRAD)
+  float* stats;          // [2][Cout] BN sum / sumsq (FWD, optional)
+  const float* bias;     // [Cout] (FWD, optional)
+  const bf16_t* addend;  // [M][N] added to the DGRAD output
+  float* slab;           // split-K partial tiles (FWD/DGRAD, splits > 1)
+  unsigned* counters;    // split-K tickets, one per output tile
+  int B, H, W, C;        // input geometry (C = Cin)
+  int OH, OW, K;         // output geometry (K = Cout)
   int KH, KW, sh, sw, ph, pw;
-  int r0, r1, s0, s1; // valid tap window
-  int M, N, Kd;       // GEMM dims
-  int Kp;             // DGRAD: Cout padded to a multiple of BK (K index = tap*Kp + cout)
-  int kchunk;         // WGRAD split-K chunk (multiple of BK)
-  int relu;           // FWD epilogue ReLU
-  int accumulate;     // WGRAD: atomicAdd (1) or store (0)
+  int r0, r1, s0, s1;    // valid tap window
+  int M, N, Kd;          // GEMM dims
+  int Kp;                // DGRAD: Cout padded to a multiple of BK (k = tap*Kp + cout)
+  int kchunk;            // split-K chunk (multiple of BK)
+  int splits;
+  int relu;
+  int accumulate;        // WGRAD: atomicAdd (1) or store (0)
+  FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
-template <int R, bool KCONTIG>
+template <int R, bool KCONTIG, int BK>
 struct TileShape {
   static constexpr int ELEMS = KCONTIG ? R * (BK + PADK) : BK * (R + PADR);
   static constexpr int CHUNKS = R * BK / 8;  // 16-byte chunks per stage
@@ -70,113 +100,171 @@ struct TileShape {
 
 __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
-// ---- operand loaders: return the 16-byte chunk q of K-tile kt (zeros when out of range) ----
+__device__ __forceinline__ void tap_rs(const ConvArgs& a, int tap, int& r, int& s) {
+  const int tr = fdiv(tap, a.fd_nts);
+  r = a.r0 + tr;
+  s = a.s0 + (tap - tr * a.fd_nts.d);
+}
 
-// A of FWD: im2col(X), row = output pixel, K-contiguous (chunk = 8 input channels of one tap)
-struct FwdA {
-  int valid, b, ih0, iw0;
-  __device__ void init(const ConvArgs& a, int m) {
+// ---------------------------------------------------------------------------------
+// Chunk address generators.  Each thread owns PER_THREAD 16-byte chunks of a stage;
+// init() runs once, ptr(kb) returns the global address for K-tile base kb (or the
+// zero page).  TAPU: the whole K-tile lies in one filter tap (block-uniform tap).
+// ---------------------------------------------------------------------------------
+
+template <int BK, bool TAPU>
+struct FwdA {  // im2col(X): LDS row = output pixel, K-contiguous over cin
+  int ih0, iw0, koff;
+  int base;    // element offset of (b, ih0, iw0, 0)
+  bool valid;
+  __device__ void init(const ConvArgs& a, int m, int q) {
     valid = m < a.M;
-    int mm = valid ? m : 0;
-    int ow = mm % a.OW; int t = mm / a.OW; int oh = t % a.OH; b = t / a.OH;
-    ih0 = oh * a.sh - a.ph; iw0 = ow * a.sw - a.pw;
+    const int mm = valid ? m : 0;
+    const int t = fdiv(mm, a.fd_OW), ow = mm - t * a.OW;
+    const int b = fdiv(t, a.fd_OH), oh = t - b * a.OH;
+    ih0 = oh * a.sh - a.ph;
+    iw0 = ow * a.sw - a.pw;
+    base = ((b * a.H + ih0) * a.W + iw0) * a.C;
+    koff = (q % (BK / 8)) * 8;
   }
-  __device__ uint4 load(const ConvArgs& a, int k) const {
-    uint4 z = {0, 0, 0, 0};
-    if (!valid || k >= a.Kd) return z;
-    int tap = k / a.C, c = k - tap * a.C;
-    int nts = a.s1 - a.s0;
-    int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
-    int ih = ih0 + r, iw = iw0 + s;
-    if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) return z;
-    return ld16(a.x + ((long long)(b * a.H + ih) * a.W + iw) * a.C + c);
-  }
-};
-
-// B of FWD: W[n][tap][cin], K-contiguous
-struct FwdB {
-  int valid; long long base;
-  __device__ void init(const ConvArgs& a, int n) {
-    valid = n < a.N; base = (long long)(valid ? n : 0) * a.KH * a.KW * a.C;
-  }
-  __device__ uint4 load(const ConvArgs& a, int k) const {
-    uint4 z = {0, 0, 0, 0};
-    if (!valid || k >= a.Kd) return z;
-    int tap = k / a.C, c = k - tap * a.C;
-    int nts = a.s1 - a.s0;
-    int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
-    return ld16(a.w + base + (r * a.KW + s) * a.C + c);
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int k = kb + koff;
+    int r, s, c;
+    if constexpr (TAPU) {
+      const int tap = fdiv(kb, a.fd_C);  // uniform
+      c = k - tap * a.C;
+      tap_rs(a, tap, r, s);
+    } else {
+      const int tap = fdiv(k, a.fd_C);
+      c = k - tap * a.C;
+      tap_rs(a, tap, r, s);
+    }
+    const int ih = ih0 + r, iw = iw0 + s;
+    const bool ok = valid && k < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    return ok ? a.x + base + (r * a.W + s) * a.C + c : a.zp;
   }
 };
 
-// A of DGRAD: dY gathered for input pixel m, K = (tap, cout), K-contiguous over cout
-struct DgradA {
-  int valid, b, ih, iw;
-  __device__ void init(const ConvArgs& a, int m) {
+template <int BK, bool TAPU>
+struct FwdB {  // W[n][tap][cin], K-contiguous
+  int base, koff;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int n, int q) {
+    valid = n < a.N;
+    base = (valid ? n : 0) * a.KH * a.KW * a.C;
+    koff = (q % (BK / 8)) * 8;
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int k = kb + koff;
+    const int tap = TAPU ? fdiv(kb, a.fd_C) : fdiv(k, a.fd_C);
+    const int c = k - tap * a.C;
+    int r, s;
+    tap_rs(a, tap, r, s);
+    return (valid && k < kend) ? a.w + base + (r * a.KW + s) * a.C + c : a.zp;
+  }
+};
+
+template <int BK>
+struct DgradA {  // dY gathered for input pixel m; K = (tap, cout); Kp % BK == 0 -> tap uniform
+  int b, ih, iw, koff;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int m, int q) {
     valid = m < a.M;
-    int mm = valid ? m : 0;
-    iw = mm % a.W; int t = mm / a.W; ih = t % a.H; b = t / a.H;
+    const int mm = valid ? m : 0;
+    const int t = fdiv(mm, a.fd_W);
+    iw = mm - t * a.W;
+    b = fdiv(t, a.fd_H);
+    ih = t - b * a.H;
+    koff = (q % (BK / 8)) * 8;
   }
-  __device__ uint4 load(const ConvArgs& a, int k) const {
-    uint4 z = {0, 0, 0, 0};
-    if (!valid) return z;
-    int tap = k / a.Kp, n = k - tap * a.Kp;
-    if (n >= a.K) return z;
-    int nts = a.s1 - a.s0;
-    int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
-    int th = ih + a.ph - r, tw = iw + a.pw - s;
-    if (th < 0 || tw < 0) return z;
-    int oh = th / a.sh, ow = tw / a.sw;
-    if (oh * a.sh != th || ow * a.sw != tw || oh >= a.OH || ow >= a.OW) return z;
-    return ld16(a.dy + ((long long)(b * a.OH + oh) * a.OW + ow) * a.K + n);
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int tap = fdiv(kb, a.fd_Kp);  // uniform
+    const int n = kb - tap * a.Kp + koff;
+    int r, s;
+    tap_rs(a, tap, r, s);
+    const int th = ih + a.ph - r, tw = iw + a.pw - s;
+    const int oh = fdiv(th < 0 ? 0 : th, a.fd_sh), ow = fdiv(tw < 0 ? 0 : tw, a.fd_sw);
+    const bool ok = valid && kb + koff < kend && n < a.K && th >= 0 && tw >= 0 && oh * a.sh == th &&
+                    ow * a.sw == tw && oh < a.OH && ow < a.OW;
+    return ok ? a.dy + ((b * a.OH + oh) * a.OW + ow) * a.K + n : a.zp;
   }
 };
 
-// B of DGRAD (K-strided): LDS row = k = (tap, cout), columns = cin; chunk = W[cout][tap][c..c+7]
-__device__ __forceinline__ uint4 dgrad_b_load(const ConvArgs& a, int k, int c) {
-  uint4 z = {0, 0, 0, 0};
-  if (c >= a.N) return z;
-  int tap = k / a.Kp, n = k - tap * a.Kp;
-  if (n >= a.K) return z;
-  int nts = a.s1 - a.s0;
-  int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
-  return ld16(a.w + ((long long)(n * a.KH + r) * a.KW + s) * a.C + c);
-}
+template <int BK, int BN>
+struct DgradB {  // LDS row = k = (tap, cout), cols = cin; chunk = W[cout][tap][c..c+7]
+  int krow, c;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int n0, int q) {
+    constexpr int CPR = BN / 8;
+    krow = q / CPR;
+    c = n0 + (q % CPR) * 8;
+    valid = c < a.N;
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int tap = fdiv(kb, a.fd_Kp);  // uniform
+    const int n = kb - tap * a.Kp + krow;
+    int r, s;
+    tap_rs(a, tap, r, s);
+    const bool ok = valid && kb + krow < kend && n < a.K;
+    return ok ? a.w + ((n * a.KH + r) * a.KW + s) * a.C + c : a.zp;
+  }
+};
 
-// A of WGRAD (K-strided): LDS row = pixel k, columns = cout; chunk = dY[k][n..n+7]
-__device__ __forceinline__ uint4 wgrad_a_load(const ConvArgs& a, int k, int kend, int n) {
-  uint4 z = {0, 0, 0, 0};
-  if (k >= kend || n >= a.M) return z;
-  return ld16(a.dy + (long long)k * a.K + n);
-}
+template <int BK, int BM>
+struct WgradA {  // LDS row = pixel k, cols = cout; chunk = dY[k][n..n+7]
+  int krow, n;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int m0, int q) {
+    constexpr int CPR = BM / 8;
+    krow = q / CPR;
+    n = m0 + (q % CPR) * 8;
+    valid = n < a.M;
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int k = kb + krow;
+    return (valid && k < kend) ? a.dy + (long long)k * a.K + n : a.zp;
+  }
+};
 
-// B of WGRAD (K-strided): LDS row = pixel k, columns j = (tap, cin); chunk = X[pix shifted][c..c+7]
-__device__ __forceinline__ uint4 wgrad_b_load(const ConvArgs& a, int k, int kend, int j) {
-  uint4 z = {0, 0, 0, 0};
-  if (k >= kend || j >= a.N) return z;
-  int tap = j / a.C, c = j - tap * a.C;
-  int nts = a.s1 - a.s0;
-  int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
-  int ow = k % a.OW; int t = k / a.OW; int oh = t % a.OH; int b = t / a.OH;
-  int ih = oh * a.sh - a.ph + r, iw = ow * a.sw - a.pw + s;
-  if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) return z;
-  return ld16(a.x + ((long long)(b * a.H + ih) * a.W + iw) * a.C + c);
-}
+template <int BK, int BN>
+struct WgradB {  // LDS row = pixel k, cols j = (tap, cin); chunk = X[pixel shifted by tap][c..c+7]
+  int krow, r, s, c;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int n0, int q) {
+    constexpr int CPR = BN / 8;
+    krow = q / CPR;
+    const int j = n0 + (q % CPR) * 8;
+    valid = j < a.N;
+    const int jj = valid ? j : 0;
+    const int tap = fdiv(jj, a.fd_C);
+    c = jj - tap * a.C;
+    tap_rs(a, tap, r, s);
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int k = kb + krow;
+    const int kk = k < kend ? k : 0;
+    const int t = fdiv(kk, a.fd_OW), ow = kk - t * a.OW;
+    const int b = fdiv(t, a.fd_OH), oh = t - b * a.OH;
+    const int ih = oh * a.sh - a.ph + r, iw = ow * a.sw - a.pw + s;
+    const bool ok = valid && k < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    return ok ? a.x + ((b * a.H + ih) * a.W + iw) * a.C + c : a.zp;
+  }
+};
 
-// ---- fragment readers ----
-template <int R>
-__device__ __forceinline__ bf16x8_t frag_kcontig(const bf16_t* lds, int row0, int lane) {
-  const bf16_t* p = lds + (row0 + (lane & 15)) * (BK + PADK) + 8 * (lane >> 4);
+// ---- fragment readers (k-substep ks covers k = 32*ks .. 32*ks+31 of the LDS tile) ----
+template <int BK>
+__device__ __forceinline__ bf16x8_t frag_kcontig(const bf16_t* lds, int row0, int ks, int lane) {
+  const bf16_t* p = lds + (row0 + (lane & 15)) * (BK + PADK) + 32 * ks + 8 * (lane >> 4);
   return *reinterpret_cast<const bf16x8_t*>(p);
 }
 
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
 
 template <int R>
-__device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, int lane) {
+__device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, int ks, int lane) {
   const int il = lane & 15, g = lane >> 4;
   const int col = row0 + 4 * (il & 3);
-  const bf16_t* p0 = lds + (8 * g + (il >> 2)) * (R + PADR) + col;
+  const bf16_t* p0 = lds + (32 * ks + 8 * g + (il >> 2)) * (R + PADR) + col;
   const bf16_t* p1 = p0 + 4 * (R + PADR);
   v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p0));
   v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p1));
@@ -184,140 +272,20 @@ __device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, i
   return f;
 }
 
-template <int MODE, int BM, int BN>
-__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
-  constexpr bool A_KC = (MODE != WGRAD);
-  constexpr bool B_KC = (MODE == FWD);
-  using TA = TileShape<BM, A_KC>;
-  using TB = TileShape<BN, B_KC>;
-  constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
-
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (TA::ELEMS + TB::ELEMS)];
-  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
-#define sA(buf) (smem + (buf) * STAGE)
-#define sB(buf) (smem + (buf) * STAGE + TA::ELEMS)
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-
-  int kbeg = 0, kend = a.Kd;
-  if (MODE == WGRAD) {
-    kbeg = blockIdx.z * a.kchunk;
-    kend = min(a.Kd, kbeg + a.kchunk);
-  }
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  // per-thread chunk bookkeeping (rows fixed across K-steps for K-contiguous operands)
-  FwdA fa[TA::PER_THREAD];
-  DgradA da[TA::PER_THREAD];
-  FwdB fb[TB::PER_THREAD];
-  if (MODE == FWD) {
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) fa[i].init(a, m0 + (tid + i * 256) / 4);
-#pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) fb[i].init(a, n0 + (tid + i * 256) / 4);
-  } else if (MODE == DGRAD) {
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) da[i].init(a, m0 + (tid + i * 256) / 4);
-  }
-
-  uint4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
-
-  auto gload = [&](int kt) {
-    const int kb = kbeg + kt * BK;
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) {
-      const int q = tid + i * 256;
-      if (q < TA::CHUNKS) {
-        if (MODE == FWD) ra[i] = fa[i].load(a, kb + (q & 3) * 8);
-        else if (MODE == DGRAD) ra[i] = da[i].load(a, kb + (q & 3) * 8);
-        else {
-          constexpr int CPR = BM / 8;  // chunks per LDS row
-          ra[i] = wgrad_a_load(a, kb + q / CPR, kend, m0 + (q % CPR) * 8);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) {
-      const int q = tid + i * 256;
-      if (q < TB::CHUNKS) {
-        if (MODE == FWD) rb[i] = fb[i].load(a, kb + (q & 3) * 8);
-        else {
-          constexpr int CPR = BN / 8;
-          if (MODE == DGRAD) rb[i] = dgrad_b_load(a, kb + q / CPR, n0 + (q % CPR) * 8);
-          else rb[i] = wgrad_b_load(a, kb + q / CPR, kend, n0 + (q % CPR) * 8);
-        }
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) {
-      const int q = tid + i * 256;
-      if (q < TA::CHUNKS) {
-        int off;
-        if (A_KC) off = (q >> 2) * (BK + PADK) + (q & 3) * 8;
-        else { constexpr int CPR = BM / 8; off = (q / CPR) * (BM + PADR) + (q % CPR) * 8; }
-        *reinterpret_cast<uint4*>(sA(buf) + off) = ra[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) {
-      const int q = tid + i * 256;
-      if (q < TB::CHUNKS) {
-        int off;
-        if (B_KC) off = (q >> 2) * (BK + PADK) + (q & 3) * 8;
-        else { constexpr int CPR = BN / 8; off = (q / CPR) * (BN + PADR) + (q % CPR) * 8; }
-        *reinterpret_cast<uint4*>(sB(buf) + off) = rb[i];
-      }
-    }
-  };
-
-  f32x4_t acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) gload(kt + 1);
-      bf16x8_t af[MR], bfr[NR];
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-        af[i] = A_KC ? frag_kcontig<BM>(sA(cur), wm * WM + i * 16, lane)
-                     : frag_kstrided<BM>(sA(cur), wm * WM + i * 16, lane);
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-        bfr[j] = B_KC ? frag_kcontig<BN>(sB(cur), wn * WN + j * 16, lane)
-                      : frag_kstrided<BN>(sB(cur), wn * WN + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      if (kt + 1 < nk) sstore(cur ^ 1);
-      __syncthreads();
-    }
-  }
-
-#undef sA
-#undef sB
-  // ---- epilogue ----
+template <int MODE, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                              int wn, int lane, int tid, int tile, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
-  if (MODE == WGRAD) {
-    const int nts = a.s1 - a.s0;
+
+  // ---------------------------------------------------------------- WGRAD epilogue
+  if constexpr (MODE == WGRAD) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int col = n0 + wn * WN + j * 16 + fr;
       if (col >= a.N) continue;
-      const int tap = col / a.C, c = col - tap * a.C;
-      const int r = a.r0 + tap / nts, s = a.s0 + tap % nts;
+      const int tap = fdiv(col, a.fd_C), c = col - tap * a.C;
+      int r, s;
+      tap_rs(a, tap, r, s);
       const long long coff = (long long)(r * a.KW + s) * a.C + c;
 #pragma unroll
       for (int i = 0; i < MR; ++i)
@@ -332,65 +300,414 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
         }
     }
     return;
-  }
-
-  const int ldc = a.N;
+  } else {
+    // ------------------------------------------------------ split-K: last arriver reduces
+    if (a.splits > 1) {
+      constexpr int NACC = MR * NR * 4;
+      float* slab = a.slab + ((long long)tile * a.splits) * (256 * NACC);
+      float4* mine = reinterpret_cast<float4*>(slab + (long long)blockIdx.z * 256 * NACC) + tid * (NACC / 4);
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int col = n0 + wn * WN + j * 16 + fr;
-    const bool cok = col < a.N;
-    float bv = 0.f;
-    if (MODE == FWD && a.bias && cok) bv = a.bias[col];
-    float s1 = 0.f, s2 = 0.f;
+      for (int i = 0; i < MR; ++i)
 #pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
-        float v = acc[i][j][e] + bv;
-        if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
-        if (MODE == DGRAD && a.addend && row < a.M && cok) v += bf2f(a.addend[(long long)row * ldc + col]);
-        if (row < a.M && cok) {
-          a.out[(long long)row * ldc + col] = f2bf(v);
-          s1 += v; s2 += v * v;
+        for (int j = 0; j < NR; ++j)
+          mine[i * NR + j] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned lastp = (t == (unsigned)a.splits - 1) ? 1u : 0u;
+        if (lastp) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        flag[0] = lastp;
       }
-    if (MODE == FWD && a.stats) {
-      s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
-      if (fq == 0 && cok) {
-        atomicAdd(a.stats + col, s1);
-        atomicAdd(a.stats + a.N + col, s2);
+      __syncthreads();
+      if (flag[0] == 0) return;
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < a.splits; ++sp) {
+        const float4* src = reinterpret_cast<const float4*>(slab + (long long)sp * 256 * NACC) + tid * (NACC / 4);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) {
+            const float4 v = src[i * NR + j];
+            acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
+          }
+      }
+    }
+
+    // ---------------------------------------------------------- FWD / DGRAD epilogue
+    const int ldc = a.N;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int col = n0 + wn * WN + j * 16 + fr;
+      const bool cok = col < a.N;
+      float bv = 0.f;
+      if (MODE == FWD && a.bias && cok) bv = a.bias[col];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
+          if (row < a.M && cok) {
+            float v = acc[i][j][e] + bv;
+            if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
+            if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
+            a.out[(long long)row * ldc + col] = f2bf(v);
+            s1 += v;
+            s2 += v * v;
+          }
+        }
+      if (MODE == FWD && a.stats) {
+        s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+        if (fq == 0 && cok) {
+          atomicAdd(a.stats + col, s1);
+          atomicAdd(a.stats + a.N + col, s2);
+        }
       }
     }
   }
 }
 
-template <int MODE, int BM, int BN>
-int launch(const ConvArgs& a, int splits, hipStream_t s) {
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN>), grid, dim3(256), 0, s, a);
+template <int MODE, int BM, int BN, int BK, bool TAPU>
+__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
+  constexpr bool A_KC = (MODE != WGRAD);
+  constexpr bool B_KC = (MODE == FWD);
+  using TA = TileShape<BM, A_KC, BK>;
+  using TB = TileShape<BN, B_KC, BK>;
+  constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  constexpr int KC = BK / 8;  // 16-byte chunks per K-contiguous row
+  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+  constexpr int PA = TA::PER_THREAD, PB = TB::PER_THREAD;
+
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tile_m = blockIdx.y, tile_n = blockIdx.x;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(a.Kd, kbeg + a.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // ---- per-thread chunk generators ----
+  using GA = typename std::conditional<MODE == FWD, FwdA<BK, TAPU>,
+             typename std::conditional<MODE == DGRAD, DgradA<BK>, WgradA<BK, BM>>::type>::type;
+  using GB = typename std::conditional<MODE == FWD, FwdB<BK, TAPU>,
+             typename std::conditional<MODE == DGRAD, DgradB<BK, BN>, WgradB<BK, BN>>::type>::type;
+  GA ga[PA];
+  GB gb[PB];
+  int offA[PA], offB[PB];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    int q = tid + i * 256;
+    if (q >= TA::CHUNKS) q = TA::CHUNKS - 1;  // surplus threads duplicate the last chunk
+    if constexpr (A_KC) { ga[i].init(a, m0 + q / KC, q); offA[i] = (q / KC) * (BK + PADK) + (q % KC) * 8; }
+    else { ga[i].init(a, m0, q); constexpr int CPR = BM / 8; offA[i] = (q / CPR) * (BM + PADR) + (q % CPR) * 8; }
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    int q = tid + i * 256;
+    if (q >= TB::CHUNKS) q = TB::CHUNKS - 1;
+    if constexpr (B_KC) { gb[i].init(a, n0 + q / KC, q); offB[i] = (q / KC) * (BK + PADK) + (q % KC) * 8; }
+    else { gb[i].init(a, n0, q); constexpr int CPR = BN / 8; offB[i] = (q / CPR) * (BN + PADR) + (q % CPR) * 8; }
+  }
+
+  uint4 ra0[PA], rb0[PB], ra1[PA], rb1[PB];
+  auto issue = [&](uint4* ra, uint4* rb, int kt) {
+    const int kb = kbeg + kt * BK;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) ra[i] = ld16(ga[i].ptr(a, kb, kend));
+#pragma unroll
+    for (int i = 0; i < PB; ++i) rb[i] = ld16(gb[i].ptr(a, kb, kend));
+  };
+  auto stash = [&](const uint4* ra, const uint4* rb, int buf) {
+    bf16_t* sA = smem + buf * STAGE;
+    bf16_t* sB = sA + TA::ELEMS;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) *reinterpret_cast<uint4*>(sA + offA[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < PB; ++i) *reinterpret_cast<uint4*>(sB + offB[i]) = rb[i];
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const bf16_t* sA = smem + buf * STAGE;
+    const bf16_t* sB = sA + TA::ELEMS;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8_t af[MR], bfr[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        af[i] = A_KC ? frag_kcontig<BK>(sA, wm * WM + i * 16, ks, lane)
+                     : frag_kstrided<BM>(sA, wm * WM + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bfr[j] = B_KC ? frag_kcontig<BK>(sB, wn * WN + j * 16, ks, lane)
+                      : frag_kstrided<BN>(sB, wn * WN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    const int last = nk - 1;
+    issue(ra0, rb0, 0);
+    issue(ra1, rb1, min(1, last));
+    stash(ra0, rb0, 0);
+    __syncthreads();
+    for (int kt = 0;; kt += 2) {
+      // even half: LDS[0] holds tile kt, stage 1 holds kt+1 (in flight), stage 0 is free
+      issue(ra0, rb0, min(kt + 2, last));
+      compute(0);
+      stash(ra1, rb1, 1);
+      __syncthreads();
+      if (kt + 1 > last) break;
+      // odd half: LDS[1] holds kt+1, stage 0 holds kt+2 (in flight), stage 1 is free
+      issue(ra1, rb1, min(kt + 3, last));
+      compute(1);
+      stash(ra0, rb0, 0);
+      __syncthreads();
+      if (kt + 2 > last) break;
+    }
+  }
+
+  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * gridDim.x + tile_n,
+                                      reinterpret_cast<unsigned*>(smem));
+}
+
+// =====================================================================================
+// Variant 1/2: LDS-DMA pipeline (global_load_lds_dwordx4), BK = 64, S-stage LDS ring.
+//
+// Operands go global -> LDS directly (no VGPR staging, no compiler-inserted register
+// waits); each wave issues NI = (BM+BN)/32 one-KiB DMA instructions per stage and the
+// loop keeps S-2 stages in flight across raw s_barriers with a counted vmcnt.  The LDS
+// image is lane-linear (the DMA writes base + 16*lane), so bank-conflict swizzles are
+// applied on the per-lane SOURCE address and undone on the read (CDNA guide §5.4 rule
+// 21): K-contiguous [row][64] tiles use chunk ^= row&7, K-strided [64][R] tiles a
+// row-bit permutation chosen per R — all verified conflict-free by tools/lds_banks.py.
+// =====================================================================================
+
+template <int R>
+__device__ __forceinline__ int swz_ks(int r) {  // K-strided [64][R] chunk swizzle
+  if constexpr (R == 32) return (r >> 2) & 3;
+  else if constexpr (R == 64) return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+  else return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+}
+
+// glds fragment readers
+__device__ __forceinline__ bf16x8_t gfrag_kcontig(const char* lds, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = 4 * ks + (lane >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
+}
+
+template <int R>
+__device__ __forceinline__ bf16x8_t gfrag_kstrided(const char* lds, int row0, int ks, int lane) {
+  const int il = lane & 15, g = lane >> 4;
+  const int col = row0 + 4 * (il & 3);
+  const int k0 = 32 * ks + 8 * g + (il >> 2);
+  const int k1 = k0 + 4;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  const char* p0 = lds + k0 * (2 * R) + ((ch ^ swz_ks<R>(k0)) << 4) + within;
+  const char* p1 = lds + k1 * (2 * R) + ((ch ^ swz_ks<R>(k1)) << 4) + within;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p0));
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p1));
+  bf16x8_t f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return f;
+}
+
+// Which tile row / logical chunk a lane's DMA covers in instruction u of an operand.
+template <int R, bool KC>
+__device__ __forceinline__ void glds_slot(int u, int lane, int& row, int& chunk) {
+  if constexpr (KC) {  // [R rows][64 k] 128-byte rows, 8 rows per KiB
+    row = 8 * u + (lane >> 3);
+    chunk = (lane & 7) ^ (row & 7);
+  } else {             // [64 k][R cols], 2R-byte rows
+    constexpr int CPR = R / 8;          // 16-byte chunks per row
+    constexpr int RPI = 64 / CPR;       // rows per KiB instruction
+    row = RPI * u + lane / CPR;
+    chunk = (lane % CPR) ^ swz_ks<R>(row);
+  }
+}
+
+template <int MODE, int BM, int BN, int S, bool TAPU>
+__global__ __launch_bounds__(256) void k_conv_glds(ConvArgs a) {
+  constexpr int BK = 64;
+  constexpr bool A_KC = (MODE != WGRAD);
+  constexpr bool B_KC = (MODE == FWD);
+  constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per stage
+  constexpr int NI = NA + NB;
+
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tile_m = blockIdx.y, tile_n = blockIdx.x;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(a.Kd, kbeg + a.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  using GA = typename std::conditional<MODE == FWD, FwdA<BK, TAPU>,
+             typename std::conditional<MODE == DGRAD, DgradA<BK>, WgradA<BK, BM>>::type>::type;
+  using GB = typename std::conditional<MODE == FWD, FwdB<BK, TAPU>,
+             typename std::conditional<MODE == DGRAD, DgradB<BK, BN>, WgradB<BK, BN>>::type>::type;
+  GA ga[NA];
+  GB gb[NB];
+  // Generators are addressed like the register-staged kernel: K-contiguous ones take
+  // (row, q) with q % 8 = logical chunk; K-strided ones take q = row*CPR + chunk.
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    int row, ch;
+    glds_slot<BM, A_KC>(wave * NA + j, lane, row, ch);
+    if constexpr (A_KC) ga[j].init(a, m0 + row, ch);
+    else ga[j].init(a, m0, row * (BM / 8) + ch);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    int row, ch;
+    glds_slot<BN, B_KC>(wave * NB + j, lane, row, ch);
+    if constexpr (B_KC) gb[j].init(a, n0 + row, ch);
+    else gb[j].init(a, n0, row * (BN / 8) + ch);
+  }
+
+  auto issue = [&](int kt, int buf) {
+    const int kb = kbeg + kt * BK;
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)ga[j].ptr(a, kb, kend),
+                                       (__attribute__((address_space(3))) void*)(base + (wave * NA + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)gb[j].ptr(a, kb, kend),
+                                       (__attribute__((address_space(3))) void*)(base + A_BYTES + (wave * NB + j) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    const int last = nk - 1;
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s) issue(min(s, last), s);
+    int cur = 0;
+    for (int t = 0; t < nk; ++t) {
+      // tile t landed for this wave; S-2 younger stages may stay in flight
+      if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      int nb = cur + S - 1;
+      if (nb >= S) nb -= S;
+      issue(min(t + S - 1, last), nb);
+      const char* sA = smem + cur * STAGE;
+      const char* sB = sA + A_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[MR], bfr[NR];
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+          af[i] = A_KC ? gfrag_kcontig(sA, wm * WM + i * 16, ks, lane)
+                       : gfrag_kstrided<BM>(sA, wm * WM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          bfr[j] = B_KC ? gfrag_kcontig(sB, wn * WN + j * 16, ks, lane)
+                        : gfrag_kstrided<BN>(sB, wn * WN + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      cur = (cur + 1 == S) ? 0 : cur + 1;
+    }
+  }
+  // drain the (clamped, redundant) tail DMAs before LDS is reused by the epilogue
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * gridDim.x + tile_n,
+                                      reinterpret_cast<unsigned*>(smem));
+}
+
+template <int MODE, int BM, int BN, int S>
+int launch_glds(const ConvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.splits);
+  const bool tapu = (MODE != FWD) || (a.C % 64 == 0);
+  if (tapu) hipLaunchKernelGGL((k_conv_glds<MODE, BM, BN, S, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_conv_glds<MODE, BM, BN, S, false>), grid, dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+template <int MODE, int BM, int BN, int BK>
+int launch(const ConvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.splits);
+  // K-tile inside one tap: FWD needs Cin % BK == 0; DGRAD/WGRAD tap math is already per-tile/per-column
+  const bool tapu = (MODE != FWD) || (a.C % BK == 0);
+  if (tapu) hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, false>), grid, dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 
 template <int MODE>
-int dispatch(const ConvArgs& a, int bm, int bn, int splits, hipStream_t s) {
-#define KML_T(BMv, BNv) if (bm == BMv && bn == BNv) return launch<MODE, BMv, BNv>(a, splits, s);
+int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
+#define KML_T(BMv, BNv)                                                  \
+  if (bm == BMv && bn == BNv) {                                          \
+    if (variant == 1) return launch_glds<MODE, BMv, BNv, 3>(a, s);       \
+    if (variant == 2) return launch_glds<MODE, BMv, BNv, 4>(a, s);       \
+    if (bk == 64) return launch<MODE, BMv, BNv, 64>(a, s);               \
+    return launch<MODE, BMv, BNv, 32>(a, s);                             \
+  }
   KML_T(32, 32) KML_T(32, 64) KML_T(64, 32) KML_T(64, 64)
   KML_T(64, 128) KML_T(128, 64) KML_T(128, 128) KML_T(32, 128) KML_T(128, 32)
 #undef KML_T
   return (int)hipErrorInvalidValue;
 }
 
-// valid tap window along one axis: taps t where some output o in [0,O) reads 0<=o*st-p+t<I
+FastDiv make_fd(int d) {
+  FastDiv f;
+  f.d = d < 1 ? 1 : d;
+  int p = 0;
+  while ((1ll << p) < f.d) ++p;
+  f.s = 31 + p;
+  f.m = (unsigned)(((1ull << (31 + p)) + f.d - 1) / f.d);
+  if (f.d == 1) { f.m = 1u << 31; f.s = 31; }
+  return f;
+}
+
 void tap_window(int I, int O, int KS, int st, int p, int* t0, int* t1) {
   int lo = KS, hi = 0;
   for (int t = 0; t < KS; ++t) {
-    // smallest/largest input coordinate read by tap t
-    int first = -p + t, last = (O - 1) * st - p + t;
     bool ok = false;
-    for (int o = 0; o < O && !ok; ++o) { int i = o * st - p + t; ok = (i >= 0 && i < I); }
-    (void)first; (void)last;
+    for (int o = 0; o < O && !ok; ++o) { const int i = o * st - p + t; ok = (i >= 0 && i < I); }
     if (ok) { if (t < lo) lo = t; if (t + 1 > hi) hi = t + 1; }
   }
   if (lo >= hi) { lo = 0; hi = 0; }
@@ -401,55 +718,101 @@ ConvArgs make_args(int B, int H, int W, int C, int K, int KH, int KW, int sh, in
   ConvArgs a = {};
   a.B = B; a.H = H; a.W = W; a.C = C; a.K = K; a.KH = KH; a.KW = KW;
   a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw;
-  a.OH = (H + 2 * ph - KH) / sh + 1; a.OW = (W + 2 * pw - KW) / sw + 1;
+  a.OH = (H + 2 * ph - KH) / sh + 1;
+  a.OW = (W + 2 * pw - KW) / sw + 1;
   tap_window(H, a.OH, KH, sh, ph, &a.r0, &a.r1);
   tap_window(W, a.OW, KW, sw, pw, &a.s0, &a.s1);
+  a.fd_C = make_fd(C);
+  a.fd_nts = make_fd(a.s1 - a.s0);
+  a.fd_OW = make_fd(a.OW);
+  a.fd_OH = make_fd(a.OH);
+  a.fd_W = make_fd(W);
+  a.fd_H = make_fd(H);
+  a.fd_sh = make_fd(sh);
+  a.fd_sw = make_fd(sw);
+  a.fd_Kp = make_fd(1);
   return a;
+}
+
+int set_splits(ConvArgs& a, int bk, int splits) {
+  if (splits < 1) splits = 1;
+  int chunk = (a.Kd + splits - 1) / splits;
+  chunk = (chunk + bk - 1) / bk * bk;
+  if (chunk < bk) chunk = bk;
+  a.kchunk = chunk;
+  a.splits = (a.Kd + chunk - 1) / chunk;
+  if (a.splits < 1) a.splits = 1;
+  return a.splits;
+}
+
+__device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];  // zero-initialised device global
+
+const bf16_t* zero_page() {
+  static const bf16_t* p = nullptr;
+  if (!p) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_zero_page)) == hipSuccess) p = (const bf16_t*)d;
+  }
+  return p;
 }
 
 }  // namespace
 
-// Host-side helper exposed for the Python planner / tests.
-KML_API int kml_conv_tap_window(int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw,
-                                int ph, int pw, int* out4) {
+KML_API int kml_conv_tap_window(int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
+                                int* out4) {
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   out4[0] = a.r0; out4[1] = a.r1; out4[2] = a.s0; out4[3] = a.s1;
   return 0;
 }
 
-KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats,
-                         int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                         int relu, int bm, int bn, hipStream_t s) {
+KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
+  ConvArgs a = {};
+  a.Kd = Kd;
+  return set_splits(a, bk, splits);
+}
+
+KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int B, int H,
+                         int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu, int bm, int bn,
+                         int bk, int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu;
+  a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu; a.zp = zero_page();
   a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
-  return dispatch<FWD>(a, bm, bn, 1, s);
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  set_splits(a, bk, splits);
+  if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
+  a.slab = slab; a.counters = counters;
+  return dispatch<FWD>(a, bm, bn, bk, variant, s);
 }
 
-KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend,
-                           int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                           int bm, int bn, hipStream_t s) {
+KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, int B, int H, int W,
+                           int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
+                           int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+  if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.Kp = (K + BK - 1) / BK * BK;
-  a.dy = dy; a.w = w; a.out = dx; a.addend = addend;
+  a.Kp = (K + bk - 1) / bk * bk;
+  a.fd_Kp = make_fd(a.Kp);
+  a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.zp = zero_page();
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
-  return dispatch<DGRAD>(a, bm, bn, 1, s);
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  set_splits(a, bk, splits);
+  if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
+  a.slab = slab; a.counters = counters;
+  return dispatch<DGRAD>(a, bm, bn, bk, variant, s);
 }
 
-KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw,
-                           int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                           int bm, int bn, int splits, int accumulate, hipStream_t s) {
+KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
+                           int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk, int splits, int variant,
+                           int accumulate, hipStream_t s) {
+  if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.x = x; a.dy = dy; a.dw = dw;
+  a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
   a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
-  if (splits < 1) splits = 1;
-  int chunk = (a.Kd + splits - 1) / splits;
-  chunk = (chunk + BK - 1) / BK * BK;
-  splits = (a.Kd + chunk - 1) / chunk;
-  a.kchunk = chunk;
-  a.accumulate = (splits > 1) ? 1 : accumulate;
-  return dispatch<WGRAD>(a, bm, bn, splits, s);
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  set_splits(a, bk, splits);
+  a.accumulate = (a.splits > 1) ? 1 : accumulate;
+  return dispatch<WGRAD>(a, bm, bn, bk, variant, s);
 }

@@ -69,6 +69,44 @@ def _compile_group(srcs, objdir, flags, jobs, verbose):
     return objs, bool(todo)
 
 
+_CTYPE_RE = None
+
+
+def _sig_of(params: str) -> str:
+    """Map a C parameter list to the ctypes signature letters used by _native."""
+    out = []
+    params = params.strip()
+    if params in ("", "void"):
+        return ""
+    for prm in params.split(","):
+        t = " ".join(prm.strip().split()[:-1]) if "*" not in prm else prm
+        if "*" in prm:
+            out.append("p")
+        elif "hipStream_t" in t:
+            out.append("s")
+        elif "double" in t:
+            out.append("d")
+        elif "float" in t:
+            out.append("f")
+        elif "long long" in t or "int64" in t or "size_t" in t:
+            out.append("l")
+        else:
+            out.append("i")
+    return " ".join(out)
+
+
+def extract_abi(paths) -> dict:
+    """Parse every ``KML_API <ret> kml_*(...)`` prototype into {name: signature}."""
+    import re
+    rx = re.compile(r"KML_API\s+([\w\s\*]+?)\s*\b(kml_\w+)\s*\(([^)]*)\)", re.S)
+    abi = {}
+    for pth in paths:
+        src = open(pth).read()
+        for ret, name, params in rx.findall(src):
+            abi[name] = {"sig": _sig_of(" ".join(params.split())), "ret": " ".join(ret.split())}
+    return abi
+
+
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> dict:
     """Compile both native libraries; returns {name: path}."""
     jobs = jobs or min(8, os.cpu_count() or 4)
@@ -87,16 +125,25 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     if changed or not os.path.exists(lib) or _newest(objs) > os.path.getmtime(lib):
         _run([_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
     out["hip"] = lib
+    import json as _json
+    with open(os.path.join(LIBDIR, "abi_hip.json"), "w") as f:
+        _json.dump(extract_abi(ksrcs), f, indent=0, sort_keys=True)
 
     # --- host runtime -------------------------------------------------------------
     rsrcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     if rsrcs:
-        rflags = ["-O2", "-fPIC", "-std=c++17", "-pthread", "-x", "c++", "-D__HIP_PLATFORM_AMD__"] + inc
+        rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+        rflags = ["-O2", "-fPIC", "-std=c++17", "-pthread", "-x", "c++", "-D__HIP_PLATFORM_AMD__",
+                  "-I" + os.path.join(rocm, "include")] + inc
         objs, changed = _compile_group(rsrcs, os.path.join(BUILD, "runtime"), rflags, jobs, verbose)
         lib = os.path.join(LIBDIR, "libkubeml_rt.so")
         if changed or not os.path.exists(lib) or _newest(objs) > os.path.getmtime(lib):
-            _run([_hipcc(), "-shared", "-fPIC", "-pthread", "-o", lib] + objs)
+            _run([_hipcc(), "-shared", "-fPIC", "-pthread", "-o", lib] + objs +
+                 ["-L" + os.path.join(rocm, "lib"), "-lamdhip64"])
         out["rt"] = lib
+        import json as _json
+        with open(os.path.join(LIBDIR, "abi_rt.json"), "w") as f:
+            _json.dump(extract_abi(rsrcs), f, indent=0, sort_keys=True)
     return out
 
 

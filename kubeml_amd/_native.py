@@ -64,12 +64,30 @@ def _load(name: str, autobuild: bool = True) -> ctypes.CDLL:
 
 
 class _Lib:
-    """Lazily-declared ctypes function table."""
+    """Lazily-declared ctypes function table.
 
-    def __init__(self, soname: str):
+    Argument types come from ``lib/abi_*.json``, which the build extracts from the
+    ``KML_API`` prototypes in the C++/HIP sources — the Python side cannot drift from
+    the C ABI.  A caller-provided signature string is checked against it.
+    """
+
+    def __init__(self, soname: str, abi: str):
         self._soname = soname
+        self._abi_file = abi
+        self._abi = None
         self._fns: dict = {}
         self._lib = None
+
+    @property
+    def abi(self) -> dict:
+        if self._abi is None:
+            import json
+            path = lib_path(self._abi_file)
+            if not os.path.exists(path):
+                self.lib  # triggers the build
+            with open(path) as f:
+                self._abi = json.load(f)
+        return self._abi
 
     @property
     def lib(self) -> ctypes.CDLL:
@@ -77,24 +95,50 @@ class _Lib:
             self._lib = _load(self._soname)
         return self._lib
 
-    def fn(self, name: str, sig: str, restype=ctypes.c_int):
+    def fn(self, name: str, sig=None, restype=None):
         f = self._fns.get(name)
         if f is None:
+            ent = self.abi.get(name)
+            if ent is None:
+                raise AttributeError(f"{name} is not exported by {self._soname}")
+            if sig is not None and " ".join(sig.split()) != ent["sig"]:
+                raise TypeError(f"{name}: caller signature {sig!r} != C ABI {ent['sig']!r}")
             f = getattr(self.lib, name)
-            f.argtypes = [_CT[c] for c in sig.split()] if sig else []
-            f.restype = restype
+            f.argtypes = [_CT[c] for c in ent["sig"].split()]
+            ret = ent["ret"]
+            if restype is not None:
+                f.restype = restype
+            elif "*" in ret:
+                f.restype = ctypes.c_void_p
+            elif ret == "void":
+                f.restype = None
+            elif ret == "double":
+                f.restype = ctypes.c_double
+            elif ret == "long long":
+                f.restype = ctypes.c_longlong
+            else:
+                f.restype = ctypes.c_int
             self._fns[name] = f
+        elif sig is not None and " ".join(sig.split()) != self.abi[name]["sig"]:
+            raise TypeError(f"{name}: caller signature {sig!r} != C ABI {self.abi[name]['sig']!r}")
         return f
 
-    def call(self, name: str, sig: str, *args):
+    def call(self, name: str, sig, *args):
+        """Call a kml_* function returning a hipError_t-style int; raise on non-zero."""
+        if len(args) != len(self.abi[name]["sig"].split()):
+            raise TypeError(f"{name}: expected {len(self.abi[name]['sig'].split())} args, got {len(args)}")
         rc = self.fn(name, sig)(*args)
         if rc != 0:
             raise RuntimeError(f"{name} failed with hipError {rc}")
         return rc
 
+    def raw(self, name: str, *args):
+        """Call without return-code interpretation (handles, pointers, void)."""
+        return self.fn(name)(*args)
 
-HIP = _Lib("libkubeml_hip.so")
-RT = _Lib("libkubeml_rt.so")
+
+HIP = _Lib("libkubeml_hip.so", "abi_hip.json")
+RT = _Lib("libkubeml_rt.so", "abi_rt.json")
 
 
 def hip() -> _Lib:

@@ -13,7 +13,9 @@ Tensor conventions
 """
 from __future__ import annotations
 
+import json
 import math
+import os
 
 import torch
 
@@ -48,7 +50,20 @@ def _chk(t, dtype, name, ndim=None):
 # --------------------------------------------------------------------------------------
 
 _TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32)]
-_TUNED: dict = {}  # (mode, M, N, K) -> (bm, bn, splits); filled by tools/tune_conv.py tables
+_TUNED: dict = {}  # (mode, M, N, Kd) -> (bm, bn, bk, splits); loaded from conv_tuning.json
+_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
+
+
+def _load_tuning():
+    if os.environ.get("KUBEML_CONV_TUNING", "1") == "0":
+        return
+    if os.path.exists(_TUNE_FILE):
+        with open(_TUNE_FILE) as f:
+            for e in json.load(f).get("entries", []):
+                _TUNED[(e["mode"], e["M"], e["N"], e["Kd"])] = tuple(e["cfg"])
+
+
+_load_tuning()
 
 
 def out_hw(H, W, KH, KW, sh, sw, ph, pw):
@@ -67,36 +82,87 @@ def tap_window(H, W, KH, KW, sh, sw, ph, pw):
     return r0, r1, s0, s1
 
 
-def _pick_tile(M, N, target=240):
+def _cdiv(a, b):
+    return -(-a // b)
+
+
+def effective_splits(Kd, bk, splits):
+    splits = max(1, splits)
+    chunk = max(bk, _cdiv(_cdiv(Kd, splits), bk) * bk)
+    return max(1, _cdiv(Kd, chunk))
+
+
+def default_plan(mode, M, N, Kd, target_blocks=512):
+    """Heuristic (bm, bn, bk, splits); tools/tune_conv.py measured tables override it."""
+    bk = 64 if Kd >= 256 else 32
     best = None
-    for bm, bn in _TILES:
-        if bm > max(32, -(-M // 32) * 32) or bn > max(32, -(-N // 32) * 32):
+    for bm, bn in [(64, 64), (128, 64), (64, 128), (128, 128), (64, 32), (32, 64), (32, 32)]:
+        if bm > max(32, _cdiv(M, 32) * 32) or bn > max(32, _cdiv(N, 32) * 32):
             continue
-        blocks = -(-M // bm) * -(-N // bn)
-        if blocks >= target:
-            return bm, bn
-        best = (bm, bn)
-    return best or (32, 32)
+        tiles = _cdiv(M, bm) * _cdiv(N, bn)
+        kiters = _cdiv(Kd, bk)
+        max_split = max(1, kiters // 4) if mode != "wgrad" else max(1, kiters // 8)
+        if mode != "wgrad":
+            max_split = min(max_split, 16)
+        splits = max(1, min(max_split, round(target_blocks / tiles)))
+        blocks = tiles * splits
+        score = (min(blocks, target_blocks), bm * bn)
+        if best is None or score > best[0]:
+            best = (score, (bm, bn, bk, splits))
+    return best[1] if best else (32, 32, 32, 1)
 
 
 def plan_conv(mode, M, N, Kd):
-    key = (mode, M, N, Kd)
-    if key in _TUNED:
-        return _TUNED[key]
-    if mode == "wgrad":
-        bm, bn = _pick_tile(M, N, target=10**9)  # smallest tile; parallelism comes from split-K
-        for cand in [(64, 64), (64, 32), (32, 64), (32, 32)]:
-            if cand[0] <= max(32, -(-M // 32) * 32) and cand[1] <= max(32, -(-N // 32) * 32):
-                bm, bn = cand
-                break
-        tiles = -(-M // bm) * -(-N // bn)
-        splits = max(1, min(-(-512 // tiles), Kd // 256))
-        return bm, bn, splits
-    bm, bn = _pick_tile(M, N)
-    return bm, bn, 1
+    """(bm, bn, bk, splits, variant); variant 0 = register-staged pipeline,
+    1/2 = LDS-DMA (global_load_lds) pipeline with 3/4 stages (BK fixed at 64)."""
+    cfg = _TUNED.get((mode, M, N, Kd))
+    cfg = cfg if cfg is not None else default_plan(mode, M, N, Kd)
+    return tuple(cfg) + (0,) * (5 - len(cfg))
 
 
-def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None):
+def _norm_cfg(cfg):
+    bm, bn, bk, splits, variant = tuple(cfg) + (0,) * (5 - len(cfg))
+    if variant:
+        bk = 64  # the LDS-DMA pipeline is BK=64 only
+    return bm, bn, bk, splits, variant
+
+
+class _CounterPool:
+    """Per-device pool of split-K ticket counters (zeroed once; kernels reset their own)."""
+
+    SIZE = 1 << 16
+
+    def __init__(self):
+        self.bufs = {}
+        self.pos = {}
+
+    def take(self, device, n):
+        buf = self.bufs.get(device)
+        if buf is None:
+            buf = torch.zeros(self.SIZE, dtype=torch.int32, device=device)
+            self.bufs[device] = buf
+            self.pos[device] = 0
+        if n > self.SIZE:
+            raise ValueError("too many split-K tiles")
+        p = self.pos[device]
+        if p + n > self.SIZE:
+            p = 0
+        self.pos[device] = p + n
+        return buf[p:p + n]
+
+
+_COUNTERS = _CounterPool()
+
+
+def _splitk_ws(device, M, N, bm, bn, splits):
+    if splits <= 1:
+        return None, None
+    tiles = _cdiv(M, bm) * _cdiv(N, bn)
+    slab = torch.empty(tiles * splits * bm * bn, dtype=F32, device=device)
+    return slab, _COUNTERS.take(device, tiles)
+
+
+def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None):
     """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats += )."""
     _chk(x, BF16, "x", 4)
     _chk(w, BF16, "w", 4)
@@ -113,18 +179,22 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
         out = torch.empty((B, OH, OW, K), dtype=BF16, device=x.device)
     if bias is not None:
         _chk(bias, F32, "bias")
+        assert bias.numel() >= K
     if stats is not None:
         _chk(stats, F32, "stats")
         assert stats.numel() >= 2 * K
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
-    bm, bn, _ = plan_conv("fwd", B * OH * OW, K, (r1 - r0) * (s1 - s0) * C)
-    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i s",
+    M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
+    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
+    splits = effective_splits(Kd, bk, splits)
+    slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
+    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i p p s",
              _p(x), _p(w), _p(out), _p(bias), _p(stats), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
-             int(relu), bm, bn, _s())
+             int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _s())
     return out
 
 
-def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None):
+def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None):
     """dx = conv input gradient (+ addend, the fused residual-gradient sum)."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
@@ -135,21 +205,29 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None):
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
     if tuple(dy.shape) != (B, OH, OW, K):
         raise ValueError(f"dy shape {tuple(dy.shape)} != {(B, OH, OW, K)}")
+    if tuple(w.shape) != (K, KH, KW, C):
+        raise ValueError(f"weight shape {tuple(w.shape)} != {(K, KH, KW, C)}")
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
     if out is None:
         out = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
-    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     if addend is not None:
         _chk(addend, BF16, "addend")
         assert addend.shape == out.shape
-    bm, bn, _ = plan_conv("dgrad", B * H * W, C, (r1 - r0) * (s1 - s0) * K)
-    HIP.call("kml_conv_dgrad", "p p p p i i i i i i i i i i i i i s",
-             _p(dy), _p(w), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, _s())
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    M = B * H * W
+    ntap = (r1 - r0) * (s1 - s0)
+    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
+    Kd = ntap * _cdiv(K, bk) * bk
+    splits = effective_splits(Kd, bk, splits)
+    slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
+    HIP.call("kml_conv_dgrad", "p p p p i i i i i i i i i i i i i i i i p p s",
+             _p(dy), _p(w), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits,
+             variant, _p(slab), _p(cnt), _s())
     return out
 
 
-def conv_wgrad(x, dy, dw, KH, KW, stride, pad):
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None):
     """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient."""
     _chk(x, BF16, "x", 4)
     _chk(dy, BF16, "dy", 4)
@@ -162,9 +240,9 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad):
     if tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
         raise ValueError("wgrad shape mismatch")
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
-    bm, bn, splits = plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW)
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i s",
-             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, splits, 1, _s())
+    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i s",
+             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, 1, _s())
     return dw
 
 

@@ -1,0 +1,124 @@
+"""KubeDataset — the user dataset API (reference python/kubeml/kubeml/dataset.py:81-227).
+
+Same surface: subclass it, call ``super().__init__("<dataset name>")``, implement
+``__getitem__`` / ``__len__`` over ``self.data`` / ``self.labels``, and use
+``is_training()`` to pick train/val transforms.  ``num_docs`` / ``num_val_docs``
+count 64-sample documents exactly like the reference's Mongo collections.
+
+Differences that matter on MI355X:
+* documents come from the native mmap shard store (no Mongo, no unpickling);
+* ``collate_batch(data, labels)`` — optional user hook: if defined, the worker feeds
+  whole contiguous batches (``self.data[i:i+b]``) to it instead of going through a
+  per-sample ``DataLoader``; the shipped ResNet function uses it to hand raw uint8
+  images to the on-device augmentation kernel;
+* ``device_split(split)`` stages a whole split into HBM once (288 GB per GPU holds
+  every dataset the reference used) for kernels that gather batches on device.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Optional, Tuple
+
+import numpy as np
+import torch.utils.data as data
+
+from ..api.errors import DatasetNotFoundError
+from .context import current_task
+
+_STORES = {}
+
+
+def _store():
+    from ..config import Config
+    from ..store.shards import ShardStore
+    ctx = current_task()
+    if ctx is not None and ctx.store is not None:
+        return ctx.store
+    root = (ctx.store_dir if ctx is not None and ctx.store_dir else None) or Config.load().store_dir
+    st = _STORES.get(root)
+    if st is None:
+        st = ShardStore(root)
+        _STORES[root] = st
+    return st
+
+
+class _KubeArgs:
+    """Task arguments of the current invocation (reference dataset.py:24-78)."""
+
+    def __init__(self, job_id: str, N: int, K: int, task: str, func_id: int, epoch: int, lr: float = 0,
+                 batch_size: int = 0):
+        self._job_id = job_id
+        self._N = N
+        self._K = K
+        self._task = task
+        self._func_id = func_id
+        self.lr = lr
+        self.batch_size = batch_size
+        self.epoch = epoch
+
+    @classmethod
+    def parse(cls) -> "_KubeArgs":
+        ctx = current_task()
+        if ctx is None:
+            from ..api.errors import InvalidArgsError
+            raise InvalidArgsError(RuntimeError("no task context: invoke through a kubeml worker"))
+        return cls(ctx.job_id, ctx.N, ctx.K, ctx.task, ctx.func_id, ctx.epoch, ctx.lr, ctx.batch_size)
+
+
+class KubeDataset(data.Dataset, ABC):
+
+    def __init__(self, dataset: str):
+        self.dataset = dataset
+        self._mode = None
+        self._store = _store()
+        self._args = None
+        self.data, self.labels = None, None
+        if not self._store.exists(dataset):
+            raise DatasetNotFoundError()
+        self.num_docs = self._store.num_docs(dataset, "train")
+        self.num_val_docs = self._store.num_docs(dataset, "test")
+        self._resident = {}
+
+    # --- mode --------------------------------------------------------------------
+    def _eval(self):
+        self._mode = "val"
+
+    def _train(self):
+        self._mode = "train"
+
+    def is_training(self) -> bool:
+        return self._mode == "train"
+
+    # --- loading (document ids are 64-sample subsets, reference semantics) ----------
+    def _load_train_data(self, start: int, end: int):
+        self.data, self.labels = self._store.load_docs(self.dataset, "train", start, end)
+        self._train()
+
+    def _load_validation_data(self, start: int, end: int):
+        self.data, self.labels = self._store.load_docs(self.dataset, "test", start, end)
+        self._eval()
+
+    def _close(self):
+        pass
+
+    # --- MI355X extras -------------------------------------------------------------
+    def device_split(self, split: str = "train", device=None) -> Tuple["object", "object"]:
+        """Whole split resident in HBM as (uint8/float data, int64 labels) tensors."""
+        import torch
+        key = (split, str(device))
+        if key not in self._resident:
+            d, l = self._store.open(self.dataset, split)
+            x = torch.from_numpy(np.ascontiguousarray(d.arr)).to(device, non_blocking=True)
+            y = torch.from_numpy(np.ascontiguousarray(l.arr).reshape(-1).astype(np.int64)).to(device)
+            self._resident[key] = (x, y)
+        return self._resident[key]
+
+    def collate_batch(self, data: np.ndarray, labels: np.ndarray):  # optional user hook
+        raise NotImplementedError
+
+    def has_batch_hook(self) -> bool:
+        return type(self).collate_batch is not KubeDataset.collate_batch
+
+    @abstractmethod
+    def __len__(self):
+        ...

@@ -37,8 +37,9 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_dgrad_wgrad(case):
+def test_conv_fwd_dgrad_wgrad(case, variant):
     from kubeml_amd.ops import kernels as K
     B, H, W, Ci, Co, k, s, p = case
     torch.manual_seed(0)
@@ -48,7 +49,11 @@ def test_conv_fwd_dgrad_wgrad(case):
     wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=s, padding=p)
     stats = torch.zeros(2 * Co, device=dev)
-    y = K.conv_fwd(x, w, k, k, (s, s), (p, p), stats=stats)
+    M, Nn = B * yr.shape[2] * yr.shape[3], Co
+    cfg = lambda mode, m, n, kd: (K.plan_conv(mode, m, n, kd)[:4] + (variant,))
+    r0, r1, s0, s1 = K.tap_window(H, W, k, k, s, s, p, p)
+    ntap = (r1 - r0) * (s1 - s0)
+    y = K.conv_fwd(x, w, k, k, (s, s), (p, p), stats=stats, cfg=cfg("fwd", M, Co, ntap * Ci))
     assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
     yf = yr.detach().permute(0, 2, 3, 1).reshape(-1, Co)
     assert torch.allclose(stats[:Co], yf.sum(0), rtol=2e-2, atol=1e-1 * (yf.shape[0] ** 0.5))
@@ -56,10 +61,43 @@ def test_conv_fwd_dgrad_wgrad(case):
     dy = _bf(torch.randn_like(yr))
     yr.backward(dy.float())
     dyn = dy.permute(0, 2, 3, 1).contiguous()
-    dx = K.conv_dgrad(dyn, w, x.shape, k, k, (s, s), (p, p))
+    dx = K.conv_dgrad(dyn, w, x.shape, k, k, (s, s), (p, p), cfg=cfg("dgrad", B * H * W, Ci, ntap * Co))
     assert _rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
     dw = torch.zeros(Co, k, k, Ci, device=dev)
-    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p))
+    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p), cfg=cfg("wgrad", Co, ntap * Ci, M))
+    assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < 1e-2
+
+
+SPLIT_CFGS = [(64, 64, 64, 8, 0), (32, 32, 32, 4, 0), (128, 64, 64, 2, 0), (64, 128, 32, 16, 0), (32, 64, 64, 1, 0),
+              (64, 64, 64, 1, 1), (32, 32, 64, 4, 1), (128, 128, 64, 2, 1), (32, 128, 64, 1, 2), (128, 32, 64, 8, 2),
+              (64, 32, 64, 3, 1)]
+
+
+@pytest.mark.parametrize("cfg", SPLIT_CFGS)
+def test_conv_splitk_configs(cfg):
+    """Every (tile, BK, split-K) path — incl. the last-arriver slab reduction — matches fp32."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(2)
+    B, H, W, Ci, Co, k, s, p = 16, 4, 4, 128, 256, 3, 1, 1
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * 0.03)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=s, padding=p)
+    stats = torch.zeros(2 * Co, device=dev)
+    for _ in range(3):  # repeated launches reuse the ticket counters (reset by last arrivers)
+        stats.zero_()
+        y = K.conv_fwd(x, w, k, k, (s, s), (p, p), stats=stats, cfg=cfg)
+        assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    assert _rel(stats[:Co], yr.detach().sum((0, 2, 3))) < 2e-2
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    dx = K.conv_dgrad(dyn, w, x.shape, k, k, (s, s), (p, p), addend=add, cfg=cfg)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
+    dw = torch.zeros(Co, k, k, Ci, device=dev)
+    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p), cfg=cfg)
     assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < 1e-2
 
 
