@@ -36,11 +36,12 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=0.0)
+    ap.add_argument("--trace-loss", action="store_true", help="print the loss of every step (debug; syncs)")
+    ap.add_argument("--seed", type=int, default=1234)
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -55,10 +56,10 @@ def main():
     from kubeml_amd.ops import kernels as K
     from kubeml_amd.optim import SGD
 
-    torch.manual_seed(1234 + rank)
     B = args.batch
-    # synthetic CIFAR-10 shard resident in HBM (each rank its own shard, like split_minibatches)
     n_local = CIFAR_TRAIN // world
+
+    # synthetic CIFAR-10 shard resident in HBM (each rank its own shard, like split_minibatches)
     g = torch.Generator(device=dev).manual_seed(rank)
     data = torch.randint(0, 256, (n_local, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
     labels = torch.randint(0, 10, (n_local,), dtype=torch.int64, device=dev, generator=g)
@@ -66,7 +67,7 @@ def main():
     xbuf = torch.empty((B, 32, 32, 8), dtype=torch.bfloat16, device=dev)
     ybuf = torch.empty((B,), dtype=torch.int64, device=dev)
 
-    torch.manual_seed(1234)  # identical init on every rank
+    torch.manual_seed(args.seed)  # identical init on every rank
     model = resnet34(num_classes=1000).to(dev)
     space = flatten_module(model)
     if world > 1:
@@ -87,8 +88,8 @@ def main():
         opt.step()
         K.advance_counter_(ctr, B, n_local)
 
-    step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph,
-                            warmup=3, bucket_mb=args.bucket_mb)
+    step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
+                            bucket_mb=args.bucket_mb)
     step.capture()
     for _ in range(args.warmup):
         loss = step()
@@ -99,8 +100,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         loss = step()
+        if args.trace_loss and rank == 0:
+            print(f"step {i} loss {float(loss.item()):.4f} gnorm {float(space.grad.norm()):.3e}", flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

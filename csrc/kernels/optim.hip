@@ -147,6 +147,8 @@ __global__ void k_scale_inv_dev(float* __restrict__ p, const float* __restrict__
 
 }  // namespace
 
+// NOTE: hipMemsetAsync is avoided on capturable paths (graph memset nodes raced with
+// kernel nodes on this ROCm build); use kml_zero from util.hip.
 KML_API int kml_memset(void* p, int value, long long bytes, hipStream_t s) {
   return (int)hipMemsetAsync(p, value, (size_t)bytes, s);
 }
@@ -172,8 +174,10 @@ KML_API int kml_increment(float* p, float by, hipStream_t s) {
   KML_LAUNCH_CHECK();
 }
 
+__global__ void k_zero1(float* p) { if (threadIdx.x == 0) *p = 0.f; }
+
 KML_API int kml_clip_grad_norm(float* g, float* ws1, float max_norm, long long n, hipStream_t s) {
-  hipMemsetAsync(ws1, 0, sizeof(float), s);
+  hipLaunchKernelGGL(k_zero1, dim3(1), dim3(64), 0, s, ws1);
   hipLaunchKernelGGL(k_sumsq, dim3(kml_stream_grid(n, 256 * 4)), dim3(256), 0, s, g, ws1, n);
   hipLaunchKernelGGL(k_clip_scale, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, g, ws1, max_norm, n);
   KML_LAUNCH_CHECK();

@@ -142,3 +142,26 @@ KML_API int kml_nchw_to_nhwc_bf16(const float* x, bf16_t* y, int B, int C, int H
   hipLaunchKernelGGL(k_nchw_to_nhwc_bf16, dim3(kml_stream_grid(total, 256)), dim3(256), 0, s, x, y, B, C, HW, CP);
   KML_LAUNCH_CHECK();
 }
+
+// Zero a byte range with a kernel.  Used instead of hipMemsetAsync everywhere on the
+// training path: a memset captured into a hipGraph (memset node) was observed on this
+// ROCm build to race with the following kernel nodes (graph-replay corruption,
+// tools/graph_stress.py), whereas a kernel node is ordered like every other kernel.
+__global__ void k_zero_bytes(unsigned char* __restrict__ p, long long bytes, int aligned) {
+  const long long n16 = aligned ? (bytes >> 4) : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  uint4 z = {0, 0, 0, 0};
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<uint4*>(p)[i] = z;
+  for (long long i = (n16 << 4) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < bytes; i += stride)
+    p[i] = 0;
+}
+
+KML_API int kml_zero(void* p, long long bytes, hipStream_t s) {
+  // unaligned base (rare; framework buffers are 256-B aligned): byte loop only
+  const int aligned = (((unsigned long long)p) & 15ull) == 0;
+  const long long work = aligned ? (bytes + 15) / 16 : bytes;
+  hipLaunchKernelGGL(k_zero_bytes, dim3(kml_stream_grid(work, 256)), dim3(256), 0, s, (unsigned char*)p, bytes,
+                     aligned);
+  KML_LAUNCH_CHECK();
+}

@@ -117,7 +117,19 @@ def plan_conv(mode, M, N, Kd):
     1/2 = LDS-DMA (global_load_lds) pipeline with 3/4 stages (BK fixed at 64)."""
     cfg = _TUNED.get((mode, M, N, Kd))
     cfg = cfg if cfg is not None else default_plan(mode, M, N, Kd)
-    return tuple(cfg) + (0,) * (5 - len(cfg))
+    cfg = list(tuple(cfg) + (0,) * (5 - len(cfg)))
+    if _DBG_NOGLDS:
+        cfg[4] = 0
+    if _DBG_NOSPLIT and mode != "wgrad":
+        cfg[3] = 1
+    if _DBG_NOSPLIT_W and mode == "wgrad":
+        cfg[3] = 1
+    return tuple(cfg)
+
+
+_DBG_NOGLDS = os.environ.get("KUBEML_CONV_NOGLDS") == "1"
+_DBG_NOSPLIT = os.environ.get("KUBEML_CONV_NOSPLIT") == "1"
+_DBG_NOSPLIT_W = os.environ.get("KUBEML_CONV_NOSPLIT_W") == "1"
 
 
 def _norm_cfg(cfg):
@@ -306,8 +318,20 @@ def add_bf16(a, b, out=None):
     return out
 
 
+def fill_(t, value=0.0):
+    """fp32 fill with a kernel (graph-safe alternative to a memset node)."""
+    _chk(t, F32, "t")
+    HIP.call("kml_fill_f32", "p f l s", _p(t), float(value), t.numel(), _s())
+    return t
+
+
 def memset_(t, value=0):
-    HIP.call("kml_memset", "p i l s", _p(t), int(value), t.numel() * t.element_size(), _s())
+    """Zero a tensor with a kernel (graph-safe; see kml_zero in util.hip)."""
+    if value != 0:
+        raise ValueError("only zero fill is supported")
+    if not t.is_contiguous():
+        raise ValueError("memset_ needs a contiguous tensor")
+    HIP.call("kml_zero", "p l s", _p(t), t.numel() * t.element_size(), _s())
     return t
 
 

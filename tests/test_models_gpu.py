@@ -44,11 +44,25 @@ def test_resnet34_forward_backward_matches_reference():
     # logits vs fp64 and ours at ~0.097 — the bound below is that drift, not slack.
     assert _rel(lo, lr_) < 0.15
     assert abs(loss_o.item() - loss_r.item()) < 0.03 * abs(loss_r.item())
-    pr = dict(ref.named_parameters())
+    # Early-layer gradients of a 36-layer net in train-mode BN on 32 images are
+    # ill-conditioned: stock bf16 autocast is itself ~0.6 rel. off the fp64 gradient
+    # there (tools/diag_resnet.py grads).  So bound ours by the autocast drift measured
+    # in the same run against an fp64 reference, parameter by parameter.
+    from kubeml_amd.models import torch_reference as R
+    ref64 = R.resnet34(1000).to(dev).double()
+    ref64.load_state_dict(ref.state_dict())
+    ref64.train()
+    F.cross_entropy(ref64(xb.double()), y).backward()
+    ac = R.resnet34(1000).to(dev)
+    ac.load_state_dict(ref.state_dict())
+    ac.train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        la = ac(xb)
+    F.cross_entropy(la.float(), y).backward()
+    p64, pac = dict(ref64.named_parameters()), dict(ac.named_parameters())
     for name, p in ours.named_parameters():
-        if name in ("conv1.weight", "fc.weight", "fc.bias", "layer1.0.conv1.weight", "layer4.2.bn2.weight",
-                    "layer3.0.downsample.0.weight", "bn1.weight"):
-            assert _rel(p.grad, pr[name].grad) < 0.2, name
+        e_ours, e_ac = _rel(p.grad.double(), p64[name].grad), _rel(pac[name].grad.double(), p64[name].grad)
+        assert e_ours < 1.3 * e_ac + 0.05, (name, e_ours, e_ac)
     # running stats updated like torch
     assert _rel(ours.layer2[0].bn1.running_mean, ref.layer2[0].bn1.running_mean) < 0.05
     sd = ours.state_dict()

@@ -1,0 +1,163 @@
+"""CPU tests: sharding math parity, API wire types, error envelope, policy, comm, K-AVG."""
+import json
+import math
+import threading
+
+import pytest
+import torch
+
+from kubeml_amd.api import types as T
+from kubeml_amd.api.errors import DatasetNotFoundError, KubeMLException, MergeError, check_function_error
+from kubeml_amd.sdk.util import get_subset_period, max_rounds, num_rounds, split_minibatches
+
+
+# ------------------------------------------------------------------ sharding parity
+def _ref_split(a, n):  # reference python/kubeml/kubeml/util.py:46-56 (verbatim semantics)
+    k, m = divmod(len(a), n)
+    return [a[i * k + min(i, m):(i + 1) * k + min(i + 1, m)] for i in range(n)]
+
+
+@pytest.mark.parametrize("docs,n", [(782, 1), (782, 2), (782, 3), (782, 8), (157, 5), (7, 8), (0, 3)])
+def test_split_minibatches_matches_reference(docs, n):
+    got = split_minibatches(range(docs), n)
+    assert got == _ref_split(range(docs), n)
+    assert sum(len(r) for r in got) == docs
+    assert max(len(r) for r in got) - min(len(r) for r in got) <= 1
+
+
+@pytest.mark.parametrize("K,b,expect", [(-1, 64, 98), (1, 64, 1), (8, 32, 4), (16, 128, 32), (10, 100, 16)])
+def test_get_subset_period(K, b, expect):
+    assigned = range(0, 98)
+    assert get_subset_period(K, b, assigned) == expect
+    if K != -1:
+        assert expect == math.ceil(b * K / 64)
+
+
+def test_rounds_schedule():
+    # uneven shards: every rank joins max_rounds collectives
+    docs, N, K, b = 101, 4, 2, 64
+    per_rank = [num_rounds(docs, N, K, b, i) for i in range(N)]
+    assert max_rounds(docs, N, K, b) == max(per_rank)
+    assert max(per_rank) - min(per_rank) <= 1
+
+
+# ------------------------------------------------------------------ wire types
+def test_train_request_json_names_match_reference():
+    req = T.TrainRequest(model_type="example", batch_size=128, epochs=3, dataset="cifar10", lr=0.1,
+                         function_name="resnet34",
+                         options=T.TrainOptions(default_parallelism=4, static_parallelism=True, validate_every=1,
+                                                k=8, goal_accuracy=90))
+    d = json.loads(req.to_json())
+    assert set(d) == {"model_type", "batch_size", "epochs", "dataset", "lr", "function_name", "options"}
+    assert set(d["options"]) == {"default_parallelism", "static_parallelism", "validate_every", "k", "goal_accuracy"}
+    back = T.TrainRequest.from_json(json.dumps(d))
+    assert back == req
+    task = T.TrainTask(request=req, job=T.JobInfo(id="abc12345", state=T.JobState(parallelism=4, elapsed_time=1.5)))
+    t2 = T.TrainTask.from_dict(json.loads(task.to_json()))
+    assert t2 == task and set(json.loads(task.to_json())) == {"request", "job"}
+    assert "validations_loss" in T.MetricUpdate().to_dict()  # reference spelling preserved
+    assert set(T.JobHistory().to_dict()) == {"validation_loss", "accuracy", "train_loss", "parallelism",
+                                             "epoch_duration"}
+    assert set(T.DatasetSummary().to_dict()) == {"name", "train_set_size", "test_set_size"}
+
+
+def test_error_envelope():
+    e = DatasetNotFoundError()
+    assert e.to_dict() == {"error": "Dataset not found in storage service", "code": 404}
+    assert MergeError(RuntimeError("x")).status_code == 500
+    err = check_function_error(500, {"error": "boom", "code": 500})
+    assert isinstance(err, KubeMLException) and err.message == "boom"
+    assert check_function_error(200, {}) is None
+
+
+# ------------------------------------------------------------------ native policy
+def test_throughput_policy_native():
+    from kubeml_amd.control.policy import ThroughputPolicy
+    p = ThroughputPolicy(max_parallelism=8)
+    par, op = p.decide("j1", default=2, parallelism=0, elapsed=0)
+    assert (par, op) == (2, "create")
+    assert p.decide("j1", 2, 2, 10.0) == (3, "update")      # no reference time -> +1
+    assert p.decide("j1", 2, 3, 10.4) == (4, "update")      # <= 1.05x -> +1
+    assert p.decide("j1", 2, 4, 11.5) == (4, "update")      # between -> keep
+    assert p.decide("j1", 2, 4, 13.0) == (3, "update")      # >= 1.2x of 10.4 -> -1
+    # clamps (reference could reach 0 / exceed the node)
+    q = ThroughputPolicy(max_parallelism=4)
+    q.decide("j", 9, 0, 0)
+    assert q.decide("j", 9, 4, 1.0)[0] == 4
+    r = ThroughputPolicy(max_parallelism=8)
+    r.decide("k", 1, 0, 0)
+    r.decide("k", 1, 1, 1.0)
+    assert r.decide("k", 1, 1, 10.0)[0] == 1
+    p.finish("j1")
+    assert p.decide("j1", 5, 0, 0) == (5, "create")
+
+
+def test_policy_thread_safety():
+    from kubeml_amd.control.policy import ThroughputPolicy
+    p = ThroughputPolicy(max_parallelism=8)
+    errs = []
+
+    def work(i):
+        try:
+            for k in range(200):
+                p.decide(f"job{i}", 2, 2, float(k % 7 + 1))
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs
+
+
+# ------------------------------------------------------------------ comm / K-AVG
+def _run_threads(n, fn):
+    from kubeml_amd.parallel.comm import ThreadComm
+    comms = ThreadComm.create(n)
+    out = [None] * n
+    errs = []
+
+    def w(r):
+        try:
+            out[r] = fn(comms[r])
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ts = [threading.Thread(target=w, args=(r,)) for r in range(n)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errs, errs
+    return out
+
+
+def test_thread_comm_masked_average():
+    def fn(c):
+        t = torch.full((1000,), float(c.rank + 1))
+        n = c.average_([t], participate=(c.rank != 2))
+        return n, float(t[0])
+    res = _run_threads(4, fn)
+    # ranks 0,1,3 contribute 1,2,4 -> mean 7/3; rank 2 excluded from the divisor
+    for n, v in res:
+        assert n == 3 and abs(v - 7 / 3) < 1e-6
+
+
+def test_kavg_model_average_and_int_buffers():
+    from kubeml_amd.parallel.kavg import ModelAverager
+    from kubeml_amd.models.torch_reference import LeNet
+
+    def fn(c):
+        torch.manual_seed(c.rank)
+        m = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.BatchNorm1d(3))
+        m[1].num_batches_tracked.fill_(c.rank * 3 + 1)  # 1, 4 -> floor(5/2) = 2
+        w0 = m[0].weight.detach().clone()
+        ModelAverager(m).average_(c, True)
+        return w0, m[0].weight.detach().clone(), int(m[1].num_batches_tracked)
+    res = _run_threads(2, fn)
+    mean = (res[0][0] + res[1][0]) / 2
+    assert torch.allclose(res[0][1], mean) and torch.allclose(res[1][1], mean)
+    assert res[0][2] == res[1][2] == 2
+
+
+def test_native_merger_sum():
+    from kubeml_amd.parallel.comm import _native_reduce
+    xs = [torch.randn(300000) for _ in range(3)]
+    got = _native_reduce(xs, "sum")
+    assert torch.allclose(got, xs[0] + xs[1] + xs[2], atol=1e-5)
