@@ -171,6 +171,112 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_reduce(
   }
 }
 
+// Two-level deterministic variant of k_bn_bwd_reduce: every block reduces a contiguous
+// row range into part[block][2C] (no atomics), then the last block to arrive (ticket)
+// sums the partials in block order and adds them into dbeta/dgamma.  Gives ~8x more
+// blocks than the atomic version without same-address atomic contention (which crosses
+// XCD L2s), and bitwise-reproducible gradients.
+__global__ __launch_bounds__(TPB) void k_bn_bwd_reduce2(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ part, unsigned* __restrict__ counter, long long M, int C,
+    int rows_per_block) {
+  const int CH = C / 8;
+  const int rows_per_iter = TPB / CH;
+  const int tid = threadIdx.x;
+  const int chunk = tid % CH, rsub = tid / CH;
+  float sd[8] = {0}, sx[8] = {0}, mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mu[i] = mean[chunk * 8 + i]; rs[i] = rstd[chunk * 8 + i]; }
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  if (rsub < rows_per_iter) {
+#pragma unroll 2
+    for (long long r = r0 + rsub; r < r1; r += rows_per_iter) {
+      const long long off = r * C + chunk * 8;
+      float d[8], xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + off), d);
+      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+      if (y) {
+        float yv[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { sd[i] += d[i]; sx[i] += d[i] * (xv[i] - mu[i]) * rs[i]; }
+    }
+  }
+  __shared__ float red[TPB][17];
+  __shared__ unsigned last;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = sd[i]; red[tid][8 + i] = sx[i]; }
+  __syncthreads();
+  float* mine = part + (long long)blockIdx.x * 2 * C;
+  if (tid < CH) {
+    float a1[8] = {0}, a2[8] = {0};
+    for (int rr = 0; rr < rows_per_iter; ++rr) {
+      const int t = rr * CH + tid;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a1[i] += red[t][i]; a2[i] += red[t][8 + i]; }
+    }
+    float4* o = reinterpret_cast<float4*>(mine);
+    o[tid * 2] = make_float4(a1[0], a1[1], a1[2], a1[3]);
+    o[tid * 2 + 1] = make_float4(a1[4], a1[5], a1[6], a1[7]);
+    o[CH * 2 + tid * 2] = make_float4(a2[0], a2[1], a2[2], a2[3]);
+    o[CH * 2 + tid * 2 + 1] = make_float4(a2[4], a2[5], a2[6], a2[7]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned l = (t == gridDim.x - 1) ? 1u : 0u;
+    if (l) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = l;
+  }
+  __syncthreads();
+  if (!last) return;
+  // last arriver: sum G partial rows of 2C floats, float4 groups x row slices
+  const int Q = C / 2;                       // float4 groups per partial row
+  const int S = Q >= TPB ? 1 : TPB / Q;      // row slices
+  const int G = gridDim.x;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int q = tid % (Q < TPB ? Q : TPB); q < Q; q += TPB) {
+    const int sl = Q >= TPB ? 0 : tid / Q;
+    if (sl >= S) break;
+    acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = sl; g < G; g += S) {
+      const float4 v = reinterpret_cast<const float4*>(part + (long long)g * 2 * C)[q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if (S == 1) {
+      float* dst = q < Q / 2 ? dbeta + q * 4 : dgamma + (q - Q / 2) * 4;
+      dst[0] += acc.x; dst[1] += acc.y; dst[2] += acc.z; dst[3] += acc.w;
+    }
+  }
+  if (S == 1) return;
+  // S > 1: combine slices through LDS (reuse red as [S][Q] float4 = 4*TPB floats)
+  float4* r4 = reinterpret_cast<float4*>(&red[0][0]);
+  __syncthreads();
+  if (tid < S * Q) r4[tid] = acc;
+  __syncthreads();
+  if (tid < Q) {
+    float4 t4 = r4[tid];
+    for (int sl = 1; sl < S; ++sl) {
+      const float4 v = r4[sl * Q + tid];
+      t4.x += v.x; t4.y += v.y; t4.z += v.z; t4.w += v.w;
+    }
+    float* dst = tid < Q / 2 ? dbeta + tid * 4 : dgamma + (tid - Q / 2) * 4;
+    dst[0] += t4.x; dst[1] += t4.y; dst[2] += t4.z; dst[3] += t4.w;
+  }
+}
+
 __global__ __launch_bounds__(TPB) void k_bn_bwd_apply(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -242,6 +348,16 @@ __global__ void k_relu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
   }
 }
 
+// blocks for k_bn_bwd_reduce2: ~4 row iterations per thread, at most 1024 blocks
+int bwd_blocks(long long M, int C, int* rows_per_block) {
+  const int rpi = TPB / (C / 8);
+  long long rpb = (long long)rpi * 4;
+  long long g = (M + rpb - 1) / rpb;
+  if (g > 1024) { rpb = ((M + 1023) / 1024 + rpi - 1) / rpi * rpi; g = (M + rpb - 1) / rpb; }
+  *rows_per_block = (int)rpb;
+  return (int)g;
+}
+
 unsigned rows_grid(long long M, int C) {
   const int rpi = TPB / (C / 8);
   long long g = (M + rpi * 8 - 1) / (rpi * 8);  // >= 8 rows per thread
@@ -269,12 +385,27 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, const float* gamma
   KML_LAUNCH_CHECK();
 }
 
+// number of fp32 workspace floats kml_bn_bwd needs for the deterministic reduce
+KML_API long long kml_bn_bwd_ws_floats(long long M, int C) {
+  int rpb;
+  return (long long)bwd_blocks(M, C, &rpb) * 2 * C;
+}
+
+// ws/counter null => single-pass atomic reduce; else two-level deterministic reduce
+// (ws holds kml_bn_bwd_ws_floats(M, C) floats, *counter == 0 on entry and on exit).
 KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
-                       const float* gamma, float* dgamma, float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C,
-                       hipStream_t s) {
+                       const float* gamma, float* dgamma, float* dbeta, bf16_t* dx, bf16_t* dres, float* ws,
+                       unsigned* counter, long long M, int C, hipStream_t s) {
   if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(rows_grid(M, C)), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta,
-                     M, C);
+  if (ws && counter) {
+    int rpb;
+    const int g = bwd_blocks(M, C, &rpb);
+    hipLaunchKernelGGL(k_bn_bwd_reduce2, dim3(g), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
+                       counter, M, C, rpb);
+  } else {
+    hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(rows_grid(M, C)), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma,
+                       dbeta, M, C);
+  }
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 5 * C * sizeof(float), s,
                      dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx, dres, M, C);
   KML_LAUNCH_CHECK();

@@ -286,6 +286,10 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
     return y
 
 
+# deterministic two-level BN-backward reduce (default); KUBEML_BN_ATOMIC=1 -> atomic path
+_BN_DET = os.environ.get("KUBEML_BN_ATOMIC", "0") != "1"
+
+
 def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
     """dgamma/dbeta (+=) and dx; y given => ReLU mask applied; dres (optional) receives dz."""
     _chk(dy, BF16, "dy")
@@ -294,9 +298,14 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
     M = x.numel() // C
     if dx is None:
         dx = torch.empty_like(x)
-    HIP.call("kml_bn_bwd", "p p p p p p p p p p l i s",
+    ws = cnt = None
+    if _BN_DET:
+        nws = HIP.raw("kml_bn_bwd_ws_floats", M, C)
+        ws = torch.empty(nws, dtype=F32, device=x.device)
+        cnt = _COUNTERS.take(x.device, 1)
+    HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i s",
              _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
-             _p(dres), M, C, _s())
+             _p(dres), _p(ws), _p(cnt), M, C, _s())
     return dx
 
 

@@ -111,7 +111,9 @@ def test_conv_fwd_bias_relu():
     assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
 
 
-@pytest.mark.parametrize("C,M,relu,res", [(64, 4096, True, False), (128, 1000, True, True), (512, 64, False, True)])
+@pytest.mark.parametrize("C,M,relu,res", [(64, 4096, True, False), (128, 1000, True, True), (512, 64, False, True),
+                                          (2048, 96, True, False), (64, 300000, True, True), (8, 50, False, False),
+                                          (1024, 1031, True, False)])
 def test_bn_train_fwd_bwd(C, M, relu, res):
     from kubeml_amd.ops import kernels as K
     torch.manual_seed(1)
@@ -148,6 +150,11 @@ def test_bn_train_fwd_bwd(C, M, relu, res):
     assert _rel(dx, xr.grad) < 2e-2
     assert _rel(dg, gr.grad) < 1e-2
     assert _rel(db, br.grad) < 1e-2
+    # the two-level reduce is deterministic: same inputs -> bitwise-identical grads
+    dg2 = torch.zeros(C, device=dev)
+    db2 = torch.zeros(C, device=dev)
+    K.bn_bwd(dy, y if relu else None, x, mean, rstd, g, dg2, db2)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
 
 
 def test_maxpool_and_gavg():
