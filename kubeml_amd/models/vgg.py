@@ -1,0 +1,124 @@
+"""VGG-11/16 (+BN) on the MI355X layers — north-star config 4 (VGG-16 / CIFAR-100) and
+the reference's VGG-11 function (ml/experiments/kubeml/function_vgg11.py:10-12 uses
+``torchvision.models.vgg11``).
+
+``state_dict`` names follow torchvision (``features.<i>.*``, ``classifier.<i>.*``) so
+checkpoints interoperate.  Two heads:
+
+* ``head="imagenet"`` — torchvision's: AdaptiveAvgPool2d(7) + 25088→4096→4096→classes.
+  On 32×32 CIFAR input the feature map is 1×1 and the 7×7 pool is a replication;
+* ``head="cifar"`` (default for the CIFAR configs) — 512→4096→4096→classes, as in the
+  pytorch-cifar100 recipe the reference cites (function_vgg11.py:14-15).
+
+Activations are NHWC bf16 on the GPU; Conv→BN→ReLU triples run as conv (MFMA
+implicit GEMM with BN-statistics epilogue) + one fused BN-apply+ReLU kernel.
+"""
+from __future__ import annotations
+
+from typing import List, Union
+
+import torch
+import torch.nn as tnn
+
+from ..nn.modules import BatchNorm2d, Conv2d, Flatten, Linear, MaxPool2d, ReLU, to_nhwc
+
+CFGS = {
+    "vgg11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
+    "vgg13": [64, 64, "M", 128, 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
+    "vgg16": [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"],
+}
+
+
+def make_features(cfg: List[Union[int, str]], batch_norm: bool, in_ch: int = 3) -> tnn.Sequential:
+    layers = []
+    c = in_ch
+    for v in cfg:
+        if v == "M":
+            layers.append(MaxPool2d(2, 2))
+        else:
+            layers.append(Conv2d(c, v, 3, padding=1))
+            if batch_norm:
+                layers.append(BatchNorm2d(v))
+            layers.append(ReLU(inplace=True))
+            c = v
+    return tnn.Sequential(*layers)
+
+
+class _Replicate7(tnn.Module):
+    """AdaptiveAvgPool2d((7, 7)) on a 1x1 map = replicate (torchvision head on CIFAR)."""
+
+    def forward(self, x):
+        B, H, W, C = x.shape
+        if (H, W) == (7, 7):
+            return x
+        if (H, W) != (1, 1):
+            raise NotImplementedError("imagenet head expects 1x1 or 7x7 feature maps")
+        return x.expand(B, 7, 7, C).contiguous()
+
+
+class VGG(tnn.Module):
+    def __init__(self, cfg: str = "vgg16", batch_norm: bool = True, num_classes: int = 100, head: str = "cifar",
+                 dropout: float = 0.5):
+        super().__init__()
+        self.features = make_features(CFGS[cfg], batch_norm)
+        self.head = head
+        if head == "imagenet":
+            self.avgpool = _Replicate7()
+            fin = 512 * 7 * 7
+        else:
+            self.avgpool = None
+            fin = 512
+        self.flatten = Flatten()
+        self.classifier = tnn.Sequential(
+            Linear(fin, 4096), ReLU(True), tnn.Dropout(dropout),
+            Linear(4096, 4096), ReLU(True), tnn.Dropout(dropout),
+            Linear(4096, num_classes))
+        for m in self.modules():
+            if isinstance(m, Conv2d):
+                tnn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+                if m.bias is not None:
+                    tnn.init.zeros_(m.bias)
+            elif isinstance(m, BatchNorm2d):
+                tnn.init.ones_(m.weight)
+                tnn.init.zeros_(m.bias)
+            elif isinstance(m, Linear):
+                tnn.init.normal_(m.weight, 0, 0.01)
+                tnn.init.zeros_(m.bias)
+
+    def _features(self, x):
+        mods = list(self.features)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, BatchNorm2d) and i + 1 < len(mods) and isinstance(mods[i + 1], ReLU):
+                x = m(x, relu=True)  # fused BN-apply + ReLU
+                i += 2
+                continue
+            x = m(x)
+            i += 1
+        return x
+
+    def forward(self, x):
+        x = to_nhwc(x, 8)
+        x = self._features(x)
+        if self.avgpool is not None:
+            x = self.avgpool(x)
+        x = self.flatten(x)
+        return self.classifier(x)
+
+
+def vgg11(num_classes: int = 1000, batch_norm: bool = False, head: str = "imagenet", **kw) -> VGG:
+    """torchvision ``vgg11()`` layout (the reference's VGG-11 function)."""
+    return VGG("vgg11", batch_norm, num_classes, head, **kw)
+
+
+def vgg11_bn(num_classes: int = 100, head: str = "cifar", **kw) -> VGG:
+    return VGG("vgg11", True, num_classes, head, **kw)
+
+
+def vgg16(num_classes: int = 100, batch_norm: bool = True, head: str = "cifar", **kw) -> VGG:
+    """VGG-16-BN / CIFAR-100 (north-star config 4)."""
+    return VGG("vgg16", batch_norm, num_classes, head, **kw)
+
+
+vgg16_bn = vgg16

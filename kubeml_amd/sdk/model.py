@@ -32,9 +32,22 @@ from torch.utils.data import DataLoader
 from ..api.errors import DataError, InvalidFormatError, KubeMLException, MergeError
 from ..parallel.comm import LocalComm
 from ..parallel.kavg import ModelAverager
+from ..utils import fault, trace
 from .context import current_task
 from .dataset import KubeDataset, _KubeArgs
 from .util import get_gpu, get_subset_period, max_rounds, split_minibatches
+
+
+def _same_but_lr(a, b) -> bool:
+    if type(a) is not type(b) or len(a.param_groups) != len(b.param_groups):
+        return False
+    for ga, gb in zip(a.param_groups, b.param_groups):
+        if [id(p) for p in ga["params"]] != [id(p) for p in gb["params"]]:
+            return False
+        for k, v in ga.items():
+            if k not in ("params", "lr", "initial_lr") and gb.get(k) != v:
+                return False
+    return True
 
 
 class KubeModel(ABC):
@@ -113,6 +126,11 @@ class KubeModel(ABC):
 
     # ---- optimizer -------------------------------------------------------------------------
     def _config_optimizer(self):
+        """``configure_optimizers`` runs at every train task, as in the reference where
+        each invocation builds a fresh optimizer (user code may derive the LR from
+        ``self.epoch``, function_resnet34.py:51-62).  On the resident GPU model an
+        optimizer that only differs in LR is kept and retuned through its device LR
+        scalar, so captured hipGraphs stay valid."""
         opt = self.configure_optimizers()
         if opt is not None and self.device is not None and self.device.type == "cuda":
             from ..optim import from_torch
@@ -120,6 +138,17 @@ class KubeModel(ABC):
                 opt = from_torch(opt)
             except TypeError:
                 pass
+        old = self.optimizer
+        if old is not None and opt is not None and _same_but_lr(old, opt):
+            lr = opt.param_groups[0]["lr"]
+            if hasattr(old, "set_lr"):
+                old.set_lr(lr)
+            else:
+                for g in old.param_groups:
+                    g["lr"] = lr
+            opt = old
+        elif old is not None and opt is not old:
+            self._graphed = None  # graphs captured the old optimizer's step
         self.optimizer = opt
         if opt is not None and hasattr(opt, "set_grad_scale"):
             opt.set_grad_scale(1.0)
@@ -137,8 +166,19 @@ class KubeModel(ABC):
     # ---- hooks -----------------------------------------------------------------------------
     def _on_train_start(self):
         self._set_device()
+        self._restore()
         self._network.train()
         self._config_optimizer()
+
+    def _restore(self):
+        """Resume / recovery: load the job's last reference-model checkpoint (the
+        rest of the workers receive it through the start-of-epoch broadcast)."""
+        ctx = current_task()
+        path = ctx.extra.get("restore") if ctx is not None else None
+        if path and getattr(self, "_restored_from", None) != path:
+            from ..store.ckpt import load_checkpoint
+            load_checkpoint(self._network, path)
+            self._restored_from = path
 
     def _on_train_end(self):
         pass
@@ -183,26 +223,35 @@ class KubeModel(ABC):
         N, fid, K = self.args._N, self.args._func_id, self.args._K
         num_docs = self._dataset.num_docs
         # every worker starts the epoch from the same reference model
-        self._averager.broadcast_(comm, 0)
+        with trace.span("broadcast"):
+            self._averager.broadcast_(comm, 0)
         assigned = split_minibatches(range(num_docs), N)[fid]
         per = max(get_subset_period(K, self.batch_size, assigned), 1)
         intervals = list(range(assigned.start, assigned.stop, per))
         rounds = max_rounds(num_docs, N, K, self.batch_size) if comm.world > 1 else len(intervals)
         self.logger.debug("subsets per iteration %d, rounds %d", per, rounds)
         loss, num_iterations = 0.0, 0
+        self.sync_seconds = 0.0
         for r in range(rounds):
+            fault.point("round", rank=fid, epoch=self.epoch, round=r, task="train", job=self.args._job_id)
             participate = r < len(intervals)
             if participate:
                 i = intervals[r]
-                self._dataset._load_train_data(start=i, end=min(assigned.stop, i + per))
+                with trace.span("load", docs=per):
+                    self._dataset._load_train_data(start=i, end=min(assigned.stop, i + per))
                 num_iterations += self._num_batches()
                 self._on_iteration_start()
-                for idx, batch in enumerate(self._batches()):
-                    batch = self._batch_to_device(batch)
-                    loss += float(self.train(batch, idx))
+                with trace.span("iteration", round=r):
+                    for idx, batch in enumerate(self._batches()):
+                        batch = self._batch_to_device(batch)
+                        loss += float(self.train(batch, idx))
                 self._on_iteration_end()
             try:
-                self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
+                import time as _t
+                t0 = _t.perf_counter()
+                with trace.span("average", round=r):
+                    self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
+                self.sync_seconds += _t.perf_counter() - t0
             except Exception as e:  # the reference surfaces merge failures as MergeError
                 raise MergeError(e)
         self._on_train_end()
@@ -238,14 +287,16 @@ class KubeModel(ABC):
         if not data:
             raise DataError()
         self._set_device()
-        if ctx is not None and ctx.checkpoint:
+        if ctx is not None and ctx.checkpoint and getattr(self, "_infer_ckpt", None) != ctx.checkpoint:
             from ..store.ckpt import load_checkpoint
             load_checkpoint(self._network, ctx.checkpoint)
+            self._infer_ckpt = ctx.checkpoint
         self._network.eval()
         with torch.no_grad():
             preds = self.infer(data)
         if isinstance(preds, torch.Tensor):
-            return preds.detach().float().cpu().numpy().tolist()
+            t = preds.detach().cpu()
+            return (t.float() if t.is_floating_point() else t).numpy().tolist()
         if isinstance(preds, np.ndarray):
             return preds.tolist()
         if isinstance(preds, list):
@@ -257,8 +308,11 @@ class KubeModel(ABC):
         if self.platform == "cpu" or not torch.cuda.is_available():
             self.device = torch.device("cpu")
             return
-        gid = get_gpu(self.args._func_id if self.args is not None else 0)
-        self.device = torch.device("cuda", gid)
+        ctx = current_task()
+        if ctx is not None and ctx.device is not None and getattr(ctx.device, "type", None) == "cuda":
+            self.device = ctx.device
+        else:
+            self.device = torch.device("cuda", get_gpu(self.args._func_id if self.args is not None else 0))
         torch.cuda.set_device(self.device)
         if getattr(self._network, "_kml_flat", None) is None or self._network._kml_flat.device != self.device:
             self._network.to(self.device)

@@ -1,0 +1,99 @@
+"""Reference-model checkpoints (the reference keeps the model only in RedisAI under
+``{jobId}:{layer}`` and deletes it at job end — ml/pkg/train/util.go:211-244 — so it
+has no durable checkpoint and ``infer`` cannot work).
+
+Format: safetensors, tensor names = the exact ``state_dict`` names (torchvision
+compatible for the ResNets), plus metadata ``{"jobId", "epoch", "format",
+"keys": "{jobId}:{name}"}`` so the reference's key scheme
+(python/kubeml/kubeml/network.py:456-458) is recoverable with :func:`reference_keys`.
+Loading never executes code from the file (safetensors only).
+
+Files: ``<store>/checkpoints/<jobId>.safetensors`` and a JSON sidecar with the epoch /
+history at save time, used for resume.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Optional
+
+import torch
+
+from ._fs import check_name, read_json, write_json
+
+FORMAT = "kubeml-ref-model-v1"
+
+
+def ckpt_dir(store_dir: str) -> str:
+    d = os.path.join(store_dir, "checkpoints")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def ckpt_path(store_dir: str, job_id: str) -> str:
+    return os.path.join(ckpt_dir(store_dir), check_name(job_id, "job id") + ".safetensors")
+
+
+def state_dict_cpu(module: torch.nn.Module) -> Dict[str, torch.Tensor]:
+    """Contiguous CPU copies of the state dict (our conv weights are strided views of
+    KRSC storage; safetensors needs dense tensors)."""
+    out = {}
+    for k, v in module.state_dict().items():
+        t = v.detach()
+        if t.dtype == torch.bfloat16:
+            t = t.float()
+        out[k] = t.to("cpu").contiguous().clone()
+    return out
+
+
+def save_checkpoint(module: torch.nn.Module, path: str, job_id: str = "", epoch: int = 0,
+                    extra: Optional[dict] = None) -> str:
+    from safetensors.torch import save_file
+    sd = state_dict_cpu(module)
+    meta = {"format": FORMAT, "jobId": job_id, "epoch": str(epoch), "keys": "{jobId}:{name}"}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    tmp = path + ".tmp"
+    save_file(sd, tmp, metadata=meta)
+    os.replace(tmp, path)
+    side = {"jobId": job_id, "epoch": epoch, "tensors": len(sd), **(extra or {})}
+    write_json(path + ".json", side)
+    return path
+
+
+def load_state(path: str) -> Dict[str, torch.Tensor]:
+    from safetensors.torch import load_file
+    return load_file(path)
+
+
+def load_checkpoint(module: torch.nn.Module, path: str, strict: bool = True) -> dict:
+    """Load a checkpoint into ``module`` (any device / flat-buffer layout); returns the
+    sidecar metadata (epoch, ...) if present."""
+    sd = load_state(path)
+    own = module.state_dict()
+    conv = {}
+    for k, v in sd.items():
+        if k in own:
+            conv[k] = v.to(dtype=own[k].dtype)
+        else:
+            conv[k] = v
+    with torch.no_grad():
+        module.load_state_dict(conv, strict=strict)
+    sp = getattr(module, "_kml_flat", None)
+    if sp is not None:
+        sp.refresh_shadow()
+    side = path + ".json"
+    return read_json(side) if os.path.exists(side) else {}
+
+
+def reference_keys(job_id: str, sd: Dict[str, torch.Tensor], func_id: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """The reference's tensor-store key names: ``{jobId}:{name}`` for the reference
+    model, ``{jobId}:{name}/{funcId}`` for a worker copy (network.py:456-458)."""
+    if func_id is None:
+        return {f"{job_id}:{k}": v for k, v in sd.items()}
+    return {f"{job_id}:{k}/{func_id}": v for k, v in sd.items()}
+
+
+def metadata(path: str) -> dict:
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        return dict(f.metadata() or {})

@@ -1,0 +1,99 @@
+"""Chrome-trace spans (``KUBEML_TRACE=1``) — the reference has no tracing at all
+(ad-hoc ``time.Since`` logs in job.go:307-327 only).
+
+Each process records complete events (``ph: "X"``) with wall-clock microseconds; on
+GPU workers a span can also be closed on the device timeline (``cuda=True`` syncs the
+current stream at both ends, so use it only in diagnostic runs).  ``flush()`` writes
+``<dir>/<name>-pid<pid>.json`` loadable in chrome://tracing / Perfetto.
+
+Span names used by the runtime: ``task:<kind>``, ``load``, ``iteration``,
+``average``, ``broadcast``, ``validate``, ``epoch``, ``sync-wait``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from contextlib import contextmanager
+from typing import List, Optional
+
+_enabled = os.environ.get("KUBEML_TRACE", "0").lower() in ("1", "true", "yes", "on")
+_events: List[dict] = []
+_lock = threading.Lock()
+_meta = {"rank": None, "name": "kubeml"}
+
+
+def enabled() -> bool:
+    return _enabled
+
+
+def enable(on: bool = True):
+    global _enabled
+    _enabled = on
+
+
+def set_process(name: str, rank: Optional[int] = None):
+    _meta["name"] = name
+    _meta["rank"] = rank
+
+
+@contextmanager
+def span(name: str, cat: str = "kubeml", cuda: bool = False, **args):
+    if not _enabled:
+        yield
+        return
+    if cuda:
+        _sync()
+    t0 = time.perf_counter_ns()
+    try:
+        yield
+    finally:
+        if cuda:
+            _sync()
+        t1 = time.perf_counter_ns()
+        ev = {"name": name, "cat": cat, "ph": "X", "ts": t0 / 1e3, "dur": (t1 - t0) / 1e3,
+              "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args}
+        with _lock:
+            _events.append(ev)
+
+
+def instant(name: str, **args):
+    if not _enabled:
+        return
+    with _lock:
+        _events.append({"name": name, "ph": "i", "s": "p", "ts": time.perf_counter_ns() / 1e3, "pid": os.getpid(),
+                        "tid": threading.get_ident() % 100000, "args": args})
+
+
+def _sync():
+    try:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.current_stream().synchronize()
+    except Exception:
+        pass
+
+
+def events() -> List[dict]:
+    with _lock:
+        return list(_events)
+
+
+def flush(directory: Optional[str] = None, clear: bool = True) -> Optional[str]:
+    """Write collected events; returns the file path (None if nothing recorded)."""
+    with _lock:
+        evs = list(_events)
+        if clear:
+            _events.clear()
+    if not evs:
+        return None
+    directory = directory or os.environ.get("KUBEML_TRACE_DIR", os.path.join(os.path.expanduser("~/.kubeml"), "traces"))
+    os.makedirs(directory, exist_ok=True)
+    rank = _meta["rank"]
+    name = _meta["name"] + (f"-rank{rank}" if rank is not None else "")
+    meta = [{"name": "process_name", "ph": "M", "pid": os.getpid(), "args": {"name": name}}]
+    path = os.path.join(directory, f"{name}-pid{os.getpid()}.json")
+    with open(path, "w") as f:
+        json.dump({"traceEvents": meta + evs, "displayTimeUnit": "ms"}, f)
+    return path
