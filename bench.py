@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=0.0)
     ap.add_argument("--trace-loss", action="store_true", help="print the loss of every step (debug; syncs)")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--segments", choices=["auto", "on", "off"], default="auto",
+                    help="stage-split backward with overlapped all-reduce (auto: on when N>1)")
     args = ap.parse_args()
 
     import torch
@@ -88,8 +90,23 @@ def main():
         opt.step()
         K.advance_counter_(ctr, B, n_local)
 
+    use_seg = args.segments == "on" or (args.segments == "auto" and world > 1)
+    segs = seg_grads = None
+    if use_seg:
+        # backward in 3 graph segments; each segment's gradients are all-reduced on the
+        # RCCL stream while the next segment computes (engine/staged.py)
+        from kubeml_amd.engine.staged import StagedForwardBackward
+
+        def pre():
+            K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True)
+            space.zero_grad()
+        staged = StagedForwardBackward(model.stages(), lambda out: cross_entropy(out, ybuf), lambda: xbuf, pre=pre)
+        segs = [staged.segment(k) for k in range(staged.n_segments)]
+        sp = model.stage_params()
+        seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
     step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
-                            bucket_mb=args.bucket_mb)
+                            bucket_mb=args.bucket_mb, segments=segs, segment_grads=seg_grads,
+                            force_segments=use_seg)
     step.capture()
     for _ in range(args.warmup):
         loss = step()
@@ -132,7 +149,7 @@ def main():
             "config": {"model": "resnet34 (torchvision, ImageNet stem, 1000-class head)", "global_batch": B * world,
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "all-reduce every step (K=1)",
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph, "overlap_segments": use_seg},
             "epoch_time_s": round(CIFAR_TRAIN / img_s, 3),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }

@@ -31,13 +31,27 @@ class GraphedTrainStep:
     fwd_bwd: callable running forward+backward and returning the loss tensor (device)
     opt_step: callable applying the optimizer (+ any counter advance)
     grad_buffers: list of flat fp32 gradient tensors to all-reduce (SUM) between them
+
+    Overlapped mode (``segments`` + ``segment_grads``): ``segments[0]`` is forward +
+    the first part of backward (returns the loss), ``segments[k]`` continue backward;
+    ``segment_grads[k]`` lists the gradient views that are final after segment ``k``.
+    Each segment is its own graph (shared pool); after replaying segment ``k`` the
+    all-reduce of its gradients is issued asynchronously (RCCL on the process group's
+    stream, ordered after the replay by an event) and the next segment's replay runs
+    concurrently.  Collectives are never captured, so the multi-GPU path only uses
+    plain, eagerly-issued RCCL calls.
     """
 
     def __init__(self, fwd_bwd: Callable[[], torch.Tensor], opt_step: Callable[[], None], grad_buffers=(),
-                 group=None, use_graph: bool = True, warmup: int = 3, bucket_mb: float = 0.0):
+                 group=None, use_graph: bool = True, warmup: int = 3, bucket_mb: float = 0.0,
+                 segments=None, segment_grads=None, force_segments: bool = False):
         self.fwd_bwd = fwd_bwd
         self.opt_step = opt_step
         self.grad_buffers = list(grad_buffers)
+        self.segments = list(segments) if segments else None
+        self.segment_grads = [list(g) for g in segment_grads] if segment_grads else None
+        self.force_segments = force_segments
+        self.g_seg = []
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.use_graph = use_graph
@@ -61,10 +75,31 @@ class GraphedTrainStep:
                 dist.all_reduce(buf, group=self.group)
 
     def _eager(self):
+        if self._segmented():
+            loss = None
+            works = []
+            for k, seg in enumerate(self.segments):
+                out = seg()
+                if k == 0:
+                    loss = out
+                works += self._issue(k)
+            for w in works:
+                w.wait()
+            self.opt_step()
+            return loss
         loss = self.fwd_bwd()
         self._allreduce()
         self.opt_step()
         return loss
+
+    def _segmented(self) -> bool:
+        return self.segments is not None and (self.world > 1 or self.force_segments)
+
+    def _issue(self, k):
+        """Async all-reduce of the gradients finished by segment k."""
+        if self.world <= 1 or not self.segment_grads:
+            return []
+        return [dist.all_reduce(t, group=self.group, async_op=True) for t in self.segment_grads[k] if t.numel()]
 
     def capture(self):
         if not self.use_graph or not torch.cuda.is_available():
@@ -76,7 +111,20 @@ class GraphedTrainStep:
                 self._eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        if self.world <= 1:
+        if self._segmented():
+            pool = torch.cuda.graph_pool_handle()
+            self.g_seg = []
+            for k, seg in enumerate(self.segments):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    out = seg()
+                if k == 0:
+                    self.loss = out
+                self.g_seg.append(g)
+            self.g_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_b, pool=pool):
+                self.opt_step()
+        elif self.world <= 1:
             self.g_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_a):
                 self.loss = self.fwd_bwd()
@@ -94,6 +142,15 @@ class GraphedTrainStep:
     def __call__(self):
         if not self.captured:
             self.loss = self._eager()
+            return self.loss
+        if self.g_seg:
+            works = []
+            for k, g in enumerate(self.g_seg):
+                g.replay()
+                works += self._issue(k)
+            for w in works:
+                w.wait()
+            self.g_b.replay()
             return self.loss
         self.g_a.replay()
         if self.g_b is not None:

@@ -139,20 +139,34 @@ class ResNet(tnn.Module):
 
     def forward(self, x):
         """x: NHWC bf16 (channels padded to 8) on GPU, or NCHW float (converted)."""
+        x = self._head(x)
+        x = self.layer4(self.layer3(x))
+        x = self.avgpool(x)
+        return self.fc(x)
+
+    def _head(self, x):
         if x.dim() == 4 and (x.shape[-1] not in (self.conv1.in_channels, self.conv1.cin_pad)
                              or x.dtype != torch.bfloat16 and x.is_cuda):
             x = M.to_nhwc(x, self.conv1.cin_pad)
         if x.is_cuda:
             if self.training:
-                from ..ops import kernels as K
                 self._arena.begin(x.device)
                 self._bump_counters()
             x = self._stem_gpu(x)
         else:
             x = self.maxpool(self.bn1(self.conv1(x), relu=True))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = self.avgpool(x)
-        return self.fc(x)
+        return self.layer2(self.layer1(x))
+
+    def stages(self):
+        """Forward split for overlapped gradient all-reduce (engine/staged.py):
+        [stem+layer1+layer2, layer3, layer4+head].  Parameters of later stages sit
+        first in the flat buffer, so each stage's gradients are one contiguous range."""
+        return [self._head, self.layer3, lambda h: self.fc(self.avgpool(self.layer4(h)))]
+
+    def stage_params(self):
+        """Parameters owned by each stage of :meth:`stages`."""
+        head = [p for n, p in self.named_parameters() if not n.startswith(("layer3.", "layer4.", "fc."))]
+        return [head, list(self.layer3.parameters()), list(self.layer4.parameters()) + list(self.fc.parameters())]
 
     def _bump_counters(self):
         # num_batches_tracked of every BN: one tiny kernel each is avoided by keeping

@@ -136,6 +136,24 @@ class FlatParamSpace:
             out.append((start, self.numel, members))
         return out
 
+    def range_of(self, params) -> tuple:
+        """[start, end) of the flat buffers covering exactly ``params`` (which must be
+        contiguous in the layout: e.g. all parameters of a trailing group of layers)."""
+        ids = {id(p) for p in params}
+        idx = [i for i, p in enumerate(self.params) if id(p) in ids]
+        if not idx:
+            return (0, 0)
+        if idx != list(range(idx[0], idx[-1] + 1)):
+            raise ValueError("parameters are not contiguous in the flat layout")
+        start = self.offsets[idx[0]][0]
+        nxt = idx[-1] + 1
+        end = self.offsets[nxt][0] if nxt < len(self.offsets) else self.numel
+        return (start, end)
+
+    def grad_view(self, params) -> torch.Tensor:
+        s, e = self.range_of(params)
+        return self.grad[s:e]
+
     def state_vector(self) -> torch.Tensor:
         return self.master
 
