@@ -46,6 +46,7 @@ class TrainOptions(_Json):
     validate_every: int = 0
     k: int = -1
     goal_accuracy: float = 100.0
+    resume_from: str = ""   # extension: continue a finished/failed job from its checkpoint
 
 
 @dataclass

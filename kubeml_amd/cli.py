@@ -67,7 +67,8 @@ def cmd_train(a):
     req = TrainRequest(model_type="example", batch_size=a.batch, epochs=a.epochs, dataset=a.dataset, lr=a.lr,
                        function_name=a.function,
                        options=TrainOptions(default_parallelism=a.parallelism, static_parallelism=a.static,
-                                            validate_every=a.validate_every, k=K, goal_accuracy=a.goal_accuracy))
+                                            validate_every=a.validate_every, k=K, goal_accuracy=a.goal_accuracy,
+                                            resume_from=a.resume or ""))
     # validateTrainRequest (train.go:150-172)
     if not (0 < req.batch_size <= MAX_BATCH):
         raise KubeMLException(f"batch size must be between 1 and {MAX_BATCH}", 400)
@@ -246,6 +247,7 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--sparse-avg", action="store_true")
     t.add_argument("--goal-accuracy", type=float, default=100.0)
     t.add_argument("--wait", action="store_true", help="block until the job ends, print its history")
+    t.add_argument("--resume", default=None, help="continue from the checkpoint/history of this job id")
     t.set_defaults(fn=cmd_train)
 
     d = sub.add_parser("dataset", help="manage datasets").add_subparsers(dest="sub", required=True)

@@ -122,6 +122,9 @@ class TrainJob:
         self.thread: Optional[threading.Thread] = None
         self.images_per_second = 0.0
         self.done = threading.Event()
+        self.resume_from = getattr(opts, "resume_from", "") or ""
+        self._pending_restore = None
+        self.start_epoch = 1
 
     # ------------------------------------------------------------------ control
     def start(self) -> "TrainJob":
@@ -135,6 +138,20 @@ class TrainJob:
 
     def stop(self):
         self._stop.set()
+
+    def router(self):
+        """The job's own REST surface (reference ml/pkg/train/api.go:141-149).  ``/next``
+        is gone: the K-AVG barrier is the RCCL all-reduce between the workers."""
+        from .http import Router
+        r = Router(f"job-{self.id}")
+        r.add("POST", "/start", lambda q: (self.start() and "") if self.thread is None else "")
+        r.add("POST", "/update", lambda q: self.update(JobState.from_dict(q.json())) or "")
+        r.add("DELETE", "/stop", lambda q: self.stop() or "")
+        r.add("GET", "/health", lambda q: "")
+        r.add("GET", "/status", lambda q: {"id": self.id, "epoch": self.epoch, "parallelism": self.parallelism,
+                                           "history": self.history.to_dict(), "done": self.done.is_set(),
+                                           "error": self.exit_err})
+        return r
 
     def _clamp(self, p) -> int:
         return max(1, min(int(p), self.max_parallelism))
@@ -170,8 +187,33 @@ class TrainJob:
         if len(layers) == 0:
             raise JobError("length of the layers is zero", 500)
         self.log.info("model initialised", layers=len(layers))
-        self._checkpoint()
+        if self.resume_from:
+            self._resume()
+        else:
+            self._checkpoint()
         return layers
+
+    def _resume(self):
+        """Continue job ``resume_from``: its checkpoint becomes this job's starting model
+        (rank 0 loads it, the epoch-start broadcast spreads it), its history and epoch
+        index carry over."""
+        import shutil
+        src = ckpt_path(self.store_dir, self.resume_from)
+        if not os.path.exists(src):
+            raise JobError(f"no checkpoint for job {self.resume_from}", 404)
+        shutil.copyfile(src, self.ckpt)
+        if os.path.exists(src + ".json"):
+            shutil.copyfile(src + ".json", self.ckpt + ".json")
+            with open(src + ".json") as f:
+                meta = json.load(f)
+            self.start_epoch = int(meta.get("epoch", 0)) + 1
+            if meta.get("history"):
+                self.history = JobHistory.from_dict(meta["history"])
+        if self.history_store is not None and self.history_store.exists(self.resume_from):
+            self.history = self.history_store.get(self.resume_from).data
+        self.have_ckpt = True
+        self._pending_restore = self.ckpt
+        self.log.info("resuming", source=self.resume_from, start_epoch=self.start_epoch)
 
     def _checkpoint(self):
         rep = self.pool.call(0, {"op": "checkpoint", "job": self.id, "path": self.ckpt, "epoch": self.epoch,
@@ -187,12 +229,13 @@ class TrainJob:
         for attempt in range(self.MAX_RECOVERIES + 1):
             self._ensure_pool()
             P = self.parallelism
-            restore = self.ckpt if (attempt > 0 and self.have_ckpt) else None
+            restore = self.ckpt if (attempt > 0 and self.have_ckpt) else self._pending_restore
             t0 = time.time()
             res = self._fanout("train", list(range(P)), N=P, restore=restore)
             ok = {r: v for r, v in res.items() if v.get("ok")}
             bad = {r: v for r, v in res.items() if not v.get("ok")}
             if not bad:
+                self._pending_restore = None
                 losses = [float(v["result"]["loss"]) for v in ok.values()]
                 hbm = max((v.get("hbm_bytes", 0) for v in ok.values()), default=0)
                 self._epoch_stats(time.time() - t0, hbm)
@@ -286,9 +329,10 @@ class TrainJob:
         self.log.info("starting train job", request=self.req.to_dict())
         try:
             self._init()
-            start = time.time()
+            prior = self.history.epoch_duration[-1] if (self.resume_from and self.history.epoch_duration) else 0.0
+            start = time.time() - prior  # epoch_duration stays cumulative across a resume
             E = int(self.req.epochs)
-            for self.epoch in range(1, E + 1):
+            for self.epoch in range(self.start_epoch, E + 1):
                 t0 = time.time()
                 with trace.span("epoch", epoch=self.epoch, P=self.parallelism):
                     loss = self._train_epoch()
@@ -317,7 +361,7 @@ class TrainJob:
                     break
                 if self.accuracy_reached:
                     break
-            if not self.accuracy_reached:
+            if not self.accuracy_reached and self.epoch >= self.start_epoch:
                 try:
                     self._validate()
                 except Exception as e:

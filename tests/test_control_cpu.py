@@ -161,3 +161,23 @@ def test_worker_loss_recovery(tmp_path):
         assert "recovering" in log
     finally:
         srv.stop()
+
+
+def test_resume_from_checkpoint(env):
+    """A job resumed from another continues its epoch count, history and weights."""
+    srv, c, _ = env
+    base = TrainRequest(batch_size=64, epochs=1, dataset="mnist", lr=0.05, function_name="lenet",
+                        options=TrainOptions(default_parallelism=1, static_parallelism=True, k=-1))
+    j1 = c.networks.train(base)
+    assert _wait(c, j1)["state"] == "finished"
+    h1 = c.histories.get(j1).data
+    res = TrainRequest(batch_size=64, epochs=3, dataset="mnist", lr=0.05, function_name="lenet",
+                       options=TrainOptions(default_parallelism=1, static_parallelism=True, k=-1, resume_from=j1))
+    j2 = c.networks.train(res)
+    st = _wait(c, j2)
+    assert st["state"] == "finished", st
+    h2 = c.histories.get(j2).data
+    assert len(h2.train_loss) == 3 and h2.train_loss[0] == h1.train_loss[0]   # carried over + 2 new epochs
+    assert h2.train_loss[1] < h1.train_loss[0]                                 # continued, not restarted
+    assert h2.epoch_duration == sorted(h2.epoch_duration)
+    assert "resuming" in c.logs(j2).decode()
