@@ -14,8 +14,20 @@ from typing import Any, Dict, List, Optional
 class _Json:
     """to_dict / from_dict with nested dataclasses and tolerant of unknown keys."""
 
+    _OMIT_EMPTY: tuple = ()  # extension fields left out of the wire form when unset
+
     def to_dict(self) -> Dict[str, Any]:
-        return asdict(self)
+        out = {}
+        for f in fields(self):
+            v = getattr(self, f.name)
+            if f.name in self._OMIT_EMPTY and not v:
+                continue
+            if isinstance(v, _Json):
+                v = v.to_dict()
+            elif isinstance(v, list):
+                v = [x.to_dict() if isinstance(x, _Json) else x for x in v]
+            out[f.name] = v
+        return out
 
     def to_json(self) -> str:
         return json.dumps(self.to_dict())
@@ -47,6 +59,7 @@ class TrainOptions(_Json):
     k: int = -1
     goal_accuracy: float = 100.0
     resume_from: str = ""   # extension: continue a finished/failed job from its checkpoint
+    _OMIT_EMPTY = ("resume_from",)
 
 
 @dataclass
