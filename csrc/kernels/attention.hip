@@ -1,0 +1,402 @@
+// attention.hip — fused multi-head attention (flash-attention style) for gfx950.
+//
+// BERT-base MLM (north-star config 5; the reference has no attention model, SURVEY
+// §2.8/§5.7): head_dim 64, non-causal, optional additive key bias (padding mask),
+// sequence length L <= any (tiles of 64, tails masked).  Scores never touch HBM:
+//
+//   fwd   : per (64 queries, b, h) block; loop over 64-key tiles: S^T = K Q^T (MFMA),
+//           online softmax in registers (exp2 domain), O^T += V^T P^T (MFMA);
+//           writes O and the per-row log-sum-exp (base 2) for backward.
+//   bwd   : dq-kernel per query tile (also computes D = rowsum(dO * O)), dkv-kernel per
+//           key tile; both recompute P from the saved LSE — no atomics, deterministic.
+//
+// MFMA v_mfma_f32_16x16x32_bf16, wave64: lane l holds A[l&15][8(l>>4)+j],
+// B[8(l>>4)+j][l&15], C[4(l>>4)+i][l&15].  Each wave owns 16 queries (or keys) so the
+// softmax statistics of a row live in one lane column (l&15) and the 4 lanes sharing it
+// (l>>4 = 0..3) combine with two xor-shuffles.  The probability tile produced in C layout
+// is reused as the next MFMA's operand without data movement by permuting the k index
+// of that MFMA: k-slot 8g+j <-> key 32ks + 4g + j (j<4) / 32ks + 16 + 4g + (j-4); the other
+// operand is read with the matching rows through ds_read_b64_tr_b16 (transpose read).
+//
+// LDS tiles are 64 rows x 128 B with a 16-byte-chunk XOR swizzle (chunk ^ (row & 7)),
+// conflict-free for both the row-fragment (ds_read_b128) and transpose reads.
+// Layout: token-major activations [B*L, ld] with head h at column offset 64 h, so the
+// fused QKV projection output / dQKV gradient buffers are used in place.
+#include "kml_common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short v4s_t;
+constexpr float LOG2E = 1.4426950408889634f;
+
+struct AttnArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* o; const bf16_t* dout;
+  bf16_t* out; bf16_t* dq; bf16_t* dk; bf16_t* dv;
+  float* lse;          // [B*H][L] base-2 log-sum-exp of scaled scores
+  float* dsum;         // [B*H][L] D = rowsum(dO * O)
+  const float* bias;   // [B][L] additive key bias (natural-log units) or null
+  int ldq, ldk, ldv, ldo, lddo, ldout, lddq, lddk, lddv;
+  int B, H, L;
+  float scale;         // softmax scale (1/sqrt(64))
+};
+
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+struct TileRegs { uint4 v[2]; };
+
+__device__ __forceinline__ void tile_load(TileRegs& R, const bf16_t* base, int ld, int row0, int L, int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (tid >> 3) + 32 * u, c = tid & 7, row = row0 + r;
+    R.v[u] = row < L ? *reinterpret_cast<const uint4*>(base + (long long)row * ld + c * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void tile_store(char* lds, const TileRegs& R, int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (tid >> 3) + 32 * u, c = tid & 7;
+    *reinterpret_cast<uint4*>(lds + swz(r, c)) = R.v[u];
+  }
+}
+
+// rows row0 + (lane & 15), k = 32 ks + 8 (lane >> 4) + j
+__device__ __forceinline__ bf16x8_t frag_rows(const char* lds, int row0, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8_t*>(lds + swz(row0 + (lane & 15), 4 * ks + (lane >> 4)));
+}
+
+// f[j] = T[key(j)][col0 + (lane & 15)], key(j) = 32ks + 4g + j (j<4), 32ks + 16 + 4g + j-4 (j>=4)
+__device__ __forceinline__ bf16x8_t frag_tr(const char* lds, int col0, int ks, int lane) {
+  const int il = lane & 15, g = lane >> 4;
+  const int col = col0 + 4 * (il & 3);
+  const int r0 = 32 * ks + 4 * g + (il >> 2), r1 = r0 + 16;
+  const char* p0 = lds + swz(r0, col >> 3) + (col & 7) * 2;
+  const char* p1 = lds + swz(r1, col >> 3) + (col & 7) * 2;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p0));
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p1));
+  bf16x8_t f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return f;
+}
+
+// bf16 operand from 8 accumulator values of tiles 2ks, 2ks+1 (the permuted k order)
+__device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& t0, const f32x4_t& t1) {
+  bf16x8_t f;
+  f[0] = (short)f2bf(t0[0]); f[1] = (short)f2bf(t0[1]); f[2] = (short)f2bf(t0[2]); f[3] = (short)f2bf(t0[3]);
+  f[4] = (short)f2bf(t1[0]); f[5] = (short)f2bf(t1[1]); f[6] = (short)f2bf(t1[2]); f[7] = (short)f2bf(t1[3]);
+  return f;
+}
+
+__device__ __forceinline__ bf16x8_t load_frag_g(const bf16_t* row_ptr, int ks, int g, bool ok) {
+  if (!ok) { bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0}; return z; }
+  return *reinterpret_cast<const bf16x8_t*>(row_ptr + 32 * ks + 8 * g);
+}
+
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ void store4(bf16_t* p, const f32x4_t& v, float s) {
+  uint2 w;
+  w.x = pack_bf2(v[0] * s, v[1] * s);
+  w.y = pack_bf2(v[2] * s, v[3] * s);
+  *reinterpret_cast<uint2*>(p) = w;
+}
+
+// ------------------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sQ[8192];
+  __shared__ __attribute__((aligned(16))) char sK[8192];
+  __shared__ __attribute__((aligned(16))) char sV[8192];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int L = a.L, q0 = blockIdx.x * 64;
+  const bf16_t* Qb = a.q + (long long)b * L * a.ldq + h * 64;
+  const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
+  const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
+  const float sl2 = a.scale * LOG2E;
+  const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
+
+  TileRegs rq, rk, rv;
+  tile_load(rq, Qb, a.ldq, q0, L, tid);
+  tile_load(rk, Kb, a.ldk, 0, L, tid);
+  tile_load(rv, Vb, a.ldv, 0, L, tid);
+  tile_store(sQ, rq, tid);
+  __syncthreads();
+  const bf16x8_t qf0 = frag_rows(sQ, 16 * w, 0, lane), qf1 = frag_rows(sQ, 16 * w, 1, lane);
+
+  float m2 = -INFINITY, lsum = 0.f;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = (L + 63) / 64;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    tile_store(sK, rk, tid);
+    tile_store(sV, rv, tid);
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      tile_load(rk, Kb, a.ldk, (kb + 1) * 64, L, tid);
+      tile_load(rv, Vb, a.ldv, (kb + 1) * 64, L, tid);
+    }
+    f32x4_t s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      s[t] = MFMA16(frag_rows(sK, 16 * t, 0, lane), qf0, s[t]);
+      s[t] = MFMA16(frag_rows(sK, 16 * t, 1, lane), qf1, s[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kb * 64 + 16 * t + 4 * g + i;
+        float v = s[t][i] * sl2;
+        if (bias && key < L) v += bias[key] * LOG2E;
+        if (key >= L) v = -INFINITY;
+        s[t][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m2, mx);
+    const bool dead = mn == -INFINITY;
+    const float alpha = dead ? 1.f : exp2f(m2 - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = dead ? 0.f : exp2f(s[t][i] - mn);
+        s[t][i] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    lsum = lsum * alpha + ps;
+    m2 = mn;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] *= alpha;
+    const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      acc[d] = MFMA16(frag_tr(sV, 16 * d, 0, lane), p0, acc[d]);
+      acc[d] = MFMA16(frag_tr(sV, 16 * d, 1, lane), p1, acc[d]);
+    }
+  }
+  const int q = q0 + 16 * w + (lane & 15);
+  if (q < L) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16_t* op = a.out + (long long)(b * L + q) * a.ldout + h * 64;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) store4(op + 16 * d + 4 * g, acc[d], inv);
+    if (g == 0) a.lse[(long long)bh * L + q] = lsum > 0.f ? m2 + log2f(lsum) : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward: dQ (+D)
+__global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sK[8192];
+  __shared__ __attribute__((aligned(16))) char sV[8192];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int L = a.L;
+  const int q = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const bool qok = q < L;
+  const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
+  const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
+  const float sl2 = a.scale * LOG2E;
+  const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
+
+  const bf16_t* qrow = a.q + (long long)(b * L + (qok ? q : 0)) * a.ldq + h * 64;
+  const bf16_t* dorow = a.dout + (long long)(b * L + (qok ? q : 0)) * a.lddo + h * 64;
+  const bf16_t* orow = a.o + (long long)(b * L + (qok ? q : 0)) * a.ldo + h * 64;
+  const bf16x8_t qf0 = load_frag_g(qrow, 0, g, qok), qf1 = load_frag_g(qrow, 1, g, qok);
+  const bf16x8_t df0 = load_frag_g(dorow, 0, g, qok), df1 = load_frag_g(dorow, 1, g, qok);
+  // D = rowsum(dO * O): lane covers d = 16g .. 16g+15
+  float D = 0.f;
+  if (qok) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint4 x = *reinterpret_cast<const uint4*>(dorow + 16 * g + 8 * u);
+      const uint4 y = *reinterpret_cast<const uint4*>(orow + 16 * g + 8 * u);
+      D += lo_bf(x.x) * lo_bf(y.x) + hi_bf(x.x) * hi_bf(y.x) + lo_bf(x.y) * lo_bf(y.y) + hi_bf(x.y) * hi_bf(y.y) +
+           lo_bf(x.z) * lo_bf(y.z) + hi_bf(x.z) * hi_bf(y.z) + lo_bf(x.w) * lo_bf(y.w) + hi_bf(x.w) * hi_bf(y.w);
+    }
+  }
+  D += __shfl_xor(D, 16, 64);
+  D += __shfl_xor(D, 32, 64);
+  if (qok && g == 0) a.dsum[(long long)bh * L + q] = D;
+  const float lse = qok ? a.lse[(long long)bh * L + q] : INFINITY;
+
+  f32x4_t acc[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  TileRegs rk, rv;
+  tile_load(rk, Kb, a.ldk, 0, L, tid);
+  tile_load(rv, Vb, a.ldv, 0, L, tid);
+  const int nkb = (L + 63) / 64;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    tile_store(sK, rk, tid);
+    tile_store(sV, rv, tid);
+    __syncthreads();
+    if (kb + 1 < nkb) {
+      tile_load(rk, Kb, a.ldk, (kb + 1) * 64, L, tid);
+      tile_load(rv, Vb, a.ldv, (kb + 1) * 64, L, tid);
+    }
+    f32x4_t s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      s[t] = MFMA16(frag_rows(sK, 16 * t, 0, lane), qf0, s[t]);
+      s[t] = MFMA16(frag_rows(sK, 16 * t, 1, lane), qf1, s[t]);
+      dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dp[t] = MFMA16(frag_rows(sV, 16 * t, 0, lane), df0, dp[t]);
+      dp[t] = MFMA16(frag_rows(sV, 16 * t, 1, lane), df1, dp[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kb * 64 + 16 * t + 4 * g + i;
+        float v = s[t][i] * sl2;
+        if (bias && key < L) v += bias[key] * LOG2E;
+        const float p = key < L ? exp2f(v - lse) : 0.f;
+        s[t][i] = p * (dp[t][i] - D);
+      }
+    const bf16x8_t d0 = pack_p(s[0], s[1]), d1 = pack_p(s[2], s[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      acc[d] = MFMA16(frag_tr(sK, 16 * d, 0, lane), d0, acc[d]);
+      acc[d] = MFMA16(frag_tr(sK, 16 * d, 1, lane), d1, acc[d]);
+    }
+  }
+  if (qok) {
+    bf16_t* op = a.dq + (long long)(b * L + q) * a.lddq + h * 64;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) store4(op + 16 * d + 4 * g, acc[d], a.scale);
+  }
+}
+
+// ------------------------------------------------------------------------------ backward: dK, dV
+__global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sQ[8192];
+  __shared__ __attribute__((aligned(16))) char sO[8192];  // dO tile
+  __shared__ float sL[64], sD[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int L = a.L;
+  const int key = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const bool kok = key < L;
+  const bf16_t* Qb = a.q + (long long)b * L * a.ldq + h * 64;
+  const bf16_t* Ob = a.dout + (long long)b * L * a.lddo + h * 64;
+  const float sl2 = a.scale * LOG2E;
+  const bf16_t* krow = a.k + (long long)(b * L + (kok ? key : 0)) * a.ldk + h * 64;
+  const bf16_t* vrow = a.v + (long long)(b * L + (kok ? key : 0)) * a.ldv + h * 64;
+  const bf16x8_t kf0 = load_frag_g(krow, 0, g, kok), kf1 = load_frag_g(krow, 1, g, kok);
+  const bf16x8_t vf0 = load_frag_g(vrow, 0, g, kok), vf1 = load_frag_g(vrow, 1, g, kok);
+  const float kb2 = !kok ? -INFINITY : (a.bias ? a.bias[(long long)b * L + key] * LOG2E : 0.f);
+
+  f32x4_t adk[4], adv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) { adk[d] = f32x4_t{0.f, 0.f, 0.f, 0.f}; adv[d] = adk[d]; }
+  TileRegs rq, ro;
+  tile_load(rq, Qb, a.ldq, 0, L, tid);
+  tile_load(ro, Ob, a.lddo, 0, L, tid);
+  float pl = 0.f, pd = 0.f;
+  if (tid < 64) {
+    pl = tid < L ? a.lse[(long long)bh * L + tid] : INFINITY;
+    pd = tid < L ? a.dsum[(long long)bh * L + tid] : 0.f;
+  }
+  const int nqb = (L + 63) / 64;
+  for (int qb = 0; qb < nqb; ++qb) {
+    __syncthreads();
+    tile_store(sQ, rq, tid);
+    tile_store(sO, ro, tid);
+    if (tid < 64) { sL[tid] = pl; sD[tid] = pd; }
+    __syncthreads();
+    if (qb + 1 < nqb) {
+      const int nq0 = (qb + 1) * 64;
+      tile_load(rq, Qb, a.ldq, nq0, L, tid);
+      tile_load(ro, Ob, a.lddo, nq0, L, tid);
+      if (tid < 64) {
+        const int qq = nq0 + tid;
+        pl = qq < L ? a.lse[(long long)bh * L + qq] : INFINITY;
+        pd = qq < L ? a.dsum[(long long)bh * L + qq] : 0.f;
+      }
+    }
+    f32x4_t s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      s[t] = MFMA16(frag_rows(sQ, 16 * t, 0, lane), kf0, s[t]);
+      s[t] = MFMA16(frag_rows(sQ, 16 * t, 1, lane), kf1, s[t]);
+      dp[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      dp[t] = MFMA16(frag_rows(sO, 16 * t, 0, lane), vf0, dp[t]);
+      dp[t] = MFMA16(frag_rows(sO, 16 * t, 1, lane), vf1, dp[t]);
+    }
+    // s[t][i] = S[q = 16t + 4g + i][key]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * t + 4 * g + i;
+        const float p = exp2f(s[t][i] * sl2 + kb2 - sL[r]);
+        s[t][i] = p;
+        dp[t][i] = p * (dp[t][i] - sD[r]);
+      }
+    const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
+    const bf16x8_t d0 = pack_p(dp[0], dp[1]), d1 = pack_p(dp[2], dp[3]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      adv[d] = MFMA16(frag_tr(sO, 16 * d, 0, lane), p0, adv[d]);
+      adv[d] = MFMA16(frag_tr(sO, 16 * d, 1, lane), p1, adv[d]);
+      adk[d] = MFMA16(frag_tr(sQ, 16 * d, 0, lane), d0, adk[d]);
+      adk[d] = MFMA16(frag_tr(sQ, 16 * d, 1, lane), d1, adk[d]);
+    }
+  }
+  if (kok) {
+    bf16_t* kp = a.dk + (long long)(b * L + key) * a.lddk + h * 64;
+    bf16_t* vp = a.dv + (long long)(b * L + key) * a.lddv + h * 64;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      store4(kp + 16 * d + 4 * g, adk[d], a.scale);
+      store4(vp + 16 * d + 4 * g, adv[d], 1.f);
+    }
+  }
+}
+
+bool aligned16(const void* p) { return (((unsigned long long)p) & 15ull) == 0; }
+
+}  // namespace
+
+// q/k/v/out: token-major [B*L, ld*] bf16, head h at column 64h (head_dim must be 64)
+KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* out, float* lse,
+                         const float* bias, int ldq, int ldk, int ldv, int ldout, int B, int H, int L, float scale,
+                         hipStream_t s) {
+  if (L <= 0 || B <= 0 || H <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldout % 4) return (int)hipErrorInvalidValue;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v)) return (int)hipErrorInvalidValue;
+  AttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.out = out; a.lse = lse; a.bias = bias;
+  a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldout = ldout;
+  a.B = B; a.H = H; a.L = L; a.scale = scale;
+  hipLaunchKernelGGL(k_attn_fwd, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
+  KML_LAUNCH_CHECK();
+}
+
+// dq/dk/dv may point into one fused [B*L, 3*H*64] buffer (ld = 3*H*64); dsum: [B*H*L] fp32 scratch
+KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                         const float* lse, float* dsum, const float* bias, bf16_t* dq, bf16_t* dk, bf16_t* dv,
+                         int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv, int B, int H,
+                         int L, float scale, hipStream_t s) {
+  if (L <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
+    return (int)hipErrorInvalidValue;
+  AttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.o = o; a.dout = dout; a.lse = const_cast<float*>(lse); a.dsum = dsum;
+  a.bias = bias; a.dq = dq; a.dk = dk; a.dv = dv;
+  a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
+  a.B = B; a.H = H; a.L = L; a.scale = scale;
+  hipLaunchKernelGGL(k_attn_bwd_dq, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_attn_bwd_dkv, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
+  KML_LAUNCH_CHECK();
+}

@@ -1,0 +1,390 @@
+// transformer.hip — the non-GEMM ops of a BERT-style encoder for gfx950:
+//   LayerNorm fwd (+ fused residual add) / bwd (dgamma, dbeta two-level deterministic),
+//   GELU (erf) fwd/bwd, counter-based dropout fwd/bwd (mask regenerated, never stored),
+//   fused embedding (word + position + token type) gather fwd / scatter-add bwd,
+//   row gather / scatter (masked-LM positions).
+// Rows are bf16 vectors of length N (N % 4 == 0); one wave per row, 8-byte lane loads;
+// statistics in fp32.  Random numbers come from a hash of (seed, step, element) with
+// seed/step in device memory, so hipGraph replays draw fresh masks.
+#include "kml_common.h"
+
+namespace {
+
+__device__ __forceinline__ void ld4(const bf16_t* p, float* f) {
+  const uint2 v = *reinterpret_cast<const uint2*>(p);
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+}
+__device__ __forceinline__ void st4(bf16_t* p, const float* f) {
+  uint2 v;
+  v.x = pack_bf2(f[0], f[1]);
+  v.y = pack_bf2(f[2], f[3]);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+constexpr int MAXV = 8;  // up to 8 x (64 lanes x 4) = 2048 columns held in registers
+
+// ------------------------------------------------------------------------------ LayerNorm fwd
+// y = LN(x [+ res]) * g + b ; sum_out (optional) = x + res (the LN input, kept for backward)
+__global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                bf16_t* __restrict__ y, bf16_t* __restrict__ sum_out,
+                                                float* __restrict__ mean, float* __restrict__ rstd, long long M,
+                                                int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* xr = x + row * N;
+  const int nv = N / 256 + ((N % 256) > 0);
+  float v[MAXV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = (u * 64 + lane) * 4;
+    if (u < nv && c < N) {
+      ld4(xr + c, v[u]);
+      if (res) {
+        float r[4];
+        ld4(res + row * N + c, r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[u][k] += r[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += v[u][k];
+    }
+  }
+  s = wave_sum(s);
+  const float mu = s / N;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = (u * 64 + lane) * 4;
+    if (u < nv && c < N)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { const float d = v[u][k] - mu; q += d * d; }
+  }
+  q = wave_sum(q);
+  const float rs = rsqrtf(q / N + eps);
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = (u * 64 + lane) * 4;
+    if (u < nv && c < N) {
+      if (sum_out) st4(sum_out + row * N + c, v[u]);
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (v[u][k] - mu) * rs * gamma[c + k] + beta[c + k];
+      st4(y + row * N + c, o);
+    }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// ------------------------------------------------------------------------------ LayerNorm bwd
+// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat));  dx (+)= into dx (accumulate flag)
+// dgamma/dbeta: per-block partials [gridDim][2N], last block reduces in block order.
+__global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xin,
+                                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                const float* __restrict__ gamma, bf16_t* __restrict__ dx,
+                                                const bf16_t* __restrict__ dx_add, float* __restrict__ dgamma,
+                                                float* __restrict__ dbeta, float* __restrict__ part,
+                                                unsigned* __restrict__ counter, long long M, int N,
+                                                int rows_per_block) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nv = N / 256 + ((N % 256) > 0);
+  float pg[MAXV][4], pb[MAXV][4];
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { pg[u][k] = 0.f; pb[u][k] = 0.f; }
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  for (long long row = r0 + wv; row < r1; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXV][4], gd[MAXV][4];
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < MAXV; ++u) {
+      const int c = (u * 64 + lane) * 4;
+      if (u < nv && c < N) {
+        float d[4], xv[4];
+        ld4(dy + row * N + c, d);
+        ld4(xin + row * N + c, xv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[u][k] = (xv[k] - mu) * rs;
+          gd[u][k] = d[k] * gamma[c + k];
+          a1 += gd[u][k];
+          a2 += gd[u][k] * xh[u][k];
+          pg[u][k] += d[k] * xh[u][k];
+          pb[u][k] += d[k];
+        }
+      }
+    }
+    a1 = wave_sum(a1) / N;
+    a2 = wave_sum(a2) / N;
+#pragma unroll
+    for (int u = 0; u < MAXV; ++u) {
+      const int c = (u * 64 + lane) * 4;
+      if (u < nv && c < N) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = rs * (gd[u][k] - a1 - xh[u][k] * a2);
+        if (dx_add) {
+          float e[4];
+          ld4(dx_add + row * N + c, e);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] += e[k];
+        }
+        st4(dx + row * N + c, o);
+      }
+    }
+  }
+  // block partials: reduce the 4 waves in LDS, then one row of 2N floats per block
+  __shared__ float red[4][2 * 2048];
+  __shared__ unsigned last;
+#pragma unroll
+  for (int u = 0; u < MAXV; ++u) {
+    const int c = (u * 64 + lane) * 4;
+    if (u < nv && c < N)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { red[wv][c + k] = pg[u][k]; red[wv][N + c + k] = pb[u][k]; }
+  }
+  __syncthreads();
+  float* mine = part + (long long)blockIdx.x * 2 * N;
+  for (int c = threadIdx.x; c < 2 * N; c += 256) mine[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned l = (t == gridDim.x - 1) ? 1u : 0u;
+    if (l) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = l;
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int c = threadIdx.x; c < 2 * N; c += 256) {
+    float acc = 0.f;
+    for (unsigned bk = 0; bk < gridDim.x; ++bk) acc += part[(long long)bk * 2 * N + c];
+    if (c < N) dgamma[c] += acc;
+    else dbeta[c - N] += acc;
+  }
+}
+
+// ------------------------------------------------------------------------------ GELU (erf form)
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+__global__ void k_gelu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n4) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float f[4];
+    ld4(x + i * 4, f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = gelu(f[k]);
+    st4(y + i * 4, f);
+  }
+}
+
+__global__ void k_gelu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, bf16_t* __restrict__ dx,
+                           long long n4) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float d[4], f[4];
+    ld4(dy + i * 4, d);
+    ld4(x + i * 4, f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] *= gelu_grad(f[k]);
+    st4(dx + i * 4, d);
+  }
+}
+
+// ------------------------------------------------------------------------------ dropout
+__device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
+  unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+// y = x * keep / (1 - p); keep = hash(seed, step, salt, i) >= p * 2^32; ctr = [seed, step]
+__global__ void k_dropout(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, const float* __restrict__ ctr,
+                          unsigned salt, float p, long long n4) {
+  const unsigned seed = (unsigned)ctr[0], step = (unsigned)ctr[1];
+  const unsigned thr = (unsigned)(p * 4294967296.0);
+  const float sc = 1.f / (1.f - p);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float f[4];
+    ld4(x + i * 4, f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned hsh = hash3(seed ^ salt, step, (unsigned)(i * 4 + k));
+      f[k] = hsh >= thr ? f[k] * sc : 0.f;
+    }
+    st4(y + i * 4, f);
+  }
+}
+
+// ------------------------------------------------------------------------------ embeddings
+// sum[t] = word[ids[t]] + pos[t % L] + type[tt[t]]   (tables fp32 master? no: bf16 shadows)
+__global__ __launch_bounds__(256) void k_embed_fwd(const long long* __restrict__ ids, const long long* __restrict__ tt,
+                                                   const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
+                                                   const bf16_t* __restrict__ type, bf16_t* __restrict__ out,
+                                                   long long T, int L, int N) {
+  const int lane = threadIdx.x & 63;
+  const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const long long w = ids[t];
+  const int p = (int)(t % L);
+  const long long ty = tt ? tt[t] : 0;
+  for (int c = lane * 4; c < N; c += 256) {
+    float a[4], b[4], e[4];
+    ld4(word + w * N + c, a);
+    ld4(pos + (long long)p * N + c, b);
+    ld4(type + ty * N + c, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += b[k] + e[k];
+    st4(out + t * N + c, a);
+  }
+}
+
+// scatter-add the embedding-sum gradient into the fp32 table gradients
+__global__ __launch_bounds__(256) void k_embed_bwd(const long long* __restrict__ ids, const long long* __restrict__ tt,
+                                                   const bf16_t* __restrict__ dsum, float* __restrict__ dword,
+                                                   float* __restrict__ dpos, float* __restrict__ dtype, long long T,
+                                                   int L, int N) {
+  const int lane = threadIdx.x & 63;
+  const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const long long w = ids[t];
+  const int p = (int)(t % L);
+  const long long ty = tt ? tt[t] : 0;
+  for (int c = lane * 4; c < N; c += 256) {
+    float d[4];
+    ld4(dsum + t * N + c, d);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (dword) atomicAdd(dword + w * N + c + k, d[k]);
+      if (dpos) atomicAdd(dpos + (long long)p * N + c + k, d[k]);
+      if (dtype) atomicAdd(dtype + ty * N + c + k, d[k]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ row gather / scatter
+__global__ void k_gather_rows(const bf16_t* __restrict__ src, const long long* __restrict__ idx,
+                              bf16_t* __restrict__ dst, long long R, int N) {
+  const long long n8 = R * (N / 8);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / (N / 8);
+    const int c = (int)(i - r * (N / 8)) * 8;
+    *reinterpret_cast<uint4*>(dst + r * N + c) = *reinterpret_cast<const uint4*>(src + idx[r] * N + c);
+  }
+}
+
+// dst rows idx[r] (+)= src rows r  (indices unique within a call)
+__global__ void k_scatter_rows(const bf16_t* __restrict__ src, const long long* __restrict__ idx,
+                               bf16_t* __restrict__ dst, long long R, int N, int accumulate) {
+  const long long n4 = R * (N / 4);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / (N / 4);
+    const int c = (int)(i - r * (N / 4)) * 4;
+    float a[4];
+    ld4(src + r * N + c, a);
+    if (accumulate) {
+      float b[4];
+      ld4(dst + idx[r] * N + c, b);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += b[k];
+    }
+    st4(dst + idx[r] * N + c, a);
+  }
+}
+
+int ln_bwd_blocks(long long M, int* rpb) {
+  long long r = 16;
+  long long g = (M + r - 1) / r;
+  if (g > 1024) { r = (M + 1023) / 1024; g = (M + r - 1) / r; }
+  *rpb = (int)r;
+  return (int)g;
+}
+
+}  // namespace
+
+KML_API int kml_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y,
+                       bf16_t* sum_out, float* mean, float* rstd, long long M, int N, float eps, hipStream_t s) {
+  if (N % 4 || N > 64 * 4 * MAXV) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ln_fwd, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, res, gamma, beta, y, sum_out, mean,
+                     rstd, M, N, eps);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API long long kml_ln_bwd_ws_floats(long long M, int N) {
+  int rpb;
+  return (long long)ln_bwd_blocks(M, &rpb) * 2 * N;
+}
+
+KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, const float* rstd, const float* gamma,
+                       bf16_t* dx, const bf16_t* dx_add, float* dgamma, float* dbeta, float* ws, unsigned* counter,
+                       long long M, int N, hipStream_t s) {
+  if (N % 4 || N > 2048) return (int)hipErrorInvalidValue;
+  int rpb;
+  const int g = ln_bwd_blocks(M, &rpb);
+  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, dgamma, dbeta, ws,
+                     counter, M, N, rpb);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_gelu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gelu_fwd, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, x, y, n / 4);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_gelu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long long n, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gelu_bwd, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, dy, x, dx, n / 4);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_dropout(const bf16_t* x, bf16_t* y, const float* ctr, unsigned salt, float p, long long n,
+                        hipStream_t s) {
+  if (n % 4 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dropout, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, x, y, ctr, salt, p, n / 4);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_embed_fwd(const long long* ids, const long long* tt, const bf16_t* word, const bf16_t* pos,
+                          const bf16_t* type, bf16_t* out, long long T, int L, int N, hipStream_t s) {
+  if (N % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_embed_fwd, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, ids, tt, word, pos, type, out, T,
+                     L, N);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_embed_bwd(const long long* ids, const long long* tt, const bf16_t* dsum, float* dword, float* dpos,
+                          float* dtype, long long T, int L, int N, hipStream_t s) {
+  if (N % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_embed_bwd, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, ids, tt, dsum, dword, dpos, dtype,
+                     T, L, N);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_gather_rows(const bf16_t* src, const long long* idx, bf16_t* dst, long long R, int N, hipStream_t s) {
+  if (N % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gather_rows, dim3(kml_stream_grid(R * (N / 8), 256)), dim3(256), 0, s, src, idx, dst, R, N);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_scatter_rows(const bf16_t* src, const long long* idx, bf16_t* dst, long long R, int N, int accumulate,
+                             hipStream_t s) {
+  if (N % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_scatter_rows, dim3(kml_stream_grid(R * (N / 4), 256)), dim3(256), 0, s, src, idx, dst, R, N,
+                     accumulate);
+  KML_LAUNCH_CHECK();
+}

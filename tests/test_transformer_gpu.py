@@ -1,0 +1,124 @@
+"""Numerics of the transformer HIP kernels vs fp32 PyTorch references."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _ref_attn(q, k, v, B, H, L, bias):
+    # q,k,v: [B*L, H*64] fp32
+    def sp(t):
+        return t.view(B, L, H, 64).permute(0, 2, 1, 3)
+    s = sp(q) @ sp(k).transpose(-1, -2) / 8.0
+    if bias is not None:
+        s = s + bias.view(B, 1, 1, L)
+    p = s.softmax(-1)
+    o = p @ sp(v)
+    return o.permute(0, 2, 1, 3).reshape(B * L, H * 64)
+
+
+@pytest.mark.parametrize("B,H,L,use_bias", [(2, 3, 128, False), (2, 2, 100, True), (1, 12, 512, False),
+                                            (3, 1, 64, True), (1, 2, 7, False)])
+def test_attention_fwd_bwd(B, H, L, use_bias):
+    from kubeml_amd.ops import transformer as T
+    torch.manual_seed(0)
+    qkv = (torch.randn(B * L, 3 * H * 64, device=dev) * 0.5).to(torch.bfloat16)
+    q, k, v = qkv[:, :H * 64], qkv[:, H * 64:2 * H * 64], qkv[:, 2 * H * 64:]
+    bias = None
+    if use_bias:
+        keep = torch.rand(B, L, device=dev) > 0.2
+        keep[:, 0] = True
+        bias = torch.where(keep, 0.0, -10000.0).float().contiguous()
+    out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias)
+    qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qf, kf, vf, B, H, L, bias)
+    assert _rel(out, ref) < 1e-2
+    dout = torch.randn(B * L, H * 64, device=dev).to(torch.bfloat16)
+    ref.backward(dout.float())
+    dqkv = torch.empty_like(qkv)
+    dq, dk, dv = dqkv[:, :H * 64], dqkv[:, H * 64:2 * H * 64], dqkv[:, 2 * H * 64:]
+    T.attn_bwd(q, k, v, out, dout, lse, B, H, L, bias=bias, dq=dq, dk=dk, dv=dv)
+    assert _rel(dq, qf.grad) < 3e-2
+    assert _rel(dk, kf.grad) < 3e-2
+    assert _rel(dv, vf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,res", [(300, 768, True), (64, 1024, False), (5, 128, True)])
+def test_layernorm_fwd_bwd(M, N, res):
+    from kubeml_amd.ops import transformer as T
+    torch.manual_seed(1)
+    x = (torch.randn(M, N, device=dev) * 2 + 0.3).to(torch.bfloat16)
+    r = torch.randn(M, N, device=dev).to(torch.bfloat16) if res else None
+    g = torch.rand(N, device=dev) + 0.5
+    b = torch.randn(N, device=dev)
+    y, xin, mean, rstd = T.ln_fwd(x, g, b, res=r, eps=1e-12)
+    xr = (x.float() + (r.float() if res else 0)).requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (N,), gr, br, eps=1e-12)
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    yr.backward(dy.float())
+    dg, db = torch.zeros(N, device=dev), torch.zeros(N, device=dev)
+    dx = T.ln_bwd(dy, xin, mean, rstd, g, dg, db)
+    assert _rel(dx, xr.grad) < 2e-2
+    assert _rel(dg, gr.grad) < 1e-2 and _rel(db, br.grad) < 1e-2
+    dg2, db2 = torch.zeros(N, device=dev), torch.zeros(N, device=dev)
+    T.ln_bwd(dy, xin, mean, rstd, g, dg2, db2)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)   # deterministic
+
+
+def test_gelu_dropout():
+    from kubeml_amd.ops import transformer as T
+    x = torch.randn(4096, 64, device=dev).to(torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    yr = F.gelu(xr)
+    assert _rel(T.gelu_fwd(x), yr) < 1e-2
+    dy = torch.randn_like(x)
+    yr.backward(dy.float())
+    assert _rel(T.gelu_bwd(dy, x), xr.grad) < 1e-2
+    ctr = torch.tensor([7.0, 3.0], device=dev)
+    y1 = T.dropout(x, ctr, 11, 0.1)
+    y2 = T.dropout(x, ctr, 11, 0.1)
+    assert torch.equal(y1, y2)                                  # regenerated mask
+    kept = (y1 != 0) | (x == 0)
+    frac = 1 - kept.float().mean().item()
+    assert 0.08 < frac < 0.12
+    assert _rel(y1[kept], x[kept].float() / 0.9) < 1e-2
+    ctr[1] += 1
+    assert not torch.equal(T.dropout(x, ctr, 11, 0.1), y1)     # new step -> new mask
+
+
+def test_embedding_and_rows():
+    from kubeml_amd.ops import transformer as T
+    torch.manual_seed(2)
+    V, N, L, B = 1000, 256, 16, 3
+    word = torch.randn(V, N, device=dev).to(torch.bfloat16)
+    pos = torch.randn(L, N, device=dev).to(torch.bfloat16)
+    typ = torch.randn(2, N, device=dev).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B * L,), device=dev)
+    tt = torch.randint(0, 2, (B * L,), device=dev)
+    out = T.embed_fwd(ids, tt, word, pos, typ, L)
+    ref = word.float()[ids] + pos.float().repeat(B, 1) + typ.float()[tt]
+    assert _rel(out, ref) < 1e-2
+    d = torch.randn(B * L, N, device=dev).to(torch.bfloat16)
+    dw, dp, dt = torch.zeros(V, N, device=dev), torch.zeros(L, N, device=dev), torch.zeros(2, N, device=dev)
+    T.embed_bwd(ids, tt, d, dw, dp, dt, L)
+    rw = torch.zeros(V, N, device=dev).index_add_(0, ids, d.float())
+    assert _rel(dw, rw) < 1e-5
+    assert _rel(dp, d.float().view(B, L, N).sum(0)) < 1e-5
+    assert _rel(dt, torch.zeros(2, N, device=dev).index_add_(0, tt, d.float())) < 1e-5
+    idx = torch.randperm(B * L, device=dev)[:10]
+    g = T.gather_rows(out, idx)
+    assert torch.equal(g, out[idx])
+    dst = torch.zeros_like(out)
+    T.scatter_rows(g, idx, dst)
+    assert torch.equal(dst[idx], g) and dst.float().abs().sum() == g.float().abs().sum()
