@@ -80,14 +80,12 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, co
 
 // ------------------------------------------------------------------------------ LayerNorm bwd
 // dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat));  dx (+)= into dx (accumulate flag)
-// dgamma/dbeta: per-block partials [gridDim][2N], last block reduces in block order.
+// dgamma/dbeta: per-block partials [gridDim][2N], then k_colreduce sums them in block order.
 __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xin,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 const float* __restrict__ gamma, bf16_t* __restrict__ dx,
-                                                const bf16_t* __restrict__ dx_add, float* __restrict__ dgamma,
-                                                float* __restrict__ dbeta, float* __restrict__ part,
-                                                unsigned* __restrict__ counter, long long M, int N,
-                                                int rows_per_block) {
+                                                const bf16_t* __restrict__ dx_add, float* __restrict__ part,
+                                                long long M, int N, int rows_per_block) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nv = N / 256 + ((N % 256) > 0);
   float pg[MAXV][4], pb[MAXV][4];
@@ -140,7 +138,6 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
   }
   // block partials: reduce the 4 waves in LDS, then one row of 2N floats per block
   __shared__ float red[4][2 * 2048];
-  __shared__ unsigned last;
 #pragma unroll
   for (int u = 0; u < MAXV; ++u) {
     const int c = (u * 64 + lane) * 4;
@@ -151,27 +148,25 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
   __syncthreads();
   float* mine = part + (long long)blockIdx.x * 2 * N;
   for (int c = threadIdx.x; c < 2 * N; c += 256) mine[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned l = (t == gridDim.x - 1) ? 1u : 0u;
-    if (l) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last = l;
+}
+
+// column sums of part[G][W] in row order (deterministic): out_a[c] += sum (c < Na), out_b[c - Na] += sum
+__global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ part, int G, int W, int Na,
+                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + tx;
+  float acc = 0.f;
+  if (col < W) {
+#pragma unroll 8
+    for (int g = ty; g < G; g += 4) acc += part[(long long)g * W + col];
   }
+  __shared__ float red[4][64];
+  red[ty][tx] = acc;
   __syncthreads();
-  if (!last) return;
-  for (int c = threadIdx.x; c < 2 * N; c += 256) {
-    float acc = 0.f;
-    for (unsigned bk = 0; bk < gridDim.x; ++bk) acc += part[(long long)bk * 2 * N + c];
-    if (c < N) dgamma[c] += acc;
-    else dbeta[c - N] += acc;
+  if (ty == 0 && col < W) {
+    const float t = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    if (col < Na) out_a[col] += t;
+    else out_b[col - Na] += t;
   }
 }
 
@@ -253,26 +248,50 @@ __global__ __launch_bounds__(256) void k_embed_fwd(const long long* __restrict__
   }
 }
 
-// scatter-add the embedding-sum gradient into the fp32 table gradients
-__global__ __launch_bounds__(256) void k_embed_bwd(const long long* __restrict__ ids, const long long* __restrict__ tt,
-                                                   const bf16_t* __restrict__ dsum, float* __restrict__ dword,
-                                                   float* __restrict__ dpos, float* __restrict__ dtype, long long T,
-                                                   int L, int N) {
+// word table: scatter-add (ids rarely repeat within a batch -> low contention atomics)
+__global__ __launch_bounds__(256) void k_embed_bwd_word(const long long* __restrict__ ids,
+                                                        const bf16_t* __restrict__ dsum, float* __restrict__ dword,
+                                                        long long T, int N) {
   const int lane = threadIdx.x & 63;
   const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   const long long w = ids[t];
-  const int p = (int)(t % L);
-  const long long ty = tt ? tt[t] : 0;
   for (int c = lane * 4; c < N; c += 256) {
     float d[4];
     ld4(dsum + t * N + c, d);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (dword) atomicAdd(dword + w * N + c + k, d[k]);
-      if (dpos) atomicAdd(dpos + (long long)p * N + c + k, d[k]);
-      if (dtype) atomicAdd(dtype + ty * N + c + k, d[k]);
+    for (int k = 0; k < 4; ++k) atomicAdd(dword + w * N + c + k, d[k]);
+  }
+}
+
+// position table: one block owns position p and sums its B tokens (no atomics)
+__global__ __launch_bounds__(256) void k_embed_bwd_pos(const bf16_t* __restrict__ dsum, float* __restrict__ dpos,
+                                                       long long T, int L, int N) {
+  const int p = blockIdx.x;
+  const long long B = T / L;
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float acc = 0.f;
+    for (long long b = 0; b < B; ++b) acc += bf2f(dsum[(b * L + p) * N + c]);
+    dpos[(long long)p * N + c] += acc;
+  }
+}
+
+// token-type table (few rows): per-block register sums over a token range, one atomic per block/column
+__global__ __launch_bounds__(256) void k_embed_bwd_type(const long long* __restrict__ tt,
+                                                        const bf16_t* __restrict__ dsum, float* __restrict__ dtype,
+                                                        long long T, int N, int ntypes, int tokens_per_block) {
+  const long long t0 = (long long)blockIdx.x * tokens_per_block;
+  const long long t1 = min(T, t0 + tokens_per_block);
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long long t = t0; t < t1; ++t) {
+      const int ty = tt ? (int)tt[t] : 0;
+      const float v = bf2f(dsum[t * N + c]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += (ty == k) ? v : 0.f;
     }
+    for (int k = 0; k < ntypes && k < 4; ++k)
+      if (acc[k] != 0.f) atomicAdd(dtype + (long long)k * N + c, acc[k]);
   }
 }
 
@@ -309,7 +328,7 @@ __global__ void k_scatter_rows(const bf16_t* __restrict__ src, const long long* 
 int ln_bwd_blocks(long long M, int* rpb) {
   long long r = 16;
   long long g = (M + r - 1) / r;
-  if (g > 1024) { r = (M + 1023) / 1024; g = (M + r - 1) / r; }
+  if (g > 512) { r = (M + 511) / 512; g = (M + r - 1) / r; }
   *rpb = (int)r;
   return (int)g;
 }
@@ -335,8 +354,9 @@ KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, c
   if (N % 4 || N > 2048) return (int)hipErrorInvalidValue;
   int rpb;
   const int g = ln_bwd_blocks(M, &rpb);
-  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, dgamma, dbeta, ws,
-                     counter, M, N, rpb);
+  (void)counter;
+  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, rpb);
+  hipLaunchKernelGGL(k_colreduce, dim3((2 * N + 63) / 64), dim3(256), 0, s, ws, g, 2 * N, N, dgamma, dbeta);
   KML_LAUNCH_CHECK();
 }
 
@@ -369,9 +389,15 @@ KML_API int kml_embed_fwd(const long long* ids, const long long* tt, const bf16_
 
 KML_API int kml_embed_bwd(const long long* ids, const long long* tt, const bf16_t* dsum, float* dword, float* dpos,
                           float* dtype, long long T, int L, int N, hipStream_t s) {
-  if (N % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_embed_bwd, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, ids, tt, dsum, dword, dpos, dtype,
-                     T, L, N);
+  if (N % 4 || T % L) return (int)hipErrorInvalidValue;
+  if (dword)
+    hipLaunchKernelGGL(k_embed_bwd_word, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, ids, dsum, dword, T, N);
+  if (dpos) hipLaunchKernelGGL(k_embed_bwd_pos, dim3(L), dim3(256), 0, s, dsum, dpos, T, L, N);
+  if (dtype) {
+    const int tpb = 64;
+    hipLaunchKernelGGL(k_embed_bwd_type, dim3((unsigned)((T + tpb - 1) / tpb)), dim3(256), 0, s, tt, dsum, dtype, T,
+                       N, 2, tpb);
+  }
   KML_LAUNCH_CHECK();
 }
 

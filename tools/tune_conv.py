@@ -51,6 +51,18 @@ def conv_layers(model_name, B, H=32, W=32, in_ch=3):
     return uniq
 
 
+def bert_linears(B, L, P=76, hidden=768, inter=3072, vocab=30522):
+    """(kind, cin, cout, k, s, p, H, W) entries for the BERT GEMMs as 1x1 convs over
+    B*L tokens (and B*P masked positions for the MLM head)."""
+    r8 = lambda c: -(-c // 8) * 8
+    T, M = B * L, B * P
+    out = []
+    for (rows, fin, fout) in ((T, hidden, 3 * hidden), (T, hidden, hidden), (T, hidden, inter), (T, inter, hidden),
+                              (M, hidden, hidden), (M, hidden, r8(vocab))):
+        out.append(("linear", fin, fout, 1, 1, 0, 1, 1, rows))
+    return out
+
+
 def bench(fn, reps=20, warm=2, inner=10):
     """Device time per call: `inner` calls captured in a hipGraph (no host launch cost in
     the measurement — these kernels are shorter than a Python launch), replayed `reps`
@@ -84,17 +96,21 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--out", default=K._TUNE_FILE)
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--bert", default=None, help="B,L: tune the BERT-base GEMM shapes instead of a CNN")
     args = ap.parse_args()
     dev = torch.device("cuda")
-    layers = conv_layers(args.model, args.batch)
+    if args.bert:
+        Bb, Lb = (int(v) for v in args.bert.split(","))
+        layers = bert_linears(Bb, Lb)
+    else:
+        layers = [l + (args.batch,) for l in conv_layers(args.model, args.batch)]
     table = {}
     if os.path.exists(args.out):
         for e in json.load(open(args.out)).get("entries", []):
             table[(e["mode"], e["M"], e["N"], e["Kd"])] = e
     report = []
     t_start = time.time()
-    for (kind, cin, cout, k, s, p, H, W) in layers:
-        B = args.batch
+    for (kind, cin, cout, k, s, p, H, W, B) in layers:
         OH, OW = K.out_hw(H, W, k, k, s, s, p, p)
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
         w = (torch.randn(cout, k, k, cin, device=dev) * 0.05).to(torch.bfloat16)
@@ -156,7 +172,7 @@ def main():
             table[key] = entry
             report.append(entry)
             print(json.dumps(entry), flush=True)
-    out = {"model": args.model, "batch": args.batch, "arch": "gfx950",
+    out = {"model": "resnet34+bert_base" if args.bert else args.model, "batch": args.batch, "arch": "gfx950",
            "entries": sorted(table.values(), key=lambda e: (e["mode"], -e["M"]))}
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
