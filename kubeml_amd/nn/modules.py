@@ -34,6 +34,29 @@ def _on_gpu(x):
     return x.is_cuda
 
 
+class _PadChannelsFn(Function):
+    """Zero-pad the last dim to ``cp`` (kernel), differentiable (backward slices)."""
+
+    @staticmethod
+    def forward(ctx, x, cp):
+        from ..ops import kernels as K
+        ctx.c = x.shape[-1]
+        return K.pad_channels(x.contiguous(), cp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[..., :ctx.c].contiguous(), None
+
+
+def pad_channels(x, cp):
+    return _PadChannelsFn.apply(x, cp) if x.requires_grad else _pad_nograd(x, cp)
+
+
+def _pad_nograd(x, cp):
+    from ..ops import kernels as K
+    return K.pad_channels(x.contiguous(), cp)
+
+
 # ======================================================================================
 # Conv2d
 # ======================================================================================
@@ -78,13 +101,18 @@ class Conv2d(tnn.Module):
         self.stride = _pair(stride)
         self.padding = _pair(padding)
         self.cin_pad = _round8(in_channels)
+        # output channels padded to 8 as well (pad filters/bias stay zero, so the extra
+        # output channels are exact zeros that the next conv's padded input expects)
+        self.cout_pad = _round8(out_channels)
         kh, kw = self.kernel_size
         self.weight = tnn.Parameter(torch.empty(out_channels, in_channels, kh, kw))
         self.bias = tnn.Parameter(torch.empty(out_channels)) if bias else None
-        cin, cp = in_channels, self.cin_pad
-        self.weight._kml_storage_shape = (out_channels, kh, kw, cp)
-        self.weight._kml_view = (lambda st: st[..., :cin].permute(0, 3, 1, 2)) if cp != cin else \
-            (lambda st: st.permute(0, 3, 1, 2))
+        cin, cp, cout = in_channels, self.cin_pad, out_channels
+        self.weight._kml_storage_shape = (self.cout_pad, kh, kw, cp)
+        self.weight._kml_view = lambda st: st[:cout, :, :, :cin].permute(0, 3, 1, 2)
+        if self.bias is not None:
+            self.bias._kml_storage_shape = (self.cout_pad,)
+            self.bias._kml_view = lambda st: st[:cout]
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -103,8 +131,7 @@ class Conv2d(tnn.Module):
             y = F.conv2d(x.permute(0, 3, 1, 2), self.weight, self.bias, self.stride, self.padding)
             return y.permute(0, 2, 3, 1)
         if x.shape[-1] != self.cin_pad:
-            from ..ops import kernels as K
-            x = K.pad_channels(x.contiguous(), self.cin_pad)
+            x = pad_channels(x, self.cin_pad)
         return _ConvFn.apply(x.contiguous(), self.weight, self.bias, self)
 
 
@@ -190,8 +217,7 @@ class Linear(tnn.Module):
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         if x.shape[1] != self.in_pad:
-            from ..ops import kernels as K
-            x = K.pad_channels(x.contiguous(), self.in_pad)
+            x = pad_channels(x, self.in_pad)
         return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, self.fused_relu)
 
 

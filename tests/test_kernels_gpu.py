@@ -238,3 +238,32 @@ def test_augment():
     assert torch.equal(lo, lab[idx])
     out2, _ = K.augment(src, lab, ctr, 16, train=True)
     assert out2.shape == (16, 32, 32, 8)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(32, 1, 1, 88, 16, 1), (32, 1, 1, 120, 88, 1), (8, 6, 6, 8, 8, 3),
+                                           (4, 5, 5, 16, 24, 3)])
+def test_conv_outputs_stay_in_bounds(B, H, W, ci, co, k):
+    """Every mode writes only its own output: a guard band after the output / weight
+    gradient must stay untouched (tiles larger than M or N, split-K, atomics)."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(3)
+    p = k // 2
+    OH, OW = K.out_hw(H, W, k, k, 1, 1, p, p)
+    x = _bf(torch.randn(B, H, W, ci, device=dev))
+    w = _bf(torch.randn(co, k, k, ci, device=dev) * 0.1)
+    dy = _bf(torch.randn(B, OH, OW, co, device=dev))
+    GUARD = 4096
+    for cfg in [None, (32, 32, 32, 1, 0), (64, 64, 64, 1, 0), (32, 32, 64, 4, 0), (64, 32, 64, 2, 1),
+                (128, 128, 64, 1, 2)]:
+        wbuf = torch.zeros(co * k * k * ci + GUARD, device=dev)
+        dw = wbuf[:co * k * k * ci].view(co, k, k, ci)
+        K.conv_wgrad(x, dy, dw, k, k, (1, 1), (p, p), cfg=cfg)
+        assert wbuf[co * k * k * ci:].abs().max().item() == 0.0, ("wgrad", cfg)
+        ybuf = torch.zeros(B * OH * OW * co + GUARD, dtype=torch.bfloat16, device=dev)
+        y = ybuf[:B * OH * OW * co].view(B, OH, OW, co)
+        K.conv_fwd(x, w, k, k, (1, 1), (p, p), out=y, cfg=cfg)
+        assert ybuf[B * OH * OW * co:].float().abs().max().item() == 0.0, ("fwd", cfg)
+        xbuf = torch.zeros(B * H * W * ci + GUARD, dtype=torch.bfloat16, device=dev)
+        dx = xbuf[:B * H * W * ci].view(B, H, W, ci)
+        K.conv_dgrad(dy, w, x.shape, k, k, (1, 1), (p, p), out=dx, cfg=cfg)
+        assert xbuf[B * H * W * ci:].float().abs().max().item() == 0.0, ("dgrad", cfg)

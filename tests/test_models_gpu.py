@@ -150,3 +150,36 @@ def test_vgg16_bn_forward_backward_matches_torch():
         e_o = _rel(p.grad.cpu().double(), p64[name].grad)
         e_a = _rel(pac[name].grad.double(), p64[name].grad)
         assert e_o < 1.3 * e_a + 0.05, (name, e_o, e_a)
+
+
+def test_lenet_on_hip_layers_matches_cpu():
+    """LeNet-5 (odd channel counts 1/6/16, fused-ReLU linears) on the HIP kernels vs the
+    same modules' CPU path in fp64; gradients bounded by stock bf16 autocast drift
+    (max-pool argmax ties flip under bf16 rounding, rerouting some gradient)."""
+    from kubeml_amd.models.lenet import LeNet
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    torch.manual_seed(0)
+    ref = LeNet().double()
+    ac = LeNet()
+    ac.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    gpu = LeNet()
+    gpu.load_state_dict(ac.state_dict())
+    gpu = gpu.to(dev)
+    flatten_module(gpu)
+    x = torch.randn(32, 1, 28, 28).to(torch.bfloat16).float()
+    y = torch.randint(0, 10, (32,))
+    l64 = ref(x.double())
+    F.cross_entropy(l64, y).backward()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        la = ac(x)
+    F.cross_entropy(la.float(), y).backward()
+    lg = gpu(x.to(dev))
+    cross_entropy(lg, y.to(dev)).backward()
+    assert _rel(lg.double().cpu(), l64) < 0.03
+    p64, pac = dict(ref.named_parameters()), dict(ac.named_parameters())
+    for n, p in gpu.named_parameters():
+        e_o = _rel(p.grad.double().cpu(), p64[n].grad)
+        e_a = _rel(pac[n].grad.double(), p64[n].grad)
+        # a single ReLU-mask flip (|pre-activation| ~ 1e-3 rounds to the other sign) moves a
+        # small layer's gradient by a few percent; measured: ours and autocast flip 1 of 2688
+        assert e_o < max(0.1, 1.3 * e_a + 0.05), (n, e_o, e_a)
