@@ -78,6 +78,7 @@ struct ConvArgs {
   const bf16_t* addend;  // [M][N] added to the DGRAD output
   float* slab;           // split-K partial tiles (FWD/DGRAD, splits > 1)
   unsigned* counters;    // split-K tickets, one per output tile
+  const bf16_t* wt;      // transposed weights for the direct dgrad variant
   int B, H, W, C;        // input geometry (C = Cin)
   int OH, OW, K;         // output geometry (K = Cout)
   int KH, KW, sh, sw, ph, pw;
@@ -677,6 +678,151 @@ int launch(const ConvArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------
+// Direct (LDS-free) variant for small-M/N, deep-K layers (ResNet layer2-4 at 32x32
+// input: M = 256..4096 pixels, K = 1152..4608).  Both operands of FWD and DGRAD (with
+// a k-contiguous transposed weight copy) are K-contiguous, so every lane loads its MFMA
+// fragments straight from global memory (16 B = 8 bf16 of one row) — no LDS staging,
+// no barriers in the k-loop.  The W waves of a block split K and keep a D-deep register
+// ring of in-flight fragments; partial tiles are summed through LDS once at the end and
+// wave 0 runs the shared epilogue.  Replaces cross-block split-K (whose agent-scope
+// release/acquire costs microseconds) with an intra-block one.
+// ---------------------------------------------------------------------------------
+template <int BK>
+struct DgradBT {  // transposed weights wT[cin][KH*KW][Kp] (k-contiguous over cout)
+  int base, koff;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int n, int q) {
+    valid = n < a.N;
+    base = (valid ? n : 0) * a.KH * a.KW * a.Kp;
+    koff = (q % (BK / 8)) * 8;
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int tap = fdiv(kb, a.fd_Kp);  // uniform
+    const int kk = kb - tap * a.Kp + koff;
+    int r, s;
+    tap_rs(a, tap, r, s);
+    const bool ok = valid && kb + koff < kend && kk < a.K;
+    return ok ? a.wt + base + (r * a.KW + s) * a.Kp + kk : a.zp;
+  }
+};
+
+template <int MODE, int MR, int NR, int NW, int D>
+__global__ __launch_bounds__(64 * NW) void k_conv_direct(ConvArgs a) {
+  static_assert(MODE != WGRAD, "direct variant: fwd/dgrad only");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int m0 = blockIdx.y * 16 * MR, n0 = blockIdx.x * 16 * NR;
+  using GA = typename std::conditional<MODE == FWD, FwdA<32, true>, DgradA<32>>::type;
+  using GB = typename std::conditional<MODE == FWD, FwdB<32, true>, DgradBT<32>>::type;
+  GA ga[MR];
+  GB gb[NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) ga[i].init(a, m0 + 16 * i + (lane & 15), g);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) gb[j].init(a, n0 + 16 * j + (lane & 15), g);
+
+  // each wave owns k-steps [s0, s1); its loop runs a multiple of D steps without any
+  // branch (steps past s1 read the zero page via kend), so the compiler can keep the
+  // D-deep ring of loads in flight with counted vmcnt waits across iterations
+  const int nst = (a.Kd + 31) / 32;
+  const int per = (nst + NW - 1) / NW;
+  const int s0 = wave * per, s1 = min(nst, s0 + per);
+  const int kend = max(0, min(a.Kd, s1 * 32));
+  const int nloop = (max(s1 - s0, 0) + D - 1) / D;
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t ra[D][MR], rb[D][NR];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int kb = (s0 + d) * 32;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) ra[d][i] = *reinterpret_cast<const bf16x8_t*>(ga[i].ptr(a, kb, kend));
+#pragma unroll
+    for (int j = 0; j < NR; ++j) rb[d][j] = *reinterpret_cast<const bf16x8_t*>(gb[j].ptr(a, kb, kend));
+  }
+  int kb_next = (s0 + D) * 32;
+  for (int it = 0; it < nloop; ++it) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra[d][i], rb[d][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) ra[d][i] = *reinterpret_cast<const bf16x8_t*>(ga[i].ptr(a, kb_next, kend));
+#pragma unroll
+      for (int j = 0; j < NR; ++j) rb[d][j] = *reinterpret_cast<const bf16x8_t*>(gb[j].ptr(a, kb_next, kend));
+      kb_next += 32;
+    }
+  }
+  // intra-block reduction of the NW partial tiles
+  constexpr int NA = MR * NR * 4;
+  __shared__ __attribute__((aligned(16))) float red[(NW > 1 ? NW - 1 : 1) * NA * 64];
+  if (NW > 1) {
+    if (wave > 0) {
+      float4* dst = reinterpret_cast<float4*>(red + (wave - 1) * NA * 64) + lane;
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          dst[(i * NR + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    __syncthreads();
+    if (wave > 0) return;
+    for (int w = 1; w < NW; ++w) {
+      const float4* src = reinterpret_cast<const float4*>(red + (w - 1) * NA * 64) + lane;
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const float4 v = src[(i * NR + j) * 64];
+          acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
+        }
+    }
+  }
+  conv_epilogue<MODE, MR, NR, 16 * MR, 16 * NR>(a, acc, m0, n0, 0, 0, lane, lane, 0, nullptr);
+}
+
+template <int MODE, int MR, int NR, int NW>
+int launch_direct(const ConvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + 16 * NR - 1) / (16 * NR), (a.M + 16 * MR - 1) / (16 * MR), 1);
+  // ring depth: keep ~16 fragment loads per lane in flight
+  constexpr int D = (MR + NR) <= 2 ? 8 : ((MR + NR) <= 4 ? 4 : 2);
+  hipLaunchKernelGGL((k_conv_direct<MODE, MR, NR, NW, D>), grid, dim3(64 * NW), 0, s, a);
+  KML_LAUNCH_CHECK();
+}
+
+template <int MODE>
+int dispatch_direct(const ConvArgs& a, int bm, int bn, int nw, hipStream_t s) {
+#define KML_D(BMv, BNv)                                                                   \
+  if (bm == BMv && bn == BNv) {                                                           \
+    if (nw == 8) return launch_direct<MODE, BMv / 16, BNv / 16, 8>(a, s);               \
+    return launch_direct<MODE, BMv / 16, BNv / 16, 4>(a, s);                            \
+  }
+  KML_D(16, 16) KML_D(16, 32) KML_D(32, 16) KML_D(32, 32) KML_D(32, 64) KML_D(64, 32) KML_D(64, 64)
+#undef KML_D
+  return (int)hipErrorInvalidValue;
+}
+
+// wT[c][t][k] = w[k][t][c] (k < K), 0 for K <= k < Kp   (t = tap index r*KW + s)
+__global__ void k_weight_transpose(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt, int K, int T, int C,
+                                   int Kp) {
+  const long long total = (long long)C * T * Kp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % Kp);
+    const long long ct = i / Kp;
+    const int t = (int)(ct % T), c = (int)(ct / T);
+    wt[i] = k < K ? w[((long long)k * T + t) * C + c] : (bf16_t)0;
+  }
+}
+
 template <int MODE>
 int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
 #define KML_T(BMv, BNv)                                                  \
@@ -775,6 +921,15 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
                          int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu, int bm, int bn,
                          int bk, int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (variant == 3) {  // direct: bk carries the wave count; needs 32-aligned taps
+    if (C % 32) return (int)hipErrorInvalidValue;
+    ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu; a.zp = zero_page();
+    a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
+    a.splits = 1; a.kchunk = a.Kd;
+    if (!a.zp) return (int)hipErrorInvalidSymbol;
+    return dispatch_direct<FWD>(a, bm, bn, bk, s);
+  }
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu; a.zp = zero_page();
@@ -801,6 +956,28 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const 
   if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
   a.slab = slab; a.counters = counters;
   return dispatch<DGRAD>(a, bm, bn, bk, variant, s);
+}
+
+// Direct dgrad: wt = kml_weight_transpose(w) (layout [C][KH*KW][Kp], Kp = roundup(K, 32)).
+KML_API int kml_conv_dgrad_direct(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* addend, int B,
+                                  int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm,
+                                  int bn, int nw, hipStream_t s) {
+  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  a.Kp = (K + 31) / 32 * 32;
+  a.fd_Kp = make_fd(a.Kp);
+  a.dy = dy; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
+  a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
+  a.splits = 1; a.kchunk = a.Kd;
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  return dispatch_direct<DGRAD>(a, bm, bn, nw, s);
+}
+
+KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int KW, int C, hipStream_t s) {
+  const int Kp = (K + 31) / 32 * 32, T = KH * KW;
+  hipLaunchKernelGGL(k_weight_transpose, dim3(kml_stream_grid((long long)C * T * Kp, 256)), dim3(256), 0, s, w, wt,
+                     K, T, C, Kp);
+  KML_LAUNCH_CHECK();
 }
 
 KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,

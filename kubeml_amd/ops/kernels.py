@@ -114,7 +114,8 @@ def default_plan(mode, M, N, Kd, target_blocks=512):
 
 def plan_conv(mode, M, N, Kd):
     """(bm, bn, bk, splits, variant); variant 0 = register-staged pipeline,
-    1/2 = LDS-DMA (global_load_lds) pipeline with 3/4 stages (BK fixed at 64)."""
+    1/2 = LDS-DMA (global_load_lds) pipeline with 3/4 stages (BK fixed at 64),
+    3 = direct LDS-free kernel (fwd/dgrad; bk = waves splitting K, splits = 1)."""
     cfg = _TUNED.get((mode, M, N, Kd))
     cfg = cfg if cfg is not None else default_plan(mode, M, N, Kd)
     cfg = list(tuple(cfg) + (0,) * (5 - len(cfg)))
@@ -134,7 +135,7 @@ _DBG_NOSPLIT_W = os.environ.get("KUBEML_CONV_NOSPLIT_W") == "1"
 
 def _norm_cfg(cfg):
     bm, bn, bk, splits, variant = tuple(cfg) + (0,) * (5 - len(cfg))
-    if variant:
+    if variant in (1, 2):
         bk = 64  # the LDS-DMA pipeline is BK=64 only
     return bm, bn, bk, splits, variant
 
@@ -174,6 +175,9 @@ def _splitk_ws(device, M, N, bm, bn, splits):
     return slab, _COUNTERS.take(device, tiles)
 
 
+DIRECT = 3  # cfg variant id of the LDS-free wave-split-K kernel (fwd / dgrad)
+
+
 def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None):
     """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats += )."""
     _chk(x, BF16, "x", 4)
@@ -198,6 +202,13 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
+    if variant == DIRECT and C % 32:
+        bm, bn, bk, splits, variant = _norm_cfg(default_plan("fwd", M, K, Kd))
+    if variant == DIRECT:  # bk carries the wave count of the direct kernel
+        HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i p p s",
+                 _p(x), _p(w), _p(out), _p(bias), _p(stats), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
+                 int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _s())
+        return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
     HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i p p s",
@@ -230,6 +241,14 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     M = B * H * W
     ntap = (r1 - r0) * (s1 - s0)
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
+    if variant == DIRECT:
+        # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
+        Kp = _cdiv(K, 32) * 32
+        wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=dy.device)
+        HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
+        HIP.call("kml_conv_dgrad_direct", "p p p p i i i i i i i i i i i i i i s",
+                 _p(dy), _p(wt), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, _s())
+        return out
     Kd = ntap * _cdiv(K, bk) * bk
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)

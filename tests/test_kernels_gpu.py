@@ -267,3 +267,33 @@ def test_conv_outputs_stay_in_bounds(B, H, W, ci, co, k):
         dx = xbuf[:B * H * W * ci].view(B, H, W, ci)
         K.conv_dgrad(dy, w, x.shape, k, k, (1, 1), (p, p), out=dx, cfg=cfg)
         assert xbuf[B * H * W * ci:].float().abs().max().item() == 0.0, ("dgrad", cfg)
+
+
+@pytest.mark.parametrize("shape", [(16, 4, 4, 128, 256, 3, 1, 1), (8, 8, 8, 64, 128, 3, 2, 1),
+                                   (32, 1, 1, 512, 512, 3, 1, 1), (8, 4, 4, 96, 40, 3, 1, 1),
+                                   (16, 2, 2, 256, 512, 1, 2, 0)])
+@pytest.mark.parametrize("tile", [(16, 16, 4), (32, 32, 8), (64, 32, 4), (32, 64, 8)])
+def test_conv_direct_variant(shape, tile):
+    """LDS-free wave-split-K kernel (variant 3): fwd (+bias/ReLU/BN stats) and dgrad
+    (+ transposed weights, + fused addend) vs fp32 torch."""
+    from kubeml_amd.ops import kernels as K
+    B, H, W, Ci, Co, k, s, p = shape
+    bm, bn, nw = tile
+    cfg = (bm, bn, nw, 1, 3)
+    torch.manual_seed(4)
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * 0.05)
+    bias = torch.randn(Co, device=dev)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2)
+    pre = F.conv2d(xr, wr, bias, stride=s, padding=p)
+    yr = F.relu(pre)
+    stats = torch.zeros(2 * Co, device=dev)
+    y = K.conv_fwd(x, w, k, k, (s, s), (p, p), bias=bias, stats=stats, relu=True, cfg=cfg)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    assert _rel(stats[:Co], yr.detach().sum((0, 2, 3))) < 2e-2
+    dy = _bf(torch.randn_like(pre))
+    pre.backward(dy.float())
+    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    dx = K.conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), w, x.shape, k, k, (s, s), (p, p), addend=add, cfg=cfg)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2

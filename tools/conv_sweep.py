@@ -36,6 +36,14 @@ def main():
             return K.conv_dgrad(dy, w, x.shape, k, k, (s, s), (p, p), cfg=cfg)
         return K.conv_wgrad(x, dy, dw, k, k, (s, s), (p, p), cfg=cfg)
     res = []
+    if a.mode != "wgrad":
+        for bm, bn in ((16, 16), (16, 32), (32, 16), (32, 32), (32, 64), (64, 32), (64, 64)):
+            for nw in (4, 8):
+                cfg = (bm, bn, nw, 1, 3)
+                try:
+                    res.append((bench(lambda: run(cfg), reps=10), cfg))
+                except Exception:
+                    pass
     for bm, bn in TILES:
         for bk, var in ((32, 0), (64, 0), (64, 1), (64, 2)):
             for sp in (1, 2, 4, 8, 16, 32):
@@ -46,7 +54,8 @@ def main():
                     continue
                 res.append((t, cfg))
     res.sort()
-    for t, cfg in res[:25]:
+    top = int(os.environ.get("SWEEP_TOP", "25"))
+    for t, cfg in res[:top]:
         print(f"{t:8.2f} us  {cfg}")
     print("worst", res[-1])
 

@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--out", default=K._TUNE_FILE)
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--bert", default=None, help="B,L: tune the BERT-base GEMM shapes instead of a CNN")
+    ap.add_argument("--fresh", action="store_true", help="ignore existing entries (re-measure every shape)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     if args.bert:
@@ -105,7 +106,7 @@ def main():
     else:
         layers = [l + (args.batch,) for l in conv_layers(args.model, args.batch)]
     table = {}
-    if os.path.exists(args.out):
+    if os.path.exists(args.out) and not args.fresh:
         for e in json.load(open(args.out)).get("entries", []):
             table[(e["mode"], e["M"], e["N"], e["Kd"])] = e
     report = []
@@ -150,6 +151,13 @@ def main():
                         if esp != sp:
                             continue
                         cands.append((bm, bn, bk, sp, variant))
+            if mode == "dgrad" or (mode == "fwd" and cin % 32 == 0):
+                # LDS-free wave-split-K kernel (variant 3; the bk slot carries the wave count)
+                for bm, bn in ((16, 16), (16, 32), (32, 16), (32, 32), (32, 64), (64, 32), (64, 64)):
+                    if bm > max(16, -(-M // 16) * 16) or bn > max(16, -(-N // 16) * 16):
+                        continue
+                    for nw in (4, 8):
+                        cands.append((bm, bn, nw, 1, 3))
             res = []
             for cfg in cands:
                 try:
