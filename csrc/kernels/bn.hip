@@ -176,6 +176,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_reduce(
 // sums the partials in block order and adds them into dbeta/dgamma.  Gives ~8x more
 // blocks than the atomic version without same-address atomic contention (which crosses
 // XCD L2s), and bitwise-reproducible gradients.
+template <int RMODE>  // 0: partials + last-arriver reduce, 1: atomics, 2: partials only
 __global__ __launch_bounds__(TPB) void k_bn_bwd_reduce2(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dgamma,
@@ -212,6 +213,24 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_reduce2(
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[tid][i] = sd[i]; red[tid][8 + i] = sx[i]; }
   __syncthreads();
+  if (RMODE == 1) {
+    // memory-side fp32 atomics: no agent-scope release (which would write back the
+    // XCD's whole dirty L2 per block) — the fast default
+    if (tid < CH) {
+      float a1[8] = {0}, a2[8] = {0};
+      for (int rr = 0; rr < rows_per_iter; ++rr) {
+        const int t = rr * CH + tid;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a1[i] += red[t][i]; a2[i] += red[t][8 + i]; }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        atomicAdd(dbeta + tid * 8 + i, a1[i]);
+        atomicAdd(dgamma + tid * 8 + i, a2[i]);
+      }
+    }
+    return;
+  }
   float* mine = part + (long long)blockIdx.x * 2 * C;
   if (tid < CH) {
     float a1[8] = {0}, a2[8] = {0};
@@ -226,6 +245,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_reduce2(
     o[CH * 2 + tid * 2] = make_float4(a2[0], a2[1], a2[2], a2[3]);
     o[CH * 2 + tid * 2 + 1] = make_float4(a2[4], a2[5], a2[6], a2[7]);
   }
+  if (RMODE == 2) return;  // the apply kernel sums the partials (kernel boundary = visibility)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -323,6 +343,94 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply(
   }
 }
 
+// bn_bwd_apply with the dgamma/dbeta reduction fused in: every block sums the G
+// per-block partials [G][2C] (dbeta | dgamma) of k_bn_bwd_reduce2<2> in a fixed order
+// (deterministic; no atomics, no fences — the kernel boundary makes them visible);
+// block 0 also adds the sums into the parameter gradients.
+__global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*TPB], ka kb kc mu rs [C]
+  float4* red4 = reinterpret_cast<float4*>(sh);
+  float* ka = sh + 4 * TPB;
+  float* kb = ka + C;
+  float* kc = ka + 2 * C;
+  float* mu = ka + 3 * C;
+  float* rs = ka + 4 * C;
+  const float invM = 1.f / (float)M;
+  // sum the G partial rows of 2C floats: float4 column groups x row slices (several
+  // independent loads in flight per thread), slices combined through LDS
+  const int Q = C / 2;                         // float4 groups per partial row
+  const int QT = Q < TPB ? Q : TPB;            // groups handled per pass
+  const int S = TPB / QT;                      // row slices per pass
+  for (int q0 = 0; q0 < Q; q0 += QT) {
+    const int q = q0 + (int)(threadIdx.x % QT);
+    const int sl = threadIdx.x / QT;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < Q) {
+      const float4* p4 = reinterpret_cast<const float4*>(part) + q;
+#pragma unroll 8
+      for (int g = sl; g < G; g += S) {
+        const float4 v = p4[(long long)g * Q];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    red4[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < QT && q < Q) {
+      float4 t4 = red4[threadIdx.x];
+      for (int k = 1; k < S; ++k) {
+        const float4 v = red4[k * QT + threadIdx.x];
+        t4.x += v.x; t4.y += v.y; t4.z += v.z; t4.w += v.w;
+      }
+      const float vals[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int col = 4 * q + k;               // [dbeta (C) | dgamma (C)]
+        if (col < C) kb[col] = vals[k];
+        else kc[col - C] = vals[k];
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < C; c += TPB) {
+    const float sb = kb[c], sg = kc[c];
+    if (blockIdx.x == 0) { dbeta[c] += sb; dgamma[c] += sg; }
+    const float gm = gamma ? gamma[c] : 1.f;
+    ka[c] = gm * rstd[c];
+    kb[c] = sb * invM;
+    kc[c] = sg * invM;
+    mu[c] = mean[c];
+    rs[c] = rstd[c];
+  }
+  __syncthreads();
+  const long long n8 = M * C / 8;
+  const int CH = C / 8;
+  for (long long i = blockIdx.x * (long long)TPB + threadIdx.x; i < n8; i += (long long)gridDim.x * TPB) {
+    const int c0 = (int)(i % CH) * 8;
+    float d[8], xv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    if (y) {
+      float yv[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+    }
+    if (dres) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float xh = (xv[k] - mu[c]) * rs[c];
+      o[k] = ka[c] * (d[k] - kb[c] - xh * kc[c]);
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
 // relu backward alone: dx = dy * [y > 0]  (bf16, x8)
 __global__ void k_relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                            bf16_t* __restrict__ dx, long long n8) {
@@ -358,6 +466,18 @@ int bwd_blocks(long long M, int C, int* rows_per_block) {
   return (int)g;
 }
 
+int fin_blocks(long long M, int C, int* rows_per_block) {
+  const int rpi = TPB / (C / 8);
+  long long gmax = 32768 / (2 * C);   // <= 128 KB of partials read per apply block
+  if (gmax > 256) gmax = 256;
+  if (gmax < 8) gmax = 8;
+  long long rpb = (long long)rpi * 4;
+  long long g = (M + rpb - 1) / rpb;
+  if (g > gmax) { rpb = ((M + gmax - 1) / gmax + rpi - 1) / rpi * rpi; g = (M + rpb - 1) / rpb; }
+  *rows_per_block = (int)rpb;
+  return (int)g;
+}
+
 unsigned rows_grid(long long M, int C) {
   const int rpi = TPB / (C / 8);
   long long g = (M + rpi * 8 - 1) / (rpi * 8);  // >= 8 rows per thread
@@ -388,23 +508,37 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, const float* gamma
 // number of fp32 workspace floats kml_bn_bwd needs for the deterministic reduce
 KML_API long long kml_bn_bwd_ws_floats(long long M, int C) {
   int rpb;
-  return (long long)bwd_blocks(M, C, &rpb) * 2 * C;
+  const long long a = (long long)bwd_blocks(M, C, &rpb) * 2 * C, b = (long long)fin_blocks(M, C, &rpb) * 2 * C;
+  return a > b ? a : b;
 }
 
-// ws/counter null => single-pass atomic reduce; else two-level deterministic reduce
-// (ws holds kml_bn_bwd_ws_floats(M, C) floats, *counter == 0 on entry and on exit).
+// ws && !counter: partial sums + reduction fused into the apply kernel (default; deterministic)
+// ws && counter : partials + in-kernel last-arriver reduce (agent-scope fences)
+// !ws           : block partials + fp32 atomics
+// (ws holds kml_bn_bwd_ws_floats(M, C) floats; *counter == 0 on entry and on exit).
 KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
                        const float* gamma, float* dgamma, float* dbeta, bf16_t* dx, bf16_t* dres, float* ws,
                        unsigned* counter, long long M, int C, hipStream_t s) {
   if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
-  if (ws && counter) {
-    int rpb;
-    const int g = bwd_blocks(M, C, &rpb);
-    hipLaunchKernelGGL(k_bn_bwd_reduce2, dim3(g), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
+  int rpb;
+  if (ws && !counter) {  // default: partials, then the apply kernel reduces them (2 launches, no sync)
+    const int gf = fin_blocks(M, C, &rpb);
+    hipLaunchKernelGGL(k_bn_bwd_reduce2<2>, dim3(gf), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
+                       nullptr, M, C, rpb);
+    long long ab = (M * C / 8 + TPB - 1) / TPB;
+    if (ab > 256) ab = 256;
+    hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s,
+                       dy, y, x, mean,
+                       rstd, gamma, ws, gf, dgamma, dbeta, dx, dres, M, C);
+    KML_LAUNCH_CHECK();
+  }
+  const int g = bwd_blocks(M, C, &rpb);
+  if (ws && counter) {  // deterministic: ordered partials + last-arriver reduce
+    hipLaunchKernelGGL(k_bn_bwd_reduce2<0>, dim3(g), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
                        counter, M, C, rpb);
-  } else {
-    hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(rows_grid(M, C)), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma,
-                       dbeta, M, C);
+  } else {              // fast: same partials, memory-side atomics
+    hipLaunchKernelGGL(k_bn_bwd_reduce2<1>, dim3(g), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta,
+                       nullptr, nullptr, M, C, rpb);
   }
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 5 * C * sizeof(float), s,
                      dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx, dres, M, C);

@@ -305,8 +305,10 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
     return y
 
 
-# deterministic two-level BN-backward reduce (default); KUBEML_BN_ATOMIC=1 -> atomic path
-_BN_DET = os.environ.get("KUBEML_BN_ATOMIC", "0") != "1"
+# BN-backward dgamma/dbeta reduction: "fused" (default) = per-block partials, summed in
+# a fixed order by the apply kernel (deterministic, no atomics / fences); "ticket" = the
+# in-kernel last-arriver reduce; "atomic" = fp32 atomics.  KUBEML_BN_REDUCE selects.
+_BN_REDUCE = os.environ.get("KUBEML_BN_REDUCE", "fused")
 
 
 def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
@@ -318,10 +320,11 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
     if dx is None:
         dx = torch.empty_like(x)
     ws = cnt = None
-    if _BN_DET:
+    if _BN_REDUCE in ("fused", "ticket"):
         nws = HIP.raw("kml_bn_bwd_ws_floats", M, C)
         ws = torch.empty(nws, dtype=F32, device=x.device)
-        cnt = _COUNTERS.take(x.device, 1)
+        if _BN_REDUCE == "ticket":
+            cnt = _COUNTERS.take(x.device, 1)
     HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i s",
              _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
              _p(dres), _p(ws), _p(cnt), M, C, _s())
