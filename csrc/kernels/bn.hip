@@ -71,21 +71,98 @@ __global__ __launch_bounds__(TPB) void k_bn_stats(const bf16_t* __restrict__ x, 
   }
 }
 
+
+// partial-row variant: block b writes its [sum | sumsq] row into part[b][2C] (plain
+// stores); bn_apply(stats_rows = gridDim) sums the rows — no zeroing, no atomics.
+__global__ __launch_bounds__(TPB) void k_bn_stats_part(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                       long long M, int C, int rows_per_block) {
+  const int CH = C / 8;
+  const int rows_per_iter = TPB / CH;
+  const int tid = threadIdx.x;
+  const int chunk = tid % CH, rsub = tid / CH;
+  float s1[8] = {0}, s2[8] = {0};
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  if (rsub < rows_per_iter) {
+#pragma unroll 2
+    for (long long r = r0 + rsub; r < r1; r += rows_per_iter) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + r * C + chunk * 8), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s1[i] += f[i]; s2[i] += f[i] * f[i]; }
+    }
+  }
+  __shared__ float red[TPB][17];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[tid][i] = s1[i]; red[tid][8 + i] = s2[i]; }
+  __syncthreads();
+  if (tid < CH) {
+    float a1[8] = {0}, a2[8] = {0};
+    for (int rr = 0; rr < rows_per_iter; ++rr) {
+      const int t = rr * CH + tid;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { a1[i] += red[t][i]; a2[i] += red[t][8 + i]; }
+    }
+    float* row = part + (long long)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { row[tid * 8 + i] = a1[i]; row[C + tid * 8 + i] = a2[i]; }
+  }
+}
+
+// Sum G rows of a [G][W4*4] fp32 partial matrix into out[W4*4] (LDS), column groups of
+// float4 x row slices with independent loads in flight; scratch: TPB float4 of LDS.
+__device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, float* out, float4* scratch) {
+  const int Q = W / 4;
+  const int QT = Q < TPB ? Q : TPB;
+  const int S = TPB / QT;
+  for (int q0 = 0; q0 < Q; q0 += QT) {
+    const int q = q0 + (int)(threadIdx.x % QT);
+    const int sl = threadIdx.x / QT;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < Q && sl < S) {
+      const float4* p4 = reinterpret_cast<const float4*>(part) + q;
+#pragma unroll 8
+      for (int g = sl; g < G; g += S) {
+        const float4 v = p4[(long long)g * Q];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    scratch[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < QT && q < Q) {
+      float4 t4 = scratch[threadIdx.x];
+      for (int k = 1; k < S; ++k) {
+        const float4 v = scratch[k * QT + threadIdx.x];
+        t4.x += v.x; t4.y += v.y; t4.z += v.z; t4.w += v.w;
+      }
+      reinterpret_cast<float4*>(out)[q] = t4;
+    }
+    __syncthreads();
+  }
+}
+
 // y = act((x - mean) * rstd * gamma + beta [+ res])
 // mode 0: training (stats = [sum, sumsq] over M rows); mode 1: eval (running stats)
 __global__ __launch_bounds__(TPB) void k_bn_apply(
     const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
-    float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C]
+    float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode,
+    int stats_rows) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], (sums[2C], scratch)
   float* scale = sh;
   float* shift = sh + C;
+  const float* st = stats;
+  if (mode == 0 && stats_rows > 0) {  // per-wave partial rows written by the conv epilogue
+    float* sums = sh + 2 * C;
+    sum_partial_rows(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 4 * C));
+    st = sums;
+  }
   for (int c = threadIdx.x; c < C; c += TPB) {
     float mean, var;
     if (mode == 0) {
-      mean = stats[c] / (float)M;
-      var = fmaxf(stats[C + c] / (float)M - mean * mean, 0.f);
+      mean = st[c] / (float)M;
+      var = fmaxf(st[C + c] / (float)M - mean * mean, 0.f);
     } else {
       mean = run_mean[c];
       var = run_var[c];
@@ -488,20 +565,37 @@ unsigned rows_grid(long long M, int C) {
 
 }  // namespace
 
+// rows of partial statistics kml_bn_stats_part writes (<= 128 KB of partials for bn_apply to sum)
+KML_API int kml_bn_stats_rows(long long M, int C) {
+  int rpb;
+  return fin_blocks(M, C, &rpb);
+}
+
+KML_API int kml_bn_stats_part(const bf16_t* x, float* part, long long M, int C, hipStream_t s) {
+  if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
+  int rpb;
+  const int g = fin_blocks(M, C, &rpb);
+  hipLaunchKernelGGL(k_bn_stats_part, dim3(g), dim3(TPB), 0, s, x, part, M, C, rpb);
+  KML_LAUNCH_CHECK();
+}
+
 KML_API int kml_bn_stats(const bf16_t* x, float* stats, long long M, int C, hipStream_t s) {
   if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_stats, dim3(rows_grid(M, C)), dim3(TPB), 0, s, x, stats, M, C);
   KML_LAUNCH_CHECK();
 }
 
-KML_API int kml_bn_apply(const bf16_t* x, const float* stats, const float* gamma, const float* beta,
+// stats_rows > 0: stats is [stats_rows][2C] partial sums (conv epilogue), summed here
+KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, const float* gamma, const float* beta,
                          const bf16_t* res, bf16_t* y, float* save_mean, float* save_rstd, float* run_mean,
                          float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
                          hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bn_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 2 * C * sizeof(float), s,
-                     x, stats, gamma, beta, res, y, save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum,
-                     relu, mode);
+  const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
+  unsigned grid = kml_stream_grid(M * C / 8, TPB);
+  if (stats_rows > 0 && grid > 256) grid = 256;  // every block re-sums the partials: fewer, fuller blocks
+  hipLaunchKernelGGL(k_bn_apply, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, save_mean, save_rstd,
+                     run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows);
   KML_LAUNCH_CHECK();
 }
 

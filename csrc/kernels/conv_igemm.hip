@@ -79,6 +79,8 @@ struct ConvArgs {
   float* slab;           // split-K partial tiles (FWD/DGRAD, splits > 1)
   unsigned* counters;    // split-K tickets, one per output tile
   const bf16_t* wt;      // transposed weights for the direct dgrad variant
+  int stats_part;        // FWD stats: 0 = atomics into stats[2N]; 1 = plain stores of per-wave
+                         //   partial rows stats[(m0/WM + wm)][2N] (summed by bn_apply)
   int B, H, W, C;        // input geometry (C = Cin)
   int OH, OW, K;         // output geometry (K = Cout)
   int KH, KW, sh, sw, ph, pw;
@@ -371,8 +373,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
         if (fq == 0 && cok) {
-          atomicAdd(a.stats + col, s1);
-          atomicAdd(a.stats + a.N + col, s2);
+          if (a.stats_part) {
+            float* prow = a.stats + (long long)(m0 / WM + wm) * 2 * a.N;
+            prow[col] = s1;
+            prow[a.N + col] = s2;
+          } else {
+            atomicAdd(a.stats + col, s1);
+            atomicAdd(a.stats + a.N + col, s2);
+          }
         }
       }
     }
@@ -917,14 +925,18 @@ KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
   return set_splits(a, bk, splits);
 }
 
-KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int B, int H,
-                         int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu, int bm, int bn,
-                         int bk, int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+// stats_part = 1: stats is [G][2K] with G = ceil(M / WM) (WM = bm for variant 3, bm/2 otherwise);
+// every row is written (no zeroing needed) and bn_apply sums the rows.
+KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int stats_part,
+                         int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu,
+                         int bm, int bn, int bk, int splits, int variant, float* slab, unsigned* counters,
+                         hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   if (variant == 3) {  // direct: bk carries the wave count; needs 32-aligned taps
     if (C % 32) return (int)hipErrorInvalidValue;
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu; a.zp = zero_page();
+    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+    a.zp = zero_page();
     a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
     a.splits = 1; a.kchunk = a.Kd;
     if (!a.zp) return (int)hipErrorInvalidSymbol;
@@ -932,7 +944,8 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   }
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.relu = relu; a.zp = zero_page();
+  a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+  a.zp = zero_page();
   a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   set_splits(a, bk, splits);

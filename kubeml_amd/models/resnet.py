@@ -20,7 +20,7 @@ import torch.nn as tnn
 import torch.nn.functional as F
 
 from ..nn import modules as M
-from ..nn.fused import BlockFn, ConvBNUnit, StatsArena, block_params
+from ..nn.fused import BlockFn, BNRegistry, ConvBNUnit, block_params
 
 
 def _gpu_train(x):
@@ -125,7 +125,7 @@ class ResNet(tnn.Module):
             elif isinstance(m, M.BatchNorm2d):
                 tnn.init.constant_(m.weight, 1)
                 tnn.init.constant_(m.bias, 0)
-        self._arena = StatsArena([m for m in self.modules() if isinstance(m, M.BatchNorm2d)])
+        self._arena = BNRegistry([m for m in self.modules() if isinstance(m, M.BatchNorm2d)])
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -150,7 +150,6 @@ class ResNet(tnn.Module):
             x = M.to_nhwc(x, self.conv1.cin_pad)
         if x.is_cuda:
             if self.training:
-                self._arena.begin(x.device)
                 self._bump_counters()
             x = self._stem_gpu(x)
         else:

@@ -15,8 +15,8 @@ Whole residual blocks are single autograd nodes (``BlockFn``) so PyTorch's autog
 never inserts its own gradient-accumulation kernels between our launches: the
 entire step runs on the HIP kernels and captures cleanly into one hipGraph.
 
-BN statistics buffers come from one per-forward arena that the model zeroes with a
-single ``hipMemsetAsync`` (see :func:`StatsArena`).
+BN statistics travel as per-wave partial rows from the conv epilogue to bn_apply (plain
+stores, summed in a fixed order: no zeroing, no atomics, deterministic).
 """
 from __future__ import annotations
 
@@ -28,36 +28,14 @@ from torch.autograd import Function
 from .flat import grad_storage_of, master_of, shadow_of
 
 
-class StatsArena:
-    """One zeroed fp32 buffer per forward holding [sum, sumsq] for every BN of a model."""
+class BNRegistry:
+    """The BatchNorm layers of a model in forward order (used for the packed
+    ``num_batches_tracked`` counters).  BN statistics need no arena: the conv epilogue
+    writes per-wave partial rows into a fresh buffer that bn_apply sums (every row is
+    written, so nothing is zeroed per step)."""
 
     def __init__(self, bns):
         self.bns = list(bns)
-        off = 0
-        for bn in self.bns:
-            bn._kml_stats_off = off
-            off += 2 * bn.num_features
-        self.numel = max(off, 1)
-
-    def begin(self, device):
-        from ..ops import kernels as K
-        buf = torch.empty(self.numel, dtype=torch.float32, device=device)
-        K.memset_(buf)
-        for bn in self.bns:
-            o = bn._kml_stats_off
-            bn._kml_stats = buf[o:o + 2 * bn.num_features]
-        self.counters = [bn.num_batches_tracked for bn in self.bns]
-        return buf
-
-
-def _stats_for(bn, device):
-    st = getattr(bn, "_kml_stats", None)
-    if st is None or st.device != device:
-        from ..ops import kernels as K
-        st = torch.empty(2 * bn.num_features, dtype=torch.float32, device=device)
-        K.memset_(st)
-    bn._kml_stats = None  # single use
-    return st
 
 
 class ConvBNUnit:
@@ -70,14 +48,18 @@ class ConvBNUnit:
         kh, kw = conv.kernel_size
         gamma, beta = master_of(bn.weight), master_of(bn.bias)
         if training:
-            stats = _stats_for(bn, x.device)
-            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats)
+            # per-wave partial statistics from the conv epilogue (plain stores, every row
+            # written: no zeroing, no atomics); bn_apply sums them in its prologue
+            K_out = w.shape[0]
+            G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding)
+            stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
+            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True)
             C = c.shape[-1]
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             rstd = torch.empty_like(mean)
             y = K.bn_apply(c, stats, gamma, beta, res=res, save_mean=mean, save_rstd=rstd,
                            run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
-                           momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu)
+                           momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
             return y, (x, c, y if relu else None, mean, rstd)
         c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding)
         y = K.bn_apply(c, None, gamma, beta, res=res, run_mean=bn.running_mean, run_var=bn.running_var,

@@ -230,12 +230,11 @@ class _BNFn(Function):
     def forward(ctx, x, weight, bias, mod, relu, res):
         from ..ops import kernels as K
         C = x.shape[-1]
-        stats = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-        K.memset_(stats)
-        K.bn_stats(x.view(-1, C), stats)
+        stats, G = K.bn_stats_part(x.view(-1, C))
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         rstd = torch.empty_like(mean)
         y = K.bn_apply(x, stats, master_of(weight), master_of(bias), res=res, save_mean=mean, save_rstd=rstd,
+                       stats_rows=G,
                        run_mean=mod.running_mean if mod.track_running_stats else None,
                        run_var=mod.running_var if mod.track_running_stats else None,
                        eps=mod.eps, momentum=mod.momentum if mod.momentum is not None else 0.1, relu=relu)

@@ -178,8 +178,19 @@ def _splitk_ws(device, M, N, bm, bn, splits):
 DIRECT = 3  # cfg variant id of the LDS-free wave-split-K kernel (fwd / dgrad)
 
 
-def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None):
-    """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats += )."""
+def conv_stats_rows(M, cfg):
+    """Partial-statistics rows the FWD epilogue writes for a plan (one per wave row band)."""
+    bm, _, _, _, variant = _norm_cfg(cfg)
+    # one row per wave row-band of every M tile (tail tiles included: their waves write zeros)
+    return _cdiv(M, bm) * (1 if variant == DIRECT else 2)
+
+
+def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False):
+    """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats).
+
+    stats: fp32 [2*Cout] accumulated with atomics, or with ``stats_part`` a [G, 2*Cout]
+    buffer of per-wave partial rows (``G = conv_stats_rows(M, plan)``, see
+    :func:`conv_fwd_plan`) that :func:`bn_apply` sums — no zeroing, no atomics."""
     _chk(x, BF16, "x", 4)
     _chk(w, BF16, "w", 4)
     B, H, W, C = x.shape
@@ -196,25 +207,42 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     if bias is not None:
         _chk(bias, F32, "bias")
         assert bias.numel() >= K
-    if stats is not None:
-        _chk(stats, F32, "stats")
-        assert stats.numel() >= 2 * K
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
-    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
-    if variant == DIRECT and C % 32:
-        bm, bn, bk, splits, variant = _norm_cfg(default_plan("fwd", M, K, Kd))
+    bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg)
+    if stats is not None:
+        _chk(stats, F32, "stats")
+        need = 2 * K * (conv_stats_rows(M, (bm, bn, bk, splits, variant)) if stats_part else 1)
+        if stats.numel() < need:
+            raise ValueError(f"stats buffer has {stats.numel()} floats, needs {need}")
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
-        HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i p p s",
-                 _p(x), _p(w), _p(out), _p(bias), _p(stats), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
-                 int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _s())
+        HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i i p p s",
+                 _p(x), _p(w), _p(out), _p(bias), _p(stats), int(stats_part), B, H, W, C, K, KH, KW, sh, sw, ph,
+                 pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _s())
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
-    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i p p s",
-             _p(x), _p(w), _p(out), _p(bias), _p(stats), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
+    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i i p p s",
+             _p(x), _p(w), _p(out), _p(bias), _p(stats), int(stats_part), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
              int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _s())
     return out
+
+
+def conv_fwd_plan(C, M, K, Kd, cfg=None):
+    """The (bm, bn, bk, splits, variant) conv_fwd will run for this shape."""
+    plan = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
+    if plan[4] == DIRECT and C % 32:
+        plan = _norm_cfg(default_plan("fwd", M, K, Kd))
+    return plan
+
+
+def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None):
+    """G of the partial-statistics buffer conv_fwd(stats_part=True) needs for this conv."""
+    B, H, W, C = x_shape
+    OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
+    return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg))
 
 
 def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None):
@@ -282,13 +310,24 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None):
 # --------------------------------------------------------------------------------------
 
 def bn_stats(x2d, stats):
+    """stats[2C] += [sum, sumsq] (atomics)."""
     _chk(x2d, BF16, "x")
     M, C = x2d.numel() // x2d.shape[-1], x2d.shape[-1]
     HIP.call("kml_bn_stats", "p p l i s", _p(x2d), _p(stats), M, C, _s())
 
 
+def bn_stats_part(x2d):
+    """Per-block partial [sum | sumsq] rows -> (buffer [G*2C], G) for bn_apply(stats_rows=G)."""
+    _chk(x2d, BF16, "x")
+    M, C = x2d.numel() // x2d.shape[-1], x2d.shape[-1]
+    G = HIP.raw("kml_bn_stats_rows", M, C)
+    part = torch.empty(G * 2 * C, dtype=F32, device=x2d.device)
+    HIP.call("kml_bn_stats_part", "p p l i s", _p(x2d), _p(part), M, C, _s())
+    return part, G
+
+
 def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=None, run_mean=None,
-             run_var=None, eps=1e-5, momentum=0.1, relu=False, training=True):
+             run_var=None, eps=1e-5, momentum=0.1, relu=False, training=True, stats_rows=0):
     _chk(x, BF16, "x")
     C = x.shape[-1]
     M = x.numel() // C
@@ -298,8 +337,8 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
         _chk(res, BF16, "res")
         if res.shape != x.shape:
             raise ValueError("residual shape mismatch")
-    HIP.call("kml_bn_apply", "p p p p p p p p p p l i f f i i s",
-             _p(x), _p(stats), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
+    HIP.call("kml_bn_apply", "p p i p p p p p p p p l i f f i i s",
+             _p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
              _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu),
              0 if training else 1, _s())
     return y

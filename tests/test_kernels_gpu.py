@@ -307,3 +307,42 @@ def test_conv_direct_variant(shape, tile):
     add = _bf(torch.randn(B, H, W, Ci, device=dev))
     dx = K.conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), w, x.shape, k, k, (s, s), (p, p), addend=add, cfg=cfg)
     assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [(32, 32, 64, 1, 0), (64, 32, 64, 2, 1), (128, 64, 64, 1, 2), (32, 32, 4, 1, 3),
+                                 (64, 64, 32, 4, 0)])
+def test_conv_partial_stats_into_bn_apply(cfg):
+    """FWD epilogue partial statistics (plain stores per wave row-band) summed by bn_apply
+    equal the atomic statistics; M not a multiple of the tile exercises the tail rows."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(5)
+    B, H, W, Ci, Co = 7, 5, 5, 64, 96   # M = 175
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * 0.05)
+    st_a = torch.zeros(2 * Co, device=dev)
+    y = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=st_a, cfg=cfg)
+    G = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, (1, 1), (1, 1), cfg=cfg)
+    guard = 1024
+    buf = torch.full((G * 2 * Co + guard,), float("nan"), device=dev)
+    y2 = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=buf[:G * 2 * Co], stats_part=True, cfg=cfg)
+    assert torch.isnan(buf[G * 2 * Co:]).all()            # nothing written past the G rows
+    assert not torch.isnan(buf[:G * 2 * Co]).any()        # every row written
+    assert torch.equal(y, y2)
+    assert _rel(buf[:G * 2 * Co].view(G, 2 * Co).sum(0), st_a) < 1e-5
+    g, b = torch.rand(Co, device=dev) + 0.5, torch.randn(Co, device=dev)
+    m1, r1 = torch.empty(Co, device=dev), torch.empty(Co, device=dev)
+    m2, r2 = torch.empty(Co, device=dev), torch.empty(Co, device=dev)
+    o1 = K.bn_apply(y, st_a, g, b, save_mean=m1, save_rstd=r1, relu=True)
+    o2 = K.bn_apply(y, buf, g, b, save_mean=m2, save_rstd=r2, relu=True, stats_rows=G)
+    assert _rel(m2, m1) < 1e-5 and _rel(r2, r1) < 1e-5 and _rel(o2, o1) < 1e-2
+
+
+@pytest.mark.parametrize("M,C", [(65536, 64), (1000, 128), (37, 512)])
+def test_bn_stats_partial_rows(M, C):
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(6)
+    x = _bf(torch.randn(M, C, device=dev) * 1.5 + 0.2)
+    part, G = K.bn_stats_part(x)
+    s = part.view(G, 2 * C).sum(0)
+    xf = x.float()
+    assert _rel(s[:C], xf.sum(0)) < 1e-4 and _rel(s[C:], (xf * xf).sum(0)) < 1e-4
