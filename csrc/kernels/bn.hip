@@ -509,6 +509,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
 }
 
 // relu backward alone: dx = dy * [y > 0]  (bf16, x8)
+// (bn_bwd_apply_partial below reuses k_bn_bwd_apply_fin with partials from a conv epilogue)
 __global__ void k_relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                            bf16_t* __restrict__ dx, long long n8) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8;
@@ -636,6 +637,19 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
   }
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(kml_stream_grid(M * C / 8, TPB)), dim3(TPB), 5 * C * sizeof(float), s,
                      dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx, dres, M, C);
+  KML_LAUNCH_CHECK();
+}
+
+// BN backward when the dgamma/dbeta partial rows were produced by the dgrad epilogue that
+// computed dy (conv_dgrad bnf_*): a single apply kernel, no reduction pass over dy/y/x.
+KML_API int kml_bn_bwd_apply_partial(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+                                     const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
+                                     float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
+  if (C % 8 || C / 8 > TPB || G <= 0) return (int)hipErrorInvalidValue;
+  long long ab = (M * C / 8 + TPB - 1) / TPB;
+  if (ab > 256) ab = 256;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s, dy, y,
+                     x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
   KML_LAUNCH_CHECK();
 }
 

@@ -79,6 +79,9 @@ struct ConvArgs {
   float* slab;           // split-K partial tiles (FWD/DGRAD, splits > 1)
   unsigned* counters;    // split-K tickets, one per output tile
   const bf16_t* wt;      // transposed weights for the direct dgrad variant
+  // DGRAD -> consumer-BN backward fusion: partial [sum dz | sum dz*xhat] rows of the BN that
+  // consumes this dX (dz = dX * [y > 0], xhat = (c - mean) * rstd), same row layout as stats_part
+  const bf16_t* bnf_y; const bf16_t* bnf_c; const float* bnf_mean; const float* bnf_rstd; float* bnf_part;
   int stats_part;        // FWD stats: 0 = atomics into stats[2N]; 1 = plain stores of per-wave
                          //   partial rows stats[(m0/WM + wm)][2N] (summed by bn_apply)
   int B, H, W, C;        // input geometry (C = Cin)
@@ -364,11 +367,30 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
             float v = acc[i][j][e] + bv;
             if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
             if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
-            a.out[(long long)row * ldc + col] = f2bf(v);
-            s1 += v;
-            s2 += v * v;
+            const bf16_t vb = f2bf(v);
+            a.out[(long long)row * ldc + col] = vb;
+            if (MODE == DGRAD && a.bnf_part) {  // consumer BN's dbeta / dgamma partials
+              const long long idx = (long long)row * ldc + col;
+              float dz = bf2f(vb);
+              if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) dz = 0.f;
+              const float xh = (bf2f(a.bnf_c[idx]) - a.bnf_mean[col]) * a.bnf_rstd[col];
+              s1 += dz;
+              s2 += dz * xh;
+            } else {
+              s1 += v;
+              s2 += v * v;
+            }
           }
         }
+      if (MODE == DGRAD && a.bnf_part) {
+        s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+        if (fq == 0 && cok) {
+          float* prow = a.bnf_part + (long long)(m0 / WM + wm) * 2 * a.N;
+          prow[col] = s1;
+          prow[a.N + col] = s2;
+        }
+      }
       if (MODE == FWD && a.stats) {
         s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
@@ -954,15 +976,18 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   return dispatch<FWD>(a, bm, bn, bk, variant, s);
 }
 
-KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, int B, int H, int W,
-                           int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
-                           int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+// bnf_*: optional consumer-BN backward partials (see ConvArgs); bnf_part = null disables.
+KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, const bf16_t* bnf_y,
+                           const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd, float* bnf_part, int B,
+                           int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn,
+                           int bk, int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
   if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.Kp = (K + bk - 1) / bk * bk;
   a.fd_Kp = make_fd(a.Kp);
   a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.zp = zero_page();
+  a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   set_splits(a, bk, splits);
@@ -972,14 +997,16 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const 
 }
 
 // Direct dgrad: wt = kml_weight_transpose(w) (layout [C][KH*KW][Kp], Kp = roundup(K, 32)).
-KML_API int kml_conv_dgrad_direct(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* addend, int B,
-                                  int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm,
-                                  int bn, int nw, hipStream_t s) {
+KML_API int kml_conv_dgrad_direct(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
+                                  const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean,
+                                  const float* bnf_rstd, float* bnf_part, int B, int H, int W, int C, int K, int KH,
+                                  int KW, int sh, int sw, int ph, int pw, int bm, int bn, int nw, hipStream_t s) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.Kp = (K + 31) / 32 * 32;
   a.fd_Kp = make_fd(a.Kp);
   a.dy = dy; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
+  a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   a.splits = 1; a.kchunk = a.Kd;
   if (!a.zp) return (int)hipErrorInvalidSymbol;

@@ -126,6 +126,12 @@ class ResNet(tnn.Module):
                 tnn.init.constant_(m.weight, 1)
                 tnn.init.constant_(m.bias, 0)
         self._arena = BNRegistry([m for m in self.modules() if isinstance(m, M.BatchNorm2d)])
+        # backward fusion chain: each block's first dgrad emits the previous block's last-BN
+        # dgamma/dbeta partials (nn/fused.py); weak links, not submodules
+        import weakref
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        for prev, b in zip([None] + blocks[:-1], blocks):
+            object.__setattr__(b, "_kml_prev_ref", weakref.ref(prev) if prev is not None else None)
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -205,7 +211,7 @@ class _StemFn(torch.autograd.Function):
         from ..ops import kernels as K
         net = ctx.net
         dy = K.maxpool_bwd(dp.contiguous(), ctx.idx, ctx.yshape, 3, 2, 1)
-        dx, _ = ConvBNUnit.backward(dy, ctx.s, net.conv1, net.bn1, False, ctx.needs_input_grad[0])
+        dx, _, _ = ConvBNUnit.backward(dy, ctx.s, net.conv1, net.bn1, False, ctx.needs_input_grad[0])
         ctx.s = ctx.idx = None
         return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 

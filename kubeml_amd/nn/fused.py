@@ -25,7 +25,13 @@ from typing import List, Optional
 import torch
 from torch.autograd import Function
 
+import os
+
 from .flat import grad_storage_of, master_of, shadow_of
+
+# KUBEML_BN_FUSE=0: every BN backward runs its own dgamma/dbeta reduction instead of
+# taking partial rows from the dgrad epilogue that produced its input gradient
+_BN_FUSE = os.environ.get("KUBEML_BN_FUSE", "1") != "0"
 
 
 class BNRegistry:
@@ -67,19 +73,25 @@ class ConvBNUnit:
         return y, None
 
     @staticmethod
-    def backward(dy, saved, conv, bn, want_dres: bool, need_dx: bool, addend=None):
+    def backward(dy, saved, conv, bn, want_dres: bool, need_dx: bool, addend=None, partial=None, consumer=None):
+        """BN backward -> conv wgrad -> conv dgrad.  ``partial``: this BN's dgamma/dbeta
+        partial rows, already produced by the dgrad that computed ``dy`` (skips the
+        reduction pass).  ``consumer``: saved state (x, c, y, mean, rstd) of the BN that
+        will consume dx — its partial rows are produced here and returned."""
         from ..ops import kernels as K
         x, c, y, mean, rstd = saved
         dres = torch.empty_like(dy) if want_dres else None
         dc = K.bn_bwd(dy, y, c, mean, rstd, master_of(bn.weight), grad_storage_of(bn.weight),
-                      grad_storage_of(bn.bias), dres=dres)
+                      grad_storage_of(bn.bias), dres=dres, partial=partial)
         kh, kw = conv.kernel_size
         K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding)
-        dx = None
+        dx, part_out = None, None
         if need_dx:
-            dx = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
-                              addend=addend)
-        return dx, dres
+            bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
+            r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
+                             addend=addend, bnf=bnf)
+            dx, part_out = r if bnf is not None else (r, None)
+        return dx, dres, part_out
 
 
 class BlockFn(Function):
@@ -110,6 +122,11 @@ class BlockFn(Function):
                 saved.append(s)
         ctx.block = block
         ctx.saved = saved
+        # the next block's first dgrad produces this block's output gradient; it can emit
+        # the dgamma/dbeta partials of our last BN if it can see that BN's saved state
+        last = [i for i, u in enumerate(block._kml_plan) if u[3] == "last"]
+        object.__setattr__(block, "_kml_last_saved", saved[last[0]] if last else None)
+        object.__setattr__(block, "_kml_in_partial", None)
         return h
 
     @staticmethod
@@ -119,11 +136,19 @@ class BlockFn(Function):
         saved = ctx.saved
         dout = dout.contiguous()
         need_x = ctx.needs_input_grad[0]
+        # partials of our last BN computed by the next block's first dgrad (same tensor only)
+        stash = getattr(block, "_kml_in_partial", None)
+        in_partial = stash[1] if stash is not None and stash[0] == dout.data_ptr() else None
+        object.__setattr__(block, "_kml_in_partial", None)
+        prev_ref = getattr(block, "_kml_prev_ref", None)
+        prev = prev_ref() if prev_ref is not None else None
+        prev_saved = getattr(prev, "_kml_last_saved", None) if prev is not None else None
         # walk main units backwards; the last unit also yields the shortcut gradient dz
         main = [(i, u) for i, u in enumerate(plan) if u[3] != "short"]
         short = [(i, u) for i, u in enumerate(plan) if u[3] == "short"]
         g = dout
         dres = None
+        partial = in_partial
         for k in range(len(main) - 1, -1, -1):
             i, (conv, bn, relu, role) = main[k]
             is_last = role == "last"
@@ -133,17 +158,24 @@ class BlockFn(Function):
                 # shortcut gradient joins here: identity -> dres, projection -> its dgrad
                 if short:
                     j, (sc, sb, sr, _) = short[0]
-                    addend, _ = ConvBNUnit.backward(dres, saved[j], sc, sb, False, need_x)
+                    addend, _, _ = ConvBNUnit.backward(dres, saved[j], sc, sb, False, need_x)
                 else:
                     addend = dres
-            dx, dz = ConvBNUnit.backward(g, saved[i], conv, bn, want_dres=is_last,
-                                         need_dx=(not is_first) or need_x, addend=addend if is_first else None)
+            consumer = saved[main[k - 1][0]] if k > 0 else (prev_saved if need_x else None)
+            if not _BN_FUSE:
+                consumer = None
+            dx, dz, part_out = ConvBNUnit.backward(g, saved[i], conv, bn, want_dres=is_last,
+                                                   need_dx=(not is_first) or need_x,
+                                                   addend=addend if is_first else None, partial=partial,
+                                                   consumer=consumer)
             if is_last:
                 dres = dz
-                if is_first and short:  # single-unit main branch (not used by ResNets)
-                    pass
             g = dx
+            partial = part_out
+        if prev is not None and partial is not None and g is not None:
+            object.__setattr__(prev, "_kml_in_partial", (g.data_ptr(), partial))
         ctx.saved = None
+        object.__setattr__(block, "_kml_last_saved", None)
         return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 

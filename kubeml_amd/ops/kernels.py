@@ -245,8 +245,12 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None):
     return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg))
 
 
-def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None):
-    """dx = conv input gradient (+ addend, the fused residual-gradient sum)."""
+def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None):
+    """dx = conv input gradient (+ addend, the fused residual-gradient sum).
+
+    bnf = (y or None, c, mean, rstd) of the BatchNorm that consumes dx: the epilogue also
+    writes that BN's dgamma/dbeta partial rows; returns (dx, (part, G)) for
+    :func:`bn_bwd(partial=...)`."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     B, H, W, C = in_shape
@@ -269,21 +273,30 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     M = B * H * W
     ntap = (r1 - r0) * (s1 - s0)
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
+    by = bc = bmean = brstd = part = None
+    G = 0
+    if bnf is not None:
+        by, bc, bmean, brstd = bnf
+        if bc.shape != out.shape or (by is not None and by.shape != out.shape):
+            raise ValueError("bnf tensors must match the dgrad output shape")
+        G = conv_stats_rows(M, (bm, bn, bk, splits, variant))
+        part = torch.empty(G * 2 * C, dtype=F32, device=dy.device)
     if variant == DIRECT:
         # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
         Kp = _cdiv(K, 32) * 32
         wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=dy.device)
         HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
-        HIP.call("kml_conv_dgrad_direct", "p p p p i i i i i i i i i i i i i i s",
-                 _p(dy), _p(wt), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, _s())
-        return out
+        HIP.call("kml_conv_dgrad_direct", "p p p p p p p p p i i i i i i i i i i i i i i s",
+                 _p(dy), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part), B, H, W, C,
+                 K, KH, KW, sh, sw, ph, pw, bm, bn, bk, _s())
+        return (out, (part, G)) if bnf is not None else out
     Kd = ntap * _cdiv(K, bk) * bk
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
-    HIP.call("kml_conv_dgrad", "p p p p i i i i i i i i i i i i i i i i p p s",
-             _p(dy), _p(w), _p(out), _p(addend), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits,
-             variant, _p(slab), _p(cnt), _s())
-    return out
+    HIP.call("kml_conv_dgrad", "p p p p p p p p p i i i i i i i i i i i i i i i i p p s",
+             _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part), B, H, W, C, K,
+             KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt), _s())
+    return (out, (part, G)) if bnf is not None else out
 
 
 def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None):
@@ -350,14 +363,21 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
 _BN_REDUCE = os.environ.get("KUBEML_BN_REDUCE", "fused")
 
 
-def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None):
-    """dgamma/dbeta (+=) and dx; y given => ReLU mask applied; dres (optional) receives dz."""
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None):
+    """dgamma/dbeta (+=) and dx; y given => ReLU mask applied; dres (optional) receives dz.
+    partial = (part, G) from conv_dgrad(bnf=...) skips the reduction pass."""
     _chk(dy, BF16, "dy")
     _chk(x, BF16, "x")
     C = x.shape[-1]
     M = x.numel() // C
     if dx is None:
         dx = torch.empty_like(x)
+    if partial is not None:
+        part, G = partial
+        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i s",
+                 _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
+                 _p(dx), _p(dres), M, C, _s())
+        return dx
     ws = cnt = None
     if _BN_REDUCE in ("fused", "ticket"):
         nws = HIP.raw("kml_bn_bwd_ws_floats", M, C)

@@ -346,3 +346,29 @@ def test_bn_stats_partial_rows(M, C):
     s = part.view(G, 2 * C).sum(0)
     xf = x.float()
     assert _rel(s[:C], xf.sum(0)) < 1e-4 and _rel(s[C:], (xf * xf).sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [(32, 32, 64, 1, 0), (64, 32, 64, 2, 1), (32, 32, 4, 1, 3), (64, 64, 32, 4, 0)])
+def test_dgrad_emits_consumer_bn_partials(cfg):
+    """conv_dgrad(bnf=...) writes the dgamma/dbeta partial rows of the BN that consumes dX;
+    bn_bwd(partial=...) then equals the unfused bn_bwd."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(7)
+    B, H, W, Ci, Co = 6, 5, 5, 64, 96
+    dy = _bf(torch.randn(B, H, W, Co, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * 0.05)
+    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    c = _bf(torch.randn(B, H, W, Ci, device=dev))            # the consumer BN's input
+    ybn = _bf(torch.randn(B, H, W, Ci, device=dev))          # its ReLU output (sign pattern)
+    mean, rstd = torch.randn(Ci, device=dev), torch.rand(Ci, device=dev) + 0.5
+    g = torch.rand(Ci, device=dev) + 0.5
+    dx0 = K.conv_dgrad(dy, w, (B, H, W, Ci), 3, 3, (1, 1), (1, 1), addend=add, cfg=cfg)
+    dx1, partial = K.conv_dgrad(dy, w, (B, H, W, Ci), 3, 3, (1, 1), (1, 1), addend=add, cfg=cfg,
+                                bnf=(ybn, c, mean, rstd))
+    assert torch.equal(dx0, dx1)
+    dg0, db0 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    dg1, db1 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    r0 = K.bn_bwd(dx0, ybn, c, mean, rstd, g, dg0, db0)
+    r1 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg1, db1, partial=partial)
+    assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
+    assert _rel(r1, r0) < 1e-2
