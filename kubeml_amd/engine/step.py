@@ -61,6 +61,14 @@ class GraphedTrainStep:
         self.loss = None
         self.captured = False
 
+    @staticmethod
+    def _run(fn):
+        """Run a forward/backward callable with conv wgrads on the side stream (joined
+        before returning, so a captured segment ends with all branches merged)."""
+        from ..nn.fused import wgrad_overlap
+        with wgrad_overlap():
+            return fn()
+
     def _allreduce(self):
         if self.world <= 1:
             return
@@ -79,7 +87,7 @@ class GraphedTrainStep:
             loss = None
             works = []
             for k, seg in enumerate(self.segments):
-                out = seg()
+                out = self._run(seg)
                 if k == 0:
                     loss = out
                 works += self._issue(k)
@@ -87,7 +95,7 @@ class GraphedTrainStep:
                 w.wait()
             self.opt_step()
             return loss
-        loss = self.fwd_bwd()
+        loss = self._run(self.fwd_bwd)
         self._allreduce()
         self.opt_step()
         return loss
@@ -117,7 +125,7 @@ class GraphedTrainStep:
             for k, seg in enumerate(self.segments):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
-                    out = seg()
+                    out = self._run(seg)
                 if k == 0:
                     self.loss = out
                 self.g_seg.append(g)
@@ -127,12 +135,12 @@ class GraphedTrainStep:
         elif self.world <= 1:
             self.g_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_a):
-                self.loss = self.fwd_bwd()
+                self.loss = self._run(self.fwd_bwd)
                 self.opt_step()
         else:
             self.g_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_a):
-                self.loss = self.fwd_bwd()
+                self.loss = self._run(self.fwd_bwd)
             self.g_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_b):
                 self.opt_step()
