@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--segments", choices=["auto", "on", "off"], default="auto",
                     help="stage-split backward with overlapped all-reduce (auto: on when N>1)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the RCCL all-reduce path even with one rank (single-GPU rehearsal of dp>1)")
     args = ap.parse_args()
 
     import torch
@@ -49,8 +51,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    comm = world > 1 or args.force_comm
+    if comm:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     from kubeml_amd.engine.step import GraphedTrainStep
     from kubeml_amd.models.resnet import resnet34
@@ -72,7 +77,7 @@ def main():
     torch.manual_seed(args.seed)  # identical init on every rank
     model = resnet34(num_classes=1000).to(dev)
     space = flatten_module(model)
-    if world > 1:
+    if comm:
         dist.broadcast(space.master, 0)
         space.refresh_shadow()
     model.train()
@@ -90,7 +95,7 @@ def main():
         opt.step()
         K.advance_counter_(ctr, B, n_local)
 
-    use_seg = args.segments == "on" or (args.segments == "auto" and world > 1)
+    use_seg = args.segments == "on" or (args.segments == "auto" and comm)
     segs = seg_grads = None
     if use_seg:
         # backward in 3 graph segments; each segment's gradients are all-reduced on the
@@ -106,14 +111,14 @@ def main():
         seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
     step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
                             bucket_mb=args.bucket_mb, segments=segs, segment_grads=seg_grads,
-                            force_segments=use_seg)
+                            force_segments=use_seg, force_comm=args.force_comm)
     step.capture()
     for _ in range(args.warmup):
         loss = step()
     torch.cuda.synchronize()
     first_loss = float(loss.item())
 
-    if world > 1:
+    if comm:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -122,11 +127,11 @@ def main():
         if args.trace_loss and rank == 0:
             print(f"step {i} loss {float(loss.item()):.4f} gnorm {float(space.grad.norm()):.3e}", flush=True)
     torch.cuda.synchronize()
-    if world > 1:
+    if comm:
         dist.barrier()
     dt = time.perf_counter() - t0
     last_loss = float(loss.item())
-    if world > 1:
+    if comm:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -154,7 +159,7 @@ def main():
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if comm:
         dist.destroy_process_group()
 
 

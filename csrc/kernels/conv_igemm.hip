@@ -97,6 +97,15 @@ struct ConvArgs {
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
+// Block coordinates of one conv tile: kernels pass blockIdx; the grouped backward kernel
+// (k_conv_pair) passes coordinates decoded from its flat block index.
+struct Blk {
+  int x, y, z, gx;
+};
+__device__ __forceinline__ Blk hw_blk() {
+  return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x};
+}
+
 template <int R, bool KCONTIG, int BK>
 struct TileShape {
   static constexpr int ELEMS = KCONTIG ? R * (BK + PADK) : BK * (R + PADR);
@@ -280,7 +289,7 @@ __device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, i
 
 template <int MODE, int MR, int NR, int WM, int WN>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
-                                              int wn, int lane, int tid, int tile, unsigned* flag) {
+                                              int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
 
   // ---------------------------------------------------------------- WGRAD epilogue
@@ -311,7 +320,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     if (a.splits > 1) {
       constexpr int NACC = MR * NR * 4;
       float* slab = a.slab + ((long long)tile * a.splits) * (256 * NACC);
-      float4* mine = reinterpret_cast<float4*>(slab + (long long)blockIdx.z * 256 * NACC) + tid * (NACC / 4);
+      float4* mine = reinterpret_cast<float4*>(slab + (long long)bz * 256 * NACC) + tid * (NACC / 4);
 #pragma unroll
       for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -410,24 +419,31 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 }
 
 template <int MODE, int BM, int BN, int BK, bool TAPU>
-__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
-  constexpr bool A_KC = (MODE != WGRAD);
-  constexpr bool B_KC = (MODE == FWD);
+struct IgemmBody {
+  static constexpr bool A_KC = (MODE != WGRAD);
+  static constexpr bool B_KC = (MODE == FWD);
   using TA = TileShape<BM, A_KC, BK>;
   using TB = TileShape<BN, B_KC, BK>;
+  static constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+  static constexpr int THREADS = 256;
+  static constexpr int SMEM = 2 * STAGE * (int)sizeof(bf16_t);
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem_raw);
+};
+
+template <int MODE, int BM, int BN, int BK, bool TAPU>
+__device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const ConvArgs& a, const Blk& bk,
+                                                                      char* smem_raw) {
   constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
   constexpr int KC = BK / 8;  // 16-byte chunks per K-contiguous row
-  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
   constexpr int PA = TA::PER_THREAD, PB = TB::PER_THREAD;
-
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  bf16_t* smem = reinterpret_cast<bf16_t*>(smem_raw);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile_m = blockIdx.y, tile_n = blockIdx.x;
+  const int tile_m = bk.y, tile_n = bk.x;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int kbeg = bk.z * a.kchunk;
   const int kend = min(a.Kd, kbeg + a.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
@@ -521,8 +537,15 @@ __global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
     }
   }
 
-  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * gridDim.x + tile_n,
+  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * bk.gx + tile_n, bk.z,
                                       reinterpret_cast<unsigned*>(smem));
+}
+
+template <int MODE, int BM, int BN, int BK, bool TAPU>
+__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
+  using Body = IgemmBody<MODE, BM, BN, BK, TAPU>;
+  __shared__ __attribute__((aligned(16))) char smem[Body::SMEM];
+  Body::run(a, hw_blk(), smem);
 }
 
 // =====================================================================================
@@ -581,23 +604,28 @@ __device__ __forceinline__ void glds_slot(int u, int lane, int& row, int& chunk)
 }
 
 template <int MODE, int BM, int BN, int S, bool TAPU>
-__global__ __launch_bounds__(256) void k_conv_glds(ConvArgs a) {
-  constexpr int BK = 64;
+struct GldsBody {
+  static constexpr int BK = 64;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int THREADS = 256;
+  static constexpr int SMEM = S * STAGE;
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem);
+};
+
+template <int MODE, int BM, int BN, int S, bool TAPU>
+__device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvArgs& a, const Blk& bk, char* smem) {
   constexpr bool A_KC = (MODE != WGRAD);
   constexpr bool B_KC = (MODE == FWD);
   constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int NA = BM / 32, NB = BN / 32;  // DMA instructions per wave per stage
   constexpr int NI = NA + NB;
 
-  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
-
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tile_m = blockIdx.y, tile_n = blockIdx.x;
+  const int tile_m = bk.y, tile_n = bk.x;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int kbeg = blockIdx.z * a.kchunk;
+  const int kbeg = bk.z * a.kchunk;
   const int kend = min(a.Kd, kbeg + a.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
@@ -685,8 +713,15 @@ __global__ __launch_bounds__(256) void k_conv_glds(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * gridDim.x + tile_n,
+  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * bk.gx + tile_n, bk.z,
                                       reinterpret_cast<unsigned*>(smem));
+}
+
+template <int MODE, int BM, int BN, int S, bool TAPU>
+__global__ __launch_bounds__(256) void k_conv_glds(ConvArgs a) {
+  using Body = GldsBody<MODE, BM, BN, S, TAPU>;
+  __shared__ __attribute__((aligned(1024))) char smem[Body::SMEM];
+  Body::run(a, hw_blk(), smem);
 }
 
 template <int MODE, int BM, int BN, int S>
@@ -739,10 +774,18 @@ struct DgradBT {  // transposed weights wT[cin][KH*KW][Kp] (k-contiguous over co
 };
 
 template <int MODE, int MR, int NR, int NW, int D>
-__global__ __launch_bounds__(64 * NW) void k_conv_direct(ConvArgs a) {
+struct DirectBody {
   static_assert(MODE != WGRAD, "direct variant: fwd/dgrad only");
+  static constexpr int NA = MR * NR * 4;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int SMEM = (NW > 1 ? NW - 1 : 1) * NA * 64 * (int)sizeof(float);
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem);
+};
+
+template <int MODE, int MR, int NR, int NW, int D>
+__device__ __forceinline__ void DirectBody<MODE, MR, NR, NW, D>::run(const ConvArgs& a, const Blk& bk, char* smem) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int m0 = blockIdx.y * 16 * MR, n0 = blockIdx.x * 16 * NR;
+  const int m0 = bk.y * 16 * MR, n0 = bk.x * 16 * NR;
   using GA = typename std::conditional<MODE == FWD, FwdA<32, true>, DgradA<32>>::type;
   using GB = typename std::conditional<MODE == FWD, FwdB<32, true>, DgradBT<32>>::type;
   GA ga[MR];
@@ -792,8 +835,7 @@ __global__ __launch_bounds__(64 * NW) void k_conv_direct(ConvArgs a) {
     }
   }
   // intra-block reduction of the NW partial tiles
-  constexpr int NA = MR * NR * 4;
-  __shared__ __attribute__((aligned(16))) float red[(NW > 1 ? NW - 1 : 1) * NA * 64];
+  float* red = reinterpret_cast<float*>(smem);
   if (NW > 1) {
     if (wave > 0) {
       float4* dst = reinterpret_cast<float4*>(red + (wave - 1) * NA * 64) + lane;
@@ -816,7 +858,14 @@ __global__ __launch_bounds__(64 * NW) void k_conv_direct(ConvArgs a) {
         }
     }
   }
-  conv_epilogue<MODE, MR, NR, 16 * MR, 16 * NR>(a, acc, m0, n0, 0, 0, lane, lane, 0, nullptr);
+  conv_epilogue<MODE, MR, NR, 16 * MR, 16 * NR>(a, acc, m0, n0, 0, 0, lane, lane, 0, 0, nullptr);
+}
+
+template <int MODE, int MR, int NR, int NW, int D>
+__global__ __launch_bounds__(64 * NW) void k_conv_direct(ConvArgs a) {
+  using Body = DirectBody<MODE, MR, NR, NW, D>;
+  __shared__ __attribute__((aligned(16))) char smem[Body::SMEM];
+  Body::run(a, hw_blk(), smem);
 }
 
 template <int MODE, int MR, int NR, int NW>
@@ -921,6 +970,125 @@ int set_splits(ConvArgs& a, int bk, int splits) {
   return a.splits;
 }
 
+// ---------------------------------------------------------------------------------
+// Grouped backward: the dgrad and the wgrad of one conv layer in ONE launch.
+//
+// Both GEMMs read the same upstream gradient and are independent of each other, so a
+// flat grid runs the dgrad tiles (blocks [0, nd), dispatched first: dgrad is the
+// critical path of backward) next to the wgrad tiles (blocks [nd, nd + nw)).  At
+// ResNet-34/CIFAR sizes each GEMM alone fills 8-72 of the 256 CUs and every dependent
+// launch costs ~4-5 us on the MI355X queue, so pairing halves the conv-backward launch
+// count and lets the two small GEMMs share the chip.
+// ---------------------------------------------------------------------------------
+template <class DB, class WB>
+__global__ __launch_bounds__(256) void k_conv_pair(ConvArgs ad, ConvArgs aw, int dgx, int dgy, int wgx, int wgy,
+                                                   int nd) {
+  static_assert(DB::THREADS == 256 && WB::THREADS == 256, "paired bodies run 256-thread blocks");
+  constexpr int SM = DB::SMEM > WB::SMEM ? DB::SMEM : WB::SMEM;
+  __shared__ __attribute__((aligned(1024))) char smem[SM];
+  int id = (int)blockIdx.x;
+  if (id < nd) {
+    Blk b;
+    b.gx = dgx;
+    b.x = id % dgx;
+    const int t = id / dgx;
+    b.y = t % dgy;
+    b.z = t / dgy;
+    DB::run(ad, b, smem);
+  } else {
+    id -= nd;
+    Blk b;
+    b.gx = wgx;
+    b.x = id % wgx;
+    const int t = id / wgx;
+    b.y = t % wgy;
+    b.z = t / wgy;
+    WB::run(aw, b, smem);
+  }
+}
+
+// Instantiated pairs: X(dgrad variant, dgrad cfg bm, bn, bk, dgrad body, dgrad tile M, N,
+// wgrad body, wgrad tile M, N).  Variant codes as in plan_conv (0 = register-staged,
+// 3 = direct with bk = waves); the wgrad side is always the register-staged BK=64 kernel.
+// Any other combination runs as two launches (kml_conv_pair_supported).
+using DgIg3264 = IgemmBody<DGRAD, 32, 64, 64, true>;
+using DgIg3232 = IgemmBody<DGRAD, 32, 32, 64, true>;
+using DgDi3232 = DirectBody<DGRAD, 2, 2, 4, 4>;
+using DgDi3216 = DirectBody<DGRAD, 2, 1, 4, 4>;
+using DgDi6432 = DirectBody<DGRAD, 4, 2, 4, 2>;
+using WgIg3232 = IgemmBody<WGRAD, 32, 32, 64, true>;
+using WgIg6432 = IgemmBody<WGRAD, 64, 32, 64, true>;
+#define KML_PAIR_LIST(X)                                   \
+  X(0, 32, 64, 64, DgIg3264, 32, 64, WgIg3232, 32, 32)     \
+  X(0, 32, 64, 64, DgIg3264, 32, 64, WgIg6432, 64, 32)     \
+  X(0, 32, 32, 64, DgIg3232, 32, 32, WgIg3232, 32, 32)     \
+  X(0, 32, 32, 64, DgIg3232, 32, 32, WgIg6432, 64, 32)     \
+  X(3, 32, 32, 4, DgDi3232, 32, 32, WgIg3232, 32, 32)      \
+  X(3, 32, 32, 4, DgDi3232, 32, 32, WgIg6432, 64, 32)      \
+  X(3, 32, 16, 4, DgDi3216, 32, 16, WgIg3232, 32, 32)      \
+  X(3, 32, 16, 4, DgDi3216, 32, 16, WgIg6432, 64, 32)      \
+  X(3, 64, 32, 4, DgDi6432, 64, 32, WgIg3232, 32, 32)      \
+  X(3, 64, 32, 4, DgDi6432, 64, 32, WgIg6432, 64, 32)
+
+template <class DB, class WB>
+int launch_pair(const ConvArgs& ad, int dbm, int dbn, const ConvArgs& aw, int wbm, int wbn, hipStream_t s) {
+  const int dgx = (ad.N + dbn - 1) / dbn, dgy = (ad.M + dbm - 1) / dbm;
+  const int wgx = (aw.N + wbn - 1) / wbn, wgy = (aw.M + wbm - 1) / wbm;
+  const long long nd = (long long)dgx * dgy * ad.splits, nw = (long long)wgx * wgy * aw.splits;
+  if (nd + nw > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_conv_pair<DB, WB>), dim3((unsigned)(nd + nw)), dim3(256), 0, s, ad, aw, dgx, dgy, wgx, wgy,
+                     (int)nd);
+  KML_LAUNCH_CHECK();
+}
+
+// 1 + index of the instantiated pair, 0 if none
+int pair_index(int dv, int dbm, int dbn, int dbk, int wv, int wbm, int wbn, int wbk) {
+  int idx = 0;
+#define KML_PAIR_FIND(DV, DBM, DBN, DBK, DB, DTM, DTN, WB, WBM, WBN)                                   \
+  ++idx;                                                                                             \
+  if (dv == DV && dbm == DBM && dbn == DBN && dbk == DBK && wv == 0 && wbm == WBM && wbn == WBN && wbk == 64) \
+    return idx;
+  KML_PAIR_LIST(KML_PAIR_FIND)
+#undef KML_PAIR_FIND
+  return 0;
+}
+
+int dispatch_pair(int which, const ConvArgs& ad, const ConvArgs& aw, hipStream_t s) {
+  int idx = 0;
+#define KML_PAIR_RUN(DV, DBM, DBN, DBK, DB, DTM, DTN, WB, WBM, WBN) \
+  if (++idx == which) return launch_pair<DB, WB>(ad, DTM, DTN, aw, WBM, WBN, s);
+  KML_PAIR_LIST(KML_PAIR_RUN)
+#undef KML_PAIR_RUN
+  return (int)hipErrorInvalidValue;
+}
+
+// wT[c][t][k] = w[k][t][c] for up to 16 weights in one launch (kml_weight_transpose_multi)
+struct TransposeJob {
+  const bf16_t* w;
+  bf16_t* wt;
+  long long begin;  // first element of this job in the launch's flat index space
+  int K, T, C, Kp;
+};
+struct TransposeBatch {
+  TransposeJob j[16];
+  int n;
+  long long total;
+};
+
+__global__ void k_weight_transpose_multi(TransposeBatch tb) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tb.total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int q = 0;
+    while (q + 1 < tb.n && i >= tb.j[q + 1].begin) ++q;
+    const TransposeJob& jb = tb.j[q];
+    const long long e = i - jb.begin;
+    const int k = (int)(e % jb.Kp);
+    const long long ct = e / jb.Kp;
+    const int t = (int)(ct % jb.T), c = (int)(ct / jb.T);
+    jb.wt[e] = k < jb.K ? jb.w[((long long)k * jb.T + t) * jb.C + c] : (bf16_t)0;
+  }
+}
+
 __device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];  // zero-initialised device global
 
 const bf16_t* zero_page() {
@@ -974,6 +1142,91 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
   a.slab = slab; a.counters = counters;
   return dispatch<FWD>(a, bm, bn, bk, variant, s);
+}
+
+namespace {
+int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
+               const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
+               float* bnf_part, int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
+               int bk, int splits, int variant, float* slab, unsigned* counters) {
+  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  const bool direct = (variant == 3);
+  if (!direct && variant) bk = 64;
+  a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  const int kq = direct ? 32 : bk;
+  a.Kp = (K + kq - 1) / kq * kq;
+  a.fd_Kp = make_fd(a.Kp);
+  a.dy = dy; a.w = w; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
+  a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
+  a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  if (direct) {
+    if (!wt) return (int)hipErrorInvalidValue;
+    a.splits = 1; a.kchunk = a.Kd;
+    return 0;
+  }
+  set_splits(a, bk, splits);
+  if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
+  a.slab = slab; a.counters = counters;
+  return 0;
+}
+
+int prep_wgrad(ConvArgs& a, const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
+               int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate) {
+  if (variant) bk = 64;
+  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
+  a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  set_splits(a, bk, splits);
+  a.accumulate = (a.splits > 1) ? 1 : accumulate;
+  return 0;
+}
+}  // namespace
+
+KML_API int kml_conv_pair_supported(int dvariant, int dbm, int dbn, int dbk, int wvariant, int wbm, int wbn, int wbk) {
+  return pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk) > 0 ? 1 : 0;
+}
+
+// dX (dgrad, + addend, + consumer-BN partials) and dW (wgrad, fp32 +=) of one conv in one
+// launch.  wt: transposed weights for the direct dgrad variant (else null).
+KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
+                              const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
+                              float* bnf_part, const bf16_t* x, float* dw, int B, int H, int W, int C, int K, int KH,
+                              int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
+                              int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
+                              int wvariant, hipStream_t s) {
+  const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
+  if (!which) return (int)hipErrorInvalidValue;
+  ConvArgs ad, aw;
+  int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, B, H, W, C, K, KH, KW, sh,
+                     sw, ph, pw, dbk, dsplits, dvariant, slab, counters);
+  if (e) return e;
+  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1);
+  if (e) return e;
+  return dispatch_pair(which, ad, aw, s);
+}
+
+// Up to 16 transposes wT = [C][KH*KW][Kp] (Kp = roundup(K, 32)) in one launch.
+// dims: n x 4 ints (K, KH*KW, C, unused).
+KML_API int kml_weight_transpose_multi(const bf16_t* const* ws, bf16_t* const* wts, const int* dims, int n,
+                                       hipStream_t s) {
+  if (n < 1 || n > 16) return (int)hipErrorInvalidValue;
+  TransposeBatch tb = {};
+  tb.n = n;
+  long long tot = 0;
+  for (int i = 0; i < n; ++i) {
+    TransposeJob& j = tb.j[i];
+    j.w = ws[i]; j.wt = wts[i];
+    j.K = dims[4 * i]; j.T = dims[4 * i + 1]; j.C = dims[4 * i + 2];
+    j.Kp = (j.K + 31) / 32 * 32;
+    j.begin = tot;
+    tot += (long long)j.C * j.T * j.Kp;
+  }
+  tb.total = tot;
+  hipLaunchKernelGGL(k_weight_transpose_multi, dim3(kml_stream_grid(tot, 256)), dim3(256), 0, s, tb);
+  KML_LAUNCH_CHECK();
 }
 
 // bnf_*: optional consumer-BN backward partials (see ConvArgs); bnf_part = null disables.

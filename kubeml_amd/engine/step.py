@@ -44,7 +44,7 @@ class GraphedTrainStep:
 
     def __init__(self, fwd_bwd: Callable[[], torch.Tensor], opt_step: Callable[[], None], grad_buffers=(),
                  group=None, use_graph: bool = True, warmup: int = 3, bucket_mb: float = 0.0,
-                 segments=None, segment_grads=None, force_segments: bool = False):
+                 segments=None, segment_grads=None, force_segments: bool = False, force_comm: bool = False):
         self.fwd_bwd = fwd_bwd
         self.opt_step = opt_step
         self.grad_buffers = list(grad_buffers)
@@ -54,6 +54,9 @@ class GraphedTrainStep:
         self.g_seg = []
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        # force_comm: issue the collectives even on a 1-rank group (exercises RCCL next to
+        # the captured graphs on a single-GPU box; the 8-GPU node is not ours to test on)
+        self.comm = self.world > 1 or (force_comm and dist.is_available() and dist.is_initialized())
         self.use_graph = use_graph
         self.warmup = warmup
         self.bucket_elems = int(bucket_mb * 2**20 / 4) if bucket_mb > 0 else 0
@@ -70,7 +73,7 @@ class GraphedTrainStep:
             return fn()
 
     def _allreduce(self):
-        if self.world <= 1:
+        if not self.comm:
             return
         for buf in self.grad_buffers:
             if self.bucket_elems and buf.numel() > self.bucket_elems:
@@ -101,11 +104,11 @@ class GraphedTrainStep:
         return loss
 
     def _segmented(self) -> bool:
-        return self.segments is not None and (self.world > 1 or self.force_segments)
+        return self.segments is not None and (self.comm or self.force_segments)
 
     def _issue(self, k):
         """Async all-reduce of the gradients finished by segment k."""
-        if self.world <= 1 or not self.segment_grads:
+        if not self.comm or not self.segment_grads:
             return []
         return [dist.all_reduce(t, group=self.group, async_op=True) for t in self.segment_grads[k] if t.numel()]
 
@@ -119,30 +122,34 @@ class GraphedTrainStep:
                 self._eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # with a process group alive, the RCCL watchdog thread polls work events while we
+        # capture; "thread_local" keeps its (uncaptured) queries from invalidating the
+        # capture.  Nothing on this thread makes an unsafe call inside a capture.
+        mode = "thread_local" if self.comm else "global"
         if self._segmented():
             pool = torch.cuda.graph_pool_handle()
             self.g_seg = []
             for k, seg in enumerate(self.segments):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                     out = self._run(seg)
                 if k == 0:
                     self.loss = out
                 self.g_seg.append(g)
             self.g_b = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_b, pool=pool):
+            with torch.cuda.graph(self.g_b, pool=pool, capture_error_mode=mode):
                 self.opt_step()
-        elif self.world <= 1:
+        elif not self.comm:
             self.g_a = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_a):
                 self.loss = self._run(self.fwd_bwd)
                 self.opt_step()
         else:
             self.g_a = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_a):
+            with torch.cuda.graph(self.g_a, capture_error_mode=mode):
                 self.loss = self._run(self.fwd_bwd)
             self.g_b = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_b):
+            with torch.cuda.graph(self.g_b, capture_error_mode=mode):
                 self.opt_step()
         torch.cuda.synchronize()
         self.captured = True

@@ -20,7 +20,7 @@ import torch.nn as tnn
 import torch.nn.functional as F
 
 from ..nn import modules as M
-from ..nn.fused import BlockFn, BNRegistry, ConvBNUnit, block_params
+from ..nn.fused import BlockFn, BNRegistry, ConvBNUnit, block_params, refresh_transposed
 
 
 def _gpu_train(x):
@@ -157,6 +157,12 @@ class ResNet(tnn.Module):
         if x.is_cuda:
             if self.training:
                 self._bump_counters()
+                if torch.is_grad_enabled():
+                    convs = getattr(self, "_kml_convs", None)
+                    if convs is None:
+                        convs = [m for m in self.modules() if isinstance(m, M.Conv2d)]
+                        object.__setattr__(self, "_kml_convs", convs)
+                    refresh_transposed(convs)
             x = self._stem_gpu(x)
         else:
             x = self.maxpool(self.bn1(self.conv1(x), relu=True))

@@ -96,6 +96,30 @@ def _wgrad(x, dc, conv):
     _WgradSide.pending = True
 
 
+def refresh_transposed(convs):
+    """Transposed bf16 weights ``[Cin][KH][KW][Kp]`` for every conv whose dgrad runs the
+    direct (LDS-free) variant, in ONE launch per 16 convs, at the start of a training
+    forward.  Which convs need them is learned from earlier backward passes
+    (ConvBNUnit.backward marks them); a conv not yet marked transposes inline.  The copy
+    is consumed (and dropped) by that conv's next backward."""
+    from ..ops import kernels as K
+    want = [c for c in convs if getattr(c, "_kml_wants_wt", False)]
+    ws, wts = [], []
+    for c in want:
+        w = shadow_of(c.weight)
+        Kc, KH, KW, C = w.shape
+        shape = (C, KH, KW, -(-Kc // 32) * 32)
+        buf = getattr(c, "_kml_wt_buf", None)
+        if buf is None or tuple(buf.shape) != shape or buf.device != w.device:
+            buf = torch.empty(shape, dtype=torch.bfloat16, device=w.device)
+            object.__setattr__(c, "_kml_wt_buf", buf)
+        ws.append(w)
+        wts.append(buf)
+        object.__setattr__(c, "_kml_wt", buf)
+    for i in range(0, len(ws), 16):
+        K.weight_transpose_multi(ws[i:i + 16], wts[i:i + 16])
+
+
 class BNRegistry:
     """The BatchNorm layers of a model in forward order (used for the packed
     ``num_batches_tracked`` counters).  BN statistics need no arena: the conv epilogue
@@ -146,10 +170,21 @@ class ConvBNUnit:
         dc = K.bn_bwd(dy, y, c, mean, rstd, master_of(bn.weight), grad_storage_of(bn.weight),
                       grad_storage_of(bn.bias), dres=dres, partial=partial)
         kh, kw = conv.kernel_size
-        _wgrad(x, dc, conv)
         dx, part_out = None, None
+        bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
+        if need_dx and _WgradSide.stream is None:
+            # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
+            w = shadow_of(conv.weight)
+            wt = getattr(conv, "_kml_wt", None)
+            if wt is None and K.dgrad_plan(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding)[4] == K.DIRECT:
+                object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
+            r = K.conv_bwd(dc, w, x, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding,
+                           addend=addend, bnf=bnf, wt=wt)
+            object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
+            dx, part_out = r if bnf is not None else (r, None)
+            return dx, dres, part_out
+        _wgrad(x, dc, conv)
         if need_dx:
-            bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
                              addend=addend, bnf=bnf)
             dx, part_out = r if bnf is not None else (r, None)

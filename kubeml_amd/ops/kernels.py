@@ -299,6 +299,116 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     return (out, (part, G)) if bnf is not None else out
 
 
+def dgrad_plan(in_shape, K, KH, KW, stride, pad, cfg=None):
+    """The (bm, bn, bk, splits, variant) plan conv_dgrad / conv_bwd run for this conv."""
+    B, H, W, C = in_shape
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    return _norm_cfg(cfg or plan_conv("dgrad", B * H * W, C, (r1 - r0) * (s1 - s0) * K))
+
+
+_PAIR_OK: dict = {}
+_PAIR_ON = os.environ.get("KUBEML_CONV_PAIR", "1") != "0"
+
+
+def conv_pair_supported(dcfg, wcfg) -> bool:
+    """True if the (dgrad plan, wgrad plan) combination has a grouped one-launch kernel."""
+    key = (tuple(dcfg), tuple(wcfg))
+    ok = _PAIR_OK.get(key)
+    if ok is None:
+        dbm, dbn, dbk, _, dv = dcfg
+        wbm, wbn, wbk, _, wv = wcfg
+        ok = _PAIR_OK[key] = bool(HIP.fn("kml_conv_pair_supported", "i i i i i i i i")(
+            dv, dbm, dbn, dbk, wv, wbm, wbn, wbk))
+    return ok
+
+
+def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None):
+    """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
+    :func:`conv_dgrad`) and ``dw += wgrad``.  Runs as ONE grouped launch
+    (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
+    instantiated pair, else as two launches.  ``wt``: precomputed transposed weights for
+    a direct-variant dgrad (:func:`weight_transpose_multi`); made here when missing.
+    Returns dx, or (dx, (part, G)) when ``bnf`` is given."""
+    _chk(dy, BF16, "dy", 4)
+    _chk(w, BF16, "w", 4)
+    _chk(x, BF16, "x", 4)
+    _chk(dw, F32, "dw", 4)
+    B, H, W, C = x.shape
+    K = w.shape[0]
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    if tuple(dy.shape) != (B, OH, OW, K) or tuple(w.shape) != (K, KH, KW, C) or tuple(dw.shape) != (K, KH, KW, C):
+        raise ValueError("conv_bwd shape mismatch")
+    if K % 8 or C % 8:
+        raise ValueError("channels must be multiples of 8")
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    ntap = (r1 - r0) * (s1 - s0)
+    M = B * H * W
+    dplan = _norm_cfg(dcfg or plan_conv("dgrad", M, C, ntap * K))
+    wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
+    if not (_PAIR_ON and conv_pair_supported(dplan, wplan)):
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan)
+        return conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf)
+    bm, bn, bk, splits, variant = dplan
+    out = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    if addend is not None:
+        _chk(addend, BF16, "addend")
+        assert addend.shape == out.shape
+    by = bc = bmean = brstd = part = None
+    G = 0
+    if bnf is not None:
+        by, bc, bmean, brstd = bnf
+        if bc.shape != out.shape or (by is not None and by.shape != out.shape):
+            raise ValueError("bnf tensors must match the dgrad output shape")
+        G = conv_stats_rows(M, dplan)
+        part = torch.empty(G * 2 * C, dtype=F32, device=dy.device)
+    slab = cnt = None
+    if variant == DIRECT:
+        Kp = _cdiv(K, 32) * 32
+        if wt is None:
+            wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=dy.device)
+            HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
+        elif tuple(wt.shape) != (C, KH, KW, Kp) or wt.dtype != BF16:
+            raise ValueError("transposed weight shape mismatch")
+        dsplits = 1
+    else:
+        wt = None
+        dsplits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
+        slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
+    wbm, wbn, wbk, wsplits, wvariant = wplan
+    HIP.call("kml_conv_bwd_pair",
+             "p p p p p p p p p p p p i i i i i i i i i i i i i i i i p p i i i i i s",
+             _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part),
+             _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant, _p(slab), _p(cnt),
+             wbm, wbn, wbk, wsplits, wvariant, _s())
+    return (out, (part, G)) if bnf is not None else out
+
+
+def weight_transpose_multi(ws, wts):
+    """wts[i][C,KH,KW,Kp] = transpose of ws[i][K,KH,KW,C] (Kp = roundup(K, 32), zero pad) for
+    up to 16 weights in one launch (direct-variant dgrad operands)."""
+    import ctypes
+    n = len(ws)
+    if n == 0:
+        return
+    if n > 16 or len(wts) != n:
+        raise ValueError("weight_transpose_multi: 1..16 pairs")
+    wp = (ctypes.c_void_p * n)()
+    tp = (ctypes.c_void_p * n)()
+    dims = (ctypes.c_int * (4 * n))()
+    for i, (w, wt) in enumerate(zip(ws, wts)):
+        _chk(w, BF16, "w", 4)
+        _chk(wt, BF16, "wt", 4)
+        K, KH, KW, C = w.shape
+        if tuple(wt.shape) != (C, KH, KW, _cdiv(K, 32) * 32):
+            raise ValueError("transposed weight shape mismatch")
+        wp[i], tp[i] = w.data_ptr(), wt.data_ptr()
+        dims[4 * i], dims[4 * i + 1], dims[4 * i + 2] = K, KH * KW, C
+    HIP.call("kml_weight_transpose_multi", "p p p i s", ctypes.addressof(wp), ctypes.addressof(tp),
+             ctypes.addressof(dims), n, _s())
+
+
 def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None):
     """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient."""
     _chk(x, BF16, "x", 4)

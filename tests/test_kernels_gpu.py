@@ -372,3 +372,64 @@ def test_dgrad_emits_consumer_bn_partials(cfg):
     r1 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg1, db1, partial=partial)
     assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
     assert _rel(r1, r0) < 1e-2
+
+
+PAIR_PLANS = [  # (dgrad plan, wgrad plan) pairs with a grouped kernel
+    ((32, 64, 64, 1, 0), (32, 32, 64, 1, 0)), ((32, 32, 64, 2, 0), (64, 32, 64, 4, 0)),
+    ((32, 32, 4, 1, 3), (32, 32, 64, 2, 0)), ((64, 32, 4, 1, 3), (64, 32, 64, 1, 0)),
+    ((32, 16, 4, 1, 3), (32, 32, 64, 8, 0)),
+]
+
+
+@pytest.mark.parametrize("plans", PAIR_PLANS)
+@pytest.mark.parametrize("shape", [(8, 8, 8, 64, 64, 3, 1, 1), (6, 5, 5, 64, 96, 3, 1, 1), (8, 8, 8, 64, 128, 3, 2, 1),
+                                   (32, 1, 1, 512, 512, 3, 1, 1), (16, 4, 4, 128, 256, 1, 2, 0)])
+def test_conv_bwd_pair_matches_separate(plans, shape):
+    """Grouped dgrad+wgrad launch (k_conv_pair) == the two separate kernels (bit-exact dX and
+    consumer-BN partials; dW equal up to atomic ordering) and the fp32 torch reference."""
+    from kubeml_amd.ops import kernels as K
+    dcfg, wcfg = plans
+    assert K.conv_pair_supported(dcfg, wcfg)
+    B, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(8)
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * 0.05)
+    OH, OW = K.out_hw(H, W, k, k, s, s, p, p)
+    dy = _bf(torch.randn(B, OH, OW, Co, device=dev))
+    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    c = _bf(torch.randn(B, H, W, Ci, device=dev))
+    ybn = _bf(torch.randn(B, H, W, Ci, device=dev))
+    mean, rstd = torch.randn(Ci, device=dev), torch.rand(Ci, device=dev) + 0.5
+    bnf = (ybn, c, mean, rstd)
+    dw0 = torch.zeros(Co, k, k, Ci, device=dev)
+    K.conv_wgrad(x, dy, dw0, k, k, (s, s), (p, p), cfg=wcfg)
+    dx0, (part0, G0) = K.conv_dgrad(dy, w, x.shape, k, k, (s, s), (p, p), addend=add, cfg=dcfg, bnf=bnf)
+    dw1 = torch.zeros_like(dw0)
+    wt = None
+    if dcfg[4] == K.DIRECT:
+        wt = torch.empty(Ci, k, k, -(-Co // 32) * 32, dtype=torch.bfloat16, device=dev)
+        K.weight_transpose_multi([w], [wt])
+    dx1, (part1, G1) = K.conv_bwd(dy, w, x, dw1, k, k, (s, s), (p, p), addend=add, bnf=bnf, wt=wt,
+                                  dcfg=dcfg, wcfg=wcfg)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    assert G0 == G1 and torch.equal(part0, part1)
+    assert _rel(dw1, dw0) < 1e-5
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(xr, wr, stride=s, padding=p).backward(dy.float().permute(0, 3, 1, 2))
+    assert _rel(dw1.permute(0, 3, 1, 2), wr.grad) < 1e-2
+    assert _rel(dx1.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
+
+
+def test_weight_transpose_multi():
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(9)
+    ws = [_bf(torch.randn(co, k, k, ci, device=dev)) for co, k, ci in [(64, 3, 64), (40, 3, 96), (512, 1, 256)]]
+    wts = [torch.full((w.shape[3], w.shape[1], w.shape[2], -(-w.shape[0] // 32) * 32), 7.0, dtype=torch.bfloat16,
+                      device=dev) for w in ws]
+    K.weight_transpose_multi(ws, wts)
+    for w, wt in zip(ws, wts):
+        Co = w.shape[0]
+        assert torch.equal(wt[..., :Co], w.permute(3, 1, 2, 0))
+        assert (wt[..., Co:] == 0).all()
