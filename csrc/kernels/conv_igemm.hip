@@ -82,6 +82,13 @@ struct ConvArgs {
   // DGRAD -> consumer-BN backward fusion: partial [sum dz | sum dz*xhat] rows of the BN that
   // consumes this dX (dz = dX * [y > 0], xhat = (c - mean) * rstd), same row layout as stats_part
   const bf16_t* bnf_y; const bf16_t* bnf_c; const float* bnf_mean; const float* bnf_rstd; float* bnf_part;
+  // Group reduction of the per-wave partial rows (FWD stats_part / DGRAD bnf_part): every
+  // grp_tiles consecutive M-tiles form a group; the last-arriving block of a group (agent-scope
+  // ticket per (group, n-tile)) sums the group's rows in a fixed order into grp_out[g][2N], so
+  // the consumer BN kernel reads ceil(tiles/grp_tiles) rows instead of one per wave.
+  float* grp_out;        // [NG][2N] or null (consumer sums the per-wave rows itself)
+  unsigned* grp_cnt;     // NG * n-tiles tickets (zero on entry; the last arriver resets)
+  int grp_tiles;
   int stats_part;        // FWD stats: 0 = atomics into stats[2N]; 1 = plain stores of per-wave
                          //   partial rows stats[(m0/WM + wm)][2N] (summed by bn_apply)
   int B, H, W, C;        // input geometry (C = Cin)
@@ -287,7 +294,65 @@ __device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, i
   return f;
 }
 
-template <int MODE, int MR, int NR, int WM, int WN>
+// Last arriver of an M-tile group sums the group's per-wave partial rows (ConvArgs::grp_*).
+// BMT/BNT: block tile, RPT: partial rows per M-tile, SINGLE: one live wave (direct variant).
+// Hand-off without fences (CDNA guide §6 G16, R1 fan-in): the rows were stored write-through
+// (sc1, store_row), every wave drains its stores before the barrier, one lane takes a relaxed
+// agent-scope ticket, and the last arriver reads the rows with sc1 loads (past its L1).  A
+// release fence here would write back the block's whole dirty L2 share (the conv output).
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// partial-row store: write-through (sc1) when a group reduction reads it in this launch
+__device__ __forceinline__ void store_row(float* p, float v, bool sc1) {
+  if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <int BMT, int BNT, int RPT, bool SINGLE>
+__device__ __forceinline__ void group_reduce_rows(const ConvArgs& a, const float* rows, int m0, int n0, int tid,
+                                                  unsigned* flag) {
+  const int tile_m = m0 / BMT, tile_n = n0 / BNT;
+  const int ntn = (a.N + BNT - 1) / BNT, ntm = (a.M + BMT - 1) / BMT;
+  const int g = tile_m / a.grp_tiles;
+  const int t0 = g * a.grp_tiles, t1 = min(ntm, t0 + a.grp_tiles);
+  unsigned* cnt = a.grp_cnt + g * ntn + tile_n;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 rows
+  unsigned last = 0;
+  if constexpr (!SINGLE) __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == (unsigned)(t1 - t0 - 1)) ? 1u : 0u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (!SINGLE) flag[0] = last;
+  }
+  if constexpr (SINGLE) {
+    last = (unsigned)__shfl((int)last, 0, 64);
+  } else {
+    __syncthreads();
+    last = flag[0];
+  }
+  if (!last) return;
+  constexpr int NT = SINGLE ? 64 : 256;
+  const int r0 = t0 * RPT, r1 = t1 * RPT;
+  for (int q = tid; q < 2 * BNT; q += NT) {
+    const int half = q / BNT, col = n0 + (q - half * BNT);
+    if (col >= a.N) continue;
+    const float* src = rows + (long long)half * a.N + col;
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int r = r0;
+    for (; r + 4 <= r1; r += 4) {  // 4 independent sc1 loads in flight, fixed summation order
+      acc0 += ld_sc1(src + (long long)r * 2 * a.N);
+      acc1 += ld_sc1(src + (long long)(r + 1) * 2 * a.N);
+      acc2 += ld_sc1(src + (long long)(r + 2) * 2 * a.N);
+      acc3 += ld_sc1(src + (long long)(r + 3) * 2 * a.N);
+    }
+    for (; r < r1; ++r) acc0 += ld_sc1(src + (long long)r * 2 * a.N);
+    a.grp_out[(long long)g * 2 * a.N + (long long)half * a.N + col] = (acc0 + acc1) + (acc2 + acc3);
+  }
+}
+
+template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
                                               int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -396,8 +461,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
         if (fq == 0 && cok) {
           float* prow = a.bnf_part + (long long)(m0 / WM + wm) * 2 * a.N;
-          prow[col] = s1;
-          prow[a.N + col] = s2;
+          store_row(prow + col, s1, a.grp_out != nullptr);
+          store_row(prow + a.N + col, s2, a.grp_out != nullptr);
         }
       }
       if (MODE == FWD && a.stats) {
@@ -406,14 +471,21 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         if (fq == 0 && cok) {
           if (a.stats_part) {
             float* prow = a.stats + (long long)(m0 / WM + wm) * 2 * a.N;
-            prow[col] = s1;
-            prow[a.N + col] = s2;
+            store_row(prow + col, s1, a.grp_out != nullptr);
+            store_row(prow + a.N + col, s2, a.grp_out != nullptr);
           } else {
             atomicAdd(a.stats + col, s1);
             atomicAdd(a.stats + a.N + col, s2);
           }
         }
       }
+    }
+    if (a.grp_out) {
+      constexpr int BMT = SINGLE ? WM : 2 * WM, BNT = SINGLE ? WN : 2 * WN, RPT = SINGLE ? 1 : 2;
+      if (MODE == FWD && a.stats && a.stats_part)
+        group_reduce_rows<BMT, BNT, RPT, SINGLE>(a, a.stats, m0, n0, tid, flag);
+      else if (MODE == DGRAD && a.bnf_part)
+        group_reduce_rows<BMT, BNT, RPT, SINGLE>(a, a.bnf_part, m0, n0, tid, flag);
     }
   }
 }
@@ -858,7 +930,7 @@ __device__ __forceinline__ void DirectBody<MODE, MR, NR, NW, D>::run(const ConvA
         }
     }
   }
-  conv_epilogue<MODE, MR, NR, 16 * MR, 16 * NR>(a, acc, m0, n0, 0, 0, lane, lane, 0, 0, nullptr);
+  conv_epilogue<MODE, MR, NR, 16 * MR, 16 * NR, true>(a, acc, m0, n0, 0, 0, lane, lane, 0, 0, nullptr);
 }
 
 template <int MODE, int MR, int NR, int NW, int D>
@@ -1062,30 +1134,50 @@ int dispatch_pair(int which, const ConvArgs& ad, const ConvArgs& aw, hipStream_t
   return (int)hipErrorInvalidValue;
 }
 
-// wT[c][t][k] = w[k][t][c] for up to 16 weights in one launch (kml_weight_transpose_multi)
+// wT[c][t][k] = w[k][t][c] for up to 16 weights in one launch (kml_weight_transpose_multi).
+// One block per 64(k) x 64(c) tile of one tap: 16-byte loads along c into an LDS tile,
+// 16-byte stores along k out of it (k >= K zero-filled up to Kp).
 struct TransposeJob {
   const bf16_t* w;
   bf16_t* wt;
-  long long begin;  // first element of this job in the launch's flat index space
-  int K, T, C, Kp;
+  int tile_begin;  // first block of this job
+  int K, T, C, Kp, tk, tc;  // tk / tc: 64-wide tiles along Kp / C
 };
 struct TransposeBatch {
   TransposeJob j[16];
   int n;
-  long long total;
 };
 
-__global__ void k_weight_transpose_multi(TransposeBatch tb) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < tb.total;
-       i += (long long)gridDim.x * blockDim.x) {
-    int q = 0;
-    while (q + 1 < tb.n && i >= tb.j[q + 1].begin) ++q;
-    const TransposeJob& jb = tb.j[q];
-    const long long e = i - jb.begin;
-    const int k = (int)(e % jb.Kp);
-    const long long ct = e / jb.Kp;
-    const int t = (int)(ct % jb.T), c = (int)(ct / jb.T);
-    jb.wt[e] = k < jb.K ? jb.w[((long long)k * jb.T + t) * jb.C + c] : (bf16_t)0;
+__global__ __launch_bounds__(256) void k_weight_transpose_multi(TransposeBatch tb) {
+  __shared__ bf16_t tile[64][64 + 8];
+  int q = 0;
+  while (q + 1 < tb.n && (int)blockIdx.x >= tb.j[q + 1].tile_begin) ++q;  // block-uniform
+  const TransposeJob& jb = tb.j[q];
+  int id = (int)blockIdx.x - jb.tile_begin;
+  const int ic = id % jb.tc;
+  id /= jb.tc;
+  const int ik = id % jb.tk;
+  const int t = id / jb.tk;
+  const int k0 = ik * 64, c0 = ic * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // 64 k-rows x 8 chunks of 8 c
+    const int q2 = tid + 256 * u, r = q2 >> 3, ch = q2 & 7;
+    const int k = k0 + r, c = c0 + ch * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k < jb.K && c < jb.C) v = *reinterpret_cast<const uint4*>(jb.w + ((long long)k * jb.T + t) * jb.C + c);
+    *reinterpret_cast<uint4*>(&tile[r][ch * 8]) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // 64 c-rows x 8 chunks of 8 k
+    const int q2 = tid + 256 * u, r = q2 >> 3, ch = q2 & 7;
+    const int c = c0 + r, k = k0 + ch * 8;
+    if (c >= jb.C || k >= jb.Kp) continue;
+    bf16_t o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = tile[ch * 8 + e][r];
+    *reinterpret_cast<uint4*>(jb.wt + ((long long)c * jb.T + t) * jb.Kp + k) = *reinterpret_cast<const uint4*>(o);
   }
 }
 
@@ -1117,15 +1209,18 @@ KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
 
 // stats_part = 1: stats is [G][2K] with G = ceil(M / WM) (WM = bm for variant 3, bm/2 otherwise);
 // every row is written (no zeroing needed) and bn_apply sums the rows.
+// grp_out / grp_cnt / grp_tiles: optional group reduction of the stats_part rows (ConvArgs).
 KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int stats_part,
                          int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu,
                          int bm, int bn, int bk, int splits, int variant, float* slab, unsigned* counters,
-                         hipStream_t s) {
+                         float* grp_out, unsigned* grp_cnt, int grp_tiles, hipStream_t s) {
+  if (grp_out && (!stats || !stats_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
   if (C % 8) return (int)hipErrorInvalidValue;
   if (variant == 3) {  // direct: bk carries the wave count; needs 32-aligned taps
     if (C % 32) return (int)hipErrorInvalidValue;
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
     a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
     a.zp = zero_page();
     a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
     a.splits = 1; a.kchunk = a.Kd;
@@ -1135,6 +1230,7 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
   a.zp = zero_page();
   a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
@@ -1147,9 +1243,11 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
 namespace {
 int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
                const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
-               float* bnf_part, int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-               int bk, int splits, int variant, float* slab, unsigned* counters) {
+               float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W, int C, int K,
+               int KH, int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, float* slab,
+               unsigned* counters) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  if (grp_out && (!bnf_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
   const bool direct = (variant == 3);
   if (!direct && variant) bk = 64;
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
@@ -1158,6 +1256,7 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
   a.fd_Kp = make_fd(a.Kp);
   a.dy = dy; a.w = w; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
   a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
+  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   if (direct) {
@@ -1193,15 +1292,16 @@ KML_API int kml_conv_pair_supported(int dvariant, int dbm, int dbn, int dbk, int
 // launch.  wt: transposed weights for the direct dgrad variant (else null).
 KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
                               const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
-                              float* bnf_part, const bf16_t* x, float* dw, int B, int H, int W, int C, int K, int KH,
+                              float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, const bf16_t* x,
+                              float* dw, int B, int H, int W, int C, int K, int KH,
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
                               int wvariant, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
-  int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, B, H, W, C, K, KH, KW, sh,
-                     sw, ph, pw, dbk, dsplits, dvariant, slab, counters);
+  int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
+                     grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters);
   if (e) return e;
   e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1);
   if (e) return e;
@@ -1215,55 +1315,38 @@ KML_API int kml_weight_transpose_multi(const bf16_t* const* ws, bf16_t* const* w
   if (n < 1 || n > 16) return (int)hipErrorInvalidValue;
   TransposeBatch tb = {};
   tb.n = n;
-  long long tot = 0;
+  long long tiles = 0;
   for (int i = 0; i < n; ++i) {
     TransposeJob& j = tb.j[i];
     j.w = ws[i]; j.wt = wts[i];
     j.K = dims[4 * i]; j.T = dims[4 * i + 1]; j.C = dims[4 * i + 2];
+    if (j.C % 8) return (int)hipErrorInvalidValue;  // 16-byte rows along c
     j.Kp = (j.K + 31) / 32 * 32;
-    j.begin = tot;
-    tot += (long long)j.C * j.T * j.Kp;
+    j.tk = (j.Kp + 63) / 64;
+    j.tc = (j.C + 63) / 64;
+    j.tile_begin = (int)tiles;
+    tiles += (long long)j.T * j.tk * j.tc;
   }
-  tb.total = tot;
-  hipLaunchKernelGGL(k_weight_transpose_multi, dim3(kml_stream_grid(tot, 256)), dim3(256), 0, s, tb);
+  if (tiles <= 0 || tiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_weight_transpose_multi, dim3((unsigned)tiles), dim3(256), 0, s, tb);
   KML_LAUNCH_CHECK();
 }
 
 // bnf_*: optional consumer-BN backward partials (see ConvArgs); bnf_part = null disables.
-KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, const bf16_t* bnf_y,
-                           const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd, float* bnf_part, int B,
-                           int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn,
-                           int bk, int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+// grp_*: optional group reduction of those partial rows.  variant 3 (direct): wt is the
+// transposed weight copy (kml_weight_transpose, Kp = roundup(K, 32)) and bk the wave count.
+KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
+                           const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
+                           float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W,
+                           int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
+                           int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+  ConvArgs a;
+  const int e = prep_dgrad(a, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
+                           grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, slab, counters);
+  if (e) return e;
+  if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
   if (variant) bk = 64;
-  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
-  ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.Kp = (K + bk - 1) / bk * bk;
-  a.fd_Kp = make_fd(a.Kp);
-  a.dy = dy; a.w = w; a.out = dx; a.addend = addend; a.zp = zero_page();
-  a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
-  a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
-  if (!a.zp) return (int)hipErrorInvalidSymbol;
-  set_splits(a, bk, splits);
-  if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
-  a.slab = slab; a.counters = counters;
   return dispatch<DGRAD>(a, bm, bn, bk, variant, s);
-}
-
-// Direct dgrad: wt = kml_weight_transpose(w) (layout [C][KH*KW][Kp], Kp = roundup(K, 32)).
-KML_API int kml_conv_dgrad_direct(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
-                                  const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean,
-                                  const float* bnf_rstd, float* bnf_part, int B, int H, int W, int C, int K, int KH,
-                                  int KW, int sh, int sw, int ph, int pw, int bm, int bn, int nw, hipStream_t s) {
-  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
-  ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.Kp = (K + 31) / 32 * 32;
-  a.fd_Kp = make_fd(a.Kp);
-  a.dy = dy; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
-  a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
-  a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
-  a.splits = 1; a.kchunk = a.Kd;
-  if (!a.zp) return (int)hipErrorInvalidSymbol;
-  return dispatch_direct<DGRAD>(a, bm, bn, nw, s);
 }
 
 KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int KW, int C, hipStream_t s) {

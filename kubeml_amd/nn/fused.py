@@ -176,7 +176,7 @@ class ConvBNUnit:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
             w = shadow_of(conv.weight)
             wt = getattr(conv, "_kml_wt", None)
-            if wt is None and K.dgrad_plan(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding)[4] == K.DIRECT:
+            if wt is None and K.bwd_plans(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding)[0][4] == K.DIRECT:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
             r = K.conv_bwd(dc, w, x, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding,
                            addend=addend, bnf=bnf, wt=wt)

@@ -51,6 +51,7 @@ def _chk(t, dtype, name, ndim=None):
 
 _TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32)]
 _TUNED: dict = {}  # (mode, M, N, Kd) -> (bm, bn, bk, splits); loaded from conv_tuning.json
+_TUNED_PAIR: dict = {}  # (dgrad M, N, Kd, wgrad M, N, Kd) -> (dgrad plan, wgrad plan) of a grouped launch
 _TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
 
 
@@ -60,7 +61,10 @@ def _load_tuning():
     if os.path.exists(_TUNE_FILE):
         with open(_TUNE_FILE) as f:
             for e in json.load(f).get("entries", []):
-                _TUNED[(e["mode"], e["M"], e["N"], e["Kd"])] = tuple(e["cfg"])
+                if e["mode"] == "pair":
+                    _TUNED_PAIR[(e["M"], e["N"], e["Kd"]) + tuple(e["wgrad"])] = (tuple(e["cfg"]), tuple(e["wcfg"]))
+                else:
+                    _TUNED[(e["mode"], e["M"], e["N"], e["Kd"])] = tuple(e["cfg"])
 
 
 _load_tuning()
@@ -178,11 +182,41 @@ def _splitk_ws(device, M, N, bm, bn, splits):
 DIRECT = 3  # cfg variant id of the LDS-free wave-split-K kernel (fwd / dgrad)
 
 
-def conv_stats_rows(M, cfg):
-    """Partial-statistics rows the FWD epilogue writes for a plan (one per wave row band)."""
+# Partial BN rows above this count are group-reduced inside the producing conv (the last
+# block of every group of M-tiles sums its group's rows): the consumer BN kernel, whose every
+# block otherwise re-reads all rows from L2, then reads at most 16 rows.  Opt-in
+# (KUBEML_BN_GROUP_MIN=N): on ResNet-34/b256 the ticket hand-off in every producer block costs
+# more than the consumer saves (1.720 ms/step off vs 1.758-1.782 at N = 64..512).
+_GRP_MIN = int(os.environ.get("KUBEML_BN_GROUP_MIN", "0"))
+_GRP_ROWS = 16
+
+
+def _stats_layout(M, cfg):
+    """(per-wave rows G, M-tiles per group or 0, rows the consumer reads)."""
     bm, _, _, _, variant = _norm_cfg(cfg)
+    tiles = _cdiv(M, bm)
     # one row per wave row-band of every M tile (tail tiles included: their waves write zeros)
-    return _cdiv(M, bm) * (1 if variant == DIRECT else 2)
+    G = tiles * (1 if variant == DIRECT else 2)
+    if _GRP_MIN <= 0 or G <= _GRP_MIN:
+        return G, 0, G
+    tpg = _cdiv(tiles, _GRP_ROWS)
+    return G, tpg, _cdiv(tiles, tpg)
+
+
+def conv_stats_rows(M, cfg):
+    """Rows of the partial-statistics buffer a conv epilogue hands to the BN kernel for a
+    plan: one per wave row band, or one per M-tile group when group-reduced."""
+    return _stats_layout(M, cfg)[2]
+
+
+def _stats_ws(device, M, N, cfg, out):
+    """(rows buffer the epilogue writes, group output or None, tickets, tiles per group)."""
+    G, tpg, ng = _stats_layout(M, cfg)
+    if not tpg:
+        return out, None, None, 0
+    bn = _norm_cfg(cfg)[1]
+    scratch = torch.empty(G * 2 * N, dtype=F32, device=device)
+    return scratch, out, _COUNTERS.take(device, ng * _cdiv(N, bn)), tpg
 
 
 def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False):
@@ -210,21 +244,23 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
     bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg)
+    rows, grp, gcnt, tpg = stats, None, None, 0
     if stats is not None:
         _chk(stats, F32, "stats")
         need = 2 * K * (conv_stats_rows(M, (bm, bn, bk, splits, variant)) if stats_part else 1)
         if stats.numel() < need:
             raise ValueError(f"stats buffer has {stats.numel()} floats, needs {need}")
+        if stats_part:
+            rows, grp, gcnt, tpg = _stats_ws(x.device, M, K, (bm, bn, bk, splits, variant), stats)
+    sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i s"
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
-        HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i i p p s",
-                 _p(x), _p(w), _p(out), _p(bias), _p(stats), int(stats_part), B, H, W, C, K, KH, KW, sh, sw, ph,
-                 pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _s())
+        HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
+                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, _s())
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
-    HIP.call("kml_conv_fwd", "p p p p p i i i i i i i i i i i i i i i i i i p p s",
-             _p(x), _p(w), _p(out), _p(bias), _p(stats), int(stats_part), B, H, W, C, K, KH, KW, sh, sw, ph, pw,
-             int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _s())
+    HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
+             sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt), tpg, _s())
     return out
 
 
@@ -245,7 +281,7 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None):
     return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg))
 
 
-def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None):
+def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None, wt=None):
     """dx = conv input gradient (+ addend, the fused residual-gradient sum).
 
     bnf = (y or None, c, mean, rstd) of the BatchNorm that consumes dx: the epilogue also
@@ -273,37 +309,71 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     M = B * H * W
     ntap = (r1 - r0) * (s1 - s0)
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
-    by = bc = bmean = brstd = part = None
-    G = 0
-    if bnf is not None:
-        by, bc, bmean, brstd = bnf
-        if bc.shape != out.shape or (by is not None and by.shape != out.shape):
-            raise ValueError("bnf tensors must match the dgrad output shape")
-        G = conv_stats_rows(M, (bm, bn, bk, splits, variant))
-        part = torch.empty(G * 2 * C, dtype=F32, device=dy.device)
+    plan = (bm, bn, bk, splits, variant)
+    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan)
+    slab = cnt = None
     if variant == DIRECT:
         # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
-        Kp = _cdiv(K, 32) * 32
-        wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=dy.device)
-        HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
-        HIP.call("kml_conv_dgrad_direct", "p p p p p p p p p i i i i i i i i i i i i i i s",
-                 _p(dy), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part), B, H, W, C,
-                 K, KH, KW, sh, sw, ph, pw, bm, bn, bk, _s())
-        return (out, (part, G)) if bnf is not None else out
-    Kd = ntap * _cdiv(K, bk) * bk
-    splits = effective_splits(Kd, bk, splits)
-    slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
-    HIP.call("kml_conv_dgrad", "p p p p p p p p p i i i i i i i i i i i i i i i i p p s",
-             _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part), B, H, W, C, K,
-             KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt), _s())
+        wt = _direct_wt(w, wt)
+        splits = 1
+    else:
+        wt = None
+        splits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
+        slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
+    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p s",
+             _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
+             _p(gcnt), tpg, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt),
+             _s())
     return (out, (part, G)) if bnf is not None else out
 
 
+def _bnf_ws(bnf, out, M, C, plan):
+    """Consumer-BN partial-row buffers of a dgrad: (y, c, mean, rstd, part the BN reads,
+    rows the epilogue writes, group output, tickets, tiles per group, rows in part)."""
+    if bnf is None:
+        return None, None, None, None, None, None, None, None, 0, 0
+    by, bc, bmean, brstd = bnf
+    if bc.shape != out.shape or (by is not None and by.shape != out.shape):
+        raise ValueError("bnf tensors must match the dgrad output shape")
+    G = conv_stats_rows(M, plan)
+    part = torch.empty(G * 2 * C, dtype=F32, device=out.device)
+    rows, grp, gcnt, tpg = _stats_ws(out.device, M, C, plan, part)
+    return by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G
+
+
+def _direct_wt(w, wt):
+    """Transposed weights [Cin][KH][KW][Kp] for the direct dgrad (made here when not given)."""
+    K, KH, KW, C = w.shape
+    Kp = _cdiv(K, 32) * 32
+    if wt is None:
+        wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=w.device)
+        HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
+    elif tuple(wt.shape) != (C, KH, KW, Kp) or wt.dtype != BF16:
+        raise ValueError("transposed weight shape mismatch")
+    return wt
+
+
 def dgrad_plan(in_shape, K, KH, KW, stride, pad, cfg=None):
-    """The (bm, bn, bk, splits, variant) plan conv_dgrad / conv_bwd run for this conv."""
+    """The (bm, bn, bk, splits, variant) plan conv_dgrad runs for this conv."""
     B, H, W, C = in_shape
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     return _norm_cfg(cfg or plan_conv("dgrad", B * H * W, C, (r1 - r0) * (s1 - s0) * K))
+
+
+def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None):
+    """(dgrad plan, wgrad plan, grouped?) conv_bwd runs for this conv: a tuned pair entry
+    when one exists, else the separately tuned plans (grouped if instantiated)."""
+    B, H, W, C = in_shape
+    sh, sw = stride
+    ph, pw = pad
+    OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
+    ntap = (r1 - r0) * (s1 - s0)
+    if dcfg is None and wcfg is None:
+        dcfg, wcfg = _TUNED_PAIR.get((B * H * W, C, ntap * K, K, ntap * C, B * OH * OW), (None, None))
+    dplan = _norm_cfg(dcfg or plan_conv("dgrad", B * H * W, C, ntap * K))
+    wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
+    return dplan, wplan, _PAIR_ON and conv_pair_supported(dplan, wplan)
 
 
 _PAIR_OK: dict = {}
@@ -345,32 +415,19 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
-    dplan = _norm_cfg(dcfg or plan_conv("dgrad", M, C, ntap * K))
-    wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
-    if not (_PAIR_ON and conv_pair_supported(dplan, wplan)):
+    dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
+    if not grouped:
         conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan)
-        return conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf)
+        return conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt)
     bm, bn, bk, splits, variant = dplan
     out = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
     if addend is not None:
         _chk(addend, BF16, "addend")
         assert addend.shape == out.shape
-    by = bc = bmean = brstd = part = None
-    G = 0
-    if bnf is not None:
-        by, bc, bmean, brstd = bnf
-        if bc.shape != out.shape or (by is not None and by.shape != out.shape):
-            raise ValueError("bnf tensors must match the dgrad output shape")
-        G = conv_stats_rows(M, dplan)
-        part = torch.empty(G * 2 * C, dtype=F32, device=dy.device)
+    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan)
     slab = cnt = None
     if variant == DIRECT:
-        Kp = _cdiv(K, 32) * 32
-        if wt is None:
-            wt = torch.empty((C, KH, KW, Kp), dtype=BF16, device=dy.device)
-            HIP.call("kml_weight_transpose", "p p i i i i s", _p(w), _p(wt), K, KH, KW, C, _s())
-        elif tuple(wt.shape) != (C, KH, KW, Kp) or wt.dtype != BF16:
-            raise ValueError("transposed weight shape mismatch")
+        wt = _direct_wt(w, wt)
         dsplits = 1
     else:
         wt = None
@@ -378,10 +435,10 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i i i i i i i i i i i i i i i i p p i i i i i s",
-             _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part),
-             _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant, _p(slab), _p(cnt),
-             wbm, wbn, wbk, wsplits, wvariant, _s())
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i s",
+             _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
+             _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
+             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, _s())
     return (out, (part, G)) if bnf is not None else out
 
 

@@ -433,3 +433,46 @@ def test_weight_transpose_multi():
         Co = w.shape[0]
         assert torch.equal(wt[..., :Co], w.permute(3, 1, 2, 0))
         assert (wt[..., Co:] == 0).all()
+
+
+@pytest.mark.parametrize("cfg", [(128, 32, 64, 1, 1), (32, 64, 64, 1, 0), (64, 32, 64, 2, 0), (32, 32, 4, 1, 3)])
+def test_grouped_partial_rows(cfg):
+    """Large-M convs group-reduce their partial BN rows in the epilogue (last arriver of each
+    M-tile group): the consumer sees <= 16 rows whose sum equals the atomic statistics, and
+    the dgrad consumer-BN partials give the same dgamma/dbeta as the unfused BN backward."""
+    from kubeml_amd.ops import kernels as K
+    old_min = K._GRP_MIN
+    K._GRP_MIN = 64
+    try:
+        _grouped_partial_rows(K, cfg)
+    finally:
+        K._GRP_MIN = old_min
+
+
+def _grouped_partial_rows(K, cfg):
+    torch.manual_seed(10)
+    B, H, W, Ci, Co = 256, 8, 8, 64, 64     # M = 16384: well above the grouping threshold
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * 0.05)
+    G = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, (1, 1), (1, 1), cfg=cfg)
+    assert G <= 16
+    st_a = torch.zeros(2 * Co, device=dev)
+    y = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=st_a, cfg=cfg)
+    for _ in range(3):   # repeated launches: the group tickets must reset themselves
+        buf = torch.full((G * 2 * Co,), float("nan"), device=dev)
+        y2 = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=buf, stats_part=True, cfg=cfg)
+        assert torch.equal(y, y2)
+        assert _rel(buf.view(G, 2 * Co).sum(0), st_a) < 1e-5
+    dy = _bf(torch.randn(B, H, W, Co, device=dev))
+    c = _bf(torch.randn(B, H, W, Ci, device=dev))
+    ybn = _bf(torch.randn(B, H, W, Ci, device=dev))
+    mean, rstd = torch.randn(Ci, device=dev), torch.rand(Ci, device=dev) + 0.5
+    g = torch.rand(Ci, device=dev) + 0.5
+    dx1, partial = K.conv_dgrad(dy, w, x.shape, 3, 3, (1, 1), (1, 1), cfg=cfg, bnf=(ybn, c, mean, rstd))
+    assert partial[1] <= 16
+    dg0, db0 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    dg1, db1 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    r0 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg0, db0)
+    r1 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg1, db1, partial=partial)
+    assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
+    assert _rel(r1, r0) < 1e-2

@@ -90,6 +90,75 @@ def bench(fn, reps=20, warm=2, inner=10):
     return ts[len(ts) // 2] * 1e3 / inner  # us per call
 
 
+PAIR_DGRAD = [(32, 64, 64, sp, 0) for sp in (1, 2, 4)] + [(32, 32, 64, sp, 0) for sp in (1, 2, 4, 8)] + \
+    [(32, 32, 4, 1, 3), (32, 16, 4, 1, 3), (64, 32, 4, 1, 3)]
+PAIR_WGRAD = [(bm, 32, 64, sp, 0) for bm in (32, 64) for sp in (1, 2, 4, 8, 16, 32)]
+
+
+def tune_pairs(layers, table, reps, dev):
+    """Grouped dgrad+wgrad launches (ops.kernels.conv_bwd): for every conv layer time each
+    instantiated (dgrad plan, wgrad plan) pair and keep the fastest when it beats the two
+    separately tuned launches.  Entries: mode "pair", keyed by the dgrad and wgrad GEMMs."""
+    out = []
+    for (kind, cin, cout, k, s, p, H, W, B) in layers:
+        if kind != "conv" or cin == 8:
+            continue
+        OH, OW = K.out_hw(H, W, k, k, s, s, p, p)
+        r0, r1, s0, s1 = K.tap_window(H, W, k, k, s, s, p, p)
+        ntap = (r1 - r0) * (s1 - s0)
+        dkey = (B * H * W, cin, ntap * cout)
+        wkey = (cout, ntap * cin, B * OH * OW)
+        key = ("pair",) + dkey + wkey
+        if key in table:
+            continue
+        x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(cout, k, k, cin, device=dev) * 0.05).to(torch.bfloat16)
+        dy = torch.randn(B, OH, OW, cout, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(cout, k, k, cin, device=dev)
+        wt = torch.empty(cin, k, k, -(-cout // 32) * 32, dtype=torch.bfloat16, device=dev)
+        K.weight_transpose_multi([w], [wt])
+        sep_d = K.dgrad_plan(x.shape, cout, k, k, (s, s), (p, p))
+        sep_w = K._norm_cfg(K.plan_conv("wgrad", *wkey))
+
+        def sep():
+            K.conv_wgrad(x, dy, dw, k, k, (s, s), (p, p), cfg=sep_w)
+            K.conv_dgrad(dy, w, x.shape, k, k, (s, s), (p, p), cfg=sep_d)
+        t_sep = bench(sep, reps=reps)
+        res = []
+        for dc in PAIR_DGRAD:
+            if dc[4] == 0 and K.effective_splits(ntap * (-(-cout // 64) * 64), 64, dc[3]) != dc[3]:
+                continue
+            for wc in PAIR_WGRAD:
+                if K.effective_splits(wkey[2], 64, wc[3]) != wc[3]:
+                    continue
+                if not K.conv_pair_supported(dc, wc):
+                    continue
+                try:
+                    t = bench(lambda: K.conv_bwd(dy, w, x, dw, k, k, (s, s), (p, p), wt=wt, dcfg=dc, wcfg=wc),
+                              reps=reps)
+                except RuntimeError:
+                    continue
+                res.append((t, dc, wc))
+        if not res:
+            continue
+        res.sort()
+        t, dc, wc = res[0]
+        # correctness of the winner vs the separate launches
+        dw.zero_(); ref_x = K.conv_dgrad(dy, w, x.shape, k, k, (s, s), (p, p), cfg=sep_d).float()
+        K.conv_wgrad(x, dy, dw, k, k, (s, s), (p, p), cfg=sep_w); ref_w = dw.clone()
+        dw.zero_(); got_x = K.conv_bwd(dy, w, x, dw, k, k, (s, s), (p, p), wt=wt, dcfg=dc, wcfg=wc).float()
+        err = max(((got_x - ref_x).norm() / (ref_x.norm() + 1e-12)).item(),
+                  ((dw - ref_w).norm() / (ref_w.norm() + 1e-12)).item())
+        entry = {"mode": "pair", "M": dkey[0], "N": dkey[1], "Kd": dkey[2], "wgrad": list(wkey),
+                 "cfg": list(dc), "wcfg": list(wc), "us": round(t, 2), "separate_us": round(t_sep, 2),
+                 "layer": [kind, cin, cout, k, s, p, H, W], "check_rel_err": err}
+        if err < 1e-2:
+            table[key] = entry
+            out.append(entry)
+        print(json.dumps(entry), flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet34")
@@ -98,6 +167,7 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--bert", default=None, help="B,L: tune the BERT-base GEMM shapes instead of a CNN")
     ap.add_argument("--fresh", action="store_true", help="ignore existing entries (re-measure every shape)")
+    ap.add_argument("--pairs", action="store_true", help="tune grouped dgrad+wgrad launches (conv layers)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     if args.bert:
@@ -108,9 +178,15 @@ def main():
     table = {}
     if os.path.exists(args.out) and not args.fresh:
         for e in json.load(open(args.out)).get("entries", []):
-            table[(e["mode"], e["M"], e["N"], e["Kd"])] = e
+            if e["mode"] == "pair":
+                table[("pair", e["M"], e["N"], e["Kd"]) + tuple(e["wgrad"])] = e
+            else:
+                table[(e["mode"], e["M"], e["N"], e["Kd"])] = e
     report = []
     t_start = time.time()
+    if args.pairs:
+        report = tune_pairs(layers, table, args.reps, dev)
+        layers = []
     for (kind, cin, cout, k, s, p, H, W, B) in layers:
         OH, OW = K.out_hw(H, W, k, k, s, s, p, p)
         x = torch.randn(B, H, W, cin, device=dev).to(torch.bfloat16)
@@ -185,7 +261,7 @@ def main():
     with open(args.out, "w") as f:
         json.dump(out, f, indent=1)
     tot = sum(e["us"] for e in report)
-    tdef = sum(e["default_us"] for e in report)
+    tdef = sum(e.get("default_us", e.get("separate_us", 0.0)) for e in report)
     print(json.dumps({"tuned_total_us": round(tot, 1), "default_total_us": round(tdef, 1),
                       "wall_s": round(time.time() - t_start, 1)}))
 
