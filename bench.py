@@ -59,7 +59,7 @@ def main():
 
     from kubeml_amd.engine.step import GraphedTrainStep
     from kubeml_amd.models.resnet import resnet34
-    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.nn import backward_loss, cross_entropy, flatten_module
     from kubeml_amd.ops import kernels as K
     from kubeml_amd.optim import SGD
 
@@ -88,7 +88,7 @@ def main():
         K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True)
         space.zero_grad()
         loss = cross_entropy(model(xbuf), ybuf)
-        loss.backward()
+        backward_loss(loss)
         return loss
 
     def opt_step():

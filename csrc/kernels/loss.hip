@@ -4,7 +4,11 @@
 //           logits, 16 B loads), writes the row's log-sum-exp, loss and whether the
 //           argmax equals the label (the reference's validation "correct" count,
 //           function_resnet34.py:86-89).  Rows whose label == ignore_index contribute 0.
-// reduce  : one block folds per-row results into [mean loss, correct, valid].
+// reduce  : one block folds per-row results into [mean loss, correct, valid] — inside the
+//           forward launch when a ticket counter is given: rows are stored write-through
+//           (sc1), every wave drains, one relaxed agent-scope ticket per block, and the last
+//           block reads all rows with sc1 loads (CDNA guide §6 G16 fan-in, no fences); else as
+//           a second launch.  Fixed summation order either way (deterministic).
 // backward: dlogits = grad_out * (softmax - onehot) / valid, recomputed from the saved
 //           log-sum-exp (no [B, C] probability tensor is kept).
 #include "kml_common.h"
@@ -15,64 +19,95 @@ template <typename T> __device__ __forceinline__ float ldf(const T* p);
 template <> __device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 template <> __device__ __forceinline__ float ldf<float>(const float* p) { return *p; }
 
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// [mean loss, correct, valid] of B rows, by one block of 1024 threads (or fewer) in a fixed order
+template <bool SC1>
+__device__ void ce_fold(const float* __restrict__ rowloss, const float* __restrict__ rowcorrect, float* __restrict__ out,
+                        int B) {
+  float l = 0.f, c = 0.f, v = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const float rc = SC1 ? ld_sc1(rowcorrect + i) : rowcorrect[i];
+    if (rc >= 0.f) { l += SC1 ? ld_sc1(rowloss + i) : rowloss[i]; c += rc; v += 1.f; }
+  }
+  l = wave_sum(l); c = wave_sum(c); v = wave_sum(v);
+  __shared__ float sh[3][16];
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][w] = l; sh[1][w] = c; sh[2][w] = v; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float L = 0, Cc = 0, V = 0;
+    for (int i = 0; i < nw; ++i) { L += sh[0][i]; Cc += sh[1][i]; V += sh[2][i]; }
+    out[0] = V > 0 ? L / V : 0.f;
+    out[1] = Cc;
+    out[2] = V;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_ce_fwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                                                 float* __restrict__ lse, float* __restrict__ rowloss,
-                                                float* __restrict__ rowcorrect, int B, int C, long long ignore) {
+                                                float* __restrict__ rowcorrect, int B, int C, long long ignore,
+                                                unsigned* __restrict__ ticket, float* __restrict__ out3) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
-  const T* x = logits + (long long)row * C;
-  float m = -INFINITY, s = 0.f;
-  int amax = 0;
-  float vmax = -INFINITY;
-  for (int c = lane; c < C; c += 64) {
-    const float v = ldf<T>(x + c);
-    if (v > vmax) { vmax = v; amax = c; }
-    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
-    else s += __expf(v - m);
+  if (row < B) {
+    const T* x = logits + (long long)row * C;
+    float m = -INFINITY, s = 0.f;
+    int amax = 0;
+    float vmax = -INFINITY;
+    for (int c = lane; c < C; c += 64) {
+      const float v = ldf<T>(x + c);
+      if (v > vmax) { vmax = v; amax = c; }
+      if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+      else s += __expf(v - m);
+    }
+    // combine (m, s) across the wave
+  #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
+      const float mn = fmaxf(m, mo);
+      s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+      m = mn;
+      const float vo = __shfl_xor(vmax, o, 64);
+      const int ao = __shfl_xor(amax, o, 64);
+      if (vo > vmax || (vo == vmax && ao < amax)) { vmax = vo; amax = ao; }
+    }
+    if (lane == 0) {
+      const long long y = labels[row];
+      const float l = m + __logf(s);
+      lse[row] = l;
+      const bool skip = (y == ignore || y < 0 || y >= C);
+      const float rl = skip ? 0.f : l - ldf<T>(x + y);
+      const float rc = skip ? -1.f : ((amax == (int)y) ? 1.f : 0.f);
+      if (ticket) { st_sc1(rowloss + row, rl); st_sc1(rowcorrect + row, rc); }
+      else { rowloss[row] = rl; rowcorrect[row] = rc; }
+    }
   }
-  // combine (m, s) across the wave
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
-    const float mn = fmaxf(m, mo);
-    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
-    m = mn;
-    const float vo = __shfl_xor(vmax, o, 64);
-    const int ao = __shfl_xor(amax, o, 64);
-    if (vo > vmax || (vo == vmax && ao < amax)) { vmax = vo; amax = ao; }
+  if (!ticket) return;
+  // in-launch fold: drain the sc1 row stores, one ticket per block, the last block folds
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned last;
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1u : 0u;
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (lane == 0) {
-    const long long y = labels[row];
-    const float l = m + __logf(s);
-    lse[row] = l;
-    if (y == ignore || y < 0 || y >= C) { rowloss[row] = 0.f; rowcorrect[row] = -1.f; }
-    else { rowloss[row] = l - ldf<T>(x + y); rowcorrect[row] = (amax == (int)y) ? 1.f : 0.f; }
-  }
+  __syncthreads();
+  if (last) ce_fold<true>(rowloss, rowcorrect, out3, B);
 }
 
 // out[0] = sum loss / valid, out[1] = correct count, out[2] = valid rows
 __global__ __launch_bounds__(1024) void k_ce_reduce(const float* __restrict__ rowloss,
                                                     const float* __restrict__ rowcorrect, float* __restrict__ out,
                                                     int B) {
-  float l = 0.f, c = 0.f, v = 0.f;
-  for (int i = threadIdx.x; i < B; i += 1024) {
-    const float rc = rowcorrect[i];
-    if (rc >= 0.f) { l += rowloss[i]; c += rc; v += 1.f; }
-  }
-  l = wave_sum(l); c = wave_sum(c); v = wave_sum(v);
-  __shared__ float sh[3][16];
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sh[0][w] = l; sh[1][w] = c; sh[2][w] = v; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float L = 0, Cc = 0, V = 0;
-    for (int i = 0; i < 16; ++i) { L += sh[0][i]; Cc += sh[1][i]; V += sh[2][i]; }
-    out[0] = V > 0 ? L / V : 0.f;
-    out[1] = Cc;
-    out[2] = V;
-  }
+  ce_fold<false>(rowloss, rowcorrect, out, B);
 }
 
 template <typename T>
@@ -98,17 +133,19 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
 
 }  // namespace
 
-// dtype: 0 = bf16 logits, 1 = fp32 logits.  ws = [3*B] fp32 workspace (lse, rowloss, rowcorrect)
+// dtype: 0 = bf16 logits, 1 = fp32 logits.  ws = [3*B] fp32 workspace (lse, rowloss, rowcorrect).
+// ticket: a zeroed device counter (reset by the kernel) -> one launch; null -> fold in a 2nd launch.
 KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, float* out3, int B, int C,
-                       long long ignore, int dtype, hipStream_t s) {
+                       long long ignore, int dtype, unsigned* ticket, hipStream_t s) {
+  if (B < 1) return (int)hipErrorInvalidValue;
   dim3 g((B + 3) / 4);
   if (dtype == 0)
     hipLaunchKernelGGL(k_ce_fwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, ws + B, ws + 2 * B,
-                       B, C, ignore);
+                       B, C, ignore, ticket, out3);
   else
     hipLaunchKernelGGL(k_ce_fwd<float>, g, dim3(256), 0, s, (const float*)logits, labels, ws, ws + B, ws + 2 * B, B,
-                       C, ignore);
-  hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, s, ws + B, ws + 2 * B, out3, B);
+                       C, ignore, ticket, out3);
+  if (!ticket) hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, s, ws + B, ws + 2 * B, out3, B);
   KML_LAUNCH_CHECK();
 }
 

@@ -60,7 +60,8 @@ class StagedForwardBackward:
             h = st(h)
             self._outs[i] = h
         loss = self.loss_fn(h)
-        loss.backward()
+        from ..nn.modules import backward_loss
+        backward_loss(loss)
         return loss
 
     def _segk(self, k: int):

@@ -168,14 +168,17 @@ class _LinearFn(Function):
         if ctx.relu:
             dy = K.relu_bwd(dy, ctx.y)
         dy4 = dy.view(B, 1, 1, op)
-        K.conv_wgrad(ctx.x.view(B, 1, 1, ip), dy4, grad_storage_of(mod.weight).view(op, 1, 1, ip),
-                     1, 1, (1, 1), (0, 0))
-        if ctx.has_bias:
-            K.colsum_(dy, grad_storage_of(mod.bias))
+        x4 = ctx.x.view(B, 1, 1, ip)
+        dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
         dx = None
         if ctx.needs_input_grad[0]:
+            # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
-            dx = K.conv_dgrad(dy4, w, (B, 1, 1, ip), 1, 1, (1, 1), (0, 0)).view(B, ip)
+            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0)).view(B, ip)
+        else:
+            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
+        if ctx.has_bias:
+            K.colsum_(dy, grad_storage_of(mod.bias))
         ctx.x = ctx.y = None
         return dx, None, None, None, None
 
@@ -437,6 +440,22 @@ def cross_entropy(logits, labels, ignore_index=-100, return_correct=False):
         out3, _, _ = K.ce_fwd(logits.contiguous(), labels, ignore_index)
         return out3[0], out3[1]
     return _CEFn.apply(logits.contiguous(), labels, ignore_index)
+
+
+_ONES: dict = {}
+
+
+def backward_loss(loss):
+    """``loss.backward()`` without autograd's seed-gradient fill launch: the seed is a
+    cached device constant, so a captured training step has one kernel less."""
+    if not loss.is_cuda or loss.numel() != 1:
+        loss.backward()
+        return
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones_like(loss)
+    torch.autograd.backward(loss, one)
 
 
 class CrossEntropyLoss(tnn.Module):

@@ -653,8 +653,9 @@ def ce_fwd(logits, labels, ignore_index=-100):
     labels = labels.to(torch.int64).contiguous()
     ws = torch.empty(3 * B, dtype=F32, device=logits.device)
     out3 = torch.empty(3, dtype=F32, device=logits.device)
-    HIP.call("kml_ce_fwd", "p p p p i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), B, C,
-             int(ignore_index), dt, _s())
+    ticket = _COUNTERS.take(logits.device, 1)   # in-launch fold of the per-row results
+    HIP.call("kml_ce_fwd", "p p p p i i l i p s", _p(logits), _p(labels), _p(ws), _p(out3), B, C,
+             int(ignore_index), dt, _p(ticket), _s())
     return out3, ws, labels
 
 

@@ -324,7 +324,7 @@ class KubeModel(ABC):
         """forward + loss + backward + optimizer step for one batch; on the GPU the first
         call for a given batch shape captures a hipGraph that later calls replay.
         Returns the (device) loss tensor."""
-        from ..nn import cross_entropy
+        from ..nn import backward_loss, cross_entropy
         loss_fn = loss_fn or cross_entropy
         key = (tuple(x.shape), tuple(y.shape), x.dtype)
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
@@ -341,7 +341,7 @@ class KubeModel(ABC):
             def fb():
                 self.optimizer.zero_grad()
                 l = loss_fn(self(xs), ys)
-                l.backward()
+                backward_loss(l)
                 return l
             st = GraphedTrainStep(fb, self.optimizer.step, warmup=2)
             st.capture()
