@@ -42,6 +42,8 @@ def main():
                     help="stage-split backward with overlapped all-reduce (auto: on when N>1)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL all-reduce path even with one rank (single-GPU rehearsal of dp>1)")
+    ap.add_argument("--graph-comm", action="store_true",
+                    help="capture the overlapped all-reduces inside the step's hipGraph (one replay per step)")
     args = ap.parse_args()
 
     import torch
@@ -111,7 +113,7 @@ def main():
         seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
     step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
                             bucket_mb=args.bucket_mb, segments=segs, segment_grads=seg_grads,
-                            force_segments=use_seg, force_comm=args.force_comm)
+                            force_segments=use_seg, force_comm=args.force_comm, graph_comm=args.graph_comm)
     step.capture()
     for _ in range(args.warmup):
         loss = step()
@@ -154,7 +156,8 @@ def main():
             "config": {"model": "resnet34 (torchvision, ImageNet stem, 1000-class head)", "global_batch": B * world,
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "all-reduce every step (K=1)",
-                       "graph": not args.no_graph, "overlap_segments": use_seg},
+                       "graph": not args.no_graph, "overlap_segments": use_seg,
+                       "graph_comm": args.graph_comm},
             "epoch_time_s": round(CIFAR_TRAIN / img_s, 3),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }

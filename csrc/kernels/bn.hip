@@ -109,6 +109,28 @@ __global__ __launch_bounds__(TPB) void k_bn_stats_part(const bf16_t* __restrict_
   }
 }
 
+// Rows g0, g0+S, ... < G of one float4 column, summed in that order with 16 loads in
+// flight per thread: the rows were just written by the producing kernel (other XCDs), so
+// every batch of loads is a full memory round trip and the batch depth sets the latency.
+// Loads past the last row re-read row G-1 (clamped, never branched around: a branch per
+// load would serialise the batch) and are selected out of the sum.
+__device__ __forceinline__ float4 sum_rows_strided(const float4* __restrict__ p4, int g0, int G, int S, int Q) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int U = 16;
+  for (int g = g0; g < G; g += U * S) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p4[(long long)min(g + u * S, G - 1) * Q];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool in = g + u * S < G;
+      acc.x += in ? v[u].x : 0.f; acc.y += in ? v[u].y : 0.f;
+      acc.z += in ? v[u].z : 0.f; acc.w += in ? v[u].w : 0.f;
+    }
+  }
+  return acc;
+}
+
 // Sum G rows of a [G][W4*4] fp32 partial matrix into out[W4*4] (LDS), column groups of
 // float4 x row slices with independent loads in flight; scratch: TPB float4 of LDS.
 __device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, float* out, float4* scratch) {
@@ -119,14 +141,7 @@ __device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, f
     const int q = q0 + (int)(threadIdx.x % QT);
     const int sl = threadIdx.x / QT;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < Q && sl < S) {
-      const float4* p4 = reinterpret_cast<const float4*>(part) + q;
-#pragma unroll 8
-      for (int g = sl; g < G; g += S) {
-        const float4 v = p4[(long long)g * Q];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-    }
+    if (q < Q && sl < S) acc = sum_rows_strided(reinterpret_cast<const float4*>(part) + q, sl, G, S, Q);
     scratch[threadIdx.x] = acc;
     __syncthreads();
     if ((int)threadIdx.x < QT && q < Q) {
@@ -152,6 +167,15 @@ __global__ __launch_bounds__(TPB) void k_bn_apply(
   extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], (sums[2C], scratch)
   float* scale = sh;
   float* shift = sh + C;
+  // first iteration's operands in flight while the statistics are summed (the prologue and
+  // this load are two dependent memory round trips otherwise)
+  const long long n8 = M * C / 8;
+  const long long i0 = blockIdx.x * (long long)TPB + threadIdx.x;
+  uint4 x0 = make_uint4(0, 0, 0, 0), r0 = make_uint4(0, 0, 0, 0);
+  if (i0 < n8) {
+    x0 = reinterpret_cast<const uint4*>(x)[i0];
+    if (res) r0 = reinterpret_cast<const uint4*>(res)[i0];
+  }
   const float* st = stats;
   if (mode == 0 && stats_rows > 0) {  // per-wave partial rows written by the conv epilogue
     float* sums = sh + 2 * C;
@@ -181,14 +205,13 @@ __global__ __launch_bounds__(TPB) void k_bn_apply(
     }
   }
   __syncthreads();
-  const long long n8 = M * C / 8;
   const int CH = C / 8;
-  for (long long i = blockIdx.x * (long long)TPB + threadIdx.x; i < n8; i += (long long)gridDim.x * TPB) {
+  for (long long i = i0; i < n8; i += (long long)gridDim.x * TPB) {
     const int c0 = (int)(i % CH) * 8;
     float f[8];
-    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+    unpack8(i == i0 ? x0 : reinterpret_cast<const uint4*>(x)[i], f);
     float r[8];
-    if (res) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+    if (res) unpack8(i == i0 ? r0 : reinterpret_cast<const uint4*>(res)[i], r);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = f[k] * scale[c0 + k] + shift[c0 + k];
@@ -437,6 +460,15 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
   float* mu = ka + 3 * C;
   float* rs = ka + 4 * C;
   const float invM = 1.f / (float)M;
+  // first iteration's operands in flight while the partial rows are summed
+  const long long n8 = M * C / 8;
+  const long long i0 = blockIdx.x * (long long)TPB + threadIdx.x;
+  uint4 dy0 = make_uint4(0, 0, 0, 0), x0 = dy0, y0 = dy0;
+  if (i0 < n8) {
+    dy0 = reinterpret_cast<const uint4*>(dy)[i0];
+    x0 = reinterpret_cast<const uint4*>(x)[i0];
+    if (y) y0 = reinterpret_cast<const uint4*>(y)[i0];
+  }
   // sum the G partial rows of 2C floats: float4 column groups x row slices (several
   // independent loads in flight per thread), slices combined through LDS
   const int Q = C / 2;                         // float4 groups per partial row
@@ -446,14 +478,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
     const int q = q0 + (int)(threadIdx.x % QT);
     const int sl = threadIdx.x / QT;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < Q) {
-      const float4* p4 = reinterpret_cast<const float4*>(part) + q;
-#pragma unroll 8
-      for (int g = sl; g < G; g += S) {
-        const float4 v = p4[(long long)g * Q];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-    }
+    if (q < Q) acc = sum_rows_strided(reinterpret_cast<const float4*>(part) + q, sl, G, S, Q);
     red4[threadIdx.x] = acc;
     __syncthreads();
     if ((int)threadIdx.x < QT && q < Q) {
@@ -483,16 +508,15 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
     rs[c] = rstd[c];
   }
   __syncthreads();
-  const long long n8 = M * C / 8;
   const int CH = C / 8;
-  for (long long i = blockIdx.x * (long long)TPB + threadIdx.x; i < n8; i += (long long)gridDim.x * TPB) {
+  for (long long i = i0; i < n8; i += (long long)gridDim.x * TPB) {
     const int c0 = (int)(i % CH) * 8;
     float d[8], xv[8];
-    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
-    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    unpack8(i == i0 ? dy0 : reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(i == i0 ? x0 : reinterpret_cast<const uint4*>(x)[i], xv);
     if (y) {
       float yv[8];
-      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+      unpack8(i == i0 ? y0 : reinterpret_cast<const uint4*>(y)[i], yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
     }

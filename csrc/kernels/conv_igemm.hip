@@ -424,7 +424,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     }
 
     // ---------------------------------------------------------- FWD / DGRAD epilogue
+    // (entered after a block barrier: the main loops end with one, so LDS is free here)
+    // tile geometry: 2x2 waves (SINGLE: one live wave owns the whole tile)
+    constexpr int BMT = SINGLE ? WM : 2 * WM, BNT = SINGLE ? WN : 2 * WN;
+    // Large tiles stage the bf16 output through LDS (past the 16-byte split-K flag word) and
+    // write it back as 16-byte row chunks instead of one 2-byte store per element.
+    constexpr bool STAGE_OK = !SINGLE && BMT * BNT >= 8192;
+    constexpr int LDO = BNT + 8;  // padded LDS row (bf16 elements)
+    constexpr int RED_OFF = 16 + (STAGE_OK ? BMT * LDO * 2 : 0);
+    const bool stage = STAGE_OK && flag != nullptr && (a.N % 8) == 0;
+    bf16_t* sout = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(flag) + 16);
+    float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(flag) + RED_OFF);  // [2][BNT]
+    // Per-channel partial rows for the BN kernel (FWD statistics / consumer-BN partials of a
+    // DGRAD), ONE row per M-tile: the two wave row-bands of a tile are summed through LDS, so
+    // the BN kernel (every block of which reads all rows) reads half as many.
+    float* rows = (MODE == DGRAD) ? a.bnf_part : ((a.stats && a.stats_part) ? a.stats : nullptr);
+    const bool sc1_rows = a.grp_out != nullptr;
+    const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
     const int ldc = a.N;
+    float k1[NR], k2[NR];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int col = n0 + wn * WN + j * 16 + fr;
@@ -442,7 +460,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
             if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
             if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
             const bf16_t vb = f2bf(v);
-            a.out[(long long)row * ldc + col] = vb;
+            if (stage) sout[(row - m0) * LDO + (col - n0)] = vb;
+            else a.out[(long long)row * ldc + col] = vb;
             if (MODE == DGRAD && a.bnf_part) {  // consumer BN's dbeta / dgamma partials
               const long long idx = (long long)row * ldc + col;
               float dz = bf2f(vb);
@@ -456,37 +475,51 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
             }
           }
         }
-      if (MODE == DGRAD && a.bnf_part) {
+      if ((MODE == DGRAD && a.bnf_part) || (MODE == FWD && a.stats)) {
         s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
         s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
+      }
+      k1[j] = s1;
+      k2[j] = s2;
+      if (MODE == FWD && a.stats && !a.stats_part) {
         if (fq == 0 && cok) {
-          float* prow = a.bnf_part + (long long)(m0 / WM + wm) * 2 * a.N;
-          store_row(prow + col, s1, a.grp_out != nullptr);
-          store_row(prow + a.N + col, s2, a.grp_out != nullptr);
+          atomicAdd(a.stats + col, s1);
+          atomicAdd(a.stats + a.N + col, s2);
+        }
+      } else if (rows != nullptr && fq == 0 && cok) {
+        if (SINGLE) {
+          store_row(rows + rrow + col, s1, sc1_rows);
+          store_row(rows + rrow + a.N + col, s2, sc1_rows);
+        } else if (wm == 1) {
+          red[col - n0] = s1;
+          red[BNT + col - n0] = s2;
         }
       }
-      if (MODE == FWD && a.stats) {
-        s1 += __shfl_xor(s1, 16, 64); s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64); s2 += __shfl_xor(s2, 32, 64);
-        if (fq == 0 && cok) {
-          if (a.stats_part) {
-            float* prow = a.stats + (long long)(m0 / WM + wm) * 2 * a.N;
-            store_row(prow + col, s1, a.grp_out != nullptr);
-            store_row(prow + a.N + col, s2, a.grp_out != nullptr);
-          } else {
-            atomicAdd(a.stats + col, s1);
-            atomicAdd(a.stats + a.N + col, s2);
+    }
+    if constexpr (!SINGLE) {
+      if (stage || rows != nullptr) __syncthreads();
+      if (rows != nullptr && wm == 0 && fq == 0) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const int col = n0 + wn * WN + j * 16 + fr;
+          if (col < a.N) {
+            store_row(rows + rrow + col, k1[j] + red[col - n0], sc1_rows);
+            store_row(rows + rrow + a.N + col, k2[j] + red[BNT + col - n0], sc1_rows);
           }
         }
       }
+      if (stage) {
+        constexpr int CPR = BNT / 8;  // 16-byte chunks per tile row
+        for (int q = tid; q < BMT * CPR; q += 256) {
+          const int r = q / CPR, c8 = (q - r * CPR) * 8;
+          const int row = m0 + r, col = n0 + c8;
+          if (row < a.M && col < a.N)
+            *reinterpret_cast<uint4*>(a.out + (long long)row * ldc + col) =
+                *reinterpret_cast<const uint4*>(sout + r * LDO + c8);
+        }
+      }
     }
-    if (a.grp_out) {
-      constexpr int BMT = SINGLE ? WM : 2 * WM, BNT = SINGLE ? WN : 2 * WN, RPT = SINGLE ? 1 : 2;
-      if (MODE == FWD && a.stats && a.stats_part)
-        group_reduce_rows<BMT, BNT, RPT, SINGLE>(a, a.stats, m0, n0, tid, flag);
-      else if (MODE == DGRAD && a.bnf_part)
-        group_reduce_rows<BMT, BNT, RPT, SINGLE>(a, a.bnf_part, m0, n0, tid, flag);
-    }
+    if (a.grp_out && rows != nullptr) group_reduce_rows<BMT, BNT, 1, SINGLE>(a, rows, m0, n0, tid, flag);
   }
 }
 
@@ -499,6 +532,9 @@ struct IgemmBody {
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;
   static constexpr int THREADS = 256;
   static constexpr int SMEM = 2 * STAGE * (int)sizeof(bf16_t);
+  static_assert(MODE == WGRAD || SMEM >= 16 + 8 * BN, "epilogue BN-row scratch must fit the LDS");
+  static_assert(MODE == WGRAD || BM * BN < 8192 || SMEM >= 16 + BM * (BN + 8) * 2 + 8 * BN,
+                "epilogue output staging must fit the LDS");
   __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem_raw);
 };
 
@@ -682,6 +718,8 @@ struct GldsBody {
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int THREADS = 256;
   static constexpr int SMEM = S * STAGE;
+  static_assert(MODE == WGRAD || BM * BN < 8192 || SMEM >= 16 + BM * (BN + 8) * 2 + 8 * BN,
+                "epilogue output staging must fit the LDS");
   __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem);
 };
 
@@ -789,11 +827,30 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
                                       reinterpret_cast<unsigned*>(smem));
 }
 
+// XCD-aware tile order (CDNA guide T1): blocks b and b+8 share an XCD (round-robin
+// dispatch), so hand each XCD a contiguous run of tiles, N-tiles fastest: neighbouring
+// tiles share their A panel (and the B panels of a row of tiles) in that XCD's L2.
+// Bijective for any grid (nwg % 8 != 0 included).
+__device__ __forceinline__ Blk xcd_blk() {
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+  const int nwg = gx * gy * (int)gridDim.z;
+  const int lin = ((int)blockIdx.z * gy + (int)blockIdx.y) * gx + (int)blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, x = lin & 7, k = lin >> 3;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  Blk b;
+  b.gx = gx;
+  b.x = id % gx;
+  const int t = id / gx;
+  b.y = t % gy;
+  b.z = t / gy;
+  return b;
+}
+
 template <int MODE, int BM, int BN, int S, bool TAPU>
 __global__ __launch_bounds__(256) void k_conv_glds(ConvArgs a) {
   using Body = GldsBody<MODE, BM, BN, S, TAPU>;
   __shared__ __attribute__((aligned(1024))) char smem[Body::SMEM];
-  Body::run(a, hw_blk(), smem);
+  Body::run(a, xcd_blk(), smem);
 }
 
 template <int MODE, int BM, int BN, int S>
@@ -986,6 +1043,10 @@ int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t
   KML_T(32, 32) KML_T(32, 64) KML_T(64, 32) KML_T(64, 64)
   KML_T(64, 128) KML_T(128, 64) KML_T(128, 128) KML_T(32, 128) KML_T(128, 32)
 #undef KML_T
+  // 256-wide tiles: LDS-DMA pipeline only (3 stages x 48 KB; each of the 4 waves owns 128x64
+  // or 64x128, 96 B/clk of fragment reads per CU instead of the 64x64 waves' 128)
+  if (variant == 1 && bm == 256 && bn == 128) return launch_glds<MODE, 256, 128, 3>(a, s);
+  if (variant == 1 && bm == 128 && bn == 256) return launch_glds<MODE, 128, 256, 3>(a, s);
   return (int)hipErrorInvalidValue;
 }
 
@@ -1207,7 +1268,7 @@ KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
   return set_splits(a, bk, splits);
 }
 
-// stats_part = 1: stats is [G][2K] with G = ceil(M / WM) (WM = bm for variant 3, bm/2 otherwise);
+// stats_part = 1: stats is [G][2K] with G = ceil(M / bm), one row per M-tile;
 // every row is written (no zeroing needed) and bn_apply sums the rows.
 // grp_out / grp_cnt / grp_tiles: optional group reduction of the stats_part rows (ConvArgs).
 KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int stats_part,

@@ -38,19 +38,24 @@ class GraphedTrainStep:
     Each segment is its own graph (shared pool); after replaying segment ``k`` the
     all-reduce of its gradients is issued asynchronously (RCCL on the process group's
     stream, ordered after the replay by an event) and the next segment's replay runs
-    concurrently.  Collectives are never captured, so the multi-GPU path only uses
-    plain, eagerly-issued RCCL calls.
+    concurrently.  By default collectives are not captured: the multi-GPU path uses
+    plain, eagerly-issued RCCL calls.  ``graph_comm=True`` instead captures the whole
+    step, segments' all-reduces included (RCCL kernels on the process group's stream,
+    forked from and joined back into the capture stream), into ONE graph: one replay
+    per step, no host gaps between the segments.
     """
 
     def __init__(self, fwd_bwd: Callable[[], torch.Tensor], opt_step: Callable[[], None], grad_buffers=(),
                  group=None, use_graph: bool = True, warmup: int = 3, bucket_mb: float = 0.0,
-                 segments=None, segment_grads=None, force_segments: bool = False, force_comm: bool = False):
+                 segments=None, segment_grads=None, force_segments: bool = False, force_comm: bool = False,
+                 graph_comm: bool = False):
         self.fwd_bwd = fwd_bwd
         self.opt_step = opt_step
         self.grad_buffers = list(grad_buffers)
         self.segments = list(segments) if segments else None
         self.segment_grads = [list(g) for g in segment_grads] if segment_grads else None
         self.force_segments = force_segments
+        self.graph_comm = graph_comm
         self.g_seg = []
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -126,7 +131,20 @@ class GraphedTrainStep:
         # capture; "thread_local" keeps its (uncaptured) queries from invalidating the
         # capture.  Nothing on this thread makes an unsafe call inside a capture.
         mode = "thread_local" if self.comm else "global"
-        if self._segmented():
+        if self._segmented() and self.graph_comm and self.comm:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode=mode):
+                works = []
+                for k, seg in enumerate(self.segments):
+                    out = self._run(seg)
+                    if k == 0:
+                        self.loss = out
+                    works += self._issue(k)
+                for w in works:
+                    w.wait()
+                self.opt_step()
+            self.g_a, self.g_b, self.g_seg = g, None, []
+        elif self._segmented():
             pool = torch.cuda.graph_pool_handle()
             self.g_seg = []
             for k, seg in enumerate(self.segments):

@@ -13,6 +13,7 @@ kernels directly into ``p.grad`` storage (``+=``), matching torch's semantics.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as tnn
@@ -32,6 +33,20 @@ def _round8(c):
 
 def _on_gpu(x):
     return x.is_cuda
+
+
+# Plain large linears (BERT: M = batch x seq tokens, no fused activation) run their forward
+# and input-gradient GEMMs on hipBLASLt (torch.mm / addmm, bias in its epilogue): at
+# M = 8192, K, N = 768-3072 it measured 1.7-2x the MFMA implicit-GEMM kernel
+# (tools/gemm_micro.py).  The fp32 weight-gradient accumulation, fused-ReLU heads, small-M
+# layers and every convolution stay on the HIP kernels.  KUBEML_LINEAR_BLAS=0/1 forces a side.
+_LIN_BLAS = os.environ.get("KUBEML_LINEAR_BLAS", "auto")
+
+
+def _linear_blas(M, ip, op, relu):
+    if relu or _LIN_BLAS == "0":
+        return False
+    return _LIN_BLAS == "1" or (M >= 4096 and ip >= 512 and op >= 512)
 
 
 class _PadChannelsFn(Function):
@@ -144,10 +159,15 @@ class _LinearFn(Function):
     def forward(ctx, x2, weight, bias, mod, relu):
         from ..ops import kernels as K
         op, ip = mod.out_pad, mod.in_pad
-        w = shadow_of(weight).view(op, 1, 1, ip)
         B = x2.shape[0]
-        bias_st = None if bias is None else master_of(bias)
-        y = K.conv_fwd(x2.view(B, 1, 1, ip), w, 1, 1, (1, 1), (0, 0), bias=bias_st, relu=relu).view(B, op)
+        ctx.blas = _linear_blas(B, ip, op, relu)
+        if ctx.blas:  # plain GEMM, bias in hipBLASLt's epilogue
+            w2 = shadow_of(weight).view(op, ip)
+            y = torch.mm(x2, w2.t()) if bias is None else torch.addmm(shadow_of(bias), x2, w2.t())
+        else:
+            w = shadow_of(weight).view(op, 1, 1, ip)
+            bias_st = None if bias is None else master_of(bias)
+            y = K.conv_fwd(x2.view(B, 1, 1, ip), w, 1, 1, (1, 1), (0, 0), bias=bias_st, relu=relu).view(B, op)
         ctx.mod, ctx.x, ctx.has_bias, ctx.relu = mod, x2, bias is not None, relu
         ctx.y = y if relu else None
         if op != mod.out_features:
@@ -171,7 +191,11 @@ class _LinearFn(Function):
         x4 = ctx.x.view(B, 1, 1, ip)
         dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.blas:
+            if ctx.needs_input_grad[0]:
+                dx = torch.mm(dy, shadow_of(mod.weight).view(op, ip))
+            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
+        elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
             dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0)).view(B, ip)

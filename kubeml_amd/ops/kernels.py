@@ -193,10 +193,10 @@ _GRP_ROWS = 16
 
 def _stats_layout(M, cfg):
     """(per-wave rows G, M-tiles per group or 0, rows the consumer reads)."""
-    bm, _, _, _, variant = _norm_cfg(cfg)
+    bm = _norm_cfg(cfg)[0]
     tiles = _cdiv(M, bm)
-    # one row per wave row-band of every M tile (tail tiles included: their waves write zeros)
-    G = tiles * (1 if variant == DIRECT else 2)
+    # one row per M tile (the epilogue sums the tile's wave row-bands; tail tiles included)
+    G = tiles
     if _GRP_MIN <= 0 or G <= _GRP_MIN:
         return G, 0, G
     tpg = _cdiv(tiles, _GRP_ROWS)
@@ -205,7 +205,7 @@ def _stats_layout(M, cfg):
 
 def conv_stats_rows(M, cfg):
     """Rows of the partial-statistics buffer a conv epilogue hands to the BN kernel for a
-    plan: one per wave row band, or one per M-tile group when group-reduced."""
+    plan: one per M-tile, or one per M-tile group when group-reduced."""
     return _stats_layout(M, cfg)[2]
 
 

@@ -181,3 +181,12 @@ def test_resume_from_checkpoint(env):
     assert h2.train_loss[1] < h1.train_loss[0]                                 # continued, not restarted
     assert h2.epoch_duration == sorted(h2.epoch_duration)
     assert "resuming" in c.logs(j2).decode()
+
+
+def test_role_clients(env):
+    """Internal role clients (reference ml/pkg/ps/client, ml/pkg/train/client) against the
+    running server's parameter-server role."""
+    from kubeml_amd.control.clients import JobClient, PSClient
+    srv, c, _ = env
+    assert isinstance(PSClient(srv.url("ps")).list_tasks(), list)
+    assert JobClient("http://127.0.0.1:9").health() is False

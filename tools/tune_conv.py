@@ -20,7 +20,8 @@ import torch
 
 from kubeml_amd.ops import kernels as K
 
-TILES = [(32, 32), (32, 64), (64, 32), (64, 64), (64, 128), (128, 64), (128, 128), (32, 128), (128, 32)]
+TILES = [(32, 32), (32, 64), (64, 32), (64, 64), (64, 128), (128, 64), (128, 128), (32, 128), (128, 32),
+         (256, 128), (128, 256)]  # the 256-wide tiles exist for the LDS-DMA variant only
 
 
 def conv_layers(model_name, B, H=32, W=32, in_ch=3):
@@ -168,13 +169,14 @@ def main():
     ap.add_argument("--bert", default=None, help="B,L: tune the BERT-base GEMM shapes instead of a CNN")
     ap.add_argument("--fresh", action="store_true", help="ignore existing entries (re-measure every shape)")
     ap.add_argument("--pairs", action="store_true", help="tune grouped dgrad+wgrad launches (conv layers)")
+    ap.add_argument("--size", type=int, default=32, help="input image size of the CNN (224 for ImageNet shapes)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     if args.bert:
         Bb, Lb = (int(v) for v in args.bert.split(","))
         layers = bert_linears(Bb, Lb)
     else:
-        layers = [l + (args.batch,) for l in conv_layers(args.model, args.batch)]
+        layers = [l + (args.batch,) for l in conv_layers(args.model, args.batch, H=args.size, W=args.size)]
     table = {}
     if os.path.exists(args.out) and not args.fresh:
         for e in json.load(open(args.out)).get("entries", []):
