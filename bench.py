@@ -42,8 +42,9 @@ def main():
                     help="stage-split backward with overlapped all-reduce (auto: on when N>1)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL all-reduce path even with one rank (single-GPU rehearsal of dp>1)")
-    ap.add_argument("--graph-comm", action="store_true",
-                    help="capture the overlapped all-reduces inside the step's hipGraph (one replay per step)")
+    ap.add_argument("--graph-comm", choices=["auto", "on", "off"], default="auto",
+                    help="capture the overlapped all-reduces inside the step's hipGraph, one replay per step "
+                         "(auto: on when N>1; KUBEML_GRAPH_COMM=0 forces off)")
     args = ap.parse_args()
 
     import torch
@@ -98,6 +99,8 @@ def main():
         K.advance_counter_(ctr, B, n_local)
 
     use_seg = args.segments == "on" or (args.segments == "auto" and comm)
+    graph_comm = use_seg and comm and os.environ.get("KUBEML_GRAPH_COMM", "1") != "0" and (
+        args.graph_comm == "on" or (args.graph_comm == "auto" and world > 1))
     segs = seg_grads = None
     if use_seg:
         # backward in 3 graph segments; each segment's gradients are all-reduced on the
@@ -113,7 +116,7 @@ def main():
         seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
     step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
                             bucket_mb=args.bucket_mb, segments=segs, segment_grads=seg_grads,
-                            force_segments=use_seg, force_comm=args.force_comm, graph_comm=args.graph_comm)
+                            force_segments=use_seg, force_comm=args.force_comm, graph_comm=graph_comm)
     step.capture()
     for _ in range(args.warmup):
         loss = step()
@@ -133,6 +136,15 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     last_loss = float(loss.item())
+    in_sync = None
+    if comm:
+        # every rank must hold identical weights after K all-reduced steps (checks that the
+        # graph-replayed collectives really ran)
+        cs = space.master.double().abs().sum().view(1)
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        in_sync = bool((hi - lo).abs().item() <= 1e-9 * max(1.0, abs(hi.item())))
     if comm:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -157,10 +169,12 @@ def main():
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "all-reduce every step (K=1)",
                        "graph": not args.no_graph, "overlap_segments": use_seg,
-                       "graph_comm": args.graph_comm},
+                       "graph_comm": graph_comm},
             "epoch_time_s": round(CIFAR_TRAIN / img_s, 3),
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
+        if in_sync is not None:
+            out["ranks_in_sync"] = in_sync
         print(json.dumps(out), flush=True)
     if comm:
         dist.destroy_process_group()

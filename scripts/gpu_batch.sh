@@ -14,9 +14,9 @@ timeout -k 10 200 python bench.py --steps 200 --warmup 10 > $out/bench.json 2> $
 cat $out/bench.json
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --segments on > $out/bench_seg.json 2>> $out/bench.err || exit 1
 cat $out/bench_seg.json
-timeout -k 10 200 python bench.py --steps 100 --warmup 10 --force-comm > $out/bench_fc.json 2>> $out/bench.err || exit 1
+timeout -k 10 200 python bench.py --steps 100 --warmup 10 --force-comm --graph-comm off > $out/bench_fc.json 2>> $out/bench.err || exit 1
 cat $out/bench_fc.json
-timeout -k 10 200 python bench.py --steps 100 --warmup 10 --force-comm --graph-comm > $out/bench_gc.json 2>> $out/bench.err || exit 1
+timeout -k 10 200 python bench.py --steps 100 --warmup 10 --force-comm --graph-comm on > $out/bench_gc.json 2>> $out/bench.err || exit 1
 cat $out/bench_gc.json
 echo "[gpu_batch] profile"
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
