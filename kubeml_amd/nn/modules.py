@@ -46,7 +46,55 @@ _LIN_BLAS = os.environ.get("KUBEML_LINEAR_BLAS", "auto")
 def _linear_blas(M, ip, op, relu):
     if relu or _LIN_BLAS == "0":
         return False
-    return _LIN_BLAS == "1" or (M >= 4096 and ip >= 512 and op >= 512)
+    return _LIN_BLAS == "1" or (M >= 2048 and ip >= 512 and op >= 512)
+
+
+# Weight gradient of those linears: hipBLASLt bf16 x bf16 -> fp32 with beta = 1 straight into
+# the fp32 gradient storage (aten addmm.dtype_out).  The BERT profile had the MFMA wgrad
+# kernel at 242 us per [16384] x [3072 x 768] GEMM (32% of the step).  Falls back to the
+# HIP wgrad kernel once, for good, if this torch build cannot run that op.
+_WGRAD_BLAS = [os.environ.get("KUBEML_LINEAR_BLAS_WGRAD", "1") != "0"]
+
+
+_WGRAD_SPLIT = int(os.environ.get("KUBEML_WGRAD_SPLIT", "0"))  # 0 = auto
+
+
+def _wgrad_splits(M, op, ip):
+    """Split-K factor for the weight-gradient GEMM: its output ([op, ip], e.g. 3072 x 768 =
+    144 tiles of 128x128) is far too small to fill 256 CUs while its reduction (M = tokens)
+    is long, so slice M into S batched GEMMs (>= ~576 tiles in flight) and sum the S fp32
+    slabs.  hipBLASLt picked no split-K itself: 190 us (405 TF/s) per BERT FFN wgrad."""
+    if _WGRAD_SPLIT > 0:
+        S = _WGRAD_SPLIT
+    else:
+        # power of two >= 576 / tiles, at most 16 (tools/wgrad_split.py on the BERT shapes:
+        # 3072x768 best at S=4, 2304x768 at 8, 768x768 at 16)
+        tiles = max(1, -(-op // 128) * -(-ip // 128))
+        S = 1
+        while S < 16 and S * tiles < 576:
+            S *= 2
+    while S > 1 and (M % S or M // S < 256):
+        S -= 1
+    return S
+
+
+def _blas_wgrad_(dw, dy, x):
+    """dw[op, ip] (fp32) += dy[M, op]^T @ x[M, ip] (bf16); False if unsupported."""
+    if not _WGRAD_BLAS[0]:
+        return False
+    try:
+        M, op, ip = dy.shape[0], dy.shape[1], x.shape[1]
+        S = _wgrad_splits(M, op, ip)
+        if S == 1:
+            torch.addmm(dw, dy.t(), x, out_dtype=torch.float32, out=dw)
+        else:
+            part = torch.bmm(dy.view(S, M // S, op).transpose(1, 2), x.view(S, M // S, ip),
+                             out_dtype=torch.float32)
+            dw.add_(part.sum(0))
+        return True
+    except (RuntimeError, TypeError, NotImplementedError):
+        _WGRAD_BLAS[0] = False
+        return False
 
 
 class _PadChannelsFn(Function):
@@ -194,7 +242,8 @@ class _LinearFn(Function):
         if ctx.blas:
             if ctx.needs_input_grad[0]:
                 dx = torch.mm(dy, shadow_of(mod.weight).view(op, ip))
-            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
+            if not _blas_wgrad_(dw4.view(op, ip), dy, ctx.x):
+                K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)

@@ -526,8 +526,9 @@ def test_conv_large_tiles(cfg, shape):
 
 @pytest.mark.parametrize("blas", ["0", "1"])
 def test_linear_paths_match_torch(blas, monkeypatch):
-    """Linear on the MFMA kernel (KUBEML_LINEAR_BLAS=0) and on hipBLASLt for the forward /
-    input-gradient GEMMs (=1; fp32 weight gradient still from the HIP wgrad kernel)."""
+    """Linear on the MFMA kernel (KUBEML_LINEAR_BLAS=0) and on hipBLASLt (=1: forward,
+    input gradient, and the weight gradient as a bf16 -> fp32 beta=1 GEMM accumulating into
+    the fp32 gradient storage — checked by a second backward doubling the gradient)."""
     from kubeml_amd.nn import flatten_module
     from kubeml_amd.nn import modules as Mo
     monkeypatch.setattr(Mo, "_LIN_BLAS", blas)
@@ -547,3 +548,7 @@ def test_linear_paths_match_torch(blas, monkeypatch):
     assert _rel(x.grad.float(), xr.grad) < 1e-2
     assert _rel(lin.weight.grad, ref.weight.grad) < 1e-2
     assert _rel(lin.bias.grad, ref.bias.grad) < 1e-2
+    if blas == "1":
+        assert Mo._WGRAD_BLAS[0], "hipBLASLt fp32-out weight-gradient GEMM unavailable"
+    lin(x.detach()).backward(g)
+    assert _rel(lin.weight.grad, 2 * ref.weight.grad) < 1e-2
