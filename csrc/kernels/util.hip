@@ -88,7 +88,83 @@ __global__ __launch_bounds__(256) void k_colsum_bf16(const bf16_t* __restrict__ 
   }
 }
 
+// Vectorised form for C % 8 == 0: 64 lanes x 8 columns (one 16-byte load each) per row,
+// the block's 4 waves on interleaved rows of its row slab, 8 independent loads in flight per
+// lane, waves combined in LDS, one atomic per column per block.  The scalar kernel above
+// issued one 2-byte load per lane per row (33 us avg per BERT bias gradient).
+__global__ __launch_bounds__(256) void k_colsum8_bf16(const bf16_t* __restrict__ x, float* __restrict__ out,
+                                                      long long M, int C, int rows_per_block) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * 8;
+  const long long r0 = (long long)blockIdx.y * rows_per_block;
+  const long long r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+    constexpr int U = 8;
+    for (long long r = r0 + w; r < r1; r += 4 * U) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long rr = min(r + 4LL * u, r1 - 1);  // clamped re-read, selected out below
+        v[u] = *reinterpret_cast<const uint4*>(x + rr * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + 4LL * u >= r1) break;
+        const unsigned* q = reinterpret_cast<const unsigned*>(&v[u]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += __uint_as_float(q[k] << 16);
+          acc[2 * k + 1] += __uint_as_float(q[k] & 0xffff0000u);
+        }
+      }
+    }
+  }
+  __shared__ float red[4][64 * 8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[w][lane * 8 + k] = acc[k];
+  __syncthreads();
+  // atomics on consecutive columns per lane (4 cache lines per wave instruction, not 32)
+  const int cb = blockIdx.x * 512;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = h * 256 + threadIdx.x;
+    if (cb + j < C) atomicAdd(out + cb + j, red[0][j] + red[1][j] + red[2][j] + red[3][j]);
+  }
+}
+
+// dst[i] += sum_s part[s][i]  (fp32, n % 4 == 0): the split-K slabs of a weight-gradient GEMM
+// folded into the gradient storage in one pass, slabs summed in order (deterministic).
+__global__ __launch_bounds__(256) void k_slab_sum_add(const float4* __restrict__ part, float4* __restrict__ dst,
+                                                      long long n4, int S) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 a = dst[i];
+    for (int k = 0; k < S; ++k) {
+      const float4 v = part[(long long)k * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    dst[i] = a;
+  }
+}
+
+KML_API int kml_slab_sum_add(const float* part, float* dst, long long n, int S, hipStream_t s) {
+  if (n % 4 || S < 1) return (int)hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_slab_sum_add, dim3(kml_stream_grid(n4, 256)), dim3(256), 0, s, (const float4*)part,
+                     (float4*)dst, n4, S);
+  KML_LAUNCH_CHECK();
+}
+
 KML_API int kml_colsum_bf16(const bf16_t* x, float* out, long long M, int C, hipStream_t s) {
+  if (C % 8 == 0 && M >= 256 && ((uintptr_t)x & 15) == 0) {
+    const int rpb = 128;
+    const long long gy = (M + rpb - 1) / rpb;
+    if (gy <= 65535) {
+      dim3 grid((C / 8 + 63) / 64, (unsigned)gy);
+      hipLaunchKernelGGL(k_colsum8_bf16, grid, dim3(256), 0, s, x, out, M, C, rpb);
+      KML_LAUNCH_CHECK();
+    }
+  }
   int rpb = 64;
   long long gy = (M + rpb - 1) / rpb;
   if (gy > 65535) { rpb = (int)((M + 65534) / 65535); gy = (M + rpb - 1) / rpb; }

@@ -90,7 +90,8 @@ def _blas_wgrad_(dw, dy, x):
         else:
             part = torch.bmm(dy.view(S, M // S, op).transpose(1, 2), x.view(S, M // S, ip),
                              out_dtype=torch.float32)
-            dw.add_(part.sum(0))
+            from ..ops import kernels as K
+            K.slab_sum_add_(part, dw)
         return True
     except (RuntimeError, TypeError, NotImplementedError):
         _WGRAD_BLAS[0] = False

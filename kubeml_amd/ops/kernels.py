@@ -732,6 +732,17 @@ def colsum_(x2d, out):
     return out
 
 
+def slab_sum_add_(part, dst):
+    """dst (fp32) += part.sum(0) for part [S, *dst.shape] fp32, one pass, slabs in order."""
+    _chk(part, F32, "part")
+    _chk(dst, F32, "dst")
+    n = dst.numel()
+    if part.numel() != part.shape[0] * n or n % 4:
+        raise ValueError(f"slab_sum_add_: part {tuple(part.shape)} vs dst {tuple(dst.shape)}")
+    HIP.call("kml_slab_sum_add", "p p l i s", _p(part), _p(dst), n, part.shape[0], _s())
+    return dst
+
+
 def add_i64_(t, v=1):
     HIP.call("kml_add_i64", "p l i s", _p(t), int(v), t.numel(), _s())
 

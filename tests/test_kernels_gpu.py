@@ -552,3 +552,21 @@ def test_linear_paths_match_torch(blas, monkeypatch):
         assert Mo._WGRAD_BLAS[0], "hipBLASLt fp32-out weight-gradient GEMM unavailable"
     lin(x.detach()).backward(g)
     assert _rel(lin.weight.grad, 2 * ref.weight.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,C", [(16384, 3072), (1000, 768), (300, 36), (100, 1000)])
+def test_colsum_and_slab_sum(M, C):
+    """Bias-gradient column sums (16-byte vectorised kernel when C % 8 == 0 and M >= 256,
+    scalar otherwise; both accumulate) and the split-K slab fold dst += sum_s part[s]."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(5)
+    x = _bf(torch.randn(M, C, device=dev))
+    out = torch.ones(C, device=dev)
+    K.colsum_(x, out)
+    ref = x.float().sum(0) + 1
+    assert (out - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item()) + 1e-2
+    part = torch.randn(4, C, 8, device=dev)
+    dst = torch.randn(C, 8, device=dev)
+    want = dst + part.sum(0)
+    K.slab_sum_add_(part, dst)
+    assert torch.allclose(dst, want, atol=1e-5)
