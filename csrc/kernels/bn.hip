@@ -133,10 +133,11 @@ __device__ __forceinline__ float4 sum_rows_strided(const float4* __restrict__ p4
 
 // Sum G rows of a [G][W4*4] fp32 partial matrix into out[W4*4] (LDS), column groups of
 // float4 x row slices with independent loads in flight; scratch: TPB float4 of LDS.
+template <int NT>
 __device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, float* out, float4* scratch) {
   const int Q = W / 4;
-  const int QT = Q < TPB ? Q : TPB;
-  const int S = TPB / QT;
+  const int QT = Q < NT ? Q : NT;
+  const int S = NT / QT;
   for (int q0 = 0; q0 < Q; q0 += QT) {
     const int q = q0 + (int)(threadIdx.x % QT);
     const int sl = threadIdx.x / QT;
@@ -158,7 +159,8 @@ __device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, f
 
 // y = act((x - mean) * rstd * gamma + beta [+ res])
 // mode 0: training (stats = [sum, sumsq] over M rows); mode 1: eval (running stats)
-__global__ __launch_bounds__(TPB) void k_bn_apply(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_bn_apply(
     const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(TPB) void k_bn_apply(
   // first iteration's operands in flight while the statistics are summed (the prologue and
   // this load are two dependent memory round trips otherwise)
   const long long n8 = M * C / 8;
-  const long long i0 = blockIdx.x * (long long)TPB + threadIdx.x;
+  const long long i0 = blockIdx.x * (long long)NT + threadIdx.x;
   uint4 x0 = make_uint4(0, 0, 0, 0), r0 = make_uint4(0, 0, 0, 0);
   if (i0 < n8) {
     x0 = reinterpret_cast<const uint4*>(x)[i0];
@@ -179,10 +181,10 @@ __global__ __launch_bounds__(TPB) void k_bn_apply(
   const float* st = stats;
   if (mode == 0 && stats_rows > 0) {  // per-wave partial rows written by the conv epilogue
     float* sums = sh + 2 * C;
-    sum_partial_rows(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 4 * C));
+    sum_partial_rows<NT>(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 4 * C));
     st = sums;
   }
-  for (int c = threadIdx.x; c < C; c += TPB) {
+  for (int c = threadIdx.x; c < C; c += NT) {
     float mean, var;
     if (mode == 0) {
       mean = st[c] / (float)M;
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(TPB) void k_bn_apply(
   }
   __syncthreads();
   const int CH = C / 8;
-  for (long long i = i0; i < n8; i += (long long)gridDim.x * TPB) {
+  for (long long i = i0; i < n8; i += (long long)gridDim.x * NT) {
     const int c0 = (int)(i % CH) * 8;
     float f[8];
     unpack8(i == i0 ? x0 : reinterpret_cast<const uint4*>(x)[i], f);
@@ -447,14 +449,15 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply(
 // per-block partials [G][2C] (dbeta | dgamma) of k_bn_bwd_reduce2<2> in a fixed order
 // (deterministic; no atomics, no fences — the kernel boundary makes them visible);
 // block 0 also adds the sums into the parameter gradients.
-__global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_bn_bwd_apply_fin(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*TPB], ka kb kc mu rs [C]
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
   float4* red4 = reinterpret_cast<float4*>(sh);
-  float* ka = sh + 4 * TPB;
+  float* ka = sh + 4 * NT;
   float* kb = ka + C;
   float* kc = ka + 2 * C;
   float* mu = ka + 3 * C;
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
   const float invM = 1.f / (float)M;
   // first iteration's operands in flight while the partial rows are summed
   const long long n8 = M * C / 8;
-  const long long i0 = blockIdx.x * (long long)TPB + threadIdx.x;
+  const long long i0 = blockIdx.x * (long long)NT + threadIdx.x;
   uint4 dy0 = make_uint4(0, 0, 0, 0), x0 = dy0, y0 = dy0;
   if (i0 < n8) {
     dy0 = reinterpret_cast<const uint4*>(dy)[i0];
@@ -472,8 +475,8 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
   // sum the G partial rows of 2C floats: float4 column groups x row slices (several
   // independent loads in flight per thread), slices combined through LDS
   const int Q = C / 2;                         // float4 groups per partial row
-  const int QT = Q < TPB ? Q : TPB;            // groups handled per pass
-  const int S = TPB / QT;                      // row slices per pass
+  const int QT = Q < NT ? Q : NT;            // groups handled per pass
+  const int S = NT / QT;                      // row slices per pass
   for (int q0 = 0; q0 < Q; q0 += QT) {
     const int q = q0 + (int)(threadIdx.x % QT);
     const int sl = threadIdx.x / QT;
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
     }
     __syncthreads();
   }
-  for (int c = threadIdx.x; c < C; c += TPB) {
+  for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
     if (blockIdx.x == 0) { dbeta[c] += sb; dgamma[c] += sg; }
     const float gm = gamma ? gamma[c] : 1.f;
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(TPB) void k_bn_bwd_apply_fin(
   }
   __syncthreads();
   const int CH = C / 8;
-  for (long long i = i0; i < n8; i += (long long)gridDim.x * TPB) {
+  for (long long i = i0; i < n8; i += (long long)gridDim.x * NT) {
     const int c0 = (int)(i % CH) * 8;
     float d[8], xv[8];
     unpack8(i == i0 ? dy0 : reinterpret_cast<const uint4*>(dy)[i], d);
@@ -610,17 +613,54 @@ KML_API int kml_bn_stats(const bf16_t* x, float* stats, long long M, int C, hipS
   KML_LAUNCH_CHECK();
 }
 
+// Partial-row summation width: every block of the apply kernels sums all G rows of 2C
+// floats before its elementwise pass.  At 256 threads a thread walks ceil(G / slices) rows
+// in batches of 16 dependent-latency loads; past one batch, 1024-thread blocks (4x the
+// slices, same grid) cut that prologue to one memory round trip.
+static bool wide_sum(int G, int C) {
+  const int Q = C / 2;  // float4 columns of a [2C] row
+  const int slices = Q >= TPB ? 1 : TPB / Q;
+  return C <= 1024 && (G + slices - 1) / slices > 16;
+}
+
+static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
+                                const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
+                                float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
+  if (wide_sum(G, C)) {
+    constexpr int NT = 1024;
+    long long ab = (M * C / 8 + NT - 1) / NT;
+    if (ab > 256) ab = 256;
+    hipLaunchKernelGGL(k_bn_bwd_apply_fin<NT>, dim3((unsigned)ab), dim3(NT), (4 * NT + 5 * C) * sizeof(float), s,
+                       dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
+    KML_LAUNCH_CHECK();
+  }
+  long long ab = (M * C / 8 + TPB - 1) / TPB;
+  if (ab > 256) ab = 256;
+  hipLaunchKernelGGL(k_bn_bwd_apply_fin<TPB>, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s,
+                     dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
+  KML_LAUNCH_CHECK();
+}
+
 // stats_rows > 0: stats is [stats_rows][2C] partial sums (conv epilogue), summed here
 KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, const float* gamma, const float* beta,
                          const bf16_t* res, bf16_t* y, float* save_mean, float* save_rstd, float* run_mean,
                          float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
                          hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (stats_rows > 0 && wide_sum(stats_rows, C)) {
+    constexpr int NT = 1024;
+    const size_t shm = (4 * C + 4 * NT) * sizeof(float);
+    unsigned grid = kml_stream_grid(M * C / 8, NT);
+    if (grid > 256) grid = 256;
+    hipLaunchKernelGGL(k_bn_apply<NT>, dim3(grid), dim3(NT), shm, s, x, stats, gamma, beta, res, y, save_mean,
+                       save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows);
+    KML_LAUNCH_CHECK();
+  }
   const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
   unsigned grid = kml_stream_grid(M * C / 8, TPB);
   if (stats_rows > 0 && grid > 256) grid = 256;  // every block re-sums the partials: fewer, fuller blocks
-  hipLaunchKernelGGL(k_bn_apply, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, save_mean, save_rstd,
-                     run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows);
+  hipLaunchKernelGGL(k_bn_apply<TPB>, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, save_mean,
+                     save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows);
   KML_LAUNCH_CHECK();
 }
 
@@ -644,12 +684,7 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
     const int gf = fin_blocks(M, C, &rpb);
     hipLaunchKernelGGL(k_bn_bwd_reduce2<2>, dim3(gf), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
                        nullptr, M, C, rpb);
-    long long ab = (M * C / 8 + TPB - 1) / TPB;
-    if (ab > 256) ab = 256;
-    hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s,
-                       dy, y, x, mean,
-                       rstd, gamma, ws, gf, dgamma, dbeta, dx, dres, M, C);
-    KML_LAUNCH_CHECK();
+    return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, ws, gf, dgamma, dbeta, dx, dres, M, C, s);
   }
   const int g = bwd_blocks(M, C, &rpb);
   if (ws && counter) {  // deterministic: ordered partials + last-arriver reduce
@@ -670,11 +705,7 @@ KML_API int kml_bn_bwd_apply_partial(const bf16_t* dy, const bf16_t* y, const bf
                                      const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
                                      float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
   if (C % 8 || C / 8 > TPB || G <= 0) return (int)hipErrorInvalidValue;
-  long long ab = (M * C / 8 + TPB - 1) / TPB;
-  if (ab > 256) ab = 256;
-  hipLaunchKernelGGL(k_bn_bwd_apply_fin, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s, dy, y,
-                     x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
-  KML_LAUNCH_CHECK();
+  return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, s);
 }
 
 KML_API int kml_relu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {
