@@ -1,22 +1,38 @@
 """Headline benchmark: ResNet-34 / CIFAR-10 data-parallel training throughput on MI355X.
 
-Metric (BASELINE.json): whole-node images/sec (+ epoch time) for torchvision-style
+Metric (BASELINE.json): whole-node images/sec + epoch time for torchvision-style
 ResNet-34 (ImageNet stem, 1000-class head, as in the reference's
 ml/experiments/kubeml/function_resnet34.py) on 32x32 CIFAR-10 images, per-worker
 batch 256, SGD(lr, weight_decay=1e-4), synchronous gradient all-reduce every step
-(north-star config 2), bf16 compute with fp32 master weights.
+(north-star config 2: K=1), bf16 compute with fp32 master weights.
+
+The step is the framework's own: :func:`kubeml_amd.engine.dp.make_train_step`, the
+builder ``KubeModel.step`` uses on resident workers (stage-split backward, overlapped
+RCCL all-reduce of the flat gradient buffer, fused SGD, one hipGraph replay per step).
 
 Data: synthetic CIFAR-10-shaped uint8 images resident in HBM (no network for the
 real dataset); every step runs the full on-device augmentation (random crop 32/pad 4,
 horizontal flip, normalise) — nothing is skipped inside the timed region.
 Weights: random init of the real architecture (21.8 M parameters).
 
-Usage: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run)
+After the timed steps a real epoch is MEASURED (not derived): every rank trains
+ceil(50000 / N / B) full batches of its shard, BN statistics are averaged over the
+ranks, then the 10,000-image validation set is evaluated (sharded over the ranks),
+the reference's epoch time definition (ml/pkg/train/job.go:222-231, 327).
+
+Usage:
+  python bench.py --gpus N --steps K --warmup W
+    N > 1 without WORLD_SIZE in the environment: the script launches N ranks itself
+    (torch.distributed.run, one process per GPU, RCCL over xGMI) before touching the GPU.
+  python bench.py --gpus N --cpu-smoke   (gloo on CPU: proves the N-rank launch path)
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,13 +40,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_IMG_S = 4900.0  # P=8, batch 256, E=40 derivation (upper end of 3.7k-4.9k)
+BASELINE_EPOCH_S = 10.0  # ~10-13.5 s/epoch at P=8, batch 256
 CIFAR_TRAIN = 50000
+CIFAR_TEST = 10000
+METRIC = "images/sec (whole node) + epoch time, ResNet-34 CIFAR-10 at 1/2/4/8 workers"
 
 
-def main():
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-worker batch (reference batch 256)")
     ap.add_argument("--lr", type=float, default=0.01)
@@ -38,41 +57,129 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=0.0)
     ap.add_argument("--trace-loss", action="store_true", help="print the loss of every step (debug; syncs)")
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--segments", choices=["auto", "on", "off"], default="auto",
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="stage-split backward with overlapped all-reduce (auto: on when N>1)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL all-reduce path even with one rank (single-GPU rehearsal of dp>1)")
-    ap.add_argument("--graph-comm", choices=["auto", "on", "off"], default="auto",
-                    help="capture the overlapped all-reduces inside the step's hipGraph, one replay per step "
-                         "(auto: on when N>1; KUBEML_GRAPH_COMM=0 forces off)")
-    args = ap.parse_args()
+    ap.add_argument("--graph-comm", choices=["on", "off"], default="on",
+                    help="capture the overlapped all-reduces inside the step's hipGraph (KUBEML_GRAPH_COMM=0: off)")
+    ap.add_argument("--no-epoch", action="store_true", help="skip the measured epoch after the timed steps")
+    ap.add_argument("--cpu-smoke", action="store_true", help="gloo/CPU rehearsal of the N-rank launch (tiny model)")
+    return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(args):
+    """--gpus N > 1 outside torchrun: start N ranks as a child torch.distributed.run (the
+    parent never initialises the GPU; device_count() does not) and exit with its code."""
+    if not args.cpu_smoke:
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) visible "
+                  f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', '<unset>')})", file=sys.stderr)
+            sys.exit(2)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def cpu_smoke(args, world, rank):
+    """N gloo ranks on CPU: LeNet, gradient all-reduce every step, one JSON line."""
+    import torch
+    import torch.distributed as dist
+    from kubeml_amd.models.lenet import LeNet
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(args.seed)
+    model = LeNet()
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(rank)
+    B = 8
+    for _ in range(args.warmup + args.steps):
+        x = torch.rand(B, 1, 28, 28, generator=g)
+        y = torch.randint(0, 10, (B,), generator=g)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(model(x), y)
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+            dist.all_reduce(flat)
+            flat /= world
+            off = 0
+            for p in model.parameters():
+                p.grad.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        opt.step()
+    cs = torch.tensor([float(sum(p.double().abs().sum() for p in model.parameters()))], dtype=torch.float64)
+    joined = torch.ones(1)
+    in_sync = True
+    if world > 1:
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(joined)
+        in_sync = bool(float(hi - lo) <= 1e-9 * max(1.0, float(hi)))
+    if rank == 0:
+        print(json.dumps({"metric": "cpu-smoke (gloo launch rehearsal; not a performance number)", "value": None,
+                          "unit": None, "n_gpus": 0, "ranks": world, "ranks_joined": int(joined.item()),
+                          "ranks_in_sync": in_sync, "steps": args.steps, "warmup": args.warmup,
+                          "config": {"model": "lenet5", "backend": "gloo"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        relaunch(args)
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    if args.cpu_smoke:
+        return cpu_smoke(args, world, rank)
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = world > 1 or args.force_comm
     if comm:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
-    from kubeml_amd.engine.step import GraphedTrainStep
+    from kubeml_amd.engine.dp import make_train_step
     from kubeml_amd.models.resnet import resnet34
-    from kubeml_amd.nn import backward_loss, cross_entropy, flatten_module
+    from kubeml_amd.nn import cross_entropy, flatten_module
     from kubeml_amd.ops import kernels as K
     from kubeml_amd.optim import SGD
+    from kubeml_amd.parallel.comm import from_env
+    from kubeml_amd.parallel.kavg import ModelAverager
 
     B = args.batch
-    n_local = CIFAR_TRAIN // world
+    n_local = CIFAR_TRAIN // world          # split_minibatches gives every rank ~1/N of the docs
+    n_val = -(-CIFAR_TEST // world)
 
-    # synthetic CIFAR-10 shard resident in HBM (each rank its own shard, like split_minibatches)
+    # synthetic CIFAR-10 shards resident in HBM (each rank its own shard)
     g = torch.Generator(device=dev).manual_seed(rank)
     data = torch.randint(0, 256, (n_local, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
     labels = torch.randint(0, 10, (n_local,), dtype=torch.int64, device=dev, generator=g)
+    vdata = torch.randint(0, 256, (n_val, 32, 32, 3), dtype=torch.uint8, device=dev, generator=g)
+    vlabels = torch.randint(0, 10, (n_val,), dtype=torch.int64, device=dev, generator=g)
     ctr = torch.tensor([float(1000 + rank), 0.0, 0.0], dtype=torch.float32, device=dev)
     xbuf = torch.empty((B, 32, 32, 8), dtype=torch.bfloat16, device=dev)
     ybuf = torch.empty((B,), dtype=torch.int64, device=dev)
@@ -80,61 +187,55 @@ def main():
     torch.manual_seed(args.seed)  # identical init on every rank
     model = resnet34(num_classes=1000).to(dev)
     space = flatten_module(model)
+    cm = from_env()
+    averager = ModelAverager(model)
     if comm:
-        dist.broadcast(space.master, 0)
-        space.refresh_shadow()
+        averager.broadcast_(cm, 0)
     model.train()
     opt = SGD(model.parameters(), lr=args.lr, weight_decay=1e-4)
-    opt.set_grad_scale(1.0 / world)
 
-    def fwd_bwd():
-        K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True)
-        space.zero_grad()
-        loss = cross_entropy(model(xbuf), ybuf)
-        backward_loss(loss)
-        return loss
-
-    def opt_step():
-        opt.step()
-        K.advance_counter_(ctr, B, n_local)
-
-    use_seg = args.segments == "on" or (args.segments == "auto" and comm)
-    graph_comm = use_seg and comm and os.environ.get("KUBEML_GRAPH_COMM", "1") != "0" and (
-        args.graph_comm == "on" or (args.graph_comm == "auto" and world > 1))
-    segs = seg_grads = None
-    if use_seg:
-        # backward in 3 graph segments; each segment's gradients are all-reduced on the
-        # RCCL stream while the next segment computes (engine/staged.py)
-        from kubeml_amd.engine.staged import StagedForwardBackward
-
-        def pre():
-            K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True)
-            space.zero_grad()
-        staged = StagedForwardBackward(model.stages(), lambda out: cross_entropy(out, ybuf), lambda: xbuf, pre=pre)
-        segs = [staged.segment(k) for k in range(staged.n_segments)]
-        sp = model.stage_params()
-        seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
-    step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], use_graph=not args.no_graph, warmup=3,
-                            bucket_mb=args.bucket_mb, segments=segs, segment_grads=seg_grads,
-                            force_segments=use_seg, force_comm=args.force_comm, graph_comm=graph_comm)
+    overlap = args.overlap == "on" or (args.overlap == "auto" and comm)
+    graph_comm = args.graph_comm == "on" and os.environ.get("KUBEML_GRAPH_COMM", "1") != "0"
+    step = make_train_step(
+        model, space, opt, cross_entropy, xbuf, ybuf,
+        pre=lambda: K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True),
+        post=lambda: K.advance_counter_(ctr, B, n_local),
+        world=world, use_graph=not args.no_graph, graph_comm=graph_comm, overlap=overlap,
+        bucket_mb=args.bucket_mb, force_comm=args.force_comm, extra_state=[ctr])
+    if comm:
+        step.prime_comm()
     step.capture()
+    loss = None
     for _ in range(args.warmup):
         loss = step()
     torch.cuda.synchronize()
-    first_loss = float(loss.item())
+    first_loss = float(loss.item()) if loss is not None else float("nan")
 
-    if comm:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step()
-        if args.trace_loss and rank == 0:
-            print(f"step {i} loss {float(loss.item()):.4f} gnorm {float(space.grad.norm()):.3e}", flush=True)
-    torch.cuda.synchronize()
-    if comm:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    def timed(fn):
+        if comm:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        if comm:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if comm:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, out
+
+    def run_steps(n):
+        l = None
+        for i in range(n):
+            l = step()
+            if args.trace_loss and rank == 0:
+                print(f"step {i} loss {float(l.item()):.4f} gnorm {float(space.grad.norm()):.3e}", flush=True)
+        return l
+
+    dt, loss = timed(lambda: run_steps(args.steps))
     last_loss = float(loss.item())
     in_sync = None
     if comm:
@@ -145,15 +246,17 @@ def main():
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         in_sync = bool((hi - lo).abs().item() <= 1e-9 * max(1.0, abs(hi.item())))
-    if comm:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     ms = dt / args.steps * 1e3
     img_s = B * world * args.steps / dt
+
+    epoch = None
+    if not args.no_epoch:
+        epoch = measure_epoch(args, model, space, step, averager, cm, comm, world, dev, timed, n_local,
+                              vdata, vlabels, ctr, xbuf, ybuf)
+
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node) + epoch time, ResNet-34 CIFAR-10 at 1/2/4/8 workers",
+            "metric": METRIC,
             "value": round(img_s, 1),
             "unit": "images/s",
             "n_gpus": world,
@@ -167,17 +270,81 @@ def main():
             "data": "synthetic (CIFAR-10-shaped uint8 in HBM, on-device crop/flip/normalize), random-init weights",
             "config": {"model": "resnet34 (torchvision, ImageNet stem, 1000-class head)", "global_batch": B * world,
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
-                       "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "all-reduce every step (K=1)",
-                       "graph": not args.no_graph, "overlap_segments": use_seg,
-                       "graph_comm": graph_comm},
-            "epoch_time_s": round(CIFAR_TRAIN / img_s, 3),
+                       "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "gradient all-reduce every step (K=1)",
+                       "graph": not args.no_graph, "overlap_segments": overlap and comm,
+                       "graph_comm": graph_comm and comm, "bucket_mb": args.bucket_mb,
+                       "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
+        if epoch is not None:
+            out.update(epoch)
+            out["epoch_vs_baseline"] = round(BASELINE_EPOCH_S / epoch["epoch_time_s"], 2)
         if in_sync is not None:
             out["ranks_in_sync"] = in_sync
+            out["rccl_world"] = dist.get_world_size()
         print(json.dumps(out), flush=True)
     if comm:
         dist.destroy_process_group()
+
+
+def measure_epoch(args, model, space, step, averager, cm, comm, world, dev, timed, n_local, vdata, vlabels, ctr,
+                  xbuf, ybuf):
+    """One measured epoch: train over the shard, average BN statistics, validate."""
+    import torch
+    import torch.distributed as dist
+    from kubeml_amd.nn import cross_entropy
+    from kubeml_amd.ops import kernels as K
+    B = args.batch
+    steps = math.ceil(n_local / B)
+    n_val = vdata.shape[0]
+    vsteps = math.ceil(n_val / B)
+    vctr = torch.zeros(3, dtype=torch.float32, device=dev)
+    acc = torch.zeros(2, dtype=torch.float64, device=dev)    # [correct, count]
+
+    def val_batch():
+        K.augment(vdata, vlabels, vctr, B, out=xbuf, labels_out=ybuf, pad=0, flip=False, train=False)
+        K.advance_counter_(vctr, B, n_val)
+        with torch.no_grad():
+            loss, correct = cross_entropy(model(xbuf), ybuf, return_correct=True)
+        acc[0] += correct
+        acc[1] += B
+    # eval forward as one graph too (captured once, outside the timed region; BN in eval mode)
+    model.eval()
+    vgraph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            val_batch()
+        torch.cuda.current_stream().wait_stream(s)
+        vgraph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(vgraph):
+            val_batch()
+    model.train()
+    acc.zero_()
+    vctr.zero_()
+
+    def train_epoch():
+        for _ in range(steps):
+            step()
+
+    def validate():
+        averager.average_buffers_(cm)          # K=1 semantics: BN statistics averaged over ranks
+        model.eval()
+        for _ in range(vsteps):
+            if vgraph is not None:
+                vgraph.replay()
+            else:
+                val_batch()
+        model.train()
+        if comm:
+            dist.all_reduce(acc)
+
+    t_train, _ = timed(train_epoch)
+    t_val, _ = timed(validate)
+    return {"epoch_time_s": round(t_train + t_val, 4), "epoch_train_s": round(t_train, 4),
+            "epoch_val_s": round(t_val, 4), "epoch_steps_per_rank": steps, "val_images": int(acc[1].item()),
+            "epoch_measured": True}
 
 
 if __name__ == "__main__":

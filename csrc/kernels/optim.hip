@@ -21,8 +21,12 @@ namespace {
 
 __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
                       bf16_t* __restrict__ shadow, const float* __restrict__ lr_ptr, float lr_host, float wd,
-                      float momentum, float dampening, int nesterov, int first, float grad_scale, long long n) {
+                      float momentum, float dampening, int nesterov, const float* __restrict__ first_ptr,
+                      int first_host, float grad_scale, long long n) {
   const float lr = lr_ptr ? *lr_ptr : lr_host;
+  // first step after a reset (torch: momentum buffer := d, no dampening).  The flag lives
+  // in device memory so a graph-captured step follows reset_state() between replays.
+  const int first = first_ptr ? (*first_ptr != 0.f) : first_host;
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -138,13 +142,6 @@ __global__ void k_clip_scale(float* __restrict__ x, const float* __restrict__ su
     x[i] *= c;
 }
 
-// p *= 1 / max(*count, 1)    (K-AVG divisor computed on device by the count all-reduce)
-__global__ void k_scale_inv_dev(float* __restrict__ p, const float* __restrict__ count, long long n) {
-  const float inv = 1.f / fmaxf(*count, 1.f);
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    p[i] *= inv;
-}
-
 }  // namespace
 
 // NOTE: hipMemsetAsync is avoided on capturable paths (graph memset nodes raced with
@@ -154,10 +151,10 @@ KML_API int kml_memset(void* p, int value, long long bytes, hipStream_t s) {
 }
 
 KML_API int kml_sgd(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr, float lr, float wd,
-                    float momentum, float dampening, int nesterov, int first, float grad_scale, long long n,
-                    hipStream_t s) {
+                    float momentum, float dampening, int nesterov, const float* first_ptr, int first,
+                    float grad_scale, long long n, hipStream_t s) {
   hipLaunchKernelGGL(k_sgd, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, w, g, mom, shadow, lr_ptr, lr,
-                     wd, momentum, dampening, nesterov, first, grad_scale, n);
+                     wd, momentum, dampening, nesterov, first_ptr, first, grad_scale, n);
   KML_LAUNCH_CHECK();
 }
 
@@ -183,7 +180,76 @@ KML_API int kml_clip_grad_norm(float* g, float* ws1, float max_norm, long long n
   KML_LAUNCH_CHECK();
 }
 
-KML_API int kml_scale_inv_dev(float* p, const float* count, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_scale_inv_dev, dim3(kml_stream_grid(n, 256)), dim3(256), 0, s, p, count, n);
+
+// ---------------------------------------------------------------------------------------
+// K-AVG model average over ONE persistent flat state buffer (reference: the TrainJob's
+// merge, ml/pkg/model/model.go:249-302 + parallelSGD.go:26-54).  Layout of `state`:
+//   [0, n_params)            fp32 master parameters (the optimizer's buffer)
+//   [n_params, i64_off)      fp32 module buffers (BN running_mean / running_var)
+//   [i64_off, i64_off+n_i64) int64 buffers (num_batches_tracked) carried as fp32
+//   [count_idx]              1 if this rank contributes to the round, else 0
+// pack:   i64 -> fp32 slots, count slot := participate (non-participants send zeros)
+// <RCCL all-reduce SUM of the whole buffer on the caller's stream>
+// finish: x *= 1/max(count, 1); bf16 shadow of the parameter range refreshed in the
+//         same pass; int64 buffers := floor(average) (the reference's integer division)
+// No host synchronisation: the divisor never leaves the device.
+// ---------------------------------------------------------------------------------------
+__global__ void k_kavg_pack(float* __restrict__ state, const long long* __restrict__ i64, long long i64_off,
+                            int n_i64, long long count_idx, int participate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_i64) state[i64_off + i] = participate ? (float)i64[i] : 0.f;
+  if (i == 0) state[count_idx] = participate ? 1.f : 0.f;
+}
+
+__global__ void k_kavg_finish(float* __restrict__ state, long long n_params, long long count_idx,
+                              bf16_t* __restrict__ shadow, long long* __restrict__ i64, long long i64_off,
+                              int n_i64) {
+  const float inv = 1.f / fmaxf(state[count_idx], 1.f);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long n4 = count_idx >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<float4*>(state)[i];
+    v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+    reinterpret_cast<float4*>(state)[i] = v;
+    const long long e = i << 2;
+    if (shadow && e + 3 < n_params) {
+      uint2 s;
+      s.x = pack_bf2(v.x, v.y);
+      s.y = pack_bf2(v.z, v.w);
+      reinterpret_cast<uint2*>(shadow)[i] = s;
+    } else if (shadow) {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int k = 0; k < 4; ++k)
+        if (e + k < n_params) shadow[e + k] = f2bf(vv[k]);
+    }
+    if (i64) {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int k = 0; k < 4; ++k) {
+        const long long j = e + k - i64_off;
+        if (j >= 0 && j < n_i64) i64[j] = (long long)floorf(vv[k] + 1e-3f);
+      }
+    }
+  }
+  for (long long e = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; e < count_idx; e += stride) {
+    const float v = state[e] * inv;
+    state[e] = v;
+    if (shadow && e < n_params) shadow[e] = f2bf(v);
+    const long long j = e - i64_off;
+    if (i64 && j >= 0 && j < n_i64) i64[j] = (long long)floorf(v + 1e-3f);
+  }
+}
+
+KML_API int kml_kavg_pack(float* state, const long long* i64, long long i64_off, int n_i64, long long count_idx,
+                          int participate, hipStream_t s) {
+  const int n = n_i64 > 1 ? n_i64 : 1;
+  hipLaunchKernelGGL(k_kavg_pack, dim3((n + 255) / 256), dim3(256), 0, s, state, i64, i64_off, n_i64, count_idx,
+                     participate);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_kavg_finish(float* state, long long n_params, long long count_idx, bf16_t* shadow, long long* i64,
+                            long long i64_off, int n_i64, hipStream_t s) {
+  hipLaunchKernelGGL(k_kavg_finish, dim3(kml_stream_grid((count_idx + 3) / 4, 256)), dim3(256), 0, s, state,
+                     n_params, count_idx, shadow, i64, i64_off, n_i64);
   KML_LAUNCH_CHECK();
 }

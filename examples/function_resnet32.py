@@ -27,12 +27,12 @@ class KubeResnet(KubeModel):
 
     def train(self, batch, batch_index) -> float:
         x, y = prepare(batch, self._dataset, train=True, seed=self.args._func_id)
-        return float(self.step(x, y))
+        return self.step(x, y)  # device tensor: no host sync per batch
 
     def validate(self, batch, batch_index) -> Tuple[float, float]:
         x, y = prepare(batch, self._dataset, train=False)
         loss, correct = cross_entropy(self(x), y, return_correct=True)
-        return float(correct) * 100 / self.batch_size, float(loss)
+        return correct * 100 / self.batch_size, loss
 
     def infer(self, data):
         x = torch.tensor(data, dtype=torch.uint8, device=self.device)

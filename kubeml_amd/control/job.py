@@ -121,6 +121,8 @@ class TrainJob:
         self.have_ckpt = False
         self.thread: Optional[threading.Thread] = None
         self.images_per_second = 0.0
+        self.last_sync_seconds = 0.0
+        self.last_grad_rounds = 0
         self.done = threading.Event()
         self.resume_from = getattr(opts, "resume_from", "") or ""
         self._pending_restore = None
@@ -238,6 +240,8 @@ class TrainJob:
                 self._pending_restore = None
                 losses = [float(v["result"]["loss"]) for v in ok.values()]
                 hbm = max((v.get("hbm_bytes", 0) for v in ok.values()), default=0)
+                self.last_sync_seconds = max((v.get("sync_seconds", 0.0) for v in ok.values()), default=0.0)
+                self.last_grad_rounds = max((v.get("grad_rounds", 0) for v in ok.values()), default=0)
                 self._epoch_stats(time.time() - t0, hbm)
                 return sum(losses) / len(losses)
             errs = "; ".join(f"worker {r}: {v.get('error')}" for r, v in sorted(bad.items()))
@@ -345,7 +349,8 @@ class TrainJob:
                 self.history.train_loss.append(loss)
                 self._push_metrics()
                 self.log.info("epoch finished", epoch=self.epoch, loss=loss, seconds=elapsed,
-                              parallelism=self.parallelism, images_per_second=self.images_per_second)
+                              parallelism=self.parallelism, images_per_second=self.images_per_second,
+                              sync_seconds=self.last_sync_seconds, grad_sync_rounds=self.last_grad_rounds)
                 if not self.static and self.epoch < E:
                     self._next_parallelism()
                 if self.validate_every and self.epoch % self.validate_every == 0 and self.epoch != E:

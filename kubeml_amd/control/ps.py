@@ -138,6 +138,7 @@ class ParameterServer:
     def _job_metrics(self, job_id: str, m: MetricUpdate, job: TrainJob):
         self.update_metrics(job_id, m)
         self.metrics.update_extra(job_id, images_per_second=job.images_per_second,
+                                  allreduce_seconds=getattr(job, "last_sync_seconds", None),
                                   hbm_bytes=getattr(job, "last_hbm", None))
 
     def job_finished(self, job_id: str, err: Optional[str] = None):

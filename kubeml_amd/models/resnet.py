@@ -186,10 +186,14 @@ class ResNet(tnn.Module):
         bns = self._arena.bns
         if arena is None or arena.device != bns[0].running_mean.device:
             dev = bns[0].running_mean.device
-            arena = torch.zeros(len(bns), dtype=torch.int64, device=dev)
-            for i, bn in enumerate(bns):
-                arena[i] = bn.num_batches_tracked.to(dev)
-                bn.num_batches_tracked = arena[i]
+            ts = [bn.num_batches_tracked for bn in bns]
+            if ts[0].device == dev and all(t.data_ptr() == ts[0].data_ptr() + 8 * i for i, t in enumerate(ts)):
+                arena = ts[0].as_strided((len(bns),), (1,))   # already packed (nn/flat.py)
+            else:
+                arena = torch.zeros(len(bns), dtype=torch.int64, device=dev)
+                for i, bn in enumerate(bns):
+                    arena[i] = bn.num_batches_tracked.to(dev)
+                    bn.num_batches_tracked = arena[i]
             self._nbt_arena = arena
         from ..ops import kernels as K
         K.add_i64_(arena)

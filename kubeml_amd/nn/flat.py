@@ -24,6 +24,11 @@ Layout rules
   of the buffer is final as soon as the corresponding layers are done, which is
   what the bucketed, backward-overlapped all-reduce exploits.
 * Regions are 64-element aligned (256 B) so every region starts on a cache line.
+* ``master`` is the head of a larger fp32 ``state`` buffer that also holds the
+  module's floating-point buffers (BN running statistics, rebound as views), fp32
+  slots for its int64 buffers (``num_batches_tracked``) and one participation-count
+  slot: a K-AVG model average is then ONE all-reduce over ``state`` plus one fused
+  scale kernel (parallel/kavg.py), instead of a per-round ``torch.cat`` of buffers.
 """
 from __future__ import annotations
 
@@ -46,7 +51,10 @@ class FlatParamSpace:
     """Owns the flat buffers for a list of parameters (all on one device)."""
 
     def __init__(self, params: Iterable[torch.nn.Parameter], device=None, reverse: bool = True,
-                 with_shadow: Optional[bool] = None):
+                 with_shadow: Optional[bool] = None, buffers=None):
+        """buffers: optional list of (module, name) of floating-point module buffers to
+        place behind the parameters in ``state``; ``n_i64`` int64 buffers are given fp32
+        slots via ``i64_buffers`` (list of (module, name))."""
         params = [p for p in params if p.requires_grad]
         seen = set()
         uniq = []
@@ -72,7 +80,21 @@ class FlatParamSpace:
             self.offsets.append((off, n))
             off += -(-n // ALIGN) * ALIGN
         self.numel = max(off, ALIGN)
-        self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        fbufs, ibufs = buffers or ([], [])
+        self.float_buffers = list(fbufs)
+        self.i64_buffers = list(ibufs)
+        boff = self.numel
+        self.buffer_offsets = []
+        for mod, name in self.float_buffers:
+            n = getattr(mod, name).numel()
+            self.buffer_offsets.append((boff, n))
+            boff += n
+        self.i64_off = -(-boff // 4) * 4
+        self.n_i64 = len(self.i64_buffers)
+        self.count_idx = self.i64_off + self.n_i64
+        self.state_numel = -(-(self.count_idx + 1) // ALIGN) * ALIGN
+        self.state = torch.zeros(self.state_numel, dtype=torch.float32, device=self.device)
+        self.master = self.state[:self.numel]
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.shadow = (torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
                        if with_shadow else None)
@@ -90,7 +112,41 @@ class FlatParamSpace:
                 if self.shadow is not None:
                     p._kml_shadow = self.shadow[o:o + n].view(shape)
                 p._kml_flat = self
+            for (mod, name), (o, n) in zip(self.float_buffers, self.buffer_offsets):
+                b = getattr(mod, name)
+                v = self.state[o:o + n].view(b.shape)
+                v.copy_(b.to(self.device))
+                setattr(mod, name, v)
+        self.i64_arena = None
+        if self.i64_buffers:
+            self._bind_i64()
         self.refresh_shadow()
+
+    def _bind_i64(self):
+        """All int64 buffers as consecutive elements of one arena (one pointer for the
+        K-AVG pack/finish kernels).  Models that keep their own arena (ResNet's packed
+        ``num_batches_tracked``) are detected and reused."""
+        ts = [getattr(m, n) for m, n in self.i64_buffers]
+        base = ts[0]
+        if all(t.numel() == 1 for t in ts) and all(
+                t.data_ptr() == base.data_ptr() + 8 * i for i, t in enumerate(ts)):
+            self.i64_arena = base.as_strided((len(ts),), (1,))
+            return
+        arena = torch.zeros(len(ts), dtype=torch.int64, device=self.device)
+        with torch.no_grad():
+            for i, ((m, n), t) in enumerate(zip(self.i64_buffers, ts)):
+                arena[i] = t.reshape(()).to(self.device)
+                setattr(m, n, arena[i])
+        self.i64_arena = arena
+
+    def i64_arena_now(self):
+        """The int64 arena, re-detected if a model rebound its counters (e.g. on device move)."""
+        if self.i64_buffers:
+            ts = [getattr(m, n) for m, n in self.i64_buffers]
+            a = self.i64_arena
+            if a is None or any(t.data_ptr() != a.data_ptr() + 8 * i for i, t in enumerate(ts)):
+                self._bind_i64()
+        return self.i64_arena
 
     # ------------------------------------------------------------------ utilities
     def refresh_shadow(self):
@@ -158,9 +214,26 @@ class FlatParamSpace:
         return self.master
 
 
-def flatten_module(module: torch.nn.Module, device=None) -> FlatParamSpace:
-    """Move all trainable parameters of ``module`` into one FlatParamSpace."""
-    space = FlatParamSpace(list(module.parameters()), device=device)
+def module_buffers(module: torch.nn.Module):
+    """([(module, name)] of floating buffers, [(module, name)] of int64 buffers) in
+    ``named_buffers`` order."""
+    fl, il = [], []
+    for mod in module.modules():
+        for name, b in mod._buffers.items():
+            if b is None or name in getattr(mod, "_non_persistent_buffers_set", ()):
+                continue
+            if b.is_floating_point():
+                fl.append((mod, name))
+            elif b.dtype == torch.int64 and b.numel() == 1:
+                il.append((mod, name))
+    return fl, il
+
+
+def flatten_module(module: torch.nn.Module, device=None, buffers: bool = True) -> FlatParamSpace:
+    """Move all trainable parameters (and, by default, the buffers) of ``module`` into
+    one FlatParamSpace."""
+    space = FlatParamSpace(list(module.parameters()), device=device,
+                           buffers=module_buffers(module) if buffers else None)
     module._kml_flat = space
     return space
 

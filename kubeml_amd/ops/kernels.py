@@ -673,10 +673,12 @@ def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100):
 # --------------------------------------------------------------------------------------
 
 def sgd_(w, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=False, first=False,
-         grad_scale=1.0, lr_dev=None):
+         grad_scale=1.0, lr_dev=None, first_dev=None):
+    """first_dev: fp32 device flag (non-zero = first step after a state reset); when given
+    it overrides ``first`` so graph replays follow reset_state()."""
     n = w.numel()
-    HIP.call("kml_sgd", "p p p p p f f f f i i f l s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
-             float(lr), float(wd), float(momentum), float(dampening), int(nesterov), int(first),
+    HIP.call("kml_sgd", "p p p p p f f f f i p i f l s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
+             float(lr), float(wd), float(momentum), float(dampening), int(nesterov), _p(first_dev), int(first),
              float(grad_scale), n, _s())
 
 
@@ -696,8 +698,28 @@ def clip_grad_norm_(g, ws1, max_norm):
     HIP.call("kml_clip_grad_norm", "p p f l s", _p(g), _p(ws1), float(max_norm), g.numel(), _s())
 
 
-def scale_inv_dev_(x, count):
-    HIP.call("kml_scale_inv_dev", "p p l s", _p(x), _p(count), x.numel(), _s())
+def kavg_pack_(state, i64, i64_off, n_i64, count_idx, participate):
+    """K-AVG round prologue on the flat state buffer (see optim.hip): int64 buffers into
+    their fp32 slots, participation flag into the count slot."""
+    _chk(state, F32, "state")
+    if i64 is not None and (i64.dtype != torch.int64 or not i64.is_contiguous() or i64.numel() < n_i64):
+        raise ValueError("kavg_pack_: int64 arena must be contiguous int64 with n_i64 elements")
+    if not (0 <= i64_off and i64_off + n_i64 <= count_idx < state.numel()):
+        raise ValueError("kavg_pack_: bad state layout")
+    HIP.call("kml_kavg_pack", "p p l i l i s", _p(state), _p(i64), int(i64_off), int(n_i64), int(count_idx),
+             int(bool(participate)), _s())
+
+
+def kavg_finish_(state, n_params, count_idx, shadow, i64, i64_off, n_i64):
+    """K-AVG round epilogue after the SUM all-reduce: scale by 1/count (device), refresh
+    the bf16 shadow of the parameter range, floor the int64 buffers back."""
+    _chk(state, F32, "state")
+    if shadow is not None and (shadow.dtype != BF16 or shadow.numel() < n_params):
+        raise ValueError("kavg_finish_: shadow must be bf16 covering the parameters")
+    if not (0 <= n_params <= count_idx < state.numel()):
+        raise ValueError("kavg_finish_: bad state layout")
+    HIP.call("kml_kavg_finish", "p l l p p l i s", _p(state), int(n_params), int(count_idx), _p(shadow), _p(i64),
+             int(i64_off), int(n_i64), _s())
 
 
 # --------------------------------------------------------------------------------------

@@ -11,7 +11,13 @@ follows LR changes (``set_lr``) without re-capture, and Adam's step counter is a
 device scalar incremented inside the captured region.
 
 ``reset_state()`` implements the reference's per-round optimizer reset under K-step
-averaging (python/kubeml/kubeml/network.py:121-128): a memset of the state buffers.
+averaging (python/kubeml/kubeml/network.py:121-128): a memset of the state buffers,
+Adam's device step counter back to 0 and SGD's device first-step flag back to 1 — all
+read by the kernels at replay time, so a captured step honours a reset between replays.
+
+``state_tensors()`` lists every device tensor a step mutates (state buffers, step
+counters, flags); graph capture snapshots and restores them around its warm-up so
+capturing a step never applies an update (engine/step.py).
 
 ``from_torch(opt)`` converts a user's ``torch.optim.SGD/Adam/AdamW`` (what
 ``KubeModel.configure_optimizers`` returns in reference code) into the fused one
@@ -49,6 +55,7 @@ class FusedOptimizer(torch.optim.Optimizer):
         self._grad_scale = 1.0
         self._first = True
         self._step_dev: Dict[torch.device, torch.Tensor] = {}
+        self._first_dev: Dict[torch.device, torch.Tensor] = {}
         self._step_host = 0
 
     # --- device scalars -------------------------------------------------------------
@@ -98,6 +105,38 @@ class FusedOptimizer(torch.optim.Optimizer):
         self._step_host = 0
         for t in self._step_dev.values():
             t.zero_()
+        for t in self._first_dev.values():
+            t.fill_(1.0)
+
+    def first_tensor(self, device):
+        """fp32 device flag: 1 until the first fused step after a reset clears it."""
+        t = self._first_dev.get(device)
+        if t is None:
+            t = torch.ones(1, dtype=torch.float32, device=device)
+            self._first_dev[device] = t
+        return t
+
+    _STATE_NAMES = ()
+
+    def prepare(self):
+        """Allocate every device state buffer now (not lazily inside a first step), so
+        :meth:`state_tensors` is complete before a graph capture."""
+        spaces, _ = self._flat_groups()
+        for sp, _ in spaces:
+            if sp.device.type != "cuda":
+                continue
+            if self._STATE_NAMES:
+                self._bufs(sp, list(self._STATE_NAMES))
+            self.lr_tensor(sp.device)
+            self.first_tensor(sp.device)
+            self._step_dev.setdefault(sp.device, torch.zeros(1, dtype=torch.float32, device=sp.device))
+        return self
+
+    def state_tensors(self) -> List[torch.Tensor]:
+        """Every device tensor :meth:`step` mutates."""
+        out = [t for bufs in self._state_bufs.values() for t in bufs.values()]
+        out += list(self._step_dev.values()) + list(self._first_dev.values())
+        return out
 
     def _bufs(self, sp, names):
         key = id(sp)
@@ -110,6 +149,10 @@ class FusedOptimizer(torch.optim.Optimizer):
 
 class SGD(FusedOptimizer):
     kind = "sgd"
+
+    @property
+    def _STATE_NAMES(self):
+        return ("momentum",) if self.param_groups[0]["momentum"] != 0 else ()
 
     def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
         super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening,
@@ -128,9 +171,12 @@ class SGD(FusedOptimizer):
                 continue
             from ..ops import kernels as K
             mom = self._bufs(sp, ["momentum"])["momentum"] if g["momentum"] != 0 else None
+            first = self.first_tensor(sp.device) if mom is not None else None
             K.sgd_(sp.master, sp.grad, mom, sp.shadow, g["lr"], wd=g["weight_decay"], momentum=g["momentum"],
                    dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
-                   grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device))
+                   grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first)
+            if first is not None:
+                K.fill_(first, 0.0)
         if loose:
             _torch_sgd(loose, g, self.state, self._grad_scale)
         self._first = False
@@ -159,6 +205,7 @@ def _torch_sgd(params, g, state, grad_scale):
 class Adam(FusedOptimizer):
     kind = "adam"
     decoupled = False
+    _STATE_NAMES = ("exp_avg", "exp_avg_sq")
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))

@@ -8,14 +8,23 @@ Reference semantics:
 * each worker continues from the average and resets its optimizer state
   (python/kubeml/kubeml/network.py:121-128, 208-217).
 
-MI355X-native: the average is ONE all-reduce over the flat fp32 parameter buffer
-(RCCL over xGMI) plus one over a packed buffer of the BN running statistics, followed
-by an in-place divide; the divisor is computed on the fly by a 1-element all-reduce,
-so workers that ran out of data (uneven ``split_minibatches``) contribute zeros and are
-excluded from the divisor, exactly like the reference's partial merge rounds.
+MI355X-native (GPU workers): the model lives in ONE persistent fp32 ``state`` buffer
+(nn/flat.py: master parameters | BN running stats | int64 counters as fp32 | count
+slot).  A round is three launches on the compute stream and no host synchronisation:
+
+    kavg_pack    int64 counters -> fp32 slots, count slot := participate
+    all-reduce   SUM of the whole buffer (RCCL over xGMI)
+    kavg_finish  x *= 1/count (divisor read on device), bf16 shadow refreshed in the
+                 same pass, counters floored back to int64
+
+Workers that ran out of data (uneven ``split_minibatches``) send zeros and a zero
+count, so the divisor is the number of contributing ranks, exactly like the
+reference's partial merge rounds (ml/pkg/train/job.go:380-431).  CPU workers (gloo /
+the in-process fake backend) run the same algorithm with torch ops.
 """
 from __future__ import annotations
 
+import time
 from typing import List, Tuple
 
 import torch
@@ -26,38 +35,56 @@ from .comm import Comm
 class ModelAverager:
     def __init__(self, module: torch.nn.Module):
         self.module = module
-
-    def _param_tensors(self) -> List[torch.Tensor]:
-        sp = getattr(self.module, "_kml_flat", None)
-        if sp is not None:
-            return [sp.master]
-        out = []
-        for p in self.module.parameters():
-            if p.data.is_contiguous():
-                out.append(p.data)
-            else:
-                out.append(p.data)  # handled by pack path below
-        return out
+        self.last_seconds = 0.0   # host time of the last average_ call (metrics)
 
     def _buffers(self) -> List[Tuple[str, torch.Tensor]]:
         return [(n, b) for n, b in self.module.named_buffers() if b is not None]
 
+    def _space(self):
+        sp = getattr(self.module, "_kml_flat", None)
+        if sp is not None and getattr(sp, "state", None) is not None and sp.device.type == "cuda":
+            return sp
+        return None
+
     @torch.no_grad()
     def average_(self, comm: Comm, participate: bool = True) -> int:
+        """Average the model over the group.  GPU: returns -1 (the participant count
+        stays on the device); CPU: returns the participant count."""
         if comm.world == 1:
             return 1 if participate else 0
-        sp = getattr(self.module, "_kml_flat", None)
+        t0 = time.perf_counter()
+        sp = self._space()
+        try:
+            if sp is not None:
+                return self._average_flat(comm, sp, participate)
+            return self._average_host(comm, participate)
+        finally:
+            self.last_seconds = time.perf_counter() - t0
+
+    def _average_flat(self, comm: Comm, sp, participate: bool) -> int:
+        from ..ops import kernels as K
+        arena = sp.i64_arena_now()
+        if not participate:
+            K.memset_(sp.state)
+        K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, participate)
+        comm.all_reduce_(sp.state)
+        K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
+        return -1
+
+    def _average_host(self, comm: Comm, participate: bool) -> int:
+        """CPU path: pack everything into one fp32 vector (+count), one all-reduce."""
         bufs = self._buffers()
-        params = [] if sp is not None else [p for p in self.module.parameters()]
-        # pack everything that is not already one flat buffer into one fp32 vector
-        pieces = [p.data.reshape(-1).float() for p in params] + [b.reshape(-1).double() if not b.is_floating_point()
-                                                                  else b.reshape(-1).float() for _, b in bufs]
-        dev = sp.master.device if sp is not None else (pieces[0].device if pieces else torch.device("cpu"))
-        pack = torch.cat([x.float().to(dev) for x in pieces]) if pieces else None
-        tensors = ([sp.master] if sp is not None else []) + ([pack] if pack is not None else [])
-        n = comm.average_(tensors, participate)
+        params = [p for p in self.module.parameters()]
+        pieces = [p.data.reshape(-1).float() for p in params] + [b.reshape(-1).float() for _, b in bufs]
+        cnt = torch.tensor([1.0 if participate else 0.0])
+        pack = torch.cat(pieces + [cnt]) if pieces else cnt
+        if not participate:
+            pack.zero_()
+        comm.all_reduce_(pack)
+        n = int(round(float(pack[-1])))
         if n == 0:
             return 0
+        pack[:-1].div_(n)
         off = 0
         for p in params:
             k = p.numel()
@@ -69,16 +96,56 @@ class ModelAverager:
             if b.is_floating_point():
                 b.copy_(v)
             else:  # reference: integer layers use integer division (parallelSGD.go:26-54)
-                b.copy_(torch.floor(v + 1e-6).to(b.dtype))
+                b.copy_(torch.floor(v + 1e-3).to(b.dtype))
             off += k
-        if sp is not None:
-            sp.refresh_shadow()
         return n
+
+    @torch.no_grad()
+    def average_buffers_(self, comm: Comm):
+        """Average only the module buffers (BN running statistics and counters) over the
+        group.  Used by the synchronous gradient-all-reduce path, where parameters are
+        identical on every rank by construction: BN running statistics follow a linear
+        recurrence with rank-independent coefficients, so averaging them once at the end
+        of an epoch equals averaging them after every step (K = 1 reference semantics)."""
+        if comm.world == 1:
+            return
+        sp = self._space()
+        if sp is not None:
+            from ..ops import kernels as K
+            arena = sp.i64_arena_now()
+            seg = sp.state[sp.numel:]
+            K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, True)
+            comm.all_reduce_(seg)
+            # parameters are untouched: finish only over the buffer range (shadow not needed)
+            K.kavg_finish_(seg, 0, sp.count_idx - sp.numel, None, arena, sp.i64_off - sp.numel, sp.n_i64)
+            return
+        bufs = self._buffers()
+        if not bufs:
+            return
+        pack = torch.cat([b.reshape(-1).float() for _, b in bufs])
+        comm.all_reduce_(pack)
+        pack.div_(comm.world)
+        off = 0
+        for _, b in bufs:
+            k = b.numel()
+            v = pack[off:off + k].view_as(b)
+            b.copy_(v if b.is_floating_point() else torch.floor(v + 1e-3).to(b.dtype))
+            off += k
 
     @torch.no_grad()
     def broadcast_(self, comm: Comm, src: int = 0):
         """Make every worker hold rank ``src``'s model (init / elastic scale-up)."""
         if comm.world == 1:
+            return
+        sp = self._space()
+        if sp is not None:
+            comm.broadcast_(sp.state, src)     # parameters + buffers + counters slots
+            from ..ops import kernels as K
+            arena = sp.i64_arena_now()
+            if arena is not None:
+                # counters travel as int64 too (their fp32 slots are only packed per round)
+                comm.broadcast_(arena, src)
+            sp.refresh_shadow()
             return
         sp = getattr(self.module, "_kml_flat", None)
         if sp is not None:

@@ -151,7 +151,9 @@ class Worker:
                     if km is not None:
                         self.jobs[job] = km
                         self.job_fn[job] = msg["code_path"]
-            out = {"ok": True, "result": _jsonable(res), "seconds": time.perf_counter() - t0}
+            out = {"ok": True, "result": _jsonable(res), "seconds": time.perf_counter() - t0,
+                   "sync_seconds": float(ctx.extra.get("sync_seconds", 0.0)),
+                   "grad_rounds": int(ctx.extra.get("grad_rounds", 0))}
             if self.use_gpu:
                 import torch
                 out["hbm_bytes"] = int(torch.cuda.max_memory_allocated(self.device))

@@ -15,12 +15,25 @@ What changed underneath (MI355X-first):
   it is transparently replaced by the fused single-launch HIP optimizer with the same
   hyper-parameters (:func:`kubeml_amd.optim.from_torch`);
 * ``self.step(x, y)`` is an optional helper that runs forward / loss / backward /
-  optimizer as one hipGraph replay for static-shape batches.
+  optimizer as one hipGraph replay (engine/dp.py; one graph per batch shape, captured
+  without applying any update);
+* K = 1 with an SGD-family optimizer and ``batch % 64 == 0`` (every K-round is exactly
+  one minibatch): rounds in which every worker has data run as synchronous data
+  parallelism — ``self.step`` all-reduces the gradients over the worker group inside
+  the captured step, overlapped with backward.  Because the reference resets the
+  optimizer state every round, one step from a common model followed by a weight
+  average equals one step on the averaged gradient, so the result is the reference's
+  K = 1 model average (python/kubeml/kubeml/network.py:276-310) at a fraction of the
+  traffic; BN running statistics (a linear recurrence) are averaged once per epoch.
+  Any round that cannot take this path uses the fused weight average;
+* ``train()`` may return the loss as a device tensor: losses are accumulated on the
+  device and read back once per task, not once per minibatch.
 """
 from __future__ import annotations
 
 import logging
 import os
+import time
 from abc import ABC
 from typing import Any, Callable, Dict, Iterable, List, Sequence, Tuple, Union
 
@@ -65,8 +78,12 @@ class KubeModel(ABC):
         self.optimizer = None
         self.epoch = None
         self._averager = ModelAverager(network)
-        self._graphed = None
+        self._graphs: Dict[tuple, dict] = {}
         self._flat = None
+        self._sync_mode = "local"      # "grad": self.step all-reduces gradients (K=1 fast path)
+        self._grad_comm = None
+        self._synced_steps = 0
+        self.sync_seconds = 0.0
         ctx = current_task()
         if ctx is not None:
             ctx.extra["kubemodel"] = self
@@ -148,7 +165,7 @@ class KubeModel(ABC):
                     g["lr"] = lr
             opt = old
         elif old is not None and opt is not old:
-            self._graphed = None  # graphs captured the old optimizer's step
+            self._graphs.clear()  # graphs captured the old optimizer's step
         self.optimizer = opt
         if opt is not None and hasattr(opt, "set_grad_scale"):
             opt.set_grad_scale(1.0)
@@ -216,6 +233,18 @@ class KubeModel(ABC):
     def _num_batches(self):
         return -(-len(self._dataset.data) // self.batch_size) if len(self._dataset.data) else 0
 
+    def _grad_sync_ok(self, comm, K) -> bool:
+        """Can K=1 rounds run as synchronous gradient all-reduce (see module docstring)?"""
+        if os.environ.get("KUBEML_GRAD_SYNC", "1") == "0":
+            return False
+        if K != 1 or comm.world <= 1 or self.device is None:
+            return False
+        if self.batch_size % 64 != 0:
+            return False
+        if self.device.type == "cuda" and getattr(comm, "group", "missing") == "missing":
+            return False      # the captured collectives need a torch.distributed group
+        return getattr(self.optimizer, "kind", None) == "sgd" or type(self.optimizer) is torch.optim.SGD
+
     # ---- train (network.py:252-310, K-AVG) ------------------------------------------------
     def _train(self) -> float:
         self._on_train_start()
@@ -225,37 +254,95 @@ class KubeModel(ABC):
         # every worker starts the epoch from the same reference model
         with trace.span("broadcast"):
             self._averager.broadcast_(comm, 0)
-        assigned = split_minibatches(range(num_docs), N)[fid]
+        splits = split_minibatches(range(num_docs), N)
+        assigned = splits[fid]
         per = max(get_subset_period(K, self.batch_size, assigned), 1)
         intervals = list(range(assigned.start, assigned.stop, per))
         rounds = max_rounds(num_docs, N, K, self.batch_size) if comm.world > 1 else len(intervals)
-        self.logger.debug("subsets per iteration %d, rounds %d", per, rounds)
-        loss, num_iterations = 0.0, 0
+        # rounds in which EVERY worker has data (uneven shards differ by at most one doc)
+        full_rounds = min(-(-len(sp) // max(get_subset_period(K, self.batch_size, sp), 1)) for sp in splits)
+        grad_ok = self._grad_sync_ok(comm, K)
+        if grad_ok:
+            self._grad_comm = comm
+            self._prime_grad_sync()
+        self.logger.debug("subsets per iteration %d, rounds %d, grad-sync %s", per, rounds, grad_ok)
+        loss_host, loss_dev, num_iterations = 0.0, None, 0
         self.sync_seconds = 0.0
-        for r in range(rounds):
-            fault.point("round", rank=fid, epoch=self.epoch, round=r, task="train", job=self.args._job_id)
-            participate = r < len(intervals)
-            if participate:
-                i = intervals[r]
-                with trace.span("load", docs=per):
-                    self._dataset._load_train_data(start=i, end=min(assigned.stop, i + per))
-                num_iterations += self._num_batches()
-                self._on_iteration_start()
-                with trace.span("iteration", round=r):
-                    for idx, batch in enumerate(self._batches()):
-                        batch = self._batch_to_device(batch)
-                        loss += float(self.train(batch, idx))
-                self._on_iteration_end()
-            try:
-                import time as _t
-                t0 = _t.perf_counter()
-                with trace.span("average", round=r):
-                    self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
-                self.sync_seconds += _t.perf_counter() - t0
-            except Exception as e:  # the reference surfaces merge failures as MergeError
-                raise MergeError(e)
+        grad_rounds = 0
+        try:
+            for r in range(rounds):
+                fault.point("round", rank=fid, epoch=self.epoch, round=r, task="train", job=self.args._job_id)
+                participate = r < len(intervals)
+                self._sync_mode = "grad" if (grad_ok and r < full_rounds) else "local"
+                self._synced_steps = 0
+                nb = 0
+                if participate:
+                    i = intervals[r]
+                    with trace.span("load", docs=per):
+                        self._dataset._load_train_data(start=i, end=min(assigned.stop, i + per))
+                    nb = self._num_batches()
+                    num_iterations += nb
+                    self._on_iteration_start()
+                    with trace.span("iteration", round=r):
+                        for idx, batch in enumerate(self._batches()):
+                            batch = self._batch_to_device(batch)
+                            l = self.train(batch, idx)
+                            if isinstance(l, torch.Tensor):
+                                l = l.detach().reshape(()).float()
+                                loss_dev = l.clone() if loss_dev is None else loss_dev.add_(l)
+                            else:
+                                loss_host += float(l)
+                    self._on_iteration_end()
+                if self._sync_mode == "grad" and self._synced_steps == nb == 1:
+                    grad_rounds += 1      # weights already identical on every rank
+                    continue
+                try:
+                    t0 = time.perf_counter()
+                    with trace.span("average", round=r):
+                        self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
+                    self.sync_seconds += time.perf_counter() - t0
+                except Exception as e:  # the reference surfaces merge failures as MergeError
+                    raise MergeError(e)
+            if grad_rounds:
+                t0 = time.perf_counter()
+                with trace.span("average_buffers"):
+                    self._averager.average_buffers_(comm)
+                self.sync_seconds += time.perf_counter() - t0
+        finally:
+            self._sync_mode = "local"
+            self._grad_comm = None
         self._on_train_end()
-        return loss / max(num_iterations, 1)
+        if loss_dev is not None:
+            loss_host += float(loss_dev.item())
+        self.grad_rounds = grad_rounds
+        ctx = current_task()
+        if ctx is not None:   # reported to the job driver with the task result (metrics)
+            ctx.extra["sync_seconds"] = self.sync_seconds
+            ctx.extra["grad_rounds"] = grad_rounds
+        return loss_host / max(num_iterations, 1)
+
+    def _allreduce_grads_eager(self):
+        """Eager (CPU / no-graph) gradient average over the grad-sync group."""
+        comm = self._grad_comm
+        if self._flat is not None:
+            comm.all_reduce_(self._flat.grad)
+            self._flat.grad.div_(comm.world)
+            return
+        ps = [p for p in self._network.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in ps])
+        comm.all_reduce_(flat)
+        flat.div_(comm.world)
+        off = 0
+        for p in ps:
+            p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+            off += p.numel()
+
+    def _prime_grad_sync(self):
+        """Every rank, same point: one eager all-reduce on the gradient buffer so RCCL's
+        connections exist before any graph containing collectives is captured."""
+        comm = self._grad_comm
+        if self._flat is not None and comm is not None and self.device.type == "cuda":
+            comm.all_reduce_(self._flat.grad)
 
     # ---- validation (network.py:320-360) --------------------------------------------------
     def _on_validation_start(self):
@@ -269,13 +356,22 @@ class KubeModel(ABC):
         self._dataset._load_validation_data(start=assigned.start, end=assigned.stop)
         self._averager.broadcast_(comm, 0)
         acc, loss, nb = 0.0, 0.0, 0
+        dev_sums = None          # device-side [acc, loss] accumulation (one read-back)
         with torch.no_grad():
             for idx, batch in enumerate(self._batches()):
                 batch = self._batch_to_device(batch)
                 a, l = self.validate(batch, idx)
-                acc += float(a)
-                loss += float(l)
+                if isinstance(a, torch.Tensor) and isinstance(l, torch.Tensor):
+                    v = torch.stack([a.detach().reshape(()).double(), l.detach().reshape(()).double()])
+                    dev_sums = v if dev_sums is None else dev_sums.add_(v)
+                else:
+                    acc += float(a)
+                    loss += float(l)
                 nb += 1
+        if dev_sums is not None:
+            a, l = dev_sums.tolist()
+            acc += a
+            loss += l
         self._network.train()
         n = len(self._dataset.data) if self._dataset.data is not None else 0
         return acc / max(nb, 1), loss / max(nb, 1), n
@@ -320,35 +416,46 @@ class KubeModel(ABC):
             self._flat = flatten_module(self._network, self.device)
 
     # ---- MI355X helper: graph-captured step --------------------------------------------------
+    MAX_GRAPHS = 8
+
     def step(self, x, y, loss_fn=None):
         """forward + loss + backward + optimizer step for one batch; on the GPU the first
-        call for a given batch shape captures a hipGraph that later calls replay.
-        Returns the (device) loss tensor."""
+        call for a given batch shape captures a hipGraph (engine/dp.py) that later calls
+        replay.  In a K=1 grad-sync round the gradients are all-reduced over the worker
+        group inside the step.  Returns the (device) loss tensor."""
         from ..nn import backward_loss, cross_entropy
         loss_fn = loss_fn or cross_entropy
-        key = (tuple(x.shape), tuple(y.shape), x.dtype)
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
             self.optimizer.zero_grad()
             loss = loss_fn(self(x), y)
             loss.backward()
+            if self._sync_mode == "grad":
+                self._allreduce_grads_eager()
+                self._synced_steps += 1
             self.optimizer.step()
             return loss
-        g = self._graphed
-        if g is None or g["key"] != key:
-            from ..engine.step import GraphedTrainStep
+        grad = self._sync_mode == "grad"
+        comm = self._grad_comm if grad else None
+        key = (tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(loss_fn), grad,
+               id(comm) if comm is not None else None)
+        g = self._graphs.get(key)
+        if g is None:
+            from ..engine.dp import make_train_step
+            if len(self._graphs) >= self.MAX_GRAPHS:
+                self._graphs.pop(next(iter(self._graphs)))
             xs, ys = x.clone(), y.clone()
-
-            def fb():
-                self.optimizer.zero_grad()
-                l = loss_fn(self(xs), ys)
-                backward_loss(l)
-                return l
-            st = GraphedTrainStep(fb, self.optimizer.step, warmup=2)
+            st = make_train_step(self._network, self._flat, self.optimizer, loss_fn, xs, ys,
+                                 group=comm.group if comm is not None else None,
+                                 world=comm.world if comm is not None else 1,
+                                 graph_comm=os.environ.get("KUBEML_GRAPH_COMM", "1") != "0")
             st.capture()
-            g = self._graphed = {"key": key, "x": xs, "y": ys, "step": st}
+            g = self._graphs[key] = {"x": xs, "y": ys, "step": st}
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
-        return g["step"]()
+        loss = g["step"]()
+        if grad:
+            self._synced_steps += 1
+        return loss
 
     # ---- user hooks (network.py:463-476) --------------------------------------------------
     def configure_optimizers(self) -> torch.optim.Optimizer:

@@ -1,0 +1,134 @@
+"""Synchronous-DP (K=1) semantics and the bench launcher, on CPU.
+
+* KubeModel with K=1 and an SGD optimizer runs rounds as gradient all-reduce
+  (``self.step``); the reference averages WEIGHTS after each one-batch round and resets
+  the optimizer state (python/kubeml/kubeml/network.py:276-310, 121-128).  The two must
+  give the same model: checked with 2 thread-ranks against KUBEML_GRAD_SYNC=0 (the
+  weight-averaging path), with momentum (reset every round) and weight decay.
+* ``bench.py --gpus 2 --cpu-smoke`` launches 2 gloo ranks through torch.distributed.run
+  and reports one JSON line with both ranks joined and in sync.
+"""
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dataset(root):
+    from kubeml_amd.store.shards import ShardStore
+    rng = np.random.default_rng(0)
+    st = ShardStore(root)
+    if not st.exists("toy"):
+        x = rng.integers(0, 255, (64 * 9 + 40, 28, 28)).astype(np.uint8)   # uneven shards, ragged last doc
+        y = rng.integers(0, 10, len(x)).astype(np.int64)
+        st.create("toy", x, y, x[:128], y[:128])
+    return st
+
+
+def _train_two_ranks(store_dir, grad_sync, epochs=2, momentum=0.9):
+    from kubeml_amd.models.lenet import LeNet
+    from kubeml_amd.parallel.comm import ThreadComm
+    from kubeml_amd.sdk.context import TaskContext, reset_task, set_task
+    from kubeml_amd.sdk.dataset import KubeDataset
+    from kubeml_amd.sdk.model import KubeModel
+    from kubeml_amd.store.shards import ShardStore
+
+    class DS(KubeDataset):
+        def __init__(self):
+            super().__init__("toy")
+
+        def __getitem__(self, i):
+            return torch.from_numpy(self.data[i].astype(np.float32) / 255.0).unsqueeze(0), int(self.labels[i])
+
+        def __len__(self):
+            return len(self.data)
+
+    class Net(KubeModel):
+        def configure_optimizers(self):
+            return torch.optim.SGD(self.parameters(), lr=0.05, momentum=momentum, weight_decay=1e-4)
+
+        def train(self, batch, idx):
+            x, y = batch
+            return self.step(x, y, torch.nn.functional.cross_entropy)
+
+    old = os.environ.get("KUBEML_GRAD_SYNC")
+    os.environ["KUBEML_GRAD_SYNC"] = "1" if grad_sync else "0"
+    comms = ThreadComm.create(2)
+    store = ShardStore(store_dir)
+    out, errs = [None, None], []
+
+    def w(r):
+        try:
+            torch.manual_seed(0)
+            net = LeNet()
+            km = None
+            rounds = 0
+            for e in range(1, epochs + 1):
+                ctx = TaskContext(job_id="j", N=2, K=1, task="train", func_id=r, lr=0.05, batch_size=64, epoch=e,
+                                  comm=comms[r], store=store, store_dir=store_dir)
+                tok = set_task(ctx)
+                try:
+                    if km is None:
+                        km = Net(net, DS())
+                    km.start()
+                    rounds += ctx.extra.get("grad_rounds", 0)
+                finally:
+                    reset_task(tok)
+            sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+            out[r] = (sd, rounds)
+        except Exception as ex:  # pragma: no cover
+            import traceback
+            errs.append(traceback.format_exc())
+    torch.set_num_threads(1)
+    ts = [threading.Thread(target=w, args=(r,)) for r in range(2)]
+    try:
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+    finally:
+        if old is None:
+            os.environ.pop("KUBEML_GRAD_SYNC", None)
+        else:
+            os.environ["KUBEML_GRAD_SYNC"] = old
+    assert not errs, errs[0]
+    return out
+
+
+def test_k1_gradient_sync_equals_weight_average(tmp_path):
+    _dataset(str(tmp_path))
+    g = _train_two_ranks(str(tmp_path), grad_sync=True)
+    a = _train_two_ranks(str(tmp_path), grad_sync=False)
+    assert g[0][1] > 0 and a[0][1] == 0           # the grad-sync path really ran (and only there)
+    for k in g[0][0]:
+        # ranks agree with each other, and grad-sync agrees with the reference weight average
+        t0, t1, ref = g[0][0][k].double(), g[1][0][k].double(), a[0][0][k].double()
+        assert torch.allclose(t0, t1, atol=1e-6), k
+        assert torch.allclose(t0, ref, rtol=1e-4, atol=2e-5), (k, float((t0 - ref).abs().max()))
+
+
+def test_bench_cpu_smoke_launches_two_ranks():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-smoke", "--steps",
+                        "3", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2 and d["ranks_joined"] == 2 and d["ranks_in_sync"] is True
+
+
+def test_bench_rejects_more_gpus_than_visible():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 2 and "only 0 GPU" in r.stderr, (r.returncode, r.stderr[-2000:])

@@ -1,0 +1,169 @@
+"""Training-engine semantics on the MI355X.
+
+* ``KubeModel.step`` (graph per batch shape) applies exactly ONE optimizer update per
+  call: capture's warm-up runs on snapshots, so batches of shapes (B, B, b_last, B)
+  give the same master weights as the same number of eager fused-SGD steps — with
+  momentum 0.9 / dampening 0.1 across a ``reset_state()`` (device first-step flag).
+* K-AVG pack/finish kernels on the flat state buffer: divisor from the device count
+  slot, bf16 shadow refresh, int64 counters floored back (reference integer division).
+* ``bench.py`` end to end: the default path (timed steps + a measured epoch with
+  validation) and the 1-rank RCCL rehearsal of the captured, overlapped all-reduce.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _km(net, opt_fn):
+    from kubeml_amd.nn import flatten_module
+    from kubeml_amd.sdk.model import KubeModel
+
+    class M(KubeModel):
+        pass
+    km = M(net, None, gpu=True)
+    net.to(dev)
+    km.device = dev
+    km._flat = flatten_module(net)
+    km.optimizer = opt_fn(net.parameters())
+    return km
+
+
+def _batches():
+    g = torch.Generator(device=dev).manual_seed(7)
+    shapes = [32, 32, 20, 32, 32]
+    out = []
+    for b in shapes:
+        x = torch.randn(b, 32, 32, 8, device=dev, generator=g).to(torch.bfloat16)
+        x[..., 3:] = 0
+        y = torch.randint(0, 10, (b,), device=dev, generator=g)
+        out.append((x, y))
+    return out
+
+
+def _pair_run(monkeypatch, lr, data, reset_at=3):
+    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.optim import SGD
+
+    def opt(ps):
+        return SGD(ps, lr=lr, momentum=0.9, dampening=0.1, weight_decay=1e-4)
+    torch.manual_seed(0)
+    a = resnet18(10)
+    b = resnet18(10)
+    b.load_state_dict(a.state_dict())
+    ka, kb = _km(a, opt), _km(b, opt)
+    w0 = ka._flat.master.clone()
+
+    def run(km, graph):
+        if graph:
+            monkeypatch.delenv("KUBEML_NO_GRAPH", raising=False)
+        else:
+            monkeypatch.setenv("KUBEML_NO_GRAPH", "1")
+        losses = []
+        for i, (x, y) in enumerate(data):
+            if i == reset_at:
+                km.optimizer.reset_state()     # K-AVG round boundary
+            losses.append(float(km.step(x, y).detach()))
+        torch.cuda.synchronize()
+        return losses
+    la = run(ka, graph=True)
+    lb = run(kb, graph=False)
+    return ka, kb, a, b, w0, la, lb
+
+
+def test_graphed_step_first_update_matches_eager(monkeypatch):
+    """One batch at a large LR: an extra warm-up update would move the weights by
+    ~lr * |g| (~1e-2); the graph and eager paths agree to rounding."""
+    ka, kb, a, b, w0, la, lb = _pair_run(monkeypatch, 0.05, _batches()[:1])
+    upd = float((kb._flat.master - w0).abs().max())
+    d = float((ka._flat.master - kb._flat.master).abs().max())
+    assert upd > 1e-3 and d <= 1e-4 * upd, (d, upd)
+    assert torch.equal(ka._flat.shadow, ka._flat.master.to(torch.bfloat16))
+
+
+def test_graphed_step_applies_one_update_per_batch(monkeypatch):
+    """Shapes (B, B, b_last, B, B) with momentum/dampening across reset_state(): the
+    accumulated update equals the eager one (small LR keeps bf16 rounding from
+    amplifying atomic-order noise, which is chaotic at large LR on random data)."""
+    data = _batches()
+    ka, kb, a, b, w0, la, lb = _pair_run(monkeypatch, 1e-3, data)
+    assert len(ka._graphs) == 2                # one graph per batch shape, re-used
+    ua, ub = ka._flat.master - w0, kb._flat.master - w0
+    rel = float((ua - ub).norm() / ub.norm())
+    assert rel < 2e-2, (rel, la, lb)
+    ratio = float(ua.norm() / ub.norm())
+    assert 0.98 < ratio < 1.02, ratio          # 3 updates per batch would give ~3x
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), (la, lb)
+    # BN running statistics and counters advanced once per batch, not per warm-up
+    for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
+        if ba.dtype == torch.int64:
+            assert int(ba) == int(bb) == len(data), n
+        else:
+            assert torch.allclose(ba, bb, rtol=1e-2, atol=1e-3), n
+
+
+def test_kavg_pack_finish_kernels():
+    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.nn import flatten_module
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(0)
+    net = resnet18(10).to(dev)
+    sp = flatten_module(net)
+    arena = sp.i64_arena_now()
+    assert arena is not None and arena.numel() == sp.n_i64 > 0
+    arena.copy_(torch.arange(sp.n_i64, device=dev) * 3 + 1)
+    ref = sp.state[:sp.count_idx].clone()
+    n = 3     # emulate the SUM all-reduce of 3 identical contributing ranks
+    K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, True)
+    assert float(sp.state[sp.count_idx]) == 1.0
+    sp.state.mul_(n)
+    K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
+    got = sp.state[:sp.i64_off]
+    assert torch.allclose(got, ref[:sp.i64_off], rtol=1e-6, atol=1e-7)
+    assert torch.equal(sp.shadow, sp.master.to(torch.bfloat16))
+    assert torch.equal(arena, torch.arange(sp.n_i64, device=dev) * 3 + 1)
+    # mixed contributions: counters 1 and 4 over 2 ranks -> floor(5/2) = 2 (reference int division)
+    arena.fill_(1)
+    K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, True)
+    sp.state[sp.i64_off:sp.i64_off + sp.n_i64] += 4
+    sp.state[sp.count_idx] += 1
+    K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
+    assert torch.equal(arena, torch.full_like(arena, 2))
+    # BN buffers are views into the state buffer
+    bn = net.bn1
+    lo, hi = sp.state.data_ptr(), sp.state.data_ptr() + 4 * sp.state.numel()
+    assert lo <= bn.running_mean.data_ptr() < hi and lo <= bn.running_var.data_ptr() < hi
+
+
+def _bench(*extra, timeout=600):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(extra), capture_output=True,
+                       text=True, timeout=timeout, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_measures_epoch_with_validation():
+    d = _bench("--steps", "10", "--warmup", "2", "--batch", "128")
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["epoch_measured"] is True
+    assert d["val_images"] >= 10000 and d["epoch_time_s"] > d["epoch_train_s"] > 0
+    assert d["loss_first_last"][1] == d["loss_first_last"][1]
+
+
+def test_bench_rccl_rehearsal_overlapped_graph_comm():
+    d = _bench("--steps", "8", "--warmup", "2", "--batch", "128", "--force-comm", "--overlap", "on",
+               "--no-epoch")
+    assert d["ranks_in_sync"] is True and d["config"]["overlap_segments"] is True
+    assert d["config"]["graph_comm"] is True and d["rccl_world"] == 1
