@@ -13,6 +13,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
 #include <mutex>
@@ -75,6 +76,7 @@ bool parse_header(const char* h, size_t len, Npy* n) {
 
 struct Slot {
   void* host = nullptr;
+  bool pinned = false;  // hipHostMalloc'd (else malloc fallback: no GPU runtime)
   size_t cap = 0;
   long long row0 = 0, nrows = 0;
   int state = 0;  // 0 free, 1 filling, 2 ready, 3 in flight (H2D queued)
@@ -103,11 +105,19 @@ void fill_loop(Prefetcher* p) {
         if (p->stop) return true;
         if (p->next_fill >= p->ranges.size()) return false;
         Slot& c = p->slots[p->next_fill % p->slots.size()];
-        return c.state == 0;
+        return c.state == 0 || c.state == 3;
       });
       if (p->stop) return;
       idx = p->next_fill++;
       s = &p->slots[idx % p->slots.size()];
+      if (s->state == 3) {
+        // slot still owned by an H2D copy: wait for it here, off the caller's thread
+        // (the consumer never has to recycle slots, so take() cannot deadlock on it)
+        hipEvent_t ev = s->ev;
+        lk.unlock();
+        if (ev) (void)hipEventSynchronize(ev);
+        lk.lock();
+      }
       s->state = 1;
       r0 = p->ranges[idx].first;
       nr = p->ranges[idx].second;
@@ -208,8 +218,9 @@ KML_API void* kml_prefetch_new(void* npy, int nslots, long long max_rows) {
   p->slots.resize(nslots < 2 ? 2 : nslots);
   for (auto& s : p->slots) {
     s.cap = (size_t)max_rows * n->row_bytes;
-    if (hipHostMalloc(&s.host, s.cap, hipHostMallocDefault) != hipSuccess) s.host = malloc(s.cap);
-    hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+    s.pinned = hipHostMalloc(&s.host, s.cap, hipHostMallocDefault) == hipSuccess;
+    if (!s.pinned) s.host = malloc(s.cap);
+    if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) s.ev = nullptr;
   }
   p->th = std::thread(fill_loop, p);
   return p;
@@ -230,32 +241,59 @@ KML_API long long kml_prefetch_push(void* h, long long row0, long long nrows) {
   return id;
 }
 
-// take the next ready range and copy it to dst_dev on stream s; returns rows copied
+namespace {
+
+// wait for the next range in order; returns its slot (state stays 2 until released)
+Slot* wait_ready(Prefetcher* p) {
+  std::unique_lock<std::mutex> lk(p->mu);
+  if (p->next_take >= p->ranges.size()) return nullptr;
+  Slot* slot = &p->slots[p->next_take % p->slots.size()];
+  p->cv.wait(lk, [&] { return slot->state == 2 || p->stop; });
+  if (p->stop) return nullptr;
+  p->next_take++;
+  return slot;
+}
+
+}  // namespace
+
+// take the next ready range and copy it to dst_dev on stream s; returns rows copied.
+// The slot is handed back to the fill thread as "in flight" (state 3): the fill thread
+// waits for the copy's event before overwriting it.
 KML_API long long kml_prefetch_take(void* h, void* dst_dev, hipStream_t s) {
   Prefetcher* p = static_cast<Prefetcher*>(h);
-  Slot* slot;
-  {
-    std::unique_lock<std::mutex> lk(p->mu);
-    if (p->next_take >= p->ranges.size()) return -1;
-    // recycle slots whose copies completed
-    for (auto& sl : p->slots)
-      if (sl.state == 3 && hipEventQuery(sl.ev) == hipSuccess) sl.state = 0;
-    p->cv.notify_all();
-    slot = &p->slots[p->next_take % p->slots.size()];
-    p->cv.wait(lk, [&] { return slot->state == 2 || p->stop; });
-    if (p->stop) return -1;
-    p->next_take++;
-  }
+  Slot* slot = wait_ready(p);
+  if (!slot) return -1;
   const size_t bytes = (size_t)slot->nrows * p->src->row_bytes;
   if (hipMemcpyAsync(dst_dev, slot->host, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
-  hipEventRecord(slot->ev, s);
+  if (slot->ev) hipEventRecord(slot->ev, s);
   {
     std::lock_guard<std::mutex> lk(p->mu);
-    slot->state = 3;
+    slot->state = slot->ev ? 3 : 0;
   }
-  // a slot in flight is released lazily (next take) or here if already done
   p->cv.notify_all();
   return slot->nrows;
+}
+
+// host-destination take (CPU workers, host tests): synchronous memcpy, slot freed at once
+KML_API long long kml_prefetch_take_host(void* h, void* dst) {
+  Prefetcher* p = static_cast<Prefetcher*>(h);
+  Slot* slot = wait_ready(p);
+  if (!slot) return -1;
+  std::memcpy(dst, slot->host, (size_t)slot->nrows * p->src->row_bytes);
+  const long long n = slot->nrows;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    slot->state = 0;
+  }
+  p->cv.notify_all();
+  return n;
+}
+
+// ranges pushed but not yet taken
+KML_API long long kml_prefetch_pending(void* h) {
+  Prefetcher* p = static_cast<Prefetcher*>(h);
+  std::lock_guard<std::mutex> lk(p->mu);
+  return (long long)(p->ranges.size() - p->next_take);
 }
 
 KML_API void kml_prefetch_free(void* h) {
@@ -268,7 +306,8 @@ KML_API void kml_prefetch_free(void* h) {
   if (p->th.joinable()) p->th.join();
   for (auto& s : p->slots) {
     if (s.ev) { hipEventSynchronize(s.ev); hipEventDestroy(s.ev); }
-    if (s.host) (void)hipHostFree(s.host);
+    if (s.host && s.pinned) (void)hipHostFree(s.host);
+    else free(s.host);
   }
   delete p;
 }

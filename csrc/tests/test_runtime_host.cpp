@@ -25,6 +25,11 @@ void* kml_npy_open(const char*);
 void kml_npy_close(void*);
 int kml_npy_info(void*, long long*);
 int kml_npy_gather(void*, long long, long long, void*, int);
+void* kml_prefetch_new(void*, int, long long);
+long long kml_prefetch_push(void*, long long, long long);
+long long kml_prefetch_take_host(void*, void*);
+long long kml_prefetch_pending(void*);
+void kml_prefetch_free(void*);
 }
 
 static int failures = 0;
@@ -118,10 +123,49 @@ static void test_npy(const char* dir) {
   CHECK(kml_npy_open((path + ".missing").c_str()) == nullptr);
 }
 
+// prefetcher: ranges pushed ahead are filled by the background thread into a small ring
+// and taken in order, byte-exact; more ranges than slots exercises slot recycling; free
+// with ranges still queued must not hang or leak
+static void test_prefetch(const char* dir) {
+  std::string path = std::string(dir) + "/rt_prefetch.npy";
+  write_npy(path.c_str(), 1000, 5);
+  void* h = kml_npy_open(path.c_str());
+  CHECK(h != nullptr);
+  if (!h) return;
+  void* pf = kml_prefetch_new(h, 3, 64);
+  CHECK(pf != nullptr);
+  CHECK(kml_prefetch_push(pf, 0, 65) == -1);      // larger than a slot
+  CHECK(kml_prefetch_push(pf, 990, 20) == -2);    // out of range
+  std::vector<long long> r0s;
+  for (long long r = 0; r + 64 <= 1000; r += 64) {
+    CHECK(kml_prefetch_push(pf, r, 64) >= 0);
+    r0s.push_back(r);
+  }
+  CHECK(kml_prefetch_push(pf, 960, 40) >= 0);
+  r0s.push_back(960);
+  CHECK(kml_prefetch_pending(pf) == (long long)r0s.size());
+  std::vector<float> dst(64 * 5);
+  for (size_t i = 0; i < r0s.size(); ++i) {
+    const long long n = kml_prefetch_take_host(pf, dst.data());
+    CHECK(n == (r0s[i] == 960 ? 40 : 64));
+    bool ok = true;
+    for (long long k = 0; k < n && ok; ++k)
+      for (int c = 0; c < 5; ++c)
+        ok = ok && dst[k * 5 + c] == (float)((r0s[i] + k) * 1000 + c);
+    CHECK(ok);
+  }
+  CHECK(kml_prefetch_take_host(pf, dst.data()) == -1);   // nothing left
+  for (int i = 0; i < 6; ++i) kml_prefetch_push(pf, 64 * i, 64);
+  (void)kml_prefetch_take_host(pf, dst.data());
+  kml_prefetch_free(pf);                                  // 5 still queued
+  kml_npy_close(h);
+}
+
 int main(int argc, char** argv) {
   test_policy();
   test_merger();
   test_npy(argc > 1 ? argv[1] : "/tmp");
+  test_prefetch(argc > 1 ? argv[1] : "/tmp");
   if (failures) {
     std::fprintf(stderr, "%d failures\n", failures);
     return 1;

@@ -12,7 +12,11 @@ Differences that matter on MI355X:
   per-sample ``DataLoader``; the shipped ResNet function uses it to hand raw uint8
   images to the on-device augmentation kernel;
 * ``device_split(split)`` stages a whole split into HBM once (288 GB per GPU holds
-  every dataset the reference used) for kernels that gather batches on device.
+  every dataset the reference used) for kernels that gather batches on device;
+* on GPU workers a dataset with the batch hook is STREAMED: every minibatch of the
+  task is queued up front on a pinned prefetcher (sdk/loader.py) so batch i+1's host
+  copy and H2D overlap step i; ``self.data`` is then a row span (``len()`` works)
+  and batches arrive as device tensors through ``collate_device``.
 """
 from __future__ import annotations
 
@@ -65,6 +69,20 @@ class _KubeArgs:
         return cls(ctx.job_id, ctx.N, ctx.K, ctx.task, ctx.func_id, ctx.epoch, ctx.lr, ctx.batch_size)
 
 
+class _RowSpan:
+    """Rows [start, start+n) of a streamed split (data lives on the device stream)."""
+
+    def __init__(self, start: int, n: int):
+        self.start, self.n = start, n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        raise TypeError("streamed dataset rows are delivered as device batches (collate_device), "
+                        "not indexed on the host; set KUBEML_PREFETCH=0 for host indexing")
+
+
 class KubeDataset(data.Dataset, ABC):
 
     def __init__(self, dataset: str):
@@ -78,6 +96,8 @@ class KubeDataset(data.Dataset, ABC):
         self.num_docs = self._store.num_docs(dataset, "train")
         self.num_val_docs = self._store.num_docs(dataset, "test")
         self._resident = {}
+        self._streamers = {}       # split -> sdk.loader.SplitStreamer (GPU workers)
+        self._streaming = None     # split whose rows currently come from the stream
 
     # --- mode --------------------------------------------------------------------
     def _eval(self):
@@ -91,12 +111,56 @@ class KubeDataset(data.Dataset, ABC):
 
     # --- loading (document ids are 64-sample subsets, reference semantics) ----------
     def _load_train_data(self, start: int, end: int):
-        self.data, self.labels = self._store.load_docs(self.dataset, "train", start, end)
+        if self._streaming == "train":
+            self._stream_span("train", start, end)
+        else:
+            self.data, self.labels = self._store.load_docs(self.dataset, "train", start, end)
         self._train()
 
     def _load_validation_data(self, start: int, end: int):
-        self.data, self.labels = self._store.load_docs(self.dataset, "test", start, end)
+        if self._streaming == "test":
+            self._stream_span("test", start, end)
+        else:
+            self.data, self.labels = self._store.load_docs(self.dataset, "test", start, end)
         self._eval()
+
+    # --- pinned streaming (GPU workers) ----------------------------------------------
+    def _stream_ok(self, device) -> bool:
+        import os
+        return (device is not None and getattr(device, "type", None) == "cuda" and self.has_batch_hook()
+                and os.environ.get("KUBEML_PREFETCH", "1") != "0")
+
+    def _plan_stream(self, split: str, doc_ranges, batch_size: int, device) -> bool:
+        """Queue every minibatch of the coming task on the split's pinned stream; returns
+        False (numpy path) if streaming does not apply."""
+        self._streaming = None
+        if not self._stream_ok(device):
+            return False
+        try:
+            st = self._streamers.get(split)
+            if st is None:
+                from .loader import SplitStreamer
+                st = SplitStreamer(self._store, self.dataset, split, device)
+                self._streamers[split] = st
+            st.plan(doc_ranges, batch_size)
+        except (RuntimeError, TypeError):
+            return False
+        self._streaming = split
+        return True
+
+    def _stream_span(self, split: str, start: int, end: int):
+        from ..api.types import STORAGE_SUBSET_SIZE
+        st = self._streamers[split]
+        r0, r1 = start * STORAGE_SUBSET_SIZE, min(end * STORAGE_SUBSET_SIZE, st.n)
+        self.data = _RowSpan(r0, max(0, r1 - r0))
+        self.labels = st.labels[r0:r1]
+
+    def _stream_end(self):
+        self._streaming = None
+
+    def collate_device(self, x, y):
+        """Batch hook for streamed device batches (default: as-is)."""
+        return x, y
 
     def _close(self):
         pass

@@ -1,0 +1,140 @@
+"""Pinned, asynchronous shard streaming into HBM.
+
+The reference's hot loader queries 64-sample Mongo documents, unpickles and
+``vstack``s them, then a per-sample ``DataLoader`` collates batches that the user code
+moves to the GPU (python/kubeml/kubeml/dataset.py:184-223, network.py:284-295).
+
+Here a dataset split is one memory-mapped ``.npy`` (store/shards.py).  For GPU workers
+whose dataset hands whole batches to the device (``collate_batch`` hook, e.g.
+:class:`~kubeml_amd.sdk.vision.ImageDataset`), :class:`PinnedBatchStream` moves the
+rows of every minibatch of a task ahead of time:
+
+    background thread (csrc/runtime/loader.cpp, kml_prefetch_*):
+        mmap rows -> pinned host slot (ring of ``nslots``)
+    copy stream:      hipMemcpyAsync pinned slot -> device ring buffer, event E_i
+    compute stream:   waits on E_i, runs the batch's kernels, records F_i
+
+so batch i+1's host copy and H2D run while step i computes; a device buffer is only
+overwritten after the compute stream has passed ``F`` of its previous batch.  All
+ranges of a task are pushed up front (in order), so the copy of a round's first batch
+also overlaps the previous round's last step and its model average.
+Labels (a few hundred KB) are kept on the device per split.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..utils import trace
+
+_NP2TORCH = {np.dtype("uint8"): torch.uint8, np.dtype("int8"): torch.int8, np.dtype("float32"): torch.float32,
+             np.dtype("float16"): torch.float16, np.dtype("int64"): torch.int64, np.dtype("int32"): torch.int32}
+
+
+class PinnedBatchStream:
+    """Ordered row ranges of one ``.npy`` split streamed into HBM through pinned memory."""
+
+    def __init__(self, view, device: torch.device, max_rows: int, nslots: int = 4):
+        from .._native import RT
+        if not getattr(view, "_h", None):
+            raise RuntimeError("native npy view unavailable")
+        self.RT = RT
+        self.view = view
+        self.device = device
+        self.max_rows = int(max_rows)
+        self.nslots = int(nslots)
+        arr = view.arr
+        if arr.dtype not in _NP2TORCH:
+            raise TypeError(f"unsupported dtype {arr.dtype}")
+        self.row_shape = tuple(arr.shape[1:])
+        self.dtype = _NP2TORCH[arr.dtype]
+        self.h = RT.raw("kml_prefetch_new", view._h, self.nslots, self.max_rows)
+        if not self.h:
+            raise RuntimeError("kml_prefetch_new failed")
+        self.copy_stream = torch.cuda.Stream(device=device)
+        self.bufs = [torch.empty((self.max_rows,) + self.row_shape, dtype=self.dtype, device=device)
+                     for _ in range(self.nslots)]
+        self.free = [None] * self.nslots          # compute-stream events: buffer consumed
+        self.k = 0                                 # batches taken so far
+        self.last_slot = None
+
+    def push(self, row0: int, nrows: int) -> int:
+        r = self.RT.raw("kml_prefetch_push", self.h, int(row0), int(nrows))
+        if r < 0:
+            raise ValueError(f"prefetch push ({row0}, {nrows}) rejected ({r})")
+        return r
+
+    def pending(self) -> int:
+        return int(self.RT.raw("kml_prefetch_pending", self.h))
+
+    def take(self) -> torch.Tensor:
+        """Device tensor of the next range (valid until ``nslots - 1`` more takes)."""
+        cur = torch.cuda.current_stream(self.device)
+        if self.last_slot is not None:
+            # everything the consumer enqueued for the previous batch precedes this point
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.free[self.last_slot] = ev
+        i = self.k % self.nslots
+        buf = self.bufs[i]
+        with trace.span("h2d", batch=self.k):
+            if self.free[i] is not None:
+                self.copy_stream.wait_event(self.free[i])
+            n = self.RT.raw("kml_prefetch_take", self.h, buf.data_ptr(), self.copy_stream.cuda_stream)
+            if n < 0:
+                raise RuntimeError(f"kml_prefetch_take failed ({n})")
+            done = torch.cuda.Event()
+            done.record(self.copy_stream)
+        cur.wait_event(done)
+        self.k += 1
+        self.last_slot = i
+        return buf[:n]
+
+    def close(self):
+        if self.h:
+            torch.cuda.current_stream(self.device).synchronize()
+            self.RT.raw("kml_prefetch_free", self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SplitStreamer:
+    """Per-split state of a dataset on a GPU worker: the stream and device labels."""
+
+    def __init__(self, store, dataset: str, split: str, device: torch.device):
+        self.data_view, self.label_view = store.open(dataset, split)
+        self.n = int(self.data_view.shape[0])
+        self.device = device
+        lab = np.ascontiguousarray(self.label_view.arr).reshape(-1).astype(np.int64)
+        self.labels = torch.from_numpy(lab).to(device)
+        self.stream: Optional[PinnedBatchStream] = None
+        self.batches: List[Tuple[int, int]] = []   # planned (row0, nrows) in order
+        self.pos = 0
+
+    def plan(self, doc_ranges: Sequence[Tuple[int, int]], batch_size: int, subset: int = 64):
+        """Queue every minibatch row range of the given document rounds, in order."""
+        if self.stream is None or self.stream.max_rows != batch_size or self.stream.pending():
+            if self.stream is not None:
+                self.stream.close()
+            self.stream = PinnedBatchStream(self.data_view, self.device, batch_size)
+        self.batches, self.pos = [], 0
+        for d0, d1 in doc_ranges:
+            r0, r1 = d0 * subset, min(d1 * subset, self.n)
+            for s in range(r0, r1, batch_size):
+                nr = min(batch_size, r1 - s)
+                self.stream.push(s, nr)
+                self.batches.append((s, nr))
+
+    def next(self):
+        r0, nr = self.batches[self.pos]
+        self.pos += 1
+        x = self.stream.take()
+        assert x.shape[0] == nr
+        return x, self.labels[r0:r0 + nr]

@@ -222,6 +222,12 @@ class KubeModel(ABC):
         is not shuffled, network.py:284)."""
         ds = self._dataset
         bs = self.batch_size
+        if ds._streaming is not None:
+            st = ds._streamers[ds._streaming]
+            for _ in range(self._num_batches()):
+                x, y = st.next()
+                yield ds.collate_device(x, y)
+            return
         if ds.has_batch_hook():
             n = len(ds.data)
             for i in range(0, n, bs):
@@ -266,6 +272,9 @@ class KubeModel(ABC):
             self._grad_comm = comm
             self._prime_grad_sync()
         self.logger.debug("subsets per iteration %d, rounds %d, grad-sync %s", per, rounds, grad_ok)
+        # every minibatch of this task queued on the pinned stream (GPU, batch-hook datasets)
+        self._dataset._plan_stream("train", [(i, min(assigned.stop, i + per)) for i in intervals],
+                                   self.batch_size, self.device)
         loss_host, loss_dev, num_iterations = 0.0, None, 0
         self.sync_seconds = 0.0
         grad_rounds = 0
@@ -311,6 +320,7 @@ class KubeModel(ABC):
         finally:
             self._sync_mode = "local"
             self._grad_comm = None
+            self._dataset._stream_end()
         self._on_train_end()
         if loss_dev is not None:
             loss_host += float(loss_dev.item())
@@ -353,6 +363,7 @@ class KubeModel(ABC):
         self._on_validation_start()
         comm = self._comm()
         assigned = split_minibatches(range(self._dataset.num_val_docs), self.args._N)[self.args._func_id]
+        self._dataset._plan_stream("test", [(assigned.start, assigned.stop)], self.batch_size, self.device)
         self._dataset._load_validation_data(start=assigned.start, end=assigned.stop)
         self._averager.broadcast_(comm, 0)
         acc, loss, nb = 0.0, 0.0, 0
@@ -373,6 +384,7 @@ class KubeModel(ABC):
             acc += a
             loss += l
         self._network.train()
+        self._dataset._stream_end()
         n = len(self._dataset.data) if self._dataset.data is not None else 0
         return acc / max(nb, 1), loss / max(nb, 1), n
 

@@ -112,6 +112,7 @@ class ShardStore:
         self.root = os.path.join(root, "datasets")
         os.makedirs(self.root, exist_ok=True)
         self._lock = threading.Lock()
+        self._views = {}
 
     def _dir(self, name: str) -> str:
         if not name or "/" in name or name.startswith("."):
@@ -157,6 +158,8 @@ class ShardStore:
         with self._lock:
             if not self.exists(name):
                 raise KubeMLException("Dataset does not exist", 404)
+            for key in [k for k in self._views if k[0] == name]:
+                self._views.pop(key)
             shutil.rmtree(self._dir(name))
 
     def manifest(self, name: str) -> dict:
@@ -184,10 +187,23 @@ class ShardStore:
         return int(self.manifest(name)[split]["docs"])
 
     def open(self, name: str, split: str) -> Tuple[NpyView, NpyView]:
-        if not self.exists(name):
+        """mmap views of a split, cached per (name, split, manifest mtime): a K-AVG round
+        loads its documents without re-opening and re-parsing the files."""
+        mf = os.path.join(self._dir(name), "manifest.json")
+        try:
+            stamp = os.path.getmtime(mf)
+        except OSError:
             raise DatasetNotFoundError()
+        key = (name, split)
+        with self._lock:
+            hit = self._views.get(key)
+            if hit is not None and hit[0] == stamp:
+                return hit[1]
         d = self._dir(name)
-        return NpyView(os.path.join(d, f"{split}_data.npy")), NpyView(os.path.join(d, f"{split}_labels.npy"))
+        views = (NpyView(os.path.join(d, f"{split}_data.npy")), NpyView(os.path.join(d, f"{split}_labels.npy")))
+        with self._lock:
+            self._views[key] = (stamp, views)
+        return views
 
     def load_docs(self, name: str, split: str, start: int, end: int) -> Tuple[np.ndarray, np.ndarray]:
         """Rows of documents [start, end) — the reference's ``_id in [start, end-1]`` query."""

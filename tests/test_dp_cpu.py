@@ -63,11 +63,14 @@ def _train_two_ranks(store_dir, grad_sync, epochs=2, momentum=0.9):
     comms = ThreadComm.create(2)
     store = ShardStore(store_dir)
     out, errs = [None, None], []
+    nets = []
+    for _ in range(2):          # the global RNG is shared by threads: initialise up front
+        torch.manual_seed(0)
+        nets.append(LeNet())
 
     def w(r):
         try:
-            torch.manual_seed(0)
-            net = LeNet()
+            net = nets[r]
             km = None
             rounds = 0
             for e in range(1, epochs + 1):
