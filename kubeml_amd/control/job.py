@@ -89,7 +89,7 @@ class TrainJob:
     def __init__(self, task: TrainTask, *, code_path: str, store_dir: str, pool_factory: Callable,
                  on_metrics: Callable, on_finish: Callable, request_update: Optional[Callable] = None,
                  history_store=None, max_parallelism: int = 8, freeze_parallelism: bool = False,
-                 task_timeout: float = 3600.0):
+                 task_timeout: float = 3600.0, inventory=None):
         self.task = task
         self.id = task.job.id
         self.req = task.request
@@ -125,6 +125,9 @@ class TrainJob:
         self.last_grad_rounds = 0
         self.done = threading.Event()
         self.resume_from = getattr(opts, "resume_from", "") or ""
+        self.inventory = inventory
+        self._shrink_to = None
+        self.checksums: List[Dict] = []   # per epoch: {rank: (start, end)} model checksums
         self._pending_restore = None
         self.start_epoch = 1
 
@@ -173,6 +176,22 @@ class TrainJob:
             self.pool = self.pool_factory(self)
             self.max_parallelism = min(self.max_parallelism, self.pool.n)
             self.parallelism = self._clamp(self.parallelism)
+
+    def _maybe_release_idle(self):
+        """Epoch boundary: an elastic job holding more slots than its parallelism gives
+        the idle ones back when another job is waiting for slots (the pool is rebuilt on
+        the kept GPUs and restores the just-written checkpoint)."""
+        inv = self.inventory
+        if inv is None or self.pool is None or self.pool.broken or not self.have_ckpt:
+            return
+        if inv.waiting > 0 and self.pool.n > self.parallelism:
+            self.log.info("releasing idle workers", keep=self.parallelism, had=self.pool.n)
+            self._shrink_to = self.parallelism
+            self.pool.broadcast({"op": "release", "job": self.id}, timeout=60)
+            self.pool.shutdown()
+            self.pool = None
+            self.max_parallelism = self.parallelism
+            self._pending_restore = self.ckpt
 
     def _fanout(self, kind: str, ranks: List[int], **kw) -> Dict[int, Dict]:
         msgs = {r: self._msg(kind, **kw) for r in ranks}
@@ -239,6 +258,7 @@ class TrainJob:
             if not bad:
                 self._pending_restore = None
                 losses = [float(v["result"]["loss"]) for v in ok.values()]
+                self.checksums.append({r: (v.get("start_checksum"), v.get("end_checksum")) for r, v in ok.items()})
                 hbm = max((v.get("hbm_bytes", 0) for v in ok.values()), default=0)
                 self.last_sync_seconds = max((v.get("sync_seconds", 0.0) for v in ok.values()), default=0.0)
                 self.last_grad_rounds = max((v.get("grad_rounds", 0) for v in ok.values()), default=0)
@@ -350,7 +370,9 @@ class TrainJob:
                 self._push_metrics()
                 self.log.info("epoch finished", epoch=self.epoch, loss=loss, seconds=elapsed,
                               parallelism=self.parallelism, images_per_second=self.images_per_second,
-                              sync_seconds=self.last_sync_seconds, grad_sync_rounds=self.last_grad_rounds)
+                              sync_seconds=self.last_sync_seconds, grad_sync_rounds=self.last_grad_rounds,
+                              checksums={str(r): c for r, c in sorted(self.checksums[-1].items())}
+                              if self.checksums else None)
                 if not self.static and self.epoch < E:
                     self._next_parallelism()
                 if self.validate_every and self.epoch % self.validate_every == 0 and self.epoch != E:
@@ -360,6 +382,7 @@ class TrainJob:
                         self.log.error("error performing validation", error=repr(e))
                 self._checkpoint()
                 self._save_history()
+                self._maybe_release_idle()
                 if self._stop.is_set():
                     self.accuracy_reached = True
                     self.exit_err = "job was force stopped"

@@ -69,3 +69,40 @@ class StaticPolicy(SchedulerPolicy):
 
     def finish(self, job_id):
         self._seen.discard(job_id)
+
+
+class ScriptedPolicy(SchedulerPolicy):
+    """Deterministic policy: the i-th decision for a job returns ``seq[i]`` (the last
+    value repeats), clamped to [1, max_parallelism].  Drives reproducible elastic
+    experiments (north-star config 4: VGG-16 at P = 2 -> 4 -> 8) and resize tests;
+    select it with ``KUBEML_POLICY=scripted:2,4,8``."""
+
+    def __init__(self, seq, max_parallelism: int = 8):
+        self.seq = [int(x) for x in seq] or [1]
+        self.max_parallelism = max_parallelism
+        self._n = {}
+        import threading
+        self._lock = threading.Lock()
+
+    def decide(self, job_id, default, parallelism, elapsed):
+        with self._lock:
+            i = self._n.get(job_id, 0)
+            self._n[job_id] = i + 1
+        p = self.seq[min(i, len(self.seq) - 1)]
+        return max(1, min(p, self.max_parallelism)), ("create" if i == 0 else "update")
+
+    def finish(self, job_id):
+        with self._lock:
+            self._n.pop(job_id, None)
+
+
+def policy_from_spec(spec: str, max_parallelism: int) -> SchedulerPolicy:
+    """``throughput`` (default) | ``static`` | ``scripted:p1,p2,...``."""
+    spec = (spec or "throughput").strip()
+    if spec == "throughput":
+        return ThroughputPolicy(max_parallelism=max_parallelism)
+    if spec == "static":
+        return StaticPolicy(max_parallelism=max_parallelism)
+    if spec.startswith("scripted:"):
+        return ScriptedPolicy(spec.split(":", 1)[1].split(","), max_parallelism=max_parallelism)
+    raise ValueError(f"unknown policy {spec!r}")

@@ -6,8 +6,9 @@ updates, metrics and finish notifications; the model averaging it is named after
 happens in the job's RedisAI merger.  Here the PS:
 
 * owns the node's worker slots (one per MI355X; CPU slots when no GPU) and hands each
-  job a set of them — jobs run concurrently on disjoint GPUs, a job waits when none is
-  free;
+  job a set of them — jobs run concurrently on disjoint GPUs; a static job takes exactly
+  its parallelism, an elastic job up to ``max_parallelism`` and returns idle slots at an
+  epoch boundary when another job is waiting; a job waits while too few are free;
 * starts a :class:`TrainJob` thread per task (``POST /start``) whose worker pool is
   spawned on the job's GPUs (``runtime.pool``);
 * relays ``POST /update/{id}`` (JobState) to the job, keeps Prometheus gauges from
@@ -38,25 +39,50 @@ log = logging.getLogger("kubeml.ps")
 
 
 class Inventory:
-    """Worker slots of this node (GPU indices, or CPU slots)."""
+    """Worker slots of this node (GPU indices, or CPU slots).
+
+    ``acquire(want, at_least)`` blocks until ``at_least`` slots are free, then takes up
+    to ``want`` of them; ``waiting`` counts blocked acquirers so elastic jobs can hand
+    idle slots back when another job needs them."""
 
     def __init__(self, n: int, use_gpu: bool):
         self.n = n
         self.use_gpu = use_gpu
         self.free = list(range(n))
         self.cv = threading.Condition()
+        self.waiting = 0
+        self.reclaimers = []      # callables that free idle slots (e.g. the inference pool)
 
-    def acquire(self, want: int, stop: Optional[threading.Event] = None, timeout: float = 86400) -> List[int]:
+    def acquire(self, want: int, stop: Optional[threading.Event] = None, timeout: float = 86400,
+                at_least: int = 1) -> List[int]:
         want = max(1, min(want, self.n))
+        at_least = max(1, min(at_least, want))
         deadline = time.time() + timeout
         with self.cv:
-            while not self.free:
-                if (stop is not None and stop.is_set()) or time.time() > deadline:
-                    raise KubeMLException("no free workers", 503)
-                self.cv.wait(0.5)
+            self.waiting += 1
+            try:
+                while len(self.free) < at_least:
+                    if (stop is not None and stop.is_set()) or time.time() > deadline:
+                        raise KubeMLException("no free workers", 503)
+                    if self.reclaimers:
+                        self.cv.release()
+                        try:
+                            for r in self.reclaimers:
+                                r()
+                        finally:
+                            self.cv.acquire()
+                        if len(self.free) >= at_least:
+                            break
+                    self.cv.wait(0.5)
+            finally:
+                self.waiting -= 1
             got = self.free[:want]
             self.free = self.free[want:]
             return got
+
+    def n_free(self) -> int:
+        with self.cv:
+            return len(self.free)
 
     def release(self, ids: List[int]):
         with self.cv:
@@ -90,14 +116,23 @@ class ParameterServer:
         self._infer_pool: Optional[WorkerPool] = None
         self._infer_lock = threading.Lock()
         self.finished: Dict[str, Optional[str]] = {}
+        self.inventory.reclaimers.append(self._reclaim_infer)
 
     # ------------------------------------------------------------------ pools
     def _pool_for(self, job: TrainJob) -> WorkerPool:
+        """Slots for a job's worker pool.  A static job takes exactly its parallelism; an
+        elastic one takes its parallelism at least and up to ``max_parallelism`` when
+        free (idle GPUs stay warm for scale-ups, the analogue of the reference's Fission
+        pool), and gives slots back above ``_shrink_to`` (recovery, or another job
+        waiting: see TrainJob._maybe_release_idle)."""
         with self._lock:
             ids = self.alloc.get(job.id)
         shrink = getattr(job, "_shrink_to", None)
+        job._shrink_to = None
         if ids is None:
-            ids = self.inventory.acquire(self.max_parallelism, stop=job._stop)
+            p = max(1, min(job.parallelism, self.max_parallelism))
+            want = p if job.static else self.max_parallelism
+            ids = self.inventory.acquire(want, stop=job._stop, at_least=p)
             with self._lock:
                 self.alloc[job.id] = ids
         elif shrink is not None and shrink < len(ids):
@@ -122,7 +157,8 @@ class ParameterServer:
                            pool_factory=self._pool_for, on_metrics=self._job_metrics, on_finish=self.job_finished,
                            request_update=(self.scheduler.update_job if self.scheduler else None),
                            history_store=self.histories, max_parallelism=self.max_parallelism,
-                           freeze_parallelism=self.freeze, task_timeout=self.task_timeout)
+                           freeze_parallelism=self.freeze, task_timeout=self.task_timeout,
+                           inventory=self.inventory)
             self.jobs[task.job.id] = job
         self.metrics.task_started("train")
         job.start()
@@ -214,6 +250,20 @@ class ParameterServer:
         if not rep.get("ok"):
             raise KubeMLException(rep.get("error", "inference failed"), int(rep.get("code", 500)))
         return rep["result"]
+
+    def _reclaim_infer(self):
+        """A training job is waiting for slots: shut the idle inference pool down (it is
+        re-created on the next inference request)."""
+        if not self._infer_lock.acquire(blocking=False):
+            return
+        try:
+            if self._infer_pool is not None:
+                self._infer_pool.shutdown()
+                self._infer_pool = None
+                self.inventory.release(getattr(self, "_infer_ids", []))
+                self.metrics.task_finished("inference")
+        finally:
+            self._infer_lock.release()
 
     def close(self):
         for j in list(self.jobs.values()):

@@ -22,7 +22,7 @@ from ..store import service as storage_service
 from ..store.shards import ShardStore
 from .controller import Controller
 from .http import Server
-from .policy import ThroughputPolicy
+from .policy import policy_from_spec
 from .ps import ParameterServer
 from .scheduler import Scheduler
 
@@ -31,7 +31,10 @@ log = logging.getLogger("kubeml.server")
 
 class KubeMLServer:
     def __init__(self, cfg: Optional[Config] = None, n_workers: Optional[int] = None, use_gpu: Optional[bool] = None,
-                 worker_env: Optional[Dict[str, str]] = None, task_timeout: float = 3600.0, worker_threads: int = 1):
+                 worker_env: Optional[Dict[str, str]] = None, task_timeout: float = 3600.0, worker_threads: int = 1,
+                 policy=None):
+        """policy: a SchedulerPolicy, or a spec string (``KUBEML_POLICY``: throughput |
+        static | scripted:p1,p2,...); default throughput (reference policy.go)."""
         self.cfg = cfg or Config.load()
         n, gpu = detect_workers(self.cfg)
         if n_workers is not None:
@@ -41,7 +44,10 @@ class KubeMLServer:
         max_p = self.cfg.max_parallelism if self.cfg.max_parallelism > 0 else n
         self.metrics = Metrics()
         self.shards = ShardStore(self.cfg.store_dir)
-        self.policy = ThroughputPolicy(max_parallelism=max_p)
+        import os
+        if policy is None or isinstance(policy, str):
+            policy = policy_from_spec(policy or os.environ.get("KUBEML_POLICY", "throughput"), max_p)
+        self.policy = policy
         self.scheduler = Scheduler(policy=self.policy, max_parallelism=max_p)
         self.ps = ParameterServer(self.cfg.store_dir, n, gpu, metrics=self.metrics, scheduler=self.scheduler,
                                   max_parallelism=max_p,

@@ -153,6 +153,8 @@ class Worker:
                         self.job_fn[job] = msg["code_path"]
             out = {"ok": True, "result": _jsonable(res), "seconds": time.perf_counter() - t0,
                    "sync_seconds": float(ctx.extra.get("sync_seconds", 0.0)),
+                   "start_checksum": ctx.extra.get("start_checksum"),
+                   "end_checksum": ctx.extra.get("end_checksum"),
                    "grad_rounds": int(ctx.extra.get("grad_rounds", 0))}
             if self.use_gpu:
                 import torch

@@ -260,6 +260,9 @@ class KubeModel(ABC):
         # every worker starts the epoch from the same reference model
         with trace.span("broadcast"):
             self._averager.broadcast_(comm, 0)
+        ctx = current_task()
+        if ctx is not None and os.environ.get("KUBEML_CHECKSUMS", "1") != "0":
+            ctx.extra["start_checksum"] = self.model_checksum()
         splits = split_minibatches(range(num_docs), N)
         assigned = splits[fid]
         per = max(get_subset_period(K, self.batch_size, assigned), 1)
@@ -325,11 +328,25 @@ class KubeModel(ABC):
         if loss_dev is not None:
             loss_host += float(loss_dev.item())
         self.grad_rounds = grad_rounds
-        ctx = current_task()
+        if ctx is not None and os.environ.get("KUBEML_CHECKSUMS", "1") != "0":
+            ctx.extra["end_checksum"] = self.model_checksum()
         if ctx is not None:   # reported to the job driver with the task result (metrics)
             ctx.extra["sync_seconds"] = self.sync_seconds
             ctx.extra["grad_rounds"] = grad_rounds
         return loss_host / max(num_iterations, 1)
+
+    @torch.no_grad()
+    def model_checksum(self) -> float:
+        """sum(|x|) over the model's parameters and floating buffers (fp64; one device
+        reduction + one read-back).  Reported per task so the job driver can check that
+        every active worker holds the same model (elastic resize, K-AVG)."""
+        sp = self._flat
+        if sp is not None and getattr(sp, "state", None) is not None:
+            return float(sp.state[:sp.i64_off].double().abs().sum())
+        tot = torch.zeros((), dtype=torch.float64)
+        for t in list(self._network.parameters()) + [b for b in self._network.buffers() if b.is_floating_point()]:
+            tot += t.detach().double().abs().sum().cpu()
+        return float(tot)
 
     def _allreduce_grads_eager(self):
         """Eager (CPU / no-graph) gradient average over the grad-sync group."""
