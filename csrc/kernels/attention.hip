@@ -10,6 +10,12 @@
 //   bwd   : dq-kernel per query tile (also computes D = rowsum(dO * O)), dkv-kernel per
 //           key tile; both recompute P from the saved LSE — no atomics, deterministic.
 //
+// Attention-probability dropout (HF BERT attention_probs_dropout_prob): keep mask
+// Z[b,h,q,key] = hash(seed ^ salt, step, b, h, q, key) >= p * 2^32 recomputed in all three
+// kernels (nothing stored).  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
+// the undropped probabilities; backward: dV = (P (.) Z/(1-p))^T dO, dP = (dO V^T) (.) Z/(1-p),
+// dS = P (.) (dP - D) with D = rowsum(dO (.) O) (unchanged by the mask).
+//
 // MFMA v_mfma_f32_16x16x32_bf16, wave64: lane l holds A[l&15][8(l>>4)+j],
 // B[8(l>>4)+j][l&15], C[4(l>>4)+i][l&15].  Each wave owns 16 queries (or keys) so the
 // softmax statistics of a row live in one lane column (l&15) and the 4 lanes sharing it
@@ -38,6 +44,36 @@ struct AttnArgs {
   int ldq, ldk, ldv, ldo, lddo, ldout, lddq, lddk, lddv;
   int B, H, L;
   float scale;         // softmax scale (1/sqrt(64))
+  const float* ctr;    // [seed, step] (device) for attention dropout, or null
+  unsigned salt;
+  float pdrop;         // dropout probability (0: off)
+};
+
+__device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
+  unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+// per-kernel dropout state: keep(q, key) = 1/(1-p) or 0
+struct Drop {
+  unsigned k0, k1, thr;
+  float sc;
+  int L;
+  bool on;
+  __device__ void init(const AttnArgs& a, int bh) {
+    on = a.ctr != nullptr && a.pdrop > 0.f;
+    L = a.L;
+    if (on) {
+      k0 = (unsigned)a.ctr[0] ^ a.salt;
+      k1 = (unsigned)a.ctr[1] * 0x632BE5ABu ^ (unsigned)bh * 0x5851F42Du;
+      thr = (unsigned)(a.pdrop * 4294967296.0f);
+      sc = 1.f / (1.f - a.pdrop);
+    }
+  }
+  __device__ __forceinline__ float keep(int q, int key) const {
+    return ahash(k0, k1, (unsigned)q * (unsigned)L + (unsigned)key) >= thr ? sc : 0.f;
+  }
 };
 
 __device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
@@ -113,6 +149,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
   const float sl2 = a.scale * LOG2E;
   const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
+  Drop drop;
+  drop.init(a, bh);
 
   TileRegs rq, rk, rv;
   tile_load(rq, Qb, a.ldq, q0, L, tid);
@@ -176,6 +214,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
     m2 = mn;
 #pragma unroll
     for (int d = 0; d < 4; ++d) acc[d] *= alpha;
+    if (drop.on) {
+      const int qq = q0 + 16 * w + (lane & 15);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[t][i] *= drop.keep(qq, kb * 64 + 16 * t + 4 * g + i);
+    }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -207,6 +252,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   const float sl2 = a.scale * LOG2E;
   const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
 
+  Drop drop;
+  drop.init(a, bh);
   const bf16_t* qrow = a.q + (long long)(b * L + (qok ? q : 0)) * a.ldq + h * 64;
   const bf16_t* dorow = a.dout + (long long)(b * L + (qok ? q : 0)) * a.lddo + h * 64;
   const bf16_t* orow = a.o + (long long)(b * L + (qok ? q : 0)) * a.ldo + h * 64;
@@ -262,7 +309,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
         float v = s[t][i] * sl2;
         if (bias && key < L) v += bias[key] * LOG2E;
         const float p = key < L ? exp2f(v - lse) : 0.f;
-        s[t][i] = p * (dp[t][i] - D);
+        const float dpv = drop.on ? dp[t][i] * drop.keep(q, key) : dp[t][i];
+        s[t][i] = p * (dpv - D);
       }
     const bf16x8_t d0 = pack_p(s[0], s[1]), d1 = pack_p(s[2], s[3]);
 #pragma unroll
@@ -296,6 +344,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
   const bf16x8_t kf0 = load_frag_g(krow, 0, g, kok), kf1 = load_frag_g(krow, 1, g, kok);
   const bf16x8_t vf0 = load_frag_g(vrow, 0, g, kok), vf1 = load_frag_g(vrow, 1, g, kok);
   const float kb2 = !kok ? -INFINITY : (a.bias ? a.bias[(long long)b * L + key] * LOG2E : 0.f);
+  Drop drop;
+  drop.init(a, bh);
 
   f32x4_t adk[4], adv[4];
 #pragma unroll
@@ -342,8 +392,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * t + 4 * g + i;
         const float p = exp2f(s[t][i] * sl2 + kb2 - sL[r]);
-        s[t][i] = p;
-        dp[t][i] = p * (dp[t][i] - sD[r]);
+        const float z = drop.on ? drop.keep(qb * 64 + r, key) : 1.f;
+        s[t][i] = p * z;
+        dp[t][i] = p * (dp[t][i] * z - sD[r]);
       }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
     const bf16x8_t d0 = pack_p(dp[0], dp[1]), d1 = pack_p(dp[2], dp[3]);
@@ -371,15 +422,18 @@ bool aligned16(const void* p) { return (((unsigned long long)p) & 15ull) == 0; }
 }  // namespace
 
 // q/k/v/out: token-major [B*L, ld*] bf16, head h at column 64h (head_dim must be 64)
+// ctr/salt/pdrop: attention-probability dropout (ctr null or pdrop 0: none)
 KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* out, float* lse,
                          const float* bias, int ldq, int ldk, int ldv, int ldout, int B, int H, int L, float scale,
-                         hipStream_t s) {
+                         const float* ctr, int salt, float pdrop, hipStream_t s) {
   if (L <= 0 || B <= 0 || H <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldout % 4) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v)) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = q; a.k = k; a.v = v; a.out = out; a.lse = lse; a.bias = bias;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldout = ldout;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop;
+  if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_attn_fwd, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();
 }
@@ -388,7 +442,7 @@ KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
 KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                          const float* lse, float* dsum, const float* bias, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                          int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv, int B, int H,
-                         int L, float scale, hipStream_t s) {
+                         int L, float scale, const float* ctr, int salt, float pdrop, hipStream_t s) {
   if (L <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
@@ -396,6 +450,8 @@ KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   a.bias = bias; a.dq = dq; a.dk = dk; a.dv = dv;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop;
+  if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_attn_bwd_dq, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_attn_bwd_dkv, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();

@@ -1,0 +1,484 @@
+// gemm.hip — large bf16 GEMMs (BERT-size linears) on gfx950 MFMA, fp32 accumulate.
+//
+//   C[m][n] = act( sum_k A[m][k] * B[n][k] + bias[n] )        (bf16 out, optional pre-act copy)
+//   C[m][n] = beta * C[m][n] + sum_k A[m][k] * B[n][k]         (fp32 out: weight gradients)
+//   C[m][n] += sum_{k in slice z} A[m][k] * B[n][k]            (fp32 split-K, agent atomics)
+//
+// Operand layouts (row = m for A, n for B):  KC: X[row][k] (k contiguous), KS: X[k][row].
+// The three GEMMs of a linear layer y = x W^T + b (x [T][in], W [out][in]):
+//   forward  y[T][out]   A = x   (KC)  B = W   (KC)
+//   dgrad    dx[T][in]   A = dy  (KC)  B = W   (KS: reduction over out, rows of W)
+//   wgrad    dW[out][in] A = dy  (KS)  B = x   (KS: reduction over tokens)
+//
+// CDNA4 mapping (CDNA guide §5):
+// * 512 threads = 8 wave64 as 2 (M) x 4 (N); a BM x BN block tile (256 or 128 per side),
+//   wave tile (BM/2) x (BN/4) of v_mfma_f32_16x16x32_bf16 fragments, BK = 64.
+// * Operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+//   instruction), two LDS stages: the DMA of K-tile t+1 is issued right after the barrier
+//   that publishes tile t and overlaps tile t's MFMAs; one barrier per K-step.  The LDS
+//   image is lane-linear, so bank swizzles go on the per-lane SOURCE address and are undone
+//   on the fragment read (guide §5.4 rule 21): KC tiles [rows][64] (128 B rows) use
+//   chunk ^= row & 7 (ds_read_b128), KS tiles [64][R] a row-bit permutation read with the
+//   transposing ds_read_b64_tr_b16 — both conflict-free (tools/lds_banks.py).
+// * The MFMA is issued with the B fragment as its first operand, so a lane's accumulator
+//   holds 4 consecutive OUTPUT COLUMNS of one output row: the epilogue (bias, erf-GELU,
+//   bf16 pack, or fp32 beta / atomic accumulate) stores 8 or 16 contiguous bytes per lane
+//   straight from registers — no LDS staging pass.
+// * Out-of-range rows / K columns read a zero page instead of branching (counted vmcnt
+//   stays straight-line); stores are masked.  XCD-aware block order (guide T1).
+//
+// Replaces hipBLASLt/Tensile on the BERT hot path (the reference has no BERT; SURVEY §2.8
+// north-star config 5).
+#include "kml_common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short v4s_t;
+
+struct GemmArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  void* c;
+  bf16_t* c2;          // optional pre-activation copy (bf16 out only)
+  const float* bias;   // [N] fp32 or null
+  const bf16_t* zp;    // >= 16 zero bytes
+  long long lda, ldb, ldc;
+  int M, N, K;
+  int act;             // 0 none, 1 erf-GELU
+  float beta;
+  int kchunk;          // split-K slice length (multiple of 64)
+};
+
+constexpr int BK = 64;
+constexpr int NT = 512;
+
+template <int R>
+__device__ __forceinline__ int swz_ks(int r) {  // K-strided [64][R] chunk swizzle (R >= 128)
+  return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+}
+
+__device__ __forceinline__ bf16x8_t frag_kc(const char* lds, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = 4 * ks + (lane >> 4);
+  return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
+}
+
+template <int R>
+__device__ __forceinline__ bf16x8_t frag_ks(const char* lds, int row0, int ks, int lane) {
+  const int il = lane & 15, g = lane >> 4;
+  const int col = row0 + 4 * (il & 3);
+  const int k0 = 32 * ks + 8 * g + (il >> 2);
+  const int k1 = k0 + 4;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  const char* p0 = lds + k0 * (2 * R) + ((ch ^ swz_ks<R>(k0)) << 4) + within;
+  const char* p1 = lds + k1 * (2 * R) + ((ch ^ swz_ks<R>(k1)) << 4) + within;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p0));
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p1));
+  bf16x8_t f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return f;
+}
+
+// One operand's DMA plan: NI instructions per wave per stage.  KC: tile [R][64], 8 rows
+// per 1 KiB instruction; KS: tile [64][R], 512/R k-rows per instruction.
+template <int R, bool KC>
+struct Stager {
+  static constexpr int NI = R / 64;   // (R * 64 * 2 bytes) / 1 KiB / 8 waves
+  const bf16_t* base[NI];              // source of K-tile 0 (before the kb offset)
+  int lim[NI];                         // KC: k offset of the lane's chunk; KS: k-row in tile
+  bool ok[NI];                         // row (KC) / column chunk (KS) in range
+  long long kstep;                     // address delta per K element
+  __device__ void init(const bf16_t* p, long long ld, int r0, int rows, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int u = wave * NI + j;
+      if constexpr (KC) {
+        const int row = 8 * u + (lane >> 3);
+        const int chunk = (lane & 7) ^ (row & 7);
+        ok[j] = r0 + row < rows;
+        base[j] = p + (long long)(ok[j] ? r0 + row : 0) * ld + chunk * 8;
+        lim[j] = chunk * 8;
+      } else {
+        constexpr int CPR = R / 8, RPI = 64 / CPR;
+        const int krow = RPI * u + lane / CPR;
+        const int chunk = (lane % CPR) ^ swz_ks<R>(krow);
+        ok[j] = r0 + chunk * 8 < rows;
+        base[j] = p + (long long)krow * ld + (ok[j] ? r0 + chunk * 8 : 0);
+        lim[j] = krow;
+      }
+    }
+    kstep = KC ? 1 : ld;
+  }
+  __device__ __forceinline__ void issue(char* lds, int kb, int kend, const bf16_t* zp, int wave) const {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const bool in = ok[j] && kb + lim[j] < kend;
+      const bf16_t* src = in ? base[j] + (long long)kb * kstep : zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
+                                       0);
+    }
+  }
+};
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a contiguous run of
+// tiles (N fastest) so neighbouring tiles share A/B panels in its L2.  Bijective.
+__device__ __forceinline__ void xcd_tile(int& tx, int& ty, int& tz) {
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+  const int nwg = gx * gy * (int)gridDim.z;
+  const int lin = ((int)blockIdx.z * gy + (int)blockIdx.y) * gx + (int)blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, x = lin & 7, k = lin >> 3;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  tx = id % gx;
+  const int t = id / gx;
+  ty = t % gy;
+  tz = t / gy;
+}
+
+// epilogue: lane holds C[m][n .. n+3], m = .. + (lane & 15), n = .. + 4 * (lane >> 4)
+template <int OUT, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                              int wn, int lane) {
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int m = m0 + wm * WM + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (OUT == 0) {
+        if (g.bias) {
+          const float4 bb = *reinterpret_cast<const float4*>(g.bias + n);
+          v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+        }
+        const long long off = (long long)m * g.ldc + n;
+        if (g.c2) {
+          uint2 p;
+          p.x = pack_bf2(v[0], v[1]);
+          p.y = pack_bf2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(g.c2 + off) = p;
+        }
+        if (g.act == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+        }
+        uint2 p;
+        p.x = pack_bf2(v[0], v[1]);
+        p.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.c) + off) = p;
+      } else if constexpr (OUT == 1) {
+        float4* p = reinterpret_cast<float4*>(static_cast<float*>(g.c) + (long long)m * g.ldc + n);
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g.beta != 0.f) {
+          o = *p;
+          o.x *= g.beta; o.y *= g.beta; o.z *= g.beta; o.w *= g.beta;
+        }
+        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        *p = o;
+      } else {
+        float* p = static_cast<float*>(g.c) + (long long)m * g.ldc + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __hip_atomic_fetch_add(p + r, v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// OUT: 0 bf16 (bias, act, optional pre-act copy), 1 fp32 beta, 2 fp32 atomic add (split-K)
+// S: LDS stages.  S = 2: the DMA of tile t+1 overlaps tile t's MFMAs, vmcnt(0) per step.
+// S = 3: tiles t+1 and t+2 in flight; each step waits with a COUNTED vmcnt for tile t only,
+// so one tile's DMA stays in flight across the raw s_barrier (CDNA guide §5 "Pipelining
+// across barriers"; trailing steps re-issue the last tile into a stage nobody reads, so
+// the count never changes).
+template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S>
+__global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
+  constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int NI = BM / 64 + BN / 64;   // DMA instructions per wave per stage
+  static_assert(S * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
+
+  int tx, ty, tz;
+  xcd_tile(tx, ty, tz);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = ty * BM, n0 = tx * BN;
+  const int kbeg = tz * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  Stager<BM, A_KC> sa;
+  Stager<BN, B_KC> sb;
+  sa.init(g.a, g.lda, m0, g.M, wave, lane);
+  sb.init(g.b, g.ldb, n0, g.N, wave, lane);
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int st) {
+    char* dst = smem + st * STAGE;
+    sa.issue(dst, kbeg + kt * BK, kend, g.zp, wave);
+    sb.issue(dst + A_BYTES, kbeg + kt * BK, kend, g.zp, wave);
+  };
+  auto compute = [&](int st) {
+    const char* sA = smem + st * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[MR], bfr[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bfr[j] = B_KC ? frag_kc(sB, wn * WN + j * 16, ks, lane) : frag_ks<BN>(sB, wn * WN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        af[i] = A_KC ? frag_kc(sA, wm * WM + i * 16, ks, lane) : frag_ks<BM>(sA, wm * WM + i * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    if constexpr (S == 2) {
+      issue(0, 0);
+      for (int t = 0; t < nk; ++t) {
+        // stage t landed for this wave's DMAs; after the barrier, for every wave's; and every
+        // wave finished reading the other stage (its fragment reads were waited for by the MFMAs)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+        compute(t & 1);
+      }
+    } else {
+      const int last = nk - 1;
+      issue(0, 0);
+      issue(min(1, last), 1);
+      int cur = 0;
+      for (int t = 0; t < nk; ++t) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");   // tile t done, t+1 may fly
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int nx = cur == 0 ? 2 : cur - 1;                       // (t + 2) % 3
+        issue(min(t + 2, last), nx);
+        compute(cur);
+        cur = cur == 2 ? 0 : cur + 1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");               // drain redundant tail DMAs
+    }
+  }
+
+  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// 256 x 256 tile, BK = 32 slots in a 4-deep LDS ring (4 x 32 KB): TWO K-tiles stay in
+// flight behind the one being consumed, and the fragments of tile t+1 are read from LDS
+// while tile t's MFMAs run (register double buffer), so neither the DMA latency nor the
+// LDS read latency sits on the MFMA path.  Per step: counted vmcnt for tile t+1, one
+// raw barrier, DMA of tile t+3 into the slot tile t-1 vacated, ds_reads of t+1, MFMAs of
+// t.  (The CDNA guide's half-tile 8-phase idea at the granularity this code can express.)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8_t frag_kc64(const char* lds, int row0, int lane) {  // [R][32] tiles
+  const int r = row0 + (lane & 15);
+  const int c = lane >> 4;
+  return *reinterpret_cast<const bf16x8_t*>(lds + r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
+}
+
+template <int R, bool KC>
+struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (512/R rows / KiB)
+  static constexpr int NI = R / 128;
+  const bf16_t* base[NI];
+  int lim[NI];
+  bool ok[NI];
+  long long kstep;
+  __device__ void init(const bf16_t* p, long long ld, int r0, int rows, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int u = wave * NI + j;
+      if constexpr (KC) {
+        const int row = 16 * u + (lane >> 2);
+        const int chunk = (lane & 3) ^ ((row >> 1) & 3);
+        ok[j] = r0 + row < rows;
+        base[j] = p + (long long)(ok[j] ? r0 + row : 0) * ld + chunk * 8;
+        lim[j] = chunk * 8;
+      } else {
+        constexpr int CPR = R / 8, RPI = 64 / CPR;
+        const int krow = RPI * u + lane / CPR;
+        const int chunk = (lane % CPR) ^ swz_ks<R>(krow);
+        ok[j] = r0 + chunk * 8 < rows;
+        base[j] = p + (long long)krow * ld + (ok[j] ? r0 + chunk * 8 : 0);
+        lim[j] = krow;
+      }
+    }
+    kstep = KC ? 1 : ld;
+  }
+  __device__ __forceinline__ void issue(char* lds, int kb, int kend, const bf16_t* zp, int wave) const {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const bool in = ok[j] && kb + lim[j] < kend;
+      const bf16_t* src = in ? base[j] + (long long)kb * kstep : zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
+                                       0);
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC, int OUT>
+__global__ __launch_bounds__(NT) void k_gemm4(GemmArgs g) {
+  constexpr int BM = 256, BN = 256, BK32 = 32;
+  constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
+  constexpr int A_BYTES = BM * BK32 * 2, B_BYTES = BN * BK32 * 2, SLOT = A_BYTES + B_BYTES;
+  constexpr int NI = BM / 128 + BN / 128;
+  __shared__ __attribute__((aligned(1024))) char smem[4 * SLOT];
+
+  int tx, ty, tz;
+  xcd_tile(tx, ty, tz);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = ty * BM, n0 = tx * BN;
+  const int kbeg = tz * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK32 - 1) / BK32 : 0;
+
+  Stager32<BM, A_KC> sa;
+  Stager32<BN, B_KC> sb;
+  sa.init(g.a, g.lda, m0, g.M, wave, lane);
+  sb.init(g.b, g.ldb, n0, g.N, wave, lane);
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int kt, int slot) {
+    char* dst = smem + slot * SLOT;
+    sa.issue(dst, kbeg + kt * BK32, kend, g.zp, wave);
+    sb.issue(dst + A_BYTES, kbeg + kt * BK32, kend, g.zp, wave);
+  };
+  auto read = [&](int slot, bf16x8_t* af, bf16x8_t* bfr) {
+    const char* sA = smem + slot * SLOT;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      bfr[j] = B_KC ? frag_kc64(sB, wn * WN + j * 16, lane) : frag_ks<BN>(sB, wn * WN + j * 16, 0, lane);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+      af[i] = A_KC ? frag_kc64(sA, wm * WM + i * 16, lane) : frag_ks<BM>(sA, wm * WM + i * 16, 0, lane);
+  };
+  auto mma = [&](const bf16x8_t* af, const bf16x8_t* bfr) {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+  if (nk > 0) {
+    const int last = nk - 1;
+    bf16x8_t a0[MR], b0[NR], a1[MR], b1[NR];
+    issue(0, 0);
+    issue(min(1, last), 1);
+    issue(min(2, last), 2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");   // tile 0 landed
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read(0, a0, b0);
+    // two K-tiles per trip so the fragment double buffer has static register names
+    for (int t = 0; t < nk; t += 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");       // tile t+1 landed, t+2 flies
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // reads of tile t done
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue(min(t + 3, last), (t + 3) & 3);                           // into tile t-1's slot
+      read((t + 1) & 3, a1, b1);
+      mma(a0, b0);
+      if (t + 1 >= nk) break;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue(min(t + 4, last), (t + 4) & 3);
+      read((t + 2) & 3, a0, b0);
+      mma(a1, b1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane);
+}
+
+template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S = (3 * (BM + BN) * BK * 2 <= 160 * 1024) ? 3 : 2>
+int launch(GemmArgs g, int splits, hipStream_t s) {
+  splits = splits < 1 ? 1 : splits;
+  int chunk = (g.K + splits - 1) / splits;
+  chunk = ((chunk + BK - 1) / BK) * BK;
+  g.kchunk = chunk > 0 ? chunk : BK;
+  const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, z);
+  hipLaunchKernelGGL((k_gemm<BM, BN, A_KC, B_KC, OUT, S>), grid, dim3(NT), 0, s, g);
+  KML_LAUNCH_CHECK();
+}
+
+template <bool A_KC, bool B_KC, int OUT>
+int launch4(GemmArgs g, int splits, hipStream_t s) {
+  splits = splits < 1 ? 1 : splits;
+  int chunk = (g.K + splits - 1) / splits;
+  chunk = ((chunk + 63) / 64) * 64;
+  g.kchunk = chunk > 0 ? chunk : 64;
+  const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
+  dim3 grid((g.N + 255) / 256, (g.M + 255) / 256, z);
+  hipLaunchKernelGGL((k_gemm4<A_KC, B_KC, OUT>), grid, dim3(NT), 0, s, g);
+  KML_LAUNCH_CHECK();
+}
+
+template <bool A_KC, bool B_KC, int OUT>
+int by_tile(const GemmArgs& g, int tile, int splits, hipStream_t s) {
+  switch (tile) {
+    case 0: return launch<256, 256, A_KC, B_KC, OUT>(g, splits, s);
+    case 1: return launch<256, 128, A_KC, B_KC, OUT>(g, splits, s);
+    case 2: return launch<128, 256, A_KC, B_KC, OUT>(g, splits, s);
+    case 3: return launch<128, 128, A_KC, B_KC, OUT>(g, splits, s);
+    case 4: return launch<128, 128, A_KC, B_KC, OUT, 2>(g, splits, s);   // 2 stages: 2 blocks per CU
+    case 5: return launch4<A_KC, B_KC, OUT>(g, splits, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// layout: 0 = forward (A KC, B KC), 1 = dgrad (A KC, B KS), 2 = wgrad (A KS, B KS)
+// out:    0 = bf16 (+bias, act, pre-act copy), 1 = fp32 beta, 2 = fp32 atomic (split-K)
+// tile:   0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128 (BM x BN; 3-stage where LDS allows),
+//         4 = 128x128 with 2 stages (64 KB: two blocks per CU), 5 = 256x256 BK=32 4-slot ring
+// Host contract (checked by ops/gemm.py): N % 4 == 0, ldc % 4 == 0, K-contiguous leading
+// dimensions % 8 == 0, 16-byte aligned pointers; a zero page of >= 16 bytes.
+KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, void* c, long long ldc,
+                     bf16_t* c2, const float* bias, const bf16_t* zp, int M, int N, int K, int layout, int out,
+                     int act, float beta, int tile, int splits, hipStream_t s) {
+  GemmArgs g;
+  g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.zp = zp;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K;
+  if (M <= 0 || N <= 0) return 0;
+  if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
+  if (layout == 0 && out == 1) return by_tile<true, true, 1>(g, tile, 1, s);
+  if (layout == 0 && out == 2) return by_tile<true, true, 2>(g, tile, splits, s);
+  if (layout == 1 && out == 2) return by_tile<true, false, 2>(g, tile, splits, s);
+  if (layout == 1 && out == 0) return by_tile<true, false, 0>(g, tile, 1, s);
+  if (layout == 2 && out == 1) return by_tile<false, false, 1>(g, tile, 1, s);
+  if (layout == 2 && out == 2) return by_tile<false, false, 2>(g, tile, splits, s);
+  return (int)hipErrorInvalidValue;
+}

@@ -5,12 +5,13 @@ HuggingFace ``BertForMaskedLM`` architecture and ``state_dict`` names
 ``cls.predictions.transform.*``, ``cls.predictions.decoder.weight`` tied to the word
 embeddings) on the MI355X layers:
 
-* token-major bf16 activations ``[B*L, 768]``; every GEMM is the MFMA implicit-GEMM
-  kernel (fused QKV projection: one ``[T, 2304]`` GEMM per layer);
+* token-major bf16 activations ``[B*L, 768]``; every large GEMM runs on the hand-written
+  LDS-DMA MFMA kernel (csrc/kernels/gemm.hip): fused QKV projection (one ``[T, 2304]`` GEMM
+  per layer), bias + erf-GELU in the FFN1 epilogue, fp32 split-K weight gradients;
 * attention is the fused flash-attention kernel (scores stay in LDS/registers);
 * LayerNorm with fused residual add, erf GELU, counter-based dropout (hidden dropout
-  0.1; attention-probability dropout is not applied by the fused kernel — set
-  ``attention_dropout=0`` semantics);
+  0.1, and attention-probability dropout 0.1 applied inside the fused attention kernels
+  from the same counter-based mask in forward and backward);
 * the MLM head runs only on the masked positions (``mlm_positions``, Google BERT's
   ``masked_lm_positions``), saving ~85 % of the 30522-way decoder GEMM.
 """
@@ -38,7 +39,7 @@ class _Dense(tnn.Module):
 class BertLayer(tnn.Module):
     def __init__(self, hidden=768, heads=12, inter=3072, eps=1e-12, dropout=0.1, rng=None):
         super().__init__()
-        self.attention = SelfAttention(hidden, heads, post_ln_eps=eps)
+        self.attention = SelfAttention(hidden, heads, post_ln_eps=eps, attn_dropout=dropout, rng=rng)
         self.intermediate = _Dense(hidden, inter)
         self.output = _Dense(inter, hidden, ln_eps=eps)
         self.act = GELU()
@@ -48,7 +49,7 @@ class BertLayer(tnn.Module):
     def forward(self, h, B: int, L: int, bias=None):
         a = self.drop1(self.attention(h, B, L, bias))
         h1 = self.attention.ln(a, residual=h)
-        i = self.act(self.intermediate.dense(h1))
+        i = self.intermediate.dense(h1, act="gelu")   # erf-GELU in the GEMM epilogue
         o = self.drop2(self.output.dense(i))
         return self.output.LayerNorm(o, residual=h1)
 
@@ -150,11 +151,59 @@ class BertForMaskedLM(tnn.Module):
             idx = (mlm_positions + base).reshape(-1).contiguous()
             h = gather_rows(h, idx)
         t = self.cls.predictions.transform
-        z = t.LayerNorm(self.act(t.dense(h)))
+        z = t.LayerNorm(t.dense(h, act="gelu"))
         logits = self.cls.predictions.decoder(z)
         if labels is None:
             return logits
         return cross_entropy(logits, labels.reshape(-1), ignore_index=-100, return_correct=return_correct)
+
+
+    def stages(self, ids, token_type_ids=None, attention_mask=None, mlm_positions=None, labels=None, n: int = 3):
+        """Forward split into ``n`` stages for backward-overlapped gradient all-reduce
+        (engine/staged.py): stage 0 = embeddings + the first encoder layers, the last stage
+        ends with the MLM head and returns the loss.  Each stage's parameters are one
+        contiguous range of the flat gradient buffer (reverse registration order; the tied
+        word embedding belongs to stage 0, whose backward finishes its gradient last).
+        Returns (stage callables h -> h, per-stage parameter lists)."""
+        B, L = ids.shape
+        layers = list(self.bert.encoder.layer)
+        per = -(-len(layers) // n)
+        groups = [layers[i * per:(i + 1) * per] for i in range(n)]
+        bias = None
+        if attention_mask is not None:
+            bias = ((1.0 - attention_mask.float()) * -10000.0).reshape(B, L).contiguous()
+
+        def first(_x):
+            if self.training and ids.is_cuda:
+                self.rng.advance(ids.device)
+            h = self.bert.embeddings(ids, token_type_ids)
+            for lay in groups[0]:
+                h = lay(h, B, L, bias)
+            return h
+
+        def mid(g):
+            def f(h):
+                for lay in g:
+                    h = lay(h, B, L, bias)
+                return h
+            return f
+
+        def last(h):
+            for lay in groups[-1]:
+                h = lay(h, B, L, bias)
+            if mlm_positions is not None:
+                base = (torch.arange(B, device=ids.device) * L).view(B, 1)
+                h = gather_rows(h, (mlm_positions + base).reshape(-1).contiguous())
+            t = self.cls.predictions.transform
+            z = t.LayerNorm(t.dense(h, act="gelu"))
+            return cross_entropy(self.cls.predictions.decoder(z), labels.reshape(-1), ignore_index=-100)
+        fns = [first] + [mid(g) for g in groups[1:-1]] + [last]
+        params = [list(self.bert.embeddings.parameters()) + [p for l in groups[0] for p in l.parameters()]]
+        params += [[p for l in g for p in l.parameters()] for g in groups[1:-1]]
+        tied = {id(p) for p in params[0]}
+        params.append([p for l in groups[-1] for p in l.parameters()] +
+                      [p for p in self.cls.parameters() if id(p) not in tied])
+        return fns, params
 
 
 def bert_base_mlm(**kw) -> BertForMaskedLM:

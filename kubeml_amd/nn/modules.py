@@ -13,6 +13,7 @@ kernels directly into ``p.grad`` storage (``+=``), matching torch's semantics.
 from __future__ import annotations
 
 import math
+from typing import Optional
 import os
 
 import torch
@@ -35,67 +36,26 @@ def _on_gpu(x):
     return x.is_cuda
 
 
-# Plain large linears (BERT: M = batch x seq tokens, no fused activation) run their forward
-# and input-gradient GEMMs on hipBLASLt (torch.mm / addmm, bias in its epilogue): at
-# M = 8192, K, N = 768-3072 it measured 1.7-2x the MFMA implicit-GEMM kernel
-# (tools/gemm_micro.py).  The fp32 weight-gradient accumulation, fused-ReLU heads, small-M
-# layers and every convolution stay on the HIP kernels.  KUBEML_LINEAR_BLAS=0/1 forces a side.
-_LIN_BLAS = os.environ.get("KUBEML_LINEAR_BLAS", "auto")
+# Large linears (BERT: M = batch x seq tokens) run their three GEMMs on the hand-written
+# 256/128-tile LDS-DMA MFMA kernel of csrc/kernels/gemm.hip (ops/gemm.py): bias and erf-GELU
+# in the forward epilogue, the weight gradient accumulated in fp32 straight into the flat
+# gradient storage (split-K with agent atomics).  Small-M layers and fused-ReLU heads stay on
+# the implicit-GEMM conv kernels.  KUBEML_LINEAR_BLAS=1 routes the large ones to hipBLASLt
+# instead (A/B comparison only; not used by default).
+_LIN_BLAS = os.environ.get("KUBEML_LINEAR_BLAS", "0")
 
 
-def _linear_blas(M, ip, op, relu):
-    if relu or _LIN_BLAS == "0":
-        return False
-    return _LIN_BLAS == "1" or (M >= 2048 and ip >= 512 and op >= 512)
-
-
-# Weight gradient of those linears: hipBLASLt bf16 x bf16 -> fp32 with beta = 1 straight into
-# the fp32 gradient storage (aten addmm.dtype_out).  The BERT profile had the MFMA wgrad
-# kernel at 242 us per [16384] x [3072 x 768] GEMM (32% of the step).  Falls back to the
-# HIP wgrad kernel once, for good, if this torch build cannot run that op.
-_WGRAD_BLAS = [os.environ.get("KUBEML_LINEAR_BLAS_WGRAD", "1") != "0"]
-
-
-_WGRAD_SPLIT = int(os.environ.get("KUBEML_WGRAD_SPLIT", "0"))  # 0 = auto
-
-
-def _wgrad_splits(M, op, ip):
-    """Split-K factor for the weight-gradient GEMM: its output ([op, ip], e.g. 3072 x 768 =
-    144 tiles of 128x128) is far too small to fill 256 CUs while its reduction (M = tokens)
-    is long, so slice M into S batched GEMMs (>= ~576 tiles in flight) and sum the S fp32
-    slabs.  hipBLASLt picked no split-K itself: 190 us (405 TF/s) per BERT FFN wgrad."""
-    if _WGRAD_SPLIT > 0:
-        S = _WGRAD_SPLIT
-    else:
-        # power of two >= 576 / tiles, at most 16 (tools/wgrad_split.py on the BERT shapes:
-        # 3072x768 best at S=4, 2304x768 at 8, 768x768 at 16)
-        tiles = max(1, -(-op // 128) * -(-ip // 128))
-        S = 1
-        while S < 16 and S * tiles < 576:
-            S *= 2
-    while S > 1 and (M % S or M // S < 256):
-        S -= 1
-    return S
+def _linear_route(M, ip, op, act):
+    """'blas' (hipBLASLt, opt-in), 'gemm' (gemm.hip) or 'conv' (implicit-GEMM kernels)."""
+    big = M >= 2048 and ip >= 256 and op >= 256 and act != 1
+    if big and _LIN_BLAS == "1" and act == 0:
+        return "blas"
+    return "gemm" if big else "conv"
 
 
 def _blas_wgrad_(dw, dy, x):
-    """dw[op, ip] (fp32) += dy[M, op]^T @ x[M, ip] (bf16); False if unsupported."""
-    if not _WGRAD_BLAS[0]:
-        return False
-    try:
-        M, op, ip = dy.shape[0], dy.shape[1], x.shape[1]
-        S = _wgrad_splits(M, op, ip)
-        if S == 1:
-            torch.addmm(dw, dy.t(), x, out_dtype=torch.float32, out=dw)
-        else:
-            part = torch.bmm(dy.view(S, M // S, op).transpose(1, 2), x.view(S, M // S, ip),
-                             out_dtype=torch.float32)
-            from ..ops import kernels as K
-            K.slab_sum_add_(part, dw)
-        return True
-    except (RuntimeError, TypeError, NotImplementedError):
-        _WGRAD_BLAS[0] = False
-        return False
+    """dw[op, ip] (fp32) += dy[M, op]^T @ x[M, ip] on hipBLASLt (KUBEML_LINEAR_BLAS=1 only)."""
+    torch.addmm(dw, dy.t(), x, out_dtype=torch.float32, out=dw)
 
 
 class _PadChannelsFn(Function):
@@ -204,21 +164,34 @@ class Conv2d(tnn.Module):
 # ======================================================================================
 
 class _LinearFn(Function):
+    """act: 0 none, 1 ReLU (implicit-GEMM path), 2 erf-GELU (gemm.hip epilogue; the
+    pre-activation is kept for backward)."""
+
     @staticmethod
-    def forward(ctx, x2, weight, bias, mod, relu):
+    def forward(ctx, x2, weight, bias, mod, act):
         from ..ops import kernels as K
         op, ip = mod.out_pad, mod.in_pad
         B = x2.shape[0]
-        ctx.blas = _linear_blas(B, ip, op, relu)
-        if ctx.blas:  # plain GEMM, bias in hipBLASLt's epilogue
+        route = _linear_route(B, ip, op, act)
+        ctx.route = route
+        pre = None
+        if route == "gemm":
+            from ..ops import gemm as G
+            w2 = shadow_of(weight).view(op, ip)
+            pre = torch.empty((B, op), dtype=torch.bfloat16, device=x2.device) if act == 2 else None
+            y = G.linear_fwd(x2, w2, None if bias is None else master_of(bias), act=1 if act == 2 else 0, pre=pre)
+        elif route == "blas":
             w2 = shadow_of(weight).view(op, ip)
             y = torch.mm(x2, w2.t()) if bias is None else torch.addmm(shadow_of(bias), x2, w2.t())
         else:
+            if act == 2:
+                raise ValueError("fused GELU needs the large-linear GEMM path")
             w = shadow_of(weight).view(op, 1, 1, ip)
             bias_st = None if bias is None else master_of(bias)
-            y = K.conv_fwd(x2.view(B, 1, 1, ip), w, 1, 1, (1, 1), (0, 0), bias=bias_st, relu=relu).view(B, op)
-        ctx.mod, ctx.x, ctx.has_bias, ctx.relu = mod, x2, bias is not None, relu
-        ctx.y = y if relu else None
+            y = K.conv_fwd(x2.view(B, 1, 1, ip), w, 1, 1, (1, 1), (0, 0), bias=bias_st, relu=act == 1).view(B, op)
+        ctx.mod, ctx.x, ctx.has_bias, ctx.act = mod, x2, bias is not None, act
+        ctx.y = y if act == 1 else None
+        ctx.pre = pre
         if op != mod.out_features:
             y = y[:, :mod.out_features].contiguous()
         return y
@@ -234,17 +207,25 @@ class _LinearFn(Function):
             dy = dy.to(torch.bfloat16)
         if op != mod.out_features:
             dy = K.pad_channels(dy, op)
-        if ctx.relu:
+        if ctx.act == 1:
             dy = K.relu_bwd(dy, ctx.y)
+        elif ctx.act == 2:
+            from ..ops import transformer as T
+            dy = T.gelu_bwd(dy, ctx.pre)
         dy4 = dy.view(B, 1, 1, op)
         x4 = ctx.x.view(B, 1, 1, ip)
         dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
         dx = None
-        if ctx.blas:
+        if ctx.route == "gemm":
+            from ..ops import gemm as G
+            w2 = shadow_of(mod.weight).view(op, ip)
+            if ctx.needs_input_grad[0]:
+                dx = G.linear_dgrad(dy, w2)
+            G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x)
+        elif ctx.route == "blas":
             if ctx.needs_input_grad[0]:
                 dx = torch.mm(dy, shadow_of(mod.weight).view(op, ip))
-            if not _blas_wgrad_(dw4.view(op, ip), dy, ctx.x):
-                K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
+            _blas_wgrad_(dw4.view(op, ip), dy, ctx.x)
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
@@ -253,7 +234,7 @@ class _LinearFn(Function):
             K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
         if ctx.has_bias:
             K.colsum_(dy, grad_storage_of(mod.bias))
-        ctx.x = ctx.y = None
+        ctx.x = ctx.y = ctx.pre = None
         return dx, None, None, None, None
 
 
@@ -285,17 +266,23 @@ class Linear(tnn.Module):
     def extra_repr(self):
         return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
 
-    def forward(self, x):
+    def forward(self, x, act: Optional[str] = None):
+        """act: None (module default: fused ReLU if constructed so), "gelu" (erf-GELU fused
+        into the GEMM epilogue on the GPU)."""
+        a = 2 if act == "gelu" else (1 if self.fused_relu else 0)
         if not _on_gpu(x):
             y = F.linear(x, self.weight, self.bias)
-            return F.relu(y) if self.fused_relu else y
+            return F.relu(y) if a == 1 else (F.gelu(y) if a == 2 else y)
         if x.dim() != 2:
             x = x.reshape(x.shape[0], -1)
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         if x.shape[1] != self.in_pad:
             x = pad_channels(x, self.in_pad)
-        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, self.fused_relu)
+        if a == 2 and _linear_route(x.shape[0], self.in_pad, self.out_pad, 2) != "gemm":
+            from .transformer import GELU
+            return GELU()(_LinearFn.apply(x.contiguous(), self.weight, self.bias, self, 0))
+        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, a)
 
 
 # ======================================================================================

@@ -139,13 +139,14 @@ class Dropout(tnn.Module):
 # ====================================================================================== attention
 class _AttnFn(Function):
     @staticmethod
-    def forward(ctx, qkv, B, H, L, bias):
+    def forward(ctx, qkv, B, H, L, bias, drop=None):
         from ..ops import transformer as T
         D = H * 64
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-        out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias)
+        out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias, drop=drop)
         ctx.save = (qkv, out, lse, bias)
         ctx.dims = (B, H, L)
+        ctx.drop = drop
         return out
 
     @staticmethod
@@ -156,20 +157,30 @@ class _AttnFn(Function):
         D = H * 64
         dqkv = torch.empty_like(qkv)
         T.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, _bf(dout).contiguous(), lse, B, H, L, bias=bias,
-                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:])
+                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=ctx.drop)
         ctx.save = None
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
 
 
-def attention_reference(qkv, B, H, L, bias=None):
-    """fp32 torch attention on a fused [B*L, 3*H*64] buffer (CPU path / tests)."""
+def attention_reference(qkv, B, H, L, bias=None, keep=None):
+    """fp32 torch attention on a fused [B*L, 3*H*64] buffer (CPU path / tests); keep:
+    optional [B, H, L, L] dropout multiplier (0 or 1/(1-p)) applied to the probabilities."""
     D = H * 64
     q, k, v = (qkv[:, i * D:(i + 1) * D].reshape(B, L, H, 64).permute(0, 2, 1, 3) for i in range(3))
     s = q @ k.transpose(-1, -2) / math.sqrt(64)
     if bias is not None:
         s = s + bias.view(B, 1, 1, L)
-    o = s.softmax(-1) @ v
+    pr = s.softmax(-1)
+    if keep is not None:
+        pr = pr * keep
+    o = pr @ v
     return o.permute(0, 2, 1, 3).reshape(B * L, D)
+
+
+def attention_reference_dropout(qkv, B, H, L, bias, p):
+    """CPU attention with probability dropout (torch RNG; same semantics as the kernel)."""
+    keep = (torch.rand(B, H, L, L) >= p).float() / (1.0 - p)
+    return attention_reference(qkv, B, H, L, bias, keep=keep)
 
 
 class SelfAttention(tnn.Module):
@@ -178,8 +189,14 @@ class SelfAttention(tnn.Module):
     (``self.query.weight`` ... ``output.dense.weight``) through hooks."""
 
     def __init__(self, hidden: int = 768, heads: int = 12, prefix_self: str = "self.", prefix_out: str = "output.dense.",
-                 post_ln_eps: Optional[float] = None, prefix_ln: str = "output.LayerNorm."):
+                 post_ln_eps: Optional[float] = None, prefix_ln: str = "output.LayerNorm.", attn_dropout: float = 0.0,
+                 rng: Optional["RNGState"] = None):
         super().__init__()
+        # attention-probability dropout (HF attention_probs_dropout_prob), inside the kernel
+        self.attn_dropout = float(attn_dropout)
+        self.rng = rng or RNGState()
+        Dropout._salt += 1
+        self.salt = Dropout._salt * 7919
         if hidden != heads * 64:
             raise ValueError("the fused attention kernel needs head_dim 64")
         self.hidden, self.heads = hidden, heads
@@ -218,9 +235,15 @@ class SelfAttention(tnn.Module):
     def forward(self, x, B: int, L: int, bias=None):
         qkv = self.qkv(x)
         if not x.is_cuda:
-            ctx = attention_reference(qkv, B, self.heads, L, bias)
+            if self.training and self.attn_dropout > 0:
+                ctx = attention_reference_dropout(qkv, B, self.heads, L, bias, self.attn_dropout)
+            else:
+                ctx = attention_reference(qkv, B, self.heads, L, bias)
         else:
-            ctx = _AttnFn.apply(qkv.contiguous(), B, self.heads, L, bias)
+            drop = None
+            if self.training and self.attn_dropout > 0:
+                drop = (self.rng.tensor(x.device), self.salt, self.attn_dropout)
+            ctx = _AttnFn.apply(qkv.contiguous(), B, self.heads, L, bias, drop)
         return self.out(ctx)
 
 

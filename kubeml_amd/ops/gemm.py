@@ -1,0 +1,148 @@
+"""Launchers for the hand-written MFMA GEMM (csrc/kernels/gemm.hip).
+
+``linear_fwd`` / ``linear_dgrad`` / ``linear_wgrad_`` are the three GEMMs of a linear
+layer ``y = x W^T + b`` with bf16 activations, the bf16 weight shadow and the fp32
+gradient storage of the flat parameter space.  Host-side checks guard every contract the
+kernel relies on (alignment, multiples of 8/4) before a launch — a wrong shape never
+reaches the GPU.  Tile and split-K choices come from a small per-shape table measured by
+``tools/gemm_micro.py`` (``gemm_tuning.json``) with a heuristic default.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+
+from .._native import HIP, stream_ptr
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5}  # (BM, BN[, stages])
+_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_TUNED: dict = {}
+if os.path.exists(_TUNE_FILE) and os.environ.get("KUBEML_GEMM_TUNING", "1") != "0":
+    with open(_TUNE_FILE) as f:
+        for e in json.load(f).get("entries", []):
+            _TUNED[(e["layout"], e["M"], e["N"], e["K"])] = (tuple(e["tile"]), int(e.get("splits", 1)))
+
+_ZP = {}
+
+
+def _zp(dev):
+    z = _ZP.get(dev)
+    if z is None:
+        z = torch.zeros(64, dtype=BF16, device=dev)
+        _ZP[dev] = z
+    return z
+
+
+def _cdiv(a, b):
+    return -(-a // b)
+
+
+def _splits_for(tiles: int, K: int, min_chunk: int) -> int:
+    """Smallest power of two s <= 8 with tiles * s >= 256 blocks (one per CU) while every
+    split keeps >= min_chunk of the reduction."""
+    s = 1
+    while s < 8 and tiles * s < 256 and K // (2 * s) >= min_chunk:
+        s *= 2
+    return s
+
+
+def plan(layout: int, M: int, N: int, K: int):
+    """(tile, splits): the measured table (tools/gemm_bench.py), else the measured-best
+    general choice — 128x128 two-stage tiles (two blocks per CU hide each other's
+    prologue / epilogue), split-K when the output tiles cannot fill 256 CUs."""
+    t = _TUNED.get((layout, M, N, K))
+    if t is not None:
+        return t
+    tile = (128, 128, 2)
+    tiles = _cdiv(M, 128) * _cdiv(N, 128)
+    if layout == 2:
+        return tile, _splits_for(tiles, K, 1024)
+    if tiles < 128 and K >= 4096:
+        return tile, _splits_for(tiles, K, 1024)
+    return tile, 1
+
+
+def _check(t, dtype, name):
+    if t.dtype != dtype or not t.is_cuda:
+        raise TypeError(f"{name}: expected CUDA {dtype}, got {t.dtype} on {t.device}")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name}: pointer must be 16-byte aligned")
+
+
+def gemm(a, lda, b, ldb, c, ldc, M, N, K, layout, out, bias=None, act=0, c2=None, beta=0.0, tile=None,
+         splits=None):
+    """Raw launcher; see gemm.hip for the layout / out codes."""
+    _check(a, BF16, "a")
+    _check(b, BF16, "b")
+    _check(c, BF16 if out == 0 else F32, "c")
+    if N % 4 or ldc % 4:
+        raise ValueError("gemm: N and ldc must be multiples of 4")
+    if lda % 8 or ldb % 8:
+        raise ValueError("gemm: leading dimensions must be multiples of 8")
+    if K % 8:
+        raise ValueError("gemm: K must be a multiple of 8")
+    if bias is not None:
+        _check(bias, F32, "bias")
+        if bias.numel() < N:
+            raise ValueError("gemm: bias shorter than N")
+    if c2 is not None:
+        _check(c2, BF16, "c2")
+    if tile is None or splits is None:
+        pt, ps = plan(layout, M, N, K)
+        tile = tile or pt
+        splits = splits or ps
+    if out != 2:
+        splits = 1
+    HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", a.data_ptr(), int(lda), b.data_ptr(), int(ldb),
+             c.data_ptr(), int(ldc), 0 if c2 is None else c2.data_ptr(), 0 if bias is None else bias.data_ptr(),
+             _zp(a.device).data_ptr(), int(M), int(N), int(K), int(layout), int(out), int(act), float(beta),
+             TILES[tuple(tile)], int(splits), stream_ptr())
+
+
+def linear_fwd(x, w, bias=None, act=0, pre=None):
+    """y[T, op] = act(x[T, ip] @ w[op, ip]^T + bias); ``pre`` receives the pre-activation."""
+    T, ip = x.shape
+    op = w.shape[0]
+    if w.shape[1] != ip:
+        raise ValueError(f"linear_fwd: x {tuple(x.shape)} vs w {tuple(w.shape)}")
+    y = torch.empty((T, op), dtype=BF16, device=x.device)
+    gemm(x, ip, w, ip, y, op, T, op, ip, 0, 0, bias=bias, act=act, c2=pre)
+    return y
+
+
+def linear_dgrad(dy, w):
+    """dx[T, ip] = dy[T, op] @ w[op, ip].  Few output tiles with a long reduction (the MLM
+    decoder: 2432 x 768 out, K = 30528) split K over fp32 atomics into a scratch tile,
+    then one bf16 conversion pass."""
+    T, op = dy.shape
+    ip = w.shape[1]
+    if w.shape[0] != op:
+        raise ValueError(f"linear_dgrad: dy {tuple(dy.shape)} vs w {tuple(w.shape)}")
+    dx = torch.empty((T, ip), dtype=BF16, device=dy.device)
+    tile, splits = plan(1, T, ip, op)
+    if splits > 1:
+        from . import kernels as KK
+        acc = torch.empty((T, ip), dtype=F32, device=dy.device)
+        KK.memset_(acc)
+        gemm(dy, op, w, ip, acc, ip, T, ip, op, 1, 2, tile=tile, splits=splits)
+        KK.f32_to_bf16(acc, dx)
+        return dx
+    gemm(dy, op, w, ip, dx, ip, T, ip, op, 1, 0, tile=tile, splits=1)
+    return dx
+
+
+def linear_wgrad_(dw, dy, x):
+    """dw[op, ip] (fp32) += dy[T, op]^T @ x[T, ip]."""
+    T, op = dy.shape
+    ip = x.shape[1]
+    if tuple(dw.shape) != (op, ip) or x.shape[0] != T:
+        raise ValueError(f"linear_wgrad_: dw {tuple(dw.shape)} dy {tuple(dy.shape)} x {tuple(x.shape)}")
+    if not dw.is_contiguous():
+        raise ValueError("linear_wgrad_: dw must be contiguous")
+    tile, splits = plan(2, op, ip, T)
+    gemm(dy, op, x, ip, dw, ip, op, ip, T, 2, 2 if splits > 1 else 1, beta=1.0, tile=tile, splits=splits)
+    return dw

@@ -26,9 +26,21 @@ def _chk_view(t, name):
         raise ValueError(f"{name}: expected a 16-byte aligned row-major 2-d view, got stride {t.stride()}")
 
 
-def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None):
+def _drop_args(drop):
+    """drop = (ctr [seed, step] device tensor, salt, p) or None."""
+    if drop is None or drop[2] <= 0.0:
+        return 0, 0, 0.0
+    ctr, salt, p = drop
+    _chk(ctr, F32, "ctr")
+    if not 0.0 <= p < 1.0:
+        raise ValueError("dropout p must be in [0, 1)")
+    return ctr.data_ptr(), int(salt) & 0x7FFFFFFF, float(p)
+
+
+def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None, drop=None):
     """q/k/v: [B*L, ld] bf16 views with head h at columns 64h..64h+63 (may be column
-    slices of one fused QKV buffer).  Returns (out [B*L, H*64], lse [B*H, L])."""
+    slices of one fused QKV buffer).  drop: (ctr, salt, p) attention-probability dropout.
+    Returns (out [B*L, H*64], lse [B*H, L])."""
     for n, t in (("q", q), ("k", k), ("v", v)):
         _chk_view(t, n)
         if t.shape[0] != B * L or t.shape[1] < H * 64:
@@ -41,12 +53,13 @@ def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None):
         out = torch.empty((B * L, H * 64), dtype=BF16, device=q.device)
     lse = torch.empty((B * H, L), dtype=F32, device=q.device)
     scale = 1.0 / math.sqrt(64) if scale is None else scale
-    HIP.call("kml_attn_fwd", "p p p p p p i i i i i i i f s", _p(q), _p(k), _p(v), _p(out), _p(lse), _p(bias),
-             q.stride(0), k.stride(0), v.stride(0), out.stride(0), B, H, L, float(scale), _s())
+    c, salt, pd = _drop_args(drop)
+    HIP.call("kml_attn_fwd", "p p p p p p i i i i i i i f p i f s", _p(q), _p(k), _p(v), _p(out), _p(lse), _p(bias),
+             q.stride(0), k.stride(0), v.stride(0), out.stride(0), B, H, L, float(scale), c, salt, pd, _s())
     return out, lse
 
 
-def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=None, scale=None):
+def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=None, scale=None, drop=None):
     """Gradients of attention; dq/dk/dv may be column views of one [B*L, 3*H*64] buffer."""
     dev = q.device
     if dq is None:
@@ -63,10 +76,11 @@ def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=Non
         raise ValueError("lse must be fp32 [B*H, L] from attn_fwd")
     dsum = torch.empty((B * H, L), dtype=F32, device=dev)
     scale = 1.0 / math.sqrt(64) if scale is None else scale
-    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f s",
+    c, salt, pd = _drop_args(drop)
+    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f p i f s",
              _p(q), _p(k), _p(v), _p(o), _p(dout), _p(lse), _p(dsum), _p(bias), _p(dq), _p(dk), _p(dv),
              q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
-             dv.stride(0), B, H, L, float(scale), _s())
+             dv.stride(0), B, H, L, float(scale), c, salt, pd, _s())
     return dq, dk, dv
 
 

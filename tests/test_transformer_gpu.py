@@ -122,3 +122,58 @@ def test_embedding_and_rows():
     dst = torch.zeros_like(out)
     T.scatter_rows(g, idx, dst)
     assert torch.equal(dst[idx], g) and dst.float().abs().sum() == g.float().abs().sum()
+
+
+def _attn_keep(seed, step, salt, B, H, L, p):
+    """Python replica of the kernel's dropout mask (attention.hip Drop::keep)."""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFF)
+
+    def mul(a, b):
+        return (a.astype(np.uint64) * np.uint64(b)) & M
+
+    thr = np.uint64(int(np.float32(p) * np.float32(4294967296.0)))
+    k0 = np.uint64((int(seed) ^ salt) & 0xFFFFFFFF)
+    keep = np.zeros((B, H, L, L), dtype=np.float32)
+    q = np.arange(L, dtype=np.uint64).reshape(L, 1)
+    key = np.arange(L, dtype=np.uint64).reshape(1, L)
+    c = (q * np.uint64(L) + key) & M
+    for b in range(B):
+        for h in range(H):
+            bh = np.uint64(b * H + h)
+            k1 = ((np.uint64(int(step)) * np.uint64(0x632BE5AB)) & M) ^ ((bh * np.uint64(0x5851F42D)) & M)
+            hh = mul(np.full_like(c, k0), 0x9E3779B1) ^ mul((np.full_like(c, k1) + np.uint64(0x7F4A7C15)) & M,
+                                                            0x85EBCA77) ^ mul(c, 0xC2B2AE3D)
+            hh ^= hh >> np.uint64(15)
+            hh = mul(hh, 0x2C1B3C6D)
+            hh ^= hh >> np.uint64(12)
+            hh = mul(hh, 0x297A2D39)
+            hh ^= hh >> np.uint64(15)
+            keep[b, h] = np.where(hh >= thr, 1.0 / (1.0 - p), 0.0)
+    return torch.from_numpy(keep)
+
+
+@pytest.mark.parametrize("L", [64, 100])
+def test_attention_dropout_matches_masked_reference(L):
+    """Fused attention with probability dropout vs fp32 autograd on the same mask
+    (forward output, dQ/dK/dV); dropout rate close to p."""
+    from kubeml_amd.nn.transformer import _AttnFn, attention_reference
+    torch.manual_seed(5)
+    B, H, p = 2, 2, 0.25
+    D = H * 64
+    qkv = (torch.randn(B * L, 3 * D, device="cuda") * 0.5).to(torch.bfloat16)
+    ctr = torch.tensor([11.0, 3.0], device="cuda")
+    salt = 7919 * 3
+    keep = _attn_keep(11, 3, salt, B, H, L, p)
+    frac = float((keep == 0).float().mean())
+    assert abs(frac - p) < 0.03, frac
+    x = qkv.clone().requires_grad_(True)
+    out = _AttnFn.apply(x, B, H, L, None, (ctr, salt, p))
+    xr = qkv.float().cpu().requires_grad_(True)
+    ref = attention_reference(xr, B, H, L, None, keep=keep)
+    g = torch.randn_like(ref)
+    out.backward(g.to("cuda").to(torch.bfloat16))
+    ref.backward(g)
+    rel = lambda a, b: float((a.float().cpu() - b).norm() / b.norm())
+    assert rel(out.detach(), ref.detach()) < 2e-2
+    assert rel(x.grad, xr.grad) < 3e-2
