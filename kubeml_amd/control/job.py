@@ -265,7 +265,7 @@ class TrainJob:
                 self._epoch_stats(time.time() - t0, hbm)
                 return sum(losses) / len(losses)
             errs = "; ".join(f"worker {r}: {v.get('error')}" for r, v in sorted(bad.items()))
-            dead = [r for r, v in bad.items() if v.get("dead")]
+            dead = [r for r, v in bad.items() if v.get("dead") or v.get("hung")]   # hung = lost
             self.log.warn("epoch failed", epoch=self.epoch, attempt=attempt, errors=errs, dead=dead)
             if not dead and self.pool is not None and not self.pool.broken:
                 # function error on a healthy pool (no lost peer): the reference fails the

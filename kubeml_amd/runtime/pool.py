@@ -10,6 +10,13 @@ process while waiting; a worker that fails while its peers are still running lea
 them blocked in a collective, so after a short grace period the pool kills the
 remaining ranks and marks itself ``broken`` — the job driver then rebuilds a pool
 (on the survivors' GPUs) and resumes from its last checkpoint.
+
+Hung collectives (a peer alive but stuck): every worker bumps a shared progress counter
+at each K-AVG round (``runtime.worker.progress``).  While a task runs, if no rank's
+counter moves for ``stall_timeout`` seconds the task is declared hung and the pool aborts
+(instead of waiting out the task timeout) — the job driver then recovers like a lost worker;
+RCCL's own watchdog (``TORCH_NCCL_ASYNC_ERROR_HANDLING``, collective timeout
+``KUBEML_COLLECTIVE_TIMEOUT``) tears down a rank stuck inside a collective.
 """
 from __future__ import annotations
 
@@ -36,7 +43,7 @@ def free_port() -> int:
 class WorkerPool:
     def __init__(self, n: int, use_gpu: bool, store_dir: str, gpu_ids: Optional[List[int]] = None,
                  timeout: float = 600.0, env: Optional[Dict[str, str]] = None, grace: float = 5.0,
-                 threads: int = 1):
+                 threads: int = 1, stall_timeout: Optional[float] = None):
         self.n = n
         self.use_gpu = use_gpu
         self.store_dir = store_dir
@@ -49,17 +56,26 @@ class WorkerPool:
         self.conns = []
         self.broken = False
         self.dead: List[int] = []
+        self.hung: List[int] = []
+        self.stall_timeout = float(stall_timeout if stall_timeout is not None
+                                   else os.environ.get("KUBEML_STALL_TIMEOUT", "300"))
+        self.progress = None
 
     # ------------------------------------------------------------------ lifecycle
     def start(self, ready_timeout: float = 600.0) -> "WorkerPool":
         ctx = mp.get_context("spawn")
         port = free_port()
-        env = {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"), **self.env}
+        env = {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               "TORCH_NCCL_ASYNC_ERROR_HANDLING": os.environ.get("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1"), **self.env}
         opts = {"use_gpu": self.use_gpu, "gpu_ids": self.gpu_ids, "store_dir": self.store_dir, "port": port,
-                "timeout": self.timeout, "env": env, "threads": self.threads}
+                "timeout": float(os.environ.get("KUBEML_COLLECTIVE_TIMEOUT", self.timeout)), "env": env,
+                "threads": self.threads}
+        # one progress counter per rank, bumped by the worker (shared memory, no locking)
+        self.progress = ctx.Array("q", self.n, lock=False)
         for r in range(self.n):
             a, b = ctx.Pipe()
-            p = ctx.Process(target=worker_entry, args=(r, self.n, b, opts), name=f"kubeml-worker{r}", daemon=True)
+            p = ctx.Process(target=worker_entry, args=(r, self.n, b, opts, self.progress), name=f"kubeml-worker{r}",
+                            daemon=True)
             p.start()
             b.close()
             self.procs.append(p)
@@ -138,6 +154,9 @@ class WorkerPool:
         out: Dict[int, Dict[str, Any]] = {}
         pending = list(msgs)
         failed_at = None
+        self.hung = []
+        last_val = {r: self._prog(r) for r in msgs}
+        last_move = {r: time.time() for r in msgs}
         while pending:
             for r in list(pending):
                 c, p = self.conns[r], self.procs[r]
@@ -158,6 +177,15 @@ class WorkerPool:
             if not pending:
                 break
             now = time.time()
+            hung = self._stalled(pending, last_val, last_move, now)
+            if hung and failed_at is None:
+                self.hung = hung
+                for r in pending:
+                    out[r] = {"ok": False, "error": f"worker {r} aborted (no progress for {self.stall_timeout:.0f}s: "
+                                                    f"hung collective, stuck ranks {hung})",
+                              "code": 500, "aborted": True, "hung": r in hung}
+                self._abort()
+                break
             if (failed_at is not None and now - failed_at > self.grace) or now > deadline:
                 why = "peer failure" if failed_at is not None else "timeout"
                 for r in pending:
@@ -169,6 +197,27 @@ class WorkerPool:
         if self.dead:
             self._abort()
         return out
+
+    def _prog(self, r: int) -> int:
+        return int(self.progress[r]) if self.progress is not None else 0
+
+    def _stalled(self, pending, last_val, last_move, now) -> List[int]:
+        """Pending ranks if no rank's progress counter has moved for stall_timeout (a rank
+        stuck in or before a collective stalls its peers inside that collective too)."""
+        if self.progress is None or self.stall_timeout <= 0:
+            return []
+        for r in last_val:
+            v = self._prog(r)
+            if v != last_val[r]:
+                last_val[r] = v
+                last_move[r] = now
+        if now - max(last_move.values()) >= self.stall_timeout:
+            # the culprit is behind its peers (they reached the next collective and wait in
+            # it); equal counters: nobody can be singled out
+            lo = min(last_val[r] for r in pending)
+            behind = [r for r in pending if last_val[r] == lo]
+            return behind if len(behind) < len(last_val) else list(pending)
+        return []
 
     def _abort(self):
         """Kill every rank: a collective with a missing peer can never complete."""

@@ -32,6 +32,8 @@ from typing import Any, Dict
 
 log = logging.getLogger("kubeml.worker")
 
+_PROGRESS = None   # (shared array, rank): bumped by progress(); watched by the pool
+
 
 def _jsonable(x):
     import numpy as np
@@ -50,6 +52,14 @@ def _jsonable(x):
     if isinstance(x, (list, tuple)):
         return [_jsonable(v) for v in x]
     return x
+
+
+def progress(n: int = 1):
+    """Mark forward progress of this worker (a K-AVG round, a minibatch).  The pool
+    declares a rank hung when its counter stops while its peers' advance."""
+    if _PROGRESS is not None:
+        arr, rank = _PROGRESS
+        arr[rank] += n
 
 
 def load_function(path: str, name: str):
@@ -140,6 +150,7 @@ class Worker:
         t0 = time.perf_counter()
         try:
             fault.point("task", rank=self.rank, epoch=ctx.epoch, task=kind, job=job)
+            progress()
             with trace.span(f"task:{kind}", job=job, epoch=ctx.epoch, N=P):
                 km = self.jobs.get(job)
                 if km is not None and self.job_fn.get(job) == msg["code_path"]:
@@ -209,8 +220,11 @@ def _local():
     return LocalComm()
 
 
-def worker_entry(rank: int, world: int, conn, opts: Dict[str, Any]):
+def worker_entry(rank: int, world: int, conn, opts: Dict[str, Any], progress_arr=None):
     """Process entry point (multiprocessing spawn target)."""
+    global _PROGRESS
+    if progress_arr is not None:
+        _PROGRESS = (progress_arr, rank)
     for k, v in (opts.get("env") or {}).items():
         os.environ[k] = str(v)
     logging.basicConfig(level=os.environ.get("KUBEML_LOG_LEVEL", "WARNING"),

@@ -51,6 +51,11 @@ from .dataset import KubeDataset, _KubeArgs
 from .util import get_gpu, get_subset_period, max_rounds, split_minibatches
 
 
+def _progress():
+    from ..runtime.worker import progress
+    progress()
+
+
 def _same_but_lr(a, b) -> bool:
     if type(a) is not type(b) or len(a.param_groups) != len(b.param_groups):
         return False
@@ -284,6 +289,7 @@ class KubeModel(ABC):
         try:
             for r in range(rounds):
                 fault.point("round", rank=fid, epoch=self.epoch, round=r, task="train", job=self.args._job_id)
+                _progress()
                 participate = r < len(intervals)
                 self._sync_mode = "grad" if (grad_ok and r < full_rounds) else "local"
                 self._synced_steps = 0
@@ -297,6 +303,7 @@ class KubeModel(ABC):
                     self._on_iteration_start()
                     with trace.span("iteration", round=r):
                         for idx, batch in enumerate(self._batches()):
+                            _progress()
                             batch = self._batch_to_device(batch)
                             l = self.train(batch, idx)
                             if isinstance(l, torch.Tensor):
@@ -387,6 +394,7 @@ class KubeModel(ABC):
         dev_sums = None          # device-side [acc, loss] accumulation (one read-back)
         with torch.no_grad():
             for idx, batch in enumerate(self._batches()):
+                _progress()
                 batch = self._batch_to_device(batch)
                 a, l = self.validate(batch, idx)
                 if isinstance(a, torch.Tensor) and isinstance(l, torch.Tensor):

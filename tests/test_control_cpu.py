@@ -163,6 +163,37 @@ def test_worker_loss_recovery(tmp_path):
         srv.stop()
 
 
+def test_hung_worker_detected_and_recovered(tmp_path):
+    """KUBEML_FAULT hangs rank 1 at epoch 1, round 2 (alive but stuck; its peer waits in the
+    round's all-reduce): no rank makes progress for KUBEML_STALL_TIMEOUT, the pool aborts
+    the task (hung collective, culprit = the rank behind) long before the task timeout, and
+    the job recovers on the survivor."""
+    srv, c = _start(tmp_path, worker_env={"KUBEML_FAULT": "hang:at=round:rank=1:epoch=1:round=2:secs=600"})
+    import kubeml_amd.runtime.pool as P
+    old = os.environ.get("KUBEML_STALL_TIMEOUT")
+    os.environ["KUBEML_STALL_TIMEOUT"] = "4"
+    try:
+        paths, _ = _write_dataset(str(tmp_path))
+        c.datasets.create("mnist", paths["xtr"], paths["ytr"], paths["xte"], paths["yte"])
+        c.functions.create("lenet", os.path.join(ROOT, "examples", "function_lenet.py"))
+        req = TrainRequest(batch_size=64, epochs=1, dataset="mnist", lr=0.05, function_name="lenet",
+                           options=TrainOptions(default_parallelism=2, static_parallelism=True, k=2))
+        t0 = time.time()
+        jid = c.networks.train(req)
+        st = _wait(c, jid, timeout=200)
+        assert st["state"] == "finished", st
+        assert time.time() - t0 < 150
+        log = c.logs(jid).decode()
+        assert "hung collective" in log and "recovering" in log
+        assert c.histories.get(jid).data.parallelism == [1.0]
+    finally:
+        if old is None:
+            os.environ.pop("KUBEML_STALL_TIMEOUT", None)
+        else:
+            os.environ["KUBEML_STALL_TIMEOUT"] = old
+        srv.stop()
+
+
 def test_resume_from_checkpoint(env):
     """A job resumed from another continues its epoch count, history and weights."""
     srv, c, _ = env
