@@ -65,6 +65,8 @@ def parse():
                     help="capture the overlapped all-reduces inside the step's hipGraph (KUBEML_GRAPH_COMM=0: off)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the measured epoch after the timed steps")
     ap.add_argument("--cpu-smoke", action="store_true", help="gloo/CPU rehearsal of the N-rank launch (tiny model)")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace (device compute/comm timeline) to this dir; "
+                                                  "collectives then run outside the step graph")
     return ap.parse_args()
 
 
@@ -156,6 +158,10 @@ def main():
 
     import torch
     import torch.distributed as dist
+    if args.trace:
+        from kubeml_amd.utils import trace as _trace
+        _trace.enable(True)
+        _trace.set_process("bench", rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = world > 1 or args.force_comm
@@ -272,7 +278,7 @@ def main():
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "gradient all-reduce every step (K=1)",
                        "graph": not args.no_graph, "overlap_segments": overlap and comm,
-                       "graph_comm": graph_comm and comm, "bucket_mb": args.bucket_mb,
+                       "graph_comm": bool(getattr(step, "graph_comm", graph_comm) and comm), "bucket_mb": args.bucket_mb,
                        "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
@@ -283,6 +289,9 @@ def main():
             out["ranks_in_sync"] = in_sync
             out["rccl_world"] = dist.get_world_size()
         print(json.dumps(out), flush=True)
+    if args.trace:
+        from kubeml_amd.utils import trace as _trace
+        _trace.flush(args.trace)
     if comm:
         dist.destroy_process_group()
 

@@ -34,6 +34,8 @@ from typing import Callable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ..utils import trace
+
 
 def train_state_tensors(module=None, space=None, optimizer=None, extra: Sequence[torch.Tensor] = ()):
     """Device tensors a training step mutates (for snapshot/restore around warm-up)."""
@@ -198,6 +200,8 @@ class GraphedTrainStep:
         # capture; "thread_local" keeps its (uncaptured) queries from invalidating the
         # capture.  Nothing on this thread makes an unsafe call inside a capture.
         mode = "thread_local" if self.comm else "global"
+        if self.comm and trace.enabled():
+            self.graph_comm = False   # keep the collectives outside the graph so they can be timed
         if not self.comm or self.graph_comm:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=mode):
@@ -225,8 +229,15 @@ class GraphedTrainStep:
             self.loss = self._body()
             return self.loss
         if self.g_all is not None:
-            self.g_all.replay()
+            if trace.enabled():
+                e0 = trace.gpu_mark()
+                self.g_all.replay()
+                trace.gpu_span("step (one graph)", e0, trace.gpu_mark(), "gpu:compute")
+            else:
+                self.g_all.replay()
             return self.loss
+        if trace.enabled():
+            return self._traced_replay()
         works = []
         for k, g in enumerate(self.g_seg):
             g.replay()
@@ -234,4 +245,35 @@ class GraphedTrainStep:
         for w in works:
             w.wait()
         self.g_opt.replay()
+        return self.loss
+
+    def _traced_replay(self):
+        """Segment replays with device-timestamped spans: each segment on the compute
+        track, each segment's all-reduce on the comm track from its issue point to its
+        completion (observed by a side stream waiting on the collective), so a trace shows
+        how much of the gradient traffic hides behind the next segment's backward."""
+        cur = torch.cuda.current_stream()
+        side = getattr(self, "_trace_side", None)
+        if side is None:
+            side = self._trace_side = torch.cuda.Stream()
+        works = []
+        for k, g in enumerate(self.g_seg):
+            e0 = trace.gpu_mark(cur)
+            g.replay()
+            e1 = trace.gpu_mark(cur)
+            trace.gpu_span(f"fwd+bwd seg{k}" if k == 0 else f"bwd seg{k}", e0, e1, "gpu:compute", segment=k)
+            wk = self._issue(k)
+            if wk:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    for w in wk:
+                        w.wait()
+                    trace.gpu_span(f"allreduce seg{k}", e1, trace.gpu_mark(side), "gpu:comm", segment=k,
+                                   bytes=sum(v.numel() * 4 for v in self._views(k)))
+            works += wk
+        for w in works:
+            w.wait()
+        e0 = trace.gpu_mark(cur)
+        self.g_opt.replay()
+        trace.gpu_span("optimizer", e0, trace.gpu_mark(cur), "gpu:compute")
         return self.loss

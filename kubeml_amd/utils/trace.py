@@ -8,6 +8,13 @@ current stream at both ends, so use it only in diagnostic runs).  ``flush()`` wr
 
 Span names used by the runtime: ``task:<kind>``, ``load``, ``iteration``,
 ``average``, ``broadcast``, ``validate``, ``epoch``, ``sync-wait``.
+
+Device timeline (SURVEY §5.1 "comm/compute overlap timeline"): :func:`gpu_span` takes
+two timing events recorded on a HIP stream and places the span on a per-track row
+(``gpu:compute``, ``gpu:comm``) of the same trace, in host-clock microseconds: the first
+device mark is anchored to the host clock once (event synchronise), every later event
+is placed by its device-side elapsed time from that anchor.  Events resolve lazily at
+:func:`flush`, so marking costs nothing on the hot path but an event record.
 """
 from __future__ import annotations
 
@@ -66,6 +73,49 @@ def instant(name: str, **args):
                         "tid": threading.get_ident() % 100000, "args": args})
 
 
+_gpu = {"anchor": None, "anchor_ns": 0, "pending": []}
+_TRACKS = {"gpu:compute": 900001, "gpu:comm": 900002, "gpu:copy": 900003}
+
+
+def gpu_mark(stream=None):
+    """A timing event recorded on ``stream`` (default: current), or None if tracing is off."""
+    if not _enabled:
+        return None
+    import torch
+    if _gpu["anchor"] is None:
+        a = torch.cuda.Event(enable_timing=True)
+        a.record(torch.cuda.current_stream())
+        a.synchronize()
+        _gpu["anchor"], _gpu["anchor_ns"] = a, time.perf_counter_ns()
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(stream if stream is not None else torch.cuda.current_stream())
+    return e
+
+
+def gpu_span(name: str, start, end, track: str = "gpu:compute", **args):
+    """Device-timeline span between two :func:`gpu_mark` events."""
+    if not _enabled or start is None or end is None:
+        return
+    with _lock:
+        _gpu["pending"].append((name, start, end, track, args))
+
+
+def _resolve_gpu():
+    pend = _gpu["pending"]
+    if not pend:
+        return []
+    anchor, a_ns = _gpu["anchor"], _gpu["anchor_ns"]
+    out = []
+    for name, e0, e1, track, args in pend:
+        e1.synchronize()
+        t0 = a_ns / 1e3 + anchor.elapsed_time(e0) * 1e3
+        t1 = a_ns / 1e3 + anchor.elapsed_time(e1) * 1e3
+        out.append({"name": name, "cat": "gpu", "ph": "X", "ts": t0, "dur": max(t1 - t0, 0.0), "pid": os.getpid(),
+                    "tid": _TRACKS.get(track, 900009), "args": args})
+    pend.clear()
+    return out
+
+
 def _sync():
     try:
         import torch
@@ -82,8 +132,12 @@ def events() -> List[dict]:
 
 def flush(directory: Optional[str] = None, clear: bool = True) -> Optional[str]:
     """Write collected events; returns the file path (None if nothing recorded)."""
+    try:
+        gevs = _resolve_gpu()
+    except Exception:
+        gevs = []
     with _lock:
-        evs = list(_events)
+        evs = list(_events) + gevs
         if clear:
             _events.clear()
     if not evs:
@@ -93,6 +147,8 @@ def flush(directory: Optional[str] = None, clear: bool = True) -> Optional[str]:
     rank = _meta["rank"]
     name = _meta["name"] + (f"-rank{rank}" if rank is not None else "")
     meta = [{"name": "process_name", "ph": "M", "pid": os.getpid(), "args": {"name": name}}]
+    meta += [{"name": "thread_name", "ph": "M", "pid": os.getpid(), "tid": tid, "args": {"name": tr}}
+             for tr, tid in _TRACKS.items()]
     path = os.path.join(directory, f"{name}-pid{os.getpid()}.json")
     with open(path, "w") as f:
         json.dump({"traceEvents": meta + evs, "displayTimeUnit": "ms"}, f)

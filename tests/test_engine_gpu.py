@@ -167,3 +167,25 @@ def test_bench_rccl_rehearsal_overlapped_graph_comm():
                "--no-epoch")
     assert d["ranks_in_sync"] is True and d["config"]["overlap_segments"] is True
     assert d["config"]["graph_comm"] is True and d["rccl_world"] == 1
+
+
+def test_bench_trace_has_compute_and_comm_tracks(tmp_path):
+    """KUBEML_TRACE timeline: per-segment compute spans and per-segment all-reduce spans
+    on their own tracks, device-timestamped, each all-reduce starting at its segment's end."""
+    d = _bench("--steps", "3", "--warmup", "1", "--batch", "64", "--force-comm", "--overlap", "on", "--no-epoch",
+               "--trace", str(tmp_path))
+    assert d["ranks_in_sync"] is True
+    files = list(tmp_path.glob("*.json"))
+    assert files
+    evs = json.load(open(files[0]))["traceEvents"]
+    comp = [e for e in evs if e.get("cat") == "gpu" and e["tid"] == 900001]
+    comm = [e for e in evs if e.get("cat") == "gpu" and e["tid"] == 900002]
+    assert len(comp) >= 3 * 4 and len(comm) >= 3 * 3
+    seg_end = {}
+    for e in comp:
+        if "segment" in e["args"]:
+            seg_end.setdefault(e["args"]["segment"], []).append(e["ts"] + e["dur"])
+    for e in comm:
+        ends = seg_end[e["args"]["segment"]]
+        assert min(abs(e["ts"] - t) for t in ends) < 1.0   # starts where its segment ended
+        assert e["dur"] >= 0
