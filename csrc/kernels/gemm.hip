@@ -31,6 +31,8 @@
 // north-star config 5).
 #include "kml_common.h"
 
+#include <type_traits>
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
@@ -123,23 +125,33 @@ struct Stager {
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a contiguous run of
-// tiles (N fastest) so neighbouring tiles share A/B panels in its L2.  Bijective.
+// tiles (bijective remap, CDNA guide T1), and walk that run in GROUPS of up to 8 tile rows
+// (column-major inside a group), so the ~32 tiles an XCD's CUs hold at once form a block
+// of 8 rows x 4 columns: 12 operand panels through its 4 MB L2 instead of 33 for a
+// row-major run (1 A panel + 32 B panels) — an operand panel of a 256-wide tile is
+// re-fetched past L2 by a quarter / an eighth of the CUs instead of by every one.
 __device__ __forceinline__ void xcd_tile(int& tx, int& ty, int& tz) {
   const int gx = (int)gridDim.x, gy = (int)gridDim.y;
   const int nwg = gx * gy * (int)gridDim.z;
   const int lin = ((int)blockIdx.z * gy + (int)blockIdx.y) * gx + (int)blockIdx.x;
   const int q = nwg >> 3, r = nwg & 7, x = lin & 7, k = lin >> 3;
   const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-  tx = id % gx;
-  const int t = id / gx;
-  ty = t % gy;
-  tz = t / gy;
+  const int per = gx * gy;
+  tz = id / per;
+  const int t = id - tz * per;
+  constexpr int G = 8;
+  const int grp = t / (G * gx);
+  const int row0 = grp * G;
+  const int rows = min(G, gy - row0);
+  const int w = t - grp * G * gx;
+  ty = row0 + w % rows;
+  tx = w / rows;
 }
 
 // epilogue: lane holds C[m][n .. n+3], m = .. + (lane & 15), n = .. + 4 * (lane >> 4)
 template <int OUT, int MR, int NR, int WM, int WN>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
-                                              int wn, int lane) {
+                                              int wn, int lane, int tz) {
 #pragma unroll
   for (int i = 0; i < MR; ++i) {
     const int m = m0 + wm * WM + i * 16 + (lane & 15);
@@ -178,11 +190,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[
         }
         o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
         *p = o;
-      } else {
+      } else if constexpr (OUT == 2) {
         float* p = static_cast<float*>(g.c) + (long long)m * g.ldc + n;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           __hip_atomic_fetch_add(p + r, v[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {   // OUT 3: this K-slice's partial tile into slab tz (plain 16-byte stores)
+        float* p = static_cast<float*>(g.c) + (long long)tz * g.M * g.ldc + (long long)m * g.ldc + n;
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
   }
@@ -279,7 +294,7 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
     }
   }
 
-  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane);
+  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tz);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -294,6 +309,41 @@ __device__ __forceinline__ bf16x8_t frag_kc64(const char* lds, int row0, int lan
   const int r = row0 + (lane & 15);
   const int c = lane >> 4;
   return *reinterpret_cast<const bf16x8_t*>(lds + r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
+}
+
+// Fragment reads as inline asm (k_gemm8): hipcc's waitcnt pass cannot count LDS reads
+// across the loop back-edge and would put lgkmcnt(0) in front of every MFMA cluster; with
+// the reads hidden from it, each C segment waits with its own counted lgkmcnt (CDNA guide
+// §5.4 rule 18: a sched_barrier(0) follows every such wait).
+__device__ __forceinline__ unsigned lds_off(const char* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ bf16x8_t ds_rd128(const char* p) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_off(p)));
+  return v;
+}
+__device__ __forceinline__ v4s_t ds_rd_tr(const char* p) {
+  v4s_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(lds_off(p)));
+  return v;
+}
+__device__ __forceinline__ bf16x8_t frag_kc64_asm(const char* lds, int row0, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = lane >> 4;
+  return ds_rd128(lds + r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
+}
+template <int R>
+__device__ __forceinline__ bf16x8_t frag_ks_asm(const char* lds, int row0, int lane) {  // k rows 0-31
+  const int il = lane & 15, g = lane >> 4;
+  const int col = row0 + 4 * (il & 3);
+  const int k0 = 8 * g + (il >> 2);
+  const int k1 = k0 + 4;
+  const int ch = col >> 3, within = (col & 7) * 2;
+  v4s_t lo = ds_rd_tr(lds + k0 * (2 * R) + ((ch ^ swz_ks<R>(k0)) << 4) + within);
+  v4s_t hi = ds_rd_tr(lds + k1 * (2 * R) + ((ch ^ swz_ks<R>(k1)) << 4) + within);
+  bf16x8_t f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return f;
 }
 
 template <int R, bool KC>
@@ -417,7 +467,217 @@ __global__ __launch_bounds__(NT) void k_gemm4(GemmArgs g) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane);
+  gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tz);
+}
+
+// ---------------------------------------------------------------------------------------
+// 256 x 256 tile, two-group phase schedule (CDNA guide §5 "256² 8-phase template", T3-T5).
+//
+// K-tiles of 64 are split into four 16 KB half-tiles {A k0-31, B k0-31, A k32-63, B
+// k32-63}; LDS holds two K-tiles (8 half-tile slots, 128 KB).  A K-tile is four PHASES:
+//   q = 0: k 0-31,  wave rows 0-63   (reads 4 A + 4 B fragments)
+//   q = 1: k 0-31,  wave rows 64-127 (reads 4 A; B fragments kept)
+//   q = 2 / 3: the same on k 32-63
+// and every phase is an L segment (fragment ds_reads + this thread's two LDS-DMAs of one
+// half-tile) and a C segment (lgkmcnt(0), 16 MFMAs under s_setprio 1), separated by raw
+// s_barriers.  Waves 4-7 (group 1, the M rows 128-255) run one barrier behind waves 0-3,
+// so on every SIMD one wave is in its MFMA segment while its partner reads / issues DMAs:
+// the matrix pipe never waits for the LDS.
+//
+// Half-tile h (= 4 * tile + q) is issued in phase h - 5, i.e. five half-tiles ahead; its
+// slot was last read >= 2 phases earlier (WAR safe for both groups).  The L segment of
+// phase P reads phase P+1's fragments (register double buffer), so the MFMAs never wait
+// for a just-issued ds_read.  Each group retires DMAs with ONE counted vmcnt per two
+// phases — group 0 vmcnt(4) after even phases, group 1 vmcnt(2) after odd phases — which
+// lands every half-tile before the barrier that precedes its first read by either group
+// (derivation in the comment of k_gemm8 below).
+//
+// Epilogue (bf16 out): bias / erf-GELU in registers, the tile staged through the (now
+// idle) LDS with a row-XOR swizzle, then 16-byte row-contiguous global stores (512 B per
+// half-wave): full cache lines instead of 16 rows x 32 B per store instruction.
+// ---------------------------------------------------------------------------------------
+template <bool A_KC, bool B_KC, int OUT>
+__global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
+  constexpr int HT = 256 * 32 * 2;  // half-tile bytes
+  constexpr int MR = 8, NR = 4;     // wave tile 128 x 64
+  __shared__ __attribute__((aligned(1024))) char smem[8 * HT];
+
+  int tx, ty, tz;
+  xcd_tile(tx, ty, tz);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = ty * 256, n0 = tx * 256;
+  const int kbeg = tz * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
+
+  Stager32<256, A_KC> sa;
+  Stager32<256, B_KC> sb;
+  sa.init(g.a, g.lda, m0, g.M, wave, lane);
+  sb.init(g.b, g.ldb, n0, g.N, wave, lane);
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile h -> slot (h/4 & 1)*4 + h%4; past the last K-tile the stager reads the zero
+  // page (kb >= kend), so the DMA count per phase never changes
+  auto issue_h = [&](int h) {
+    const int u = h >> 2, q = h & 3;
+    char* dst = smem + ((u & 1) * 4 + q) * HT;
+    const int kb = kbeg + u * 64 + ((q & 2) ? 32 : 0);
+    if (q & 1) sb.issue(dst, kb, kend, g.zp, wave);
+    else sa.issue(dst, kb, kend, g.zp, wave);
+  };
+
+  if (nk > 0) {
+    // fragment double buffer: the L segment of phase P reads phase P+1's fragments, so the
+    // C segment's counted lgkmcnt only waits for reads issued a whole phase earlier
+    bf16x8_t af0[4], af1[4], bf0[NR], bf1[NR];
+    auto read_frags = [&](auto qc, int u, bf16x8_t(&af)[4], bf16x8_t(&bfr)[NR]) {
+      constexpr int q = decltype(qc)::value;
+      const char* sA = smem + ((u & 1) * 4 + ((q & 2) ? 2 : 0)) * HT;
+      const char* sB = smem + ((u & 1) * 4 + ((q & 2) ? 3 : 1)) * HT;
+      if constexpr ((q & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          bfr[j] = B_KC ? frag_kc64_asm(sB, wn * 64 + j * 16, lane) : frag_ks_asm<256>(sB, wn * 64 + j * 16, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + (q & 1) * 64 + i * 16;
+        af[i] = A_KC ? frag_kc64_asm(sA, r, lane) : frag_ks_asm<256>(sA, r, lane);
+      }
+    };
+    // LDS read instructions one L segment issues for phase q (B fragments on even q only)
+    constexpr int RA = A_KC ? 4 : 8, RB = B_KC ? 4 : 8;
+    // Phase P = 4u + q.  Group 0: L_P between barriers 2P and 2P+1, C_P between 2P+1 and
+    // 2P+2; group 1 one barrier later.  L_P reads phase P+1's fragments; C_P's lgkmcnt
+    // retires phase P's reads (issued in L_{P-1}) before barrier 2P+2 (group 0) / 2P+3
+    // (group 1).  WAR: a slot holding phase-R data is refilled by the DMA of L_{R+2}, past
+    // barrier 2R+4 for both groups.  RAW: the lo half-tiles of tile u+1 (issued in phases
+    // 4u-1, 4u) are first read in L_{4u+3} (group 0 after barrier 8u+6): group 0's vmcnt(4)
+    // after C_{4u+2} and group 1's vmcnt(2) after C_{4u+1} retire them before barriers
+    // 8u+6 / 8u+5.  The hi half-tiles (issued 4u+1, 4u+2) are first read in L_{4u+5} (after
+    // barrier 8u+10): group 0's wait after C_{4u+4}, group 1's after C_{4u+3}.
+    auto phase = [&](auto qc, int u, bf16x8_t(&afc)[4], bf16x8_t(&bfc)[NR], bf16x8_t(&afn)[4],
+                     bf16x8_t(&bfn)[NR]) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int qn = (q + 1) & 3;
+      const int P = 4 * u + q;
+      // ---- L segment: next phase's fragments + one half-tile of DMA
+      read_frags(std::integral_constant<int, qn>{}, qn == 0 ? u + 1 : u, afn, bfn);
+      issue_h(P + 5);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- C segment: retire phase P's fragment reads (issued in L_{P-1}); L_P's stay in flight
+      constexpr int NREAD = RA + ((qn & 1) == 0 ? RB : 0);
+      if constexpr (NREAD >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+      else if constexpr (NREAD == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+      else if constexpr (NREAD == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[(q & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfc[j], afc[i], acc[(q & 1) * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (q & 1) {
+        if (wm == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        if (wm == 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+#pragma unroll
+    for (int h = 0; h < 5; ++h) issue_h(h);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // tile 0 landed (half-tile 4 may fly)
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();           // group 1 starts one barrier behind
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(std::integral_constant<int, 0>{}, 0, af0, bf0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int u = 0; u < nk; ++u) {
+      phase(std::integral_constant<int, 0>{}, u, af0, bf0, af1, bf0);   // reads phase 1 (A only)
+      phase(std::integral_constant<int, 1>{}, u, af1, bf0, af0, bf1);   // reads phase 2 (A + B)
+      phase(std::integral_constant<int, 2>{}, u, af0, bf1, af1, bf1);   // reads phase 3 (A only)
+      phase(std::integral_constant<int, 3>{}, u, af1, bf1, af0, bf0);   // reads phase 4 = next tile q 0
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // trailing DMAs / reads touch LDS
+  }
+
+  if constexpr (OUT != 0) {
+    gemm_epilogue<OUT, MR, NR, 128, 64>(g, acc, m0, n0, wm, wn, lane, tz);
+  } else {
+    __syncthreads();
+    float4 bias4[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      bias4[j] = (g.bias && n < g.N) ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // fp32 accumulators -> (+bias, act) bf16 -> swizzled LDS tile [256][256]
+    auto stage = [&](bool act) {
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const int row = wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const int col = wn * 64 + j * 16 + 4 * (lane >> 4);
+          float v0 = acc[i][j][0] + bias4[j].x, v1 = acc[i][j][1] + bias4[j].y;
+          float v2 = acc[i][j][2] + bias4[j].z, v3 = acc[i][j][3] + bias4[j].w;
+          if (act) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3); }
+          uint2 p;
+          p.x = pack_bf2(v0, v1);
+          p.y = pack_bf2(v2, v3);
+          const int off = row * 512 + (((col >> 3) ^ (row & 15)) << 4) + ((col >> 2) & 1) * 8;
+          *reinterpret_cast<uint2*>(smem + off) = p;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one fragment row at a time: bounds the temporaries
+      }
+      __syncthreads();
+    };
+    // LDS tile -> 16-byte row-contiguous global stores (512 B per half-wave)
+    auto store = [&](bf16_t* dst) {
+#pragma unroll 2
+      for (int it = 0; it < 16; ++it) {
+        const int idx = it * NT + tid;
+        const int row = idx >> 5, ch = idx & 31;
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * 512 + ((ch ^ (row & 15)) << 4));
+        const int m = m0 + row, n = n0 + ch * 8;
+        if (m < g.M && n < g.N) *reinterpret_cast<uint4*>(dst + (long long)m * g.ldc + n) = v;
+      }
+      __syncthreads();
+    };
+    if (g.c2) {   // pre-activation copy first: the accumulators stay live across it
+      stage(false);
+      store(g.c2);
+    }
+    stage(g.act == 1);
+    store(static_cast<bf16_t*>(g.c));
+  }
+}
+
+template <bool A_KC, bool B_KC, int OUT>
+int launch8(GemmArgs g, int splits, hipStream_t s) {
+  splits = splits < 1 ? 1 : splits;
+  int chunk = (g.K + splits - 1) / splits;
+  chunk = ((chunk + 63) / 64) * 64;
+  g.kchunk = chunk > 0 ? chunk : 64;
+  const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
+  dim3 grid((g.N + 255) / 256, (g.M + 255) / 256, z);
+  hipLaunchKernelGGL((k_gemm8<A_KC, B_KC, OUT>), grid, dim3(NT), 0, s, g);
+  KML_LAUNCH_CHECK();
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S = (3 * (BM + BN) * BK * 2 <= 160 * 1024) ? 3 : 2>
@@ -453,8 +713,31 @@ int by_tile(const GemmArgs& g, int tile, int splits, hipStream_t s) {
     case 3: return launch<128, 128, A_KC, B_KC, OUT>(g, splits, s);
     case 4: return launch<128, 128, A_KC, B_KC, OUT, 2>(g, splits, s);   // 2 stages: 2 blocks per CU
     case 5: return launch4<A_KC, B_KC, OUT>(g, splits, s);
+    case 6: return launch8<A_KC, B_KC, OUT>(g, splits, s);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// dw[i] = beta * dw[i] + sum_z slab[z][i] over float4 columns, in slab order (deterministic).
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ slab, float* __restrict__ dw,
+                                                       long long n4, int S, float beta) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 acc = beta != 0.f ? reinterpret_cast<const float4*>(dw)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (beta != 0.f && beta != 1.f) { acc.x *= beta; acc.y *= beta; acc.z *= beta; acc.w *= beta; }
+    int z = 0;
+    for (; z + 4 <= S; z += 4) {   // four slabs in flight per thread
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const float4*>(slab)[(long long)(z + u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; z < S; ++z) {
+      const float4 v = reinterpret_cast<const float4*>(slab)[(long long)z * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[i] = acc;
+  }
 }
 
 }  // namespace
@@ -462,9 +745,11 @@ int by_tile(const GemmArgs& g, int tile, int splits, hipStream_t s) {
 // layout: 0 = forward (A KC, B KC), 1 = dgrad (A KC, B KS), 2 = wgrad (A KS, B KS)
 // out:    0 = bf16 (+bias, act, pre-act copy), 1 = fp32 beta, 2 = fp32 atomic (split-K)
 // tile:   0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128 (BM x BN; 3-stage where LDS allows),
-//         4 = 128x128 with 2 stages (64 KB: two blocks per CU), 5 = 256x256 BK=32 4-slot ring
+//         4 = 128x128 with 2 stages (64 KB: two blocks per CU), 5 = 256x256 BK=32 4-slot ring,
+//         6 = 256x256 two-group phase schedule (k_gemm8)
 // Host contract (checked by ops/gemm.py): N % 4 == 0, ldc % 4 == 0, K-contiguous leading
-// dimensions % 8 == 0, 16-byte aligned pointers; a zero page of >= 16 bytes.
+// dimensions % 8 == 0, 16-byte aligned pointers; a zero page of >= 16 bytes.  Tile 6 with
+// bf16 output also needs N % 8 == 0 and ldc % 8 == 0 (16-byte staged stores).
 KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, void* c, long long ldc,
                      bf16_t* c2, const float* bias, const bf16_t* zp, int M, int N, int K, int layout, int out,
                      int act, float beta, int tile, int splits, hipStream_t s) {
@@ -481,4 +766,28 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   if (layout == 2 && out == 1) return by_tile<false, false, 1>(g, tile, 1, s);
   if (layout == 2 && out == 2) return by_tile<false, false, 2>(g, tile, splits, s);
   return (int)hipErrorInvalidValue;
+}
+
+// Deterministic split-K weight gradient: dw[M][N] = beta * dw + sum_k A^T B (layout 2), each
+// K-slice's fp32 partial tile stored to slab[z] (plain coalesced stores, no atomics), then one
+// bandwidth-bound pass sums the slabs in order into dw.  dw and slab are contiguous (ldc == N);
+// slab holds splits * M * N floats.
+KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, float* dw,
+                                  float* slab, const bf16_t* zp, int M, int N, int K, float beta, int tile, int splits,
+                                  hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  GemmArgs g;
+  g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
+  g.lda = lda; g.ldb = ldb; g.ldc = N;
+  g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K;
+  splits = splits < 1 ? 1 : splits;
+  int rc = by_tile<false, false, 3>(g, tile, splits, s);
+  if (rc) return rc;
+  // the launcher rounds the K chunk up to the tile's K step: count the slices it produced
+  int step = (tile == 5 || tile == 6) ? 64 : BK;
+  int chunk = ((K + splits - 1) / splits + step - 1) / step * step;
+  const int z = K > 0 ? (K + chunk - 1) / chunk : 1;
+  const long long n4 = (long long)M * N / 4;
+  hipLaunchKernelGGL(k_splitk_reduce, dim3(kml_stream_grid(n4, 256)), dim3(256), 0, s, slab, dw, n4, z, beta);
+  KML_LAUNCH_CHECK();
 }

@@ -18,7 +18,8 @@ from .._native import HIP, stream_ptr
 
 BF16 = torch.bfloat16
 F32 = torch.float32
-TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5}  # (BM, BN[, stages])
+TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5,
+         (256, 256, 8): 6}  # (BM, BN[, stages])
 _TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _TUNED: dict = {}
 if os.path.exists(_TUNE_FILE) and os.environ.get("KUBEML_GEMM_TUNING", "1") != "0":
@@ -95,12 +96,41 @@ def gemm(a, lda, b, ldb, c, ldc, M, N, K, layout, out, bias=None, act=0, c2=None
         pt, ps = plan(layout, M, N, K)
         tile = tile or pt
         splits = splits or ps
+    if out == 3:
+        return wgrad_splitk_(c, a, lda, b, ldb, M, N, K, beta=beta, tile=tile, splits=splits)
     if out != 2:
         splits = 1
+    if TILES[tuple(tile)] == 6 and out == 0 and (N % 8 or ldc % 8):
+        raise ValueError("gemm: the 256x256 phase tile with bf16 output needs N and ldc % 8 == 0")
     HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", a.data_ptr(), int(lda), b.data_ptr(), int(ldb),
              c.data_ptr(), int(ldc), 0 if c2 is None else c2.data_ptr(), 0 if bias is None else bias.data_ptr(),
              _zp(a.device).data_ptr(), int(M), int(N), int(K), int(layout), int(out), int(act), float(beta),
              TILES[tuple(tile)], int(splits), stream_ptr())
+
+
+def wgrad_splitk_(dw, a, lda, b, ldb, M, N, K, beta=1.0, tile=(256, 256, 8), splits=None):
+    """dw[M][N] (fp32, contiguous) = beta * dw + A^T B with A [K][M], B [K][N] (layout 2):
+    every K-slice stores its fp32 partial tile to a slab, one pass sums the slabs in order
+    (deterministic, no atomics).  ``splits`` defaults to filling 256 CUs with one tile each."""
+    _check(a, BF16, "a")
+    _check(b, BF16, "b")
+    _check(dw, F32, "dw")
+    if not dw.is_contiguous() or dw.numel() != M * N:
+        raise ValueError("wgrad_splitk_: dw must be a contiguous [M][N] fp32 tensor")
+    if N % 4 or lda % 8 or ldb % 8:
+        raise ValueError("wgrad_splitk_: N % 4 and leading dimensions % 8 must be 0")
+    bm, bn = tile[0], tile[1]
+    if splits is None:
+        tiles = _cdiv(M, bm) * _cdiv(N, bn)
+        splits = max(1, min(64, round(256 / tiles), K // 256))
+    step = 64
+    chunk = _cdiv(_cdiv(K, splits), step) * step
+    nz = _cdiv(K, chunk)
+    slab = torch.empty(nz * M * N, dtype=F32, device=dw.device)
+    HIP.call("kml_gemm_wgrad_splitk", "p l p l p p p i i i f i i s", a.data_ptr(), int(lda), b.data_ptr(), int(ldb),
+             dw.data_ptr(), slab.data_ptr(), _zp(a.device).data_ptr(), int(M), int(N), int(K), float(beta),
+             TILES[tuple(tile)], int(splits), stream_ptr())
+    return dw
 
 
 def linear_fwd(x, w, bias=None, act=0, pre=None):
@@ -144,5 +174,7 @@ def linear_wgrad_(dw, dy, x):
     if not dw.is_contiguous():
         raise ValueError("linear_wgrad_: dw must be contiguous")
     tile, splits = plan(2, op, ip, T)
+    if len(tile) == 4:    # (BM, BN, stages, "slab"): deterministic slab split-K
+        return wgrad_splitk_(dw, dy, op, x, ip, op, ip, T, beta=1.0, tile=tile[:3], splits=splits)
     gemm(dy, op, x, ip, dw, ip, op, ip, T, 2, 2 if splits > 1 else 1, beta=1.0, tile=tile, splits=splits)
     return dw

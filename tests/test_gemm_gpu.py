@@ -17,7 +17,8 @@ def _rand(*s, scale=1.0):
     return (torch.randn(*s, device=dev) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 128), (128, 256), (128, 128), (128, 128, 2)])
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128),
+                                  (128, 128, 2)])
 @pytest.mark.parametrize("T,ip,op", [(512, 768, 2304), (200, 72, 136), (1216, 768, 1000)])
 def test_forward_bias_gelu(tile, T, ip, op):
     from kubeml_amd.ops import gemm as G
@@ -32,7 +33,7 @@ def test_forward_bias_gelu(tile, T, ip, op):
     assert _rel(y, torch.nn.functional.gelu(h)) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (128, 128)])
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (128, 128)])
 @pytest.mark.parametrize("T,ip,op", [(512, 768, 3072), (200, 72, 136)])
 def test_dgrad(tile, T, ip, op):
     from kubeml_amd.ops import gemm as G
@@ -43,7 +44,8 @@ def test_dgrad(tile, T, ip, op):
     assert _rel(dx, dy.float() @ w.float()) < 1e-2
 
 
-@pytest.mark.parametrize("tile,splits", [((256, 256), 1), ((256, 256, 4), 1), ((256, 256, 4), 2), ((128, 128), 1),
+@pytest.mark.parametrize("tile,splits", [((256, 256), 1), ((256, 256, 4), 1), ((256, 256, 4), 2), ((256, 256, 8), 1),
+                                         ((256, 256, 8), 3), ((128, 128), 1),
                                          ((256, 128), 4), ((128, 128), 3)])
 @pytest.mark.parametrize("T,ip,op", [(2048, 768, 768), (200, 72, 136)])
 def test_wgrad_accumulates(tile, splits, T, ip, op):
@@ -55,6 +57,54 @@ def test_wgrad_accumulates(tile, splits, T, ip, op):
     G.gemm(dy, op, x, ip, dw, ip, op, ip, T, 2, 2 if splits > 1 else 1, beta=1.0, tile=tile, splits=splits)
     ref = dw0.double() + dy.double().t() @ x.double()
     assert _rel(dw, ref) < 1e-4
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2])
+@pytest.mark.parametrize("K", [8, 64, 96, 128, 320, 4096])
+def test_phase_tile_reduction_lengths(layout, K):
+    """k_gemm8's five-half-tiles-ahead DMA schedule and group stagger at every pipeline
+    depth: a single partial K-tile up to a long reduction; ragged M / N edges."""
+    from kubeml_amd.ops import gemm as G
+    torch.manual_seed(5 + K)
+    M, N = 296, 264
+    if layout == 0:
+        A, B = _rand(M, K), _rand(N, K, scale=0.05)
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        G.gemm(A, K, B, K, C, N, M, N, K, 0, 0, tile=(256, 256, 8), splits=1)
+        ref = A.double() @ B.double().t()
+        tol = 1e-2
+    elif layout == 1:
+        A, B = _rand(M, K), _rand(K, N, scale=0.05)
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        G.gemm(A, K, B, N, C, N, M, N, K, 1, 0, tile=(256, 256, 8), splits=1)
+        ref = A.double() @ B.double()
+        tol = 1e-2
+    else:
+        A, B = _rand(K, M), _rand(K, N)
+        C = torch.zeros(M, N, device=dev)
+        G.gemm(A, M, B, N, C, N, M, N, K, 2, 1, beta=1.0, tile=(256, 256, 8), splits=1)
+        ref = A.double().t() @ B.double()
+        tol = 1e-4
+    assert _rel(C, ref) < tol
+
+
+@pytest.mark.parametrize("tile,splits", [((256, 256, 8), None), ((256, 256, 8), 5), ((256, 256, 4), 3),
+                                         ((128, 128, 2), 2), ((128, 128), 7)])
+@pytest.mark.parametrize("T,ip,op", [(4096, 768, 2304), (1000, 72, 136)])
+def test_wgrad_slab_split_k(tile, splits, T, ip, op):
+    """Deterministic slab split-K weight gradient: fp32 partial tiles summed in slice order,
+    bit-identical across repeated launches (no atomics)."""
+    from kubeml_amd.ops import gemm as G
+    torch.manual_seed(6)
+    dy, x = _rand(T, op), _rand(T, ip)
+    dw0 = torch.randn(op, ip, device=dev)
+    dw = dw0.clone()
+    G.wgrad_splitk_(dw, dy, op, x, ip, op, ip, T, beta=1.0, tile=tile, splits=splits)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    assert _rel(dw, ref) < 1e-4
+    dw2 = dw0.clone()
+    G.wgrad_splitk_(dw2, dy, op, x, ip, op, ip, T, beta=1.0, tile=tile, splits=splits)
+    assert torch.equal(dw, dw2)
 
 
 def test_dgrad_split_k_long_reduction():

@@ -38,12 +38,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--write", default=None, help="write the winners to this tuning json")
+    ap.add_argument("--shapes", default=None, help="custom shapes 'layout:M:N:K;...' instead of BERT's")
+    ap.add_argument("--tiles", default="all", help="comma list of tile names to try, e.g. 256x256x8,128x128x2")
     a = ap.parse_args()
     from kubeml_amd.ops import gemm as G
     dev = torch.device("cuda", 0)
     T = a.tokens
     entries, rows = [], []
-    for name, layout, M, N, K in shapes(T):
+    todo = shapes(T)
+    if a.shapes:
+        todo = [("custom", *[int(v) for v in sh.split(":")]) for sh in a.shapes.split(";")]
+    for name, layout, M, N, K in todo:
         # operands in their natural buffers
         if layout == 0:
             A = torch.randn(M, K, device=dev).to(torch.bfloat16)              # x [T][ip]
@@ -64,16 +69,29 @@ def main():
             lda, ldb, out = M, N, 1
             ref = lambda: torch.addmm(C, A.t(), B, out_dtype=torch.float32)
         cands = []
-        for tile in ((256, 256), (256, 256, 4), (256, 128), (128, 256), (128, 128), (128, 128, 2)):
+        for tile in ((256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128), (128, 128, 2)):
+            tname = "x".join(str(v) for v in tile)
+            if a.tiles != "all" and tname not in a.tiles.split(","):
+                continue
             for s in ((1,) if layout != 2 else (1, 2, 4, 8, 16)):
                 if layout == 2 and s > 1 and K // s < 256:
                     continue
                 cands.append((tile, s))
+            if layout == 2:   # deterministic slab split-K (kml_gemm_wgrad_splitk)
+                tiles = -(-M // tile[0]) * -(-N // tile[1])
+                base = max(1, round(256 / tiles))
+                for s in sorted({max(1, base // 2), base, base * 2}):
+                    if K // s >= 256:
+                        cands.append((tile + ("slab",), s))
 
         def run(tile, s):
+            if tile[-1] == "slab":
+                G.wgrad_splitk_(C, A, lda, B, ldb, M, N, K, beta=1.0, tile=tile[:-1], splits=s)
+                return
             G.gemm(A, lda, B, ldb, C, N, M, N, K, layout, out if s == 1 else 2, beta=1.0 if layout == 2 else 0.0,
                    tile=tile, splits=s)
-        nm = lambda t, s: f"{t[0]}x{t[1]}" + (f"x{t[2]}st" if len(t) > 2 else "") + f"/s{s}"
+        nm = lambda t, s: (f"{t[0]}x{t[1]}" + (f"x{t[2]}st" if len(t) > 2 and t[2] != "slab" else "")
+                           + (f"/k{s}" if t[-1] == "slab" else f"/s{s}"))
         fns = [("torch", ref)] + [(nm(t, s), (lambda t=t, s=s: run(t, s))) for t, s in cands]
         for _, f in fns:
             f()
