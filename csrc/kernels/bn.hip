@@ -157,6 +157,52 @@ __device__ void sum_partial_rows(const float* __restrict__ part, int G, int W, f
   }
 }
 
+// sum_partial_rows split in two so its first batch of loads can be ISSUED before the
+// caller's data loads (vmcnt retires in issue order: a row sum issued after the data
+// would wait for the data's HBM round trip).  Single pass over the columns (W/4 <= NT);
+// rows beyond the first batch of 16 per slice are summed in finish().
+struct EarlyRows {
+  float4 v[16];
+  int q, sl, S, Q;
+  __device__ __forceinline__ void issue(const float* __restrict__ part, int G, int W, int nt) {
+    Q = W / 4;
+    S = nt / Q;
+    q = (int)threadIdx.x % Q;
+    sl = (int)threadIdx.x / Q;
+    const float4* p4 = reinterpret_cast<const float4*>(part) + q;
+    if (sl < S) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p4[(long long)min(sl + u * S, G - 1) * Q];
+    }
+  }
+  __device__ __forceinline__ void finish(const float* __restrict__ part, int G, float* out, float4* scratch) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (sl < S) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const bool in = sl + u * S < G;
+        acc.x += in ? v[u].x : 0.f; acc.y += in ? v[u].y : 0.f;
+        acc.z += in ? v[u].z : 0.f; acc.w += in ? v[u].w : 0.f;
+      }
+      if (sl + 16 * S < G) {
+        const float4 r = sum_rows_strided(reinterpret_cast<const float4*>(part) + q, sl + 16 * S, G, S, Q);
+        acc.x += r.x; acc.y += r.y; acc.z += r.z; acc.w += r.w;
+      }
+    }
+    scratch[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < Q) {
+      float4 t4 = scratch[threadIdx.x];
+      for (int k = 1; k < S; ++k) {
+        const float4 w = scratch[k * Q + threadIdx.x];
+        t4.x += w.x; t4.y += w.y; t4.z += w.z; t4.w += w.w;
+      }
+      reinterpret_cast<float4*>(out)[threadIdx.x] = t4;
+    }
+    __syncthreads();
+  }
+};
+
 // y = act((x - mean) * rstd * gamma + beta [+ res])
 // mode 0: training (stats = [sum, sumsq] over M rows); mode 1: eval (running stats)
 template <int NT>
@@ -535,6 +581,177 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_fin(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Register-resident apply kernels (the default).  Each thread owns V 16-byte chunks
+// i0, i0 + T, ..., T = grid * NT a multiple of C/8, so all its chunks hold the SAME 8
+// channels: their scale / shift (or the backward coefficients) are read from LDS once,
+// into registers, and no per-element channel division or LDS read remains.  All V chunks
+// of every operand are loaded up front — before the statistics prologue — so the data
+// round trip overlaps the partial-row reduction instead of following it, and a thread
+// never waits on more than one memory round trip.  Out-of-range chunks load a clamped
+// (valid) index and skip the store (no branch around a load: straight-line vmcnt).
+// ---------------------------------------------------------------------------------------
+template <int NT, int V>
+__global__ __launch_bounds__(NT) void k_bn_apply_v(
+    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
+    float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode,
+    int stats_rows) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], (sums[2C], scratch)
+  float* scale = sh;
+  float* shift = sh + C;
+  const int n8 = (int)(M * C / 8);
+  const int T = (int)gridDim.x * NT;
+  const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
+  const bool parts = mode == 0 && stats_rows > 0;
+  const bool early = parts && C / 2 <= NT;
+  EarlyRows er;
+  if (early) er.issue(stats, stats_rows, 2 * C, NT);
+  uint4 xv[V], rv[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) xv[v] = reinterpret_cast<const uint4*>(x)[min(i0 + v * T, n8 - 1)];
+  if (res) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) rv[v] = reinterpret_cast<const uint4*>(res)[min(i0 + v * T, n8 - 1)];
+  }
+  const float* st = stats;
+  if (parts) {
+    float* sums = sh + 2 * C;
+    if (early) er.finish(stats, stats_rows, sums, reinterpret_cast<float4*>(sh + 4 * C));
+    else sum_partial_rows<NT>(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 4 * C));
+    st = sums;
+  }
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float mean, var;
+    if (mode == 0) {
+      mean = st[c] / (float)M;
+      var = fmaxf(st[C + c] / (float)M - mean * mean, 0.f);
+    } else {
+      mean = run_mean[c];
+      var = run_var[c];
+    }
+    const float rstd = rsqrtf(var + eps);
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    scale[c] = g * rstd;
+    shift[c] = bb - mean * g * rstd;
+    if (mode == 0 && blockIdx.x == 0) {
+      if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
+      if (run_mean) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+      }
+    }
+  }
+  __syncthreads();
+  const int c0 = (i0 % (C / 8)) * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sf[k] = shift[c0 + k]; }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    float f[8], r[8];
+    unpack8(xv[v], f);
+    if (res) unpack8(rv[v], r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = f[k] * sc[k] + sf[k];
+      if (res) o += r[k];
+      if (relu) o = fmaxf(o, 0.f);
+      f[k] = o;
+    }
+    const int i = i0 + v * T;
+    if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+template <int NT, int V>
+__global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
+    const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
+  float4* red4 = reinterpret_cast<float4*>(sh);
+  float* ka = sh + 4 * NT;
+  float* kb = ka + C;
+  float* kc = ka + 2 * C;
+  float* mu = ka + 3 * C;
+  float* rs = ka + 4 * C;
+  const float invM = 1.f / (float)M;
+  const int n8 = (int)(M * C / 8);
+  const int T = (int)gridDim.x * NT;
+  const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
+  const bool early = C / 2 <= NT;
+  EarlyRows er;
+  if (early) er.issue(part, G, 2 * C, NT);
+  uint4 dv[V], xv[V], yv[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int i = min(i0 + v * T, n8 - 1);
+    dv[v] = reinterpret_cast<const uint4*>(dy)[i];
+    xv[v] = reinterpret_cast<const uint4*>(x)[i];
+  }
+  if (y) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) yv[v] = reinterpret_cast<const uint4*>(y)[min(i0 + v * T, n8 - 1)];
+  }
+  // the G partial rows [dbeta (C) | dgamma (C)] summed in a fixed order (deterministic)
+  // kb | kc are contiguous: kb[0..C) kc[0..C)
+  if (early) er.finish(part, G, kb, red4);
+  else sum_partial_rows<NT>(part, G, 2 * C, kb, red4);
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const float sb = kb[c], sg = kc[c];
+    if (blockIdx.x == 0) { dbeta[c] += sb; dgamma[c] += sg; }
+    const float gm = gamma ? gamma[c] : 1.f;
+    ka[c] = gm * rstd[c];
+    mu[c] = mean[c];
+    rs[c] = rstd[c];
+  }
+  __syncthreads();
+  const int c0 = (i0 % (C / 8)) * 8;
+  float a8[8], b8[8], g8[8], m8[8], r8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a8[k] = ka[c0 + k]; b8[k] = kb[c0 + k] * invM; g8[k] = kc[c0 + k] * invM;
+    m8[k] = mu[c0 + k]; r8[k] = rs[c0 + k];
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    float d[8], xf[8];
+    unpack8(dv[v], d);
+    unpack8(xv[v], xf);
+    if (y) {
+      float yf[8];
+      unpack8(yv[v], yf);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+    }
+    const int i = i0 + v * T;
+    if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (xf[k] - m8[k]) * r8[k];
+      o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+    }
+    if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+  }
+}
+
+// chunks per thread for the register-resident kernels: about 256 blocks, at most VMAX
+static int pick_v(long long n8, int vmax) {
+  long long v = (n8 + 256LL * TPB - 1) / (256LL * TPB);
+  int r = 1;
+  while (r < v && r < vmax) r *= 2;
+  return r;
+}
+
+static bool reg_ok(long long M, int C) {
+  return C % 8 == 0 && (TPB % (C / 8)) == 0 && M * C / 8 < (1LL << 30);
+}
+
 // relu backward alone: dx = dy * [y > 0]  (bf16, x8)
 // (bn_bwd_apply_partial below reuses k_bn_bwd_apply_fin with partials from a conv epilogue)
 __global__ void k_relu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
@@ -626,6 +843,20 @@ static bool wide_sum(int G, int C) {
 static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                                 const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
                                 float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
+  if (reg_ok(M, C)) {
+    const long long n8 = M * C / 8;
+    const int V = pick_v(n8, 4);
+    const unsigned grid = (unsigned)((n8 + (long long)TPB * V - 1) / ((long long)TPB * V));
+    const size_t shm = (4 * TPB + 5 * C) * sizeof(float);
+#define KML_BWD_V(VV)                                                                                          \
+  hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, dy, y, x, mean, rstd, gamma, part, \
+                     G, dgamma, dbeta, dx, dres, M, C)
+    if (V == 1) KML_BWD_V(1);
+    else if (V == 2) KML_BWD_V(2);
+    else KML_BWD_V(4);
+#undef KML_BWD_V
+    KML_LAUNCH_CHECK();
+  }
   if (wide_sum(G, C)) {
     constexpr int NT = 1024;
     long long ab = (M * C / 8 + NT - 1) / NT;
@@ -647,6 +878,21 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
                          float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
                          hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (reg_ok(M, C)) {
+    const long long n8 = M * C / 8;
+    const int V = pick_v(n8, 8);
+    const unsigned grid = (unsigned)((n8 + (long long)TPB * V - 1) / ((long long)TPB * V));
+    const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
+#define KML_AP_V(VV)                                                                                           \
+  hipLaunchKernelGGL((k_bn_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y,        \
+                     save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows)
+    if (V == 1) KML_AP_V(1);
+    else if (V == 2) KML_AP_V(2);
+    else if (V == 4) KML_AP_V(4);
+    else KML_AP_V(8);
+#undef KML_AP_V
+    KML_LAUNCH_CHECK();
+  }
   if (stats_rows > 0 && wide_sum(stats_rows, C)) {
     constexpr int NT = 1024;
     const size_t shm = (4 * C + 4 * NT) * sizeof(float);
