@@ -649,20 +649,31 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
   float sc[8], sf[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sf[k] = shift[c0 + k]; }
+  // grid-stride batches of V chunks (large tensors); T % (C/8) == 0 keeps the channels
+  for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
+    if (it > 0) {
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    float f[8], r[8];
-    unpack8(xv[v], f);
-    if (res) unpack8(rv[v], r);
+      for (int v = 0; v < V; ++v) xv[v] = reinterpret_cast<const uint4*>(x)[min(base + v * T, n8 - 1)];
+      if (res) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float o = f[k] * sc[k] + sf[k];
-      if (res) o += r[k];
-      if (relu) o = fmaxf(o, 0.f);
-      f[k] = o;
+        for (int v = 0; v < V; ++v) rv[v] = reinterpret_cast<const uint4*>(res)[min(base + v * T, n8 - 1)];
+      }
     }
-    const int i = i0 + v * T;
-    if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float f[8], r[8];
+      unpack8(xv[v], f);
+      if (res) unpack8(rv[v], r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = f[k] * sc[k] + sf[k];
+        if (res) o += r[k];
+        if (relu) o = fmaxf(o, 0.f);
+        f[k] = o;
+      }
+      const int i = base + v * T;
+      if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+    }
   }
 }
 
@@ -717,36 +728,91 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
     a8[k] = ka[c0 + k]; b8[k] = kb[c0 + k] * invM; g8[k] = kc[c0 + k] * invM;
     m8[k] = mu[c0 + k]; r8[k] = rs[c0 + k];
   }
+  for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
+    if (it > 0) {
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    float d[8], xf[8];
-    unpack8(dv[v], d);
-    unpack8(xv[v], xf);
-    if (y) {
-      float yf[8];
-      unpack8(yv[v], yf);
+      for (int v = 0; v < V; ++v) {
+        const int i = min(base + v * T, n8 - 1);
+        dv[v] = reinterpret_cast<const uint4*>(dy)[i];
+        xv[v] = reinterpret_cast<const uint4*>(x)[i];
+      }
+      if (y) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+        for (int v = 0; v < V; ++v) yv[v] = reinterpret_cast<const uint4*>(y)[min(base + v * T, n8 - 1)];
+      }
     }
-    const int i = i0 + v * T;
-    if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
-    float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float xh = (xf[k] - m8[k]) * r8[k];
-      o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+    for (int v = 0; v < V; ++v) {
+      float d[8], xf[8];
+      unpack8(dv[v], d);
+      unpack8(xv[v], xf);
+      if (y) {
+        float yf[8];
+        unpack8(yv[v], yf);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+      }
+      const int i = base + v * T;
+      if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (xf[k] - m8[k]) * r8[k];
+        o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+      }
+      if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
     }
-    if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
   }
 }
 
-// chunks per thread for the register-resident kernels: about 256 blocks, at most VMAX
+// Fold G partial rows [G][W] into ceil(G / R) rows (fixed order: deterministic), so the
+// apply kernels' per-block prologue stays small when a large conv (ResNet-50 at 56x56:
+// 3136 M-tiles) left thousands of rows.  grid = (ceil(W / 4 / 64), ceil(G / R)).
+__global__ __launch_bounds__(256) void k_rows_fold(const float* __restrict__ part, float* __restrict__ out, int G,
+                                                   int W, int R) {
+  const int Q = W / 4;
+  const int q = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6;                 // 4 row slices
+  const int r0 = blockIdx.y * R, r1 = min(G, r0 + R);
+  __shared__ float4 red[256];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < Q) {
+    const float4* p4 = reinterpret_cast<const float4*>(part) + q;
+    for (int r = r0 + sl; r < r1; r += 4) {
+      const float4 v = p4[(long long)r * Q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64 && q < Q) {
+    float4 t = red[threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 v = red[k * 64 + threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[(long long)blockIdx.y * Q + q] = t;
+  }
+}
+
+// chunks per thread for the register-resident kernels: about 256 blocks, at most VMAX;
+// past VMAX the grid grows to at most 1024 blocks and the kernel grid-strides
 static int pick_v(long long n8, int vmax) {
   long long v = (n8 + 256LL * TPB - 1) / (256LL * TPB);
   int r = 1;
   while (r < v && r < vmax) r *= 2;
   return r;
 }
+static unsigned v_grid(long long n8, int V) {
+  long long g = (n8 + (long long)TPB * V - 1) / ((long long)TPB * V);
+  if (g > 1024) g = 1024;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// G partial rows of W floats above this many bytes are folded by k_rows_fold first
+constexpr long long FOLD_BYTES = 64 * 1024;
+constexpr int FOLD_R = 32;
 
 static bool reg_ok(long long M, int C) {
   return C % 8 == 0 && (TPB % (C / 8)) == 0 && M * C / 8 < (1LL << 30);
@@ -846,7 +912,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 4);
-    const unsigned grid = (unsigned)((n8 + (long long)TPB * V - 1) / ((long long)TPB * V));
+    const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 5 * C) * sizeof(float);
 #define KML_BWD_V(VV)                                                                                          \
   hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, dy, y, x, mean, rstd, gamma, part, \
@@ -873,15 +939,31 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
 }
 
 // stats_rows > 0: stats is [stats_rows][2C] partial sums (conv epilogue), summed here
+// fold rows [G][W] -> ws [ceil(G / FOLD_R)][W] when they are large; returns the rows to use
+static const float* maybe_fold(const float* part, int& G, int W, float* ws, hipStream_t s) {
+  if (!ws || (long long)G * W * 4 <= FOLD_BYTES) return part;
+  const int NG = (G + FOLD_R - 1) / FOLD_R;
+  hipLaunchKernelGGL(k_rows_fold, dim3((unsigned)((W / 4 + 63) / 64), (unsigned)NG), dim3(256), 0, s, part, ws, G, W,
+                     FOLD_R);
+  G = NG;
+  return ws;
+}
+
+// rows of fp32 workspace (x 2C floats) kml_bn_apply / kml_bn_bwd_apply_partial may use to fold G rows
+KML_API int kml_bn_fold_rows(int G, int C) {
+  return (long long)G * 2 * C * 4 <= FOLD_BYTES ? 0 : (G + FOLD_R - 1) / FOLD_R;
+}
+
 KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, const float* gamma, const float* beta,
                          const bf16_t* res, bf16_t* y, float* save_mean, float* save_rstd, float* run_mean,
                          float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
-                         hipStream_t s) {
+                         float* fold_ws, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (mode == 0 && stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 8);
-    const unsigned grid = (unsigned)((n8 + (long long)TPB * V - 1) / ((long long)TPB * V));
+    const unsigned grid = v_grid(n8, V);
     const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
 #define KML_AP_V(VV)                                                                                           \
   hipLaunchKernelGGL((k_bn_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y,        \
@@ -949,8 +1031,10 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
 // computed dy (conv_dgrad bnf_*): a single apply kernel, no reduction pass over dy/y/x.
 KML_API int kml_bn_bwd_apply_partial(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                                      const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
-                                     float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
+                                     float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, float* fold_ws,
+                                     hipStream_t s) {
   if (C % 8 || C / 8 > TPB || G <= 0) return (int)hipErrorInvalidValue;
+  part = maybe_fold(part, G, 2 * C, fold_ws, s);
   return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, s);
 }
 

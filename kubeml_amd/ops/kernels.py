@@ -506,6 +506,12 @@ def bn_stats_part(x2d):
     return part, G
 
 
+def _fold_ws(G, C, dev):
+    """Workspace for folding a large [G][2C] partial-row buffer (kml_bn_fold_rows) or None."""
+    n = HIP.fn("kml_bn_fold_rows", "i i")(int(G), int(C))
+    return torch.empty(n * 2 * C, dtype=F32, device=dev) if n > 0 else None
+
+
 def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=None, run_mean=None,
              run_var=None, eps=1e-5, momentum=0.1, relu=False, training=True, stats_rows=0):
     _chk(x, BF16, "x")
@@ -517,10 +523,11 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
         _chk(res, BF16, "res")
         if res.shape != x.shape:
             raise ValueError("residual shape mismatch")
-    HIP.call("kml_bn_apply", "p p i p p p p p p p p l i f f i i s",
+    ws = _fold_ws(stats_rows, C, x.device) if training and stats_rows > 0 else None
+    HIP.call("kml_bn_apply", "p p i p p p p p p p p l i f f i i p s",
              _p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
              _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu),
-             0 if training else 1, _s())
+             0 if training else 1, _p(ws), _s())
     return y
 
 
@@ -541,9 +548,9 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         dx = torch.empty_like(x)
     if partial is not None:
         part, G = partial
-        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i s",
+        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p s",
                  _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
-                 _p(dx), _p(dres), M, C, _s())
+                 _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), _s())
         return dx
     ws = cnt = None
     if _BN_REDUCE in ("fused", "ticket"):
