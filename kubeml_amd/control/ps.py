@@ -288,7 +288,20 @@ class ParameterServer:
         r.add("DELETE", "/stop/{jobId}", lambda q: self.stop_task(q.params["jobId"]) or "")
         r.add("GET", "/tasks", lambda q: [t.to_dict() for t in self.list_tasks()])
         r.add("GET", "/health", lambda q: "")
+        # each TrainJob's own REST surface (reference: one job pod per TrainJob serving
+        # ml/pkg/train/api.go:141-149), reached through the PS on this single node
+        r.add("GET|POST|DELETE", "/job/{jobId}/{op}", self._job_dispatch)
         return r
+
+    def _job_dispatch(self, q):
+        from ..api.errors import NotFoundError
+        job = self.jobs.get(q.params["jobId"])
+        if job is None:
+            raise NotFoundError(f"job {q.params['jobId']}")
+        jr = getattr(job, "_router", None)
+        if jr is None:
+            jr = job._router = job.router()
+        return jr.dispatch(q.method, "/" + q.params["op"], q.query, q.headers, q.body)
 
     def metrics_router(self) -> Router:
         from .http import Response

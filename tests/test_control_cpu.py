@@ -114,6 +114,31 @@ def test_train_validate_history_infer(env):
     assert jid in [x.id for x in c.histories.list()]
 
 
+def test_job_rest_surface_through_ps(env):
+    """The TrainJob's own routes (reference ml/pkg/train/api.go) are served via the PS:
+    /job/{id}/status while the job runs, 404 for an unknown job."""
+    import time
+    from kubeml_amd.control.http import call
+    srv, c, _ = env
+    req = TrainRequest(batch_size=64, epochs=4, dataset="mnist", lr=0.05, function_name="lenet",
+                       options=TrainOptions(default_parallelism=1, static_parallelism=True, validate_every=0, k=4,
+                                            goal_accuracy=100))
+    jid = c.networks.train(req)
+    st, t0 = None, time.time()
+    while time.time() - t0 < 60:
+        try:
+            st = call("GET", srv.url("ps") + f"/job/{jid}/status")
+            break
+        except HttpError:
+            time.sleep(0.05)
+    assert st is not None and st["id"] == jid and st["parallelism"] == 1, st
+    assert call("GET", srv.url("ps") + f"/job/{jid}/health") in ("", b"", None)
+    with pytest.raises(HttpError) as e:
+        call("GET", srv.url("ps") + "/job/nosuchjob/status")
+    assert e.value.status_code == 404
+    assert _wait(c, jid)["state"] == "finished"
+
+
 def test_request_validation_errors(env):
     srv, c, _ = env
     with pytest.raises(HttpError) as e:
