@@ -27,7 +27,7 @@ def _ref_attn(q, k, v, B, H, L, bias):
 
 
 @pytest.mark.parametrize("B,H,L,use_bias", [(2, 3, 128, False), (2, 2, 100, True), (1, 12, 512, False),
-                                            (3, 1, 64, True), (1, 2, 7, False)])
+                                            (3, 1, 64, True), (1, 2, 7, False), (2, 2, 300, True)])
 def test_attention_fwd_bwd(B, H, L, use_bias):
     from kubeml_amd.ops import transformer as T
     torch.manual_seed(0)
@@ -153,7 +153,7 @@ def _attn_keep(seed, step, salt, B, H, L, p):
     return torch.from_numpy(keep)
 
 
-@pytest.mark.parametrize("L", [64, 100])
+@pytest.mark.parametrize("L", [64, 100, 300])
 def test_attention_dropout_matches_masked_reference(L):
     """Fused attention with probability dropout vs fp32 autograd on the same mask
     (forward output, dQ/dK/dV); dropout rate close to p."""

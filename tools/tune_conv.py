@@ -137,7 +137,7 @@ def tune_pairs(layers, table, reps, dev):
                 try:
                     t = bench(lambda: K.conv_bwd(dy, w, x, dw, k, k, (s, s), (p, p), wt=wt, dcfg=dc, wcfg=wc),
                               reps=reps)
-                except RuntimeError:
+                except (RuntimeError, ValueError):
                     continue
                 res.append((t, dc, wc))
         if not res:
@@ -240,7 +240,7 @@ def main():
             for cfg in cands:
                 try:
                     res.append((bench(lambda: run(cfg), reps=args.reps), cfg))
-                except RuntimeError:
+                except (RuntimeError, ValueError):
                     pass
             res.sort()
             t_def = bench(lambda: run(default), reps=args.reps)
