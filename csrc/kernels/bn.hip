@@ -811,7 +811,7 @@ static unsigned v_grid(long long n8, int V) {
 }
 
 // G partial rows of W floats above this many bytes are folded by k_rows_fold first
-constexpr long long FOLD_BYTES = 64 * 1024;
+constexpr long long FOLD_BYTES = 512 * 1024;   // ResNet-50 56x56 rows fold; ResNet-34 never (a fold launch costs ~5 us)
 constexpr int FOLD_R = 32;
 
 static bool reg_ok(long long M, int C) {
