@@ -11,8 +11,8 @@
 //           key tile; both recompute P from the saved LSE — no atomics, deterministic.
 //
 // Attention-probability dropout (HF BERT attention_probs_dropout_prob): keep mask
-// Z[b,h,q,key] = hash(seed ^ salt, step, b, h, q, key) >= p * 2^32 recomputed in all three
-// kernels (nothing stored).  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
+// Z[b,h,q,key] = half16(hash(seed ^ salt, step, b, h, q, key / 2), key & 1) >= p * 2^16,
+// recomputed in all three kernels (nothing stored; one hash per key pair).  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
 // the undropped probabilities; backward: dV = (P (.) Z/(1-p))^T dO, dP = (dO V^T) (.) Z/(1-p),
 // dS = P (.) (dP - D) with D = rowsum(dO (.) O) (unchanged by the mask).
 //
@@ -55,24 +55,29 @@ __device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
   return h;
 }
 
-// per-kernel dropout state: keep(q, key) = 1/(1-p) or 0
+// per-kernel dropout state.  One 32-bit hash per (q, key pair): its low 16 bits decide the
+// even key, the high 16 bits the odd one (threshold p * 2^16) — half the hashing of one hash
+// per element, and the inner loops always visit keys in aligned pairs.
 struct Drop {
   unsigned k0, k1, thr;
   float sc;
-  int L;
+  unsigned LP;   // key pairs per query row
   bool on;
   __device__ void init(const AttnArgs& a, int bh) {
     on = a.ctr != nullptr && a.pdrop > 0.f;
-    L = a.L;
+    LP = (unsigned)(a.L + 1) >> 1;
     if (on) {
       k0 = (unsigned)a.ctr[0] ^ a.salt;
       k1 = (unsigned)a.ctr[1] * 0x632BE5ABu ^ (unsigned)bh * 0x5851F42Du;
-      thr = (unsigned)(a.pdrop * 4294967296.0f);
+      thr = (unsigned)(a.pdrop * 65536.0f);
       sc = 1.f / (1.f - a.pdrop);
     }
   }
-  __device__ __forceinline__ float keep(int q, int key) const {
-    return ahash(k0, k1, (unsigned)q * (unsigned)L + (unsigned)key) >= thr ? sc : 0.f;
+  // keep factors of keys (key, key + 1), key even
+  __device__ __forceinline__ void keep2(int q, int key, float& z0, float& z1) const {
+    const unsigned h = ahash(k0, k1, (unsigned)q * LP + ((unsigned)key >> 1));
+    z0 = (h & 0xFFFFu) >= thr ? sc : 0.f;
+    z1 = (h >> 16) >= thr ? sc : 0.f;
   }
 };
 
@@ -115,12 +120,18 @@ __device__ __forceinline__ bf16x8_t frag_tr(const char* lds, int col0, int ks, i
 }
 
 // bf16 operand from 8 accumulator values of tiles 2ks, 2ks+1 (the permuted k order)
-__device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& t0, const f32x4_t& t1) {
-  bf16x8_t f;
-  f[0] = (short)f2bf(t0[0]); f[1] = (short)f2bf(t0[1]); f[2] = (short)f2bf(t0[2]); f[3] = (short)f2bf(t0[3]);
-  f[4] = (short)f2bf(t1[0]); f[5] = (short)f2bf(t1[1]); f[6] = (short)f2bf(t1[2]); f[7] = (short)f2bf(t1[3]);
-  return f;
+// (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN — one instruction per pair)
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned cvt2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t{a, b}), bf16x2_hw));
 }
+__device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& t0, const f32x4_t& t1) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  const u32x4_t u = {cvt2(t0[0], t0[1]), cvt2(t0[2], t0[3]), cvt2(t1[0], t1[1]), cvt2(t1[2], t1[3])};
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }  // v_exp_f32
 
 __device__ __forceinline__ bf16x8_t load_frag_g(const bf16_t* row_ptr, int ks, int g, bool ok) {
   if (!ok) { bf16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0}; return z; }
@@ -198,13 +209,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m2, mx);
     const bool dead = mn == -INFINITY;
-    const float alpha = dead ? 1.f : exp2f(m2 - mn);
+    const float alpha = dead ? 1.f : fexp2(m2 - mn);
     float ps = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float p = dead ? 0.f : exp2f(s[t][i] - mn);
+        const float p = dead ? 0.f : fexp2(s[t][i] - mn);
         s[t][i] = p;
         ps += p;
       }
@@ -219,7 +230,12 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s[t][i] *= drop.keep(qq, kb * 64 + 16 * t + 4 * g + i);
+        for (int i = 0; i < 4; i += 2) {
+          float z0, z1;
+          drop.keep2(qq, kb * 64 + 16 * t + 4 * g + i, z0, z1);
+          s[t][i] *= z0;
+          s[t][i + 1] *= z1;
+        }
     }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
 #pragma unroll
@@ -304,13 +320,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; i += 2) {
         const int key = kb * 64 + 16 * t + 4 * g + i;
-        float v = s[t][i] * sl2;
-        if (bias && key < L) v += bias[key] * LOG2E;
-        const float p = key < L ? exp2f(v - lse) : 0.f;
-        const float dpv = drop.on ? dp[t][i] * drop.keep(q, key) : dp[t][i];
-        s[t][i] = p * (dpv - D);
+        float z0 = 1.f, z1 = 1.f;
+        if (drop.on) drop.keep2(q, key, z0, z1);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          float v = s[t][i + e] * sl2;
+          if (bias && key + e < L) v += bias[key + e] * LOG2E;
+          const float p = key + e < L ? fexp2(v - lse) : 0.f;
+          s[t][i + e] = p * (dp[t][i + e] * (e ? z1 : z0) - D);
+        }
       }
     const bf16x8_t d0 = pack_p(s[0], s[1]), d1 = pack_p(s[2], s[3]);
 #pragma unroll
@@ -391,8 +411,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * t + 4 * g + i;
-        const float p = exp2f(s[t][i] * sl2 + kb2 - sL[r]);
-        const float z = drop.on ? drop.keep(qb * 64 + r, key) : 1.f;
+        const float p = fexp2(s[t][i] * sl2 + kb2 - sL[r]);
+        float z = 1.f;
+        if (drop.on) {   // this lane's key pairs with the neighbour lane's key (key ^ 1)
+          float z0, z1;
+          drop.keep2(qb * 64 + r, key & ~1, z0, z1);
+          z = (key & 1) ? z1 : z0;
+        }
         s[t][i] = p * z;
         dp[t][i] = p * (dp[t][i] * z - sD[r]);
       }

@@ -132,12 +132,12 @@ def _attn_keep(seed, step, salt, B, H, L, p):
     def mul(a, b):
         return (a.astype(np.uint64) * np.uint64(b)) & M
 
-    thr = np.uint64(int(np.float32(p) * np.float32(4294967296.0)))
+    thr = np.uint64(int(np.float32(p) * np.float32(65536.0)))
     k0 = np.uint64((int(seed) ^ salt) & 0xFFFFFFFF)
     keep = np.zeros((B, H, L, L), dtype=np.float32)
     q = np.arange(L, dtype=np.uint64).reshape(L, 1)
     key = np.arange(L, dtype=np.uint64).reshape(1, L)
-    c = (q * np.uint64(L) + key) & M
+    c = (q * np.uint64((L + 1) // 2) + (key >> np.uint64(1))) & M   # one hash per key pair
     for b in range(B):
         for h in range(H):
             bh = np.uint64(b * H + h)
@@ -149,7 +149,8 @@ def _attn_keep(seed, step, salt, B, H, L, p):
             hh ^= hh >> np.uint64(12)
             hh = mul(hh, 0x297A2D39)
             hh ^= hh >> np.uint64(15)
-            keep[b, h] = np.where(hh >= thr, 1.0 / (1.0 - p), 0.0)
+            half = np.where((key & np.uint64(1)) == 1, hh >> np.uint64(16), hh & np.uint64(0xFFFF))
+            keep[b, h] = np.where(half >= thr, 1.0 / (1.0 - p), 0.0)
     return torch.from_numpy(keep)
 
 
