@@ -21,17 +21,16 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((unsigned)v) << 16);
 }
 
-// round-to-nearest-even; NaN stays NaN (quiet bit forced)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
 
+// two floats -> packed bf16 pair with gfx950's v_cvt_pk_bf16_f32 (round-to-nearest-even,
+// NaN stays NaN): one VALU instruction instead of two software roundings
+typedef __bf16 kml_bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float kml_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack_bf2(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((kml_f32x2_t{a, b}), kml_bf16x2_hw));
 }
+// round-to-nearest-even; NaN stays NaN
+__device__ __forceinline__ bf16_t f2bf(float f) { return (bf16_t)(pack_bf2(f, 0.f) & 0xffffu); }
 
 __device__ __forceinline__ float lo_bf(unsigned w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
