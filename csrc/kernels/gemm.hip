@@ -122,7 +122,7 @@ struct Stager {
   }
 };
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf(float x) { return kml_gelu(x); }
 
 // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a contiguous run of
 // tiles (bijective remap, CDNA guide T1), and walk that run in GROUPS of up to 8 tile rows

@@ -171,12 +171,8 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ par
 }
 
 // ------------------------------------------------------------------------------ GELU (erf form)
-__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+__device__ __forceinline__ float gelu(float x) { return kml_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return kml_gelu_grad(x); }
 
 __global__ void k_gelu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long long n4) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -207,21 +203,26 @@ __device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
   return h;
 }
 
-// y = x * keep / (1 - p); keep = hash(seed, step, salt, i) >= p * 2^32; ctr = [seed, step]
+// y = x * keep / (1 - p); ctr = [seed, step].  One hash per element PAIR j (elements 2j,
+// 2j+1): keep = 16-bit half of hash(seed ^ salt, step, j) >= p * 2^16.  8 elements (16 B)
+// per thread per iteration, 4 hashes.
 __global__ void k_dropout(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, const float* __restrict__ ctr,
-                          unsigned salt, float p, long long n4) {
+                          unsigned salt, float p, long long n8) {
   const unsigned seed = (unsigned)ctr[0], step = (unsigned)ctr[1];
-  const unsigned thr = (unsigned)(p * 4294967296.0);
+  const unsigned thr = (unsigned)(p * 65536.0f);
   const float sc = 1.f / (1.f - p);
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    float f[4];
-    ld4(x + i * 4, f);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 v = reinterpret_cast<const uint4*>(x)[i];
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+    unsigned o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const unsigned hsh = hash3(seed ^ salt, step, (unsigned)(i * 4 + k));
-      f[k] = hsh >= thr ? f[k] * sc : 0.f;
+      const float a = (hsh & 0xFFFFu) >= thr ? lo_bf(w[k]) * sc : 0.f;
+      const float b = (hsh >> 16) >= thr ? hi_bf(w[k]) * sc : 0.f;
+      o[k] = pack_bf2(a, b);
     }
-    st4(y + i * 4, f);
+    reinterpret_cast<uint4*>(y)[i] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -374,8 +375,8 @@ KML_API int kml_gelu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long lon
 
 KML_API int kml_dropout(const bf16_t* x, bf16_t* y, const float* ctr, unsigned salt, float p, long long n,
                         hipStream_t s) {
-  if (n % 4 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_dropout, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, x, y, ctr, salt, p, n / 4);
+  if (n % 8 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dropout, dim3(kml_stream_grid(n / 8, 256)), dim3(256), 0, s, x, y, ctr, salt, p, n / 8);
   KML_LAUNCH_CHECK();
 }
 
