@@ -49,23 +49,65 @@ __device__ void ce_fold(const float* __restrict__ rowloss, const float* __restri
   }
 }
 
+// bf16 rows with C % 8 == 0 (16-byte aligned): 8 logits per lane per load; the running
+// max is updated once per 8-element chunk (one rescale v_exp per chunk instead of a
+// dependent exp + branch per element), exponentials in the base-2 domain (v_exp_f32).
+constexpr float LOG2E_CE = 1.4426950408889634f;
+__device__ __forceinline__ void unpack8f(const uint4& v, float* f) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+// (m2, s): running max of x*log2e and sum of 2^(x*log2e - m2); argmax over the lane's elements
+__device__ __forceinline__ void row_pass_vec(const bf16_t* __restrict__ x, int C, int lane, float& m2, float& s,
+                                             float& vmax, int& amax) {
+  m2 = -INFINITY; s = 0.f; vmax = -INFINITY; amax = 0;
+  const uint4* x8 = reinterpret_cast<const uint4*>(x);
+  const int n8 = (C + 7) / 8;   // the row is padded to a multiple of 8 (ld); pad columns masked
+  for (int c8 = lane; c8 < n8; c8 += 64) {
+    float f[8];
+    unpack8f(x8[c8], f);
+    if (c8 * 8 + 8 > C) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) if (c8 * 8 + k >= C) f[k] = -INFINITY;
+    }
+    float cm = f[0];
+    int ci = 0;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) if (f[k] > cm) { cm = f[k]; ci = k; }
+    if (cm > vmax) { vmax = cm; amax = c8 * 8 + ci; }
+    const float mn = fmaxf(m2, cm * LOG2E_CE);
+    float add = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) add += __builtin_amdgcn_exp2f(fmaf(f[k], LOG2E_CE, -mn));
+    s = (m2 == -INFINITY ? 0.f : s * __builtin_amdgcn_exp2f(m2 - mn)) + add;
+    m2 = mn;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_ce_fwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                                                 float* __restrict__ lse, float* __restrict__ rowloss,
-                                                float* __restrict__ rowcorrect, int B, int C, long long ignore,
-                                                unsigned* __restrict__ ticket, float* __restrict__ out3) {
+                                                float* __restrict__ rowcorrect, int B, int C, int ld,
+                                                long long ignore, unsigned* __restrict__ ticket,
+                                                float* __restrict__ out3) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row < B) {
-    const T* x = logits + (long long)row * C;
+    const T* x = logits + (long long)row * ld;
     float m = -INFINITY, s = 0.f;
     int amax = 0;
     float vmax = -INFINITY;
-    for (int c = lane; c < C; c += 64) {
-      const float v = ldf<T>(x + c);
-      if (v > vmax) { vmax = v; amax = c; }
-      if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
-      else s += __expf(v - m);
+    if (sizeof(T) == 2 && (ld & 7) == 0) {
+      float m2;
+      row_pass_vec(reinterpret_cast<const bf16_t*>(x), C, lane, m2, s, vmax, amax);
+      m = m2 * 0.69314718055994531f;   // back to natural-log units for the combine below
+    } else {
+      for (int c = lane; c < C; c += 64) {
+        const float v = ldf<T>(x + c);
+        if (v > vmax) { vmax = v; amax = c; }
+        if (v > m) { s = s * __expf(m - v) + 1.f; m = v; }
+        else s += __expf(v - m);
+      }
     }
     // combine (m, s) across the wave
   #pragma unroll
@@ -118,7 +160,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, const long long* __restrict__ labels,
                                                 const float* __restrict__ lse, const float* __restrict__ red,
                                                 const float* __restrict__ grad_out, T* __restrict__ dlogits, int B,
-                                                int C, long long ignore) {
+                                                int C, int ld, long long ignore) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -127,10 +169,33 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
   const float valid = red[2];
   const float g = (grad_out ? *grad_out : 1.f) / fmaxf(valid, 1.f);
   const float l = lse[row];
-  const T* x = logits + (long long)row * C;
-  T* d = dlogits + (long long)row * C;
-  for (int c = lane; c < C; c += 64) {
-    float v = skip ? 0.f : (__expf(ldf<T>(x + c) - l) - (c == y ? 1.f : 0.f)) * g;
+  const T* x = logits + (long long)row * ld;
+  T* d = dlogits + (long long)row * ld;
+  if constexpr (sizeof(T) == 2) {
+    if ((ld & 7) == 0) {   // 16-byte loads / stores, base-2 exponentials; pad columns -> 0
+      const uint4* x8 = reinterpret_cast<const uint4*>(x);
+      uint4* d8 = reinterpret_cast<uint4*>(d);
+      const float l2 = l * LOG2E_CE;
+      for (int c8 = lane; c8 < ld / 8; c8 += 64) {
+        float f[8];
+        unpack8f(x8[c8], f);
+        unsigned o[4];
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const int c = c8 * 8 + k;
+          const float a = (skip || c >= C) ? 0.f
+                          : (__builtin_amdgcn_exp2f(fmaf(f[k], LOG2E_CE, -l2)) - (c == y ? 1.f : 0.f)) * g;
+          const float b = (skip || c + 1 >= C) ? 0.f
+                          : (__builtin_amdgcn_exp2f(fmaf(f[k + 1], LOG2E_CE, -l2)) - (c + 1 == y ? 1.f : 0.f)) * g;
+          o[k / 2] = pack_bf2(a, b);
+        }
+        d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      return;
+    }
+  }
+  for (int c = lane; c < ld; c += 64) {
+    float v = (skip || c >= C) ? 0.f : (__expf(ldf<T>(x + c) - l) - (c == y ? 1.f : 0.f)) * g;
     if constexpr (sizeof(T) == 2) d[c] = f2bf(v); else d[c] = v;
   }
 }
@@ -139,29 +204,32 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
 
 // dtype: 0 = bf16 logits, 1 = fp32 logits.  ws = [3*B] fp32 workspace (lse, rowloss, rowcorrect).
 // ticket: a zeroed device counter (reset by the kernel) -> one launch; null -> fold in a 2nd launch.
-KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, float* out3, int B, int C,
+// ld: row stride of the logits (>= C; a row padded to 16 bytes keeps the vector path, the
+// pad columns are ignored in the forward and written as 0 in the gradient)
+KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, float* out3, int B, int C, int ld,
                        long long ignore, int dtype, unsigned* ticket, hipStream_t s) {
-  if (B < 1) return (int)hipErrorInvalidValue;
+  if (B < 1 || ld < C) return (int)hipErrorInvalidValue;
   dim3 g((B + 3) / 4);
   if (dtype == 0)
     hipLaunchKernelGGL(k_ce_fwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, ws + B, ws + 2 * B,
-                       B, C, ignore, ticket, out3);
+                       B, C, ld, ignore, ticket, out3);
   else
     hipLaunchKernelGGL(k_ce_fwd<float>, g, dim3(256), 0, s, (const float*)logits, labels, ws, ws + B, ws + 2 * B, B,
-                       C, ignore, ticket, out3);
+                       C, ld, ignore, ticket, out3);
   if (!ticket) hipLaunchKernelGGL(k_ce_reduce, dim3(1), dim3(1024), 0, s, ws + B, ws + 2 * B, out3, B);
   KML_LAUNCH_CHECK();
 }
 
 KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
-                       const float* grad_out, void* dlogits, int B, int C, long long ignore, int dtype,
+                       const float* grad_out, void* dlogits, int B, int C, int ld, long long ignore, int dtype,
                        hipStream_t s) {
+  if (ld < C) return (int)hipErrorInvalidValue;
   dim3 g((B + 3) / 4);
   if (dtype == 0)
     hipLaunchKernelGGL(k_ce_bwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, out3, grad_out,
-                       (bf16_t*)dlogits, B, C, ignore);
+                       (bf16_t*)dlogits, B, C, ld, ignore);
   else
     hipLaunchKernelGGL(k_ce_bwd<float>, g, dim3(256), 0, s, (const float*)logits, labels, ws, out3, grad_out,
-                       (float*)dlogits, B, C, ignore);
+                       (float*)dlogits, B, C, ld, ignore);
   KML_LAUNCH_CHECK();
 }

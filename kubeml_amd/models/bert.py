@@ -152,10 +152,12 @@ class BertForMaskedLM(tnn.Module):
             h = gather_rows(h, idx)
         t = self.cls.predictions.transform
         z = t.LayerNorm(t.dense(h, act="gelu"))
-        logits = self.cls.predictions.decoder(z)
         if labels is None:
-            return logits
-        return cross_entropy(logits, labels.reshape(-1), ignore_index=-100, return_correct=return_correct)
+            return self.cls.predictions.decoder(z)
+        # vocab-padded logits used in place (no slice copy / gradient re-pad of [T, 30528])
+        logits = self.cls.predictions.decoder(z, keep_pad=True)
+        return cross_entropy(logits, labels.reshape(-1), ignore_index=-100, return_correct=return_correct,
+                             classes=self.vocab)
 
 
     def stages(self, ids, token_type_ids=None, attention_mask=None, mlm_positions=None, labels=None, n: int = 3):
@@ -196,7 +198,8 @@ class BertForMaskedLM(tnn.Module):
                 h = gather_rows(h, (mlm_positions + base).reshape(-1).contiguous())
             t = self.cls.predictions.transform
             z = t.LayerNorm(t.dense(h, act="gelu"))
-            return cross_entropy(self.cls.predictions.decoder(z), labels.reshape(-1), ignore_index=-100)
+            return cross_entropy(self.cls.predictions.decoder(z, keep_pad=True), labels.reshape(-1),
+                                 ignore_index=-100, classes=self.vocab)
         fns = [first] + [mid(g) for g in groups[1:-1]] + [last]
         params = [list(self.bert.embeddings.parameters()) + [p for l in groups[0] for p in l.parameters()]]
         params += [[p for l in g for p in l.parameters()] for g in groups[1:-1]]

@@ -168,7 +168,7 @@ class _LinearFn(Function):
     pre-activation is kept for backward)."""
 
     @staticmethod
-    def forward(ctx, x2, weight, bias, mod, act):
+    def forward(ctx, x2, weight, bias, mod, act, keep_pad=False):
         from ..ops import kernels as K
         op, ip = mod.out_pad, mod.in_pad
         B = x2.shape[0]
@@ -192,7 +192,8 @@ class _LinearFn(Function):
         ctx.mod, ctx.x, ctx.has_bias, ctx.act = mod, x2, bias is not None, act
         ctx.y = y if act == 1 else None
         ctx.pre = pre
-        if op != mod.out_features:
+        ctx.keep_pad = keep_pad
+        if op != mod.out_features and not keep_pad:
             y = y[:, :mod.out_features].contiguous()
         return y
 
@@ -205,7 +206,7 @@ class _LinearFn(Function):
         dy = dy.contiguous()
         if dy.dtype != torch.bfloat16:
             dy = dy.to(torch.bfloat16)
-        if op != mod.out_features:
+        if op != mod.out_features and dy.shape[1] != op:
             dy = K.pad_channels(dy, op)
         if ctx.act == 1:
             dy = K.relu_bwd(dy, ctx.y)
@@ -235,7 +236,7 @@ class _LinearFn(Function):
         if ctx.has_bias:
             K.colsum_(dy, grad_storage_of(mod.bias))
         ctx.x = ctx.y = ctx.pre = None
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
 class Linear(tnn.Module):
@@ -266,9 +267,11 @@ class Linear(tnn.Module):
     def extra_repr(self):
         return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
 
-    def forward(self, x, act: Optional[str] = None):
+    def forward(self, x, act: Optional[str] = None, keep_pad: bool = False):
         """act: None (module default: fused ReLU if constructed so), "gelu" (erf-GELU fused
-        into the GEMM epilogue on the GPU)."""
+        into the GEMM epilogue on the GPU).  keep_pad: on the GPU return the [N, out_pad]
+        output whose columns past out_features are zero (no slice copy; a consumer that
+        knows the real width — ``cross_entropy(classes=...)`` — uses it in place)."""
         a = 2 if act == "gelu" else (1 if self.fused_relu else 0)
         if not _on_gpu(x):
             y = F.linear(x, self.weight, self.bias)
@@ -282,7 +285,7 @@ class Linear(tnn.Module):
         if a == 2 and _linear_route(x.shape[0], self.in_pad, self.out_pad, 2) != "gemm":
             from .transformer import GELU
             return GELU()(_LinearFn.apply(x.contiguous(), self.weight, self.bias, self, 0))
-        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, a)
+        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, a, keep_pad)
 
 
 # ======================================================================================
@@ -468,26 +471,31 @@ def to_nhwc(x, cin_pad=None):
 
 class _CEFn(Function):
     @staticmethod
-    def forward(ctx, logits, labels, ignore_index):
+    def forward(ctx, logits, labels, ignore_index, classes=None):
         from ..ops import kernels as K
-        out3, ws, lab = K.ce_fwd(logits, labels, ignore_index)
-        ctx.save = (logits, lab, ws, out3, ignore_index)
+        out3, ws, lab = K.ce_fwd(logits, labels, ignore_index, classes=classes)
+        ctx.save = (logits, lab, ws, out3, ignore_index, classes)
         ctx.out3 = out3
         return out3[0]
 
     @staticmethod
     def backward(ctx, g):
         from ..ops import kernels as K
-        logits, lab, ws, out3, ig = ctx.save
-        d = K.ce_bwd(logits, lab, ws, out3, grad_out=g.reshape(1).float().contiguous(), ignore_index=ig)
+        logits, lab, ws, out3, ig, classes = ctx.save
+        d = K.ce_bwd(logits, lab, ws, out3, grad_out=g.reshape(1).float().contiguous(), ignore_index=ig,
+                     classes=classes)
         ctx.save = None
-        return d, None, None
+        return d, None, None, None
 
 
-def cross_entropy(logits, labels, ignore_index=-100, return_correct=False):
+def cross_entropy(logits, labels, ignore_index=-100, return_correct=False, classes=None):
     """Mean softmax cross-entropy (fused HIP kernel on GPU).  With return_correct the
-    device-side argmax==label count of the same pass is returned as well."""
+    device-side argmax==label count of the same pass is returned as well.  ``classes``:
+    the real class count when ``logits`` rows are padded past it (a ``keep_pad`` Linear
+    output; the pad columns are ignored and get a zero gradient)."""
     if not logits.is_cuda:
+        if classes is not None:
+            logits = logits[:, :classes]
         loss = F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
         if return_correct:
             valid = labels != ignore_index
@@ -496,11 +504,11 @@ def cross_entropy(logits, labels, ignore_index=-100, return_correct=False):
     if return_correct:
         from ..ops import kernels as K
         if torch.is_grad_enabled() and logits.requires_grad:
-            loss = _CEFn.apply(logits.contiguous(), labels, ignore_index)
+            loss = _CEFn.apply(logits.contiguous(), labels, ignore_index, classes)
             return loss, loss.grad_fn.out3[1]  # grad_fn is the Function ctx; same fused pass
-        out3, _, _ = K.ce_fwd(logits.contiguous(), labels, ignore_index)
+        out3, _, _ = K.ce_fwd(logits.contiguous(), labels, ignore_index, classes=classes)
         return out3[0], out3[1]
-    return _CEFn.apply(logits.contiguous(), labels, ignore_index)
+    return _CEFn.apply(logits.contiguous(), labels, ignore_index, classes)
 
 
 _ONES: dict = {}

@@ -649,29 +649,36 @@ def gavgpool_bwd(dy, in_shape):
 # loss
 # --------------------------------------------------------------------------------------
 
-def ce_fwd(logits, labels, ignore_index=-100):
-    """Returns (out3, ws): out3 = [mean loss, correct, valid] fp32 on device."""
+def ce_fwd(logits, labels, ignore_index=-100, classes=None):
+    """Returns (out3, ws): out3 = [mean loss, correct, valid] fp32 on device.  ``classes``:
+    number of real classes when ``logits`` is [B, ld] with the rows padded past them (a
+    padded Linear output used in place: no slice copy)."""
     if logits.dim() != 2:
         raise ValueError("logits must be [B, C]")
     if not logits.is_contiguous():
         logits = logits.contiguous()
     dt = {BF16: 0, F32: 1}[logits.dtype]
-    B, C = logits.shape
+    B, ld = logits.shape
+    C = ld if classes is None else int(classes)
+    if C > ld:
+        raise ValueError("classes exceeds the logits row")
     labels = labels.to(torch.int64).contiguous()
     ws = torch.empty(3 * B, dtype=F32, device=logits.device)
     out3 = torch.empty(3, dtype=F32, device=logits.device)
     ticket = _COUNTERS.take(logits.device, 1)   # in-launch fold of the per-row results
-    HIP.call("kml_ce_fwd", "p p p p i i l i p s", _p(logits), _p(labels), _p(ws), _p(out3), B, C,
+    HIP.call("kml_ce_fwd", "p p p p i i i l i p s", _p(logits), _p(labels), _p(ws), _p(out3), B, C, ld,
              int(ignore_index), dt, _p(ticket), _s())
     return out3, ws, labels
 
 
-def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100):
+def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=None):
+    """dlogits (same [B, ld] layout as the logits; pad columns 0)."""
     dt = {BF16: 0, F32: 1}[logits.dtype]
-    B, C = logits.shape
+    B, ld = logits.shape
+    C = ld if classes is None else int(classes)
     d = torch.empty_like(logits)
-    HIP.call("kml_ce_bwd", "p p p p p p i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
-             _p(d), B, C, int(ignore_index), dt, _s())
+    HIP.call("kml_ce_bwd", "p p p p p p i i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
+             _p(d), B, C, ld, int(ignore_index), dt, _s())
     return d
 
 

@@ -212,6 +212,30 @@ def test_cross_entropy(dtype):
         assert int(o3[2].item()) == int((bl != -100).sum())
 
 
+@pytest.mark.parametrize("C,ld", [(30522, 30528), (1000, 1000), (77, 80), (10, 10)])
+def test_cross_entropy_padded_rows(C, ld):
+    """Vector (16-byte) and scalar CE paths, with logits rows padded past the real classes
+    (the MLM decoder's vocab 30522 in a 30528-wide row): loss, argmax count and gradient vs
+    torch on the unpadded logits; the gradient's pad columns are zero."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(3)
+    B = 45
+    full = (torch.randn(B, ld, device=dev) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, C, (B,), device=dev)
+    labels[5] = -100
+    out3, ws, lab = K.ce_fwd(full, labels, classes=C)
+    lr = full[:, :C].float().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, ignore_index=-100)
+    assert abs(out3[0].item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    valid = labels != -100
+    assert int(out3[1].item()) == int((lr.argmax(1) == labels)[valid].sum().item())
+    ref.backward()
+    d = K.ce_bwd(full, lab, ws, out3, classes=C)
+    assert _rel(d[:, :C], lr.grad) < 1e-2
+    if ld > C:
+        assert float(d[:, C:].float().abs().max()) == 0.0
+
+
 def test_sgd_adam():
     from kubeml_amd.ops import kernels as K
     n = 10007
