@@ -995,7 +995,9 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
 // number of fp32 workspace floats kml_bn_bwd needs for the deterministic reduce
 KML_API long long kml_bn_bwd_ws_floats(long long M, int C) {
   int rpb;
-  const long long a = (long long)bwd_blocks(M, C, &rpb) * 2 * C, b = (long long)fin_blocks(M, C, &rpb) * 2 * C;
+  const int g = bwd_blocks(M, C, &rpb);
+  const long long a = (long long)g * 2 * C + (long long)((g + FOLD_R - 1) / FOLD_R) * 2 * C;  // + fold rows
+  const long long b = (long long)fin_blocks(M, C, &rpb) * 2 * C;
   return a > b ? a : b;
 }
 
@@ -1009,10 +1011,13 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
   if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
   int rpb;
   if (ws && !counter) {  // default: partials, then the apply kernel reduces them (2 launches, no sync)
-    const int gf = fin_blocks(M, C, &rpb);
+    // enough blocks to stream dy / y / x at full bandwidth (the old <= 128 KB-of-partials
+    // cap left ResNet-50's 56x56 BNs on 64 blocks); large partial sets are folded first
+    int gf = bwd_blocks(M, C, &rpb);
     hipLaunchKernelGGL(k_bn_bwd_reduce2<2>, dim3(gf), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
                        nullptr, M, C, rpb);
-    return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, ws, gf, dgamma, dbeta, dx, dres, M, C, s);
+    const float* part = maybe_fold(ws, gf, 2 * C, ws + (long long)gf * 2 * C, s);
+    return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, gf, dgamma, dbeta, dx, dres, M, C, s);
   }
   const int g = bwd_blocks(M, C, &rpb);
   if (ws && counter) {  // deterministic: ordered partials + last-arriver reduce
