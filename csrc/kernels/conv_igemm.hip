@@ -101,6 +101,15 @@ struct ConvArgs {
   int splits;
   int relu;
   int accumulate;        // WGRAD: atomicAdd (1) or store (0)
+  // Unrolled small-map convs (ops.kernels.unrolled): a 3x3/s1/p1 conv on a 2x2 map runs as a
+  // 1x1 conv of 4C -> 4K channels on a 1x1 map (only the taps that touch the image; the
+  // im2col of the 3x3 form is 5/9 zero padding).  fold_c: the FWD/DGRAD output channel col =
+  // (pos, c) belongs to BN channel c = col % fold_c, so a partial row is written as fold
+  // rows of [sum(fold_c) | sumsq(fold_c)] (BN kernels see ordinary rows of the real
+  // channels).  u_k0 / u_c0: WGRAD rows (p, n) and cols (q, c) scatter-add into the 3x3
+  // gradient dW[n][tap(p, q)][c], tap = (qh - ph + 1, qw - pw + 1).
+  int fold_c;
+  int u_k0, u_c0;
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
@@ -352,6 +361,15 @@ __device__ __forceinline__ void group_reduce_rows(const ConvArgs& a, const float
   }
 }
 
+// Offset of column col's sum inside a partial row (sumsq at + sq_off): [sum(N) | sumsq(N)],
+// or with fold_c the row holds N / fold_c sub-rows [sum(fold_c) | sumsq(fold_c)].
+__device__ __forceinline__ int row_off(const ConvArgs& a, int col) {
+  if (!a.fold_c) return col;
+  const int p = col / a.fold_c;
+  return col + p * a.fold_c;
+}
+__device__ __forceinline__ int sq_off(const ConvArgs& a) { return a.fold_c ? a.fold_c : a.N; }
+
 template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
                                               int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
@@ -359,6 +377,26 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 
   // ---------------------------------------------------------------- WGRAD epilogue
   if constexpr (MODE == WGRAD) {
+    if (a.u_k0) {  // unrolled 2x2 conv: scatter-add into the 3x3 gradient (see ConvArgs)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fr;
+        if (col >= a.N) continue;
+        const int q = col / a.u_c0, c = col - q * a.u_c0;
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
+            if (row < a.M) {
+              const int p = row / a.u_k0, n = row - p * a.u_k0;
+              const int tap = ((q >> 1) - (p >> 1) + 1) * 3 + ((q & 1) - (p & 1) + 1);
+              atomicAdd(a.dw + ((long long)n * 9 + tap) * a.u_c0 + c, acc[i][j][e]);
+            }
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int col = n0 + wn * WN + j * 16 + fr;
@@ -448,7 +486,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
       const int col = n0 + wn * WN + j * 16 + fr;
       const bool cok = col < a.N;
       float bv = 0.f;
-      if (MODE == FWD && a.bias && cok) bv = a.bias[col];
+      const int bc = a.fold_c ? col % a.fold_c : col;  // BN / bias channel of this column
+      if (MODE == FWD && a.bias && cok) bv = a.bias[bc];
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int i = 0; i < MR; ++i)
@@ -466,7 +505,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
               const long long idx = (long long)row * ldc + col;
               float dz = bf2f(vb);
               if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) dz = 0.f;
-              const float xh = (bf2f(a.bnf_c[idx]) - a.bnf_mean[col]) * a.bnf_rstd[col];
+              const float xh = (bf2f(a.bnf_c[idx]) - a.bnf_mean[bc]) * a.bnf_rstd[bc];
               s1 += dz;
               s2 += dz * xh;
             } else {
@@ -488,8 +527,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         }
       } else if (rows != nullptr && fq == 0 && cok) {
         if (SINGLE) {
-          store_row(rows + rrow + col, s1, sc1_rows);
-          store_row(rows + rrow + a.N + col, s2, sc1_rows);
+          store_row(rows + rrow + row_off(a, col), s1, sc1_rows);
+          store_row(rows + rrow + row_off(a, col) + sq_off(a), s2, sc1_rows);
         } else if (wm == 1) {
           red[col - n0] = s1;
           red[BNT + col - n0] = s2;
@@ -503,8 +542,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         for (int j = 0; j < NR; ++j) {
           const int col = n0 + wn * WN + j * 16 + fr;
           if (col < a.N) {
-            store_row(rows + rrow + col, k1[j] + red[col - n0], sc1_rows);
-            store_row(rows + rrow + a.N + col, k2[j] + red[BNT + col - n0], sc1_rows);
+            store_row(rows + rrow + row_off(a, col), k1[j] + red[col - n0], sc1_rows);
+            store_row(rows + rrow + row_off(a, col) + sq_off(a), k2[j] + red[BNT + col - n0], sc1_rows);
           }
         }
       }
@@ -1242,6 +1281,46 @@ __global__ __launch_bounds__(256) void k_weight_transpose_multi(TransposeBatch t
   }
 }
 
+// Unrolled-conv weights (ConvArgs::fold_c): wu[(p, n)][(q, c)] = w[n][tap(p, q)][c] for a
+// 3x3 / stride 1 / pad 1 conv on a 2x2 map (p, q = output / input position, tap =
+// (qh - ph + 1, qw - pw + 1)), up to 16 convs per launch, one 16-byte chunk per thread.
+struct UnrollJob {
+  const bf16_t* w;
+  bf16_t* wu;
+  int block_begin;
+  int K, C;
+};
+struct UnrollBatch {
+  UnrollJob j[16];
+  int n;
+};
+
+constexpr int UNROLL_V = 4;  // 16-byte chunks per thread (all loads issued before the stores)
+
+__global__ __launch_bounds__(256) void k_unroll22_multi(UnrollBatch ub) {
+  int q = 0;
+  while (q + 1 < ub.n && (int)blockIdx.x >= ub.j[q + 1].block_begin) ++q;  // block-uniform
+  const UnrollJob& jb = ub.j[q];
+  const int cpr = jb.C / 2;  // 16-byte chunks per wu row (4C / 8)
+  const int total = 4 * jb.K * cpr;
+  const int base = ((int)blockIdx.x - jb.block_begin) * 256 * UNROLL_V + (int)threadIdx.x;
+  uint4 v[UNROLL_V];
+  long long dst[UNROLL_V];
+#pragma unroll
+  for (int u = 0; u < UNROLL_V; ++u) {
+    const int idx = min(base + u * 256, total - 1);  // clamped: tail lanes reload / rewrite the last chunk
+    const int row = idx / cpr, col = (idx - row * cpr) * 8;
+    const int p = row / jb.K, n = row - p * jb.K;
+    const int qq = col / jb.C, c = col - qq * jb.C;
+    const int tap = ((qq >> 1) - (p >> 1) + 1) * 3 + ((qq & 1) - (p & 1) + 1);
+    v[u] = *reinterpret_cast<const uint4*>(jb.w + ((long long)n * 9 + tap) * jb.C + c);
+    dst[u] = (long long)row * 4 * jb.C + col;
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL_V; ++u)
+    if (base + u * 256 < total) *reinterpret_cast<uint4*>(jb.wu + dst[u]) = v[u];
+}
+
 __device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];  // zero-initialised device global
 
 const bf16_t* zero_page() {
@@ -1274,14 +1353,15 @@ KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
 KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int stats_part,
                          int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu,
                          int bm, int bn, int bk, int splits, int variant, float* slab, unsigned* counters,
-                         float* grp_out, unsigned* grp_cnt, int grp_tiles, hipStream_t s) {
+                         float* grp_out, unsigned* grp_cnt, int grp_tiles, int fold_c, hipStream_t s) {
   if (grp_out && (!stats || !stats_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (fold_c && (grp_out || K % fold_c || (stats && !stats_part))) return (int)hipErrorInvalidValue;
   if (C % 8) return (int)hipErrorInvalidValue;
   if (variant == 3) {  // direct: bk carries the wave count; needs 32-aligned taps
     if (C % 32) return (int)hipErrorInvalidValue;
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
     a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
-    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
     a.zp = zero_page();
     a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
     a.splits = 1; a.kchunk = a.Kd;
@@ -1291,7 +1371,7 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
-  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
   a.zp = zero_page();
   a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
@@ -1306,9 +1386,10 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
                const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W, int C, int K,
                int KH, int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, float* slab,
-               unsigned* counters) {
+               unsigned* counters, int fold_c) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   if (grp_out && (!bnf_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (fold_c && (grp_out || C % fold_c)) return (int)hipErrorInvalidValue;
   const bool direct = (variant == 3);
   if (!direct && variant) bk = 64;
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
@@ -1317,7 +1398,7 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
   a.fd_Kp = make_fd(a.Kp);
   a.dy = dy; a.w = w; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
   a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
-  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   if (direct) {
@@ -1332,15 +1413,19 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
 }
 
 int prep_wgrad(ConvArgs& a, const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
-               int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate) {
+               int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate, int u_k0,
+               int u_c0) {
   if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  if ((u_k0 || u_c0) && (!u_k0 || !u_c0 || K != 4 * u_k0 || C != 4 * u_c0 || KH != 1 || KW != 1))
+    return (int)hipErrorInvalidValue;
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
   a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   set_splits(a, bk, splits);
-  a.accumulate = (a.splits > 1) ? 1 : accumulate;
+  a.accumulate = (a.splits > 1 || u_k0) ? 1 : accumulate;
+  a.u_k0 = u_k0; a.u_c0 = u_c0;
   return 0;
 }
 }  // namespace
@@ -1357,14 +1442,15 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               float* dw, int B, int H, int W, int C, int K, int KH,
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
-                              int wvariant, hipStream_t s) {
+                              int wvariant, int fold_c, int u_k0, int u_c0, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
   int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
-                     grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters);
+                     grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
+                     fold_c);
   if (e) return e;
-  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1);
+  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1, u_k0, u_c0);
   if (e) return e;
   return dispatch_pair(which, ad, aw, s);
 }
@@ -1393,6 +1479,27 @@ KML_API int kml_weight_transpose_multi(const bf16_t* const* ws, bf16_t* const* w
   KML_LAUNCH_CHECK();
 }
 
+// wus[i][4K][4C] = unrolled 2x2-map form of ws[i][K][3][3][C] (k_unroll22_multi), up to 16
+// convs in one launch.  dims: n x 2 ints (K, C).
+KML_API int kml_conv_unroll22_multi(const bf16_t* const* ws, bf16_t* const* wus, const int* dims, int n,
+                                    hipStream_t s) {
+  if (n < 1 || n > 16) return (int)hipErrorInvalidValue;
+  UnrollBatch ub = {};
+  ub.n = n;
+  long long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    UnrollJob& j = ub.j[i];
+    j.w = ws[i]; j.wu = wus[i];
+    j.K = dims[2 * i]; j.C = dims[2 * i + 1];
+    if (j.C % 8 || j.K < 1 || !j.w || !j.wu) return (int)hipErrorInvalidValue;
+    j.block_begin = (int)blocks;
+    blocks += ((long long)4 * j.K * (j.C / 2) + 256 * UNROLL_V - 1) / (256 * UNROLL_V);
+  }
+  if (blocks <= 0 || blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_unroll22_multi, dim3((unsigned)blocks), dim3(256), 0, s, ub);
+  KML_LAUNCH_CHECK();
+}
+
 // bnf_*: optional consumer-BN backward partials (see ConvArgs); bnf_part = null disables.
 // grp_*: optional group reduction of those partial rows.  variant 3 (direct): wt is the
 // transposed weight copy (kml_weight_transpose, Kp = roundup(K, 32)) and bk the wave count.
@@ -1400,10 +1507,11 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
                            const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                            float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W,
                            int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
-                           int splits, int variant, float* slab, unsigned* counters, hipStream_t s) {
+                           int splits, int variant, float* slab, unsigned* counters, int fold_c, hipStream_t s) {
   ConvArgs a;
   const int e = prep_dgrad(a, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
-                           grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, slab, counters);
+                           grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, slab, counters,
+                           fold_c);
   if (e) return e;
   if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
   if (variant) bk = 64;
@@ -1419,14 +1527,11 @@ KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int
 
 KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                            int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk, int splits, int variant,
-                           int accumulate, hipStream_t s) {
+                           int accumulate, int u_k0, int u_c0, hipStream_t s) {
+  ConvArgs a;
+  const int e = prep_wgrad(a, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, accumulate,
+                           u_k0, u_c0);
+  if (e) return e;
   if (variant) bk = 64;
-  if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
-  ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
-  a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
-  if (!a.zp) return (int)hipErrorInvalidSymbol;
-  set_splits(a, bk, splits);
-  a.accumulate = (a.splits > 1) ? 1 : accumulate;
   return dispatch<WGRAD>(a, bm, bn, bk, variant, s);
 }

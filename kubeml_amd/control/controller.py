@@ -59,6 +59,8 @@ class Controller:
         self.ps.stop_task(job_id)
 
     def job_status(self, job_id: str):
+        if self.scheduler.is_pending(job_id):
+            return {"id": job_id, "state": "running", "queued": True, "parallelism": 0}
         running = {t.job.id: t for t in self.ps.list_tasks()}
         if job_id in running:
             t = running[job_id]
@@ -68,6 +70,8 @@ class Controller:
             return {"id": job_id, "state": "failed" if err else "finished", "error": err}
         if self.histories.exists(job_id):
             return {"id": job_id, "state": "finished", "error": None}
+        if job_id in self.scheduler.failed:
+            return {"id": job_id, "state": "failed", "error": self.scheduler.failed[job_id]}
         raise NotFoundError(f"job {job_id}")
 
     # --- logs ----------------------------------------------------------------------

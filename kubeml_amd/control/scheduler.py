@@ -58,6 +58,8 @@ class Scheduler:
         self.ps = ps
         self.policy = policy or ThroughputPolicy(max_parallelism=max_parallelism)
         self._q = collections.deque()
+        self._pending = set()        # submitted jobs the PS has not taken yet
+        self.failed = {}             # job id -> error for jobs the PS refused to start
         self._lock = threading.Lock()
         self._wake = threading.Event()
         self._stop = threading.Event()
@@ -81,8 +83,16 @@ class Scheduler:
     def submit_train(self, req: TrainRequest) -> str:
         validate_request(req)
         jid = create_job_id()
+        with self._lock:
+            self._pending.add(jid)
         self._push(TrainTask(request=req, job=JobInfo(id=jid, state=JobState())))
         return jid
+
+    def is_pending(self, job_id: str) -> bool:
+        """Submitted but not yet running on the parameter server (status polls between
+        ``/train`` and the PS start see the job as queued, not unknown)."""
+        with self._lock:
+            return job_id in self._pending
 
     def update_job(self, task: TrainTask):
         self._push(task)
@@ -108,6 +118,11 @@ class Scheduler:
                 self.ps.update_task(task.job.id, JobState(parallelism=p, elapsed_time=task.job.state.elapsed_time))
         except Exception as e:
             log.error("error sending task %s to the parameter server: %r", op, e)
+            if op == "create":
+                self.failed[task.job.id] = repr(e)
+        finally:
+            with self._lock:
+                self._pending.discard(task.job.id)
         return True
 
     def _loop(self):

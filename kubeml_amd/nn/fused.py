@@ -80,33 +80,80 @@ def join_wgrad():
         _WgradSide.pending = False
 
 
-def _wgrad(x, dc, conv):
+def _wgrad(x, dc, conv, unroll=False):
     from ..ops import kernels as K
     kh, kw = conv.kernel_size
     side = _WgradSide.stream
     if side is None:
-        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding)
+        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding, unroll=unroll)
         return
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding)
+        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding, unroll=unroll)
     # the allocator must not hand these blocks to the main stream before the side reads them
     x.record_stream(side)
     dc.record_stream(side)
     _WgradSide.pending = True
 
 
-def refresh_transposed(convs):
-    """Transposed bf16 weights ``[Cin][KH][KW][Kp]`` for every conv whose dgrad runs the
-    direct (LDS-free) variant, in ONE launch per 16 convs, at the start of a training
-    forward.  Which convs need them is learned from earlier backward passes
-    (ConvBNUnit.backward marks them); a conv not yet marked transposes inline.  The copy
-    is consumed (and dropped) by that conv's next backward."""
+def _wu_buf(conv, w):
+    """Persistent [4K,1,1,4C] buffer of a conv's unrolled weight (stable address: graphs)."""
+    Kc, _, _, C = w.shape
+    shape = (4 * Kc, 1, 1, 4 * C)
+    buf = getattr(conv, "_kml_wu_buf", None)
+    if buf is None or tuple(buf.shape) != shape or buf.device != w.device:
+        buf = torch.empty(shape, dtype=torch.bfloat16, device=w.device)
+        object.__setattr__(conv, "_kml_wu_buf", buf)
+    return buf
+
+
+def unrolled_for(conv, x):
+    """Unrolled weight for this training forward of ``conv`` on ``x`` (ops.kernels.unrolled22),
+    or None when the conv runs in its ordinary form.  Uses the copy refresh_transposed made
+    at the start of this forward, else gathers it now (and marks the conv for batching);
+    kept on the module for this forward's backward."""
     from ..ops import kernels as K
+    if not x.is_cuda:
+        return None
+    kh, kw = conv.kernel_size
+    if not K.unrolled22(x.shape[1], x.shape[2], kh, kw, conv.stride, conv.padding):
+        return None
+    w = shadow_of(conv.weight)
+    buf = _wu_buf(conv, w)
+    if not getattr(conv, "_kml_wu_fresh", False):
+        object.__setattr__(conv, "_kml_wants_wu", True)
+        K.unroll22_multi([w], [buf])
+    object.__setattr__(conv, "_kml_wu_fresh", False)   # one forward per refresh
+    object.__setattr__(conv, "_kml_wu", buf)           # for this forward's backward
+    return buf
+
+
+def refresh_transposed(convs):
+    """Derived bf16 weights of this training step, each kind in ONE launch per 16 convs,
+    at the start of a training forward:
+
+    * unrolled weights ``[4K,1,1,4C]`` of the convs that run in the dense 2x2-map form
+      (:func:`unrolled_for`, ops.kernels.unrolled22);
+    * transposed weights ``[Cin][KH][KW][Kp]`` for every conv whose dgrad runs the direct
+      (LDS-free) variant (of the unrolled weight for an unrolled conv).
+
+    Which convs need them is learned from earlier passes (the forward / backward mark
+    them); a conv not yet marked makes its copy inline.  A transposed copy is consumed
+    (and dropped) by that conv's next backward."""
+    from ..ops import kernels as K
+    unr = [c for c in convs if getattr(c, "_kml_wants_wu", False)]
+    ws, wus = [], []
+    for c in unr:
+        w = shadow_of(c.weight)
+        ws.append(w)
+        wus.append(_wu_buf(c, w))
+        object.__setattr__(c, "_kml_wu_fresh", True)
+    for i in range(0, len(ws), 16):
+        K.unroll22_multi(ws[i:i + 16], wus[i:i + 16])
     want = [c for c in convs if getattr(c, "_kml_wants_wt", False)]
     ws, wts = [], []
     for c in want:
-        w = shadow_of(c.weight)
+        w = c._kml_wu_buf if getattr(c, "_kml_wants_wu", False) else shadow_of(c.weight)
         Kc, KH, KW, C = w.shape
         shape = (C, KH, KW, -(-Kc // 32) * 32)
         buf = getattr(c, "_kml_wt_buf", None)
@@ -143,9 +190,10 @@ class ConvBNUnit:
             # per-wave partial statistics from the conv epilogue (plain stores, every row
             # written: no zeroing, no atomics); bn_apply sums them in its prologue
             K_out = w.shape[0]
-            G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding)
+            wu = unrolled_for(conv, x)
+            G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, unroll=wu is not None)
             stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
-            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True)
+            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True, wu=wu)
             C = c.shape[-1]
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             rstd = torch.empty_like(mean)
@@ -172,21 +220,24 @@ class ConvBNUnit:
         kh, kw = conv.kernel_size
         dx, part_out = None, None
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
+        wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
+        object.__setattr__(conv, "_kml_wu", None)
         if need_dx and _WgradSide.stream is None:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
             w = shadow_of(conv.weight)
             wt = getattr(conv, "_kml_wt", None)
-            if wt is None and K.bwd_plans(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding)[0][4] == K.DIRECT:
+            if wt is None and K.bwd_plans(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding,
+                                          unroll=wu is not None)[0][4] == K.DIRECT:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
             r = K.conv_bwd(dc, w, x, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding,
-                           addend=addend, bnf=bnf, wt=wt)
+                           addend=addend, bnf=bnf, wt=wt, wu=wu)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out
-        _wgrad(x, dc, conv)
+        _wgrad(x, dc, conv, unroll=wu is not None)
         if need_dx:
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
-                             addend=addend, bnf=bnf)
+                             addend=addend, bnf=bnf, wu=wu)
             dx, part_out = r if bnf is not None else (r, None)
         return dx, dres, part_out
 

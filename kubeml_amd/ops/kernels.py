@@ -52,7 +52,8 @@ def _chk(t, dtype, name, ndim=None):
 _TILES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32)]
 _TUNED: dict = {}  # (mode, M, N, Kd) -> (bm, bn, bk, splits); loaded from conv_tuning.json
 _TUNED_PAIR: dict = {}  # (dgrad M, N, Kd, wgrad M, N, Kd) -> (dgrad plan, wgrad plan) of a grouped launch
-_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
+_TUNE_FILE = os.environ.get("KUBEML_CONV_TUNING_FILE") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
 
 
 def _load_tuning():
@@ -219,14 +220,97 @@ def _stats_ws(device, M, N, cfg, out):
     return scratch, out, _COUNTERS.take(device, ng * _cdiv(N, bn)), tpg
 
 
-def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False):
+def unrolled22(H, W, KH, KW, stride, pad) -> bool:
+    """True for the convs that run unrolled: 3x3 / stride 1 / pad 1 on a 2x2 map.
+
+    There every output pixel sees only 4 of the 9 taps (the other 5 read padding), so
+    the conv is the dense map [B, 4C] -> [B, 4K] of the NHWC rows with the gathered weight
+    wu[(p, n)][(q, c)] = w[n][tap(p, q)][c] (:func:`unroll22_multi`): a 1x1 conv with 4/9 of
+    the im2col FLOPs (ResNet-34/18 layer3 at 32x32 input, 2x2 maps).  BN statistics fold the
+    4 positions back onto the K channels in the epilogue (``fold_c``) and the weight
+    gradient scatters back onto the 3x3 taps (``u_k0/u_c0``)."""
+    return (H, W, KH, KW) == (2, 2, 3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1) and \
+        _UNROLL_ON
+
+
+_UNROLL_ON = os.environ.get("KUBEML_CONV_UNROLL", "1") != "0"
+
+
+def unroll22_multi(ws, wus):
+    """wus[i][4K,1,1,4C] = unrolled form of ws[i][K,3,3,C] for up to 16 convs, one launch."""
+    import ctypes
+    n = len(ws)
+    if n == 0:
+        return
+    if n > 16 or len(wus) != n:
+        raise ValueError("unroll22_multi: 1..16 pairs")
+    wp = (ctypes.c_void_p * n)()
+    up = (ctypes.c_void_p * n)()
+    dims = (ctypes.c_int * (2 * n))()
+    for i, (w, wu) in enumerate(zip(ws, wus)):
+        _chk(w, BF16, "w", 4)
+        _chk(wu, BF16, "wu", 4)
+        K, KH, KW, C = w.shape
+        if (KH, KW) != (3, 3) or tuple(wu.shape) != (4 * K, 1, 1, 4 * C) or C % 8:
+            raise ValueError("unrolled weight shape mismatch")
+        wp[i], up[i] = w.data_ptr(), wu.data_ptr()
+        dims[2 * i], dims[2 * i + 1] = K, C
+    HIP.call("kml_conv_unroll22_multi", "p p p i s", ctypes.addressof(wp), ctypes.addressof(up),
+             ctypes.addressof(dims), n, _s())
+
+
+def unrolled_weight(w, out=None):
+    """The [4K,1,1,4C] unrolled weight of a 3x3 conv (one launch)."""
+    K, KH, KW, C = w.shape
+    if out is None:
+        out = torch.empty((4 * K, 1, 1, 4 * C), dtype=BF16, device=w.device)
+    unroll22_multi([w], [out])
+    return out
+
+
+def unroll22_reference(w):
+    """Plain-PyTorch form of the unrolled weight (any device/dtype; the kernel's mapping):
+    wu[(p, n)][(q, c)] = w[n][qh - ph + 1][qw - pw + 1][c] for positions p, q of a 2x2 map."""
+    K, KH, KW, C = w.shape
+    wu = w.new_zeros((4, K, 4, C))
+    for p in range(4):
+        for q in range(4):
+            r, s = (q >> 1) - (p >> 1) + 1, (q & 1) - (p & 1) + 1
+            wu[p, :, q, :] = w[:, r, s, :]
+    return wu.reshape(4 * K, 1, 1, 4 * C)
+
+
+def _check_wu(x_shape, w, wu, KH, KW, stride, pad):
+    B, H, W, C = x_shape
+    if not unrolled22(H, W, KH, KW, stride, pad):
+        raise ValueError("wu given for a conv that is not unrolled (3x3/s1/p1 on 2x2)")
+    K = w.shape[0]
+    _chk(wu, BF16, "wu", 4)
+    if tuple(wu.shape) != (4 * K, 1, 1, 4 * C):
+        raise ValueError(f"unrolled weight shape {tuple(wu.shape)} != {(4 * K, 1, 1, 4 * C)}")
+    return B, C, K
+
+
+def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False,
+             wu=None, _fold=0):
     """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats).
 
     stats: fp32 [2*Cout] accumulated with atomics, or with ``stats_part`` a [G, 2*Cout]
     buffer of per-wave partial rows (``G = conv_stats_rows(M, plan)``, see
-    :func:`conv_fwd_plan`) that :func:`bn_apply` sums — no zeroing, no atomics."""
+    :func:`conv_fwd_plan`) that :func:`bn_apply` sums — no zeroing, no atomics.
+    wu: unrolled weight (:func:`unrolled22`): the conv runs as its dense 1x1 form."""
     _chk(x, BF16, "x", 4)
     _chk(w, BF16, "w", 4)
+    if wu is not None:
+        B, C, K = _check_wu(x.shape, w, wu, KH, KW, stride, pad)
+        if stats is not None and not stats_part:
+            raise ValueError("unrolled conv: BN statistics need stats_part")
+        if out is not None and tuple(out.shape) != (B, 2, 2, K):
+            raise ValueError("out shape mismatch")
+        o = None if out is None else out.view(B, 1, 1, 4 * K)
+        y = conv_fwd(x.view(B, 1, 1, 4 * C), wu, 1, 1, (1, 1), (0, 0), bias=bias, stats=stats, relu=relu, out=o,
+                     cfg=cfg, stats_part=stats_part, _fold=K)
+        return y.view(B, 2, 2, K)
     B, H, W, C = x.shape
     K = w.shape[0]
     if tuple(w.shape[1:]) != (KH, KW, C):
@@ -248,19 +332,25 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     if stats is not None:
         _chk(stats, F32, "stats")
         need = 2 * K * (conv_stats_rows(M, (bm, bn, bk, splits, variant)) if stats_part else 1)
+        if _fold and (not stats_part or K % _fold):
+            raise ValueError("folded statistics need stats_part and K % fold == 0")
         if stats.numel() < need:
             raise ValueError(f"stats buffer has {stats.numel()} floats, needs {need}")
         if stats_part:
             rows, grp, gcnt, tpg = _stats_ws(x.device, M, K, (bm, bn, bk, splits, variant), stats)
-    sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i s"
+    if _fold and grp is not None:
+        raise ValueError("folded statistics cannot be group-reduced")
+    sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i i s"
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
-                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, _s())
+                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, int(_fold),
+                 _s())
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
     HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
-             sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt), tpg, _s())
+             sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt), tpg,
+             int(_fold), _s())
     return out
 
 
@@ -272,23 +362,45 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None):
     return plan
 
 
-def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None):
-    """G of the partial-statistics buffer conv_fwd(stats_part=True) needs for this conv."""
+def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False):
+    """G of the partial-statistics buffer conv_fwd(stats_part=True) needs for this conv
+    (``unroll``: the conv runs with its unrolled weight, 4 folded rows per M-tile)."""
     B, H, W, C = x_shape
+    if unroll:
+        if not unrolled22(H, W, KH, KW, stride, pad):
+            raise ValueError("conv is not unrolled")
+        return 4 * conv_stats_rows(B, conv_fwd_plan(4 * C, B, 4 * K, 4 * C, cfg))
     OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
     return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg))
 
 
-def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None, wt=None):
+def _u22_views(B, C, K, dy=None, x=None, addend=None, bnf=None):
+    """Views of the NHWC [B,2,2,*] tensors of an unrolled conv as its 1x1 form [B,1,1,4*]."""
+    v = lambda t, n: None if t is None else t.reshape(B, 1, 1, 4 * n)
+    b = None if bnf is None else (v(bnf[0], C), v(bnf[1], C), bnf[2], bnf[3])
+    return v(dy, K), v(x, C), v(addend, C), b
+
+
+def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None, wt=None, wu=None,
+               _fold=0):
     """dx = conv input gradient (+ addend, the fused residual-gradient sum).
 
     bnf = (y or None, c, mean, rstd) of the BatchNorm that consumes dx: the epilogue also
     writes that BN's dgamma/dbeta partial rows; returns (dx, (part, G)) for
-    :func:`bn_bwd(partial=...)`."""
+    :func:`bn_bwd(partial=...)`.  wu: unrolled weight (:func:`unrolled22`)."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
+    if wu is not None:
+        B, C, K = _check_wu(in_shape, w, wu, KH, KW, stride, pad)
+        dy1, _, add1, bnf1 = _u22_views(B, C, K, dy=dy, addend=addend, bnf=bnf)
+        o = None if out is None else out.view(B, 1, 1, 4 * C)
+        r = conv_dgrad(dy1, wu, (B, 1, 1, 4 * C), 1, 1, (1, 1), (0, 0), out=o, addend=add1, cfg=cfg, bnf=bnf1, wt=wt,
+                       _fold=C)
+        if bnf is not None:
+            return r[0].view(B, 2, 2, C), r[1]
+        return r.view(B, 2, 2, C)
     B, H, W, C = in_shape
     K = w.shape[0]
     sh, sw = stride
@@ -310,7 +422,7 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     ntap = (r1 - r0) * (s1 - s0)
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
     plan = (bm, bn, bk, splits, variant)
-    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan)
+    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan, _fold)
     slab = cnt = None
     if variant == DIRECT:
         # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
@@ -320,16 +432,17 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         wt = None
         splits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
-    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p s",
+    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt),
-             _s())
+             int(_fold), _s())
     return (out, (part, G)) if bnf is not None else out
 
 
-def _bnf_ws(bnf, out, M, C, plan):
+def _bnf_ws(bnf, out, M, C, plan, fold=0):
     """Consumer-BN partial-row buffers of a dgrad: (y, c, mean, rstd, part the BN reads,
-    rows the epilogue writes, group output, tickets, tiles per group, rows in part)."""
+    rows the epilogue writes, group output, tickets, tiles per group, rows in part).
+    fold: the BN's channel count when the dgrad output holds C / fold positions per row."""
     if bnf is None:
         return None, None, None, None, None, None, None, None, 0, 0
     by, bc, bmean, brstd = bnf
@@ -338,6 +451,10 @@ def _bnf_ws(bnf, out, M, C, plan):
     G = conv_stats_rows(M, plan)
     part = torch.empty(G * 2 * C, dtype=F32, device=out.device)
     rows, grp, gcnt, tpg = _stats_ws(out.device, M, C, plan, part)
+    if fold:
+        if grp is not None or C % fold:
+            raise ValueError("folded BN partials cannot be group-reduced")
+        G *= C // fold
     return by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G
 
 
@@ -360,10 +477,13 @@ def dgrad_plan(in_shape, K, KH, KW, stride, pad, cfg=None):
     return _norm_cfg(cfg or plan_conv("dgrad", B * H * W, C, (r1 - r0) * (s1 - s0) * K))
 
 
-def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None):
+def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None, unroll=False):
     """(dgrad plan, wgrad plan, grouped?) conv_bwd runs for this conv: a tuned pair entry
-    when one exists, else the separately tuned plans (grouped if instantiated)."""
+    when one exists, else the separately tuned plans (grouped if instantiated).
+    unroll: plans of the unrolled 1x1 form (:func:`unrolled22`)."""
     B, H, W, C = in_shape
+    if unroll:
+        return bwd_plans((B, 1, 1, 4 * C), 4 * K, 1, 1, (1, 1), (0, 0), dcfg, wcfg)
     sh, sw = stride
     ph, pw = pad
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
@@ -392,13 +512,15 @@ def conv_pair_supported(dcfg, wcfg) -> bool:
     return ok
 
 
-def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None):
+def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
     :func:`conv_dgrad`) and ``dw += wgrad``.  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
     instantiated pair, else as two launches.  ``wt``: precomputed transposed weights for
     a direct-variant dgrad (:func:`weight_transpose_multi`); made here when missing.
-    Returns dx, or (dx, (part, G)) when ``bnf`` is given."""
+    Returns dx, or (dx, (part, G)) when ``bnf`` is given.  wu: unrolled weight
+    (:func:`unrolled22`): both GEMMs run in the dense 1x1 form, the weight gradient
+    scatter-adds back onto the 3x3 taps of ``dw``."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -412,19 +534,34 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         raise ValueError("conv_bwd shape mismatch")
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
+    fold, u = 0, (0, 0)
+    if wu is not None:
+        _check_wu(x.shape, w, wu, KH, KW, stride, pad)
+        dy, x, addend, bnf = _u22_views(B, C, K, dy=dy, x=x, addend=addend, bnf=bnf)
+        w, fold, u = wu, C, (K, C)
+        H = W = OH = OW = 1
+        KH = KW = sh = sw = 1
+        ph = pw = 0
+        C, K = 4 * C, 4 * K
+        stride, pad = (1, 1), (0, 0)
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
     if not grouped:
-        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan)
-        return conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt)
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, _u=u)
+        r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold)
+        if not fold:
+            return r
+        if bnf is not None:
+            return r[0].view(B, 2, 2, C // 4), r[1]
+        return r.view(B, 2, 2, C // 4)
     bm, bn, bk, splits, variant = dplan
     out = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
     if addend is not None:
         _chk(addend, BF16, "addend")
         assert addend.shape == out.shape
-    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan)
+    by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan, fold)
     slab = cnt = None
     if variant == DIRECT:
         wt = _direct_wt(w, wt)
@@ -435,10 +572,12 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
-             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, _s())
+             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold), u[0], u[1], _s())
+    if fold:
+        out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out
 
 
@@ -466,22 +605,34 @@ def weight_transpose_multi(ws, wts):
              ctypes.addressof(dims), n, _s())
 
 
-def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None):
-    """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient."""
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0)):
+    """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient.  unroll: run the dense 1x1 form
+    of an unrolled conv (:func:`unrolled22`), scatter-adding onto the 3x3 taps."""
     _chk(x, BF16, "x", 4)
     _chk(dy, BF16, "dy", 4)
     _chk(dw, F32, "dw", 4)
+    if unroll:
+        B, H, W, C = x.shape
+        K = dy.shape[3]
+        if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (K, 3, 3, C):
+            raise ValueError("conv is not unrolled")
+        _, x1, _, _ = _u22_views(B, C, K, x=x)
+        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, _u=(K, C))
     B, H, W, C = x.shape
     K = dy.shape[3]
     sh, sw = stride
     ph, pw = pad
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
-    if tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
+    if _u[0]:
+        if tuple(dw.shape) != (_u[0], 3, 3, _u[1]) or (K, C) != (4 * _u[0], 4 * _u[1]) or (KH, KW) != (1, 1):
+            raise ValueError("unrolled wgrad shape mismatch")
+    elif tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
         raise ValueError("wgrad shape mismatch")
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i s",
-             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, 1, _s())
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i i i s",
+             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, 1, int(_u[0]),
+             int(_u[1]), _s())
     return dw
 
 

@@ -592,3 +592,77 @@ def test_colsum_and_slab_sum(M, C):
     want = dst + part.sum(0)
     K.slab_sum_add_(part, dst)
     assert torch.allclose(dst, want, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------
+# unrolled 2x2-map convs (3x3 / s1 / p1 run as their dense 1x1 form, ops.kernels.unrolled22)
+# ---------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("B,C,Kc", [(256, 256, 256), (37, 64, 128), (8, 32, 24)])
+def test_unrolled_conv_fwd_bn_matches_3x3(B, C, Kc):
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(0)
+    x = _bf(torch.randn(B, 2, 2, C, device=dev))
+    w = _bf(torch.randn(Kc, 3, 3, C, device=dev) * 0.05)
+    wu = K.unrolled_weight(w)
+    torch.testing.assert_close(wu, K.unroll22_reference(w), rtol=0, atol=0)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    args = (3, 3, (1, 1), (1, 1))
+    G3 = K.conv_fwd_stats_rows(x.shape, Kc, *args)
+    Gu = K.conv_fwd_stats_rows(x.shape, Kc, *args, unroll=True)
+    s3 = torch.empty(G3 * 2 * Kc, device=dev)
+    su = torch.empty(Gu * 2 * Kc, device=dev)
+    y3 = K.conv_fwd(x, w, *args, stats=s3, stats_part=True)
+    yu = K.conv_fwd(x, w, *args, stats=su, stats_part=True, wu=wu)
+    assert yu.shape == (B, 2, 2, Kc)
+    assert _rel(yu, ref) < 1e-2 and _rel(y3, ref) < 1e-2
+    # folded partial rows: ordinary [sum | sumsq] rows of the Kc channels (from the fp32
+    # conv values, like the 3x3 path's rows: compare the two)
+    tot = su.view(Gu, 2, Kc).sum(0)
+    tot3 = s3.view(G3, 2, Kc).sum(0)
+    torch.testing.assert_close(tot, tot3, rtol=1e-3, atol=5e-2)
+    yf = yu.float().reshape(-1, Kc)
+    assert _rel(tot[1], (yf * yf).sum(0)) < 1e-2
+    gamma = torch.rand(Kc, device=dev) + 0.5
+    beta = torch.randn(Kc, device=dev) * 0.1
+    a3 = K.bn_apply(y3, s3, gamma, beta, relu=True, stats_rows=G3)
+    au = K.bn_apply(yu, su, gamma, beta, relu=True, stats_rows=Gu)
+    assert _rel(au, a3) < 2e-2
+
+
+@pytest.mark.parametrize("B,C,Kc", [(256, 256, 256), (37, 64, 128)])
+def test_unrolled_conv_bwd_matches_3x3(B, C, Kc):
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(1)
+    x = _bf(torch.randn(B, 2, 2, C, device=dev))
+    w = _bf(torch.randn(Kc, 3, 3, C, device=dev) * 0.05)
+    dy = _bf(torch.randn(B, 2, 2, Kc, device=dev))
+    addend = _bf(torch.randn(B, 2, 2, C, device=dev))
+    wu = K.unrolled_weight(w)
+    args = (3, 3, (1, 1), (1, 1))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_()
+    (F.conv2d(xr, wr, padding=1) * dy.float().permute(0, 3, 1, 2)).sum().backward()
+    dx_ref = xr.grad.permute(0, 2, 3, 1) + addend.float()
+    dw_ref = wr.grad.permute(0, 2, 3, 1)
+    # consumer BN of dx (channels C): its dgamma/dbeta partial rows come out folded
+    yc = _bf(torch.randn(B, 2, 2, C, device=dev))
+    cc = _bf(torch.randn(B, 2, 2, C, device=dev))
+    mean = torch.randn(C, device=dev) * 0.1
+    rstd = torch.rand(C, device=dev) + 0.5
+    dw = torch.zeros(Kc, 3, 3, C, device=dev)
+    dx, (part, G) = K.conv_bwd(dy, w, x, dw, *args, addend=addend, bnf=(yc, cc, mean, rstd), wu=wu)
+    assert dx.shape == (B, 2, 2, C)
+    assert _rel(dx, dx_ref) < 1e-2
+    assert _rel(dw, dw_ref) < 1e-2
+    dz = dx.float() * (yc.float() > 0)
+    xh = (cc.float() - mean) * rstd
+    tot = part.view(G, 2, C).sum(0)
+    torch.testing.assert_close(tot[0], dz.reshape(-1, C).sum(0), rtol=2e-3, atol=2e-1)
+    torch.testing.assert_close(tot[1], (dz * xh).reshape(-1, C).sum(0), rtol=2e-3, atol=2e-1)
+    # the separate dgrad / wgrad entry points
+    dw2 = torch.zeros_like(dw)
+    K.conv_wgrad(x, dy, dw2, *args, unroll=True)
+    assert _rel(dw2, dw_ref) < 1e-2
+    dx2 = K.conv_dgrad(dy, w, x.shape, *args, addend=addend, wu=wu)
+    assert _rel(dx2, dx_ref) < 1e-2

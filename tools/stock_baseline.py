@@ -38,27 +38,41 @@ def main():
     probe_native()
     torch.backends.cudnn.benchmark = True
     m = resnet34().cuda().to(memory_format=torch.channels_last)
-    opt = torch.optim.SGD(m.parameters(), lr=0.01, weight_decay=1e-4)
+    opt = torch.optim.SGD(m.parameters(), lr=0.01, weight_decay=1e-4, foreach=True)
     x = torch.randn(args.batch, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (args.batch,), device="cuda")
 
     def step():
         opt.zero_grad(set_to_none=False)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
             loss = F.cross_entropy(m(x), y)
         loss.backward()
         opt.step()
         return loss
 
+    run = step
+    if args.graph:
+        # whole step (zero_grad, autocast forward, backward, SGD) as one captured graph:
+        # stock PyTorch at its launch-overhead-free best
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        run = g.replay
     for _ in range(args.warmup):
-        step()
+        run()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
-    print(json.dumps({"stock_resnet34_bf16_autocast": True, "batch": args.batch,
+    print(json.dumps({"stock_resnet34_bf16_autocast": True, "graph": bool(args.graph), "batch": args.batch,
                       "ms_per_step": dt * 1e3, "img_per_s": args.batch / dt}), flush=True)
 
 

@@ -34,6 +34,10 @@ def conv_layers(model_name, B, H=32, W=32, in_ch=3):
         x = inp[0]
         if isinstance(mod, Conv2d):
             b, h, w, c = x.shape
+            if K.unrolled22(h, w, mod.kernel_size[0], mod.kernel_size[1], mod.stride, mod.padding):
+                # runs as its dense 1x1 form (ops.kernels.unrolled22): tune those GEMMs
+                shapes.append(("conv", 4 * mod.cin_pad, 4 * mod.out_channels, 1, 1, 0, 1, 1))
+                return
             shapes.append(("conv", mod.cin_pad, mod.out_channels, mod.kernel_size[0], mod.stride[0],
                            mod.padding[0], h, w))
         elif isinstance(mod, Linear):
