@@ -164,6 +164,29 @@ def tune_pairs(layers, table, reps, dev):
     return out
 
 
+def candidates(mode, M, N, Kd, cin, cout, ntap):
+    """Every (bm, bn, bk, splits, variant) plan worth timing for one conv GEMM."""
+    cands = []
+    split_opts = [1, 2, 4, 8, 16] if mode != "wgrad" else [1, 2, 4, 8, 16, 32, 64]
+    for bm, bn in TILES:
+        if bm > max(32, -(-M // 32) * 32) or bn > max(32, -(-N // 32) * 32):
+            continue
+        for bk, variant in ((32, 0), (64, 0), (64, 1), (64, 2)):
+            for sp in split_opts:
+                esp = K.effective_splits(Kd if mode != "dgrad" else ntap * (-(-cout // bk) * bk), bk, sp)
+                if esp != sp:
+                    continue
+                cands.append((bm, bn, bk, sp, variant))
+    if mode == "dgrad" or (mode == "fwd" and cin % 32 == 0):
+        # LDS-free wave-split-K kernel (variant 3; the bk slot carries the wave count)
+        for bm, bn in ((16, 16), (16, 32), (32, 16), (32, 32), (32, 64), (64, 32), (64, 64)):
+            if bm > max(16, -(-M // 16) * 16) or bn > max(16, -(-N // 16) * 16):
+                continue
+            for nw in (4, 8):
+                cands.append((bm, bn, nw, 1, 3))
+    return cands
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet34")
@@ -222,24 +245,7 @@ def main():
                 return K.conv_wgrad(x, dy, dw, k, k, (s, s), (p, p), cfg=cfg)
 
             default = K.default_plan(mode, M, N, Kd)
-            cands = []
-            split_opts = [1, 2, 4, 8, 16] if mode != "wgrad" else [1, 2, 4, 8, 16, 32, 64]
-            for bm, bn in TILES:
-                if bm > max(32, -(-M // 32) * 32) or bn > max(32, -(-N // 32) * 32):
-                    continue
-                for bk, variant in ((32, 0), (64, 0), (64, 1), (64, 2)):
-                    for sp in split_opts:
-                        esp = K.effective_splits(Kd if mode != "dgrad" else ntap * (-(-cout // bk) * bk), bk, sp)
-                        if esp != sp:
-                            continue
-                        cands.append((bm, bn, bk, sp, variant))
-            if mode == "dgrad" or (mode == "fwd" and cin % 32 == 0):
-                # LDS-free wave-split-K kernel (variant 3; the bk slot carries the wave count)
-                for bm, bn in ((16, 16), (16, 32), (32, 16), (32, 32), (32, 64), (64, 32), (64, 64)):
-                    if bm > max(16, -(-M // 16) * 16) or bn > max(16, -(-N // 16) * 16):
-                        continue
-                    for nw in (4, 8):
-                        cands.append((bm, bn, nw, 1, 3))
+            cands = candidates(mode, M, N, Kd, cin, cout, ntap)
             res = []
             for cfg in cands:
                 try:
