@@ -156,7 +156,6 @@ def main():
     t_start = time.time()
     B = args.batch
     layers = TC.conv_layers("resnet34", B)
-    layers = [l for l in layers if not (l[0] == "conv" and l[1] == 8)]   # stem: single plan family
     model, make = build_step(B, dev)
     timer = StepTimer(model, make, args.steps)
     inc = timer.capture()
@@ -203,6 +202,13 @@ def main():
     if "bwd" in args.only:
         for layer in layers:
             if layer[0] != "conv":
+                continue
+            if layer[1] == 8:   # stem: no input gradient, the weight gradient runs alone
+                wkey, wc = rank_isolated(layer, "wgrad", B, dev, args.topk, args.reps)
+
+                def install_w(c, wkey=wkey):
+                    K._TUNED[("wgrad",) + wkey] = tuple(c)
+                accept(f"wgrad{wkey}", wc, install_w, plan_of("wgrad", wkey))
                 continue
             dkey, dc = rank_isolated(layer, "dgrad", B, dev, args.topk, args.reps)
             wkey, wc = rank_isolated(layer, "wgrad", B, dev, args.topk, args.reps)
