@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--graph-comm", choices=["on", "off"], default="on",
                     help="capture the overlapped all-reduces inside the step's hipGraph (KUBEML_GRAPH_COMM=0: off)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the measured epoch after the timed steps")
+    ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="gradient all-reduce precision (bf16 = compressed, half the xGMI bytes)")
     ap.add_argument("--cpu-smoke", action="store_true", help="gloo/CPU rehearsal of the N-rank launch (tiny model)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace (device compute/comm timeline) to this dir; "
                                                   "collectives then run outside the step graph")
@@ -207,7 +209,8 @@ def main():
         pre=lambda: K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True),
         post=lambda: K.advance_counter_(ctr, B, n_local),
         world=world, use_graph=not args.no_graph, graph_comm=graph_comm, overlap=overlap,
-        bucket_mb=args.bucket_mb, force_comm=args.force_comm, extra_state=[ctr])
+        bucket_mb=args.bucket_mb, force_comm=args.force_comm, extra_state=[ctr],
+        comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
     if comm:
         step.prime_comm()
     step.capture()
@@ -279,7 +282,7 @@ def main():
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "gradient all-reduce every step (K=1)",
                        "graph": not args.no_graph, "overlap_segments": overlap and comm,
                        "graph_comm": bool(getattr(step, "graph_comm", graph_comm) and comm), "bucket_mb": args.bucket_mb,
-                       "step": "kubeml_amd.engine.dp.make_train_step"},
+                       "grad_comm_dtype": args.comm_dtype, "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
         if epoch is not None:

@@ -12,6 +12,7 @@ Reference: the per-iteration HTTP fan-out + Redis weight round trip of K=1 train
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -24,7 +25,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     post: Optional[Callable[[], None]] = None, group=None, world: int = 1,
                     use_graph: bool = True, graph_comm: bool = True, overlap: bool = True,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
-                    extra_state: Sequence[torch.Tensor] = ()) -> GraphedTrainStep:
+                    extra_state: Sequence[torch.Tensor] = (), comm_dtype=None) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
     pre():  runs first inside the step (e.g. on-device augmentation into ``x``)
@@ -33,7 +34,12 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             optimizer's gradient scale to 1/world
     overlap: split backward at ``model.stages()`` (if the model has them) so each
             stage's gradients are all-reduced while the next stage's backward runs
+    comm_dtype: torch.bfloat16 all-reduces bf16-rounded gradients (half the bytes; see
+            :class:`GraphedTrainStep`); None = ``KUBEML_COMM_DTYPE`` (``bf16`` or fp32, default)
     """
+    if comm_dtype is None:
+        comm_dtype = torch.bfloat16 if os.environ.get("KUBEML_COMM_DTYPE", "fp32").lower() in (
+            "bf16", "bfloat16") else torch.float32
     from ..nn import backward_loss
     comm = world > 1 or force_comm
     scale = 1.0 / max(world, 1)
@@ -68,5 +74,5 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     optimizer.set_grad_scale(scale)
     return GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
-                            graph_comm=graph_comm,
+                            graph_comm=graph_comm, comm_dtype=comm_dtype,
                             state_tensors=train_state_tensors(model, space, optimizer, extra_state))

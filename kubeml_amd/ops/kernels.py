@@ -756,6 +756,12 @@ def f32_to_bf16(x, out=None):
     return out
 
 
+def bf16_to_f32(x, out=None):
+    out = torch.empty(x.shape, dtype=F32, device=x.device) if out is None else out
+    HIP.call("kml_bf16_to_f32", "p p l s", _p(x), _p(out), x.numel(), _s())
+    return out
+
+
 def scale_(x, a):
     HIP.call("kml_scale_f32", "p f l s", _p(x), float(a), x.numel(), _s())
     return x

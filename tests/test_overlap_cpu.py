@@ -9,7 +9,7 @@ import torch.multiprocessing as mp
 import torch.nn.functional as F
 
 
-def _run(rank, world, port, q):
+def _run(rank, world, port, q, comm_dtype=torch.float32):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -36,24 +36,47 @@ def _run(rank, world, port, q):
         segs = [staged.segment(k) for k in range(staged.n_segments)]
         stp = m.stage_params()
         seg_grads = [[sp.grad_view(stp[len(stp) - 1 - k])] for k in range(len(stp))]
-        step = GraphedTrainStep(None, lambda: None, use_graph=False, segments=segs, segment_grads=seg_grads)
+        step = GraphedTrainStep(None, lambda: None, use_graph=False, segments=segs, segment_grads=seg_grads,
+                                comm_dtype=comm_dtype)
         step()
+        if comm_dtype == torch.bfloat16:
+            # reference of the compressed path: every rank's bf16-rounded gradients, summed
+            mine = sp.grad.clone()
+            sp.zero_grad()
+            F.cross_entropy(m(x), y).backward()
+            lp = sp.grad.to(torch.bfloat16)
+            dist.all_reduce(lp)
+            ref = lp.float()
+            q.put((rank, float((mine - ref).abs().max()), float(ref.abs().max())))
+            return
         q.put((rank, float((sp.grad - ref).abs().max()), float(ref.abs().max())))
     finally:
         dist.destroy_process_group()
 
 
-def test_overlapped_segments_match_plain_allreduce():
+def _spawn(comm_dtype):
     from kubeml_amd.runtime.pool import free_port
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=_run, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_run, args=(r, 2, port, q, comm_dtype)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
     for p in ps:
         p.join(60)
-    for rank, diff, mag in res:
+    return res
+
+
+def test_overlapped_segments_match_plain_allreduce():
+    for rank, diff, mag in _spawn(torch.float32):
         assert mag > 0
         assert diff <= 1e-5 * mag, (rank, diff, mag)
+
+
+def test_bf16_gradient_compression_sums_rounded_gradients():
+    """comm_dtype=bf16: each rank's finished gradient ranges go out bf16-rounded and come
+    back widened into the fp32 buffer (the sum of the rounded gradients)."""
+    for rank, diff, mag in _spawn(torch.bfloat16):
+        assert mag > 0
+        assert diff <= 1e-2 * mag, (rank, diff, mag)
