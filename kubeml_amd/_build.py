@@ -126,8 +126,11 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         _run([_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs)
     out["hip"] = lib
     import json as _json
-    with open(os.path.join(LIBDIR, "abi_hip.json"), "w") as f:
+    # write-then-rename: a process loading the library meanwhile never reads a partial file
+    tmp = os.path.join(LIBDIR, f".abi_hip.json.{os.getpid()}")
+    with open(tmp, "w") as f:
         _json.dump(extract_abi(ksrcs), f, indent=0, sort_keys=True)
+    os.replace(tmp, os.path.join(LIBDIR, "abi_hip.json"))
 
     # --- host runtime -------------------------------------------------------------
     rsrcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
@@ -142,8 +145,10 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
                  ["-L" + os.path.join(rocm, "lib"), "-lamdhip64"])
         out["rt"] = lib
         import json as _json
-        with open(os.path.join(LIBDIR, "abi_rt.json"), "w") as f:
+        tmp = os.path.join(LIBDIR, f".abi_rt.json.{os.getpid()}")
+        with open(tmp, "w") as f:
             _json.dump(extract_abi(rsrcs), f, indent=0, sort_keys=True)
+        os.replace(tmp, os.path.join(LIBDIR, "abi_rt.json"))
     return out
 
 
