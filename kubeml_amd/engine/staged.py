@@ -13,8 +13,9 @@ are already final (a contiguous range of the flat grad buffer, because the flat
 layout stores parameters in reverse registration order) on the process-group stream,
 while the next segment's backward keeps the CUs busy.  For ResNet-34 at batch 256 the
 tail (fc + layer4 + layer3) holds 94 % of the 87 MB of gradients and the head
-(stem, layer1, layer2) most of the backward FLOPs, so almost the whole all-reduce
-hides behind compute — the MI355X/xGMI counterpart of DDP's bucketed overlap
+(stem, layer1, layer2) most of the backward FLOPs; with the head itself split at
+layer1/layer2 only the stem + layer1 gradients (~1 MB) are all-reduced after the last
+backward kernel, so almost the whole all-reduce hides behind compute — the MI355X/xGMI counterpart of DDP's bucketed overlap
 (SURVEY §5.8 item 4).
 """
 from __future__ import annotations

@@ -151,6 +151,9 @@ class ResNet(tnn.Module):
         return self.fc(x)
 
     def _head(self, x):
+        return self.layer2(self._stem_l1(x))
+
+    def _stem_l1(self, x):
         if x.dim() == 4 and (x.shape[-1] not in (self.conv1.in_channels, self.conv1.cin_pad)
                              or x.dtype != torch.bfloat16 and x.is_cuda):
             x = M.to_nhwc(x, self.conv1.cin_pad)
@@ -166,18 +169,22 @@ class ResNet(tnn.Module):
             x = self._stem_gpu(x)
         else:
             x = self.maxpool(self.bn1(self.conv1(x), relu=True))
-        return self.layer2(self.layer1(x))
+        return self.layer1(x)
 
     def stages(self):
         """Forward split for overlapped gradient all-reduce (engine/staged.py):
-        [stem+layer1+layer2, layer3, layer4+head].  Parameters of later stages sit
-        first in the flat buffer, so each stage's gradients are one contiguous range."""
-        return [self._head, self.layer3, lambda h: self.fc(self.avgpool(self.layer4(h)))]
+        [stem+layer1, layer2, layer3, layer4+head].  Parameters of later stages sit first in
+        the flat buffer, so each stage's gradients are one contiguous range.  Backward runs
+        the stages in reverse, so the all-reduce that nothing can hide (the first stage's)
+        carries only the stem + layer1 gradients (~1 % of ResNet-34's 87 MB)."""
+        return [self._stem_l1, self.layer2, self.layer3, lambda h: self.fc(self.avgpool(self.layer4(h)))]
 
     def stage_params(self):
         """Parameters owned by each stage of :meth:`stages`."""
-        head = [p for n, p in self.named_parameters() if not n.startswith(("layer3.", "layer4.", "fc."))]
-        return [head, list(self.layer3.parameters()), list(self.layer4.parameters()) + list(self.fc.parameters())]
+        later = ("layer2.", "layer3.", "layer4.", "fc.")
+        head = [p for n, p in self.named_parameters() if not n.startswith(later)]
+        return [head, list(self.layer2.parameters()), list(self.layer3.parameters()),
+                list(self.layer4.parameters()) + list(self.fc.parameters())]
 
     def _bump_counters(self):
         # num_batches_tracked of every BN: one tiny kernel each is avoided by keeping
