@@ -874,6 +874,197 @@ unsigned rows_grid(long long M, int C) {
   return (unsigned)g;
 }
 
+// Stem fusion: y = maxpool_{k,s,p}(relu(bn(x))) with the window argmax (uint8 row-major tap,
+// the k_maxpool_fwd format, so kml_maxpool_bwd runs the backward).  The normalised map is
+// never written: one pass reads x and writes the pooled map (for the ResNet stem a quarter
+// of the BN output's bytes) instead of BN-apply (read x, write y) + max-pool (read y).
+// Statistics prologue as k_bn_apply (partial rows of the conv epilogue summed per block,
+// block 0 updates running / saved statistics).  Every value is rounded to bf16 before the
+// comparison, so maxima and argmax equal the unfused pair's exactly.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_bn_relu_maxpool(
+    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ y, unsigned char* __restrict__ idx,
+    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
+    float* __restrict__ run_var, int B, int H, int W, int C, int OH, int OW, int k, int st, int pd, float eps,
+    float momentum, int stats_rows) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], sums[2C], scratch
+  float* scale = sh;
+  float* shift = sh + C;
+  const long long M = (long long)B * H * W;
+  const float* sums = stats;
+  if (stats_rows > 0) {  // same row-summation order as k_bn_apply_v: bit-identical statistics
+    float* acc = sh + 2 * C;
+    if (C / 2 <= NT) {
+      EarlyRows er;
+      er.issue(stats, stats_rows, 2 * C, NT);
+      er.finish(stats, stats_rows, acc, reinterpret_cast<float4*>(sh + 4 * C));
+    } else {
+      sum_partial_rows<NT>(stats, stats_rows, 2 * C, acc, reinterpret_cast<float4*>(sh + 4 * C));
+    }
+    sums = acc;
+  }
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const float mean = sums[c] / (float)M;
+    const float var = fmaxf(sums[C + c] / (float)M - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    scale[c] = g * rstd;
+    shift[c] = bb - mean * g * rstd;
+    if (blockIdx.x == 0) {
+      if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
+      if (run_mean) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+      }
+    }
+  }
+  __syncthreads();
+  const int CH = C / 8;
+  const long long total = (long long)B * OH * OW * CH;
+  for (long long t = blockIdx.x * (long long)NT + threadIdx.x; t < total; t += (long long)gridDim.x * NT) {
+    const int ch = (int)(t % CH);
+    long long pix = t / CH;
+    const int ow = (int)(pix % OW); pix /= OW;
+    const int oh = (int)(pix % OH);
+    const int b = (int)(pix / OH);
+    float sc[8], sf[8], best[8];
+    int bi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale[ch * 8 + i];
+      sf[i] = shift[ch * 8 + i];
+      best[i] = -INFINITY;
+      bi[i] = 0;
+    }
+    for (int r = 0; r < k; ++r) {
+      const int ih = oh * st - pd + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int iw = ow * st - pd + q;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + ((long long)(b * H + ih) * W + iw) * C + ch * 8), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float v = bf2f(f2bf(fmaxf(f[i] * sc[i] + sf[i], 0.f)));
+          if (v > best[i] || (v != v)) { best[i] = v; bi[i] = r * k + q; }
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[t] = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    reinterpret_cast<uint2*>(idx)[t] = packed;
+  }
+}
+
+// k_bn_relu_maxpool specialised for the 3x3 window of the ResNet stem: each thread owns IPT
+// output chunks per grid-stride round and issues ALL their window loads (IPT x 9 x 16 B, taps
+// outside the image clamped to the centre and masked) before the statistics prologue
+// finishes, so one memory round trip covers both (the generic kernel's per-tap loop
+// serialised nine).  Same statistics order and rounding as k_bn_apply_v.
+template <int NT, int IPT>
+__global__ __launch_bounds__(NT) void k_bn_relu_maxpool3(
+    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ y, unsigned char* __restrict__ idx,
+    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
+    float* __restrict__ run_var, int B, int H, int W, int C, int OH, int OW, int st, int pd, float eps,
+    float momentum, int stats_rows) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* scale = sh;
+  float* shift = sh + C;
+  const long long M = (long long)B * H * W;
+  const int CH = C / 8;
+  const long long total = (long long)B * OH * OW * CH;
+  const long long T = (long long)gridDim.x * NT;
+  const bool parts = stats_rows > 0;
+  const bool early = parts && C / 2 <= NT;
+  EarlyRows er;
+  if (early) er.issue(stats, stats_rows, 2 * C, NT);
+  uint4 v[IPT][9];
+  unsigned okm[IPT];
+  auto load = [&](long long base) {
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const long long t = min(base + j * T, total - 1);
+      long long pix = t / CH;
+      const int ch = (int)(t - pix * CH);
+      const int ow = (int)(pix % OW); pix /= OW;
+      const int oh = (int)(pix % OH);
+      const int b = (int)(pix / OH);
+      okm[j] = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int ih = oh * st - pd + r, iw = ow * st - pd + q;
+          const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+          okm[j] |= ok ? (1u << (r * 3 + q)) : 0u;
+          const int ih2 = ok ? ih : min(max(ih, 0), H - 1), iw2 = ok ? iw : min(max(iw, 0), W - 1);
+          v[j][r * 3 + q] = *reinterpret_cast<const uint4*>(x + ((long long)(b * H + ih2) * W + iw2) * C + ch * 8);
+        }
+    }
+  };
+  const long long i0 = blockIdx.x * (long long)NT + threadIdx.x;
+  load(i0);
+  const float* sums = stats;
+  if (parts) {
+    float* acc = sh + 2 * C;
+    if (early) er.finish(stats, stats_rows, acc, reinterpret_cast<float4*>(sh + 4 * C));
+    else sum_partial_rows<NT>(stats, stats_rows, 2 * C, acc, reinterpret_cast<float4*>(sh + 4 * C));
+    sums = acc;
+  }
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const float mean = sums[c] / (float)M;
+    const float var = fmaxf(sums[C + c] / (float)M - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    scale[c] = g * rstd;
+    shift[c] = bb - mean * g * rstd;
+    if (blockIdx.x == 0) {
+      if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
+      if (run_mean) {
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+      }
+    }
+  }
+  __syncthreads();
+  for (long long base = i0, it = 0; base < total; base += IPT * T, ++it) {
+    if (it > 0) load(base);
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const long long t = base + j * T;
+      if (t >= total) continue;
+      const int ch = (int)(t % CH);
+      float best[8];
+      int bi[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; bi[i] = 0; }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (!((okm[j] >> tap) & 1u)) continue;
+        float f[8];
+        unpack8(v[j][tap], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float o = bf2f(f2bf(fmaxf(f[i] * scale[ch * 8 + i] + shift[ch * 8 + i], 0.f)));
+          if (o > best[i] || (o != o)) { best[i] = o; bi[i] = tap; }
+        }
+      }
+      reinterpret_cast<uint4*>(y)[t] = pack8(best);
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+      reinterpret_cast<uint2*>(idx)[t] = packed;
+    }
+  }
+}
+
 }  // namespace
 
 // rows of partial statistics kml_bn_stats_part writes (<= 128 KB of partials for bn_apply to sum)
@@ -1052,5 +1243,45 @@ KML_API int kml_relu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s)
 KML_API int kml_relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long long n, hipStream_t s) {
   if (n % 8) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_relu_bwd, dim3(kml_stream_grid(n / 8, 256)), dim3(256), 0, s, dy, y, dx, n / 8);
+  KML_LAUNCH_CHECK();
+}
+
+// Training forward of the ResNet stem's BN -> ReLU -> max-pool as one pass (k_bn_relu_maxpool):
+// x [B][H][W][C] conv output, stats = [stats_rows][2C] partial rows (or final [2C] sums with
+// stats_rows = 0), y [B][OH][OW][C] pooled output, idx its window argmax.
+KML_API int kml_bn_relu_maxpool(const bf16_t* x, const float* stats, int stats_rows, const float* gamma,
+                                const float* beta, bf16_t* y, unsigned char* idx, float* save_mean,
+                                float* save_rstd, float* run_mean, float* run_var, int B, int H, int W, int C, int k,
+                                int st, int pd, float eps, float momentum, float* fold_ws, hipStream_t s) {
+  if (C % 8 || k * k > 255 || k < 1 || st < 1 || pd < 0 || 2 * pd > k) return (int)hipErrorInvalidValue;
+  if (stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
+  const int OH = (H + 2 * pd - k) / st + 1, OW = (W + 2 * pd - k) / st + 1;
+  const long long total = (long long)B * OH * OW * (C / 8);
+  unsigned grid = kml_stream_grid(total, TPB);
+  if (stats_rows > 0 && grid > 256) grid = 256;  // every block re-sums the partial rows
+  const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
+  if (k == 3 && stats_rows >= 128) {
+    // many partial rows (ResNet stem: one per 128-pixel conv tile): 512-thread blocks sum
+    // them in half the load batches (1024 threads would spill the window registers)
+    constexpr int NT = 512;
+    long long g3 = (total + NT - 1) / NT;
+    if (g3 > 256) g3 = 256;
+    const size_t shm3 = (4 * C + 4 * NT) * sizeof(float);
+    hipLaunchKernelGGL((k_bn_relu_maxpool3<NT, 1>), dim3((unsigned)g3), dim3(NT), shm3, s, x, stats, gamma, beta,
+                       y, idx, save_mean, save_rstd, run_mean, run_var, B, H, W, C, OH, OW, st, pd, eps, momentum,
+                       stats_rows);
+    KML_LAUNCH_CHECK();
+  }
+  if (k == 3) {
+    constexpr int IPT = 2;
+    long long g3 = (total + (long long)TPB * IPT - 1) / ((long long)TPB * IPT);
+    if (g3 > 256) g3 = 256;
+    hipLaunchKernelGGL((k_bn_relu_maxpool3<TPB, IPT>), dim3((unsigned)g3), dim3(TPB), shm, s, x, stats, gamma, beta,
+                       y, idx, save_mean, save_rstd, run_mean, run_var, B, H, W, C, OH, OW, st, pd, eps, momentum,
+                       stats_rows);
+    KML_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_bn_relu_maxpool<TPB>, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, y, idx, save_mean,
+                     save_rstd, run_mean, run_var, B, H, W, C, OH, OW, k, st, pd, eps, momentum, stats_rows);
   KML_LAUNCH_CHECK();
 }

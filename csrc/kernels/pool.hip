@@ -58,8 +58,11 @@ __global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__
   }
 }
 
+// relu_out (optional): the pooled forward output of a fused BN -> ReLU -> max-pool; a window
+// whose maximum is not > 0 passes no gradient (its argmax sat at ReLU's zero), so dx is
+// already dz = d(BN output) and the BN backward needs no ReLU mask.
 __global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char* __restrict__ idx,
-                              bf16_t* __restrict__ dx, PoolGeom g) {
+                              const bf16_t* __restrict__ relu_out, bf16_t* __restrict__ dx, PoolGeom g) {
   const int CH = g.C / 8;
   const long long total = (long long)g.B * g.H * g.W * CH;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
@@ -82,6 +85,12 @@ __global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char
         const uint2 pk = reinterpret_cast<const uint2*>(idx)[o];
         float d[8];
         unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+        if (relu_out) {
+          float m[8];
+          unpack8(reinterpret_cast<const uint4*>(relu_out)[o], m);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) d[i] = m[i] > 0.f ? d[i] : 0.f;
+        }
         const int tap = r * g.k + q;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -140,12 +149,13 @@ KML_API int kml_maxpool_fwd(const bf16_t* x, bf16_t* y, unsigned char* idx, int 
   KML_LAUNCH_CHECK();
 }
 
-KML_API int kml_maxpool_bwd(const bf16_t* dy, const unsigned char* idx, bf16_t* dx, int B, int H, int W, int C,
-                            int k, int s, int p, hipStream_t st) {
+KML_API int kml_maxpool_bwd(const bf16_t* dy, const unsigned char* idx, const bf16_t* relu_out, bf16_t* dx, int B,
+                            int H, int W, int C, int k, int s, int p, hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
   PoolGeom g{B, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   long long total = (long long)B * H * W * (C / 8);
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, idx, dx, g);
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, idx, relu_out, dx,
+                     g);
   KML_LAUNCH_CHECK();
 }
 

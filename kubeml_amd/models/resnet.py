@@ -215,22 +215,47 @@ class ResNet(tnn.Module):
 
 
 class _StemFn(torch.autograd.Function):
+    """conv1 -> bn1 -> ReLU -> max-pool of the training forward.  BN-apply, ReLU and the pool
+    run as ONE pass (``bn_relu_maxpool``: the full-resolution normalised map is never
+    written); backward folds the ReLU mask into the gather max-pool backward, so the BN
+    backward reads dz and the conv output only.  ``KUBEML_STEM_FUSE=0``: unfused path."""
+
     @staticmethod
     def forward(ctx, x, net, *params):
         from ..ops import kernels as K
-        y, s = ConvBNUnit.forward(x, net.conv1, net.bn1, True, None, True)
-        p, idx = K.maxpool_fwd(y, 3, 2, 1)
-        ctx.net, ctx.s, ctx.idx, ctx.yshape = net, s, idx, y.shape
+        if not _STEM_FUSE:
+            y, s = ConvBNUnit.forward(x, net.conv1, net.bn1, True, None, True)
+            p, idx = K.maxpool_fwd(y, 3, 2, 1)
+            ctx.net, ctx.s, ctx.idx, ctx.yshape, ctx.p = net, s, idx, y.shape, None
+            return p
+        conv, bn = net.conv1, net.bn1
+        from ..nn.flat import master_of, shadow_of
+        w = shadow_of(conv.weight)
+        kh, kw = conv.kernel_size
+        G = K.conv_fwd_stats_rows(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding)
+        stats = torch.empty(G * 2 * w.shape[0], dtype=torch.float32, device=x.device)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True)
+        C = c.shape[-1]
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        p, idx = K.bn_relu_maxpool(c, stats, master_of(bn.weight), master_of(bn.bias), 3, 2, 1, save_mean=mean,
+                                   save_rstd=rstd, run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
+                                   momentum=bn.momentum if bn.momentum is not None else 0.1, stats_rows=G)
+        # saved like a ConvBNUnit without ReLU: the mask travels in the pooled output
+        ctx.net, ctx.s, ctx.idx, ctx.yshape, ctx.p = net, (x, c, None, mean, rstd), idx, c.shape, p
         return p
 
     @staticmethod
     def backward(ctx, dp):
         from ..ops import kernels as K
         net = ctx.net
-        dy = K.maxpool_bwd(dp.contiguous(), ctx.idx, ctx.yshape, 3, 2, 1)
+        dy = K.maxpool_bwd(dp.contiguous(), ctx.idx, ctx.yshape, 3, 2, 1, relu_out=ctx.p)
         dx, _, _ = ConvBNUnit.backward(dy, ctx.s, net.conv1, net.bn1, False, ctx.needs_input_grad[0])
-        ctx.s = ctx.idx = None
+        ctx.s = ctx.idx = ctx.p = None
         return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+_STEM_FUSE = __import__("os").environ.get("KUBEML_STEM_FUSE", "1") != "0"
 
 
 def resnet18(num_classes=1000, **kw):

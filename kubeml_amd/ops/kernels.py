@@ -781,11 +781,34 @@ def maxpool_fwd(x, k, s, p):
     return y, idx
 
 
-def maxpool_bwd(dy, idx, in_shape, k, s, p):
+def maxpool_bwd(dy, idx, in_shape, k, s, p, relu_out=None):
+    """Gather max-pool backward.  relu_out: the pooled output of :func:`bn_relu_maxpool`;
+    windows whose maximum is not > 0 pass no gradient (the ReLU mask folded in)."""
     B, H, W, C = in_shape
+    if relu_out is not None and relu_out.shape != dy.shape:
+        raise ValueError("relu_out must have the pooled shape")
     dx = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
-    HIP.call("kml_maxpool_bwd", "p p p i i i i i i i s", _p(dy), _p(idx), _p(dx), B, H, W, C, k, s, p, _s())
+    HIP.call("kml_maxpool_bwd", "p p p p i i i i i i i s", _p(dy), _p(idx), _p(relu_out), _p(dx), B, H, W, C, k, s,
+             p, _s())
     return dx
+
+
+def bn_relu_maxpool(x, stats, gamma, beta, k, s, p, save_mean=None, save_rstd=None, run_mean=None, run_var=None,
+                    eps=1e-5, momentum=0.1, stats_rows=0):
+    """Training BN (batch statistics from ``stats``: [stats_rows][2C] conv-epilogue partial
+    rows, or final [2C] sums) -> ReLU -> max-pool(k, s, p) in one pass; returns (pooled,
+    argmax idx).  The normalised map is never materialised — backward is
+    ``maxpool_bwd(..., relu_out=pooled)`` then ``bn_bwd`` without a ReLU mask."""
+    _chk(x, BF16, "x", 4)
+    B, H, W, C = x.shape
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    y = torch.empty((B, OH, OW, C), dtype=BF16, device=x.device)
+    idx = torch.empty((B, OH, OW, C), dtype=torch.uint8, device=x.device)
+    ws = _fold_ws(stats_rows, C, x.device) if stats_rows > 0 else None
+    HIP.call("kml_bn_relu_maxpool", "p p i p p p p p p p p i i i i i i i f f p s",
+             _p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(y), _p(idx), _p(save_mean), _p(save_rstd),
+             _p(run_mean), _p(run_var), B, H, W, C, k, s, p, float(eps), float(momentum), _p(ws), _s())
+    return y, idx
 
 
 def gavgpool_fwd(x):

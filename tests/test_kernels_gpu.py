@@ -666,3 +666,45 @@ def test_unrolled_conv_bwd_matches_3x3(B, C, Kc):
     assert _rel(dw2, dw_ref) < 1e-2
     dx2 = K.conv_dgrad(dy, w, x.shape, *args, addend=addend, wu=wu)
     assert _rel(dx2, dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,C", [(16, 16, 64), (3, 112, 64), (5, 9, 24)])
+def test_bn_relu_maxpool_matches_unfused(B, H, C):
+    """Fused stem BN -> ReLU -> max-pool (one pass, normalised map never written) against
+    bn_apply + maxpool_fwd, and its backward (ReLU mask folded into the gather max-pool
+    backward) against maxpool_bwd * [y > 0]; batch statistics from conv-style partial rows."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(5)
+    c = _bf(torch.randn(B, H, H, C, device=dev) * 2 + 0.3)
+    cf = c.float().reshape(-1, C)
+    G = 7
+    rows = torch.zeros(G, 2, C, device=dev)
+    for g, chunk in enumerate(cf.chunk(G)):
+        rows[g, 0] = chunk.sum(0)
+        rows[g, 1] = (chunk * chunk).sum(0)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.2
+    rm1, rv1 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    m1, r1 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    m2, r2 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    y = K.bn_apply(c, rows.reshape(-1), gamma, beta, save_mean=m1, save_rstd=r1, run_mean=rm1, run_var=rv1,
+                   relu=True, stats_rows=G)
+    p_ref, idx_ref = K.maxpool_fwd(y, 3, 2, 1)
+    p, idx = K.bn_relu_maxpool(c, rows.reshape(-1), gamma, beta, 3, 2, 1, save_mean=m2, save_rstd=r2, run_mean=rm2,
+                               run_var=rv2, stats_rows=G)
+    assert p.shape == p_ref.shape
+    # same statistics; values can differ by one bf16 rounding step where the two kernels'
+    # FMA orders differ, which may flip an argmax between near-equal window elements
+    for a, b in ((m2, m1), (r2, r1), (rm2, rm1), (rv2, rv1)):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p.float(), p_ref.float(), rtol=1e-2, atol=1e-2)
+    assert (idx == idx_ref).float().mean() > 0.995
+    # exact-semantics check against fp32 torch
+    ref = F.max_pool2d(torch.relu((c.float() - m1) * r1 * gamma + beta).permute(0, 3, 1, 2), 3, 2, 1)
+    assert _rel(p.permute(0, 3, 1, 2), ref) < 1e-2
+    dp = _bf(torch.randn_like(p.float()))
+    dz = K.maxpool_bwd(dp, idx, c.shape, 3, 2, 1, relu_out=p)
+    dz_ref = K.maxpool_bwd(dp, idx, c.shape, 3, 2, 1).float() * (y.float() > 0)
+    agree = (dz.float() - dz_ref).abs() <= 1e-6
+    assert agree.float().mean() > 0.995

@@ -65,6 +65,9 @@ def test_resnet34_forward_backward_matches_reference():
         assert e_ours < 1.3 * e_ac + 0.05, (name, e_ours, e_ac)
     # running stats updated like torch
     assert _rel(ours.layer2[0].bn1.running_mean, ref.layer2[0].bn1.running_mean) < 0.05
+    # stem BN (fused BN -> ReLU -> max-pool pass) updates its running stats too
+    assert _rel(ours.bn1.running_mean, ref.bn1.running_mean) < 0.05
+    assert _rel(ours.bn1.running_var, ref.bn1.running_var) < 0.05
     sd = ours.state_dict()
     for k, v in ref.state_dict().items():
         assert sd[k].shape == v.shape, k
@@ -241,3 +244,55 @@ def test_resnet32_cifar_learns_on_gpu():
         opt.step()
         losses.append(float(loss))
     assert all(v == v for v in losses) and losses[-1] < 0.8 * losses[0], losses
+
+
+def test_resnet_fused_stem_matches_unfused_stem():
+    """KUBEML_STEM_FUSE path (one BN->ReLU->max-pool pass, ReLU mask folded into the pool
+    backward) vs the unfused BN-apply + max-pool pair and an fp32 torch stem, on the stem
+    alone (conv1 -> bn1 -> ReLU -> max-pool -> fixed random readout): output, running stats
+    and the conv1 / bn1 gradients."""
+    from kubeml_amd.models import resnet as RN
+    from kubeml_amd.nn import flatten_module
+    torch.manual_seed(0)
+    x = torch.randn(128, 32, 32, 3, device=dev).to(torch.bfloat16)
+    xp = torch.zeros(128, 32, 32, 8, device=dev, dtype=torch.bfloat16)
+    xp[..., :3] = x
+    R = torch.randn(128, 8, 8, 64, device=dev)
+    res = []
+    old = RN._STEM_FUSE
+    try:
+        for fuse in (False, True):
+            RN._STEM_FUSE = fuse
+            torch.manual_seed(1)
+            m = RN.resnet18(10).to(dev)
+            sp = flatten_module(m)
+            m.train()
+            sp.zero_grad()
+            p = m._stem_gpu(xp)
+            (p.float() * R).sum().backward()
+            torch.cuda.synchronize()
+            res.append((p.float(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(), m.bn1.bias.grad.clone(),
+                        m.bn1.running_mean.clone(), m.bn1.running_var.clone()))
+    finally:
+        RN._STEM_FUSE = old
+    (p0, w0, g0, b0, rm0, rv0), (p1, w1, g1, b1, rm1, rv1) = res
+    # statistics summed in a different (equally exact) order: ulp-level differences only
+    torch.testing.assert_close(rm1, rm0, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(rv1, rv0, rtol=1e-5, atol=1e-7)
+    assert _rel(p1, p0) < 1e-3
+    for a, b in ((w1, w0), (g1, g0), (b1, b0)):
+        assert _rel(a, b) < 1e-2, (_rel(a, b))
+    # fp32 torch stem on the same weights
+    torch.manual_seed(1)
+    m = RN.resnet18(10).to(dev)
+    w = m.conv1.weight.detach().float().clone().requires_grad_()
+    gam = m.bn1.weight.detach().float().clone().requires_grad_()
+    bet = m.bn1.bias.detach().float().clone().requires_grad_()
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = w if w.shape[1] == 3 else w[:, :3]
+    h = F.conv2d(xr, wr, stride=2, padding=3)
+    h = F.batch_norm(h, None, None, gam, bet, training=True, eps=1e-5)
+    pr = F.max_pool2d(torch.relu(h), 3, 2, 1)
+    (pr * R.permute(0, 3, 1, 2)).sum().backward()
+    assert _rel(p1.permute(0, 3, 1, 2), pr) < 2e-2
+    assert _rel(g1, gam.grad) < 5e-2 and _rel(b1, bet.grad) < 5e-2
