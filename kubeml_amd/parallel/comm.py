@@ -106,14 +106,26 @@ class TorchComm(Comm):
         self.world = len(self.ranks)
         self._subs: Dict[int, "TorchComm"] = {}
         self._parent = parent
+        self.oneshot = None
 
     @property
     def member(self) -> bool:
         return self.rank >= 0
 
+    def enable_oneshot(self, cap_bytes: Optional[int] = None):
+        """Collective over this group: route fp32 sums/averages of at most ``cap_bytes``
+        (default ``KUBEML_ONESHOT_MB``, 8 MB) through the one-shot peer-memory all-reduce
+        (:mod:`kubeml_amd.parallel.oneshot`) instead of RCCL.  GPU groups of one node only."""
+        if self.world > 1 and self.oneshot is None:
+            from .oneshot import DEFAULT_CAP, OneShotAllReduce
+            self.oneshot = OneShotAllReduce(self.group, cap_bytes or DEFAULT_CAP)
+        return self
+
     def all_reduce_(self, t, op="sum"):
         if self.world == 1:
             return t
+        if self.oneshot is not None and op in ("sum", "avg") and self.oneshot.supports(t):
+            return self.oneshot.all_reduce_(t, 1.0 / self.world if op == "avg" else 1.0)
         o = getattr(self.dist.ReduceOp, _OPS[op])
         self.dist.all_reduce(t, op=o, group=self.group)
         return t

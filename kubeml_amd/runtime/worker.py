@@ -115,6 +115,10 @@ class Worker:
                                     **kw)
             self.comm = TorchComm()
             self.comm.prepare_subgroups(self.world)
+            if self.use_gpu and os.environ.get("KUBEML_ONESHOT", "0") == "1":
+                # small fp32 reductions (K-AVG rounds of small models, BN statistics, counts)
+                # over the world group go through the one-shot peer-memory all-reduce
+                self.comm.enable_oneshot()
         else:
             self.comm = LocalComm()
         self.store = ShardStore(self.store_dir)

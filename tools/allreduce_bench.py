@@ -14,8 +14,12 @@ NCCL_ALGO / NCCL_PROTO can be swept through the environment).  The graph column 
 the same all-reduce captured ``--graph-batch`` times into one hipGraph and replayed:
 the launch-overhead-free latency the training step sees (its collectives are captured).
 
-The framework's payloads are marked: ResNet-34 gradients (87.3 MB fp32 in 3 stage
-segments of ~2.3 / 19 / 66 MB), LeNet (0.18 MB), BN buffers (34 KB).  One JSON line per
+``--oneshot`` adds the one-shot peer-memory all-reduce (``kubeml_amd.parallel.oneshot``:
+one hop over the fully connected xGMI mesh instead of a ring) for fp32 sizes up to
+``--oneshot-mb``, eager and graph-captured, next to RCCL.
+
+The framework's payloads are marked: ResNet-34 gradients (87.2 MB fp32 in 4 stage
+segments of 0.93 / 4.5 / 27.3 / 54.5 MB), LeNet (0.18 MB), BN buffers (34 KB).  One JSON line per
 size on rank 0, then a summary line.
 """
 import argparse
@@ -29,9 +33,9 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-MARKS = {"lenet grads": 178_000, "bn buffers (resnet34)": 34_000, "resnet34 seg0 (stem+l1+l2)": 2_400_000,
-         "resnet34 seg1 (layer3)": 19_000_000, "resnet34 seg2 (layer4+fc)": 66_000_000,
-         "resnet34 all grads": 87_300_000}
+MARKS = {"lenet grads": 178_000, "bn buffers (resnet34)": 34_000, "resnet34 stage stem+layer1": 925_952,
+         "resnet34 stage layer2": 4_465_664, "resnet34 stage layer3": 27_289_600,
+         "resnet34 stage layer4+fc": 54_509_472, "resnet34 all grads": 87_190_688}
 
 
 def main():
@@ -44,6 +48,10 @@ def main():
     ap.add_argument("--graph-batch", type=int, default=10)
     ap.add_argument("--dtypes", default="fp32,bf16")
     ap.add_argument("--cpu", action="store_true", help="gloo on CPU (rehearsal)")
+    ap.add_argument("--oneshot", action="store_true",
+                    help="also time the one-shot peer-memory all-reduce (kubeml_amd.parallel.oneshot) for fp32 "
+                         "sizes up to --oneshot-mb")
+    ap.add_argument("--oneshot-mb", type=int, default=8)
     a = ap.parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         s = socket.socket()
@@ -77,6 +85,11 @@ def main():
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    oneshot = None
+    if a.oneshot and dev.type == "cuda" and world > 1:
+        from kubeml_amd.parallel.oneshot import OneShotAllReduce
+        oneshot = OneShotAllReduce(None, cap_bytes=a.oneshot_mb << 20, device=dev)
 
     sizes = []
     b = a.min_bytes
@@ -124,12 +137,42 @@ def main():
                     g.replay()
                 sync()
                 tg = tmax((time.perf_counter() - t0) / (3 * a.graph_batch))
+            t1 = t1g = None
+            if oneshot is not None and oneshot.supports(x):
+                for _ in range(a.warmup):
+                    oneshot.all_reduce_(x)
+                sync()
+                ts = []
+                for _ in range(a.iters):
+                    dist.barrier()
+                    sync()
+                    t0 = time.perf_counter()
+                    oneshot.all_reduce_(x)
+                    sync()
+                    ts.append(time.perf_counter() - t0)
+                ts.sort()
+                t1 = tmax(ts[len(ts) // 2])
+                g1 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1):
+                    for _ in range(a.graph_batch):
+                        oneshot.all_reduce_(x)
+                g1.replay()
+                sync()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(3):
+                    g1.replay()
+                sync()
+                t1g = tmax((time.perf_counter() - t0) / (3 * a.graph_batch))
             algbw = n * es / t / 1e9
             bus = algbw * (2 * (world - 1) / world if world > 1 else 1.0)
             mark = [k for k, v in MARKS.items() if v == nbytes]
             rec = {"dtype": dt_name, "bytes": n * es, "us": round(t * 1e6, 2),
                    "us_graph": round(tg * 1e6, 2) if tg else None, "algbw_GBs": round(algbw, 2),
                    "busbw_GBs": round(bus, 2), "world": world}
+            if t1 is not None:
+                rec["oneshot_us"] = round(t1 * 1e6, 2)
+                rec["oneshot_us_graph"] = round(t1g * 1e6, 2)
             if mark:
                 rec["payload"] = mark[0]
             results.append(rec)
@@ -144,6 +187,10 @@ def main():
                           "small_latency_graph_us": min((r["us_graph"] for r in results if r["us_graph"]), default=None),
                           "env": {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))}}),
               flush=True)
+    if oneshot is not None:
+        if oneshot.errors():
+            print(json.dumps({"oneshot_spin_giveups": oneshot.errors()}), flush=True)
+        oneshot.close()
     dist.destroy_process_group()
 
 
