@@ -251,12 +251,28 @@ class GraphedTrainStep:
         mode = "thread_local" if self.comm else "global"
         if self.comm and trace.enabled():
             self.graph_comm = False   # keep the collectives outside the graph so they can be timed
+        captured_all = False
         if not self.comm or self.graph_comm:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=mode):
-                self.loss = self._body()
-            self.g_all, self.g_seg, self.g_opt = g, [], None
-        else:
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode=mode):
+                    self.loss = self._body()
+                self.g_all, self.g_seg, self.g_opt = g, [], None
+                captured_all = True
+            except RuntimeError as e:
+                if not self.comm:
+                    raise
+                # the collectives would not capture on this RCCL/driver build: every rank hits
+                # the same op, so all fall back together to per-segment graphs with eager
+                # collectives between the replays
+                import sys
+                print(f"[kubeml] all-reduce capture failed ({str(e)[:200]}); falling back to per-segment "
+                      f"graphs with eager collectives", file=sys.stderr, flush=True)
+                torch.cuda.synchronize()
+                self._pending_widen = []
+                self.graph_comm = False
+                self.graph_comm_fallback = True
+        if not captured_all:
             pool = torch.cuda.graph_pool_handle()
             self.g_seg = []
             for k, seg in enumerate(self.segments):
