@@ -98,7 +98,7 @@ def relaunch(args):
     sys.exit(subprocess.call(cmd, env=env))
 
 
-def cpu_smoke(args, world, rank):
+def cpu_smoke(args, world, rank, json_out=None):
     """N gloo ranks on CPU: LeNet, gradient all-reduce every step, one JSON line."""
     import torch
     import torch.distributed as dist
@@ -138,9 +138,19 @@ def cpu_smoke(args, world, rank):
         print(json.dumps({"metric": "cpu-smoke (gloo launch rehearsal; not a performance number)", "value": None,
                           "unit": None, "n_gpus": 0, "ranks": world, "ranks_joined": int(joined.item()),
                           "ranks_in_sync": in_sync, "steps": args.steps, "warmup": args.warmup,
-                          "config": {"model": "lenet5", "backend": "gloo"}}), flush=True)
+                          "config": {"model": "lenet5", "backend": "gloo"}}), file=json_out or sys.stdout, flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _claim_stdout():
+    """Keep stdout for the ONE JSON line: native libraries (RCCL prints its version banner
+    to fd 1 when a communicator is created) write to stderr instead.  Returns the stream
+    the JSON line goes to."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
 
 
 def main():
@@ -148,6 +158,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         relaunch(args)
+    json_out = _claim_stdout()
     if "WORLD_SIZE" in os.environ and world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
@@ -156,7 +167,7 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     if args.cpu_smoke:
-        return cpu_smoke(args, world, rank)
+        return cpu_smoke(args, world, rank, json_out)
 
     import torch
     import torch.distributed as dist
@@ -291,7 +302,7 @@ def main():
         if in_sync is not None:
             out["ranks_in_sync"] = in_sync
             out["rccl_world"] = dist.get_world_size()
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if args.trace:
         from kubeml_amd.utils import trace as _trace
         _trace.flush(args.trace)

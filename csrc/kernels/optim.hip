@@ -150,11 +150,15 @@ KML_API int kml_memset(void* p, int value, long long bytes, hipStream_t s) {
   return (int)hipMemsetAsync(p, value, (size_t)bytes, s);
 }
 
+// max_blocks > 0 caps the grid (a range update running next to latency-bound backward
+// kernels on a side stream should take a slice of the CUs, not all of them)
 KML_API int kml_sgd(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr, float lr, float wd,
                     float momentum, float dampening, int nesterov, const float* first_ptr, int first,
-                    float grad_scale, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_sgd, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, w, g, mom, shadow, lr_ptr, lr,
-                     wd, momentum, dampening, nesterov, first_ptr, first, grad_scale, n);
+                    float grad_scale, long long n, int max_blocks, hipStream_t s) {
+  unsigned grid = kml_stream_grid((n + 3) / 4, 256);
+  if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
+  hipLaunchKernelGGL(k_sgd, dim3(grid), dim3(256), 0, s, w, g, mom, shadow, lr_ptr, lr, wd, momentum, dampening,
+                     nesterov, first_ptr, first, grad_scale, n);
   KML_LAUNCH_CHECK();
 }
 

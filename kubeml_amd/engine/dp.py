@@ -25,7 +25,8 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     post: Optional[Callable[[], None]] = None, group=None, world: int = 1,
                     use_graph: bool = True, graph_comm: bool = True, overlap: bool = True,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
-                    extra_state: Sequence[torch.Tensor] = (), comm_dtype=None) -> GraphedTrainStep:
+                    extra_state: Sequence[torch.Tensor] = (), comm_dtype=None,
+                    opt_overlap: Optional[bool] = None) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
     pre():  runs first inside the step (e.g. on-device augmentation into ``x``)
@@ -36,6 +37,13 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             stage's gradients are all-reduced while the next stage's backward runs
     comm_dtype: torch.bfloat16 all-reduces bf16-rounded gradients (half the bytes; see
             :class:`GraphedTrainStep`); None = ``KUBEML_COMM_DTYPE`` (``bf16`` or fp32, default)
+    opt_overlap: apply the optimizer per backward stage on a side stream as soon as the
+            stage's gradients are final (after its all-reduce when world > 1), overlapping the
+            bandwidth-bound update with the rest of the latency-bound backward; needs a model
+            with stages, an optimizer with ``step_range`` and the whole step in one graph.
+            None = ``KUBEML_OPT_OVERLAP`` (default OFF: on one MI355X the concurrent
+            side-stream update slows the backward's latency-bound kernel stream, ResNet-34
+            1.40 -> 1.73-1.81 ms/step whatever its grid; profiles/launch_fusion_r2.md)
     """
     if comm_dtype is None:
         comm_dtype = torch.bfloat16 if os.environ.get("KUBEML_COMM_DTYPE", "fp32").lower() in (
@@ -50,8 +58,13 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         if post is not None:
             post()
 
-    segs = seg_grads = None
-    if comm and overlap and hasattr(model, "stages") and hasattr(model, "stage_params"):
+    segs = seg_grads = seg_opt = opt_finish = None
+    staged_ok = hasattr(model, "stages") and hasattr(model, "stage_params")
+    if opt_overlap is None:
+        opt_overlap = os.environ.get("KUBEML_OPT_OVERLAP", "0") == "1"
+    opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm)
+                       and getattr(optimizer, "supports_ranges", lambda: False)())
+    if (comm and overlap and staged_ok) or opt_overlap:
         from .staged import StagedForwardBackward
 
         def pre0():
@@ -61,8 +74,21 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         staged = StagedForwardBackward(model.stages(), lambda out: loss_fn(out, y), lambda: x, pre=pre0)
         segs = [staged.segment(k) for k in range(staged.n_segments)]
         sp = model.stage_params()
-        seg_grads = [[space.grad_view(sp[len(sp) - 1 - k])] for k in range(len(sp))]
+        stage_of_seg = [sp[len(sp) - 1 - k] for k in range(len(sp))]
+        seg_grads = [[space.grad_view(ps)] for ps in stage_of_seg]
         fwd_bwd = None
+        if opt_overlap:
+            ranges = [space.range_of(ps) for ps in stage_of_seg]
+            tiles = sorted(ranges)
+            if tiles[0][0] != 0 or tiles[-1][1] != space.numel or any(
+                    a[1] != b[0] for a, b in zip(tiles, tiles[1:])):
+                raise ValueError("stage ranges must tile the flat parameter space")
+            seg_opt = [(lambda s=s, e=e: optimizer.step_range(s, e)) for s, e in ranges]
+
+            def opt_finish():
+                optimizer.finish_ranges()
+                if post is not None:
+                    post()
     else:
         def fwd_bwd():
             if pre is not None:
@@ -75,4 +101,5 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     return GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
                             graph_comm=graph_comm, comm_dtype=comm_dtype,
-                            state_tensors=train_state_tensors(model, space, optimizer, extra_state))
+                            state_tensors=train_state_tensors(model, space, optimizer, extra_state),
+                            segment_opt=seg_opt, opt_finish=opt_finish)

@@ -90,6 +90,11 @@ def _widen(lp, v):
         v.reshape(-1).copy_(lp)
 
 
+import os as _os
+
+_DEBUG_FORK = _os.environ.get("KUBEML_DEBUG_FORK", "0") == "1"
+
+
 class _Snapshot:
     def __init__(self, tensors):
         self.tensors = list(tensors)
@@ -125,7 +130,9 @@ class GraphedTrainStep:
     def __init__(self, fwd_bwd: Optional[Callable[[], torch.Tensor]], opt_step: Callable[[], None],
                  grad_buffers=(), group=None, use_graph: bool = True, warmup: int = 1, bucket_mb: float = 0.0,
                  segments=None, segment_grads=None, force_comm: bool = False, graph_comm: bool = True,
-                 state_tensors: Sequence[torch.Tensor] = (), comm_dtype=torch.float32):
+                 state_tensors: Sequence[torch.Tensor] = (), comm_dtype=torch.float32,
+                 segment_opt: Optional[Sequence[Callable[[], None]]] = None,
+                 opt_finish: Optional[Callable[[], None]] = None):
         if segments is None:
             if fwd_bwd is None:
                 raise ValueError("need fwd_bwd or segments")
@@ -152,6 +159,13 @@ class GraphedTrainStep:
         self.comm_dtype = comm_dtype
         self._lp = {}      # fp32 view key -> persistent bf16 communication buffer
         self._pending_widen = []
+        # optimizer overlapped with backward: segment_opt[k] applies the update to segment
+        # k's (final, all-reduced) gradients on a side stream; opt_finish closes the step
+        if segment_opt is not None and (len(segment_opt) != len(self.segments) or opt_finish is None):
+            raise ValueError("segment_opt needs one callable per segment and opt_finish")
+        self.segment_opt = list(segment_opt) if segment_opt is not None else None
+        self.opt_finish = opt_finish
+        self._opt_side = None
         self.g_seg: List[torch.cuda.CUDAGraph] = []
         self.g_all = None
         self.g_opt = None
@@ -207,6 +221,10 @@ class GraphedTrainStep:
         self._pending_widen = []
 
     def _body(self):
+        if self.segment_opt is not None:
+            return self._body_opt_overlap()
+        if _DEBUG_FORK and torch.cuda.is_available():
+            self._debug_fork()
         loss, works = None, []
         for k, seg in enumerate(self.segments):
             out = self._run(seg)
@@ -215,6 +233,50 @@ class GraphedTrainStep:
             works += self._issue(k)
         self._finish_comm(works)
         self.opt_step()
+        return loss
+
+    def _debug_fork(self):
+        """KUBEML_DEBUG_FORK=1: one empty side-stream branch per step (fork + tiny kernel +
+        join) — measures what a multi-stream graph costs by itself."""
+        from ..ops import kernels as K
+        if self._opt_side is None:
+            self._opt_side = torch.cuda.Stream()
+            self._fork_buf = torch.zeros(64, device="cuda")
+        cur = torch.cuda.current_stream()
+        self._opt_side.wait_stream(cur)
+        with torch.cuda.stream(self._opt_side):
+            K.fill_(self._fork_buf, 1.0)
+        cur.wait_stream(self._opt_side)
+
+    def _body_opt_overlap(self):
+        """Per-segment update on a side stream: after segment k's backward (and its
+        all-reduce, which the side stream waits for) the optimizer applies segment k's
+        gradient range while segment k+1's backward runs; the compute stream joins the side
+        stream before the step ends.  Segment k's weights are not read again this step
+        (stage k's backward is complete), so updating them early is exact."""
+        cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+        side = None
+        if cur is not None and any(t.is_cuda for g in self.segment_grads for t in g):
+            if self._opt_side is None:
+                self._opt_side = torch.cuda.Stream()
+            side = self._opt_side
+        loss = None
+        for k, seg in enumerate(self.segments):
+            out = self._run(seg)
+            if k == 0:
+                loss = out
+            works = self._issue(k)
+            if side is None:
+                self._finish_comm(works)
+                self.segment_opt[k]()
+                continue
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._finish_comm(works)      # the side stream waits for this segment's all-reduce
+                self.segment_opt[k]()
+        if side is not None:
+            cur.wait_stream(side)
+        self.opt_finish()
         return loss
 
     def prime_comm(self):
@@ -272,6 +334,7 @@ class GraphedTrainStep:
                 self._pending_widen = []
                 self.graph_comm = False
                 self.graph_comm_fallback = True
+                self.segment_opt = None       # per-segment graphs run the optimizer at the end
         if not captured_all:
             pool = torch.cuda.graph_pool_handle()
             self.g_seg = []

@@ -183,6 +183,69 @@ class SGD(FusedOptimizer):
         return loss
 
 
+    # ---- per-range steps (optimizer overlapped with backward, engine/dp.py) -------------
+    def supports_ranges(self) -> bool:
+        """True when every parameter lives in one flat space (no loose parameters)."""
+        spaces, loose = self._flat_groups()
+        return len(spaces) == 1 and not loose
+
+    @torch.no_grad()
+    def step_range(self, start: int, end: int):
+        """The fused step restricted to flat elements [start, end): the gradients of a
+        finished backward stage are applied while earlier stages still run backward.  The
+        first-step flag stays set until :meth:`finish_ranges` (every range of the step
+        reads the same value); the union of one step's ranges must cover the space once."""
+        g = self.param_groups[0]
+        spaces, loose = self._flat_groups()
+        if len(spaces) != 1 or loose:
+            raise ValueError("step_range needs all parameters in one flat space")
+        sp = spaces[0][0]
+        mom = self._bufs(sp, ["momentum"])["momentum"] if g["momentum"] != 0 else None
+        if sp.device.type != "cuda":
+            _sgd_range_cpu(sp, start, end, g, mom, self._first, self._grad_scale)
+            return
+        from ..ops import kernels as K
+        first = self.first_tensor(sp.device) if mom is not None else None
+        K.sgd_(sp.master[start:end], sp.grad[start:end], None if mom is None else mom[start:end],
+               None if sp.shadow is None else sp.shadow[start:end], g["lr"], wd=g["weight_decay"],
+               momentum=g["momentum"], dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
+               grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first,
+               max_blocks=_RANGE_BLOCKS)
+
+    @torch.no_grad()
+    def finish_ranges(self):
+        """End of a step applied through :meth:`step_range`: clear the first-step flag."""
+        spaces, _ = self._flat_groups()
+        sp = spaces[0][0]
+        if self.param_groups[0]["momentum"] != 0 and sp.device.type == "cuda":
+            from ..ops import kernels as K
+            K.fill_(self.first_tensor(sp.device), 0.0)
+        self._first = False
+
+# grid cap of a range update (it runs beside the backward on a side stream)
+_RANGE_BLOCKS = int(__import__("os").environ.get("KUBEML_OPT_OVERLAP_BLOCKS", "64"))
+
+
+def _sgd_range_cpu(sp, start, end, g, mom, first, grad_scale):
+    """torch form of k_sgd over [start, end) of a CPU flat space (same math as the kernel).
+    Through ``.data``: parameters are views of the flat buffer and share its autograd version
+    counter, which a range update must not bump while other stages' backward still runs."""
+    w, gr = sp.master.data[start:end], sp.grad.data[start:end]
+    d = gr * grad_scale if grad_scale != 1.0 else gr          # op for op as _torch_sgd
+    if g["weight_decay"]:
+        d = d.add(w, alpha=g["weight_decay"])
+    if mom is not None:
+        m = mom.data[start:end]
+        if first:
+            m.copy_(d)
+        else:
+            m.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+        d = d.add(m, alpha=g["momentum"]) if g["nesterov"] else m
+    w.add_(d, alpha=-g["lr"])
+    if sp.shadow is not None:
+        sp.shadow.data[start:end].copy_(w)
+
+
 def _torch_sgd(params, g, state, grad_scale):
     for p in params:
         if p.grad is None:

@@ -135,3 +135,37 @@ def test_bench_rejects_more_gpus_than_visible():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
                        text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 2 and "only 0 GPU" in r.stderr, (r.returncode, r.stderr[-2000:])
+
+
+def _opt_overlap_run(opt_overlap, steps=3):
+    from kubeml_amd.engine.dp import make_train_step
+    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.nn import flatten_module
+    from kubeml_amd.optim import SGD
+    torch.manual_seed(0)
+    m = resnet18(10)
+    m.train()
+    sp = flatten_module(m)
+    opt = SGD(m.parameters(), lr=0.05, momentum=0.9, dampening=0.1, weight_decay=1e-4)
+    x = torch.empty(4, 3, 32, 32)
+    y = torch.empty(4, dtype=torch.int64)
+    g = torch.Generator().manual_seed(5)
+
+    def pre():
+        x.copy_(torch.randn(4, 3, 32, 32, generator=g))
+        y.copy_(torch.randint(0, 10, (4,), generator=g))
+    step = make_train_step(m, sp, opt, torch.nn.functional.cross_entropy, x, y, pre=pre,
+                           opt_overlap=opt_overlap)
+    assert (step.segment_opt is not None) == opt_overlap
+    losses = [float(step()) for _ in range(steps)]
+    return sp.master.clone(), losses
+
+
+def test_optimizer_overlapped_with_backward_matches_one_update():
+    """opt_overlap: the update of each backward stage's parameter range runs as soon as the
+    stage's gradients are final.  Same weights and losses as one optimizer step after the
+    whole backward (momentum + dampening + weight decay, 3 steps)."""
+    wa, la = _opt_overlap_run(True)
+    wb, lb = _opt_overlap_run(False)
+    assert la == pytest.approx(lb, rel=1e-6, abs=1e-6)
+    torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-6)

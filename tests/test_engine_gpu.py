@@ -195,3 +195,51 @@ def test_bench_trace_has_compute_and_comm_tracks(tmp_path):
         ends = seg_end[e["args"]["segment"]]
         assert min(abs(e["ts"] - t) for t in ends) < 1.0   # starts where its segment ended
         assert e["dur"] >= 0
+
+
+def _graphed_run(opt_overlap, steps=3):
+    from kubeml_amd.engine.dp import make_train_step
+    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.optim import SGD
+    torch.manual_seed(0)
+    m = resnet18(10).to(dev)
+    m.train()
+    sp = flatten_module(m)
+    opt = SGD(m.parameters(), lr=1e-3, momentum=0.9, dampening=0.1, weight_decay=1e-4)
+    g = torch.Generator(device=dev).manual_seed(11)
+    xs = torch.randn(steps + 2, 32, 32, 32, 8, device=dev, generator=g).to(torch.bfloat16)
+    xs[..., 3:] = 0
+    ys = torch.randint(0, 10, (steps + 2, 32), device=dev, generator=g)
+    x = torch.empty(32, 32, 32, 8, dtype=torch.bfloat16, device=dev)
+    y = torch.empty(32, dtype=torch.int64, device=dev)
+    i = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def pre():
+        x.copy_(xs.index_select(0, i.view(1)).squeeze(0))
+        y.copy_(ys.index_select(0, i.view(1)).squeeze(0))
+
+    def post():
+        i.add_(1)
+    w0 = sp.master.clone()
+    step = make_train_step(m, sp, opt, cross_entropy, x, y, pre=pre, post=post, opt_overlap=opt_overlap,
+                           extra_state=[i])
+    assert (step.segment_opt is not None) == opt_overlap
+    step.capture()
+    losses = [float(step()) for _ in range(steps)]
+    torch.cuda.synchronize()
+    return sp.master - w0, sp, losses
+
+
+def test_graphed_optimizer_overlap_matches_end_of_step_update():
+    """make_train_step(opt_overlap=True): each backward stage's SGD range runs on a side
+    stream inside the captured step.  Same updates as the single end-of-step SGD (to the
+    split-K atomic-order noise of the weight gradients), shadow = bf16(master)."""
+    ua, spa, la = _graphed_run(True)
+    ub, spb, lb = _graphed_run(False)
+    assert float(ub.abs().max()) > 1e-5
+    rel = float((ua - ub).norm() / ub.norm())
+    assert rel < 1e-2, rel
+    for p, q in zip(la, lb):
+        assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (la, lb)
+    assert torch.equal(spa.shadow, spa.master.to(torch.bfloat16))
