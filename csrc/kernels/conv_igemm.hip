@@ -82,6 +82,9 @@ struct ConvArgs {
   // DGRAD -> consumer-BN backward fusion: partial [sum dz | sum dz*xhat] rows of the BN that
   // consumes this dX (dz = dX * [y > 0], xhat = (c - mean) * rstd), same row layout as stats_part
   const bf16_t* bnf_y; const bf16_t* bnf_c; const float* bnf_mean; const float* bnf_rstd; float* bnf_part;
+  // bnf_mask_out: store dz = dX * [y > 0] (the consumer BN's ReLU mask applied) instead of dX,
+  // so that BN's backward needs no mask and never reads y
+  int bnf_mask_out;
   // Group reduction of the per-wave partial rows (FWD stats_part / DGRAD bnf_part): every
   // grp_tiles consecutive M-tiles form a group; the last-arriving block of a group (agent-scope
   // ticket per (group, n-tile)) sums the group's rows in a fixed order into grp_out[g][2N], so
@@ -498,13 +501,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
             float v = acc[i][j][e] + bv;
             if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
             if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
-            const bf16_t vb = f2bf(v);
-            if (stage) sout[(row - m0) * LDO + (col - n0)] = vb;
-            else a.out[(long long)row * ldc + col] = vb;
+            bf16_t vb = f2bf(v);
             if (MODE == DGRAD && a.bnf_part) {  // consumer BN's dbeta / dgamma partials
               const long long idx = (long long)row * ldc + col;
               float dz = bf2f(vb);
-              if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) dz = 0.f;
+              if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) {
+                dz = 0.f;
+                if (a.bnf_mask_out) vb = 0;
+              }
               const float xh = (bf2f(a.bnf_c[idx]) - a.bnf_mean[bc]) * a.bnf_rstd[bc];
               s1 += dz;
               s2 += dz * xh;
@@ -512,6 +516,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
               s1 += v;
               s2 += v * v;
             }
+            if (stage) sout[(row - m0) * LDO + (col - n0)] = vb;
+            else a.out[(long long)row * ldc + col] = vb;
           }
         }
       if ((MODE == DGRAD && a.bnf_part) || (MODE == FWD && a.stats)) {
@@ -1386,9 +1392,10 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
                const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W, int C, int K,
                int KH, int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, float* slab,
-               unsigned* counters, int fold_c) {
+               unsigned* counters, int fold_c, int bnf_mask_out) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
   if (grp_out && (!bnf_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (bnf_mask_out && !bnf_part) return (int)hipErrorInvalidValue;
   if (fold_c && (grp_out || C % fold_c)) return (int)hipErrorInvalidValue;
   const bool direct = (variant == 3);
   if (!direct && variant) bk = 64;
@@ -1398,6 +1405,7 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
   a.fd_Kp = make_fd(a.Kp);
   a.dy = dy; a.w = w; a.wt = wt; a.out = dx; a.addend = addend; a.zp = zero_page();
   a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
+  a.bnf_mask_out = bnf_mask_out;
   a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
@@ -1442,13 +1450,13 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               float* dw, int B, int H, int W, int C, int K, int KH,
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
-                              int wvariant, int fold_c, int u_k0, int u_c0, hipStream_t s) {
+                              int wvariant, int fold_c, int u_k0, int u_c0, int bnf_mask_out, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
   int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
                      grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
-                     fold_c);
+                     fold_c, bnf_mask_out);
   if (e) return e;
   e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1, u_k0, u_c0);
   if (e) return e;
@@ -1507,11 +1515,12 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
                            const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                            float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W,
                            int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
-                           int splits, int variant, float* slab, unsigned* counters, int fold_c, hipStream_t s) {
+                           int splits, int variant, float* slab, unsigned* counters, int fold_c, int bnf_mask_out,
+                           hipStream_t s) {
   ConvArgs a;
   const int e = prep_dgrad(a, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
                            grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, slab, counters,
-                           fold_c);
+                           fold_c, bnf_mask_out);
   if (e) return e;
   if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
   if (variant) bk = 64;

@@ -209,14 +209,16 @@ class ConvBNUnit:
     @staticmethod
     def backward(dy, saved, conv, bn, want_dres: bool, need_dx: bool, addend=None, partial=None, consumer=None):
         """BN backward -> conv wgrad -> conv dgrad.  ``partial``: this BN's dgamma/dbeta
-        partial rows, already produced by the dgrad that computed ``dy`` (skips the
-        reduction pass).  ``consumer``: saved state (x, c, y, mean, rstd) of the BN that
-        will consume dx — its partial rows are produced here and returned."""
+        partial rows, already produced by the dgrad that computed ``dy`` — that dgrad also
+        applied this BN's ReLU mask (``bnf_mask``), so ``dy`` is already dz: the BN backward
+        skips the reduction pass and never reads y.  ``consumer``: saved state
+        (x, c, y, mean, rstd) of the BN that will consume dx — its partial rows are produced
+        here, its mask applied to dx, and the partials returned."""
         from ..ops import kernels as K
         x, c, y, mean, rstd = saved
         dres = torch.empty_like(dy) if want_dres else None
-        dc = K.bn_bwd(dy, y, c, mean, rstd, master_of(bn.weight), grad_storage_of(bn.weight),
-                      grad_storage_of(bn.bias), dres=dres, partial=partial)
+        dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
+                      grad_storage_of(bn.weight), grad_storage_of(bn.bias), dres=dres, partial=partial)
         kh, kw = conv.kernel_size
         dx, part_out = None, None
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
@@ -230,14 +232,14 @@ class ConvBNUnit:
                                           unroll=wu is not None)[0][4] == K.DIRECT:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
             r = K.conv_bwd(dc, w, x, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding,
-                           addend=addend, bnf=bnf, wt=wt, wu=wu)
+                           addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out
         _wgrad(x, dc, conv, unroll=wu is not None)
         if need_dx:
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
-                             addend=addend, bnf=bnf, wu=wu)
+                             addend=addend, bnf=bnf, wu=wu, bnf_mask=True)
             dx, part_out = r if bnf is not None else (r, None)
         return dx, dres, part_out
 

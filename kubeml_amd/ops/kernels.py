@@ -384,12 +384,14 @@ def _u22_views(B, C, K, dy=None, x=None, addend=None, bnf=None):
 
 
 def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None, wt=None, wu=None,
-               _fold=0):
+               _fold=0, bnf_mask=False):
     """dx = conv input gradient (+ addend, the fused residual-gradient sum).
 
     bnf = (y or None, c, mean, rstd) of the BatchNorm that consumes dx: the epilogue also
     writes that BN's dgamma/dbeta partial rows; returns (dx, (part, G)) for
-    :func:`bn_bwd(partial=...)`.  wu: unrolled weight (:func:`unrolled22`)."""
+    :func:`bn_bwd(partial=...)`.  bnf_mask: return dz = dx * [y > 0] instead (the consumer's
+    ReLU mask applied here, so its bn_bwd runs with y=None and never reads y).
+    wu: unrolled weight (:func:`unrolled22`)."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     if wu is not None:
@@ -397,7 +399,7 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         dy1, _, add1, bnf1 = _u22_views(B, C, K, dy=dy, addend=addend, bnf=bnf)
         o = None if out is None else out.view(B, 1, 1, 4 * C)
         r = conv_dgrad(dy1, wu, (B, 1, 1, 4 * C), 1, 1, (1, 1), (0, 0), out=o, addend=add1, cfg=cfg, bnf=bnf1, wt=wt,
-                       _fold=C)
+                       _fold=C, bnf_mask=bnf_mask)
         if bnf is not None:
             return r[0].view(B, 2, 2, C), r[1]
         return r.view(B, 2, 2, C)
@@ -432,10 +434,10 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         wt = None
         splits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
-    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p i s",
+    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p i i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt),
-             int(_fold), _s())
+             int(_fold), int(bool(bnf_mask) and bnf is not None), _s())
     return (out, (part, G)) if bnf is not None else out
 
 
@@ -512,7 +514,8 @@ def conv_pair_supported(dcfg, wcfg) -> bool:
     return ok
 
 
-def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None):
+def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None,
+             bnf_mask=False):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
     :func:`conv_dgrad`) and ``dw += wgrad``.  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
@@ -520,7 +523,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     a direct-variant dgrad (:func:`weight_transpose_multi`); made here when missing.
     Returns dx, or (dx, (part, G)) when ``bnf`` is given.  wu: unrolled weight
     (:func:`unrolled22`): both GEMMs run in the dense 1x1 form, the weight gradient
-    scatter-adds back onto the 3x3 taps of ``dw``."""
+    scatter-adds back onto the 3x3 taps of ``dw``.  bnf_mask: as in :func:`conv_dgrad`."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -550,7 +553,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
     if not grouped:
         conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, _u=u)
-        r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold)
+        r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
+                       bnf_mask=bnf_mask)
         if not fold:
             return r
         if bnf is not None:
@@ -572,10 +576,11 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
-             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold), u[0], u[1], _s())
+             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold), u[0], u[1],
+             int(bool(bnf_mask) and bnf is not None), _s())
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out

@@ -405,6 +405,19 @@ def test_dgrad_emits_consumer_bn_partials(cfg):
     r1 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg1, db1, partial=partial)
     assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
     assert _rel(r1, r0) < 1e-2
+    # bnf_mask: the dgrad writes dz = dX * [y > 0] itself; the BN backward then runs without
+    # y (no mask, y never read) and gives the same dx / dres / dgamma / dbeta
+    dz, partial2 = K.conv_dgrad(dy, w, (B, H, W, Ci), 3, 3, (1, 1), (1, 1), addend=add, cfg=cfg,
+                                bnf=(ybn, c, mean, rstd), bnf_mask=True)
+    assert torch.equal(dz, torch.where(ybn > 0, dx1, torch.zeros_like(dx1)))
+    assert torch.equal(partial2[0], partial[0])
+    dg2, db2 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    res1, res2 = torch.empty_like(dx1), torch.empty_like(dx1)
+    dg3, db3 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+    r3 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg3, db3, dres=res1, partial=partial)
+    r2 = K.bn_bwd(dz, None, c, mean, rstd, g, dg2, db2, dres=res2, partial=partial2)
+    assert torch.equal(r2, r3) and torch.equal(res2, res1)
+    assert torch.equal(dg2, dg3) and torch.equal(db2, db3)
 
 
 PAIR_PLANS = [  # (dgrad plan, wgrad plan) pairs with a grouped kernel
