@@ -37,11 +37,14 @@ namespace {
 
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
 
+constexpr int GEMM_ADD_C2 = 3;  // act code: C = bf16(bf16(A B) + c2)
+
 struct GemmArgs {
   const bf16_t* a;
   const bf16_t* b;
   void* c;
-  bf16_t* c2;          // optional pre-activation copy (bf16 out only)
+  bf16_t* c2;          // optional pre-activation copy (bf16 out only); with act == GEMM_ADD_C2 a
+                       // bf16 addend summed into the output (fused residual-gradient sum)
   const float* bias;   // [N] fp32 or null
   const bf16_t* zp;    // >= 16 zero bytes
   long long lda, ldb, ldc;
@@ -167,7 +170,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[
           v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
         }
         const long long off = (long long)m * g.ldc + n;
-        if (g.c2) {
+        if (g.act == GEMM_ADD_C2) {  // + bf16 addend: round, add, round (= a separate bf16 add)
+          const uint2 ad = *reinterpret_cast<const uint2*>(g.c2 + off);
+          const uint2 q = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+          v[0] = lo_bf(q.x) + lo_bf(ad.x); v[1] = hi_bf(q.x) + hi_bf(ad.x);
+          v[2] = lo_bf(q.y) + lo_bf(ad.y); v[3] = hi_bf(q.y) + hi_bf(ad.y);
+        } else if (g.c2) {
           uint2 p;
           p.x = pack_bf2(v[0], v[1]);
           p.y = pack_bf2(v[2], v[3]);
@@ -653,13 +661,22 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       for (int it = 0; it < 16; ++it) {
         const int idx = it * NT + tid;
         const int row = idx >> 5, ch = idx & 31;
-        const uint4 v = *reinterpret_cast<const uint4*>(smem + row * 512 + ((ch ^ (row & 15)) << 4));
+        uint4 v = *reinterpret_cast<const uint4*>(smem + row * 512 + ((ch ^ (row & 15)) << 4));
         const int m = m0 + row, n = n0 + ch * 8;
-        if (m < g.M && n < g.N) *reinterpret_cast<uint4*>(dst + (long long)m * g.ldc + n) = v;
+        if (m < g.M && n < g.N) {
+          if (g.act == GEMM_ADD_C2) {  // + bf16 addend (the staged tile is already bf16-rounded)
+            const uint4 ad = *reinterpret_cast<const uint4*>(g.c2 + (long long)m * g.ldc + n);
+            v.x = pack_bf2(lo_bf(v.x) + lo_bf(ad.x), hi_bf(v.x) + hi_bf(ad.x));
+            v.y = pack_bf2(lo_bf(v.y) + lo_bf(ad.y), hi_bf(v.y) + hi_bf(ad.y));
+            v.z = pack_bf2(lo_bf(v.z) + lo_bf(ad.z), hi_bf(v.z) + hi_bf(ad.z));
+            v.w = pack_bf2(lo_bf(v.w) + lo_bf(ad.w), hi_bf(v.w) + hi_bf(ad.w));
+          }
+          *reinterpret_cast<uint4*>(dst + (long long)m * g.ldc + n) = v;
+        }
       }
       __syncthreads();
     };
-    if (g.c2) {   // pre-activation copy first: the accumulators stay live across it
+    if (g.c2 && g.act != GEMM_ADD_C2) {   // pre-activation copy first: the accumulators stay live across it
       stage(false);
       store(g.c2);
     }

@@ -45,6 +45,10 @@ class BertLayer(tnn.Module):
         self.act = GELU()
         self.drop1 = Dropout(dropout, rng)
         self.drop2 = Dropout(dropout, rng)
+        # each LayerNorm's residual input also feeds a Linear (h -> qkv, h1 -> FFN1): its
+        # residual gradient is summed in that Linear's dgrad epilogue (nn/transformer.py)
+        object.__setattr__(self.attention.ln, "_kml_res_linear", self.attention.qkv)
+        object.__setattr__(self.output.LayerNorm, "_kml_res_linear", self.intermediate.dense)
 
     def forward(self, h, B: int, L: int, bias=None):
         a = self.drop1(self.attention(h, B, L, bias))

@@ -217,11 +217,21 @@ class _LinearFn(Function):
         x4 = ctx.x.view(B, 1, 1, ip)
         dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
         dx = None
+        # residual gradient handed over by a LayerNorm that shares this Linear's input
+        # (nn/transformer.py): summed into dx here instead of by an autograd add
+        stash = getattr(mod, "_kml_res_grad", None)
+        addend = None
+        if stash is not None:
+            object.__setattr__(mod, "_kml_res_grad", None)
+            if stash[0] != ctx.x.data_ptr():
+                raise RuntimeError("residual-gradient hand-off: the LayerNorm residual is not this Linear's input")
+            addend = stash[1]
         if ctx.route == "gemm":
             from ..ops import gemm as G
             w2 = shadow_of(mod.weight).view(op, ip)
             if ctx.needs_input_grad[0]:
-                dx = G.linear_dgrad(dy, w2)
+                dx = G.linear_dgrad(dy, w2, addend=addend)
+                addend = None
             G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x)
         elif ctx.route == "blas":
             if ctx.needs_input_grad[0]:
@@ -235,6 +245,8 @@ class _LinearFn(Function):
             K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
         if ctx.has_bias:
             K.colsum_(dy, grad_storage_of(mod.bias))
+        if addend is not None and dx is not None:
+            dx = K.add_bf16(dx, addend)
         ctx.x = ctx.y = ctx.pre = None
         return dx, None, None, None, None, None
 

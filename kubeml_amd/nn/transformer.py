@@ -27,6 +27,11 @@ def _bf(x):
     return x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
 
 
+# KUBEML_RES_FUSE=0: residual gradients summed by autograd (a separate add) instead of the
+# consuming Linear's dgrad epilogue
+_RES_FUSE = __import__("os").environ.get("KUBEML_RES_FUSE", "1") != "0"
+
+
 # ====================================================================================== LayerNorm
 class _LNFn(Function):
     @staticmethod
@@ -36,6 +41,7 @@ class _LNFn(Function):
         ctx.save = (xin, mean, rstd)
         ctx.mod = mod
         ctx.has_res = res is not None
+        ctx.res_ptr = res.data_ptr() if res is not None else None
         return y
 
     @staticmethod
@@ -46,7 +52,14 @@ class _LNFn(Function):
         dx = T.ln_bwd(_bf(dy).contiguous(), xin, mean, rstd, master_of(mod.weight), grad_storage_of(mod.weight),
                       grad_storage_of(mod.bias))
         ctx.save = None
-        return dx, None, None, None, (dx if ctx.has_res else None)
+        dres = dx if ctx.has_res else None
+        lin = getattr(mod, "_kml_res_linear", None)
+        if dres is not None and lin is not None and _RES_FUSE:
+            # the residual also feeds ``lin`` (whose backward runs next on this path): hand it
+            # this gradient so its dgrad GEMM adds it in the epilogue (no separate add kernel)
+            object.__setattr__(lin, "_kml_res_grad", (ctx.res_ptr, dres))
+            dres = None
+        return dx, None, None, None, dres
 
 
 class LayerNorm(tnn.LayerNorm):

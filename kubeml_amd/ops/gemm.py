@@ -30,6 +30,9 @@ if os.path.exists(_TUNE_FILE) and os.environ.get("KUBEML_GEMM_TUNING", "1") != "
 _ZP = {}
 
 
+ADD_C2 = 3  # kml_gemm act code: bf16 output = bf16(bf16(A B) + c2)
+
+
 def _zp(dev):
     z = _ZP.get(dev)
     if z is None:
@@ -144,14 +147,18 @@ def linear_fwd(x, w, bias=None, act=0, pre=None):
     return y
 
 
-def linear_dgrad(dy, w):
-    """dx[T, ip] = dy[T, op] @ w[op, ip].  Few output tiles with a long reduction (the MLM
+def linear_dgrad(dy, w, addend=None):
+    """dx[T, ip] = dy[T, op] @ w[op, ip] (+ addend, a bf16 [T, ip] gradient summed in the
+    epilogue exactly as a separate bf16 add would: the residual-gradient sum of a
+    transformer layer, nn/transformer.py).  Few output tiles with a long reduction (the MLM
     decoder: 2432 x 768 out, K = 30528) split K over fp32 atomics into a scratch tile,
     then one bf16 conversion pass."""
     T, op = dy.shape
     ip = w.shape[1]
     if w.shape[0] != op:
         raise ValueError(f"linear_dgrad: dy {tuple(dy.shape)} vs w {tuple(w.shape)}")
+    if addend is not None and (tuple(addend.shape) != (T, ip) or not addend.is_contiguous()):
+        raise ValueError("linear_dgrad: addend must be a contiguous [T, ip] tensor")
     dx = torch.empty((T, ip), dtype=BF16, device=dy.device)
     tile, splits = plan(1, T, ip, op)
     if splits > 1:
@@ -160,8 +167,11 @@ def linear_dgrad(dy, w):
         KK.memset_(acc)
         gemm(dy, op, w, ip, acc, ip, T, ip, op, 1, 2, tile=tile, splits=splits)
         KK.f32_to_bf16(acc, dx)
+        if addend is not None:
+            KK.add_bf16(dx, addend, out=dx)
         return dx
-    gemm(dy, op, w, ip, dx, ip, T, ip, op, 1, 0, tile=tile, splits=1)
+    gemm(dy, op, w, ip, dx, ip, T, ip, op, 1, 0, tile=tile, splits=1, c2=addend,
+         act=ADD_C2 if addend is not None else 0)
     return dx
 
 

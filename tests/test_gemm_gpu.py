@@ -132,3 +132,36 @@ def test_linear_helpers_match_torch():
     assert _rel(dw, dy.double().t() @ x.double()) < 1e-4
     with pytest.raises(ValueError):
         G.linear_fwd(x, w[:, :700])
+
+
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128),
+                                  (128, 128, 2)])
+@pytest.mark.parametrize("T,ip,op", [(512, 768, 2304), (200, 72, 136)])
+def test_dgrad_plus_addend_equals_separate_add(tile, T, ip, op):
+    """act=ADD_C2 (the transformer's residual-gradient sum fused into the dgrad epilogue):
+    bit-identical to the plain dgrad followed by a bf16 add."""
+    from kubeml_amd.ops import gemm as G
+    torch.manual_seed(3)
+    dy, w = _rand(T, op), _rand(op, ip, scale=0.05)
+    add = _rand(T, ip)
+    dx = torch.empty(T, ip, dtype=torch.bfloat16, device=dev)
+    G.gemm(dy, op, w, ip, dx, ip, T, ip, op, 1, 0, tile=tile, splits=1)
+    dx2 = torch.empty_like(dx)
+    G.gemm(dy, op, w, ip, dx2, ip, T, ip, op, 1, 0, tile=tile, splits=1, c2=add, act=G.ADD_C2)
+    torch.testing.assert_close(dx2, (dx.float() + add.float()).to(torch.bfloat16), rtol=0, atol=0)
+
+
+def test_linear_dgrad_addend_paths():
+    """linear_dgrad(addend=...) on the direct and the split-K (fp32 scratch) routes."""
+    from kubeml_amd.ops import gemm as G
+    torch.manual_seed(4)
+    for T, ip, op in [(1024, 768, 3072), (2432, 768, 30528)]:
+        dy, w = _rand(T, op), _rand(op, ip, scale=0.02)
+        add = _rand(T, ip)
+        ref = G.linear_dgrad(dy, w)
+        out = G.linear_dgrad(dy, w, addend=add)
+        want = (ref.float() + add.float()).to(torch.bfloat16)
+        if G.plan(1, T, ip, op)[1] == 1:
+            torch.testing.assert_close(out, want, rtol=0, atol=0)
+        else:   # fp32 split-K atomics: summation order differs run to run
+            assert _rel(out, want) < 1e-2
