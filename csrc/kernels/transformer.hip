@@ -23,13 +23,39 @@ __device__ __forceinline__ void st4(bf16_t* p, const float* f) {
 
 constexpr int MAXV = 8;  // up to 8 x (64 lanes x 4) = 2048 columns held in registers
 
+__device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
+  unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+// dropout of 4 consecutive elements starting at flat (even) index e, bit-identical to
+// k_dropout: element pair j = e / 2 keeps its low / high element when the matching 16-bit
+// half of hash(seed ^ salt, step, j) >= p * 2^16; kept values are bf16(x / (1 - p))
+__device__ __forceinline__ void drop4(float* v, long long e, const float* ctr, unsigned salt, float p) {
+  const unsigned seed = (unsigned)ctr[0], step = (unsigned)ctr[1];
+  const unsigned thr = (unsigned)(p * 65536.0f);
+  const float sc = 1.f / (1.f - p);
+  const unsigned j = (unsigned)(e >> 1);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const unsigned h = hash3(seed ^ salt, step, j + q);
+    const float a = (h & 0xFFFFu) >= thr ? v[2 * q] * sc : 0.f;
+    const float b = (h >> 16) >= thr ? v[2 * q + 1] * sc : 0.f;
+    const unsigned pk = pack_bf2(a, b);
+    v[2 * q] = lo_bf(pk);
+    v[2 * q + 1] = hi_bf(pk);
+  }
+}
+
 // ------------------------------------------------------------------------------ LayerNorm fwd
 // y = LN(x [+ res]) * g + b ; sum_out (optional) = x + res (the LN input, kept for backward)
 __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 bf16_t* __restrict__ y, bf16_t* __restrict__ sum_out,
                                                 float* __restrict__ mean, float* __restrict__ rstd, long long M,
-                                                int N, float eps) {
+                                                int N, float eps, const float* __restrict__ dctr, unsigned dsalt,
+                                                float dp) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -42,6 +68,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, co
     const int c = (u * 64 + lane) * 4;
     if (u < nv && c < N) {
       ld4(xr + c, v[u]);
+      if (dctr) drop4(v[u], row * N + c, dctr, dsalt, dp);  // x = dropout(x), as k_dropout
       if (res) {
         float r[4];
         ld4(res + row * N + c, r);
@@ -85,7 +112,8 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 const float* __restrict__ gamma, bf16_t* __restrict__ dx,
                                                 const bf16_t* __restrict__ dx_add, float* __restrict__ part,
-                                                long long M, int N, int rows_per_block) {
+                                                long long M, int N, int rows_per_block, bf16_t* __restrict__ dx_drop,
+                                                const float* __restrict__ dctr, unsigned dsalt, float dp) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nv = N / 256 + ((N % 256) > 0);
   float pg[MAXV][4], pb[MAXV][4];
@@ -133,6 +161,13 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
           for (int k = 0; k < 4; ++k) o[k] += e[k];
         }
         st4(dx + row * N + c, o);
+        if (dx_drop) {  // gradient through the fused forward dropout: dropout(bf16(dx)), as k_dropout
+          float od[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) od[k] = bf2f(f2bf(o[k]));
+          drop4(od, row * N + c, dctr, dsalt, dp);
+          st4(dx_drop + row * N + c, od);
+        }
       }
     }
   }
@@ -197,12 +232,6 @@ __global__ void k_gelu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restri
 }
 
 // ------------------------------------------------------------------------------ dropout
-__device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
-  unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
-  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
-  return h;
-}
-
 // y = x * keep / (1 - p); ctr = [seed, step].  One hash per element PAIR j (elements 2j,
 // 2j+1): keep = 16-bit half of hash(seed ^ salt, step, j) >= p * 2^16.  8 elements (16 B)
 // per thread per iteration, 4 hashes.
@@ -336,11 +365,15 @@ int ln_bwd_blocks(long long M, int* rpb) {
 
 }  // namespace
 
+// dctr (optional): dropout (ctr = [seed, step], salt, p; k_dropout's mask) applied to x as it
+// is loaded — LN(dropout(x) + res) in one pass; sum_out then holds dropout(x) + res
 KML_API int kml_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y,
-                       bf16_t* sum_out, float* mean, float* rstd, long long M, int N, float eps, hipStream_t s) {
+                       bf16_t* sum_out, float* mean, float* rstd, long long M, int N, float eps, const float* dctr,
+                       unsigned dsalt, float dp, hipStream_t s) {
   if (N % 4 || N > 64 * 4 * MAXV) return (int)hipErrorInvalidValue;
+  if (dctr && (dp < 0.f || dp >= 1.f)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_ln_fwd, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, res, gamma, beta, y, sum_out, mean,
-                     rstd, M, N, eps);
+                     rstd, M, N, eps, dctr, dsalt, dp);
   KML_LAUNCH_CHECK();
 }
 
@@ -349,14 +382,19 @@ KML_API long long kml_ln_bwd_ws_floats(long long M, int N) {
   return (long long)ln_bwd_blocks(M, &rpb) * 2 * N;
 }
 
+// dx_drop (optional, with dctr/dsalt/dp of the fused forward dropout): also the gradient of
+// the pre-dropout input, dropout(dx) — one pass instead of LN backward + dropout backward
 KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, const float* rstd, const float* gamma,
                        bf16_t* dx, const bf16_t* dx_add, float* dgamma, float* dbeta, float* ws, unsigned* counter,
-                       long long M, int N, hipStream_t s) {
+                       long long M, int N, bf16_t* dx_drop, const float* dctr, unsigned dsalt, float dp,
+                       hipStream_t s) {
   if (N % 4 || N > 2048) return (int)hipErrorInvalidValue;
+  if (dx_drop && (!dctr || dp < 0.f || dp >= 1.f)) return (int)hipErrorInvalidValue;
   int rpb;
   const int g = ln_bwd_blocks(M, &rpb);
   (void)counter;
-  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, rpb);
+  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, rpb,
+                     dx_drop, dctr, dsalt, dp);
   hipLaunchKernelGGL(k_colreduce, dim3((2 * N + 63) / 64), dim3(256), 0, s, ws, g, 2 * N, N, dgamma, dbeta);
   KML_LAUNCH_CHECK();
 }

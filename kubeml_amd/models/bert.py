@@ -51,11 +51,10 @@ class BertLayer(tnn.Module):
         object.__setattr__(self.output.LayerNorm, "_kml_res_linear", self.intermediate.dense)
 
     def forward(self, h, B: int, L: int, bias=None):
-        a = self.drop1(self.attention(h, B, L, bias))
-        h1 = self.attention.ln(a, residual=h)
+        # hidden dropout runs inside the LayerNorm kernels (LN(dropout(a) + h))
+        h1 = self.attention.ln(self.attention(h, B, L, bias), residual=h, dropout=self.drop1)
         i = self.intermediate.dense(h1, act="gelu")   # erf-GELU in the GEMM epilogue
-        o = self.drop2(self.output.dense(i))
-        return self.output.LayerNorm(o, residual=h1)
+        return self.output.LayerNorm(self.output.dense(i), residual=h1, dropout=self.drop2)
 
 
 class BertEncoder(tnn.Module):

@@ -35,13 +35,14 @@ _RES_FUSE = __import__("os").environ.get("KUBEML_RES_FUSE", "1") != "0"
 # ====================================================================================== LayerNorm
 class _LNFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, mod, res):
+    def forward(ctx, x, weight, bias, mod, res, drop=None):
         from ..ops import transformer as T
-        y, xin, mean, rstd = T.ln_fwd(x, master_of(weight), master_of(bias), res=res, eps=mod.eps)
+        y, xin, mean, rstd = T.ln_fwd(x, master_of(weight), master_of(bias), res=res, eps=mod.eps, drop=drop)
         ctx.save = (xin, mean, rstd)
         ctx.mod = mod
         ctx.has_res = res is not None
         ctx.res_ptr = res.data_ptr() if res is not None else None
+        ctx.drop = drop
         return y
 
     @staticmethod
@@ -49,9 +50,10 @@ class _LNFn(Function):
         from ..ops import transformer as T
         xin, mean, rstd = ctx.save
         mod = ctx.mod
-        dx = T.ln_bwd(_bf(dy).contiguous(), xin, mean, rstd, master_of(mod.weight), grad_storage_of(mod.weight),
-                      grad_storage_of(mod.bias))
-        ctx.save = None
+        r = T.ln_bwd(_bf(dy).contiguous(), xin, mean, rstd, master_of(mod.weight), grad_storage_of(mod.weight),
+                     grad_storage_of(mod.bias), drop=ctx.drop)
+        dx, dxin = r if ctx.drop is not None else (r, r)   # dxin: gradient of the (pre-dropout) input
+        ctx.save = ctx.drop = None
         dres = dx if ctx.has_res else None
         lin = getattr(mod, "_kml_res_linear", None)
         if dres is not None and lin is not None and _RES_FUSE:
@@ -59,13 +61,22 @@ class _LNFn(Function):
             # this gradient so its dgrad GEMM adds it in the epilogue (no separate add kernel)
             object.__setattr__(lin, "_kml_res_grad", (ctx.res_ptr, dres))
             dres = None
-        return dx, None, None, None, dres
+        return dxin, None, None, None, dres, None
 
 
 class LayerNorm(tnn.LayerNorm):
-    """LayerNorm over the last dim; ``forward(x, residual)`` normalises ``x + residual``."""
+    """LayerNorm over the last dim; ``forward(x, residual, dropout)`` normalises
+    ``dropout(x) + residual``.  On the GPU in training the dropout runs inside the LayerNorm
+    kernels (same counter-hash mask as :class:`Dropout`): no separate dropout pass forward
+    or backward (``KUBEML_LN_DROP_FUSE=0`` keeps it separate)."""
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, dropout=None):
+        drop = None
+        if dropout is not None and dropout.training and dropout.p > 0.0:
+            if x.is_cuda and _LN_DROP_FUSE:
+                drop = (dropout.rng.tensor(x.device), dropout.salt, dropout.p)
+            else:
+                x = dropout(x)
         if not x.is_cuda:
             if residual is not None:
                 x = x + residual
@@ -73,10 +84,12 @@ class LayerNorm(tnn.LayerNorm):
         shp = x.shape
         x2 = _bf(x).reshape(-1, shp[-1]).contiguous()
         r2 = None if residual is None else _bf(residual).reshape(-1, shp[-1]).contiguous()
-        return _LNFn.apply(x2, self.weight, self.bias, self, r2).view(shp)
+        return _LNFn.apply(x2, self.weight, self.bias, self, r2, drop).view(shp)
 
 
-# ====================================================================================== GELU / dropout
+_LN_DROP_FUSE = __import__("os").environ.get("KUBEML_LN_DROP_FUSE", "1") != "0"
+
+
 class _GELUFn(Function):
     @staticmethod
     def forward(ctx, x):

@@ -84,33 +84,41 @@ def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=Non
     return dq, dk, dv
 
 
-def ln_fwd(x, gamma, beta, res=None, eps=1e-12, keep_sum=True):
+def ln_fwd(x, gamma, beta, res=None, eps=1e-12, keep_sum=True, drop=None):
     """LayerNorm over the last dim of a [T, N] bf16 tensor (optionally of x + res).
-    Returns (y, ln_input, mean, rstd) — ln_input is x + res (or x)."""
+    Returns (y, ln_input, mean, rstd) — ln_input is x + res (or x).  drop = (ctr, salt, p):
+    x goes through :func:`dropout` (same mask) as it is loaded — LN(dropout(x) + res) in one
+    pass; ln_input is then dropout(x) + res."""
     _chk(x, BF16, "x")
     N = x.shape[-1]
     M = x.numel() // N
     y = torch.empty_like(x)
-    s = torch.empty_like(x) if (res is not None and keep_sum) else None
+    s = torch.empty_like(x) if ((res is not None or drop is not None) and keep_sum) else None
     mean = torch.empty(M, dtype=F32, device=x.device)
     rstd = torch.empty(M, dtype=F32, device=x.device)
-    HIP.call("kml_ln_fwd", "p p p p p p p p l i f s", _p(x), _p(res), _p(gamma), _p(beta), _p(y), _p(s), _p(mean),
-             _p(rstd), M, N, float(eps), _s())
+    ctr, salt, p = drop if drop is not None else (None, 0, 0.0)
+    HIP.call("kml_ln_fwd", "p p p p p p p p l i f p i f s", _p(x), _p(res), _p(gamma), _p(beta), _p(y), _p(s),
+             _p(mean), _p(rstd), M, N, float(eps), _p(ctr), int(salt) & 0x7FFFFFFF, float(p), _s())
     return y, (s if s is not None else x), mean, rstd
 
 
-def ln_bwd(dy, xin, mean, rstd, gamma, dgamma, dbeta, dx_add=None):
-    """dx (+ dx_add) ; dgamma/dbeta += (deterministic two-level reduce)."""
+def ln_bwd(dy, xin, mean, rstd, gamma, dgamma, dbeta, dx_add=None, drop=None):
+    """dx (+ dx_add) ; dgamma/dbeta += (deterministic two-level reduce).  drop = (ctr, salt,
+    p) of a forward :func:`ln_fwd` dropout: returns (dx, dropout(dx)) — the gradients of the
+    residual input and of the pre-dropout input — from one pass."""
     _chk(dy, BF16, "dy")
     N = dy.shape[-1]
     M = dy.numel() // N
     dx = torch.empty_like(dy)
+    dxd = torch.empty_like(dy) if drop is not None else None
+    ctr, salt, p = drop if drop is not None else (None, 0, 0.0)
     nws = HIP.raw("kml_ln_bwd_ws_floats", M, N)
     ws = torch.empty(nws, dtype=F32, device=dy.device)
     cnt = _COUNTERS.take(dy.device, 1)
-    HIP.call("kml_ln_bwd", "p p p p p p p p p p p l i s", _p(dy), _p(xin), _p(mean), _p(rstd), _p(gamma), _p(dx),
-             _p(dx_add), _p(dgamma), _p(dbeta), _p(ws), _p(cnt), M, N, _s())
-    return dx
+    HIP.call("kml_ln_bwd", "p p p p p p p p p p p l i p p i f s", _p(dy), _p(xin), _p(mean), _p(rstd), _p(gamma),
+             _p(dx), _p(dx_add), _p(dgamma), _p(dbeta), _p(ws), _p(cnt), M, N, _p(dxd), _p(ctr),
+             int(salt) & 0x7FFFFFFF, float(p), _s())
+    return (dx, dxd) if drop is not None else dx
 
 
 def gelu_fwd(x):

@@ -178,3 +178,44 @@ def test_attention_dropout_matches_masked_reference(L):
     rel = lambda a, b: float((a.float().cpu() - b).norm() / b.norm())
     assert rel(out.detach(), ref.detach()) < 2e-2
     assert rel(x.grad, xr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("N,res", [(768, True), (1024, False)])
+def test_layernorm_fused_dropout_matches_separate(N, res):
+    """LayerNorm(x, residual, dropout=...) with the dropout inside the LN kernels: output
+    and the gradients of x (through the mask) and of the residual are bit-identical to a
+    separate Dropout followed by the LayerNorm (same counter-hash mask)."""
+    from kubeml_amd.nn import transformer as TR
+    from kubeml_amd.nn.flat import flatten_module
+    torch.manual_seed(2)
+    out = []
+    old = TR._LN_DROP_FUSE
+    try:
+        for fuse in (False, True):
+            TR._LN_DROP_FUSE = fuse
+            torch.manual_seed(3)
+            ln = TR.LayerNorm(N, eps=1e-12).to(dev)
+            with torch.no_grad():
+                ln.weight.uniform_(0.5, 1.5)
+                ln.bias.uniform_(-0.2, 0.2)
+            flatten_module(ln)
+            drop = TR.Dropout(0.1, TR.RNGState(seed=5)).to(dev)
+            drop.salt = 1234
+            drop.train()
+            g = torch.Generator(device=dev).manual_seed(9)
+            x = torch.randn(300, N, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+            r = torch.randn(300, N, device=dev, generator=g).to(torch.bfloat16).requires_grad_() if res else None
+            y = ln(x, residual=r, dropout=drop)
+            dy = torch.randn(300, N, device=dev, generator=g).to(torch.bfloat16)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            out.append((y.detach().clone(), x.grad.clone(), None if r is None else r.grad.clone()))
+    finally:
+        TR._LN_DROP_FUSE = old
+    (ya, gxa, gra), (yb, gxb, grb) = out
+    torch.testing.assert_close(yb, ya, rtol=0, atol=0)
+    torch.testing.assert_close(gxb, gxa, rtol=0, atol=0)
+    if res:
+        torch.testing.assert_close(grb, gra, rtol=0, atol=0)
+    # the mask really dropped ~p of the elements
+    assert 0.05 < float((gxb == 0).float().mean()) < 0.15
