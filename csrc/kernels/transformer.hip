@@ -113,14 +113,15 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
                                                 const float* __restrict__ gamma, bf16_t* __restrict__ dx,
                                                 const bf16_t* __restrict__ dx_add, float* __restrict__ part,
                                                 long long M, int N, int rows_per_block, bf16_t* __restrict__ dx_drop,
-                                                const float* __restrict__ dctr, unsigned dsalt, float dp) {
+                                                const float* __restrict__ dctr, unsigned dsalt, float dp,
+                                                int with_in) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nv = N / 256 + ((N % 256) > 0);
-  float pg[MAXV][4], pb[MAXV][4];
+  float pg[MAXV][4], pb[MAXV][4], pi[MAXV][4];  // pi: column sums of the input gradient (part_in)
 #pragma unroll
   for (int u = 0; u < MAXV; ++u)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { pg[u][k] = 0.f; pb[u][k] = 0.f; }
+    for (int k = 0; k < 4; ++k) { pg[u][k] = 0.f; pb[u][k] = 0.f; pi[u][k] = 0.f; }
   const long long r0 = (long long)blockIdx.x * rows_per_block;
   const long long r1 = min(M, r0 + rows_per_block);
   for (long long row = r0 + wv; row < r1; row += 4) {
@@ -161,12 +162,16 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
           for (int k = 0; k < 4; ++k) o[k] += e[k];
         }
         st4(dx + row * N + c, o);
-        if (dx_drop) {  // gradient through the fused forward dropout: dropout(bf16(dx)), as k_dropout
-          float od[4];
+        float od[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) od[k] = bf2f(f2bf(o[k]));
+        for (int k = 0; k < 4; ++k) od[k] = bf2f(f2bf(o[k]));
+        if (dx_drop) {  // gradient through the fused forward dropout: dropout(bf16(dx)), as k_dropout
           drop4(od, row * N + c, dctr, dsalt, dp);
           st4(dx_drop + row * N + c, od);
+        }
+        if (with_in) {  // bias gradient of the Linear that produced the LN input
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pi[u][k] += od[k];
         }
       }
     }
@@ -181,13 +186,29 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
       for (int k = 0; k < 4; ++k) { red[wv][c + k] = pg[u][k]; red[wv][N + c + k] = pb[u][k]; }
   }
   __syncthreads();
-  float* mine = part + (long long)blockIdx.x * 2 * N;
+  // one partial row per block: [dgamma(N) | dbeta(N) (| input-gradient column sums(N))]
+  float* mine = part + (long long)blockIdx.x * (with_in ? 3 : 2) * N;
   for (int c = threadIdx.x; c < 2 * N; c += 256) mine[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  if (with_in) {  // third segment, through the same LDS (uniform branch)
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MAXV; ++u) {
+      const int c = (u * 64 + lane) * 4;
+      if (u < nv && c < N)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) red[wv][c + k] = pi[u][k];
+    }
+    __syncthreads();
+    float* mi = mine + 2 * N;
+    for (int c = threadIdx.x; c < N; c += 256) mi[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  }
 }
 
-// column sums of part[G][W] in row order (deterministic): out_a[c] += sum (c < Na), out_b[c - Na] += sum
+// column sums of part[G][W] in row order (deterministic): out_a[c] += sum (c < Na),
+// out_b[c - Na] += sum (c < Na + Nb), out_c[c - Na - Nb] += sum (the rest)
 __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ part, int G, int W, int Na,
-                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
+                                                   float* __restrict__ out_a, float* __restrict__ out_b,
+                                                   int Nb = 0x7fffffff, float* __restrict__ out_c = nullptr) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + tx;
   float acc = 0.f;
@@ -201,7 +222,8 @@ __global__ __launch_bounds__(256) void k_colreduce(const float* __restrict__ par
   if (ty == 0 && col < W) {
     const float t = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
     if (col < Na) out_a[col] += t;
-    else out_b[col - Na] += t;
+    else if (col - Na < Nb) out_b[col - Na] += t;
+    else out_c[col - Na - Nb] += t;
   }
 }
 
@@ -377,9 +399,10 @@ KML_API int kml_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, c
   KML_LAUNCH_CHECK();
 }
 
+// workspace floats of kml_ln_bwd: [g][2N] gamma/beta partials (+ [g][N] with dbias_in)
 KML_API long long kml_ln_bwd_ws_floats(long long M, int N) {
   int rpb;
-  return (long long)ln_bwd_blocks(M, &rpb) * 2 * N;
+  return (long long)ln_bwd_blocks(M, &rpb) * 3 * N;
 }
 
 // dx_drop (optional, with dctr/dsalt/dp of the fused forward dropout): also the gradient of
@@ -387,15 +410,19 @@ KML_API long long kml_ln_bwd_ws_floats(long long M, int N) {
 KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, const float* rstd, const float* gamma,
                        bf16_t* dx, const bf16_t* dx_add, float* dgamma, float* dbeta, float* ws, unsigned* counter,
                        long long M, int N, bf16_t* dx_drop, const float* dctr, unsigned dsalt, float dp,
-                       hipStream_t s) {
+                       float* dbias_in, hipStream_t s) {
   if (N % 4 || N > 2048) return (int)hipErrorInvalidValue;
   if (dx_drop && (!dctr || dp < 0.f || dp >= 1.f)) return (int)hipErrorInvalidValue;
   int rpb;
   const int g = ln_bwd_blocks(M, &rpb);
   (void)counter;
+  // dbias_in (optional): += column sums of the input gradient (dx_drop, else dx) — the bias
+  // gradient of the Linear feeding this LayerNorm; partials in ws after the [g][2N] block
+  const int with_in = dbias_in ? 1 : 0;
   hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, rpb,
-                     dx_drop, dctr, dsalt, dp);
-  hipLaunchKernelGGL(k_colreduce, dim3((2 * N + 63) / 64), dim3(256), 0, s, ws, g, 2 * N, N, dgamma, dbeta);
+                     dx_drop, dctr, dsalt, dp, with_in);
+  const int W = (2 + with_in) * N;
+  hipLaunchKernelGGL(k_colreduce, dim3((W + 63) / 64), dim3(256), 0, s, ws, g, W, N, dgamma, dbeta, N, dbias_in);
   KML_LAUNCH_CHECK();
 }
 

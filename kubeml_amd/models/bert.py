@@ -49,6 +49,10 @@ class BertLayer(tnn.Module):
         # residual gradient is summed in that Linear's dgrad epilogue (nn/transformer.py)
         object.__setattr__(self.attention.ln, "_kml_res_linear", self.attention.qkv)
         object.__setattr__(self.output.LayerNorm, "_kml_res_linear", self.intermediate.dense)
+        # ... and its input is the (dropped-out) output of the out-projection / FFN2 Linear
+        # alone: that Linear's bias gradient is summed inside the LayerNorm backward
+        object.__setattr__(self.attention.ln, "_kml_in_linear", self.attention.out)
+        object.__setattr__(self.output.LayerNorm, "_kml_in_linear", self.output.dense)
 
     def forward(self, h, B: int, L: int, bias=None):
         # hidden dropout runs inside the LayerNorm kernels (LN(dropout(a) + h))

@@ -244,7 +244,10 @@ class _LinearFn(Function):
         else:
             K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
         if ctx.has_bias:
-            K.colsum_(dy, grad_storage_of(mod.bias))
+            if getattr(mod, "_kml_bias_done", False):
+                object.__setattr__(mod, "_kml_bias_done", False)   # summed by the consumer LayerNorm
+            else:
+                K.colsum_(dy, grad_storage_of(mod.bias))
         if addend is not None and dx is not None:
             dx = K.add_bf16(dx, addend)
         ctx.x = ctx.y = ctx.pre = None

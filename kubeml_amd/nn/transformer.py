@@ -35,7 +35,7 @@ _RES_FUSE = __import__("os").environ.get("KUBEML_RES_FUSE", "1") != "0"
 # ====================================================================================== LayerNorm
 class _LNFn(Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, mod, res, drop=None):
+    def forward(ctx, x, weight, bias, mod, res, drop=None, sep_dropout=False):
         from ..ops import transformer as T
         y, xin, mean, rstd = T.ln_fwd(x, master_of(weight), master_of(bias), res=res, eps=mod.eps, drop=drop)
         ctx.save = (xin, mean, rstd)
@@ -43,6 +43,7 @@ class _LNFn(Function):
         ctx.has_res = res is not None
         ctx.res_ptr = res.data_ptr() if res is not None else None
         ctx.drop = drop
+        ctx.sep_dropout = sep_dropout   # x came through a separate Dropout (not the Linear output)
         return y
 
     @staticmethod
@@ -50,8 +51,16 @@ class _LNFn(Function):
         from ..ops import transformer as T
         xin, mean, rstd = ctx.save
         mod = ctx.mod
+        # bias gradient of the Linear whose output is this LN's input (``_kml_in_linear``):
+        # summed from the input gradient inside the LN backward; that Linear then skips its
+        # own column-sum pass (``_kml_bias_done``)
+        lin_in = getattr(mod, "_kml_in_linear", None) if _RES_FUSE and not ctx.sep_dropout else None
+        dbias = None
+        if lin_in is not None and getattr(lin_in, "bias", None) is not None and lin_in.out_pad == xin.shape[-1]:
+            dbias = grad_storage_of(lin_in.bias)
+            object.__setattr__(lin_in, "_kml_bias_done", True)
         r = T.ln_bwd(_bf(dy).contiguous(), xin, mean, rstd, master_of(mod.weight), grad_storage_of(mod.weight),
-                     grad_storage_of(mod.bias), drop=ctx.drop)
+                     grad_storage_of(mod.bias), drop=ctx.drop, dbias_in=dbias)
         dx, dxin = r if ctx.drop is not None else (r, r)   # dxin: gradient of the (pre-dropout) input
         ctx.save = ctx.drop = None
         dres = dx if ctx.has_res else None
@@ -61,7 +70,7 @@ class _LNFn(Function):
             # this gradient so its dgrad GEMM adds it in the epilogue (no separate add kernel)
             object.__setattr__(lin, "_kml_res_grad", (ctx.res_ptr, dres))
             dres = None
-        return dxin, None, None, None, dres, None
+        return dxin, None, None, None, dres, None, None
 
 
 class LayerNorm(tnn.LayerNorm):
@@ -71,12 +80,13 @@ class LayerNorm(tnn.LayerNorm):
     or backward (``KUBEML_LN_DROP_FUSE=0`` keeps it separate)."""
 
     def forward(self, x, residual=None, dropout=None):
-        drop = None
+        drop, sep = None, False
         if dropout is not None and dropout.training and dropout.p > 0.0:
             if x.is_cuda and _LN_DROP_FUSE:
                 drop = (dropout.rng.tensor(x.device), dropout.salt, dropout.p)
             else:
                 x = dropout(x)
+                sep = True
         if not x.is_cuda:
             if residual is not None:
                 x = x + residual
@@ -84,7 +94,7 @@ class LayerNorm(tnn.LayerNorm):
         shp = x.shape
         x2 = _bf(x).reshape(-1, shp[-1]).contiguous()
         r2 = None if residual is None else _bf(residual).reshape(-1, shp[-1]).contiguous()
-        return _LNFn.apply(x2, self.weight, self.bias, self, r2, drop).view(shp)
+        return _LNFn.apply(x2, self.weight, self.bias, self, r2, drop, sep).view(shp)
 
 
 _LN_DROP_FUSE = __import__("os").environ.get("KUBEML_LN_DROP_FUSE", "1") != "0"

@@ -102,10 +102,11 @@ def ln_fwd(x, gamma, beta, res=None, eps=1e-12, keep_sum=True, drop=None):
     return y, (s if s is not None else x), mean, rstd
 
 
-def ln_bwd(dy, xin, mean, rstd, gamma, dgamma, dbeta, dx_add=None, drop=None):
+def ln_bwd(dy, xin, mean, rstd, gamma, dgamma, dbeta, dx_add=None, drop=None, dbias_in=None):
     """dx (+ dx_add) ; dgamma/dbeta += (deterministic two-level reduce).  drop = (ctr, salt,
     p) of a forward :func:`ln_fwd` dropout: returns (dx, dropout(dx)) — the gradients of the
-    residual input and of the pre-dropout input — from one pass."""
+    residual input and of the pre-dropout input — from one pass.  dbias_in (fp32 [N]) +=
+    column sums of the input gradient: the bias gradient of the Linear feeding the LN."""
     _chk(dy, BF16, "dy")
     N = dy.shape[-1]
     M = dy.numel() // N
@@ -115,9 +116,13 @@ def ln_bwd(dy, xin, mean, rstd, gamma, dgamma, dbeta, dx_add=None, drop=None):
     nws = HIP.raw("kml_ln_bwd_ws_floats", M, N)
     ws = torch.empty(nws, dtype=F32, device=dy.device)
     cnt = _COUNTERS.take(dy.device, 1)
-    HIP.call("kml_ln_bwd", "p p p p p p p p p p p l i p p i f s", _p(dy), _p(xin), _p(mean), _p(rstd), _p(gamma),
+    if dbias_in is not None:
+        _chk(dbias_in, F32, "dbias_in")
+        if dbias_in.numel() < N:
+            raise ValueError("dbias_in shorter than N")
+    HIP.call("kml_ln_bwd", "p p p p p p p p p p p l i p p i f p s", _p(dy), _p(xin), _p(mean), _p(rstd), _p(gamma),
              _p(dx), _p(dx_add), _p(dgamma), _p(dbeta), _p(ws), _p(cnt), M, N, _p(dxd), _p(ctr),
-             int(salt) & 0x7FFFFFFF, float(p), _s())
+             int(salt) & 0x7FFFFFFF, float(p), _p(dbias_in), _s())
     return (dx, dxd) if drop is not None else dx
 
 

@@ -79,3 +79,37 @@ def test_bert_tiny_graphed_adam_learns():
             first = float(l)
     last = float(l)
     assert first > 4.0 and last < 0.5 * first, (first, last)  # 3 steps already taken by warmup+capture
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_bert_fused_residual_and_bias_gradients_match_unfused(dropout):
+    """Residual-gradient sums in the dgrad epilogue and the out-projection / FFN2 bias
+    gradients summed inside the LayerNorm backward (KUBEML_RES_FUSE, default on) give the
+    same loss and gradients as autograd adds + column-sum kernels (same dropout masks)."""
+    from kubeml_amd.models.bert import bert_tiny_mlm
+    from kubeml_amd.nn import flatten_module
+    from kubeml_amd.nn import transformer as TR
+    ids, tt, pos, lab, mask = _data(2, 128, 20, 1000, seed=3)
+    out = []
+    old = TR._RES_FUSE
+    try:
+        for fuse in (False, True):
+            TR._RES_FUSE = fuse
+            torch.manual_seed(0)
+            TR.Dropout._salt = 0            # same per-layer salts (dropout masks) in both models
+            m = bert_tiny_mlm(dropout=dropout).to(dev)
+            sp = flatten_module(m)
+            m.train()
+            sp.zero_grad()
+            loss = m(ids.to(dev), tt.to(dev), mask.to(dev), pos.to(dev), lab.to(dev))
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((float(loss), sp.grad.clone(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    finally:
+        TR._RES_FUSE = old
+    (l0, g0, p0), (l1, g1, p1) = out
+    assert l1 == l0
+    assert _rel(g1, g0) < 1e-3, _rel(g1, g0)
+    for n in p0:
+        if n.endswith("bias"):
+            assert _rel(p1[n], p0[n]) < 1e-2, (n, _rel(p1[n], p0[n]))
