@@ -253,6 +253,32 @@ __global__ void k_gelu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restri
   }
 }
 
+// GELU backward of a [M][N] row-major map that also writes per-row-block column sums of dx
+// (part[blockIdx.y][N]; k_colreduce adds them to the bias gradient of the Linear whose
+// pre-activation x is): the FFN1 bias gradient without a second pass over dx.  A block covers
+// rows [y * rpb, +rpb) x 1024 columns; each thread owns 4 columns (8-byte accesses, a block
+// row is 2 KB contiguous) and sums the bf16-rounded dx it stores.
+__global__ __launch_bounds__(256) void k_gelu_bwd_colsum(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                        bf16_t* __restrict__ dx, float* __restrict__ part,
+                                                        long long M, int N, int rpb) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const long long r0 = (long long)blockIdx.y * rpb;
+  const long long r1 = min(M, r0 + rpb);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long long r = r0; r < r1; ++r) {
+    float d[4], f[4];
+    ld4(dy + r * N + c, d);
+    ld4(x + r * N + c, f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = bf2f(f2bf(d[k] * gelu_grad(f[k])));
+    st4(dx + r * N + c, d);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += d[k];
+  }
+  *reinterpret_cast<float4*>(part + (long long)blockIdx.y * N + c) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
 // ------------------------------------------------------------------------------ dropout
 // y = x * keep / (1 - p); ctr = [seed, step].  One hash per element PAIR j (elements 2j,
 // 2j+1): keep = 16-bit half of hash(seed ^ salt, step, j) >= p * 2^16.  8 elements (16 B)
@@ -435,6 +461,33 @@ KML_API int kml_gelu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s)
 KML_API int kml_gelu_bwd(const bf16_t* dy, const bf16_t* x, bf16_t* dx, long long n, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_gelu_bwd, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, dy, x, dx, n / 4);
+  KML_LAUNCH_CHECK();
+}
+
+// rows per block / row blocks of kml_gelu_bwd_colsum (its workspace is G x N floats)
+static int gelu_cs_blocks(long long M, int* rpb) {
+  long long r = 64;
+  long long g = (M + r - 1) / r;
+  if (g > 1024) { r = (M + 1023) / 1024; g = (M + r - 1) / r; }
+  *rpb = (int)r;
+  return (int)g;
+}
+
+KML_API long long kml_gelu_bwd_colsum_ws_floats(long long M, int N) {
+  int rpb;
+  return (long long)gelu_cs_blocks(M, &rpb) * N;
+}
+
+// dx = dy * gelu'(x) over [M][N] and dbias[c] += sum_r dx[r][c] (deterministic row-block order)
+KML_API int kml_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* x, bf16_t* dx, float* dbias, float* ws, long long M,
+                                int N, hipStream_t s) {
+  if (N % 4 || M <= 0) return (int)hipErrorInvalidValue;
+  int rpb;
+  const int g = gelu_cs_blocks(M, &rpb);
+  hipLaunchKernelGGL(k_gelu_bwd_colsum, dim3((unsigned)((N / 4 + 255) / 256), (unsigned)g), dim3(256), 0, s, dy, x,
+                     dx, ws, M, N, rpb);
+  hipLaunchKernelGGL(k_colreduce, dim3((N + 63) / 64), dim3(256), 0, s, ws, g, N, N, dbias, (float*)nullptr, 0,
+                     (float*)nullptr);
   KML_LAUNCH_CHECK();
 }
 

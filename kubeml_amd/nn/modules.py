@@ -208,11 +208,14 @@ class _LinearFn(Function):
             dy = dy.to(torch.bfloat16)
         if op != mod.out_features and dy.shape[1] != op:
             dy = K.pad_channels(dy, op)
+        bias_done = False
         if ctx.act == 1:
             dy = K.relu_bwd(dy, ctx.y)
         elif ctx.act == 2:
             from ..ops import transformer as T
-            dy = T.gelu_bwd(dy, ctx.pre)
+            # the bias gradient comes out of the GELU backward pass (no column-sum pass)
+            dy = T.gelu_bwd(dy, ctx.pre, dbias=grad_storage_of(mod.bias) if ctx.has_bias else None)
+            bias_done = ctx.has_bias
         dy4 = dy.view(B, 1, 1, op)
         x4 = ctx.x.view(B, 1, 1, ip)
         dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
@@ -243,7 +246,7 @@ class _LinearFn(Function):
             dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0)).view(B, ip)
         else:
             K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
-        if ctx.has_bias:
+        if ctx.has_bias and not bias_done:
             if getattr(mod, "_kml_bias_done", False):
                 object.__setattr__(mod, "_kml_bias_done", False)   # summed by the consumer LayerNorm
             else:

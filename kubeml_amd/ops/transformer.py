@@ -132,8 +132,19 @@ def gelu_fwd(x):
     return y
 
 
-def gelu_bwd(dy, x):
+def gelu_bwd(dy, x, dbias=None):
+    """dx = dy * gelu'(x).  dbias (fp32 [N]) += column sums of dx over the rows of the
+    [M, N] map, from the same pass (the bias gradient of the Linear whose pre-activation x is)."""
     dx = torch.empty_like(dy)
+    if dbias is not None:
+        _chk(dbias, F32, "dbias")
+        N = dy.shape[-1]
+        M = dy.numel() // N
+        if dbias.numel() < N:
+            raise ValueError("dbias shorter than N")
+        ws = torch.empty(HIP.raw("kml_gelu_bwd_colsum_ws_floats", M, N), dtype=F32, device=dy.device)
+        HIP.call("kml_gelu_bwd_colsum", "p p p p p l i s", _p(dy), _p(x), _p(dx), _p(dbias), _p(ws), M, N, _s())
+        return dx
     HIP.call("kml_gelu_bwd", "p p p l s", _p(dy), _p(x), _p(dx), dy.numel(), _s())
     return dx
 

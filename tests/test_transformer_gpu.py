@@ -219,3 +219,21 @@ def test_layernorm_fused_dropout_matches_separate(N, res):
         torch.testing.assert_close(grb, gra, rtol=0, atol=0)
     # the mask really dropped ~p of the elements
     assert 0.05 < float((gxb == 0).float().mean()) < 0.15
+
+
+@pytest.mark.parametrize("M,N", [(16384, 3072), (300, 72), (7, 1028)])
+def test_gelu_bwd_with_bias_colsum(M, N):
+    """gelu_bwd(dbias=...) writes the same dx and adds the column sums of dx to dbias (the FFN1
+    bias gradient) in the same pass."""
+    from kubeml_amd.ops import kernels as K
+    from kubeml_amd.ops import transformer as T
+    torch.manual_seed(6)
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    x = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    ref = T.gelu_bwd(dy, x)
+    db = torch.full((N,), 0.5, device=dev)
+    dx = T.gelu_bwd(dy, x, dbias=db)
+    torch.testing.assert_close(dx, ref, rtol=0, atol=0)
+    want = torch.full((N,), 0.5, device=dev)
+    K.colsum_(ref, want)
+    assert _rel(db, want) < 1e-5
