@@ -266,7 +266,25 @@ __global__ __launch_bounds__(256) void k_gelu_bwd_colsum(const bf16_t* __restric
   const long long r0 = (long long)blockIdx.y * rpb;
   const long long r1 = min(M, r0 + rpb);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (long long r = r0; r < r1; ++r) {
+  constexpr int U = 8;  // rows in flight per thread (loads of U rows issued before any math)
+  long long r = r0;
+  for (; r + U <= r1; r += U) {
+    float d[U][4], f[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ld4(dy + (r + u) * N + c, d[u]);
+      ld4(x + (r + u) * N + c, f[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[u][k] = bf2f(f2bf(d[u][k] * gelu_grad(f[u][k])));
+      st4(dx + (r + u) * N + c, d[u]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += d[u][k];
+    }
+  }
+  for (; r < r1; ++r) {
     float d[4], f[4];
     ld4(dy + r * N + c, d);
     ld4(x + r * N + c, f);
