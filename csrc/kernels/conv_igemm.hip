@@ -1301,7 +1301,7 @@ struct UnrollBatch {
   int n;
 };
 
-constexpr int UNROLL_V = 4;  // 16-byte chunks per thread (all loads issued before the stores)
+constexpr int UNROLL_V = 8;  // 16-byte chunks per thread (all loads issued before the stores)
 
 __global__ __launch_bounds__(256) void k_unroll22_multi(UnrollBatch ub) {
   int q = 0;

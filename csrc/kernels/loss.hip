@@ -200,6 +200,53 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
   }
 }
 
+// k_ce_bwd (bf16 vector path) that also adds the column sums of dlogits to dbias — the bias
+// gradient of the Linear that produced the logits (its own column-sum pass is skipped).  The
+// block's 4 rows are summed through LDS ([4][ld] fp32, ld <= 4096), then one fp32 atomic per
+// column per block.
+__global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ logits,
+                                                     const long long* __restrict__ labels,
+                                                     const float* __restrict__ lse, const float* __restrict__ red,
+                                                     const float* __restrict__ grad_out, bf16_t* __restrict__ dlogits,
+                                                     float* __restrict__ dbias, int B, int C, int ld,
+                                                     long long ignore) {
+  extern __shared__ float colsh[];  // [4][ld]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  const bool have = row < B;
+  const long long y = have ? labels[row] : -1;
+  const bool skip = !have || (y == ignore || y < 0 || y >= C);
+  const float valid = red[2];
+  const float g = (grad_out ? *grad_out : 1.f) / fmaxf(valid, 1.f);
+  const float l = have ? lse[row] : 0.f;
+  const float l2 = l * LOG2E_CE;
+  const uint4* x8 = reinterpret_cast<const uint4*>(logits + (long long)(have ? row : 0) * ld);
+  uint4* d8 = reinterpret_cast<uint4*>(dlogits + (long long)(have ? row : 0) * ld);
+  float* mine = colsh + w * ld;
+  for (int c8 = lane; c8 < ld / 8; c8 += 64) {
+    float f[8];
+    unpack8f(x8[c8], f);
+    unsigned o[4];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      const int c = c8 * 8 + k;
+      const float a = (skip || c >= C) ? 0.f
+                      : (__builtin_amdgcn_exp2f(fmaf(f[k], LOG2E_CE, -l2)) - (c == y ? 1.f : 0.f)) * g;
+      const float b = (skip || c + 1 >= C) ? 0.f
+                      : (__builtin_amdgcn_exp2f(fmaf(f[k + 1], LOG2E_CE, -l2)) - (c + 1 == y ? 1.f : 0.f)) * g;
+      o[k / 2] = pack_bf2(a, b);
+      mine[c] = lo_bf(o[k / 2]);          // the bf16 gradient the Linear would column-sum
+      mine[c + 1] = hi_bf(o[k / 2]);
+    }
+    if (have) d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float t = (colsh[c] + colsh[ld + c]) + (colsh[2 * ld + c] + colsh[3 * ld + c]);
+    atomicAdd(dbias + c, t);
+  }
+}
+
 }  // namespace
 
 // dtype: 0 = bf16 logits, 1 = fp32 logits.  ws = [3*B] fp32 workspace (lse, rowloss, rowcorrect).
@@ -220,11 +267,18 @@ KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, f
   KML_LAUNCH_CHECK();
 }
 
+// dbias (optional; bf16 logits, ld % 8 == 0, ld <= 4096): += column sums of dlogits
 KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
                        const float* grad_out, void* dlogits, int B, int C, int ld, long long ignore, int dtype,
-                       hipStream_t s) {
+                       float* dbias, hipStream_t s) {
   if (ld < C) return (int)hipErrorInvalidValue;
   dim3 g((B + 3) / 4);
+  if (dbias) {
+    if (dtype != 0 || ld % 8 || ld > 4096) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ce_bwd_bias, g, dim3(256), (size_t)4 * ld * sizeof(float), s, (const bf16_t*)logits, labels,
+                       ws, out3, grad_out, (bf16_t*)dlogits, dbias, B, C, ld, ignore);
+    KML_LAUNCH_CHECK();
+  }
   if (dtype == 0)
     hipLaunchKernelGGL(k_ce_bwd<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)logits, labels, ws, out3, grad_out,
                        (bf16_t*)dlogits, B, C, ld, ignore);

@@ -303,7 +303,10 @@ class Linear(tnn.Module):
         if a == 2 and _linear_route(x.shape[0], self.in_pad, self.out_pad, 2) != "gemm":
             from .transformer import GELU
             return GELU()(_LinearFn.apply(x.contiguous(), self.weight, self.bias, self, 0))
-        return _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, a, keep_pad)
+        y = _LinearFn.apply(x.contiguous(), self.weight, self.bias, self, a, keep_pad)
+        if a == 0:
+            y._kml_linear = self   # raw linear output: a consuming cross_entropy may sum our bias grad
+        return y
 
 
 # ======================================================================================
@@ -489,21 +492,32 @@ def to_nhwc(x, cin_pad=None):
 
 class _CEFn(Function):
     @staticmethod
-    def forward(ctx, logits, labels, ignore_index, classes=None):
+    def forward(ctx, logits, labels, ignore_index, classes=None, lin=None):
         from ..ops import kernels as K
         out3, ws, lab = K.ce_fwd(logits, labels, ignore_index, classes=classes)
         ctx.save = (logits, lab, ws, out3, ignore_index, classes)
         ctx.out3 = out3
+        ctx.lin = lin
         return out3[0]
 
     @staticmethod
     def backward(ctx, g):
         from ..ops import kernels as K
         logits, lab, ws, out3, ig, classes = ctx.save
+        # the logits came straight out of a Linear: its bias gradient (the column sums of
+        # dlogits) is added by the CE backward pass itself, and the Linear skips its own
+        lin, dbias = ctx.lin, None
+        if (lin is not None and getattr(lin, "bias", None) is not None and _CE_BIAS_FUSE
+                and lin.out_pad == logits.shape[1] and K.ce_bias_fusable(logits)):
+            dbias = grad_storage_of(lin.bias)
+            object.__setattr__(lin, "_kml_bias_done", True)
         d = K.ce_bwd(logits, lab, ws, out3, grad_out=g.reshape(1).float().contiguous(), ignore_index=ig,
-                     classes=classes)
-        ctx.save = None
-        return d, None, None, None
+                     classes=classes, dbias=dbias)
+        ctx.save = ctx.lin = None
+        return d, None, None, None, None
+
+
+_CE_BIAS_FUSE = __import__("os").environ.get("KUBEML_CE_BIAS_FUSE", "1") != "0"
 
 
 def cross_entropy(logits, labels, ignore_index=-100, return_correct=False, classes=None):
@@ -522,11 +536,11 @@ def cross_entropy(logits, labels, ignore_index=-100, return_correct=False, class
     if return_correct:
         from ..ops import kernels as K
         if torch.is_grad_enabled() and logits.requires_grad:
-            loss = _CEFn.apply(logits.contiguous(), labels, ignore_index, classes)
+            loss = _CEFn.apply(logits.contiguous(), labels, ignore_index, classes, getattr(logits, "_kml_linear", None))
             return loss, loss.grad_fn.out3[1]  # grad_fn is the Function ctx; same fused pass
         out3, _, _ = K.ce_fwd(logits.contiguous(), labels, ignore_index, classes=classes)
         return out3[0], out3[1]
-    return _CEFn.apply(logits.contiguous(), labels, ignore_index, classes)
+    return _CEFn.apply(logits.contiguous(), labels, ignore_index, classes, getattr(logits, "_kml_linear", None))
 
 
 _ONES: dict = {}

@@ -856,14 +856,24 @@ def ce_fwd(logits, labels, ignore_index=-100, classes=None):
     return out3, ws, labels
 
 
-def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=None):
-    """dlogits (same [B, ld] layout as the logits; pad columns 0)."""
+def ce_bias_fusable(logits) -> bool:
+    """ce_bwd can add the logits' column sums to a bias gradient in the same pass."""
+    return logits.dtype == BF16 and logits.dim() == 2 and logits.shape[1] % 8 == 0 and logits.shape[1] <= 4096
+
+
+def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=None, dbias=None):
+    """dlogits (same [B, ld] layout as the logits; pad columns 0).  dbias (fp32, needs
+    :func:`ce_bias_fusable`): += column sums of dlogits (the logits Linear's bias gradient)."""
     dt = {BF16: 0, F32: 1}[logits.dtype]
     B, ld = logits.shape
     C = ld if classes is None else int(classes)
     d = torch.empty_like(logits)
-    HIP.call("kml_ce_bwd", "p p p p p p i i i l i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
-             _p(d), B, C, ld, int(ignore_index), dt, _s())
+    if dbias is not None:
+        _chk(dbias, F32, "dbias")
+        if not ce_bias_fusable(logits) or dbias.numel() < C:
+            raise ValueError("ce_bwd: bias fusion needs bf16 logits with ld % 8 == 0, ld <= 4096")
+    HIP.call("kml_ce_bwd", "p p p p p p i i i l i p s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
+             _p(d), B, C, ld, int(ignore_index), dt, _p(dbias), _s())
     return d
 
 

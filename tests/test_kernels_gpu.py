@@ -721,3 +721,22 @@ def test_bn_relu_maxpool_matches_unfused(B, H, C):
     dz_ref = K.maxpool_bwd(dp, idx, c.shape, 3, 2, 1).float() * (y.float() > 0)
     agree = (dz.float() - dz_ref).abs() <= 1e-6
     assert agree.float().mean() > 0.995
+
+
+@pytest.mark.parametrize("B,C,ld", [(256, 1000, 1000), (37, 10, 16), (130, 1000, 1008)])
+def test_ce_bwd_adds_bias_gradient(B, C, ld):
+    """ce_bwd(dbias=...): same dlogits, and dbias += column sums of dlogits (the logits
+    Linear's bias gradient, which that Linear then skips)."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(8)
+    logits = _bf(torch.randn(B, ld, device=dev) * 3)
+    labels = torch.randint(0, C, (B,), device=dev)
+    labels[3] = -100
+    out3, ws, lab = K.ce_fwd(logits, labels, -100, classes=C)
+    d0 = K.ce_bwd(logits, lab, ws, out3, classes=C)
+    db = torch.full((ld,), 0.25, device=dev)
+    d1 = K.ce_bwd(logits, lab, ws, out3, classes=C, dbias=db)
+    torch.testing.assert_close(d1, d0, rtol=0, atol=0)
+    want = torch.full((ld,), 0.25, device=dev)
+    want[:C] += d0.float()[:, :C].sum(0)
+    torch.testing.assert_close(db, want, rtol=1e-5, atol=1e-6)
