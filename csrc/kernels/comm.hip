@@ -109,15 +109,19 @@ KML_API int kml_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 // region (flags + 2 slots of cap bytes) + zeroed local control block [epoch, ticket, errors]
 KML_API int kml_oneshot_alloc(long long cap, void** region, void** ctrl) {
   if (cap <= 0 || cap % 16) return (int)hipErrorInvalidValue;
+  *region = nullptr;
+  *ctrl = nullptr;
   hipError_t e = hipMalloc(region, OS_FLAGS_BYTES + 2 * cap);
-  if (e != hipSuccess) return (int)e;
-  e = hipMemset(*region, 0, OS_FLAGS_BYTES);
-  if (e != hipSuccess) return (int)e;
-  e = hipMalloc(ctrl, 64);
-  if (e != hipSuccess) return (int)e;
-  e = hipMemset(*ctrl, 0, 64);
-  if (e != hipSuccess) return (int)e;
-  return (int)hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemset(*region, 0, OS_FLAGS_BYTES);
+  if (e == hipSuccess) e = hipMalloc(ctrl, 64);
+  if (e == hipSuccess) e = hipMemset(*ctrl, 0, 64);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {  // nothing half-allocated survives a failure
+    if (*region) (void)hipFree(*region);
+    if (*ctrl) (void)hipFree(*ctrl);
+    *region = *ctrl = nullptr;
+  }
+  return (int)e;
 }
 
 KML_API int kml_oneshot_free(void* region, void* ctrl) {
