@@ -887,8 +887,10 @@ __global__ __launch_bounds__(NT) void k_bn_relu_maxpool(
     const float* __restrict__ beta, bf16_t* __restrict__ y, unsigned char* __restrict__ idx,
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
     float* __restrict__ run_var, int B, int H, int W, int C, int OH, int OW, int k, int st, int pd, float eps,
-    float momentum, int stats_rows) {
+    float momentum, int stats_rows, long long* __restrict__ counters, int n_counters) {
   extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], sums[2C], scratch
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < n_counters; i += NT) counters[i] += 1;  // BN num_batches_tracked
   float* scale = sh;
   float* shift = sh + C;
   const long long M = (long long)B * H * W;
@@ -972,8 +974,10 @@ __global__ __launch_bounds__(NT) void k_bn_relu_maxpool3(
     const float* __restrict__ beta, bf16_t* __restrict__ y, unsigned char* __restrict__ idx,
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
     float* __restrict__ run_var, int B, int H, int W, int C, int OH, int OW, int st, int pd, float eps,
-    float momentum, int stats_rows) {
+    float momentum, int stats_rows, long long* __restrict__ counters, int n_counters) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < n_counters; i += NT) counters[i] += 1;  // BN num_batches_tracked
   float* scale = sh;
   float* shift = sh + C;
   const long long M = (long long)B * H * W;
@@ -1252,7 +1256,9 @@ KML_API int kml_relu_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long lon
 KML_API int kml_bn_relu_maxpool(const bf16_t* x, const float* stats, int stats_rows, const float* gamma,
                                 const float* beta, bf16_t* y, unsigned char* idx, float* save_mean,
                                 float* save_rstd, float* run_mean, float* run_var, int B, int H, int W, int C, int k,
-                                int st, int pd, float eps, float momentum, float* fold_ws, hipStream_t s) {
+                                int st, int pd, float eps, float momentum, float* fold_ws, long long* counters,
+                                int n_counters, hipStream_t s) {
+  if (n_counters < 0 || (n_counters > 0 && !counters)) return (int)hipErrorInvalidValue;
   if (C % 8 || k * k > 255 || k < 1 || st < 1 || pd < 0 || 2 * pd > k) return (int)hipErrorInvalidValue;
   if (stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   const int OH = (H + 2 * pd - k) / st + 1, OW = (W + 2 * pd - k) / st + 1;
@@ -1269,7 +1275,7 @@ KML_API int kml_bn_relu_maxpool(const bf16_t* x, const float* stats, int stats_r
     const size_t shm3 = (4 * C + 4 * NT) * sizeof(float);
     hipLaunchKernelGGL((k_bn_relu_maxpool3<NT, 1>), dim3((unsigned)g3), dim3(NT), shm3, s, x, stats, gamma, beta,
                        y, idx, save_mean, save_rstd, run_mean, run_var, B, H, W, C, OH, OW, st, pd, eps, momentum,
-                       stats_rows);
+                       stats_rows, counters, n_counters);
     KML_LAUNCH_CHECK();
   }
   if (k == 3) {
@@ -1278,10 +1284,11 @@ KML_API int kml_bn_relu_maxpool(const bf16_t* x, const float* stats, int stats_r
     if (g3 > 256) g3 = 256;
     hipLaunchKernelGGL((k_bn_relu_maxpool3<TPB, IPT>), dim3((unsigned)g3), dim3(TPB), shm, s, x, stats, gamma, beta,
                        y, idx, save_mean, save_rstd, run_mean, run_var, B, H, W, C, OH, OW, st, pd, eps, momentum,
-                       stats_rows);
+                       stats_rows, counters, n_counters);
     KML_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(k_bn_relu_maxpool<TPB>, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, y, idx, save_mean,
-                     save_rstd, run_mean, run_var, B, H, W, C, OH, OW, k, st, pd, eps, momentum, stats_rows);
+                     save_rstd, run_mean, run_var, B, H, W, C, OH, OW, k, st, pd, eps, momentum, stats_rows, counters,
+                     n_counters);
   KML_LAUNCH_CHECK();
 }

@@ -159,7 +159,8 @@ class ResNet(tnn.Module):
             x = M.to_nhwc(x, self.conv1.cin_pad)
         if x.is_cuda:
             if self.training:
-                self._bump_counters()
+                if not (torch.is_grad_enabled() and _STEM_FUSE):
+                    self._bump_counters()      # else the fused stem kernel bumps them
                 if torch.is_grad_enabled():
                     convs = getattr(self, "_kml_convs", None)
                     if convs is None:
@@ -187,6 +188,10 @@ class ResNet(tnn.Module):
                 list(self.layer4.parameters()) + list(self.fc.parameters())]
 
     def _bump_counters(self):
+        from ..ops import kernels as K
+        K.add_i64_(self._counter_arena())
+
+    def _counter_arena(self):
         # num_batches_tracked of every BN: one tiny kernel each is avoided by keeping
         # the counters in one int64 arena (allocated on first use)
         arena = getattr(self, "_nbt_arena", None)
@@ -202,8 +207,7 @@ class ResNet(tnn.Module):
                     arena[i] = bn.num_batches_tracked.to(dev)
                     bn.num_batches_tracked = arena[i]
             self._nbt_arena = arena
-        from ..ops import kernels as K
-        K.add_i64_(arena)
+        return arena
 
     def _stem_gpu(self, x):
         if torch.is_grad_enabled() and self.training:
@@ -238,9 +242,12 @@ class _StemFn(torch.autograd.Function):
         C = c.shape[-1]
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         rstd = torch.empty_like(mean)
+        # the model's BN num_batches_tracked counters are bumped by this kernel's block 0 (one
+        # launch less per step; _stem_l1 skips its own bump on this path)
         p, idx = K.bn_relu_maxpool(c, stats, master_of(bn.weight), master_of(bn.bias), 3, 2, 1, save_mean=mean,
                                    save_rstd=rstd, run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
-                                   momentum=bn.momentum if bn.momentum is not None else 0.1, stats_rows=G)
+                                   momentum=bn.momentum if bn.momentum is not None else 0.1, stats_rows=G,
+                                   counters=net._counter_arena())
         # saved like a ConvBNUnit without ReLU: the mask travels in the pooled output
         ctx.net, ctx.s, ctx.idx, ctx.yshape, ctx.p = net, (x, c, None, mean, rstd), idx, c.shape, p
         return p

@@ -799,20 +799,24 @@ def maxpool_bwd(dy, idx, in_shape, k, s, p, relu_out=None):
 
 
 def bn_relu_maxpool(x, stats, gamma, beta, k, s, p, save_mean=None, save_rstd=None, run_mean=None, run_var=None,
-                    eps=1e-5, momentum=0.1, stats_rows=0):
+                    eps=1e-5, momentum=0.1, stats_rows=0, counters=None):
     """Training BN (batch statistics from ``stats``: [stats_rows][2C] conv-epilogue partial
     rows, or final [2C] sums) -> ReLU -> max-pool(k, s, p) in one pass; returns (pooled,
     argmax idx).  The normalised map is never materialised — backward is
-    ``maxpool_bwd(..., relu_out=pooled)`` then ``bn_bwd`` without a ReLU mask."""
+    ``maxpool_bwd(..., relu_out=pooled)`` then ``bn_bwd`` without a ReLU mask.  counters:
+    an int64 tensor (the model's BN ``num_batches_tracked`` arena) incremented by one."""
     _chk(x, BF16, "x", 4)
     B, H, W, C = x.shape
     OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     y = torch.empty((B, OH, OW, C), dtype=BF16, device=x.device)
     idx = torch.empty((B, OH, OW, C), dtype=torch.uint8, device=x.device)
     ws = _fold_ws(stats_rows, C, x.device) if stats_rows > 0 else None
-    HIP.call("kml_bn_relu_maxpool", "p p i p p p p p p p p i i i i i i i f f p s",
+    if counters is not None and (counters.dtype != torch.int64 or not counters.is_contiguous()):
+        raise ValueError("counters must be a contiguous int64 tensor")
+    HIP.call("kml_bn_relu_maxpool", "p p i p p p p p p p p i i i i i i i f f p p i s",
              _p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(y), _p(idx), _p(save_mean), _p(save_rstd),
-             _p(run_mean), _p(run_var), B, H, W, C, k, s, p, float(eps), float(momentum), _p(ws), _s())
+             _p(run_mean), _p(run_var), B, H, W, C, k, s, p, float(eps), float(momentum), _p(ws), _p(counters),
+             0 if counters is None else counters.numel(), _s())
     return y, idx
 
 
