@@ -218,7 +218,7 @@ def main():
     step = make_train_step(
         model, space, opt, cross_entropy, xbuf, ybuf,
         pre=lambda: K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True),
-        post=lambda: K.advance_counter_(ctr, B, n_local),
+        advance=(ctr, B, n_local),   # data-counter advance, folded into the SGD launch
         world=world, use_graph=not args.no_graph, graph_comm=graph_comm, overlap=overlap,
         bucket_mb=args.bucket_mb, force_comm=args.force_comm, extra_state=[ctr],
         comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)

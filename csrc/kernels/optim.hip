@@ -22,7 +22,16 @@ namespace {
 __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ mom,
                       bf16_t* __restrict__ shadow, const float* __restrict__ lr_ptr, float lr_host, float wd,
                       float momentum, float dampening, int nesterov, const float* __restrict__ first_ptr,
-                      int first_host, float grad_scale, long long n) {
+                      int first_host, float grad_scale, long long n, float* __restrict__ adv_ctr,
+                      float adv_batch, float adv_n) {
+  // data-sampler counter advance (k_advance's job) folded into this launch: one thread, no
+  // other block reads the counter, the next step's augment reads it after the launch boundary
+  if (adv_ctr && blockIdx.x == 0 && threadIdx.x == 0) {
+    adv_ctr[1] += 1.f;
+    float st = adv_ctr[2] + adv_batch;
+    if (st >= adv_n) st -= adv_n;
+    adv_ctr[2] = st;
+  }
   const float lr = lr_ptr ? *lr_ptr : lr_host;
   // first step after a reset (torch: momentum buffer := d, no dampening).  The flag lives
   // in device memory so a graph-captured step follows reset_state() between replays.
@@ -154,11 +163,12 @@ KML_API int kml_memset(void* p, int value, long long bytes, hipStream_t s) {
 // kernels on a side stream should take a slice of the CUs, not all of them)
 KML_API int kml_sgd(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr, float lr, float wd,
                     float momentum, float dampening, int nesterov, const float* first_ptr, int first,
-                    float grad_scale, long long n, int max_blocks, hipStream_t s) {
+                    float grad_scale, long long n, int max_blocks, float* adv_ctr, float adv_batch, float adv_n,
+                    hipStream_t s) {
   unsigned grid = kml_stream_grid((n + 3) / 4, 256);
   if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
   hipLaunchKernelGGL(k_sgd, dim3(grid), dim3(256), 0, s, w, g, mom, shadow, lr_ptr, lr, wd, momentum, dampening,
-                     nesterov, first_ptr, first, grad_scale, n);
+                     nesterov, first_ptr, first, grad_scale, n, adv_ctr, adv_batch, adv_n);
   KML_LAUNCH_CHECK();
 }
 

@@ -26,11 +26,14 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     use_graph: bool = True, graph_comm: bool = True, overlap: bool = True,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
                     extra_state: Sequence[torch.Tensor] = (), comm_dtype=None,
-                    opt_overlap: Optional[bool] = None) -> GraphedTrainStep:
+                    opt_overlap: Optional[bool] = None, advance=None) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
     pre():  runs first inside the step (e.g. on-device augmentation into ``x``)
-    post(): runs after the optimizer (e.g. advance the data counter)
+    post(): runs after the optimizer
+    advance: (ctr, batch, n) -- advance the on-device data counter after the optimizer
+            (``ops.kernels.advance_counter_``); folded into the fused SGD launch when the
+            optimizer can (``fuse_advance``; ``KUBEML_ADV_IN_OPT=0`` keeps it a separate launch)
     world:  ranks in ``group``; > 1 adds the gradient all-reduce (SUM) and sets the
             optimizer's gradient scale to 1/world
     overlap: split backward at ``model.stages()`` (if the model has them) so each
@@ -64,6 +67,17 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         opt_overlap = os.environ.get("KUBEML_OPT_OVERLAP", "0") == "1"
     opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm)
                        and getattr(optimizer, "supports_ranges", lambda: False)())
+    if advance is not None:
+        fused = (not opt_overlap and os.environ.get("KUBEML_ADV_IN_OPT", "1") != "0"
+                 and getattr(optimizer, "fuse_advance", lambda *a: False)(*advance))
+        if not fused:
+            user_post = post
+
+            def post():
+                if user_post is not None:
+                    user_post()
+                from ..ops import kernels as K
+                K.advance_counter_(*advance)
     if (comm and overlap and staged_ok) or opt_overlap:
         from .staged import StagedForwardBackward
 

@@ -886,13 +886,21 @@ def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=N
 # --------------------------------------------------------------------------------------
 
 def sgd_(w, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=False, first=False,
-         grad_scale=1.0, lr_dev=None, first_dev=None, max_blocks=0):
+         grad_scale=1.0, lr_dev=None, first_dev=None, max_blocks=0, advance=None):
     """first_dev: fp32 device flag (non-zero = first step after a state reset); when given
-    it overrides ``first`` so graph replays follow reset_state().  max_blocks: grid cap."""
+    it overrides ``first`` so graph replays follow reset_state().  max_blocks: grid cap.
+    advance: (ctr, batch, n) -- also do :func:`advance_counter_` (ctr, batch, n) in this launch."""
     n = w.numel()
-    HIP.call("kml_sgd", "p p p p p f f f f i p i f l i s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
+    ctr, ab, an = None, 0.0, 0.0
+    if advance is not None:
+        ctr, ab, an = advance
+        _chk(ctr, F32, "ctr")
+        if ctr.numel() < 3 or ctr.device != w.device:
+            raise ValueError("advance counter must be a [3] fp32 tensor on the parameters' device")
+        ab, an = float(ab), float(an)
+    HIP.call("kml_sgd", "p p p p p f f f f i p i f l i p f f s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
              float(lr), float(wd), float(momentum), float(dampening), int(nesterov), _p(first_dev), int(first),
-             float(grad_scale), n, int(max_blocks), _s())
+             float(grad_scale), n, int(max_blocks), _p(ctr), ab, an, _s())
 
 
 def adam_(w, g, m, v, shadow, lr, step, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, decoupled=False,

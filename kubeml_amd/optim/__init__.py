@@ -160,12 +160,24 @@ class SGD(FusedOptimizer):
         if len(self.param_groups) > 1:
             raise ValueError("fused SGD supports a single param group")
 
+    _advance = None  # (ctr, batch, n) folded into the fused step, see fuse_advance
+
+    def fuse_advance(self, ctr, batch, n) -> bool:
+        """Advance the on-device data-sampler counter ``ctr`` (``ops.kernels.advance_counter_``)
+        inside every fused step's SGD launch instead of a one-thread launch of its own.
+        Returns False (nothing attached) when no GPU flat space holds the counter's device."""
+        spaces, _ = self._flat_groups()
+        if not spaces or spaces[0][0].device.type != "cuda" or ctr.device != spaces[0][0].device:
+            return False
+        self._advance = (ctr, batch, n)
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
         spaces, loose = self._flat_groups()
-        for sp, members in spaces:
+        for k, (sp, members) in enumerate(spaces):
             if sp.device.type != "cuda":
                 loose += members
                 continue
@@ -174,7 +186,8 @@ class SGD(FusedOptimizer):
             first = self.first_tensor(sp.device) if mom is not None else None
             K.sgd_(sp.master, sp.grad, mom, sp.shadow, g["lr"], wd=g["weight_decay"], momentum=g["momentum"],
                    dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
-                   grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first)
+                   grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first,
+                   advance=self._advance if k == 0 else None)
             if first is not None:
                 K.fill_(first, 0.0)
         if loose:

@@ -265,6 +265,26 @@ def test_sgd_adam():
     assert torch.allclose(w2, p2.data, atol=1e-5)
 
 
+
+def test_sgd_folds_the_data_counter_advance():
+    """sgd_(advance=(ctr, B, n)): identical update, and ctr ends where advance_counter_
+    leaves it (step + 1, start + B wrapped at n), over launches that wrap around."""
+    from kubeml_amd.ops import kernels as K
+    n = 10007
+    w1 = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    w2 = w1.clone()
+    s1 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    s2 = torch.empty_like(s1)
+    c1 = torch.tensor([3.0, 0.0, 0.0], device=dev)
+    c2 = c1.clone()
+    for _ in range(7):
+        K.sgd_(w1, g, None, s1, 0.05, wd=1e-4)
+        K.advance_counter_(c1, 48, 100)
+        K.sgd_(w2, g, None, s2, 0.05, wd=1e-4, advance=(c2, 48, 100))
+    assert torch.equal(w2, w1) and torch.equal(s2, s1)
+    assert torch.equal(c2, c1) and c2.tolist() == [3.0, 7.0, 36.0]
+
 def test_augment():
     from kubeml_amd.ops import kernels as K
     N = 50
