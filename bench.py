@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--no-epoch", action="store_true", help="skip the measured epoch after the timed steps")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="gradient all-reduce precision (bf16 = compressed, half the xGMI bytes)")
+    ap.add_argument("--comm-plan", default="auto",
+                    help="gradient transport backend:schedule:wire[:blocks] (e.g. peer:end:bf16:256, "
+                         "rccl:overlap:fp32); auto = kubeml_amd/parallel/comm_plan.json's measured choice")
+    ap.add_argument("--comm-timing", type=int, default=20,
+                    help="sample the in-graph gradient all-reduce time every N steps (0 = off)")
     ap.add_argument("--cpu-smoke", action="store_true", help="gloo/CPU rehearsal of the N-rank launch (tiny model)")
     ap.add_argument("--trace", default=None, help="write a Chrome trace (device compute/comm timeline) to this dir; "
                                                   "collectives then run outside the step graph")
@@ -215,13 +220,19 @@ def main():
 
     overlap = args.overlap == "on" or (args.overlap == "auto" and comm)
     graph_comm = args.graph_comm == "on" and os.environ.get("KUBEML_GRAPH_COMM", "1") != "0"
+    plan = None
+    if comm:
+        from kubeml_amd.parallel.plan import choose_plan
+        plan = choose_plan(world, space.grad.numel() * 4,
+                           override=None if args.comm_plan == "auto" else args.comm_plan)
     step = make_train_step(
         model, space, opt, cross_entropy, xbuf, ybuf,
         pre=lambda: K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True),
         advance=(ctr, B, n_local),   # data-counter advance, folded into the SGD launch
         world=world, use_graph=not args.no_graph, graph_comm=graph_comm, overlap=overlap,
         bucket_mb=args.bucket_mb, force_comm=args.force_comm, extra_state=[ctr],
-        comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32)
+        comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else torch.float32,
+        plan=plan, comm_timing=args.comm_timing if comm else 0)
     if comm:
         step.prime_comm()
     step.capture()
@@ -257,6 +268,8 @@ def main():
 
     dt, loss = timed(lambda: run_steps(args.steps))
     last_loss = float(loss.item())
+    if getattr(step, "peer", None) is not None:
+        step.peer.check()          # a timed-out peer barrier poisons the sums: fail loudly
     in_sync = None
     if comm:
         # every rank must hold identical weights after K all-reduced steps (checks that the
@@ -291,14 +304,20 @@ def main():
             "config": {"model": "resnet34 (torchvision, ImageNet stem, 1000-class head)", "global_batch": B * world,
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
                        "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "gradient all-reduce every step (K=1)",
-                       "graph": not args.no_graph, "overlap_segments": overlap and comm,
+                       "graph": not args.no_graph,
+                       "overlap_segments": bool(comm and len(step.segments) > 1),
                        "graph_comm": bool(getattr(step, "graph_comm", graph_comm) and comm), "bucket_mb": args.bucket_mb,
-                       "grad_comm_dtype": args.comm_dtype, "step": "kubeml_amd.engine.dp.make_train_step"},
+                       "grad_comm_dtype": plan.wire if plan is not None else args.comm_dtype,
+                       "comm_plan": plan.tag() if plan is not None else None,
+                       "comm_plan_source": plan.source if plan is not None else None,
+                       "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
         if epoch is not None:
             out.update(epoch)
             out["epoch_vs_baseline"] = round(BASELINE_EPOCH_S / epoch["epoch_time_s"], 2)
+        if comm and step.comm_seconds() > 0:
+            out["allreduce_ms"] = round(step.comm_seconds() * 1e3, 4)
         if in_sync is not None:
             out["ranks_in_sync"] = in_sync
             out["rccl_world"] = dist.get_world_size()

@@ -1,103 +1,388 @@
-// comm.hip — one-shot all-reduce for small buffers over peer-mapped HBM (gfx950, xGMI).
+// comm.hip — peer-memory all-reduce over IPC-mapped HBM (gfx950, xGMI), graph-capturable.
 //
-// RCCL's ring/tree all-reduce pays 2(P-1) latency-bound steps; for the small buffers of this
-// framework (LeNet's 60k parameters, packed BN statistics of a K-AVG round, loss / count
-// scalars) that latency is the whole cost.  The one-shot form: every rank
-// exposes one IPC-shared region in its HBM, copies its input into it, tells every peer
-// "epoch e is ready" with one system-scope store into the peer's flag slot, and then reads the
-// P inputs straight over the fully connected xGMI links and sums them — one hop, no ring.
-// The P inputs are summed in rank order on every rank, so all ranks get bit-identical sums.
+// Every rank of a one-node group exposes ONE IPC-shared region in its HBM; every peer maps it,
+// so on the fully connected xGMI mesh a rank reads any peer's bytes directly.
+// Two algorithms share the region and the synchronisation protocol:
+//
+//   one-shot  (small buffers: LeNet's parameters, BN statistics, loss / count scalars)
+//     copy-in   in -> own slot
+//     reduce    barrier; read all P slots over xGMI, sum in rank order -> out
+//     bytes read per rank: P * n     latency: ONE barrier
+//
+//   two-shot  (large buffers: the 87 MB ResNet-34 gradient; reduce-scatter + all-gather)
+//     copy-in   in -> own slot (fp32, or rounded to bf16 = half the link bytes)
+//     rs        barrier; rank r sums chunk r of all P slots (rank order) -> own slot chunk r + out
+//     ag        barrier; rank r reads chunk q of peer q's slot for every q != r -> out
+//     bytes read per rank: 2 (P-1)/P * n (the ring optimum)     latency: TWO barriers
+//
+// Chunk q is reduced by rank q alone and copied verbatim by the others, so every rank ends with
+// bit-identical values (also with the bf16 wire: a rank's own chunk is widened from the same
+// rounded bf16 it publishes).  Every launch takes a block cap: at the end of a step the whole
+// chip may move bytes; beside a running backward the cap keeps the collective on a few CUs.
 //
 // Region of rank r (hipMalloc, shared with hipIpcGetMemHandle):
-//   [0, 256)                 uint32 flags[64]: flags[p] = last epoch peer p published
-//   [256, 256 + cap)         slot 0   (double buffer selected by epoch parity)
+//   [0, 256)                 uint32 flags[64]: flags[p] = barrier sequence number peer p reached
+//   [256, 256 + cap)         slot 0 (double buffer selected by call parity)
 //   [256 + cap, 256 + 2 cap) slot 1
-// Local control block (not shared): epoch, block ticket, give-up counter.
+// Local control block (not shared), uint32: [0] seq (barriers passed) [1] block ticket
+// [2] failures [3] calls.
 //
-// Two stream-ordered launches per call (both graph-capturable; the epoch lives on the device):
-//   k_os_copyin : in -> own slot[(epoch + 1) & 1]
-//   k_os_reduce : block 0 publishes epoch + 1 to every peer's flags[rank] (release, system
-//                 scope); every block waits until all flags >= epoch + 1 (acquire), sums its
-//                 range of the P slots into out; the last block to finish advances the epoch.
-// Slot reuse is safe with two slots: a rank overwrites slot s again only two calls later,
-// after every peer has published the call in between — which each peer does only after its
-// reads of slot s (previous call, same stream) have completed.
-// No deadlock: a waiting block only needs its peers' block 0 (the first block they dispatch)
-// to run, never another block of its own grid.  The spin is bounded: after ~2^22 polls (~1 s)
-// the block gives up, counts the failure in ctrl[2] and proceeds (wrong sums, no hang);
-// the host checks the counter (kml_oneshot_errors).
+// Barrier b of a call: block 0 of the launch stores seq + b into every peer's flags[rank]
+// (release, system scope); thread 0 of every block polls its own flags until all P are
+// >= seq + b (wrap-safe), then a system-scope acquire.  The last block of a call's final launch
+// advances seq and calls (stream order makes the new values visible to the next launch).
+// Slot reuse is safe with two slots: a rank rewrites slot s two calls later, after passing the
+// next call's first barrier, which every peer enters only after its reads of slot s finished.
+// No deadlock: a waiting block needs only its peers' block 0 (the first block they dispatch).
+//
+// Failure is loud, never a silent wrong sum: a wait is bounded by wall time (s_memrealtime,
+// 100 MHz); on expiry the call writes NaN to its output range AND to the slot bytes peers would
+// read from it, and counts the failure in ctrl[2].  A group with a failure is poisoned: every
+// later call skips the waits (still publishing its flags) and writes NaN, so a late peer reads NaN
+// rather than stale bytes; the host turns ctrl[2] != 0 into an error at its next check
+// (kml_peer_errors).
+//
+// All payload bytes a peer reads are stored write-through at system scope (sc0 sc1) and read
+// with system-scope loads (buffer_load ... sc0 sc1), so no L2 of either GPU can serve stale
+// lines; the 16-byte forms keep the link traffic at full width.
 #include "kml_common.h"
 
 namespace {
 
-constexpr int OS_MAX_RANKS = 8;
-constexpr int OS_FLAGS_BYTES = 256;
-constexpr unsigned OS_SPIN_LIMIT = 1u << 22;
+constexpr int PC_MAX_RANKS = 8;
+constexpr int PC_FLAGS_BYTES = 256;
+constexpr int PC_BLOCK = 256;
+constexpr int PC_AUX_SYS = 17;  // cache-policy bits sc0 | sc1: system-coherent access
+enum { C_SEQ = 0, C_TICKET = 1, C_ERR = 2, C_CALLS = 3 };
 
-struct OsPeers {
-  const char* region[OS_MAX_RANKS];  // every rank's region, mapped into this process
+struct PcPeers {
+  const char* region[PC_MAX_RANKS];  // every rank's region, mapped into this process
 };
 
-// system-coherent 4-byte accesses: the slot bytes cross the xGMI link while other XCDs'
-// L2s of the owner may still hold them, so stores write through (sc0 sc1) and peer loads
-// bypass the caches — no L2 write-back / invalidate of whole XCD caches is needed
-__device__ __forceinline__ void st_sys(float* p, float v) {
-  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ float ld_sys(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc(const char* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-__global__ __launch_bounds__(256) void k_os_copyin(const float* __restrict__ in, char* __restrict__ region,
-                                                   const unsigned* __restrict__ ctrl, long long cap, long long n) {
-  const unsigned e1 = ctrl[0] + 1u;
-  float* dst = reinterpret_cast<float*>(region + OS_FLAGS_BYTES + (e1 & 1u) * cap);
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) st_sys(dst + i, in[i]);
+// ---- wire formats: one 16-byte vector = 4 fp32 or 8 bf16 ---------------------------------
+template <bool BF16>
+struct Wire;
+template <>
+struct Wire<false> {
+  static constexpr int VE = 4;
+  __device__ static uint4 pack(const float (&x)[4]) {
+    return make_uint4(__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3]));
+  }
+  __device__ static void unpack(uint4 w, float (&x)[4]) {
+    x[0] = __uint_as_float(w.x);
+    x[1] = __uint_as_float(w.y);
+    x[2] = __uint_as_float(w.z);
+    x[3] = __uint_as_float(w.w);
+  }
+};
+template <>
+struct Wire<true> {
+  static constexpr int VE = 8;
+  __device__ static uint4 pack(const float (&x)[8]) {
+    return make_uint4(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]), pack_bf2(x[4], x[5]), pack_bf2(x[6], x[7]));
+  }
+  __device__ static void unpack(uint4 w, float (&x)[8]) {
+    x[0] = lo_bf(w.x), x[1] = hi_bf(w.x), x[2] = lo_bf(w.y), x[3] = hi_bf(w.y);
+    x[4] = lo_bf(w.z), x[5] = hi_bf(w.z), x[6] = lo_bf(w.w), x[7] = hi_bf(w.w);
+  }
+};
+
+__device__ __forceinline__ uint4 ld_sys16(__amdgpu_buffer_rsrc_t r, long long off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, PC_AUX_SYS);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, long long off, uint4 w) {
+  __attribute__((ext_vector_type(4))) unsigned v = {w.x, w.y, w.z, w.w};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, PC_AUX_SYS);
 }
 
-__global__ __launch_bounds__(256) void k_os_reduce(float* __restrict__ out, OsPeers peers, char* __restrict__ region,
-                                                   unsigned* __restrict__ ctrl, int rank, int world, long long cap,
-                                                   long long n, float scale) {
-  __shared__ unsigned e1_sh;
-  if (threadIdx.x == 0) e1_sh = __hip_atomic_load(ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  __syncthreads();
-  const unsigned e1 = e1_sh;
-  unsigned* flags = reinterpret_cast<unsigned*>(region);
+// VE fp32 values of `in` starting at element e (zero beyond n); 16-byte loads when aligned
+template <int VE>
+__device__ __forceinline__ void load_in(const float* __restrict__ in, long long e, long long n, bool aligned,
+                                        float (&x)[VE]) {
+  if (aligned && e + VE <= n) {
+#pragma unroll
+    for (int j = 0; j < VE; j += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(in + e + j);
+      x[j] = v.x, x[j + 1] = v.y, x[j + 2] = v.z, x[j + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VE; ++j) x[j] = (e + j < n) ? in[e + j] : 0.f;
+  }
+}
+
+template <int VE>
+__device__ __forceinline__ void store_out(float* __restrict__ out, long long e, long long n, bool aligned,
+                                          const float (&x)[VE], float scale) {
+  if (aligned && e + VE <= n) {
+#pragma unroll
+    for (int j = 0; j < VE; j += 4)
+      *reinterpret_cast<float4*>(out + e + j) =
+          make_float4(x[j] * scale, x[j + 1] * scale, x[j + 2] * scale, x[j + 3] * scale);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VE; ++j)
+      if (e + j < n) out[e + j] = x[j] * scale;
+  }
+}
+
+// Barrier `target` (= seq + b): block 0 publishes, every block's thread 0 waits; returns whether
+// every peer arrived in time (false at once when the group is already poisoned).
+__device__ bool pc_barrier(const PcPeers& peers, const char* region, unsigned* ctrl, int rank, int world,
+                           unsigned target, unsigned long long limit_ticks) {
+  __shared__ int ok_sh;
   if (blockIdx.x == 0 && (int)threadIdx.x < world) {
-    // this rank's slot for epoch e1 is complete (k_os_copyin finished: stream order)
+    // every payload byte this rank published before this launch was stored write-through
+    // and completed in stream order; the release orders the flag after them
     unsigned* peer_flags = reinterpret_cast<unsigned*>(const_cast<char*>(peers.region[threadIdx.x]));
-    __hip_atomic_store(peer_flags + rank, e1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(peer_flags + rank, target, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x == 0) {
-    unsigned polls = 0;
-    for (int p = 0; p < world; ++p) {
-      while (__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e1 > 0x7fffffffu &&
-             polls < OS_SPIN_LIMIT) {  // wrap-safe "flag < e1"
+    int ok = __hip_atomic_load(ctrl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    const unsigned* flags = reinterpret_cast<const unsigned*>(region);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int p = 0; p < world && ok; ++p) {
+      while ((int)(__hip_atomic_load(flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit_ticks) {
+          ok = 0;
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
-        ++polls;
       }
     }
-    if (polls >= OS_SPIN_LIMIT) __hip_atomic_fetch_add(ctrl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ok) __hip_atomic_fetch_add(ctrl + C_ERR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acquire at system scope: nothing this CU caches of the peers' regions survives
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ok_sh = ok;
   }
   __syncthreads();
-  const long long off = OS_FLAGS_BYTES + (long long)(e1 & 1u) * cap;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    float acc = 0.f;
-    for (int p = 0; p < world; ++p)  // rank order on every rank: identical sums everywhere
-      acc += ld_sys(reinterpret_cast<const float*>(peers.region[p] + off) + i);
-    out[i] = acc * scale;
-  }
-  // the last block to finish advances the epoch (every block has read it at its start)
+  return ok_sh != 0;
+}
+
+// the last block of a call's final launch advances the barrier sequence and the call count
+__device__ void pc_finish_call(unsigned* ctrl, unsigned barriers) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(ctrl + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(ctrl + C_TICKET, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
-      __hip_atomic_store(ctrl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctrl, e1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctrl + C_TICKET, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned s = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned c = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctrl + C_CALLS, c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctrl + C_SEQ, s + barriers, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+}
+
+__device__ __forceinline__ const char* slot_of(const char* region, unsigned calls, long long cap) {
+  return region + PC_FLAGS_BYTES + (long long)(calls & 1u) * cap;
+}
+
+// in (n fp32) -> own slot as nvec wire vectors (zero padding beyond n)
+template <bool BF16>
+__global__ __launch_bounds__(PC_BLOCK) void k_pc_copyin(const float* __restrict__ in, char* __restrict__ region,
+                                                        const unsigned* __restrict__ ctrl, long long cap, long long n,
+                                                        long long nvec, int aligned) {
+  using W = Wire<BF16>;
+  constexpr int VE = W::VE;
+  const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // a poisoned rank publishes NaN, so a late peer reading this slot cannot sum stale bytes
+  const bool poisoned = __hip_atomic_load(ctrl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  const auto r = pc_rsrc(slot_of(region, calls, cap), cap);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float x[VE];
+    load_in<VE>(in, v * VE, n, aligned != 0, x);
+    if (poisoned)
+#pragma unroll
+      for (int j = 0; j < VE; ++j) x[j] = __builtin_nanf("");
+    st_sys16(r, v * 16, W::pack(x));
+  }
+}
+
+// one-shot: out[0, n) = scale * sum over ranks (rank order) of the slots' first nvec vectors
+template <bool BF16, int P>
+__global__ __launch_bounds__(PC_BLOCK) void k_pc_oneshot(float* __restrict__ out, PcPeers peers, char* region,
+                                                         unsigned* ctrl, int rank, long long cap, long long n,
+                                                         long long nvec, float scale, int aligned,
+                                                         unsigned long long limit) {
+  using W = Wire<BF16>;
+  constexpr int VE = W::VE;
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool ok = pc_barrier(peers, region, ctrl, rank, P, seq + 1u, limit);
+  __amdgpu_buffer_rsrc_t rs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(slot_of(peers.region[p], calls, cap), cap);
+  const auto own = pc_rsrc(slot_of(region, calls, cap), cap);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float acc[VE];
+    if (ok) {
+      uint4 w[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) w[p] = ld_sys16(rs[p], v * 16);
+      W::unpack(w[0], acc);
+#pragma unroll
+      for (int p = 1; p < P; ++p) {
+        float x[VE];
+        W::unpack(w[p], x);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) acc[j] += x[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VE; ++j) acc[j] = __builtin_nanf("");
+      st_sys16(own, v * 16, W::pack(acc));  // a late peer reads NaN, never a stale slot
+    }
+    store_out<VE>(out, v * VE, n, aligned != 0, acc, scale);
+  }
+  pc_finish_call(ctrl, 1u);
+}
+
+// two-shot, reduce-scatter: chunk `rank` (cv vectors) summed over the P slots in rank order,
+// published back into the own slot (write-through) and widened into out
+template <bool BF16, int P>
+__global__ __launch_bounds__(PC_BLOCK) void k_pc_rs(float* __restrict__ out, PcPeers peers, char* region,
+                                                    unsigned* ctrl, int rank, long long cap, long long n, long long cv,
+                                                    float scale, int aligned, unsigned long long limit) {
+  using W = Wire<BF16>;
+  constexpr int VE = W::VE;
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool ok = pc_barrier(peers, region, ctrl, rank, P, seq + 1u, limit);
+  __amdgpu_buffer_rsrc_t rs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(slot_of(peers.region[p], calls, cap), cap);
+  const auto own = pc_rsrc(slot_of(region, calls, cap), cap);
+  const long long base = (long long)rank * cv;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < cv; v += stride) {
+    const long long g = base + v;  // global vector index
+    float acc[VE];
+    if (ok) {
+      uint4 w[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) w[p] = ld_sys16(rs[p], g * 16);
+      W::unpack(w[0], acc);
+#pragma unroll
+      for (int p = 1; p < P; ++p) {
+        float x[VE];
+        W::unpack(w[p], x);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) acc[j] += x[j];
+      }
+      const uint4 red = W::pack(acc);
+      st_sys16(own, g * 16, red);
+      W::unpack(red, acc);  // the exact wire value every peer will read
+    } else {
+#pragma unroll
+      for (int j = 0; j < VE; ++j) acc[j] = __builtin_nanf("");
+      st_sys16(own, g * 16, W::pack(acc));  // peers gathering this chunk read NaN
+    }
+    store_out<VE>(out, g * VE, n, aligned != 0, acc, scale);
+  }
+}
+
+// two-shot, all-gather: every chunk q != rank copied from peer q's slot (its reduced chunk)
+template <bool BF16, int P>
+__global__ __launch_bounds__(PC_BLOCK) void k_pc_ag(float* __restrict__ out, PcPeers peers, char* region,
+                                                    unsigned* ctrl, int rank, long long cap, long long n, long long cv,
+                                                    float scale, int aligned, unsigned long long limit) {
+  using W = Wire<BF16>;
+  constexpr int VE = W::VE;
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool ok = pc_barrier(peers, region, ctrl, rank, P, seq + 2u, limit);
+  __amdgpu_buffer_rsrc_t rs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(slot_of(peers.region[p], calls, cap), cap);
+  const long long total = (long long)(P - 1) * cv;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < total; j += stride) {
+    int q = (int)(j / cv);
+    const long long v = j - (long long)q * cv;
+    q += (q >= rank);
+    const long long g = (long long)q * cv + v;
+    float x[VE];
+    if (ok) {
+      uint4 w = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int p = 0; p < P; ++p)  // uniform-index select keeps the descriptors in SGPRs
+        if (p == q) w = ld_sys16(rs[p], g * 16);
+      W::unpack(w, x);
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < VE; ++jj) x[jj] = __builtin_nanf("");
+    }
+    store_out<VE>(out, g * VE, n, aligned != 0, x, scale);
+  }
+  pc_finish_call(ctrl, 2u);
+}
+
+// side-stream HBM streamer for the interference probe: `passes` copies of n 16-byte vectors
+__global__ __launch_bounds__(PC_BLOCK) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          long long n, int passes) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (int it = 0; it < passes; ++it)
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+      uint4 v = src[i];
+      v.x += (unsigned)it;
+      dst[i] = v;
+    }
+}
+
+template <bool BF16, int P>
+hipError_t launch_all(const float* in, float* out, const PcPeers& peers, char* region, unsigned* ctrl, int rank,
+                      long long cap, long long n, float scale, int algo, int max_blocks, unsigned long long limit,
+                      hipStream_t s) {
+  constexpr int VE = Wire<BF16>::VE;
+  const int aligned = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  auto grid_for = [&](long long items) {
+    long long g = (items + PC_BLOCK - 1) / PC_BLOCK;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+  };
+  if (algo == 0) {
+    const long long nvec = (n + VE - 1) / VE;
+    if (nvec * 16 > cap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pc_copyin<BF16>, dim3(grid_for(nvec)), dim3(PC_BLOCK), 0, s, in, region, ctrl, cap, n, nvec,
+                       aligned);
+    hipLaunchKernelGGL((k_pc_oneshot<BF16, P>), dim3(grid_for(nvec)), dim3(PC_BLOCK), 0, s, out, peers, region, ctrl,
+                       rank, cap, n, nvec, scale, aligned, limit);
+  } else {
+    const long long cv = ((n + VE - 1) / VE + P - 1) / P;  // vectors per chunk
+    const long long nvec = cv * P;
+    if (nvec * 16 > cap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pc_copyin<BF16>, dim3(grid_for(nvec)), dim3(PC_BLOCK), 0, s, in, region, ctrl, cap, n, nvec,
+                       aligned);
+    hipLaunchKernelGGL((k_pc_rs<BF16, P>), dim3(grid_for(cv)), dim3(PC_BLOCK), 0, s, out, peers, region, ctrl, rank,
+                       cap, n, cv, scale, aligned, limit);
+    hipLaunchKernelGGL((k_pc_ag<BF16, P>), dim3(grid_for((long long)(P - 1) * cv)), dim3(PC_BLOCK), 0, s, out, peers,
+                       region, ctrl, rank, cap, n, cv, scale, aligned, limit);
+  }
+  return hipGetLastError();
+}
+
+template <bool BF16>
+hipError_t launch_world(int world, const float* in, float* out, const PcPeers& peers, char* region, unsigned* ctrl,
+                        int rank, long long cap, long long n, float scale, int algo, int max_blocks,
+                        unsigned long long limit, hipStream_t s) {
+  switch (world) {
+#define PC_CASE(P) \
+  case P:          \
+    return launch_all<BF16, P>(in, out, peers, region, ctrl, rank, cap, n, scale, algo, max_blocks, limit, s);
+    PC_CASE(1) PC_CASE(2) PC_CASE(3) PC_CASE(4) PC_CASE(5) PC_CASE(6) PC_CASE(7) PC_CASE(8)
+#undef PC_CASE
+    default:
+      return hipErrorInvalidValue;
   }
 }
 
@@ -106,13 +391,13 @@ __global__ __launch_bounds__(256) void k_os_reduce(float* __restrict__ out, OsPe
 // ---- IPC regions ---------------------------------------------------------------------
 KML_API int kml_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
-// region (flags + 2 slots of cap bytes) + zeroed local control block [epoch, ticket, errors]
-KML_API int kml_oneshot_alloc(long long cap, void** region, void** ctrl) {
-  if (cap <= 0 || cap % 16) return (int)hipErrorInvalidValue;
+// region (flags + 2 slots of cap bytes) + zeroed local control block
+KML_API int kml_peer_alloc(long long cap, void** region, void** ctrl) {
+  if (cap <= 0 || cap % 16 || cap >= (1ll << 31)) return (int)hipErrorInvalidValue;
   *region = nullptr;
   *ctrl = nullptr;
-  hipError_t e = hipMalloc(region, OS_FLAGS_BYTES + 2 * cap);
-  if (e == hipSuccess) e = hipMemset(*region, 0, OS_FLAGS_BYTES);
+  hipError_t e = hipMalloc(region, PC_FLAGS_BYTES + 2 * cap);
+  if (e == hipSuccess) e = hipMemset(*region, 0, PC_FLAGS_BYTES);
   if (e == hipSuccess) e = hipMalloc(ctrl, 64);
   if (e == hipSuccess) e = hipMemset(*ctrl, 0, 64);
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -124,7 +409,7 @@ KML_API int kml_oneshot_alloc(long long cap, void** region, void** ctrl) {
   return (int)e;
 }
 
-KML_API int kml_oneshot_free(void* region, void* ctrl) {
+KML_API int kml_peer_free(void* region, void* ctrl) {
   hipError_t e = hipSuccess;
   if (region) e = hipFree(region);
   if (ctrl) {
@@ -146,29 +431,57 @@ KML_API int kml_ipc_open(const void* handle, void** ptr_out) {
 
 KML_API int kml_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
-// give-up count of the bounded spins so far (host-side health check; synchronises)
-KML_API int kml_oneshot_errors(const void* ctrl, unsigned* out) {
-  return (int)hipMemcpy(out, reinterpret_cast<const unsigned*>(ctrl) + 2, sizeof(unsigned), hipMemcpyDeviceToHost);
+// failed (timed-out) waits so far; non-zero = the group is poisoned (synchronises)
+KML_API int kml_peer_errors(const void* ctrl, unsigned* out) {
+  return (int)hipMemcpy(out, reinterpret_cast<const unsigned*>(ctrl) + C_ERR, sizeof(unsigned),
+                        hipMemcpyDeviceToHost);
 }
 
-// out = scale * sum over ranks of in (n floats, n * 4 <= cap); regions[world]: every rank's
-// region as mapped in this process (own region at [rank]).  in and out may alias.
-KML_API int kml_oneshot_allreduce(const float* in, float* out, const void* const* regions, void* region, void* ctrl,
-                                  int rank, int world, long long cap, long long n, float scale, hipStream_t s) {
-  if (world < 1 || world > OS_MAX_RANKS || rank < 0 || rank >= world || n < 0 || n * 4 > cap || cap % 16)
+// out = scale * sum over ranks of in (n fp32; in and out may alias).
+// regions[world]: every rank's region as mapped here (own at [rank]).  algo 0 = one-shot,
+// 1 = two-shot.  wire_bf16: the slots carry bf16 (half the link bytes; sums stay fp32).
+// max_blocks caps every launch's grid; timeout_s bounds each barrier wait.
+KML_API int kml_peer_allreduce(const float* in, float* out, const void* const* regions, void* region, void* ctrl,
+                               int rank, int world, long long cap, long long n, float scale, int algo, int wire_bf16,
+                               int max_blocks, double timeout_s, hipStream_t s) {
+  if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || n < 0 || cap % 16 || max_blocks < 1 ||
+      (algo != 0 && algo != 1) || !(timeout_s > 0.0))
     return (int)hipErrorInvalidValue;
-  OsPeers peers = {};
+  if (n == 0) return (int)hipSuccess;
+  PcPeers peers = {};
   for (int p = 0; p < world; ++p) {
     if (!regions[p]) return (int)hipErrorInvalidValue;
     peers.region[p] = reinterpret_cast<const char*>(regions[p]);
   }
   if (peers.region[rank] != region) return (int)hipErrorInvalidValue;
-  unsigned grid = (unsigned)((n + 1023) / 1024);
-  if (grid < 1) grid = 1;
-  if (grid > 128) grid = 128;
-  hipLaunchKernelGGL(k_os_copyin, dim3(grid), dim3(256), 0, s, in, reinterpret_cast<char*>(region),
-                     reinterpret_cast<const unsigned*>(ctrl), cap, n);
-  hipLaunchKernelGGL(k_os_reduce, dim3(grid), dim3(256), 0, s, out, peers, reinterpret_cast<char*>(region),
-                     reinterpret_cast<unsigned*>(ctrl), rank, world, cap, n, scale);
+  const double ticks = timeout_s * 1.0e8;  // s_memrealtime runs at 100 MHz
+  const unsigned long long limit = ticks > 1.8e19 ? ~0ull : (unsigned long long)ticks;
+  hipError_t e = wire_bf16
+                     ? launch_world<true>(world, in, out, peers, reinterpret_cast<char*>(region),
+                                          reinterpret_cast<unsigned*>(ctrl), rank, cap, n, scale, algo, max_blocks,
+                                          limit, s)
+                     : launch_world<false>(world, in, out, peers, reinterpret_cast<char*>(region),
+                                           reinterpret_cast<unsigned*>(ctrl), rank, cap, n, scale, algo, max_blocks,
+                                           limit, s);
+  return (int)e;
+}
+
+// device wall-clock stamp (100 MHz ticks) into buf[idx]: brackets the collectives inside a
+// captured step so their time is known without events or a host sync
+__global__ void k_stamp(unsigned long long* buf, int idx) {
+  if (threadIdx.x == 0) buf[idx] = __builtin_amdgcn_s_memrealtime();
+}
+
+KML_API int kml_stamp(void* buf, int idx, hipStream_t s) {
+  if (!buf || idx < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, reinterpret_cast<unsigned long long*>(buf), idx);
+  KML_LAUNCH_CHECK();
+}
+
+// interference probe: `passes` copies of `bytes` (multiple of 16) on `blocks` workgroups
+KML_API int kml_stream_copy(const void* src, void* dst, long long bytes, int blocks, int passes, hipStream_t s) {
+  if (bytes <= 0 || bytes % 16 || blocks < 1 || passes < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stream_copy, dim3(blocks), dim3(PC_BLOCK), 0, s, reinterpret_cast<const uint4*>(src),
+                     reinterpret_cast<uint4*>(dst), bytes / 16, passes);
   KML_LAUNCH_CHECK();
 }

@@ -26,7 +26,8 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     use_graph: bool = True, graph_comm: bool = True, overlap: bool = True,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
                     extra_state: Sequence[torch.Tensor] = (), comm_dtype=None,
-                    opt_overlap: Optional[bool] = None, advance=None) -> GraphedTrainStep:
+                    opt_overlap: Optional[bool] = None, advance=None, plan=None, peer=None,
+                    comm_timing: int = 0) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
     pre():  runs first inside the step (e.g. on-device augmentation into ``x``)
@@ -47,12 +48,27 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             None = ``KUBEML_OPT_OVERLAP`` (default OFF: on one MI355X the concurrent
             side-stream update slows the backward's latency-bound kernel stream, ResNet-34
             1.40 -> 1.73-1.81 ms/step whatever its grid; profiles/launch_fusion_r2.md)
+    plan:   a :class:`kubeml_amd.parallel.plan.CommPlan` (transport, schedule, wire, block cap);
+            it overrides ``overlap`` and ``comm_dtype``.  ``backend="peer"`` uses ``peer`` (a
+            :class:`kubeml_amd.parallel.peer.PeerAllReduce` over ``group``) or, when None,
+            creates one sized for the flat gradient — collective over ``group``.
+    comm_timing: T > 0 stamps the collectives on the device every step and samples their time
+            every T-th step (``step.comm_seconds()``; exported as kubeml_allreduce_seconds)
     """
+    comm = world > 1 or force_comm
+    if plan is not None:
+        overlap = plan.schedule == "overlap"
+        comm_dtype = plan.wire_dtype
+        if plan.backend == "peer" and comm and peer is None and torch.cuda.is_available() and space.grad.is_cuda:
+            from ..parallel.peer import PeerAllReduce, slot_bytes
+            peer = PeerAllReduce(group, cap_bytes=slot_bytes(space.grad.numel(), world, "twoshot", comm_dtype),
+                                 device=space.grad.device)
+        if plan.backend != "peer":
+            peer = None
     if comm_dtype is None:
         comm_dtype = torch.bfloat16 if os.environ.get("KUBEML_COMM_DTYPE", "fp32").lower() in (
             "bf16", "bfloat16") else torch.float32
     from ..nn import backward_loss
-    comm = world > 1 or force_comm
     scale = 1.0 / max(world, 1)
 
     def opt_step():
@@ -65,7 +81,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     staged_ok = hasattr(model, "stages") and hasattr(model, "stage_params")
     if opt_overlap is None:
         opt_overlap = os.environ.get("KUBEML_OPT_OVERLAP", "0") == "1"
-    opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm)
+    opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm) and peer is None
                        and getattr(optimizer, "supports_ranges", lambda: False)())
     if advance is not None:
         fused = (not opt_overlap and os.environ.get("KUBEML_ADV_IN_OPT", "1") != "0"
@@ -116,4 +132,6 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
                             graph_comm=graph_comm, comm_dtype=comm_dtype,
                             state_tensors=train_state_tensors(model, space, optimizer, extra_state),
-                            segment_opt=seg_opt, opt_finish=opt_finish)
+                            segment_opt=seg_opt, opt_finish=opt_finish, peer=peer,
+                            schedule=plan.schedule if plan is not None else "overlap",
+                            peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing)

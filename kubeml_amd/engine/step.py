@@ -95,6 +95,17 @@ import os as _os
 _DEBUG_FORK = _os.environ.get("KUBEML_DEBUG_FORK", "0") == "1"
 
 
+class _SideJoin:
+    """'Work' handle of a side-stream collective: waiting joins the side stream into the
+    current one (a graph join edge when captured)."""
+
+    def __init__(self, side):
+        self.side = side
+
+    def wait(self):
+        torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+
+
 class _Snapshot:
     def __init__(self, tensors):
         self.tensors = list(tensors)
@@ -132,7 +143,8 @@ class GraphedTrainStep:
                  segments=None, segment_grads=None, force_comm: bool = False, graph_comm: bool = True,
                  state_tensors: Sequence[torch.Tensor] = (), comm_dtype=torch.float32,
                  segment_opt: Optional[Sequence[Callable[[], None]]] = None,
-                 opt_finish: Optional[Callable[[], None]] = None):
+                 opt_finish: Optional[Callable[[], None]] = None, peer=None, schedule: str = "overlap",
+                 peer_blocks: int = 256, comm_timing: int = 0):
         if segments is None:
             if fwd_bwd is None:
                 raise ValueError("need fwd_bwd or segments")
@@ -166,6 +178,31 @@ class GraphedTrainStep:
         self.segment_opt = list(segment_opt) if segment_opt is not None else None
         self.opt_finish = opt_finish
         self._opt_side = None
+        # peer backend (parallel/peer.py): plain kernels, so the collectives always live in
+        # the step's one graph; "end" = one all-reduce per view after the whole backward on
+        # the compute stream, "overlap" = per segment on a side stream (block-capped)
+        if schedule not in ("end", "overlap"):
+            raise ValueError("schedule must be 'end' or 'overlap'")
+        self.peer = peer if self.comm else None
+        self.schedule = schedule
+        self.peer_blocks = int(peer_blocks)
+        self._peer_side = None
+        if self.peer is not None and self.segment_opt is not None:
+            raise ValueError("the peer backend does not combine with the per-segment optimizer overlap")
+        # comm_timing = T > 0: every T-th replay records HIP events around the collectives
+        # (a separate graph with event nodes), read back lazily -> comm_seconds()
+        self.comm_timing = int(comm_timing)
+        self._replays = 0
+        self._timed = None          # (graph, [(start, end) events]) of the timed variant
+        self._pending_times = []
+        self.comm_time_total = 0.0
+        self.comm_time_samples = 0
+        self._dev = next((t.device for g in self.segment_grads for t in g), None)
+        self._stamps = self._host_stamps = self._pending_stamp = None
+        if self.comm_timing and self.comm and self._dev is not None and self._dev.type == "cuda":
+            # allocated here, never inside a capture
+            self._stamps = torch.zeros(2, dtype=torch.int64, device=self._dev)
+            self._host_stamps = torch.zeros(2, dtype=torch.int64).pin_memory()
         self.g_seg: List[torch.cuda.CUDAGraph] = []
         self.g_all = None
         self.g_opt = None
@@ -198,15 +235,74 @@ class GraphedTrainStep:
             b = self._lp[key] = torch.empty(v.numel(), dtype=torch.bfloat16, device=v.device)
         return b
 
+    # ------------------------------------------------------------------ comm timing
+    def _stamp(self, idx, dev):
+        """Device wall-clock stamp of the collectives' start (0) / end (1) on the current
+        stream (only when ``comm_timing`` is on)."""
+        if self._stamps is None:
+            return
+        from ..parallel.peer import stamp
+        stamp(self._stamps, idx)
+
+    def _sample_comm_time(self):
+        """After a replay: every ``comm_timing``-th step copy the stamps to pinned memory
+        (non-blocking) and fold the previous sample in once its copy has landed."""
+        if self._stamps is None:
+            return
+        self._replays += 1
+        pend = self._pending_stamp
+        if pend is not None and pend.query():
+            t0, t1 = self._host_stamps.tolist()
+            if t1 >= t0:
+                self.comm_time_total += (t1 - t0) / 1e8      # s_memrealtime: 100 MHz
+                self.comm_time_samples += 1
+            self._pending_stamp = pend = None
+        if pend is None and self._replays % self.comm_timing == 0:
+            self._host_stamps.copy_(self._stamps, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending_stamp = ev
+
+    def comm_seconds(self) -> float:
+        """Mean seconds of one step's gradient collectives over the sampled steps (0.0 if
+        unsampled).  Peer/end: the all-reduce itself (peer wait included); overlap: from the
+        first segment's collective to the last one's completion."""
+        return self.comm_time_total / self.comm_time_samples if self.comm_time_samples else 0.0
+
+    # ------------------------------------------------------------------ collectives
+    def _peer_call(self, v):
+        self.peer.all_reduce_(v, algo="twoshot", wire=self.comm_dtype, max_blocks=self.peer_blocks)
+
     def _issue(self, k):
         """Async all-reduce of the gradients finished by segment k (bf16-compressed with
         ``comm_dtype=torch.bfloat16``: the widening back runs in :meth:`_finish_comm`)."""
         if not (self.comm and self._comm_on):
             return []
+        views = list(self._views(k))
+        if not views:
+            return []
+        if self.peer is not None:
+            if self.schedule == "end":
+                return []                     # all views go after the backward (_finish_comm)
+            cur = torch.cuda.current_stream(views[0].device)
+            if self._peer_side is None:
+                self._peer_side = torch.cuda.Stream(views[0].device)
+            side = self._peer_side
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                if k == 0:
+                    self._stamp(0, views[0].device)
+                for v in views:
+                    self._peer_call(v)
+                if k == len(self.segments) - 1:
+                    self._stamp(1, views[0].device)
+            return [_SideJoin(side)]
+        if k == 0:
+            self._stamp(0, views[0].device)
         if self.comm_dtype == torch.float32:
-            return [dist.all_reduce(v, group=self.group, async_op=True) for v in self._views(k)]
+            return [dist.all_reduce(v, group=self.group, async_op=True) for v in views]
         works = []
-        for v in self._views(k):
+        for v in views:
             lp = self._lp_buf(v)
             _narrow(v, lp)
             works.append(dist.all_reduce(lp, group=self.group, async_op=True))
@@ -214,11 +310,20 @@ class GraphedTrainStep:
         return works
 
     def _finish_comm(self, works):
+        if self.peer is not None and self.schedule == "end" and self.comm and self._comm_on:
+            views = [v for k in range(len(self.segments)) for v in self._views(k)]
+            if views:
+                self._stamp(0, views[0].device)
+                for v in views:
+                    self._peer_call(v)
+                self._stamp(1, views[0].device)
         for w in works:
             w.wait()
         for lp, v in self._pending_widen:
             _widen(lp, v)
         self._pending_widen = []
+        if self.peer is None and works and self.comm and self._comm_on and self._dev is not None:
+            self._stamp(1, self._dev)
 
     def _body(self):
         if self.segment_opt is not None:
@@ -282,7 +387,7 @@ class GraphedTrainStep:
     def prime_comm(self):
         """One eager all-reduce of every gradient view (sets up RCCL connections before
         the first capture).  Call on ALL ranks at the same point."""
-        if not self.comm:
+        if not self.comm or self.peer is not None:
             return
         for k in range(len(self.segments)):
             for v in self._views(k):
@@ -363,6 +468,7 @@ class GraphedTrainStep:
                 trace.gpu_span("step (one graph)", e0, trace.gpu_mark(), "gpu:compute")
             else:
                 self.g_all.replay()
+            self._sample_comm_time()
             return self.loss
         if trace.enabled():
             return self._traced_replay()

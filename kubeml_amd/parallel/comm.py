@@ -40,6 +40,9 @@ class Comm:
     def all_gather_object(self, obj) -> list:
         raise NotImplementedError
 
+    def check(self):
+        """Raise if a collective of this group failed asynchronously (peer transport)."""
+
     # ------------------------------------------------------------------ helpers
     def average_(self, tensors: List[torch.Tensor], participate: bool = True) -> int:
         """Masked average: ranks with ``participate=False`` contribute zeros and are
@@ -106,26 +109,37 @@ class TorchComm(Comm):
         self.world = len(self.ranks)
         self._subs: Dict[int, "TorchComm"] = {}
         self._parent = parent
-        self.oneshot = None
+        self.peer = None          # small/large fp32 reductions (enable_peer)
+        self.grad_peer = None     # the train step's gradient all-reduce (engine/dp.py, plan "peer")
 
     @property
     def member(self) -> bool:
         return self.rank >= 0
 
-    def enable_oneshot(self, cap_bytes: Optional[int] = None):
-        """Collective over this group: route fp32 sums/averages of at most ``cap_bytes``
-        (default ``KUBEML_ONESHOT_MB``, 8 MB) through the one-shot peer-memory all-reduce
-        (:mod:`kubeml_amd.parallel.oneshot`) instead of RCCL.  GPU groups of one node only."""
-        if self.world > 1 and self.oneshot is None:
-            from .oneshot import DEFAULT_CAP, OneShotAllReduce
-            self.oneshot = OneShotAllReduce(self.group, cap_bytes or DEFAULT_CAP)
+    def enable_peer(self, cap_bytes: Optional[int] = None):
+        """Collective over this group: route fp32 sums/averages that fit ``cap_bytes`` per slot
+        (default ``KUBEML_PEER_MB``, 8 MB) through the peer-memory all-reduce over xGMI
+        (:mod:`kubeml_amd.parallel.peer`: one-shot for small, two-shot for large buffers)
+        instead of RCCL.  GPU groups of one node only."""
+        if self.world > 1 and self.peer is None:
+            from .peer import DEFAULT_CAP, PeerAllReduce
+            self.peer = PeerAllReduce(self.group, cap_bytes or DEFAULT_CAP)
         return self
+
+    def check(self):
+        """Raise :class:`~kubeml_amd.parallel.peer.PeerCommError` if a peer all-reduce of
+        this group (or of its sub-groups) timed out; synchronises the device."""
+        for p in (self.peer, self.grad_peer):
+            if p is not None:
+                p.check()
+        for c in self._subs.values():
+            c.check()
 
     def all_reduce_(self, t, op="sum"):
         if self.world == 1:
             return t
-        if self.oneshot is not None and op in ("sum", "avg") and self.oneshot.supports(t):
-            return self.oneshot.all_reduce_(t, 1.0 / self.world if op == "avg" else 1.0)
+        if self.peer is not None and op in ("sum", "avg") and self.peer.supports(t):
+            return self.peer.all_reduce_(t, 1.0 / self.world if op == "avg" else 1.0)
         o = getattr(self.dist.ReduceOp, _OPS[op])
         self.dist.all_reduce(t, op=o, group=self.group)
         return t

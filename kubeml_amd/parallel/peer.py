@@ -1,0 +1,172 @@
+"""Peer-memory all-reduce over IPC-mapped HBM on one xGMI-connected node.
+
+On an MI355X node every GPU reaches every peer's HBM over its own xGMI link, so a collective
+can be a handful of ordinary kernels that read the peers' bytes directly — no ring, no proxy
+thread, nothing outside the stream (``csrc/kernels/comm.hip``):
+
+* **one-shot** (small buffers: LeNet's parameters, BN statistics, loss / count scalars): one
+  barrier, then every rank reads all P inputs and sums them — latency-optimal.
+* **two-shot** (large buffers: the flat gradient of a ResNet-34 step): reduce-scatter, then
+  all-gather — each rank reads 2(P-1)/P of the buffer over its 7 links, the ring optimum,
+  with two barriers instead of the ring's 2(P-1) steps.  ``wire=torch.bfloat16`` rounds the
+  slots to bf16 (half the link bytes; sums accumulate in fp32).
+
+Both are stream-ordered launches whose state (barrier sequence, call parity) lives on the
+device, so they capture into a hipGraph and replay; every rank ends with bit-identical
+results (chunk q is reduced once, by rank q, in rank order).  ``max_blocks`` caps every
+launch's grid: the whole chip at the end of a step, a few CUs beside a running backward.
+
+Failure is loud.  A barrier wait is bounded by wall time (``KUBEML_PEER_TIMEOUT_S``, default
+60 s); on expiry the call writes NaN and the group is poisoned — every later call writes NaN
+at once — and :meth:`check` raises :class:`PeerCommError` (a ``MergeError``, the reference's
+merge-failure error, ml/pkg/train/api.go:120-123).  Workers call :meth:`check` at every
+K-AVG round and task end.
+
+Regions are exchanged once, at construction, through the job's process group
+(``all_gather_object`` of the IPC handles): construction is collective over the group.
+
+Reference counterpart: the Go merger's sum of the per-function weights pulled from RedisAI
+(ml/pkg/model/model.go:249-302) and the ParallelSGD average (ml/pkg/model/parallelSGD.go:26-54).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+import torch
+
+from .._native import HIP
+from ..api.errors import MergeError
+
+DEFAULT_CAP = int(float(os.environ.get("KUBEML_PEER_MB", os.environ.get("KUBEML_ONESHOT_MB", "8"))) * 2**20)
+ONESHOT_MAX_BYTES = int(os.environ.get("KUBEML_ONESHOT_MAX_KB", "512")) * 1024
+DEFAULT_TIMEOUT_S = float(os.environ.get("KUBEML_PEER_TIMEOUT_S", "60"))
+ALGOS = {"oneshot": 0, "twoshot": 1}
+
+
+class PeerCommError(MergeError):
+    def __init__(self, message: str):
+        super().__init__(message)
+
+
+def slot_bytes(n: int, world: int, algo: str, wire=torch.float32) -> int:
+    """Slot bytes one call of ``n`` fp32 elements needs (the region holds two slots)."""
+    ve = 8 if wire == torch.bfloat16 else 4
+    nvec = -(-n // ve)
+    if algo == "twoshot":
+        nvec = -(-nvec // world) * world
+    return nvec * 16
+
+
+class PeerAllReduce:
+    """Collective over ``group`` (a torch.distributed group, or None for the world)."""
+
+    MAX_RANKS = 8
+
+    def __init__(self, group=None, cap_bytes: int = DEFAULT_CAP, device: Optional[torch.device] = None,
+                 timeout_s: float = DEFAULT_TIMEOUT_S):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > self.MAX_RANKS:
+            raise ValueError(f"peer all-reduce supports up to {self.MAX_RANKS} ranks (one node)")
+        self.cap = (int(cap_bytes) + 15) // 16 * 16
+        self.timeout_s = float(timeout_s)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(self.device):
+            region, ctrl = ctypes.c_void_p(), ctypes.c_void_p()
+            HIP.call("kml_peer_alloc", "l p p", self.cap, ctypes.addressof(region), ctypes.addressof(ctrl))
+            self.region, self.ctrl = region.value, ctrl.value
+            nb = HIP.raw("kml_ipc_handle_bytes")
+            h = (ctypes.c_char * nb)()
+            HIP.call("kml_ipc_get_handle", "p p", self.region, ctypes.addressof(h))
+            handles: List[bytes] = [b""] * self.world
+            dist.all_gather_object(handles, bytes(h), group=group)
+            self.opened: List[int] = []
+            ptrs = []
+            for p, hb in enumerate(handles):
+                if p == self.rank:
+                    ptrs.append(self.region)
+                    continue
+                buf = (ctypes.c_char * nb).from_buffer_copy(hb)
+                out = ctypes.c_void_p()
+                HIP.call("kml_ipc_open", "p p", ctypes.addressof(buf), ctypes.addressof(out))
+                self.opened.append(out.value)
+                ptrs.append(out.value)
+            self._regions = (ctypes.c_void_p * self.world)(*ptrs)
+            torch.cuda.synchronize(self.device)
+        dist.barrier(group=group)   # every rank has mapped every region before the first call
+
+    # ------------------------------------------------------------------ calls
+    def pick_algo(self, t: torch.Tensor) -> str:
+        return "oneshot" if t.numel() * 4 <= ONESHOT_MAX_BYTES or self.world == 1 else "twoshot"
+
+    def supports(self, t: torch.Tensor, algo: str = "auto", wire=torch.float32) -> bool:
+        if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.device == self.device):
+            return False
+        algo = self.pick_algo(t) if algo == "auto" else algo
+        return slot_bytes(t.numel(), self.world, algo, wire) <= self.cap
+
+    def all_reduce_(self, t: torch.Tensor, scale: float = 1.0, algo: str = "auto", wire=torch.float32,
+                    max_blocks: Optional[int] = None) -> torch.Tensor:
+        """t := scale * sum over ranks of t (in place; every rank, same order; capturable)."""
+        if self.region is None:
+            raise PeerCommError("peer all-reduce used after close()")
+        algo = self.pick_algo(t) if algo == "auto" else algo
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {sorted(ALGOS)} or 'auto'")
+        if wire not in (torch.float32, torch.bfloat16):
+            raise ValueError("wire must be torch.float32 or torch.bfloat16")
+        if not self.supports(t, algo, wire):
+            raise ValueError(f"peer all-reduce: contiguous fp32 tensor on {self.device} needing at most "
+                             f"{self.cap} slot bytes (got {t.numel()} elements, {t.dtype}, {t.device})")
+        HIP.call("kml_peer_allreduce", "p p p p p i i l l f i i i d s", t.data_ptr(), t.data_ptr(),
+                 ctypes.addressof(self._regions), self.region, self.ctrl, self.rank, self.world, self.cap,
+                 t.numel(), float(scale), ALGOS[algo], int(wire == torch.bfloat16), int(max_blocks or 256),
+                 self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
+        return t
+
+    # ------------------------------------------------------------------ health
+    def errors(self) -> int:
+        """Timed-out barrier waits so far (non-zero: the group is poisoned, outputs are NaN)."""
+        if self.ctrl is None:
+            return 0
+        out = ctypes.c_uint(0)
+        HIP.call("kml_peer_errors", "p p", self.ctrl, ctypes.addressof(out))
+        return int(out.value)
+
+    def check(self):
+        """Raise :class:`PeerCommError` if any wait of this group ever timed out (synchronises)."""
+        n = self.errors()
+        if n:
+            raise PeerCommError(f"peer all-reduce: {n} barrier wait(s) on rank {self.rank}/{self.world} timed out "
+                                f"after {self.timeout_s:g} s (a peer stopped calling); results since then are NaN")
+
+    def close(self):
+        """Collective: unmap the peers' regions after everyone is done, then free our own."""
+        if self.region is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self.dist.barrier(group=self.group)
+        for p in self.opened:
+            HIP.call("kml_ipc_close", "p", p)
+        self.opened = []
+        self.dist.barrier(group=self.group)
+        HIP.call("kml_peer_free", "p p", self.region, self.ctrl)
+        self.region = self.ctrl = None
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor, nbytes: int, blocks: int, passes: int = 1):
+    """Interference-probe streamer: ``passes`` copies of ``nbytes`` on ``blocks`` workgroups."""
+    HIP.call("kml_stream_copy", "p p l i i s", src.data_ptr(), dst.data_ptr(), int(nbytes), int(blocks), int(passes),
+             torch.cuda.current_stream(src.device).cuda_stream)
+
+
+def stamp(buf: torch.Tensor, idx: int):
+    """Device wall-clock stamp (100 MHz ticks) into ``buf[idx]`` (int64) on the current stream."""
+    if not (buf.is_cuda and buf.dtype == torch.int64 and 0 <= idx < buf.numel()):
+        raise ValueError("stamp: int64 CUDA buffer and an index inside it")
+    HIP.call("kml_stamp", "p i s", buf.data_ptr(), int(idx), torch.cuda.current_stream(buf.device).cuda_stream)

@@ -115,10 +115,10 @@ class Worker:
                                     **kw)
             self.comm = TorchComm()
             self.comm.prepare_subgroups(self.world)
-            if self.use_gpu and os.environ.get("KUBEML_ONESHOT", "0") == "1":
-                # small fp32 reductions (K-AVG rounds of small models, BN statistics, counts)
-                # over the world group go through the one-shot peer-memory all-reduce
-                self.comm.enable_oneshot()
+            if self.use_gpu and os.environ.get("KUBEML_PEER", os.environ.get("KUBEML_ONESHOT", "0")) == "1":
+                # fp32 reductions over the world group (K-AVG rounds, BN statistics, counts) go
+                # through the peer-memory all-reduce over xGMI instead of RCCL
+                self.comm.enable_peer()
         else:
             self.comm = LocalComm()
         self.store = ShardStore(self.store_dir)
@@ -166,6 +166,8 @@ class Worker:
                     if km is not None:
                         self.jobs[job] = km
                         self.job_fn[job] = msg["code_path"]
+            if self.comm is not None:
+                self.comm.check()       # a timed-out peer collective fails the task, loudly
             out = {"ok": True, "result": _jsonable(res), "seconds": time.perf_counter() - t0,
                    "sync_seconds": float(ctx.extra.get("sync_seconds", 0.0)),
                    "start_checksum": ctx.extra.get("start_checksum"),

@@ -322,7 +322,14 @@ class KubeModel(ABC):
                     self.sync_seconds += time.perf_counter() - t0
                 except Exception as e:  # the reference surfaces merge failures as MergeError
                     raise MergeError(e)
+                if self.PEER_CHECK_EVERY and (r + 1) % self.PEER_CHECK_EVERY == 0:
+                    comm.check()     # a timed-out peer collective stops the task within a few rounds
             if grad_rounds:
+                # in-graph gradient all-reduce time (device stamps sampled by the step)
+                cs = [g["step"].comm_seconds() for k, g in self._graphs.items() if k[5]]
+                cs = [c for c in cs if c > 0]
+                if cs:
+                    self.sync_seconds += sum(cs) / len(cs) * grad_rounds
                 t0 = time.perf_counter()
                 with trace.span("average_buffers"):
                     self._averager.average_buffers_(comm)
@@ -454,6 +461,8 @@ class KubeModel(ABC):
 
     # ---- MI355X helper: graph-captured step --------------------------------------------------
     MAX_GRAPHS = 8
+    PEER_CHECK_EVERY = int(os.environ.get("KUBEML_PEER_CHECK_EVERY", "16"))
+    COMM_TIMING = int(os.environ.get("KUBEML_COMM_TIMING", "50"))   # sample the in-graph all-reduce every N steps
 
     def step(self, x, y, loss_fn=None):
         """forward + loss + backward + optimizer step for one batch; on the GPU the first
@@ -481,10 +490,18 @@ class KubeModel(ABC):
             if len(self._graphs) >= self.MAX_GRAPHS:
                 self._graphs.pop(next(iter(self._graphs)))
             xs, ys = x.clone(), y.clone()
+            plan = peer = None
+            if comm is not None:
+                from ..parallel.plan import choose_plan
+                plan = choose_plan(comm.world, self._flat.grad.numel() * 4)
+                peer = getattr(comm, "grad_peer", None) if plan.backend == "peer" else None
             st = make_train_step(self._network, self._flat, self.optimizer, loss_fn, xs, ys,
                                  group=comm.group if comm is not None else None,
                                  world=comm.world if comm is not None else 1,
-                                 graph_comm=os.environ.get("KUBEML_GRAPH_COMM", "1") != "0")
+                                 graph_comm=os.environ.get("KUBEML_GRAPH_COMM", "1") != "0",
+                                 plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0)
+            if st.peer is not None and comm is not None:
+                comm.grad_peer = st.peer          # one gradient transport per group, reused
             st.capture()
             g = self._graphs[key] = {"x": xs, "y": ys, "step": st}
         g["x"].copy_(x, non_blocking=True)

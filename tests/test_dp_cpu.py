@@ -169,3 +169,26 @@ def test_optimizer_overlapped_with_backward_matches_one_update():
     wb, lb = _opt_overlap_run(False)
     assert la == pytest.approx(lb, rel=1e-6, abs=1e-6)
     torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-6)
+
+
+def test_comm_plan_parse_and_choice(tmp_path, monkeypatch):
+    import json as _json
+    from kubeml_amd.parallel.plan import CommPlan, choose_plan, parse_plan
+    p = parse_plan("peer:overlap:bf16:32")
+    assert (p.backend, p.schedule, p.wire, p.max_blocks) == ("peer", "overlap", "bf16", 32)
+    assert p.tag() == "peer:overlap:bf16:32" and p.wire_dtype == torch.bfloat16
+    assert parse_plan("rccl:end:fp32").tag() == "rccl:end:fp32"
+    for bad in ("peer:end", "nccl:end:fp32", "peer:sometimes:fp32", "peer:end:fp16"):
+        with pytest.raises(ValueError):
+            parse_plan(bad)
+    monkeypatch.delenv("KUBEML_COMM_PLAN", raising=False)
+    table = {"choice": {"2": "peer:end:fp32:256", "8": "peer:overlap:bf16:64"}}
+    assert choose_plan(8, 1 << 20, table=table).tag() == "peer:overlap:bf16:64"
+    assert choose_plan(2, 1 << 20, table=table).tag() == "peer:end:fp32:256"
+    assert choose_plan(6, 1 << 20, table=table).tag() == "peer:overlap:bf16:64"     # nearest N
+    assert choose_plan(4, 1 << 20, table={}).source == "default"
+    assert choose_plan(4, 1 << 20, gpu=False).backend == "rccl"
+    monkeypatch.setenv("KUBEML_COMM_PLAN", "rccl:overlap:fp32")
+    assert choose_plan(8, 1 << 20, table=table).tag() == "rccl:overlap:fp32"
+    assert choose_plan(8, 1 << 20, override="peer:end:bf16:128", table=table).tag() == "peer:end:bf16:128"
+    assert CommPlan().tag() == "peer:end:fp32:256"

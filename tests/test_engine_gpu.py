@@ -243,3 +243,79 @@ def test_graphed_optimizer_overlap_matches_end_of_step_update():
     for p, q in zip(la, lb):
         assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (la, lb)
     assert torch.equal(spa.shadow, spa.master.to(torch.bfloat16))
+
+
+def test_bench_peer_plans_rehearsal():
+    """The peer transport inside the captured step (1-rank group: copy-in, reduce-scatter and
+    all-gather kernels run; the link does not): end of step and overlapped with a block cap,
+    fp32 and bf16 wire; the device-stamped all-reduce time is reported."""
+    for spec in ("peer:end:fp32:256", "peer:overlap:bf16:32"):
+        d = _bench("--steps", "30", "--warmup", "2", "--batch", "128", "--force-comm", "--no-epoch",
+                   "--comm-plan", spec, "--comm-timing", "5")
+        assert d["ranks_in_sync"] is True and d["config"]["comm_plan"] == spec, d
+        assert d["config"]["overlap_segments"] is (":overlap:" in spec)
+        assert d["allreduce_ms"] > 0, d
+        assert d["loss_first_last"][1] == d["loss_first_last"][1]
+
+
+def _plan_run(spec, steps=3):
+    """_graphed_run's workload through make_train_step with a comm plan on a 1-rank group."""
+    import torch.distributed as dist
+    from kubeml_amd.engine.dp import make_train_step
+    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.optim import SGD
+    from kubeml_amd.parallel.plan import parse_plan
+    from kubeml_amd.runtime.pool import free_port
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        m = resnet18(10).to(dev)
+        m.train()
+        sp = flatten_module(m)
+        opt = SGD(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        g = torch.Generator(device=dev).manual_seed(11)
+        xs = torch.randn(steps + 2, 32, 32, 32, 8, device=dev, generator=g).to(torch.bfloat16)
+        xs[..., 3:] = 0
+        ys = torch.randint(0, 10, (steps + 2, 32), device=dev, generator=g)
+        x = torch.empty(32, 32, 32, 8, dtype=torch.bfloat16, device=dev)
+        y = torch.empty(32, dtype=torch.int64, device=dev)
+        i = torch.zeros((), dtype=torch.int64, device=dev)
+
+        def pre():
+            x.copy_(xs.index_select(0, i.view(1)).squeeze(0))
+            y.copy_(ys.index_select(0, i.view(1)).squeeze(0))
+
+        def post():
+            i.add_(1)
+        w0 = sp.master.clone()
+        plan = parse_plan(spec) if spec else None
+        step = make_train_step(m, sp, opt, cross_entropy, x, y, pre=pre, post=post, extra_state=[i],
+                               plan=plan, force_comm=plan is not None, world=1)
+        step.capture()
+        losses = [float(step()) for _ in range(steps)]
+        torch.cuda.synchronize()
+        if step.peer is not None:
+            step.peer.check()
+            step.peer.close()
+        return sp.master - w0, losses
+    finally:
+        if own:
+            dist.destroy_process_group()
+
+
+def test_peer_plans_on_one_rank_match_the_local_step():
+    """World 1: the fp32 peer all-reduce is the identity (same updates as no comm, to the conv
+    wgrad's atomic-order noise); the bf16 wire rounds the gradient to bf16 (a small change)."""
+    ub, lb = _plan_run(None)
+    for spec in ("peer:end:fp32:256", "peer:overlap:fp32:16"):
+        ua, la = _plan_run(spec)
+        rel = float((ua - ub).norm() / ub.norm())
+        assert rel < 1e-2, (spec, rel)
+        for p, q in zip(la, lb):
+            assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (spec, la, lb)
+    ua, la = _plan_run("peer:end:bf16:256")
+    rel = float((ua - ub).norm() / ub.norm())
+    assert rel < 5e-2, rel
