@@ -170,7 +170,7 @@ def test_bench_measures_epoch_with_validation():
 
 def test_bench_rccl_rehearsal_overlapped_graph_comm():
     d = _bench("--steps", "8", "--warmup", "2", "--batch", "128", "--force-comm", "--overlap", "on",
-               "--no-epoch")
+               "--no-epoch", "--comm-plan", "rccl:overlap:fp32")
     assert d["ranks_in_sync"] is True and d["config"]["overlap_segments"] is True
     assert d["config"]["graph_comm"] is True and d["rccl_world"] == 1
 
@@ -179,7 +179,7 @@ def test_bench_trace_has_compute_and_comm_tracks(tmp_path):
     """KUBEML_TRACE timeline: per-segment compute spans and per-segment all-reduce spans
     on their own tracks, device-timestamped, each all-reduce starting at its segment's end."""
     d = _bench("--steps", "3", "--warmup", "1", "--batch", "64", "--force-comm", "--overlap", "on", "--no-epoch",
-               "--trace", str(tmp_path))
+               "--trace", str(tmp_path), "--comm-plan", "rccl:overlap:fp32")
     assert d["ranks_in_sync"] is True
     files = list(tmp_path.glob("*.json"))
     assert files
