@@ -500,7 +500,7 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_fin(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C, int acc) {
   extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
   float4* red4 = reinterpret_cast<float4*>(sh);
   float* ka = sh + 4 * NT;
@@ -548,7 +548,10 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_fin(
   }
   for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
-    if (blockIdx.x == 0) { dbeta[c] += sb; dgamma[c] += sg; }
+    if (blockIdx.x == 0) {  // one writer: store (overwrite) or add (accumulate)
+      dbeta[c] = acc ? dbeta[c] + sb : sb;
+      dgamma[c] = acc ? dgamma[c] + sg : sg;
+    }
     const float gm = gamma ? gamma[c] : 1.f;
     ka[c] = gm * rstd[c];
     kb[c] = sb * invM;
@@ -682,7 +685,7 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C, int acc) {
   extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
   float4* red4 = reinterpret_cast<float4*>(sh);
   float* ka = sh + 4 * NT;
@@ -714,7 +717,10 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   else sum_partial_rows<NT>(part, G, 2 * C, kb, red4);
   for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
-    if (blockIdx.x == 0) { dbeta[c] += sb; dgamma[c] += sg; }
+    if (blockIdx.x == 0) {  // one writer: store (overwrite) or add (accumulate)
+      dbeta[c] = acc ? dbeta[c] + sb : sb;
+      dgamma[c] = acc ? dgamma[c] + sg : sg;
+    }
     const float gm = gamma ? gamma[c] : 1.f;
     ka[c] = gm * rstd[c];
     mu[c] = mean[c];
@@ -1103,7 +1109,8 @@ static bool wide_sum(int G, int C) {
 
 static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                                 const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
-                                float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, hipStream_t s) {
+                                float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, int acc,
+                                hipStream_t s) {
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 4);
@@ -1111,7 +1118,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const size_t shm = (4 * TPB + 5 * C) * sizeof(float);
 #define KML_BWD_V(VV)                                                                                          \
   hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, dy, y, x, mean, rstd, gamma, part, \
-                     G, dgamma, dbeta, dx, dres, M, C)
+                     G, dgamma, dbeta, dx, dres, M, C, acc)
     if (V == 1) KML_BWD_V(1);
     else if (V == 2) KML_BWD_V(2);
     else KML_BWD_V(4);
@@ -1123,13 +1130,13 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     long long ab = (M * C / 8 + NT - 1) / NT;
     if (ab > 256) ab = 256;
     hipLaunchKernelGGL(k_bn_bwd_apply_fin<NT>, dim3((unsigned)ab), dim3(NT), (4 * NT + 5 * C) * sizeof(float), s,
-                       dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
+                       dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc);
     KML_LAUNCH_CHECK();
   }
   long long ab = (M * C / 8 + TPB - 1) / TPB;
   if (ab > 256) ab = 256;
   hipLaunchKernelGGL(k_bn_bwd_apply_fin<TPB>, dim3((unsigned)ab), dim3(TPB), (4 * TPB + 5 * C) * sizeof(float), s,
-                     dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C);
+                     dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc);
   KML_LAUNCH_CHECK();
 }
 
@@ -1200,9 +1207,12 @@ KML_API long long kml_bn_bwd_ws_floats(long long M, int C) {
 // ws && counter : partials + in-kernel last-arriver reduce (agent-scope fences)
 // !ws           : block partials + fp32 atomics
 // (ws holds kml_bn_bwd_ws_floats(M, C) floats; *counter == 0 on entry and on exit).
+extern "C" int kml_zero(void* p, long long bytes, hipStream_t s);  // util.hip
+
+// accumulate: dgamma/dbeta += (1) or = (0) this pass's sums
 KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
                        const float* gamma, float* dgamma, float* dbeta, bf16_t* dx, bf16_t* dres, float* ws,
-                       unsigned* counter, long long M, int C, hipStream_t s) {
+                       unsigned* counter, long long M, int C, int accumulate, hipStream_t s) {
   if (C % 8 || C / 8 > TPB) return (int)hipErrorInvalidValue;
   int rpb;
   if (ws && !counter) {  // default: partials, then the apply kernel reduces them (2 launches, no sync)
@@ -1212,9 +1222,15 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
     hipLaunchKernelGGL(k_bn_bwd_reduce2<2>, dim3(gf), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
                        nullptr, M, C, rpb);
     const float* part = maybe_fold(ws, gf, 2 * C, ws + (long long)gf * 2 * C, s);
-    return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, gf, dgamma, dbeta, dx, dres, M, C, s);
+    return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, gf, dgamma, dbeta, dx, dres, M, C, accumulate, s);
   }
   const int g = bwd_blocks(M, C, &rpb);
+  // these two variants reduce INTO dgamma / dbeta (the apply kernel reads them back)
+  if (!accumulate) {  // zeroing kernels, not memset nodes (util.hip kml_zero)
+    int e = kml_zero(dgamma, C * (long long)sizeof(float), s);
+    if (!e) e = kml_zero(dbeta, C * (long long)sizeof(float), s);
+    if (e) return e;
+  }
   if (ws && counter) {  // deterministic: ordered partials + last-arriver reduce
     hipLaunchKernelGGL(k_bn_bwd_reduce2<0>, dim3(g), dim3(TPB), 0, s, dy, y, x, mean, rstd, dgamma, dbeta, ws,
                        counter, M, C, rpb);
@@ -1232,10 +1248,10 @@ KML_API int kml_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const
 KML_API int kml_bn_bwd_apply_partial(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                                      const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
                                      float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, float* fold_ws,
-                                     hipStream_t s) {
+                                     int accumulate, hipStream_t s) {
   if (C % 8 || C / 8 > TPB || G <= 0) return (int)hipErrorInvalidValue;
   part = maybe_fold(part, G, 2 * C, fold_ws, s);
-  return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, s);
+  return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, accumulate, s);
 }
 
 KML_API int kml_relu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {

@@ -5,7 +5,7 @@
 //
 //   FWD   : Y[m=(b,oh,ow)][n=cout]   = sum_k im2col(X)[m][k=(tap,cin)] * W[n][k]
 //   DGRAD : dX[m=(b,ih,iw)][n=cin]   = sum_k dY[(b,oh,ow)][cout] * W[cout][tap][cin],  k=(tap,cout)
-//   WGRAD : dW[m=cout][n=(tap,cin)] += sum_k dY[k=pixel][cout] * im2col(X)[k][n]
+//   WGRAD : dW[m=cout][n=(tap,cin)] (=|+=) sum_k dY[k=pixel][cout] * im2col(X)[k][n]
 //
 // Layouts: activations NHWC bf16 (C % 8 == 0), weights KRSC bf16 ([Cout][KH][KW][Cin]),
 // weight gradients KRSC fp32 — written straight into the flat fp32 gradient buffer that
@@ -37,8 +37,8 @@
 //   partial tile to a slab (fragment order, coalesced float4), releases at agent scope,
 //   takes a ticket; the last arriver acquires, sums the slabs in split order
 //   (deterministic) and runs the epilogue; tickets are reset by the last arriver
-//   (graph-replay safe, no memset per call).  WGRAD: fp32 atomics into the
-//   zeroed-per-step gradient buffer.
+//   (graph-replay safe, no memset per call).  WGRAD uses the same slabs: one writer per
+//   weight-gradient element, stored (or added) without atomics.
 // * Epilogues: FWD bias / ReLU / per-channel BatchNorm sum+sumsq from the fp32 values
 //   (BN needs no statistics pass); DGRAD adds an optional bf16 addend (the other
 //   branch of a residual block) so gradient merges need no add kernel.
@@ -109,10 +109,8 @@ struct ConvArgs {
   // im2col of the 3x3 form is 5/9 zero padding).  fold_c: the FWD/DGRAD output channel col =
   // (pos, c) belongs to BN channel c = col % fold_c, so a partial row is written as fold
   // rows of [sum(fold_c) | sumsq(fold_c)] (BN kernels see ordinary rows of the real
-  // channels).  u_k0 / u_c0: WGRAD rows (p, n) and cols (q, c) scatter-add into the 3x3
-  // gradient dW[n][tap(p, q)][c], tap = (qh - ph + 1, qw - pw + 1).
+  // channels).  The WGRAD of an unrolled conv runs in the plain 3x3 form (prep_wgrad).
   int fold_c;
-  int u_k0, u_c0;
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
@@ -378,28 +376,52 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
                                               int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
 
+  // -------------------------------------------------------- split-K: last arriver reduces
+  // (every mode: the fp32 partial tiles are summed in split order by the last block of a
+  // tile, so FWD/DGRAD outputs and WGRAD weight gradients are bitwise reproducible)
+  if (a.splits > 1) {
+    constexpr int NACC = MR * NR * 4;
+    float* slab = a.slab + ((long long)tile * a.splits) * (256 * NACC);
+    float4* mine = reinterpret_cast<float4*>(slab + (long long)bz * 256 * NACC) + tid * (NACC / 4);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        mine[i * NR + j] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned lastp = (t == (unsigned)a.splits - 1) ? 1u : 0u;
+      if (lastp) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      flag[0] = lastp;
+    }
+    __syncthreads();
+    if (flag[0] == 0) return;
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < a.splits; ++sp) {
+      const float4* src = reinterpret_cast<const float4*>(slab + (long long)sp * 256 * NACC) + tid * (NACC / 4);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          const float4 v = src[i * NR + j];
+          acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
+        }
+    }
+  }
+
   // ---------------------------------------------------------------- WGRAD epilogue
   if constexpr (MODE == WGRAD) {
-    if (a.u_k0) {  // unrolled 2x2 conv: scatter-add into the 3x3 gradient (see ConvArgs)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int col = n0 + wn * WN + j * 16 + fr;
-        if (col >= a.N) continue;
-        const int q = col / a.u_c0, c = col - q * a.u_c0;
-#pragma unroll
-        for (int i = 0; i < MR; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
-            if (row < a.M) {
-              const int p = row / a.u_k0, n = row - p * a.u_k0;
-              const int tap = ((q >> 1) - (p >> 1) + 1) * 3 + ((q & 1) - (p & 1) + 1);
-              atomicAdd(a.dw + ((long long)n * 9 + tap) * a.u_c0 + c, acc[i][j][e]);
-            }
-          }
-      }
-      return;
-    }
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int col = n0 + wn * WN + j * 16 + fr;
@@ -414,56 +436,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
         for (int e = 0; e < 4; ++e) {
           const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
           if (row < a.M) {
+            // one writer per element (split-K partials were summed above): no atomics
             float* p = a.dw + (long long)row * a.KH * a.KW * a.C + coff;
-            if (a.accumulate) atomicAdd(p, acc[i][j][e]);
+            if (a.accumulate) *p += acc[i][j][e];
             else *p = acc[i][j][e];
           }
         }
     }
     return;
   } else {
-    // ------------------------------------------------------ split-K: last arriver reduces
-    if (a.splits > 1) {
-      constexpr int NACC = MR * NR * 4;
-      float* slab = a.slab + ((long long)tile * a.splits) * (256 * NACC);
-      float4* mine = reinterpret_cast<float4*>(slab + (long long)bz * 256 * NACC) + tid * (NACC / 4);
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-          mine[i * NR + j] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned lastp = (t == (unsigned)a.splits - 1) ? 1u : 0u;
-        if (lastp) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        flag[0] = lastp;
-      }
-      __syncthreads();
-      if (flag[0] == 0) return;
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < a.splits; ++sp) {
-        const float4* src = reinterpret_cast<const float4*>(slab + (long long)sp * 256 * NACC) + tid * (NACC / 4);
-#pragma unroll
-        for (int i = 0; i < MR; ++i)
-#pragma unroll
-          for (int j = 0; j < NR; ++j) {
-            const float4 v = src[i * NR + j];
-            acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
-          }
-      }
-    }
-
     // ---------------------------------------------------------- FWD / DGRAD epilogue
     // (entered after a block barrier: the main loops end with one, so LDS is free here)
     // tile geometry: 2x2 waves (SINGLE: one live wave owns the whole tile)
@@ -1420,20 +1401,32 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
   return 0;
 }
 
+// WGRAD overwrites dw (accumulate = 0) or adds to it (1); either way every element has ONE
+// writer — split-K partial tiles go through the slab and are summed in split order by the
+// last block of the tile — so weight gradients are bitwise reproducible and need no zeroed
+// buffer.  An unrolled conv (u_k0 / u_c0: the 1x1 form of a 3x3/s1/p1 conv on a 2x2 map,
+// whose GEMM output would scatter-add 4 positions onto one tap) computes its weight gradient
+// in the plain 3x3 form instead: the same NHWC bytes read as [B,2,2,C], taps gathered by the
+// implicit im2col, one writer per dW element.
 int prep_wgrad(ConvArgs& a, const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate, int u_k0,
-               int u_c0) {
+               int u_c0, float* slab, unsigned* counters) {
   if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
-  if ((u_k0 || u_c0) && (!u_k0 || !u_c0 || K != 4 * u_k0 || C != 4 * u_c0 || KH != 1 || KW != 1))
+  if ((u_k0 || u_c0) && (!u_k0 || !u_c0 || K != 4 * u_k0 || C != 4 * u_c0 || KH != 1 || KW != 1 || H != 1 ||
+                         W != 1))
     return (int)hipErrorInvalidValue;
+  if (u_k0) {  // plain form of the unrolled conv
+    H = W = 2; C = u_c0; K = u_k0; KH = KW = 3; sh = sw = 1; ph = pw = 1;
+  }
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
   a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   set_splits(a, bk, splits);
-  a.accumulate = (a.splits > 1 || u_k0) ? 1 : accumulate;
-  a.u_k0 = u_k0; a.u_c0 = u_c0;
+  if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
+  a.slab = slab; a.counters = counters;
+  a.accumulate = accumulate ? 1 : 0;
   return 0;
 }
 }  // namespace
@@ -1450,7 +1443,8 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               float* dw, int B, int H, int W, int C, int K, int KH,
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
-                              int wvariant, int fold_c, int u_k0, int u_c0, int bnf_mask_out, hipStream_t s) {
+                              int wvariant, int fold_c, int u_k0, int u_c0, int bnf_mask_out, float* wslab,
+                              unsigned* wcounters, int waccumulate, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
@@ -1458,7 +1452,8 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                      grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
                      fold_c, bnf_mask_out);
   if (e) return e;
-  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, 1, u_k0, u_c0);
+  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, u_k0, u_c0,
+                 wslab, wcounters);
   if (e) return e;
   return dispatch_pair(which, ad, aw, s);
 }
@@ -1536,10 +1531,10 @@ KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int
 
 KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                            int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk, int splits, int variant,
-                           int accumulate, int u_k0, int u_c0, hipStream_t s) {
+                           int accumulate, int u_k0, int u_c0, float* slab, unsigned* counters, hipStream_t s) {
   ConvArgs a;
   const int e = prep_wgrad(a, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, accumulate,
-                           u_k0, u_c0);
+                           u_k0, u_c0, slab, counters);
   if (e) return e;
   if (variant) bk = 64;
   return dispatch<WGRAD>(a, bm, bn, bk, variant, s);

@@ -200,16 +200,19 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
   }
 }
 
-// k_ce_bwd (bf16 vector path) that also adds the column sums of dlogits to dbias — the bias
+// k_ce_bwd (bf16 vector path) that also produces the column sums of dlogits — the bias
 // gradient of the Linear that produced the logits (its own column-sum pass is skipped).  The
-// block's 4 rows are summed through LDS ([4][ld] fp32, ld <= 4096), then one fp32 atomic per
-// column per block.
+// block's 4 rows are summed through LDS ([4][ld] fp32, ld <= 4096) into one partial row
+// part[block][C] (plain stores); the last block to arrive (agent-scope ticket) sums the rows
+// in block order and stores (acc = 0) or adds (acc = 1) them into dbias: deterministic, one
+// writer per element, no zeroed buffer needed.
 __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ logits,
                                                      const long long* __restrict__ labels,
                                                      const float* __restrict__ lse, const float* __restrict__ red,
                                                      const float* __restrict__ grad_out, bf16_t* __restrict__ dlogits,
                                                      float* __restrict__ dbias, int B, int C, int ld,
-                                                     long long ignore) {
+                                                     long long ignore, float* __restrict__ part,
+                                                     unsigned* __restrict__ ticket, int acc) {
   extern __shared__ float colsh[];  // [4][ld]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
@@ -241,9 +244,38 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
     if (have) d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
+  float* mine_row = part + (long long)blockIdx.x * C;
+  for (int c = threadIdx.x; c < C; c += 256)
+    mine_row[c] = (colsh[c] + colsh[ld + c]) + (colsh[2 * ld + c] + colsh[3 * ld + c]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned last;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // graph-replay safe
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const int G = (int)gridDim.x;
   for (int c = threadIdx.x; c < C; c += 256) {
-    const float t = (colsh[c] + colsh[ld + c]) + (colsh[2 * ld + c] + colsh[3 * ld + c]);
-    atomicAdd(dbias + c, t);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;   // 4 chains, combined in a fixed order
+    int g = 0;
+    for (; g + 4 <= G; g += 4) {
+      a0 += part[(long long)g * C + c];
+      a1 += part[(long long)(g + 1) * C + c];
+      a2 += part[(long long)(g + 2) * C + c];
+      a3 += part[(long long)(g + 3) * C + c];
+    }
+    for (; g < G; ++g) a0 += part[(long long)g * C + c];
+    const float t = (a0 + a1) + (a2 + a3);
+    dbias[c] = acc ? dbias[c] + t : t;
   }
 }
 
@@ -267,16 +299,17 @@ KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, f
   KML_LAUNCH_CHECK();
 }
 
-// dbias (optional; bf16 logits, ld % 8 == 0, ld <= 4096): += column sums of dlogits
+// dbias (optional; bf16 logits, ld % 8 == 0, ld <= 4096): column sums of dlogits, stored
+// (accumulate = 0) or added (1); needs part = [ceil(B/4)][C] fp32 scratch and a zeroed ticket
 KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
                        const float* grad_out, void* dlogits, int B, int C, int ld, long long ignore, int dtype,
-                       float* dbias, hipStream_t s) {
+                       float* dbias, float* part, unsigned* ticket, int accumulate, hipStream_t s) {
   if (ld < C) return (int)hipErrorInvalidValue;
   dim3 g((B + 3) / 4);
   if (dbias) {
-    if (dtype != 0 || ld % 8 || ld > 4096) return (int)hipErrorInvalidValue;
+    if (dtype != 0 || ld % 8 || ld > 4096 || !part || !ticket) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ce_bwd_bias, g, dim3(256), (size_t)4 * ld * sizeof(float), s, (const bf16_t*)logits, labels,
-                       ws, out3, grad_out, (bf16_t*)dlogits, dbias, B, C, ld, ignore);
+                       ws, out3, grad_out, (bf16_t*)dlogits, dbias, B, C, ld, ignore, part, ticket, accumulate);
     KML_LAUNCH_CHECK();
   }
   if (dtype == 0)

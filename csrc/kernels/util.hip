@@ -241,3 +241,48 @@ KML_API int kml_zero(void* p, long long bytes, hipStream_t s) {
                      aligned);
   KML_LAUNCH_CHECK();
 }
+
+// Zero up to ZR_MAX fp32 ranges of one buffer in ONE launch (the flat gradient buffer's
+// accumulate-only parameters, nn/flat.py FlatParamSpace.zero_grad): ranges passed by value,
+// so nothing is copied to the device and the launch captures into a graph as one node.
+namespace {
+constexpr int ZR_MAX = 96;
+struct ZeroRanges {
+  long long off[ZR_MAX];  // element offsets (multiples of 4: 16-byte aligned)
+  int n[ZR_MAX];          // element counts
+  int count;
+};
+__global__ __launch_bounds__(256) void k_zero_ranges(float* __restrict__ base, ZeroRanges zr) {
+  // one block-row per range, grid-stride inside it
+  for (int r = blockIdx.y; r < zr.count; r += gridDim.y) {
+    float* p = base + zr.off[r];
+    const int n = zr.n[r];
+    const int n4 = n >> 2;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x)
+      reinterpret_cast<float4*>(p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = (n4 << 2) + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0.f;
+  }
+}
+}  // namespace
+
+KML_API int kml_zero_ranges_max() { return ZR_MAX; }
+
+// offs / ns: host arrays of `count` ranges (count <= kml_zero_ranges_max())
+KML_API int kml_zero_ranges(float* base, const long long* offs, const int* ns, int count, hipStream_t s) {
+  if (count < 0 || count > ZR_MAX || (((unsigned long long)base) & 15ull)) return (int)hipErrorInvalidValue;
+  if (count == 0) return (int)hipSuccess;
+  ZeroRanges zr = {};
+  int widest = 1;
+  for (int i = 0; i < count; ++i) {
+    if (offs[i] % 4 || ns[i] < 0) return (int)hipErrorInvalidValue;
+    zr.off[i] = offs[i];
+    zr.n[i] = ns[i];
+    if (ns[i] > widest) widest = ns[i];
+  }
+  zr.count = count;
+  int gx = (widest / 4 + 255) / 256;
+  if (gx > 64) gx = 64;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(k_zero_ranges, dim3(gx, count), dim3(256), 0, s, base, zr);
+  KML_LAUNCH_CHECK();
+}

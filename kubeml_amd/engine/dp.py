@@ -71,9 +71,14 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     from ..nn import backward_loss
     scale = 1.0 / max(world, 1)
 
+    fold = None           # (ctr, batch, n) advanced inside the fused SGD launch (per call)
+
     def opt_step():
         optimizer.set_grad_scale(scale)
-        optimizer.step()
+        if fold is not None:
+            optimizer.step(advance=fold)
+        else:
+            optimizer.step()
         if post is not None:
             post()
 
@@ -86,7 +91,9 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     if advance is not None:
         fused = (not opt_overlap and os.environ.get("KUBEML_ADV_IN_OPT", "1") != "0"
                  and getattr(optimizer, "fuse_advance", lambda *a: False)(*advance))
-        if not fused:
+        if fused:
+            fold = tuple(advance)
+        else:
             user_post = post
 
             def post():
@@ -102,9 +109,18 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                 pre()
             space.zero_grad()
         staged = StagedForwardBackward(model.stages(), lambda out: loss_fn(out, y), lambda: x, pre=pre0)
-        segs = [staged.segment(k) for k in range(staged.n_segments)]
         sp = model.stage_params()
         stage_of_seg = [sp[len(sp) - 1 - k] for k in range(len(sp))]
+
+        def _seg(k):
+            run = staged.segment(k)
+
+            def seg():
+                out = run()
+                space.finish_grads(stage_of_seg[k])   # this stage's gradients are final
+                return out
+            return seg
+        segs = [_seg(k) for k in range(staged.n_segments)]
         seg_grads = [[space.grad_view(ps)] for ps in stage_of_seg]
         fwd_bwd = None
         if opt_overlap:
@@ -126,6 +142,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             space.zero_grad()
             loss = loss_fn(model(x), y)
             backward_loss(loss)
+            space.finish_grads()
             return loss
     optimizer.set_grad_scale(scale)
     return GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,

@@ -250,23 +250,28 @@ class GraphedTrainStep:
         if self._stamps is None:
             return
         self._replays += 1
+        self._fold_stamp()
+        if self._pending_stamp is None and self._replays % self.comm_timing == 0:
+            self._host_stamps.copy_(self._stamps, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending_stamp = ev
+
+    def _fold_stamp(self):
         pend = self._pending_stamp
         if pend is not None and pend.query():
             t0, t1 = self._host_stamps.tolist()
             if t1 >= t0:
                 self.comm_time_total += (t1 - t0) / 1e8      # s_memrealtime: 100 MHz
                 self.comm_time_samples += 1
-            self._pending_stamp = pend = None
-        if pend is None and self._replays % self.comm_timing == 0:
-            self._host_stamps.copy_(self._stamps, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._pending_stamp = ev
+            self._pending_stamp = None
 
     def comm_seconds(self) -> float:
         """Mean seconds of one step's gradient collectives over the sampled steps (0.0 if
         unsampled).  Peer/end: the all-reduce itself (peer wait included); overlap: from the
         first segment's collective to the last one's completion."""
+        if self._stamps is not None:
+            self._fold_stamp()          # a sample whose copy has landed since the last replay
         return self.comm_time_total / self.comm_time_samples if self.comm_time_samples else 0.0
 
     # ------------------------------------------------------------------ collectives

@@ -14,8 +14,12 @@ Layout rules
   shape (``[Cout, Cin, KH, KW]``).  ``state_dict()`` therefore carries exactly the
   torchvision names and shapes, and torch optimizers / ``load_state_dict`` keep
   working.
-* ``p.grad`` is bound to the matching view of the grad buffer; our backward kernels
-  accumulate into it (``+=``), which is torch's ``.grad`` accumulation semantics.
+* ``p.grad`` is bound to the matching view of the grad buffer with torch's
+  zero-then-accumulate semantics, but the buffer is not memset every step: producers
+  that can store (conv / linear weight gradients, BN dgamma/dbeta, the fused CE bias
+  gradient) ask :func:`grad_out` whether to overwrite or add; ``zero_grad()`` zeroes only
+  the regions whose producers can only add (learned from the previous backward), in one
+  launch; ``finish_grads()`` zeroes any overwrite region nobody wrote this step.
 * ``p._kml_shadow`` is the bf16 copy in storage layout that the forward kernels
   consume; it is refreshed by the fused optimizers, or lazily when ``p._version``
   moved (a foreign optimizer or ``load_state_dict`` wrote the master).
@@ -32,6 +36,7 @@ Layout rules
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Iterable, List, Optional
 
 import torch
@@ -121,6 +126,11 @@ class FlatParamSpace:
         if self.i64_buffers:
             self._bind_i64()
         self.refresh_shadow()
+        self._index = {id(p): i for i, p in enumerate(self.params)}
+        self._overwriters: set = set()   # param index -> its producer stored (grad_out) last backward
+        self._accumulators: set = set()  # ... went through grad_storage_of (add-only producer)
+        self._fresh: set = set()         # overwriters not yet written since zero_grad()
+        self._zeroed_once = False
 
     def _bind_i64(self):
         """All int64 buffers as consecutive elements of one arena (one pointer for the
@@ -165,13 +175,85 @@ class FlatParamSpace:
         for p in self.params:
             p.grad = p._kml_grad
 
-    def zero_grad(self):
-        if self.device.type == "cuda":
-            from ..ops import kernels as K
+    def _region(self, i):
+        o, n = self.offsets[i]
+        return o, -(-n // ALIGN) * ALIGN
+
+    def _zero_params(self, idx):
+        """Zero the grad regions of the given parameter indices (merged runs, one launch per
+        ``kml_zero_ranges_max()`` runs; the whole buffer when that is fewer launches)."""
+        if not idx:
+            return
+        runs = []
+        for i in sorted(idx):
+            o, n = self._region(i)
+            if runs and runs[-1][0] + runs[-1][1] == o:
+                runs[-1][1] += n
+            else:
+                runs.append([o, n])
+        from ..ops import kernels as K
+        if len(runs) > K.zero_ranges_max():
             K.memset_(self.grad)
         else:
+            K.zero_ranges_(self.grad, runs)
+
+    def zero_grad(self):
+        """torch semantics (every gradient reads as zero until its first producer writes),
+        at the cost of zeroing only what an add-only producer will accumulate into."""
+        if self.device.type != "cuda":
             self.grad.zero_()
+        elif not self._zeroed_once or os.environ.get("KUBEML_FULL_ZERO") == "1":
+            from ..ops import kernels as K
+            K.memset_(self.grad)          # first step: learn which producers overwrite
+            self._zeroed_once = True
+            self._fresh = set()
+        else:
+            self._zero_params([i for i in range(len(self.params)) if i not in self._overwriters])
+            self._fresh = set(self._overwriters)
         self.rebind_grads()
+
+    def grad_out(self, p) -> bool:
+        """For a producer that can store: True = add to the region, False = overwrite it
+        (the first write after zero_grad())."""
+        i = self._index.get(id(p))
+        if i is None:
+            return True
+        if i not in self._accumulators:
+            self._overwriters.add(i)
+        if i in self._fresh:
+            self._fresh.discard(i)
+            return False
+        return True
+
+    def grad_for_add(self, p):
+        """For an add-only producer: make sure the region holds zeros if it is fresh, and
+        remember that this parameter must be zeroed by zero_grad() from now on."""
+        i = self._index.get(id(p))
+        if i is None:
+            return
+        self._accumulators.add(i)
+        self._overwriters.discard(i)
+        if i in self._fresh:
+            self._fresh.discard(i)
+            self._zero_params([i])
+
+    def finish_grads(self, params=None):
+        """Zero the regions of overwrite parameters nobody wrote since zero_grad() (a
+        parameter without a gradient this step); call before the gradients are consumed."""
+        if not self._fresh:
+            return
+        if params is None:
+            left = set(self._fresh)
+        else:
+            left = {self._index[id(p)] for p in params if id(p) in self._index} & self._fresh
+        self._fresh -= left
+        self._zero_params(left)
+
+    def finish_grads_range(self, start: int, end: int):
+        """finish_grads for the parameters whose regions lie in flat elements [start, end)."""
+        if self._fresh:
+            self.finish_grads([p for i, p in enumerate(self.params)
+                               if start <= self.offsets[i][0] < end])
 
     def buckets(self, bucket_bytes: int):
         """Contiguous [start, end) element ranges of the grad buffer, ~bucket_bytes each,
@@ -257,15 +339,39 @@ def shadow_of(p: torch.nn.Parameter) -> torch.Tensor:
 
 
 def grad_storage_of(p: torch.nn.Parameter) -> torch.Tensor:
-    """fp32 storage-layout grad region of p (zeroed and re-bound if p.grad was reset)."""
+    """fp32 storage-layout grad region of p for a producer that ADDS into it (zeroed if
+    fresh, re-bound if p.grad was reset)."""
     ensure_param_ready(p)
     if p.grad is None:
         p._kml_grad_storage.zero_()
         p.grad = p._kml_grad
+    p._kml_flat.grad_for_add(p)
     return p._kml_grad_storage
+
+
+def grad_out(p: torch.nn.Parameter):
+    """(fp32 storage-layout grad region, accumulate) for a producer that can either store
+    (accumulate False: first write since zero_grad) or add."""
+    ensure_param_ready(p)
+    if p.grad is None:
+        p._kml_grad_storage.zero_()
+        p.grad = p._kml_grad
+    return p._kml_grad_storage, p._kml_flat.grad_out(p)
 
 
 def master_of(p: torch.nn.Parameter) -> torch.Tensor:
     """fp32 storage-layout master region of p (contiguous; what the kernels read)."""
     ensure_param_ready(p)
     return p._kml_master_storage
+
+
+def grad_out_pair(p1: torch.nn.Parameter, p2: torch.nn.Parameter):
+    """grad_out for two parameters one kernel writes with ONE store/add flag (BN dgamma and
+    dbeta): (g1, g2, accumulate), the fresh one zeroed first if their states differ."""
+    g1, a1 = grad_out(p1)
+    g2, a2 = grad_out(p2)
+    if a1 == a2:
+        return g1, g2, a1
+    fresh = p1 if not a1 else p2
+    fresh._kml_flat._zero_params([fresh._kml_flat._index[id(fresh)]])
+    return g1, g2, True

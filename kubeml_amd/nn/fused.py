@@ -27,7 +27,7 @@ from torch.autograd import Function
 
 import os
 
-from .flat import grad_storage_of, master_of, shadow_of
+from .flat import grad_out, grad_out_pair, master_of, shadow_of
 
 # KUBEML_BN_FUSE=0: every BN backward runs its own dgamma/dbeta reduction instead of
 # taking partial rows from the dgrad epilogue that produced its input gradient
@@ -84,12 +84,13 @@ def _wgrad(x, dc, conv, unroll=False):
     from ..ops import kernels as K
     kh, kw = conv.kernel_size
     side = _WgradSide.stream
+    dw, acc = grad_out(conv.weight)
     if side is None:
-        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding, unroll=unroll)
+        K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
         return
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        K.conv_wgrad(x, dc, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding, unroll=unroll)
+        K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
     # the allocator must not hand these blocks to the main stream before the side reads them
     x.record_stream(side)
     dc.record_stream(side)
@@ -217,8 +218,9 @@ class ConvBNUnit:
         from ..ops import kernels as K
         x, c, y, mean, rstd = saved
         dres = torch.empty_like(dy) if want_dres else None
+        dg, db, acc = grad_out_pair(bn.weight, bn.bias)
         dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
-                      grad_storage_of(bn.weight), grad_storage_of(bn.bias), dres=dres, partial=partial)
+                      dg, db, dres=dres, partial=partial, accumulate=acc)
         kh, kw = conv.kernel_size
         dx, part_out = None, None
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
@@ -231,8 +233,9 @@ class ConvBNUnit:
             if wt is None and K.bwd_plans(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding,
                                           unroll=wu is not None)[0][4] == K.DIRECT:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
-            r = K.conv_bwd(dc, w, x, grad_storage_of(conv.weight), kh, kw, conv.stride, conv.padding,
-                           addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True)
+            dw, acc = grad_out(conv.weight)
+            r = K.conv_bwd(dc, w, x, dw, kh, kw, conv.stride, conv.padding,
+                           addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True, accumulate=acc)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out

@@ -21,7 +21,7 @@ import torch.nn as tnn
 import torch.nn.functional as F
 from torch.autograd import Function
 
-from .flat import grad_storage_of, master_of, shadow_of
+from .flat import grad_out, grad_out_pair, grad_storage_of, master_of, shadow_of
 
 
 def _pair(v):
@@ -102,8 +102,8 @@ class _ConvFn(Function):
         from ..ops import kernels as K
         mod = ctx.mod
         dy = dy.contiguous()
-        K.conv_wgrad(ctx.x, dy, grad_storage_of(mod.weight), mod.kernel_size[0], mod.kernel_size[1],
-                     mod.stride, mod.padding)
+        dw, acc = grad_out(mod.weight)
+        K.conv_wgrad(ctx.x, dy, dw, mod.kernel_size[0], mod.kernel_size[1], mod.stride, mod.padding, accumulate=acc)
         if ctx.has_bias:
             K.colsum_(dy.view(-1, dy.shape[-1]), grad_storage_of(mod.bias))
         dx = None
@@ -218,7 +218,11 @@ class _LinearFn(Function):
             bias_done = ctx.has_bias
         dy4 = dy.view(B, 1, 1, op)
         x4 = ctx.x.view(B, 1, 1, ip)
-        dw4 = grad_storage_of(mod.weight).view(op, 1, 1, ip)
+        if ctx.route == "conv":          # implicit-GEMM wgrad: stores or adds, deterministic
+            dwst, wacc = grad_out(mod.weight)
+        else:                            # gemm.hip / hipBLASLt wgrad: adds
+            dwst, wacc = grad_storage_of(mod.weight), True
+        dw4 = dwst.view(op, 1, 1, ip)
         dx = None
         # residual gradient handed over by a LayerNorm that shares this Linear's input
         # (nn/transformer.py): summed into dx here instead of by an autograd add
@@ -243,9 +247,9 @@ class _LinearFn(Function):
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
-            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0)).view(B, ip)
+            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc).view(B, ip)
         else:
-            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0))
+            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc)
         if ctx.has_bias and not bias_done:
             if getattr(mod, "_kml_bias_done", False):
                 object.__setattr__(mod, "_kml_bias_done", False)   # summed by the consumer LayerNorm
@@ -335,8 +339,9 @@ class _BNFn(Function):
         mod = ctx.mod
         dy = dy.contiguous()
         dres = torch.empty_like(dy) if ctx.has_res else None
+        dg, db, acc = grad_out_pair(mod.weight, mod.bias)
         dx = K.bn_bwd(dy, ctx.y if ctx.relu else None, ctx.x, ctx.mean, ctx.rstd, master_of(mod.weight),
-                      grad_storage_of(mod.weight), grad_storage_of(mod.bias), dres=dres)
+                      dg, db, dres=dres, accumulate=acc)
         ctx.x = ctx.y = None
         return dx, None, None, None, None, dres
 
@@ -506,13 +511,13 @@ class _CEFn(Function):
         logits, lab, ws, out3, ig, classes = ctx.save
         # the logits came straight out of a Linear: its bias gradient (the column sums of
         # dlogits) is added by the CE backward pass itself, and the Linear skips its own
-        lin, dbias = ctx.lin, None
+        lin, dbias, acc = ctx.lin, None, True
         if (lin is not None and getattr(lin, "bias", None) is not None and _CE_BIAS_FUSE
                 and lin.out_pad == logits.shape[1] and K.ce_bias_fusable(logits)):
-            dbias = grad_storage_of(lin.bias)
+            dbias, acc = grad_out(lin.bias)
             object.__setattr__(lin, "_kml_bias_done", True)
         d = K.ce_bwd(logits, lab, ws, out3, grad_out=g.reshape(1).float().contiguous(), ignore_index=ig,
-                     classes=classes, dbias=dbias)
+                     classes=classes, dbias=dbias, accumulate=acc)
         ctx.save = ctx.lin = None
         return d, None, None, None, None
 

@@ -9,7 +9,8 @@ Tensor conventions
 ------------------
 * activations: bf16, NHWC contiguous, C % 8 == 0
 * conv weights: bf16 KRSC ``[Cout, KH, KW, Cin]`` contiguous (the bf16 shadow)
-* weight gradients: fp32 KRSC, accumulated (``+=``) into the caller's buffer
+* weight gradients: fp32 KRSC, stored (``=``) or accumulated (``+=``) into the caller's buffer,
+  one writer per element (no atomics: bitwise reproducible)
 """
 from __future__ import annotations
 
@@ -515,15 +516,15 @@ def conv_pair_supported(dcfg, wcfg) -> bool:
 
 
 def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None,
-             bnf_mask=False):
+             bnf_mask=False, accumulate=True):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
-    :func:`conv_dgrad`) and ``dw += wgrad``.  Runs as ONE grouped launch
+    :func:`conv_dgrad`) and ``dw += wgrad`` (``accumulate=False``: ``dw = wgrad``).  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
     instantiated pair, else as two launches.  ``wt``: precomputed transposed weights for
     a direct-variant dgrad (:func:`weight_transpose_multi`); made here when missing.
     Returns dx, or (dx, (part, G)) when ``bnf`` is given.  wu: unrolled weight
-    (:func:`unrolled22`): both GEMMs run in the dense 1x1 form, the weight gradient
-    scatter-adds back onto the 3x3 taps of ``dw``.  bnf_mask: as in :func:`conv_dgrad`."""
+    (:func:`unrolled22`): the dgrad runs in the dense 1x1 form, the weight gradient in the
+    plain 3x3 form (one writer per element).  bnf_mask: as in :func:`conv_dgrad`."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -552,7 +553,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
     if not grouped:
-        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, _u=u)
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, _u=u, accumulate=accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
                        bnf_mask=bnf_mask)
         if not fold:
@@ -575,12 +576,13 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         dsplits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
+    wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan, u)
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i i p p i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
              _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold), u[0], u[1],
-             int(bool(bnf_mask) and bnf is not None), _s())
+             int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _s())
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out
@@ -610,9 +612,25 @@ def weight_transpose_multi(ws, wts):
              ctypes.addressof(dims), n, _s())
 
 
-def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0)):
-    """dw[Cout,KH,KW,Cin] (fp32) += conv weight gradient.  unroll: run the dense 1x1 form
-    of an unrolled conv (:func:`unrolled22`), scatter-adding onto the 3x3 taps."""
+def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg, u):
+    """Split-K slab + tickets of a weight-gradient GEMM (None, None without split-K).  An
+    unrolled conv (u = (K, C) of the 3x3 conv, geometry = its 1x1 form) computes its weight
+    gradient in the plain 3x3 form on the 2x2 map (conv_igemm.hip prep_wgrad)."""
+    if u[0]:
+        B, H, W, C, K, KH, KW, stride, pad = B, 2, 2, u[1], u[0], 3, 3, (1, 1), (1, 1)
+    bm, bn, bk, splits, variant = cfg
+    if variant:
+        bk = 64
+    OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    return _splitk_ws(device, K, (r1 - r0) * (s1 - s0) * C, bm, bn, effective_splits(B * OH * OW, bk, splits))
+
+
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0), accumulate=True):
+    """Conv weight gradient into dw[Cout,KH,KW,Cin] (fp32): ``dw += wgrad`` (accumulate) or
+    ``dw = wgrad`` (overwrite: the buffer need not be zeroed).  Deterministic: one writer per
+    element, split-K partials summed in split order.  unroll: an unrolled conv
+    (:func:`unrolled22`); its weight gradient runs in the plain 3x3 form."""
     _chk(x, BF16, "x", 4)
     _chk(dy, BF16, "dy", 4)
     _chk(dw, F32, "dw", 4)
@@ -622,7 +640,8 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0)
         if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (K, 3, 3, C):
             raise ValueError("conv is not unrolled")
         _, x1, _, _ = _u22_views(B, C, K, x=x)
-        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, _u=(K, C))
+        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, _u=(K, C),
+                          accumulate=accumulate)
     B, H, W, C = x.shape
     K = dy.shape[3]
     sh, sw = stride
@@ -634,10 +653,12 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0)
     elif tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
         raise ValueError("wgrad shape mismatch")
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
-    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i i i s",
-             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, 1, int(_u[0]),
-             int(_u[1]), _s())
+    cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
+    bm, bn, bk, splits, variant = cfg
+    slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg, _u)
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i i i p p s",
+             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant,
+             int(bool(accumulate)), int(_u[0]), int(_u[1]), _p(slab), _p(cnt), _s())
     return dw
 
 
@@ -693,9 +714,10 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
 _BN_REDUCE = os.environ.get("KUBEML_BN_REDUCE", "fused")
 
 
-def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None):
-    """dgamma/dbeta (+=) and dx; y given => ReLU mask applied; dres (optional) receives dz.
-    partial = (part, G) from conv_dgrad(bnf=...) skips the reduction pass."""
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None, accumulate=True):
+    """dgamma/dbeta (``+=``, or ``=`` with accumulate=False) and dx; y given => ReLU mask
+    applied; dres (optional) receives dz.  partial = (part, G) from conv_dgrad(bnf=...) skips
+    the reduction pass."""
     _chk(dy, BF16, "dy")
     _chk(x, BF16, "x")
     C = x.shape[-1]
@@ -704,9 +726,9 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         dx = torch.empty_like(x)
     if partial is not None:
         part, G = partial
-        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p s",
+        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s",
                  _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
-                 _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), _s())
+                 _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), int(bool(accumulate)), _s())
         return dx
     ws = cnt = None
     if _BN_REDUCE in ("fused", "ticket"):
@@ -714,9 +736,9 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         ws = torch.empty(nws, dtype=F32, device=x.device)
         if _BN_REDUCE == "ticket":
             cnt = _COUNTERS.take(x.device, 1)
-    HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i s",
+    HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s",
              _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
-             _p(dres), _p(ws), _p(cnt), M, C, _s())
+             _p(dres), _p(ws), _p(cnt), M, C, int(bool(accumulate)), _s())
     return dx
 
 
@@ -742,6 +764,34 @@ def fill_(t, value=0.0):
     """fp32 fill with a kernel (graph-safe alternative to a memset node)."""
     _chk(t, F32, "t")
     HIP.call("kml_fill_f32", "p f l s", _p(t), float(value), t.numel(), _s())
+    return t
+
+
+_ZR_MAX = None
+
+
+def zero_ranges_max() -> int:
+    global _ZR_MAX
+    if _ZR_MAX is None:
+        _ZR_MAX = int(HIP.raw("kml_zero_ranges_max"))
+    return _ZR_MAX
+
+
+def zero_ranges_(t, runs):
+    """Zero [offset, offset + n) element runs of the fp32 buffer ``t`` in one launch
+    (offsets multiples of 4; at most :func:`zero_ranges_max` runs)."""
+    import ctypes
+    _chk(t, F32, "t")
+    k = len(runs)
+    if k == 0:
+        return t
+    if k > zero_ranges_max():
+        raise ValueError("zero_ranges_: too many runs")
+    offs = (ctypes.c_longlong * k)(*[int(o) for o, _ in runs])
+    ns = (ctypes.c_int * k)(*[int(n) for _, n in runs])
+    if any(int(o) + int(n) > t.numel() for o, n in runs):
+        raise ValueError("zero_ranges_: run outside the buffer")
+    HIP.call("kml_zero_ranges", "p p p i s", _p(t), ctypes.addressof(offs), ctypes.addressof(ns), k, _s())
     return t
 
 
@@ -865,9 +915,10 @@ def ce_bias_fusable(logits) -> bool:
     return logits.dtype == BF16 and logits.dim() == 2 and logits.shape[1] % 8 == 0 and logits.shape[1] <= 4096
 
 
-def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=None, dbias=None):
+def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=None, dbias=None, accumulate=True):
     """dlogits (same [B, ld] layout as the logits; pad columns 0).  dbias (fp32, needs
-    :func:`ce_bias_fusable`): += column sums of dlogits (the logits Linear's bias gradient)."""
+    :func:`ce_bias_fusable`): the column sums of dlogits (the logits Linear's bias gradient),
+    added (accumulate) or stored; deterministic (ordered partial rows, no atomics)."""
     dt = {BF16: 0, F32: 1}[logits.dtype]
     B, ld = logits.shape
     C = ld if classes is None else int(classes)
@@ -876,8 +927,12 @@ def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=N
         _chk(dbias, F32, "dbias")
         if not ce_bias_fusable(logits) or dbias.numel() < C:
             raise ValueError("ce_bwd: bias fusion needs bf16 logits with ld % 8 == 0, ld <= 4096")
-    HIP.call("kml_ce_bwd", "p p p p p p i i i l i p s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
-             _p(d), B, C, ld, int(ignore_index), dt, _p(dbias), _s())
+    part = cnt = None
+    if dbias is not None:
+        part = torch.empty(_cdiv(B, 4) * C, dtype=F32, device=logits.device)
+        cnt = _COUNTERS.take(logits.device, 1)
+    HIP.call("kml_ce_bwd", "p p p p p p i i i l i p p p i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
+             _p(d), B, C, ld, int(ignore_index), dt, _p(dbias), _p(part), _p(cnt), int(bool(accumulate)), _s())
     return d
 
 

@@ -160,20 +160,17 @@ class SGD(FusedOptimizer):
         if len(self.param_groups) > 1:
             raise ValueError("fused SGD supports a single param group")
 
-    _advance = None  # (ctr, batch, n) folded into the fused step, see fuse_advance
-
     def fuse_advance(self, ctr, batch, n) -> bool:
-        """Advance the on-device data-sampler counter ``ctr`` (``ops.kernels.advance_counter_``)
-        inside every fused step's SGD launch instead of a one-thread launch of its own.
-        Returns False (nothing attached) when no GPU flat space holds the counter's device."""
+        """Can ``step(advance=(ctr, batch, n))`` advance the on-device data-sampler counter
+        ``ctr`` (``ops.kernels.advance_counter_``) inside its SGD launch instead of a
+        one-thread launch of its own?  False when no GPU flat space holds the counter's
+        device.  Nothing is attached to the optimizer: the advance is per call."""
         spaces, _ = self._flat_groups()
-        if not spaces or spaces[0][0].device.type != "cuda" or ctr.device != spaces[0][0].device:
-            return False
-        self._advance = (ctr, batch, n)
-        return True
+        return bool(spaces and spaces[0][0].device.type == "cuda" and ctr.device == spaces[0][0].device)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, advance=None):
+        """advance: (ctr, batch, n) folded into this step's launch (see fuse_advance)."""
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
         spaces, loose = self._flat_groups()
@@ -181,13 +178,14 @@ class SGD(FusedOptimizer):
             if sp.device.type != "cuda":
                 loose += members
                 continue
+            sp.finish_grads()
             from ..ops import kernels as K
             mom = self._bufs(sp, ["momentum"])["momentum"] if g["momentum"] != 0 else None
             first = self.first_tensor(sp.device) if mom is not None else None
             K.sgd_(sp.master, sp.grad, mom, sp.shadow, g["lr"], wd=g["weight_decay"], momentum=g["momentum"],
                    dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
                    grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first,
-                   advance=self._advance if k == 0 else None)
+                   advance=advance if k == 0 else None)
             if first is not None:
                 K.fill_(first, 0.0)
         if loose:
@@ -217,6 +215,7 @@ class SGD(FusedOptimizer):
         if sp.device.type != "cuda":
             _sgd_range_cpu(sp, start, end, g, mom, self._first, self._grad_scale)
             return
+        sp.finish_grads_range(start, end)
         from ..ops import kernels as K
         first = self.first_tensor(sp.device) if mom is not None else None
         K.sgd_(sp.master[start:end], sp.grad[start:end], None if mom is None else mom[start:end],
@@ -306,6 +305,7 @@ class Adam(FusedOptimizer):
             if sp.device.type != "cuda":
                 loose += members
                 continue
+            sp.finish_grads()
             from ..ops import kernels as K
             st = self._step_dev_inc(sp.device)
             bufs = self._bufs(sp, ["exp_avg", "exp_avg_sq"])

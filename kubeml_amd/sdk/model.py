@@ -366,6 +366,7 @@ class KubeModel(ABC):
         """Eager (CPU / no-graph) gradient average over the grad-sync group."""
         comm = self._grad_comm
         if self._flat is not None:
+            self._flat.finish_grads()
             comm.all_reduce_(self._flat.grad)
             self._flat.grad.div_(comm.world)
             return

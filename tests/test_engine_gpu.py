@@ -97,13 +97,9 @@ def test_graphed_step_applies_one_update_per_batch(monkeypatch):
     assert len(ka._graphs) == 2                # one graph per batch shape, re-used
     ua, ub = ka._flat.master - w0, kb._flat.master - w0
     rel = float((ua - ub).norm() / ub.norm())
-    # Graph and eager agree to ~4e-7 unless the conv weight gradients' fp32 split-K atomics
-    # land in a different order and flip a bf16 shadow rounding: batch-20 BatchNorm over 1x1
-    # maps then amplifies that into a ~0.12 relative update difference in EITHER path
-    # (tools/determinism_check.py shows the same two outcomes for graph and eager runs;
-    # tools/conv_bwd_check.py shows conv_bwd itself exact to fp32 noise).  Still far below
-    # what an extra update per batch produces (rel ~ 2; the norm ratio below checks it too).
-    assert rel < 0.25, (rel, la, lb)
+    # every gradient producer is deterministic (no atomics): graph and eager replay the same
+    # kernels, so the updates agree to fp32 rounding of the update order only
+    assert rel <= 1e-5, (rel, la, lb)
     ratio = float(ua.norm() / ub.norm())
     assert 0.98 < ratio < 1.02, ratio          # 3 updates per batch would give ~3x
     for x, y in zip(la, lb):
@@ -113,7 +109,7 @@ def test_graphed_step_applies_one_update_per_batch(monkeypatch):
         if ba.dtype == torch.int64:
             assert int(ba) == int(bb) == len(data), n
         else:
-            assert torch.allclose(ba, bb, rtol=5e-2, atol=5e-3), n   # same atomic-order caveat
+            assert torch.allclose(ba, bb, rtol=1e-5, atol=1e-6), n
 
 
 def test_kavg_pack_finish_kernels():
@@ -239,7 +235,7 @@ def test_graphed_optimizer_overlap_matches_end_of_step_update():
     ub, spb, lb = _graphed_run(False)
     assert float(ub.abs().max()) > 1e-5
     rel = float((ua - ub).norm() / ub.norm())
-    assert rel < 1e-2, rel
+    assert rel <= 1e-5, rel
     for p, q in zip(la, lb):
         assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (la, lb)
     assert torch.equal(spa.shadow, spa.master.to(torch.bfloat16))
@@ -307,15 +303,12 @@ def _plan_run(spec, steps=3):
 
 
 def test_peer_plans_on_one_rank_match_the_local_step():
-    """World 1: the fp32 peer all-reduce is the identity (same updates as no comm, to the conv
-    wgrad's atomic-order noise); the bf16 wire rounds the gradient to bf16 (a small change)."""
+    """World 1: the fp32 peer all-reduce is the identity (bitwise the same updates as no comm:
+    every gradient producer is deterministic); the bf16 wire rounds the gradient to bf16."""
     ub, lb = _plan_run(None)
     for spec in ("peer:end:fp32:256", "peer:overlap:fp32:16"):
         ua, la = _plan_run(spec)
-        rel = float((ua - ub).norm() / ub.norm())
-        assert rel < 1e-2, (spec, rel)
-        for p, q in zip(la, lb):
-            assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (spec, la, lb)
+        assert torch.equal(ua, ub) and la == lb, (spec, float((ua - ub).abs().max()), la, lb)
     ua, la = _plan_run("peer:end:bf16:256")
     rel = float((ua - ub).norm() / ub.norm())
     assert rel < 5e-2, rel
