@@ -90,8 +90,8 @@ def test_graphed_step_first_update_matches_eager(monkeypatch):
 
 def test_graphed_step_applies_one_update_per_batch(monkeypatch):
     """Shapes (B, B, b_last, B, B) with momentum/dampening across reset_state(): the
-    accumulated update equals the eager one (small LR keeps bf16 rounding from
-    amplifying atomic-order noise, which is chaotic at large LR on random data)."""
+    accumulated update equals the eager one: every gradient producer is deterministic, so
+    graph and eager differ only by fp32 rounding of the update order."""
     data = _batches()
     ka, kb, a, b, w0, la, lb = _pair_run(monkeypatch, 1e-3, data)
     assert len(ka._graphs) == 2                # one graph per batch shape, re-used
@@ -309,6 +309,9 @@ def test_peer_plans_on_one_rank_match_the_local_step():
     for spec in ("peer:end:fp32:256", "peer:overlap:fp32:16"):
         ua, la = _plan_run(spec)
         assert torch.equal(ua, ub) and la == lb, (spec, float((ua - ub).abs().max()), la, lb)
-    ua, la = _plan_run("peer:end:bf16:256")
-    rel = float((ua - ub).norm() / ub.norm())
-    assert rel < 5e-2, rel
+    # one step (later steps amplify any perturbation chaotically through batch-32 BN over
+    # 1x1 maps): the update differs only by the bf16 rounding of the gradient (2^-9 relative)
+    ua, _ = _plan_run("peer:end:bf16:256", steps=1)
+    ub1, _ = _plan_run(None, steps=1)
+    rel = float((ua - ub1).norm() / ub1.norm())
+    assert 0 < rel < 1e-2, rel
