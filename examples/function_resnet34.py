@@ -1,6 +1,7 @@
 """ResNet-34 / CIFAR-10 function — the reference's headline workload
 (ml/experiments/kubeml/function_resnet34.py): torchvision-layout resnet34 with the
-ImageNet stem and 1000-class head, SGD(lr, wd 1e-4), LR x0.1 after epoch 80,
+ImageNet stem and 1000-class head, SGD(lr, wd 1e-4), LR x0.1 after epoch 80 (the
+reference's never-firing x0.01 branch kept as written),
 RandomCrop(32, 4) + RandomHorizontalFlip + Normalize(ImageNet mean/std), accuracy
 = correct * 100 / batch_size.
 
@@ -29,11 +30,13 @@ class KubeResnet34(KubeModel):
         super().__init__(network, dataset, gpu=True)
 
     def configure_optimizers(self) -> torch.optim.Optimizer:
+        # the reference's schedule, quirk included (function_resnet34.py:57-60): the `elif`
+        # can never fire (epoch > 120 implies epoch > 80), so the LR stays at x0.1 after 80
         lr = self.lr
-        if self.epoch > 120:
-            lr *= 0.01
-        elif self.epoch > 80:
+        if self.epoch > 80:
             lr *= 0.1
+        elif self.epoch > 120:
+            lr *= 0.01
         return SGD(self.parameters(), lr=lr, weight_decay=1e-4)
 
     def train(self, batch, batch_index) -> float:

@@ -104,6 +104,10 @@ class JobHistory(_Json):
     train_loss: List[float] = field(default_factory=list)
     parallelism: List[float] = field(default_factory=list)
     epoch_duration: List[float] = field(default_factory=list)
+    # extension (omitted from the wire form when empty): how each epoch synchronised the
+    # workers — "kavg" (reference K-AVG), "kavg-async-staleness1", "grad-allreduce" (K=1 DP)
+    sync_mode: List[str] = field(default_factory=list)
+    _OMIT_EMPTY = ("sync_mode",)
 
 
 @dataclass

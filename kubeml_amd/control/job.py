@@ -262,6 +262,9 @@ class TrainJob:
                 hbm = max((v.get("hbm_bytes", 0) for v in ok.values()), default=0)
                 self.last_sync_seconds = max((v.get("sync_seconds", 0.0) for v in ok.values()), default=0.0)
                 self.last_grad_rounds = max((v.get("grad_rounds", 0) for v in ok.values()), default=0)
+                modes = sorted({v.get("sync_mode") for v in ok.values() if v.get("sync_mode")})
+                if modes:
+                    self.history.sync_mode.append("+".join(modes))
                 self._epoch_stats(time.time() - t0, hbm)
                 return sum(losses) / len(losses)
             errs = "; ".join(f"worker {r}: {v.get('error')}" for r, v in sorted(bad.items()))

@@ -161,3 +161,91 @@ class ModelAverager:
             b.copy_(t)
         if sp is not None:
             sp.refresh_shadow()
+
+
+class AsyncModelAverager(ModelAverager):
+    """Overlapped K-AVG with staleness 1 (opt-in, recorded in the history).
+
+    The synchronous round (reference python/kubeml/kubeml/network.py:289-306) stops every
+    worker until the average is back.  Here the all-reduce of round r is launched on the
+    communicator's stream and the workers keep training round r+1 from their own model;
+    at the end of round r+1 the average of round r replaces the stale base the local
+    progress was made on:
+
+        x_i  <-  mean_j x_j^(r)  +  (x_i^now - x_i^(r))
+
+    and round r+1's all-reduce starts from the corrected model.  :meth:`flush_` applies the
+    last pending average and then averages synchronously, so every worker ends the task with
+    the same model (the reference's final merge).  Every rank must take part in every round
+    (uneven tails go through :meth:`flush_` and the synchronous path).  Memory: two extra
+    copies of the model state (the in-flight sum and the snapshot it was taken from).
+    """
+
+    def __init__(self, module: torch.nn.Module):
+        super().__init__(module)
+        self._pending = None      # (work | None, send, snap, tensors)
+        self.rounds_overlapped = 0
+
+    def _tensors(self):
+        sp = self._space()
+        if sp is not None:
+            return [sp.state[:sp.i64_off]], sp
+        return [p.data for p in self.module.parameters()] + [b for _, b in self._buffers() if b.is_floating_point()], None
+
+    def _launch(self, comm: Comm, flat: torch.Tensor):
+        """Async SUM of ``flat`` over the group; returns a waitable (None when the comm
+        backend has no async collectives: the sum is then already done)."""
+        dist_ = getattr(comm, "dist", None)
+        if dist_ is not None and comm.world > 1:
+            return dist_.all_reduce(flat, group=comm.group, async_op=True)
+        comm.all_reduce_(flat)
+        return None
+
+    @property
+    def pending(self) -> bool:
+        return self._pending is not None
+
+    @torch.no_grad()
+    def average_(self, comm: Comm, participate: bool = True) -> int:
+        """One overlapped round.  Every rank must participate (callers route rounds in which
+        some worker has no data through :meth:`flush_`, on every rank alike)."""
+        if comm.world == 1:
+            return 1 if participate else 0
+        if not participate:
+            raise ValueError("AsyncModelAverager.average_: every rank must participate (use flush_)")
+        t0 = time.perf_counter()
+        ts, sp = self._tensors()
+        self._apply_pending(comm, ts, sp)
+        flat = torch.cat([t.reshape(-1).float() for t in ts]) if len(ts) > 1 else ts[0].detach().clone()
+        snap = flat.clone()
+        work = self._launch(comm, flat)
+        self._pending = (work, flat, snap)
+        self.rounds_overlapped += 1
+        self.last_seconds = time.perf_counter() - t0
+        return -1
+
+    def _apply_pending(self, comm: Comm, ts, sp):
+        if self._pending is None:
+            return
+        work, flat, snap = self._pending
+        self._pending = None
+        if work is not None:
+            work.wait()
+        # x <- avg + (x - snap), per tensor of the flat layout
+        flat.div_(comm.world).sub_(snap)
+        off = 0
+        for t in ts:
+            k = t.numel()
+            t.add_(flat[off:off + k].view_as(t).to(t.dtype))
+            off += k
+        if sp is not None:
+            sp.refresh_shadow()
+
+    @torch.no_grad()
+    def flush_(self, comm: Comm, participate: bool = True):
+        """Apply the in-flight average, then one synchronous average (all ranks identical)."""
+        if comm.world == 1:
+            return
+        ts, sp = self._tensors()
+        self._apply_pending(comm, ts, sp)
+        ModelAverager.average_(self, comm, participate)

@@ -172,7 +172,8 @@ class Worker:
                    "sync_seconds": float(ctx.extra.get("sync_seconds", 0.0)),
                    "start_checksum": ctx.extra.get("start_checksum"),
                    "end_checksum": ctx.extra.get("end_checksum"),
-                   "grad_rounds": int(ctx.extra.get("grad_rounds", 0))}
+                   "grad_rounds": int(ctx.extra.get("grad_rounds", 0)),
+                   "sync_mode": ctx.extra.get("sync_mode")}
             if self.use_gpu:
                 import torch
                 out["hbm_bytes"] = int(torch.cuda.max_memory_allocated(self.device))

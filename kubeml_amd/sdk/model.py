@@ -276,6 +276,12 @@ class KubeModel(ABC):
         # rounds in which EVERY worker has data (uneven shards differ by at most one doc)
         full_rounds = min(-(-len(sp) // max(get_subset_period(K, self.batch_size, sp), 1)) for sp in splits)
         grad_ok = self._grad_sync_ok(comm, K)
+        # overlapped staleness-1 K-AVG (opt-in: class attribute ASYNC_KAVG or KUBEML_KAVG_ASYNC=1)
+        use_async = (not grad_ok and comm.world > 1 and
+                     (getattr(self, "ASYNC_KAVG", False) or os.environ.get("KUBEML_KAVG_ASYNC") == "1"))
+        if use_async and getattr(self, "_async_averager", None) is None:
+            from ..parallel.kavg import AsyncModelAverager
+            self._async_averager = AsyncModelAverager(self._network)
         if grad_ok:
             self._grad_comm = comm
             self._prime_grad_sync()
@@ -318,12 +324,22 @@ class KubeModel(ABC):
                 try:
                     t0 = time.perf_counter()
                     with trace.span("average", round=r):
-                        self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
+                        if use_async and r < full_rounds:
+                            self._async_averager.average_(comm)          # overlapped with the next round
+                        elif use_async:
+                            self._async_averager.flush_(comm, participate)   # ragged tail: synchronous
+                        else:
+                            self._averager.average_(comm, participate)  # replaces save + /next + merge + reload
                     self.sync_seconds += time.perf_counter() - t0
                 except Exception as e:  # the reference surfaces merge failures as MergeError
                     raise MergeError(e)
                 if self.PEER_CHECK_EVERY and (r + 1) % self.PEER_CHECK_EVERY == 0:
                     comm.check()     # a timed-out peer collective stops the task within a few rounds
+            if use_async and self._async_averager.pending:
+                t0 = time.perf_counter()
+                with trace.span("average_flush"):
+                    self._async_averager.flush_(comm)          # every worker ends on the same model
+                self.sync_seconds += time.perf_counter() - t0
             if grad_rounds:
                 # in-graph gradient all-reduce time (device stamps sampled by the step)
                 cs = [g["step"].comm_seconds() for k, g in self._graphs.items() if k[5]]
@@ -347,6 +363,8 @@ class KubeModel(ABC):
         if ctx is not None:   # reported to the job driver with the task result (metrics)
             ctx.extra["sync_seconds"] = self.sync_seconds
             ctx.extra["grad_rounds"] = grad_rounds
+            ctx.extra["sync_mode"] = ("grad-allreduce" if grad_rounds else
+                                      "kavg-async-staleness1" if use_async else "kavg")
         return loss_host / max(num_iterations, 1)
 
     @torch.no_grad()
