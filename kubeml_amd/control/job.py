@@ -236,9 +236,11 @@ class TrainJob:
         self._pending_restore = self.ckpt
         self.log.info("resuming", source=self.resume_from, start_epoch=self.start_epoch)
 
-    def _checkpoint(self):
+    def _checkpoint(self, wait: bool = False):
+        """Rank 0 snapshots the reference model and writes it in the background (off the
+        epoch's critical path); ``wait`` = the file is on disk when this returns."""
         rep = self.pool.call(0, {"op": "checkpoint", "job": self.id, "path": self.ckpt, "epoch": self.epoch,
-                                 "extra": {"history": self.history.to_dict()}})
+                                 "extra": {"history": self.history.to_dict()}, "wait": bool(wait)})
         if rep.get("ok"):
             self.have_ckpt = True
         else:
@@ -397,7 +399,7 @@ class TrainJob:
                     self._validate()
                 except Exception as e:
                     self.log.error("error performing validation", error=repr(e))
-            self._checkpoint()
+            self._checkpoint(wait=True)          # inference / resume read it right after
             self._save_history()
             self.log.info("training finished", epochs=self.epoch, history=self.history.to_dict())
         except Exception as e:

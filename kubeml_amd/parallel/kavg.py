@@ -36,6 +36,13 @@ class ModelAverager:
     def __init__(self, module: torch.nn.Module):
         self.module = module
         self.last_seconds = 0.0   # host time of the last average_ call (metrics)
+        self.force = False        # run rounds on a 1-rank group too (single-GPU rehearsal)
+
+    def _all_reduce(self, comm: Comm, t: torch.Tensor):
+        if comm.world == 1 and self.force and hasattr(comm, "dist"):
+            comm.dist.all_reduce(t, group=comm.group)      # 1-rank rehearsal: the collective runs
+            return t
+        return comm.all_reduce_(t)
 
     def _buffers(self) -> List[Tuple[str, torch.Tensor]]:
         return [(n, b) for n, b in self.module.named_buffers() if b is not None]
@@ -50,7 +57,7 @@ class ModelAverager:
     def average_(self, comm: Comm, participate: bool = True) -> int:
         """Average the model over the group.  GPU: returns -1 (the participant count
         stays on the device); CPU: returns the participant count."""
-        if comm.world == 1:
+        if comm.world == 1 and not (self.force and hasattr(comm, "dist")):
             return 1 if participate else 0
         t0 = time.perf_counter()
         sp = self._space()
@@ -67,7 +74,7 @@ class ModelAverager:
         if not participate:
             K.memset_(sp.state)
         K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, participate)
-        comm.all_reduce_(sp.state)
+        self._all_reduce(comm, sp.state)
         K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
         return -1
 
@@ -80,7 +87,7 @@ class ModelAverager:
         pack = torch.cat(pieces + [cnt]) if pieces else cnt
         if not participate:
             pack.zero_()
-        comm.all_reduce_(pack)
+        self._all_reduce(comm, pack)
         n = int(round(float(pack[-1])))
         if n == 0:
             return 0
@@ -196,9 +203,9 @@ class AsyncModelAverager(ModelAverager):
         """Async SUM of ``flat`` over the group; returns a waitable (None when the comm
         backend has no async collectives: the sum is then already done)."""
         dist_ = getattr(comm, "dist", None)
-        if dist_ is not None and comm.world > 1:
+        if dist_ is not None and (comm.world > 1 or self.force):
             return dist_.all_reduce(flat, group=comm.group, async_op=True)
-        comm.all_reduce_(flat)
+        self._all_reduce(comm, flat)
         return None
 
     @property
@@ -209,7 +216,7 @@ class AsyncModelAverager(ModelAverager):
     def average_(self, comm: Comm, participate: bool = True) -> int:
         """One overlapped round.  Every rank must participate (callers route rounds in which
         some worker has no data through :meth:`flush_`, on every rank alike)."""
-        if comm.world == 1:
+        if comm.world == 1 and not (self.force and hasattr(comm, "dist")):
             return 1 if participate else 0
         if not participate:
             raise ValueError("AsyncModelAverager.average_: every rank must participate (use flush_)")
@@ -244,7 +251,7 @@ class AsyncModelAverager(ModelAverager):
     @torch.no_grad()
     def flush_(self, comm: Comm, participate: bool = True):
         """Apply the in-flight average, then one synchronous average (all ranks identical)."""
-        if comm.world == 1:
+        if comm.world == 1 and not (self.force and hasattr(comm, "dist")):
             return
         ts, sp = self._tensors()
         self._apply_pending(comm, ts, sp)

@@ -87,6 +87,7 @@ class Worker:
         self.device = None
         self.comm = None
         self.store = None
+        self.ckpt = None                     # AsyncCheckpointer (background writes)
 
     # ------------------------------------------------------------------ setup
     def setup(self):
@@ -150,6 +151,8 @@ class Worker:
                           comm=self.comm.sub(P) if P > 1 else _local(), store=self.store,
                           store_dir=self.store_dir, device=self.device, checkpoint=msg.get("checkpoint"))
         ctx.extra["restore"] = msg.get("restore")
+        if msg.get("restore") or kind == "infer":
+            self._flush_checkpoint()         # the file a restore / inference reads is complete
         token = set_task(ctx)
         t0 = time.perf_counter()
         try:
@@ -188,15 +191,29 @@ class Worker:
                 trace.flush(os.path.join(self.store_dir, "traces"))
 
     def _checkpoint(self, msg):
-        from ..store.ckpt import save_checkpoint
+        """Snapshot now, write in the background (``"wait": True`` — job end, before a
+        restore — returns only once the file is on disk)."""
+        from ..store.ckpt import AsyncCheckpointer
         km = self.jobs.get(msg["job"])
         if km is None:
             return {"ok": False, "error": f"job {msg['job']} has no model on worker {self.rank}", "code": 404}
-        path = save_checkpoint(km.network, msg["path"], job_id=msg["job"], epoch=int(msg.get("epoch", 0)),
-                               extra=msg.get("extra"))
+        if self.ckpt is None:
+            self.ckpt = AsyncCheckpointer()
+        try:
+            path = self.ckpt.save(km.network, msg["path"], job_id=msg["job"], epoch=int(msg.get("epoch", 0)),
+                                  extra=msg.get("extra"))
+            if msg.get("wait"):
+                self.ckpt.wait()
+        except Exception as e:
+            return {"ok": False, "error": f"checkpoint failed: {e!r}", "code": 500}
         return {"ok": True, "result": path}
 
+    def _flush_checkpoint(self):
+        if self.ckpt is not None:
+            self.ckpt.wait()
+
     def _release(self, job):
+        self._flush_checkpoint()
         self.jobs.pop(job, None)
         self.job_fn.pop(job, None)
         import gc

@@ -60,6 +60,73 @@ def save_checkpoint(module: torch.nn.Module, path: str, job_id: str = "", epoch:
     return path
 
 
+class AsyncCheckpointer:
+    """Checkpoint writes off the epoch's critical path.
+
+    ``save()`` takes a consistent snapshot of the model synchronously — device-to-host
+    copies into pinned buffers that are allocated once and reused every epoch (an 87 MB
+    ResNet-34 state is ~5 ms at PCIe-class bandwidth) — and returns; a writer thread
+    serialises the snapshot (safetensors) and renames it into place.  A new ``save()``
+    first waits for the previous write (one snapshot buffer); :meth:`wait` blocks until
+    the last write landed (job end, before a restore reads the file)."""
+
+    def __init__(self):
+        import threading
+        self._thread: Optional["threading.Thread"] = None
+        self._pinned: Dict[str, torch.Tensor] = {}
+        self.error: Optional[BaseException] = None
+        self.writes = 0
+
+    def _snapshot(self, module: torch.nn.Module) -> Dict[str, torch.Tensor]:
+        sd = module.state_dict()
+        out = {}
+        for k, v in sd.items():
+            t = v.detach()
+            if t.dtype == torch.bfloat16:
+                t = t.float()
+            buf = self._pinned.get(k)
+            if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+                buf = torch.empty(t.shape, dtype=t.dtype, pin_memory=t.is_cuda)
+                self._pinned[k] = buf
+            buf.copy_(t, non_blocking=t.is_cuda)
+            out[k] = buf
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        return out
+
+    def save(self, module: torch.nn.Module, path: str, job_id: str = "", epoch: int = 0,
+             extra: Optional[dict] = None) -> str:
+        import threading
+        self.wait()
+        sd = self._snapshot(module)
+        meta = {"format": FORMAT, "jobId": job_id, "epoch": str(epoch), "keys": "{jobId}:{name}"}
+        side = {"jobId": job_id, "epoch": epoch, "tensors": len(sd), **(extra or {})}
+
+        def write():
+            try:
+                from safetensors.torch import save_file
+                os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+                tmp = path + ".tmp"
+                save_file(sd, tmp, metadata=meta)
+                os.replace(tmp, path)
+                write_json(path + ".json", side)
+                self.writes += 1
+            except BaseException as e:  # surfaced by the next wait()
+                self.error = e
+        self._thread = threading.Thread(target=write, name="kubeml-ckpt", daemon=True)
+        self._thread.start()
+        return path
+
+    def wait(self):
+        """Block until the last write is on disk; re-raise a failed write."""
+        t, self._thread = self._thread, None
+        if t is not None:
+            t.join()
+        if self.error is not None:
+            e, self.error = self.error, None
+            raise e
+
+
 def load_state(path: str) -> Dict[str, torch.Tensor]:
     from safetensors.torch import load_file
     return load_file(path)
