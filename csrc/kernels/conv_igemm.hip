@@ -378,21 +378,29 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
 
   // -------------------------------------------------------- split-K: last arriver reduces
   // (every mode: the fp32 partial tiles are summed in split order by the last block of a
-  // tile, so FWD/DGRAD outputs and WGRAD weight gradients are bitwise reproducible)
+  // tile, so FWD/DGRAD outputs and WGRAD weight gradients are bitwise reproducible).
+  // Publish without a release fence (CDNA guide §6 G16 R1): the partial tile is stored
+  // write-through (16-byte sc1 stores), every storing wave drains, one lane takes the
+  // relaxed agent-scope ticket; only the last arriver pays one agent acquire before its
+  // plain loads.  A release fence would write back each split block's whole dirty XCD L2.
   if (a.splits > 1) {
     constexpr int NACC = MR * NR * 4;
     float* slab = a.slab + ((long long)tile * a.splits) * (256 * NACC);
-    float4* mine = reinterpret_cast<float4*>(slab + (long long)bz * 256 * NACC) + tid * (NACC / 4);
+    {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab + (long long)bz * 256 * NACC, (short)0,
+                                                        256 * NACC * 4, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < MR; ++i)
+      for (int i = 0; i < MR; ++i)
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
-        mine[i * NR + j] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int j = 0; j < NR; ++j) {
+          __attribute__((ext_vector_type(4))) float v = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                 rs, (tid * (NACC / 4) + i * NR + j) * 16, 0, 16 /* sc1 */);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned t = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned lastp = (t == (unsigned)a.splits - 1) ? 1u : 0u;
       if (lastp) {
@@ -1404,21 +1412,13 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
 // WGRAD overwrites dw (accumulate = 0) or adds to it (1); either way every element has ONE
 // writer — split-K partial tiles go through the slab and are summed in split order by the
 // last block of the tile — so weight gradients are bitwise reproducible and need no zeroed
-// buffer.  An unrolled conv (u_k0 / u_c0: the 1x1 form of a 3x3/s1/p1 conv on a 2x2 map,
-// whose GEMM output would scatter-add 4 positions onto one tap) computes its weight gradient
-// in the plain 3x3 form instead: the same NHWC bytes read as [B,2,2,C], taps gathered by the
-// implicit im2col, one writer per dW element.
+// buffer.  (An unrolled conv's dense 1x1-form gradient goes to a scratch that
+// kml_conv_fold22_multi folds onto the 3x3 taps in a fixed order.)
 int prep_wgrad(ConvArgs& a, const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
-               int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate, int u_k0,
-               int u_c0, float* slab, unsigned* counters) {
+               int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate, float* slab,
+               unsigned* counters) {
   if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
-  if ((u_k0 || u_c0) && (!u_k0 || !u_c0 || K != 4 * u_k0 || C != 4 * u_c0 || KH != 1 || KW != 1 || H != 1 ||
-                         W != 1))
-    return (int)hipErrorInvalidValue;
-  if (u_k0) {  // plain form of the unrolled conv
-    H = W = 2; C = u_c0; K = u_k0; KH = KW = 3; sh = sw = 1; ph = pw = 1;
-  }
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
   a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
@@ -1443,8 +1443,8 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               float* dw, int B, int H, int W, int C, int K, int KH,
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
-                              int wvariant, int fold_c, int u_k0, int u_c0, int bnf_mask_out, float* wslab,
-                              unsigned* wcounters, int waccumulate, hipStream_t s) {
+                              int wvariant, int fold_c, int bnf_mask_out, float* wslab, unsigned* wcounters,
+                              int waccumulate, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
@@ -1452,8 +1452,8 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                      grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
                      fold_c, bnf_mask_out);
   if (e) return e;
-  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, u_k0, u_c0,
-                 wslab, wcounters);
+  e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, wslab,
+                 wcounters);
   if (e) return e;
   return dispatch_pair(which, ad, aw, s);
 }
@@ -1531,11 +1531,81 @@ KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int
 
 KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                            int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk, int splits, int variant,
-                           int accumulate, int u_k0, int u_c0, float* slab, unsigned* counters, hipStream_t s) {
+                           int accumulate, float* slab, unsigned* counters, hipStream_t s) {
   ConvArgs a;
   const int e = prep_wgrad(a, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, accumulate,
-                           u_k0, u_c0, slab, counters);
+                           slab, counters);
   if (e) return e;
   if (variant) bk = 64;
   return dispatch<WGRAD>(a, bm, bn, bk, variant, s);
+}
+
+// ---------------------------------------------------------------------------------
+// Weight gradient of an unrolled conv (3x3/s1/p1 on a 2x2 map, run as its dense 1x1 form):
+// the 1x1-form GEMM leaves G[(p, n)][(q, c)] (p, q = output / input position 0..3) in a
+// scratch, and dW[n][tap][c] = sum over the (p, q) with tap(p, q) = tap of G — 4 pairs on the
+// centre tap, 2 on an edge, 1 on a corner, 9 taps — summed here in a fixed pair order and
+// stored (acc = 0) or added (acc = 1): deterministic, no atomics.  Up to 16 convs per launch
+// (all the unrolled convs of one backward stage); one thread per (n, c4) of one job.
+// ---------------------------------------------------------------------------------
+struct Fold22Job {
+  const float* g;  // [4K][4C]
+  float* dw;       // [K][3][3][C]
+  int K, C, acc, block_begin;
+};
+struct Fold22Batch {
+  Fold22Job j[16];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_fold22_multi(Fold22Batch fb) {
+  int q = 0;
+  while (q + 1 < fb.n && (int)blockIdx.x >= fb.j[q + 1].block_begin) ++q;  // block-uniform
+  const Fold22Job& jb = fb.j[q];
+  const long long idx = (long long)((int)blockIdx.x - jb.block_begin) * 256 + threadIdx.x;
+  const int C4 = jb.C / 4;
+  if (idx >= (long long)jb.K * C4) return;
+  const int n = (int)(idx / C4), c = (int)(idx - (long long)n * C4) * 4;
+  const long long ldg = 4LL * jb.C;  // G row length
+  float4 t[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) t[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {  // fixed (p, q) order: bitwise reproducible
+      const int tap = ((qq >> 1) - (p >> 1) + 1) * 3 + ((qq & 1) - (p & 1) + 1);
+      const float4 v = *reinterpret_cast<const float4*>(jb.g + ((long long)p * jb.K + n) * ldg + (long long)qq * jb.C + c);
+      t[tap].x += v.x; t[tap].y += v.y; t[tap].z += v.z; t[tap].w += v.w;
+    }
+  float* base = jb.dw + (long long)n * 9 * jb.C + c;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    float4* d = reinterpret_cast<float4*>(base + (long long)k * jb.C);
+    if (jb.acc) {
+      const float4 o = *d;
+      *d = make_float4(o.x + t[k].x, o.y + t[k].y, o.z + t[k].z, o.w + t[k].w);
+    } else {
+      *d = t[k];
+    }
+  }
+}
+
+// gs[i] = [4K][4C] fp32 1x1-form gradient, dws[i] = [K][3][3][C] fp32; dims: n x 3 ints (K, C, acc)
+KML_API int kml_conv_fold22_multi(const float* const* gs, float* const* dws, const int* dims, int n, hipStream_t s) {
+  if (n < 1 || n > 16) return (int)hipErrorInvalidValue;
+  Fold22Batch fb = {};
+  fb.n = n;
+  long long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    Fold22Job& j = fb.j[i];
+    j.g = gs[i]; j.dw = dws[i];
+    j.K = dims[3 * i]; j.C = dims[3 * i + 1]; j.acc = dims[3 * i + 2];
+    if (!j.g || !j.dw || j.K < 1 || j.C % 4 || (((uintptr_t)j.g | (uintptr_t)j.dw) & 15)) return (int)hipErrorInvalidValue;
+    j.block_begin = (int)blocks;
+    blocks += ((long long)j.K * (j.C / 4) + 255) / 256;
+  }
+  if (blocks <= 0 || blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fold22_multi, dim3((unsigned)blocks), dim3(256), 0, s, fb);
+  KML_LAUNCH_CHECK();
 }

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
                                                      float* __restrict__ dbias, int B, int C, int ld,
                                                      long long ignore, float* __restrict__ part,
                                                      unsigned* __restrict__ ticket, int acc) {
-  extern __shared__ float colsh[];  // [4][ld]
+  extern __shared__ float colsh[];  // [4][ld], reused as [4][64] float4 by the last block
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int row = blockIdx.x * 4 + w;
   const bool have = row < B;
@@ -244,15 +244,18 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
     if (have) d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
-  float* mine_row = part + (long long)blockIdx.x * C;
-  for (int c = threadIdx.x; c < C; c += 256)
-    mine_row[c] = (colsh[c] + colsh[ld + c]) + (colsh[2 * ld + c] + colsh[3 * ld + c]);
+  // partial row [C] of this block, published write-through (sc1): no release fence
+  // (CDNA guide §6 G16 R1); the row is padded to CP (multiple of 4) for 16-byte access
+  const int CP = (C + 3) & ~3;
+  float* mine_row = part + (long long)blockIdx.x * CP;
+  for (int c = threadIdx.x; c < CP; c += 256) {
+    const float v = c < C ? (colsh[c] + colsh[ld + c]) + (colsh[2 * ld + c] + colsh[3 * ld + c]) : 0.f;
+    __hip_atomic_store(mine_row + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ unsigned last;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (t == gridDim.x - 1) ? 1u : 0u;
     if (last) {
@@ -263,19 +266,48 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
   }
   __syncthreads();
   if (!last) return;
+  // last block: column sums of the G rows in a fixed order.  Thread = (row slice s of 4,
+  // float4 column j): 16 independent 16-byte loads in flight per batch, the 4 slices combined
+  // through LDS in slice order — bitwise reproducible.
   const int G = (int)gridDim.x;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;   // 4 chains, combined in a fixed order
-    int g = 0;
-    for (; g + 4 <= G; g += 4) {
-      a0 += part[(long long)g * C + c];
-      a1 += part[(long long)(g + 1) * C + c];
-      a2 += part[(long long)(g + 2) * C + c];
-      a3 += part[(long long)(g + 3) * C + c];
+  const int C4 = CP / 4;
+  const int s = threadIdx.x >> 6, jl = threadIdx.x & 63;
+  float4* red4 = reinterpret_cast<float4*>(colsh);  // reuse: [4][64] float4
+  for (int j0 = 0; j0 < C4; j0 += 64) {
+    const int j = j0 + jl;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < C4) {
+      const float4* col = reinterpret_cast<const float4*>(part) + j;
+      int g = s;
+      for (; g + 12 < G; g += 16) {
+        const float4 v0 = col[(long long)g * C4], v1 = col[(long long)(g + 4) * C4];
+        const float4 v2 = col[(long long)(g + 8) * C4], v3 = col[(long long)(g + 12) * C4];
+        a.x += (v0.x + v1.x) + (v2.x + v3.x);
+        a.y += (v0.y + v1.y) + (v2.y + v3.y);
+        a.z += (v0.z + v1.z) + (v2.z + v3.z);
+        a.w += (v0.w + v1.w) + (v2.w + v3.w);
+      }
+      for (; g < G; g += 4) {
+        const float4 v = col[(long long)g * C4];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
     }
-    for (; g < G; ++g) a0 += part[(long long)g * C + c];
-    const float t = (a0 + a1) + (a2 + a3);
-    dbias[c] = acc ? dbias[c] + t : t;
+    __syncthreads();
+    red4[s * 64 + jl] = a;
+    __syncthreads();
+    if (s == 0 && j < C4) {
+      float4 t = red4[jl];
+      for (int k = 1; k < 4; ++k) {
+        const float4 v = red4[k * 64 + jl];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 4 * j + e;
+        if (c < C) dbias[c] = acc ? dbias[c] + tv[e] : tv[e];
+      }
+    }
   }
 }
 
@@ -300,7 +332,8 @@ KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, f
 }
 
 // dbias (optional; bf16 logits, ld % 8 == 0, ld <= 4096): column sums of dlogits, stored
-// (accumulate = 0) or added (1); needs part = [ceil(B/4)][C] fp32 scratch and a zeroed ticket
+// (accumulate = 0) or added (1); needs part = [ceil(B/4)][roundup(C, 4)] fp32 scratch and a
+// zeroed ticket
 KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
                        const float* grad_out, void* dlogits, int B, int C, int ld, long long ignore, int dtype,
                        float* dbias, float* part, unsigned* ticket, int accumulate, hipStream_t s) {
@@ -308,7 +341,8 @@ KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float*
   dim3 g((B + 3) / 4);
   if (dbias) {
     if (dtype != 0 || ld % 8 || ld > 4096 || !part || !ticket) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ce_bwd_bias, g, dim3(256), (size_t)4 * ld * sizeof(float), s, (const bf16_t*)logits, labels,
+    const size_t shm = (size_t)(4 * ld > 1024 ? 4 * ld : 1024) * sizeof(float);  // rows, then [4][64] float4
+    hipLaunchKernelGGL(k_ce_bwd_bias, g, dim3(256), shm, s, (const bf16_t*)logits, labels,
                        ws, out3, grad_out, (bf16_t*)dlogits, dbias, B, C, ld, ignore, part, ticket, accumulate);
     KML_LAUNCH_CHECK();
   }

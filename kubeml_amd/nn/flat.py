@@ -131,6 +131,7 @@ class FlatParamSpace:
         self._accumulators: set = set()  # ... went through grad_storage_of (add-only producer)
         self._fresh: set = set()         # overwriters not yet written since zero_grad()
         self._zeroed_once = False
+        self._folds: list = []           # (param, 1x1-form scratch, grad region, accumulate) to fold
 
     def _bind_i64(self):
         """All int64 buffers as consecutive elements of one arena (one pointer for the
@@ -237,9 +238,25 @@ class FlatParamSpace:
             self._fresh.discard(i)
             self._zero_params([i])
 
+    def defer_fold22(self, p, g):
+        """An unrolled conv left its weight gradient in the dense 1x1 form in ``g``; fold it
+        onto p's 3x3 taps at :meth:`finish_grads` (one launch for all of a stage's convs)."""
+        dw, acc = grad_out(p)
+        self._folds.append((p, g, dw, acc))
+
     def finish_grads(self, params=None):
-        """Zero the regions of overwrite parameters nobody wrote since zero_grad() (a
-        parameter without a gradient this step); call before the gradients are consumed."""
+        """Make the gradients of ``params`` (all if None) final before they are consumed:
+        run the deferred folds, zero the regions of overwrite parameters nobody wrote since
+        zero_grad() (a parameter without a gradient this step)."""
+        if self._folds:
+            ids = None if params is None else {id(p) for p in params}
+            run = [f for f in self._folds if ids is None or id(f[0]) in ids]
+            if run:
+                self._folds = [f for f in self._folds if not (ids is None or id(f[0]) in ids)]
+                from ..ops import kernels as K
+                from .fused import join_wgrad
+                join_wgrad()          # side-stream wgrads (KUBEML_WGRAD_SIDE) wrote the scratch
+                K.fold22_multi([(g, dw, acc) for _, g, dw, acc in run])
         if not self._fresh:
             return
         if params is None:

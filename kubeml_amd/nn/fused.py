@@ -80,13 +80,34 @@ def join_wgrad():
         _WgradSide.pending = False
 
 
+def _wg_buf(conv, x):
+    """Persistent [4K,1,1,4C] fp32 scratch of an unrolled conv's 1x1-form weight gradient
+    (stable address: graphs), folded onto the 3x3 taps by the flat space (defer_fold22)."""
+    Kc, _, _, C = conv.weight._kml_grad_storage.shape
+    shape = (4 * Kc, 1, 1, 4 * C)
+    buf = getattr(conv, "_kml_wg_buf", None)
+    if buf is None or tuple(buf.shape) != shape or buf.device != x.device:
+        buf = torch.empty(shape, dtype=torch.float32, device=x.device)
+        object.__setattr__(conv, "_kml_wg_buf", buf)
+    return buf
+
+
+def _wgrad_target(conv, x, unroll):
+    """(weight-gradient destination, accumulate) — the 1x1-form scratch for an unrolled conv."""
+    if unroll:
+        return _wg_buf(conv, x), False
+    return grad_out(conv.weight)
+
+
 def _wgrad(x, dc, conv, unroll=False):
     from ..ops import kernels as K
     kh, kw = conv.kernel_size
     side = _WgradSide.stream
-    dw, acc = grad_out(conv.weight)
+    dw, acc = _wgrad_target(conv, x, unroll)
     if side is None:
         K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
+        if unroll:
+            conv.weight._kml_flat.defer_fold22(conv.weight, dw)
         return
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -95,6 +116,8 @@ def _wgrad(x, dc, conv, unroll=False):
     x.record_stream(side)
     dc.record_stream(side)
     _WgradSide.pending = True
+    if unroll:
+        conv.weight._kml_flat.defer_fold22(conv.weight, dw)   # runs after join_wgrad()
 
 
 def _wu_buf(conv, w):
@@ -233,9 +256,11 @@ class ConvBNUnit:
             if wt is None and K.bwd_plans(x.shape, w.shape[0], kh, kw, conv.stride, conv.padding,
                                           unroll=wu is not None)[0][4] == K.DIRECT:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
-            dw, acc = grad_out(conv.weight)
+            dw, acc = _wgrad_target(conv, x, wu is not None)
             r = K.conv_bwd(dc, w, x, dw, kh, kw, conv.stride, conv.padding,
                            addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True, accumulate=acc)
+            if wu is not None:
+                conv.weight._kml_flat.defer_fold22(conv.weight, dw)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out

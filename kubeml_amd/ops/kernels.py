@@ -523,8 +523,9 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     instantiated pair, else as two launches.  ``wt``: precomputed transposed weights for
     a direct-variant dgrad (:func:`weight_transpose_multi`); made here when missing.
     Returns dx, or (dx, (part, G)) when ``bnf`` is given.  wu: unrolled weight
-    (:func:`unrolled22`): the dgrad runs in the dense 1x1 form, the weight gradient in the
-    plain 3x3 form (one writer per element).  bnf_mask: as in :func:`conv_dgrad`."""
+    (:func:`unrolled22`): both GEMMs run in the dense 1x1 form; ``dw`` is then the
+    ``[4K,1,1,4C]`` fp32 scratch of the 1x1-form weight gradient (stored), which
+    :func:`fold22_multi` folds onto the 3x3 taps.  bnf_mask: as in :func:`conv_dgrad`."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -534,15 +535,16 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     sh, sw = stride
     ph, pw = pad
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
-    if tuple(dy.shape) != (B, OH, OW, K) or tuple(w.shape) != (K, KH, KW, C) or tuple(dw.shape) != (K, KH, KW, C):
+    want_dw = (4 * K, 1, 1, 4 * C) if wu is not None else (K, KH, KW, C)
+    if tuple(dy.shape) != (B, OH, OW, K) or tuple(w.shape) != (K, KH, KW, C) or tuple(dw.shape) != want_dw:
         raise ValueError("conv_bwd shape mismatch")
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
-    fold, u = 0, (0, 0)
+    fold = 0
     if wu is not None:
         _check_wu(x.shape, w, wu, KH, KW, stride, pad)
         dy, x, addend, bnf = _u22_views(B, C, K, dy=dy, x=x, addend=addend, bnf=bnf)
-        w, fold, u = wu, C, (K, C)
+        w, fold, accumulate = wu, C, False
         H = W = OH = OW = 1
         KH = KW = sh = sw = 1
         ph = pw = 0
@@ -553,7 +555,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
     if not grouped:
-        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, _u=u, accumulate=accumulate)
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, accumulate=accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
                        bnf_mask=bnf_mask)
         if not fold:
@@ -576,12 +578,12 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         dsplits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
-    wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan, u)
+    wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan)
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i i i p p i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
-             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold), u[0], u[1],
+             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
              int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _s())
     if fold:
         out = out.view(B, 2, 2, C // 4)
@@ -612,12 +614,8 @@ def weight_transpose_multi(ws, wts):
              ctypes.addressof(dims), n, _s())
 
 
-def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg, u):
-    """Split-K slab + tickets of a weight-gradient GEMM (None, None without split-K).  An
-    unrolled conv (u = (K, C) of the 3x3 conv, geometry = its 1x1 form) computes its weight
-    gradient in the plain 3x3 form on the 2x2 map (conv_igemm.hip prep_wgrad)."""
-    if u[0]:
-        B, H, W, C, K, KH, KW, stride, pad = B, 2, 2, u[1], u[0], 3, 3, (1, 1), (1, 1)
+def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg):
+    """Split-K slab + tickets of a weight-gradient GEMM (None, None without split-K)."""
     bm, bn, bk, splits, variant = cfg
     if variant:
         bk = 64
@@ -626,40 +624,59 @@ def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg, u):
     return _splitk_ws(device, K, (r1 - r0) * (s1 - s0) * C, bm, bn, effective_splits(B * OH * OW, bk, splits))
 
 
-def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, _u=(0, 0), accumulate=True):
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulate=True):
     """Conv weight gradient into dw[Cout,KH,KW,Cin] (fp32): ``dw += wgrad`` (accumulate) or
     ``dw = wgrad`` (overwrite: the buffer need not be zeroed).  Deterministic: one writer per
     element, split-K partials summed in split order.  unroll: an unrolled conv
-    (:func:`unrolled22`); its weight gradient runs in the plain 3x3 form."""
+    (:func:`unrolled22`): ``dw`` is then the ``[4K,1,1,4C]`` fp32 scratch of its dense 1x1-form
+    gradient, stored; :func:`fold22_multi` folds it onto the 3x3 taps."""
     _chk(x, BF16, "x", 4)
     _chk(dy, BF16, "dy", 4)
     _chk(dw, F32, "dw", 4)
     if unroll:
         B, H, W, C = x.shape
         K = dy.shape[3]
-        if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (K, 3, 3, C):
-            raise ValueError("conv is not unrolled")
+        if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (4 * K, 1, 1, 4 * C):
+            raise ValueError("unrolled wgrad: needs the [4K,1,1,4C] fp32 scratch")
         _, x1, _, _ = _u22_views(B, C, K, x=x)
-        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, _u=(K, C),
-                          accumulate=accumulate)
+        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, accumulate=False)
     B, H, W, C = x.shape
     K = dy.shape[3]
     sh, sw = stride
     ph, pw = pad
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
-    if _u[0]:
-        if tuple(dw.shape) != (_u[0], 3, 3, _u[1]) or (K, C) != (4 * _u[0], 4 * _u[1]) or (KH, KW) != (1, 1):
-            raise ValueError("unrolled wgrad shape mismatch")
-    elif tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
+    if tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
         raise ValueError("wgrad shape mismatch")
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
     bm, bn, bk, splits, variant = cfg
-    slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg, _u)
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i i i p p s",
+    slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg)
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i p p s",
              _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant,
-             int(bool(accumulate)), int(_u[0]), int(_u[1]), _p(slab), _p(cnt), _s())
+             int(bool(accumulate)), _p(slab), _p(cnt), _s())
     return dw
+
+
+def fold22_multi(jobs):
+    """jobs: [(g [4K,1,1,4C] fp32, dw [K,3,3,C] fp32 region, accumulate)] — the unrolled convs'
+    weight gradients folded onto their 3x3 taps (fixed pair order, no atomics), 16 per launch."""
+    import ctypes
+    for i in range(0, len(jobs), 16):
+        part = jobs[i:i + 16]
+        n = len(part)
+        gp = (ctypes.c_void_p * n)()
+        dp = (ctypes.c_void_p * n)()
+        dims = (ctypes.c_int * (3 * n))()
+        for k, (g, dw, acc) in enumerate(part):
+            _chk(g, F32, "g", 4)
+            _chk(dw, F32, "dw", 4)
+            K, _, _, C = dw.shape
+            if tuple(dw.shape) != (K, 3, 3, C) or tuple(g.shape) != (4 * K, 1, 1, 4 * C):
+                raise ValueError("fold22_multi: shape mismatch")
+            gp[k], dp[k] = g.data_ptr(), dw.data_ptr()
+            dims[3 * k], dims[3 * k + 1], dims[3 * k + 2] = K, C, int(bool(acc))
+        HIP.call("kml_conv_fold22_multi", "p p p i s", ctypes.addressof(gp), ctypes.addressof(dp),
+                 ctypes.addressof(dims), n, _s())
 
 
 # --------------------------------------------------------------------------------------
@@ -929,7 +946,7 @@ def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=N
             raise ValueError("ce_bwd: bias fusion needs bf16 logits with ld % 8 == 0, ld <= 4096")
     part = cnt = None
     if dbias is not None:
-        part = torch.empty(_cdiv(B, 4) * C, dtype=F32, device=logits.device)
+        part = torch.empty(_cdiv(B, 4) * _cdiv(C, 4) * 4, dtype=F32, device=logits.device)
         cnt = _COUNTERS.take(logits.device, 1)
     HIP.call("kml_ce_bwd", "p p p p p p i i i l i p p p i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
              _p(d), B, C, ld, int(ignore_index), dt, _p(dbias), _p(part), _p(cnt), int(bool(accumulate)), _s())

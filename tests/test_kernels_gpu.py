@@ -683,20 +683,32 @@ def test_unrolled_conv_bwd_matches_3x3(B, C, Kc):
     cc = _bf(torch.randn(B, 2, 2, C, device=dev))
     mean = torch.randn(C, device=dev) * 0.1
     rstd = torch.rand(C, device=dev) + 0.5
-    dw = torch.zeros(Kc, 3, 3, C, device=dev)
-    dx, (part, G) = K.conv_bwd(dy, w, x, dw, *args, addend=addend, bnf=(yc, cc, mean, rstd), wu=wu)
+    # weight gradient: the dense 1x1 form into a [4K,1,1,4C] scratch, folded onto the 3x3
+    # taps by fold22_multi (fixed pair order: stored, or added onto what dw holds)
+    g = torch.full((4 * Kc, 1, 1, 4 * C), float("nan"), device=dev)   # every element written
+    dx, (part, G) = K.conv_bwd(dy, w, x, g, *args, addend=addend, bnf=(yc, cc, mean, rstd), wu=wu)
     assert dx.shape == (B, 2, 2, C)
     assert _rel(dx, dx_ref) < 1e-2
+    dw = torch.full((Kc, 3, 3, C), float("nan"), device=dev)
+    K.fold22_multi([(g, dw, False)])
     assert _rel(dw, dw_ref) < 1e-2
+    dw_acc = torch.ones(Kc, 3, 3, C, device=dev)
+    K.fold22_multi([(g, dw_acc, True)])
+    torch.testing.assert_close(dw_acc, dw + 1.0, rtol=0, atol=1e-5)
+    g2 = torch.empty_like(g)
+    K.conv_bwd(dy, w, x, g2, *args, addend=addend, bnf=(yc, cc, mean, rstd), wu=wu)
+    assert torch.equal(g, g2)                                           # deterministic
     dz = dx.float() * (yc.float() > 0)
     xh = (cc.float() - mean) * rstd
     tot = part.view(G, 2, C).sum(0)
     torch.testing.assert_close(tot[0], dz.reshape(-1, C).sum(0), rtol=2e-3, atol=2e-1)
     torch.testing.assert_close(tot[1], (dz * xh).reshape(-1, C).sum(0), rtol=2e-3, atol=2e-1)
     # the separate dgrad / wgrad entry points
-    dw2 = torch.zeros_like(dw)
-    K.conv_wgrad(x, dy, dw2, *args, unroll=True)
-    assert _rel(dw2, dw_ref) < 1e-2
+    g3 = torch.empty_like(g)
+    K.conv_wgrad(x, dy, g3, *args, unroll=True)
+    dw2 = torch.empty_like(dw)
+    K.fold22_multi([(g3, dw2, False)])
+    assert torch.equal(dw2, dw)
     dx2 = K.conv_dgrad(dy, w, x.shape, *args, addend=addend, wu=wu)
     assert _rel(dx2, dx_ref) < 1e-2
 
@@ -760,3 +772,10 @@ def test_ce_bwd_adds_bias_gradient(B, C, ld):
     want = torch.full((ld,), 0.25, device=dev)
     want[:C] += d0.float()[:, :C].sum(0)
     torch.testing.assert_close(db, want, rtol=1e-5, atol=1e-6)
+    # overwrite mode (no zeroed buffer needed) and bitwise reproducibility (ordered rows)
+    db2 = torch.full((ld,), float("nan"), device=dev)
+    K.ce_bwd(logits, lab, ws, out3, classes=C, dbias=db2, accumulate=False)
+    torch.testing.assert_close(db2[:C], d0.float()[:, :C].sum(0), rtol=1e-5, atol=1e-6)
+    db3 = torch.empty_like(db2)
+    K.ce_bwd(logits, lab, ws, out3, classes=C, dbias=db3, accumulate=False)
+    assert torch.equal(db2[:C], db3[:C])
