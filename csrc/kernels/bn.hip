@@ -636,8 +636,11 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
     }
     const float rstd = rsqrtf(var + eps);
     const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
-    scale[c] = g * rstd;
-    shift[c] = bb - mean * g * rstd;
+    // channel-transposed slots (c % 8) * C/8 + c / 8: the 8-channel reads below then hit
+    // consecutive words across consecutive lanes (no LDS bank conflicts)
+    const int tslot = (c & 7) * (C >> 3) + (c >> 3);
+    scale[tslot] = g * rstd;
+    shift[tslot] = bb - mean * g * rstd;
     if (mode == 0 && blockIdx.x == 0) {
       if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
       if (run_mean) {
@@ -648,10 +651,10 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
     }
   }
   __syncthreads();
-  const int c0 = (i0 % (C / 8)) * 8;
+  const int CH8 = C >> 3, j8 = i0 % CH8;
   float sc[8], sf[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sf[k] = shift[c0 + k]; }
+  for (int k = 0; k < 8; ++k) { sc[k] = scale[k * CH8 + j8]; sf[k] = shift[k * CH8 + j8]; }
   // grid-stride batches of V chunks (large tensors); T % (C/8) == 0 keeps the channels
   for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
     if (it > 0) {
@@ -715,6 +718,10 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   // kb | kc are contiguous: kb[0..C) kc[0..C)
   if (early) er.finish(part, G, kb, red4);
   else sum_partial_rows<NT>(part, G, 2 * C, kb, red4);
+  // per-channel coefficients into channel-transposed slots (c % 8) * C/8 + c / 8 of a second
+  // area (kb | kc stay readable by other channels' threads until the barrier): the 8-channel
+  // reads below hit consecutive words across consecutive lanes (no LDS bank conflicts)
+  float* tco = ka + 5 * C;  // [5][C]: ka, kb/M, kc/M, mu, rs transposed
   for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
     if (blockIdx.x == 0) {  // one writer: store (overwrite) or add (accumulate)
@@ -722,17 +729,21 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
       dgamma[c] = acc ? dgamma[c] + sg : sg;
     }
     const float gm = gamma ? gamma[c] : 1.f;
-    ka[c] = gm * rstd[c];
-    mu[c] = mean[c];
-    rs[c] = rstd[c];
+    const int tslot = (c & 7) * (C >> 3) + (c >> 3);
+    tco[tslot] = gm * rstd[c];
+    tco[C + tslot] = sb * invM;
+    tco[2 * C + tslot] = sg * invM;
+    tco[3 * C + tslot] = mean[c];
+    tco[4 * C + tslot] = rstd[c];
   }
   __syncthreads();
-  const int c0 = (i0 % (C / 8)) * 8;
+  const int CH8 = C >> 3, j8 = i0 % CH8;
   float a8[8], b8[8], g8[8], m8[8], r8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    a8[k] = ka[c0 + k]; b8[k] = kb[c0 + k] * invM; g8[k] = kc[c0 + k] * invM;
-    m8[k] = mu[c0 + k]; r8[k] = rs[c0 + k];
+    const int t = k * CH8 + j8;
+    a8[k] = tco[t]; b8[k] = tco[C + t]; g8[k] = tco[2 * C + t];
+    m8[k] = tco[3 * C + t]; r8[k] = tco[4 * C + t];
   }
   for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
     if (it > 0) {
@@ -1115,7 +1126,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 4);
     const unsigned grid = v_grid(n8, V);
-    const size_t shm = (4 * TPB + 5 * C) * sizeof(float);
+    const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
 #define KML_BWD_V(VV)                                                                                          \
   hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, dy, y, x, mean, rstd, gamma, part, \
                      G, dgamma, dbeta, dx, dres, M, C, acc)

@@ -123,9 +123,18 @@ __device__ __forceinline__ Blk hw_blk() {
   return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x};
 }
 
+// K-strided [BK][R] tiles of R = 32/64/128 columns use the XOR chunk swizzle of the glds
+// kernels (swz_ks, conflict-free reads and writes per tools/lds_banks.py); other widths keep
+// the +PADR row padding (2-3-way conflicts).
+template <int R>
+struct KsSwz {
+  static constexpr bool ON = (R == 32 || R == 64 || R == 128);
+  static constexpr int LD = ON ? R : R + PADR;  // row length in bf16
+};
+
 template <int R, bool KCONTIG, int BK>
 struct TileShape {
-  static constexpr int ELEMS = KCONTIG ? R * (BK + PADK) : BK * (R + PADR);
+  static constexpr int ELEMS = KCONTIG ? R * (BK + PADK) : BK * KsSwz<R>::LD;
   static constexpr int CHUNKS = R * BK / 8;  // 16-byte chunks per stage
   static constexpr int PER_THREAD = (CHUNKS + 255) / 256;
 };
@@ -293,11 +302,23 @@ __device__ __forceinline__ bf16x8_t frag_kcontig(const bf16_t* lds, int row0, in
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
 
 template <int R>
+__device__ __forceinline__ int swz_ks(int r);
+
+template <int R>
 __device__ __forceinline__ bf16x8_t frag_kstrided(const bf16_t* lds, int row0, int ks, int lane) {
   const int il = lane & 15, g = lane >> 4;
   const int col = row0 + 4 * (il & 3);
-  const bf16_t* p0 = lds + (32 * ks + 8 * g + (il >> 2)) * (R + PADR) + col;
-  const bf16_t* p1 = p0 + 4 * (R + PADR);
+  const int k0 = 32 * ks + 8 * g + (il >> 2);
+  const bf16_t* p0;
+  const bf16_t* p1;
+  if constexpr (KsSwz<R>::ON) {  // swizzled 16-byte chunk (col / 8) of rows k0, k0 + 4
+    const int ch = col >> 3, within = col & 7;
+    p0 = lds + k0 * R + ((ch ^ swz_ks<R>(k0)) << 3) + within;
+    p1 = lds + (k0 + 4) * R + ((ch ^ swz_ks<R>(k0 + 4)) << 3) + within;
+  } else {
+    p0 = lds + k0 * (R + PADR) + col;
+    p1 = p0 + 4 * (R + PADR);
+  }
   v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p0));
   v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s_t*)(p1));
   bf16x8_t f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -602,14 +623,24 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const Con
     int q = tid + i * 256;
     if (q >= TA::CHUNKS) q = TA::CHUNKS - 1;  // surplus threads duplicate the last chunk
     if constexpr (A_KC) { ga[i].init(a, m0 + q / KC, q); offA[i] = (q / KC) * (BK + PADK) + (q % KC) * 8; }
-    else { ga[i].init(a, m0, q); constexpr int CPR = BM / 8; offA[i] = (q / CPR) * (BM + PADR) + (q % CPR) * 8; }
+    else {
+      ga[i].init(a, m0, q);
+      constexpr int CPR = BM / 8;
+      const int r = q / CPR, c = q % CPR;
+      offA[i] = KsSwz<BM>::ON ? r * BM + ((c ^ swz_ks<BM>(r)) << 3) : r * (BM + PADR) + c * 8;
+    }
   }
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
     int q = tid + i * 256;
     if (q >= TB::CHUNKS) q = TB::CHUNKS - 1;
     if constexpr (B_KC) { gb[i].init(a, n0 + q / KC, q); offB[i] = (q / KC) * (BK + PADK) + (q % KC) * 8; }
-    else { gb[i].init(a, n0, q); constexpr int CPR = BN / 8; offB[i] = (q / CPR) * (BN + PADR) + (q % CPR) * 8; }
+    else {
+      gb[i].init(a, n0, q);
+      constexpr int CPR = BN / 8;
+      const int r = q / CPR, c = q % CPR;
+      offB[i] = KsSwz<BN>::ON ? r * BN + ((c ^ swz_ks<BN>(r)) << 3) : r * (BN + PADR) + c * 8;
+    }
   }
 
   uint4 ra0[PA], rb0[PB], ra1[PA], rb1[PB];
