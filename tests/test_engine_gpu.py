@@ -158,10 +158,20 @@ def _bench(*extra, timeout=600):
 
 
 def test_bench_measures_epoch_with_validation():
-    d = _bench("--steps", "10", "--warmup", "2", "--batch", "128")
+    d = _bench("--steps", "10", "--warmup", "2", "--batch", "128", "--e2e", "off")
     assert d["n_gpus"] == 1 and d["value"] > 0 and d["epoch_measured"] is True
     assert d["val_images"] >= 10000 and d["epoch_time_s"] > d["epoch_train_s"] > 0
     assert d["loss_first_last"][1] == d["loss_first_last"][1]
+    assert "e2e_epoch_time_s" not in d
+
+
+def test_bench_reports_the_framework_epoch():
+    """bench.py's default (N = 1) also runs the epoch through the whole stack: server, worker,
+    storage upload, `kubeml train` with validation every epoch (experiments/e2e.py)."""
+    d = _bench("--steps", "10", "--warmup", "2", "--e2e", "on", timeout=900)
+    assert d.get("e2e_error") is None, d.get("e2e_error")
+    assert d["e2e_epoch_time_s"] > 0 and len(d["e2e_epoch_wall_s"]) == 3
+    assert d["e2e_train_task_img_s"] > 0 and d["e2e_vs_bench_step_rate"] > 0
 
 
 def test_bench_rccl_rehearsal_overlapped_graph_comm():
