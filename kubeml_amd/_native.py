@@ -52,7 +52,9 @@ def _load(name: str, autobuild: bool = True) -> ctypes.CDLL:
         if not os.path.exists(path) and autobuild and os.environ.get("KUBEML_NO_AUTOBUILD") != "1":
             try:
                 from . import _build
-                _build.build()
+                from .runtime.worker import busy
+                with busy(10.0):                   # first hipcc build: minutes, not a hang
+                    _build.build()
             except Exception as e:  # pragma: no cover - surfaced below
                 raise NativeLibraryMissing(f"{name} missing and build failed: {e}") from e
         if not os.path.exists(path):

@@ -313,26 +313,31 @@ class FlatParamSpace:
         return self.master
 
 
-def module_buffers(module: torch.nn.Module):
-    """([(module, name)] of floating buffers, [(module, name)] of int64 buffers) in
-    ``named_buffers`` order."""
-    fl, il = [], []
+def module_buffers(module: torch.nn.Module, with_other: bool = False):
+    """([(module, name)] of fp32 buffers, [(module, name)] of scalar int64 buffers) in
+    ``named_buffers`` order; with ``with_other`` also the remaining persistent buffers (other
+    floating dtypes, int32 / bool, non-scalar int64), which stay out of the fp32 state buffer
+    and are averaged / broadcast through a side pack (parallel/kavg.py)."""
+    fl, il, other = [], [], []
     for mod in module.modules():
         for name, b in mod._buffers.items():
             if b is None or name in getattr(mod, "_non_persistent_buffers_set", ()):
                 continue
-            if b.is_floating_point():
+            if b.dtype == torch.float32:
                 fl.append((mod, name))
             elif b.dtype == torch.int64 and b.numel() == 1:
                 il.append((mod, name))
-    return fl, il
+            else:
+                other.append((mod, name))
+    return (fl, il, other) if with_other else (fl, il)
 
 
 def flatten_module(module: torch.nn.Module, device=None, buffers: bool = True) -> FlatParamSpace:
     """Move all trainable parameters (and, by default, the buffers) of ``module`` into
     one FlatParamSpace."""
-    space = FlatParamSpace(list(module.parameters()), device=device,
-                           buffers=module_buffers(module) if buffers else None)
+    fl, il, other = module_buffers(module, with_other=True) if buffers else ([], [], [])
+    space = FlatParamSpace(list(module.parameters()), device=device, buffers=(fl, il) if buffers else None)
+    space.other_buffers = other      # not in ``state``: averaged / broadcast by a side pack
     module._kml_flat = space
     return space
 

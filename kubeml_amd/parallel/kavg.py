@@ -76,7 +76,33 @@ class ModelAverager:
         K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, participate)
         self._all_reduce(comm, sp.state)
         K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
+        self._average_other(comm, sp, participate)
         return -1
+
+    def _average_other(self, comm: Comm, sp, participate: bool):
+        """Buffers outside the fp32 state (other float dtypes, int32 / bool, non-scalar int64):
+        one fp64 side pack + count, averaged like the reference's merger (integer buffers use
+        floor division, parallelSGD.go:26-54)."""
+        others = getattr(sp, "other_buffers", None)
+        if not others:
+            return
+        ts = [getattr(m, n) for m, n in others]
+        pack = torch.cat([t.detach().reshape(-1).double() for t in ts] +
+                         [torch.ones(1, dtype=torch.float64, device=ts[0].device)])
+        if not participate:
+            pack.zero_()
+        self._all_reduce(comm, pack)
+        cnt = pack[-1:].clamp_min(1.0)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                k = t.numel()
+                v = pack[off:off + k].view(t.shape) / cnt
+                if t.is_floating_point():
+                    t.copy_(v.to(t.dtype))
+                else:
+                    t.copy_(torch.floor(v + 1e-9).to(t.dtype))
+                off += k
 
     def _average_host(self, comm: Comm, participate: bool) -> int:
         """CPU path: pack everything into one fp32 vector (+count), one all-reduce."""
@@ -125,6 +151,7 @@ class ModelAverager:
             comm.all_reduce_(seg)
             # parameters are untouched: finish only over the buffer range (shadow not needed)
             K.kavg_finish_(seg, 0, sp.count_idx - sp.numel, None, arena, sp.i64_off - sp.numel, sp.n_i64)
+            self._average_other(comm, sp, True)
             return
         bufs = self._buffers()
         if not bufs:
@@ -147,6 +174,12 @@ class ModelAverager:
         sp = self._space()
         if sp is not None:
             comm.broadcast_(sp.state, src)     # parameters + buffers + counters slots
+            for m, n in getattr(sp, "other_buffers", None) or ():
+                t = getattr(m, n)
+                c = t.contiguous()
+                comm.broadcast_(c, src)
+                if c.data_ptr() != t.data_ptr():
+                    t.copy_(c)
             from ..ops import kernels as K
             arena = sp.i64_arena_now()
             if arena is not None:

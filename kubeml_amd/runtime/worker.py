@@ -62,6 +62,39 @@ def progress(n: int = 1):
         arr[rank] += n
 
 
+class busy:
+    """Keep this worker's progress counter moving during a long phase that makes no
+    K-AVG / minibatch progress of its own (first native build, checkpoint restore, graph
+    capture, importing the user's file): a heartbeat thread ticks every ``interval`` seconds,
+    so the pool's stall watchdog only fires on a real hang.  No-op outside a pool worker."""
+
+    def __init__(self, interval: float = 5.0):
+        self.interval = interval
+        self._stop = None
+        self._t = None
+
+    def __enter__(self):
+        if _PROGRESS is None:
+            return self
+        import threading
+        self._stop = threading.Event()
+
+        def tick():
+            while not self._stop.wait(self.interval):
+                progress()
+        progress()
+        self._t = threading.Thread(target=tick, name="kubeml-busy", daemon=True)
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._stop is not None:
+            self._stop.set()
+            self._t.join()
+            progress()
+        return False
+
+
 def load_function(path: str, name: str):
     """Import the user's function file under a unique module name (``/specialize``)."""
     mod_name = f"kubeml_fn_{name}_{abs(hash((path, os.path.getmtime(path)))) % 10**8}"
@@ -71,7 +104,8 @@ def load_function(path: str, name: str):
     spec = importlib.util.spec_from_file_location(mod_name, path)
     mod = importlib.util.module_from_spec(spec)
     sys.modules[mod_name] = mod
-    spec.loader.exec_module(mod)
+    with busy():
+        spec.loader.exec_module(mod)
     if not hasattr(mod, "main"):
         raise AttributeError(f"function {name} has no main()")
     return mod

@@ -198,8 +198,10 @@ class KubeModel(ABC):
         ctx = current_task()
         path = ctx.extra.get("restore") if ctx is not None else None
         if path and getattr(self, "_restored_from", None) != path:
+            from ..runtime.worker import busy
             from ..store.ckpt import load_checkpoint
-            load_checkpoint(self._network, path)
+            with busy():
+                load_checkpoint(self._network, path)
             self._restored_from = path
 
     def _on_train_end(self):
@@ -521,7 +523,9 @@ class KubeModel(ABC):
                                  plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0)
             if st.peer is not None and comm is not None:
                 comm.grad_peer = st.peer          # one gradient transport per group, reused
-            st.capture()
+            from ..runtime.worker import busy
+            with busy():                          # capture + warm-up can take seconds
+                st.capture()
             g = self._graphs[key] = {"x": xs, "y": ys, "step": st}
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)

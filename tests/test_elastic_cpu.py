@@ -112,3 +112,42 @@ def test_two_static_jobs_share_the_node(tmp_path):
             assert _wait(c, j)["state"] == "finished"
     finally:
         srv.stop()
+
+
+def test_non_fp32_buffers_are_averaged_by_the_side_pack():
+    """Buffers outside the fp32 state (fp64, int32, bool, non-scalar int64) are averaged with
+    the reference's rules (floats averaged, integers floor-divided) and broadcast."""
+    import threading
+
+    import torch
+    from kubeml_amd.nn.flat import flatten_module
+    from kubeml_amd.parallel.comm import ThreadComm
+    from kubeml_amd.parallel.kavg import ModelAverager
+
+    class Odd(torch.nn.Module):
+        def __init__(self, r):
+            super().__init__()
+            self.lin = torch.nn.Linear(2, 2)
+            self.register_buffer("f64", torch.full((3,), float(r), dtype=torch.float64))
+            self.register_buffer("i32", torch.full((2,), 3 * r + 1, dtype=torch.int32))
+            self.register_buffer("vec64", torch.tensor([r, 2 * r], dtype=torch.int64))
+
+    world = 3
+    comms = ThreadComm.create(world)
+    mods = [Odd(r) for r in range(world)]
+    for m in mods:
+        flatten_module(m)
+        assert {n for _, n in m._kml_flat.other_buffers} == {"f64", "i32", "vec64"}
+
+    def body(r):
+        av = ModelAverager(mods[r])
+        av._average_other(comms[r], mods[r]._kml_flat, True)
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30)
+    for m in mods:
+        assert m.f64.dtype == torch.float64 and torch.allclose(m.f64, torch.full((3,), 1.0, dtype=torch.float64))
+        assert m.i32.dtype == torch.int32 and m.i32.tolist() == [4, 4]          # floor((1+4+7)/3)
+        assert m.vec64.tolist() == [1, 2]                                         # floor(3/3), floor(6/3)
