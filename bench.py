@@ -313,6 +313,8 @@ def main():
                        "grad_comm_dtype": plan.wire if plan is not None else args.comm_dtype,
                        "comm_plan": plan.tag() if plan is not None else None,
                        "comm_plan_source": plan.source if plan is not None else None,
+                       "comm_transport": (("peer" if getattr(step, "peer", None) is not None else "rccl")
+                                          if comm else None),
                        "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }

@@ -103,7 +103,13 @@ struct ConvArgs {
   int kchunk;            // split-K chunk (multiple of BK)
   int splits;
   int relu;
-  int accumulate;        // WGRAD: atomicAdd (1) or store (0)
+  int accumulate;        // WGRAD: add (1) or store (0)
+  // WGRAD of a 1x1/s1/p0 conv (a Linear): the bias gradient sum_k dY[k][m] comes out of the
+  // same GEMM as one extra column n = C whose B operand is all ones (the ones page), so no
+  // separate column-sum pass and no cross-block reduction.  N then counts that column.
+  float* dbias;          // [Cout] fp32 or null
+  int bias_acc;          // dbias: add (1) or store (0)
+  const bf16_t* op;      // 16-byte ones page: bf16 {1, 0, 0, 0, 0, 0, 0, 0}
   // Unrolled small-map convs (ops.kernels.unrolled): a 3x3/s1/p1 conv on a 2x2 map runs as a
   // 1x1 conv of 4C -> 4K channels on a 1x1 map (only the taps that touch the image; the
   // im2col of the 3x3 form is 5/9 zero padding).  fold_c: the FWD/DGRAD output channel col =
@@ -270,12 +276,14 @@ struct WgradA {  // LDS row = pixel k, cols = cout; chunk = dY[k][n..n+7]
 template <int BK, int BN>
 struct WgradB {  // LDS row = pixel k, cols j = (tap, cin); chunk = X[pixel shifted by tap][c..c+7]
   int krow, r, s, c;
-  bool valid;
+  bool valid, ones;
   __device__ void init(const ConvArgs& a, int n0, int q) {
     constexpr int CPR = BN / 8;
     krow = q / CPR;
     const int j = n0 + (q % CPR) * 8;
-    valid = j < a.N;
+    const int nreal = a.dbias ? a.N - 1 : a.N;  // the bias column (if any) is n = nreal
+    valid = j < nreal;
+    ones = a.dbias && j == nreal;
     const int jj = valid ? j : 0;
     const int tap = fdiv(jj, a.fd_C);
     c = jj - tap * a.C;
@@ -288,6 +296,7 @@ struct WgradB {  // LDS row = pixel k, cols j = (tap, cin); chunk = X[pixel shif
     const int b = fdiv(t, a.fd_OH), oh = t - b * a.OH;
     const int ih = oh * a.sh - a.ph + r, iw = ow * a.sw - a.pw + s;
     const bool ok = valid && k < kend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    if (ones) return k < kend ? a.op : a.zp;
     return ok ? a.x + ((b * a.H + ih) * a.W + iw) * a.C + c : a.zp;
   }
 };
@@ -437,7 +446,31 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     for (int i = 0; i < MR; ++i)
 #pragma unroll
       for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < a.splits; ++sp) {
+    // Batches of U slabs are loaded before any of them is added: the reduce costs
+    // ceil(splits / U) memory round trips instead of one per split (the additions stay in
+    // split order, so the sum is unchanged bit for bit).  U keeps the batch at 8 float4.
+    constexpr int NV = MR * NR;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    int sp = 0;
+    for (; sp + U <= a.splits; sp += U) {
+      float4 v[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float4* src = reinterpret_cast<const float4*>(slab + (long long)(sp + u) * 256 * NACC) + tid * (NACC / 4);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[u][k] = src[k];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) {
+            const float4 w = v[u][i * NR + j];
+            acc[i][j][0] += w.x; acc[i][j][1] += w.y; acc[i][j][2] += w.z; acc[i][j][3] += w.w;
+          }
+    }
+    for (; sp < a.splits; ++sp) {
       const float4* src = reinterpret_cast<const float4*>(slab + (long long)sp * 256 * NACC) + tid * (NACC / 4);
 #pragma unroll
       for (int i = 0; i < MR; ++i)
@@ -455,6 +488,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     for (int j = 0; j < NR; ++j) {
       const int col = n0 + wn * WN + j * 16 + fr;
       if (col >= a.N) continue;
+      if (a.dbias && col == a.N - 1) {  // the ones column: bias gradient of output channel row
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = m0 + wm * WM + i * 16 + fq * 4 + e;
+            if (row < a.M) a.dbias[row] = a.bias_acc ? a.dbias[row] + acc[i][j][e] : acc[i][j][e];
+          }
+        continue;
+      }
       const int tap = fdiv(col, a.fd_C), c = col - tap * a.C;
       int r, s;
       tap_rs(a, tap, r, s);
@@ -1348,12 +1391,22 @@ __global__ __launch_bounds__(256) void k_unroll22_multi(UnrollBatch ub) {
 }
 
 __device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];  // zero-initialised device global
+__device__ __attribute__((aligned(64))) bf16_t g_one_page[8] = {0x3F80, 0, 0, 0, 0, 0, 0, 0};  // bf16 1.0, 0 x 7
 
 const bf16_t* zero_page() {
   static const bf16_t* p = nullptr;
   if (!p) {
     void* d = nullptr;
     if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_zero_page)) == hipSuccess) p = (const bf16_t*)d;
+  }
+  return p;
+}
+
+const bf16_t* one_page() {
+  static const bf16_t* p = nullptr;
+  if (!p) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_one_page)) == hipSuccess) p = (const bf16_t*)d;
   }
   return p;
 }
@@ -1447,13 +1500,16 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
 // kml_conv_fold22_multi folds onto the 3x3 taps in a fixed order.)
 int prep_wgrad(ConvArgs& a, const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, int accumulate, float* slab,
-               unsigned* counters) {
+               unsigned* counters, float* dbias, int bias_acc) {
   if (variant) bk = 64;
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  // the ones column needs every pixel to see every input channel once: 1x1, stride 1, no pad
+  if (dbias && (KH != 1 || KW != 1 || sh != 1 || sw != 1 || ph || pw)) return (int)hipErrorInvalidValue;
   a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.dy = dy; a.dw = dw; a.zp = zero_page();
-  a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C; a.Kd = B * a.OH * a.OW;
-  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  a.dbias = dbias; a.bias_acc = bias_acc ? 1 : 0; a.op = one_page();
+  a.M = K; a.N = (a.r1 - a.r0) * (a.s1 - a.s0) * C + (dbias ? 1 : 0); a.Kd = B * a.OH * a.OW;
+  if (!a.zp || !a.op) return (int)hipErrorInvalidSymbol;
   set_splits(a, bk, splits);
   if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
   a.slab = slab; a.counters = counters;
@@ -1475,7 +1531,7 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
                               int wvariant, int fold_c, int bnf_mask_out, float* wslab, unsigned* wcounters,
-                              int waccumulate, hipStream_t s) {
+                              int waccumulate, float* wbias, int wbias_acc, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
@@ -1484,7 +1540,7 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                      fold_c, bnf_mask_out);
   if (e) return e;
   e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, wslab,
-                 wcounters);
+                 wcounters, wbias, wbias_acc);
   if (e) return e;
   return dispatch_pair(which, ad, aw, s);
 }
@@ -1562,10 +1618,11 @@ KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int
 
 KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, int H, int W, int C, int K, int KH,
                            int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk, int splits, int variant,
-                           int accumulate, float* slab, unsigned* counters, hipStream_t s) {
+                           int accumulate, float* slab, unsigned* counters, float* dbias, int bias_acc,
+                           hipStream_t s) {
   ConvArgs a;
   const int e = prep_wgrad(a, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, accumulate,
-                           slab, counters);
+                           slab, counters, dbias, bias_acc);
   if (e) return e;
   if (variant) bk = 64;
   return dispatch<WGRAD>(a, bm, bn, bk, variant, s);

@@ -201,11 +201,15 @@ __global__ __launch_bounds__(256) void k_ce_bwd(const T* __restrict__ logits, co
 }
 
 // k_ce_bwd (bf16 vector path) that also produces the column sums of dlogits — the bias
-// gradient of the Linear that produced the logits (its own column-sum pass is skipped).  The
-// block's 4 rows are summed through LDS ([4][ld] fp32, ld <= 4096) into one partial row
-// part[block][C] (plain stores); the last block to arrive (agent-scope ticket) sums the rows
-// in block order and stores (acc = 0) or adds (acc = 1) them into dbias: deterministic, one
-// writer per element, no zeroed buffer needed.
+// gradient of the Linear that produced the logits (its own column-sum pass is skipped).  A
+// block owns CE_BIAS_ROWS rows: each wave sums its 4 rows (in row order) into its own LDS row
+// ([4][ld] fp32, ld <= 4096), the 4 wave rows are combined into one partial row
+// part[block][CP] (write-through stores); the last block to arrive (agent-scope ticket) sums
+// the G = ceil(B / 16) partial rows in block order — one thread per float4 column, all G loads
+// in flight at once — and stores (acc = 0) or adds (acc = 1) them into dbias: deterministic,
+// one writer per element, no zeroed buffer needed.
+constexpr int CE_BIAS_ROWS = 16;
+
 __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ logits,
                                                      const long long* __restrict__ labels,
                                                      const float* __restrict__ lse, const float* __restrict__ red,
@@ -213,38 +217,42 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
                                                      float* __restrict__ dbias, int B, int C, int ld,
                                                      long long ignore, float* __restrict__ part,
                                                      unsigned* __restrict__ ticket, int acc) {
-  extern __shared__ float colsh[];  // [4][ld], reused as [4][64] float4 by the last block
+  extern __shared__ float colsh[];  // [4][ld]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int row = blockIdx.x * 4 + w;
-  const bool have = row < B;
-  const long long y = have ? labels[row] : -1;
-  const bool skip = !have || (y == ignore || y < 0 || y >= C);
   const float valid = red[2];
   const float g = (grad_out ? *grad_out : 1.f) / fmaxf(valid, 1.f);
-  const float l = have ? lse[row] : 0.f;
-  const float l2 = l * LOG2E_CE;
-  const uint4* x8 = reinterpret_cast<const uint4*>(logits + (long long)(have ? row : 0) * ld);
-  uint4* d8 = reinterpret_cast<uint4*>(dlogits + (long long)(have ? row : 0) * ld);
   float* mine = colsh + w * ld;
-  for (int c8 = lane; c8 < ld / 8; c8 += 64) {
-    float f[8];
-    unpack8f(x8[c8], f);
-    unsigned o[4];
+  for (int r = 0; r < CE_BIAS_ROWS / 4; ++r) {
+    const int row = blockIdx.x * CE_BIAS_ROWS + w * (CE_BIAS_ROWS / 4) + r;
+    const bool have = row < B;
+    const long long y = have ? labels[row] : -1;
+    const bool skip = !have || (y == ignore || y < 0 || y >= C);
+    const float l = have ? lse[row] : 0.f;
+    const float l2 = l * LOG2E_CE;
+    const uint4* x8 = reinterpret_cast<const uint4*>(logits + (long long)(have ? row : 0) * ld);
+    uint4* d8 = reinterpret_cast<uint4*>(dlogits + (long long)(have ? row : 0) * ld);
+    for (int c8 = lane; c8 < ld / 8; c8 += 64) {
+      float f[8];
+      unpack8f(x8[c8], f);
+      unsigned o[4];
 #pragma unroll
-    for (int k = 0; k < 8; k += 2) {
-      const int c = c8 * 8 + k;
-      const float a = (skip || c >= C) ? 0.f
-                      : (__builtin_amdgcn_exp2f(fmaf(f[k], LOG2E_CE, -l2)) - (c == y ? 1.f : 0.f)) * g;
-      const float b = (skip || c + 1 >= C) ? 0.f
-                      : (__builtin_amdgcn_exp2f(fmaf(f[k + 1], LOG2E_CE, -l2)) - (c + 1 == y ? 1.f : 0.f)) * g;
-      o[k / 2] = pack_bf2(a, b);
-      mine[c] = lo_bf(o[k / 2]);          // the bf16 gradient the Linear would column-sum
-      mine[c + 1] = hi_bf(o[k / 2]);
+      for (int k = 0; k < 8; k += 2) {
+        const int c = c8 * 8 + k;
+        const float a = (skip || c >= C) ? 0.f
+                        : (__builtin_amdgcn_exp2f(fmaf(f[k], LOG2E_CE, -l2)) - (c == y ? 1.f : 0.f)) * g;
+        const float b = (skip || c + 1 >= C) ? 0.f
+                        : (__builtin_amdgcn_exp2f(fmaf(f[k + 1], LOG2E_CE, -l2)) - (c + 1 == y ? 1.f : 0.f)) * g;
+        o[k / 2] = pack_bf2(a, b);
+        // the bf16 gradient the Linear would column-sum; each lane owns its columns, so the
+        // running sum over the wave's rows needs no barrier
+        mine[c] = r ? mine[c] + lo_bf(o[k / 2]) : lo_bf(o[k / 2]);
+        mine[c + 1] = r ? mine[c + 1] + hi_bf(o[k / 2]) : hi_bf(o[k / 2]);
+      }
+      if (have) d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    if (have) d8[c8] = make_uint4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
-  // partial row [C] of this block, published write-through (sc1): no release fence
+  // partial row of this block, published write-through (sc1): no release fence
   // (CDNA guide §6 G16 R1); the row is padded to CP (multiple of 4) for 16-byte access
   const int CP = (C + 3) & ~3;
   float* mine_row = part + (long long)blockIdx.x * CP;
@@ -266,47 +274,26 @@ __global__ __launch_bounds__(256) void k_ce_bwd_bias(const bf16_t* __restrict__ 
   }
   __syncthreads();
   if (!last) return;
-  // last block: column sums of the G rows in a fixed order.  Thread = (row slice s of 4,
-  // float4 column j): 16 independent 16-byte loads in flight per batch, the 4 slices combined
-  // through LDS in slice order — bitwise reproducible.
+  // last block: column sums of the G partial rows in block order, 16 loads per batch
   const int G = (int)gridDim.x;
   const int C4 = CP / 4;
-  const int s = threadIdx.x >> 6, jl = threadIdx.x & 63;
-  float4* red4 = reinterpret_cast<float4*>(colsh);  // reuse: [4][64] float4
-  for (int j0 = 0; j0 < C4; j0 += 64) {
-    const int j = j0 + jl;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (j < C4) {
-      const float4* col = reinterpret_cast<const float4*>(part) + j;
-      int g = s;
-      for (; g + 12 < G; g += 16) {
-        const float4 v0 = col[(long long)g * C4], v1 = col[(long long)(g + 4) * C4];
-        const float4 v2 = col[(long long)(g + 8) * C4], v3 = col[(long long)(g + 12) * C4];
-        a.x += (v0.x + v1.x) + (v2.x + v3.x);
-        a.y += (v0.y + v1.y) + (v2.y + v3.y);
-        a.z += (v0.z + v1.z) + (v2.z + v3.z);
-        a.w += (v0.w + v1.w) + (v2.w + v3.w);
-      }
-      for (; g < G; g += 4) {
-        const float4 v = col[(long long)g * C4];
-        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  for (int j = threadIdx.x; j < C4; j += 256) {
+    const float4* col = reinterpret_cast<const float4*>(part) + j;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g0 = 0; g0 < G; g0 += 16) {
+      float4 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = g0 + k < G ? col[(long long)(g0 + k) * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        t.x += v[k].x; t.y += v[k].y; t.z += v[k].z; t.w += v[k].w;
       }
     }
-    __syncthreads();
-    red4[s * 64 + jl] = a;
-    __syncthreads();
-    if (s == 0 && j < C4) {
-      float4 t = red4[jl];
-      for (int k = 1; k < 4; ++k) {
-        const float4 v = red4[k * 64 + jl];
-        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-      }
-      const float tv[4] = {t.x, t.y, t.z, t.w};
+    const float tv[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = 4 * j + e;
-        if (c < C) dbias[c] = acc ? dbias[c] + tv[e] : tv[e];
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * j + e;
+      if (c < C) dbias[c] = acc ? dbias[c] + tv[e] : tv[e];
     }
   }
 }
@@ -332,7 +319,7 @@ KML_API int kml_ce_fwd(const void* logits, const long long* labels, float* ws, f
 }
 
 // dbias (optional; bf16 logits, ld % 8 == 0, ld <= 4096): column sums of dlogits, stored
-// (accumulate = 0) or added (1); needs part = [ceil(B/4)][roundup(C, 4)] fp32 scratch and a
+// (accumulate = 0) or added (1); needs part = [ceil(B/16)][roundup(C, 4)] fp32 scratch and a
 // zeroed ticket
 KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float* ws, const float* out3,
                        const float* grad_out, void* dlogits, int B, int C, int ld, long long ignore, int dtype,
@@ -341,8 +328,8 @@ KML_API int kml_ce_bwd(const void* logits, const long long* labels, const float*
   dim3 g((B + 3) / 4);
   if (dbias) {
     if (dtype != 0 || ld % 8 || ld > 4096 || !part || !ticket) return (int)hipErrorInvalidValue;
-    const size_t shm = (size_t)(4 * ld > 1024 ? 4 * ld : 1024) * sizeof(float);  // rows, then [4][64] float4
-    hipLaunchKernelGGL(k_ce_bwd_bias, g, dim3(256), shm, s, (const bf16_t*)logits, labels,
+    const size_t shm = (size_t)4 * ld * sizeof(float);
+    hipLaunchKernelGGL(k_ce_bwd_bias, dim3((B + CE_BIAS_ROWS - 1) / CE_BIAS_ROWS), dim3(256), shm, s, (const bf16_t*)logits, labels,
                        ws, out3, grad_out, (bf16_t*)dlogits, dbias, B, C, ld, ignore, part, ticket, accumulate);
     KML_LAUNCH_CHECK();
   }

@@ -15,9 +15,13 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Sequence
 
+import logging
+
 import torch
 
 from .step import GraphedTrainStep, train_state_tensors
+
+_log = logging.getLogger("kubeml.dp")
 
 
 def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable, x: torch.Tensor,
@@ -60,9 +64,11 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         overlap = plan.schedule == "overlap"
         comm_dtype = plan.wire_dtype
         if plan.backend == "peer" and comm and peer is None and torch.cuda.is_available() and space.grad.is_cuda:
-            from ..parallel.peer import PeerAllReduce, slot_bytes
-            peer = PeerAllReduce(group, cap_bytes=slot_bytes(space.grad.numel(), world, "twoshot", comm_dtype),
-                                 device=space.grad.device)
+            from ..parallel.peer import slot_bytes, verified_peer
+            # collective; None (on every rank) when the node cannot map peers or the self-test
+            # fails — the step then runs the same schedule over RCCL
+            peer = verified_peer(group, cap_bytes=slot_bytes(space.grad.numel(), world, "twoshot", comm_dtype),
+                                 device=space.grad.device, log=_log.warning)
         if plan.backend != "peer":
             peer = None
     if comm_dtype is None:

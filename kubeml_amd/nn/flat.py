@@ -132,6 +132,7 @@ class FlatParamSpace:
         self._fresh: set = set()         # overwriters not yet written since zero_grad()
         self._zeroed_once = False
         self._folds: list = []           # (param, 1x1-form scratch, grad region, accumulate) to fold
+        self._fold_cb = False            # an end-of-backward fold callback is queued
 
     def _bind_i64(self):
         """All int64 buffers as consecutive elements of one arena (one pointer for the
@@ -243,6 +244,23 @@ class FlatParamSpace:
         onto p's 3x3 taps at :meth:`finish_grads` (one launch for all of a stage's convs)."""
         dw, acc = grad_out(p)
         self._folds.append((p, g, dw, acc))
+        if not self._fold_cb:
+            # the folds also run when this backward pass ends, so .grad is final for any
+            # reader (eager loops, tests); a later explicit finish_grads finds nothing left
+            self._fold_cb = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+
+    def _end_of_backward(self):
+        self._fold_cb = False
+        if self._folds:
+            self._run_folds(self._folds)
+            self._folds = []
+
+    def _run_folds(self, run):
+        from ..ops import kernels as K
+        from .fused import join_wgrad
+        join_wgrad()          # side-stream wgrads (KUBEML_WGRAD_SIDE) wrote the scratch
+        K.fold22_multi([(g, dw, acc) for _, g, dw, acc in run])
 
     def finish_grads(self, params=None):
         """Make the gradients of ``params`` (all if None) final before they are consumed:
@@ -253,10 +271,7 @@ class FlatParamSpace:
             run = [f for f in self._folds if ids is None or id(f[0]) in ids]
             if run:
                 self._folds = [f for f in self._folds if not (ids is None or id(f[0]) in ids)]
-                from ..ops import kernels as K
-                from .fused import join_wgrad
-                join_wgrad()          # side-stream wgrads (KUBEML_WGRAD_SIDE) wrote the scratch
-                K.fold22_multi([(g, dw, acc) for _, g, dw, acc in run])
+                self._run_folds(run)
         if not self._fresh:
             return
         if params is None:
@@ -268,7 +283,7 @@ class FlatParamSpace:
 
     def finish_grads_range(self, start: int, end: int):
         """finish_grads for the parameters whose regions lie in flat elements [start, end)."""
-        if self._fresh:
+        if self._fresh or self._folds:
             self.finish_grads([p for i, p in enumerate(self.params)
                                if start <= self.offsets[i][0] < end])
 

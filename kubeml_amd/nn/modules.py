@@ -174,6 +174,7 @@ class _LinearFn(Function):
         B = x2.shape[0]
         route = _linear_route(B, ip, op, act)
         ctx.route = route
+        object.__setattr__(mod, "_kml_route", route)
         pre = None
         if route == "gemm":
             from ..ops import gemm as G
@@ -223,6 +224,12 @@ class _LinearFn(Function):
         else:                            # gemm.hip / hipBLASLt wgrad: adds
             dwst, wacc = grad_storage_of(mod.weight), True
         dw4 = dwst.view(op, 1, 1, ip)
+        # implicit-GEMM route: the bias gradient is one more column of the wgrad GEMM (a ones
+        # column in its input operand) — no column-sum pass
+        dbias, bacc = None, True
+        if ctx.route == "conv" and ctx.has_bias and not bias_done and not getattr(mod, "_kml_bias_done", False):
+            dbias, bacc = grad_out(mod.bias)
+            bias_done = True
         dx = None
         # residual gradient handed over by a LayerNorm that shares this Linear's input
         # (nn/transformer.py): summed into dx here instead of by an autograd add
@@ -247,9 +254,10 @@ class _LinearFn(Function):
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
-            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc).view(B, ip)
+            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc, dbias=dbias,
+                            bias_accumulate=bacc).view(B, ip)
         else:
-            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc)
+            K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc, dbias=dbias, bias_accumulate=bacc)
         if ctx.has_bias and not bias_done:
             if getattr(mod, "_kml_bias_done", False):
                 object.__setattr__(mod, "_kml_bias_done", False)   # summed by the consumer LayerNorm
@@ -510,9 +518,12 @@ class _CEFn(Function):
         from ..ops import kernels as K
         logits, lab, ws, out3, ig, classes = ctx.save
         # the logits came straight out of a Linear: its bias gradient (the column sums of
-        # dlogits) is added by the CE backward pass itself, and the Linear skips its own
+        # dlogits) is added by the CE backward pass itself, and the Linear skips its own —
+        # unless the Linear runs on the implicit-GEMM route, whose wgrad GEMM produces the bias
+        # gradient as one extra column for free
         lin, dbias, acc = ctx.lin, None, True
         if (lin is not None and getattr(lin, "bias", None) is not None and _CE_BIAS_FUSE
+                and getattr(lin, "_kml_route", None) != "conv"
                 and lin.out_pad == logits.shape[1] and K.ce_bias_fusable(logits)):
             dbias, acc = grad_out(lin.bias)
             object.__setattr__(lin, "_kml_bias_done", True)

@@ -516,7 +516,7 @@ def conv_pair_supported(dcfg, wcfg) -> bool:
 
 
 def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None,
-             bnf_mask=False, accumulate=True):
+             bnf_mask=False, accumulate=True, dbias=None, bias_accumulate=True):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
     :func:`conv_dgrad`) and ``dw += wgrad`` (``accumulate=False``: ``dw = wgrad``).  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
@@ -525,7 +525,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     Returns dx, or (dx, (part, G)) when ``bnf`` is given.  wu: unrolled weight
     (:func:`unrolled22`): both GEMMs run in the dense 1x1 form; ``dw`` is then the
     ``[4K,1,1,4C]`` fp32 scratch of the 1x1-form weight gradient (stored), which
-    :func:`fold22_multi` folds onto the 3x3 taps.  bnf_mask: as in :func:`conv_dgrad`."""
+    :func:`fold22_multi` folds onto the 3x3 taps.  bnf_mask: as in :func:`conv_dgrad`.
+    dbias: as in :func:`conv_wgrad` (1x1/s1/p0 convs)."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -554,8 +555,11 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
+    if dbias is not None and wu is not None:
+        raise ValueError("conv_bwd: dbias needs a 1x1 conv")
     if not grouped:
-        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, accumulate=accumulate)
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, accumulate=accumulate, dbias=dbias,
+                   bias_accumulate=bias_accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
                        bnf_mask=bnf_mask)
         if not fold:
@@ -578,13 +582,15 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         dsplits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, dsplits)
     wbm, wbn, wbk, wsplits, wvariant = wplan
-    wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan)
+    _chk_dbias(dbias, K, KH, KW, stride, pad)
+    wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan, dbias is not None)
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
              _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
-             int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _s())
+             int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _p(dbias),
+             int(bool(bias_accumulate)), _s())
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out
@@ -614,26 +620,41 @@ def weight_transpose_multi(ws, wts):
              ctypes.addressof(dims), n, _s())
 
 
-def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg):
-    """Split-K slab + tickets of a weight-gradient GEMM (None, None without split-K)."""
+def _wgrad_ws(device, B, H, W, C, K, KH, KW, stride, pad, cfg, bias_col=False):
+    """Split-K slab + tickets of a weight-gradient GEMM (None, None without split-K);
+    bias_col: the GEMM carries the extra ones column of a fused bias gradient."""
     bm, bn, bk, splits, variant = cfg
     if variant:
         bk = 64
     OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
-    return _splitk_ws(device, K, (r1 - r0) * (s1 - s0) * C, bm, bn, effective_splits(B * OH * OW, bk, splits))
+    return _splitk_ws(device, K, (r1 - r0) * (s1 - s0) * C + int(bias_col), bm, bn,
+                      effective_splits(B * OH * OW, bk, splits))
 
 
-def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulate=True):
+def _chk_dbias(dbias, K, KH, KW, stride, pad):
+    if dbias is None:
+        return
+    _chk(dbias, F32, "dbias")
+    if dbias.numel() < K or (KH, KW) != (1, 1) or tuple(stride) != (1, 1) or tuple(pad) != (0, 0):
+        raise ValueError("fused bias gradient: 1x1/s1/p0 conv and a [Cout] fp32 dbias")
+
+
+def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulate=True, dbias=None,
+               bias_accumulate=True):
     """Conv weight gradient into dw[Cout,KH,KW,Cin] (fp32): ``dw += wgrad`` (accumulate) or
     ``dw = wgrad`` (overwrite: the buffer need not be zeroed).  Deterministic: one writer per
     element, split-K partials summed in split order.  unroll: an unrolled conv
     (:func:`unrolled22`): ``dw`` is then the ``[4K,1,1,4C]`` fp32 scratch of its dense 1x1-form
-    gradient, stored; :func:`fold22_multi` folds it onto the 3x3 taps."""
+    gradient, stored; :func:`fold22_multi` folds it onto the 3x3 taps.  dbias (1x1/s1/p0 convs,
+    i.e. a Linear): the bias gradient sum over pixels of dy, from the same GEMM (an extra
+    ones column of the input operand), stored or added per ``bias_accumulate``."""
     _chk(x, BF16, "x", 4)
     _chk(dy, BF16, "dy", 4)
     _chk(dw, F32, "dw", 4)
     if unroll:
+        if dbias is not None:
+            raise ValueError("conv_wgrad: dbias needs a 1x1 conv")
         B, H, W, C = x.shape
         K = dy.shape[3]
         if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (4 * K, 1, 1, 4 * C):
@@ -650,10 +671,11 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulat
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
     bm, bn, bk, splits, variant = cfg
-    slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg)
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i p p s",
+    _chk_dbias(dbias, K, KH, KW, stride, pad)
+    slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg, dbias is not None)
+    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i p p p i s",
              _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant,
-             int(bool(accumulate)), _p(slab), _p(cnt), _s())
+             int(bool(accumulate)), _p(slab), _p(cnt), _p(dbias), int(bool(bias_accumulate)), _s())
     return dw
 
 
@@ -946,7 +968,7 @@ def ce_bwd(logits, labels, ws, out3, grad_out=None, ignore_index=-100, classes=N
             raise ValueError("ce_bwd: bias fusion needs bf16 logits with ld % 8 == 0, ld <= 4096")
     part = cnt = None
     if dbias is not None:
-        part = torch.empty(_cdiv(B, 4) * _cdiv(C, 4) * 4, dtype=F32, device=logits.device)
+        part = torch.empty(_cdiv(B, 16) * _cdiv(C, 4) * 4, dtype=F32, device=logits.device)
         cnt = _COUNTERS.take(logits.device, 1)
     HIP.call("kml_ce_bwd", "p p p p p p i i i l i p p p i s", _p(logits), _p(labels), _p(ws), _p(out3), _p(grad_out),
              _p(d), B, C, ld, int(ignore_index), dt, _p(dbias), _p(part), _p(cnt), int(bool(accumulate)), _s())

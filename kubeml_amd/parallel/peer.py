@@ -86,19 +86,26 @@ class PeerAllReduce:
             handles: List[bytes] = [b""] * self.world
             dist.all_gather_object(handles, bytes(h), group=group)
             self.opened: List[int] = []
-            ptrs = []
-            for p, hb in enumerate(handles):
-                if p == self.rank:
-                    ptrs.append(self.region)
-                    continue
-                buf = (ctypes.c_char * nb).from_buffer_copy(hb)
-                out = ctypes.c_void_p()
-                HIP.call("kml_ipc_open", "p p", ctypes.addressof(buf), ctypes.addressof(out))
-                self.opened.append(out.value)
-                ptrs.append(out.value)
-            self._regions = (ctypes.c_void_p * self.world)(*ptrs)
-            torch.cuda.synchronize(self.device)
-        dist.barrier(group=group)   # every rank has mapped every region before the first call
+            ptrs, err = [], ""
+            try:
+                for p, hb in enumerate(handles):
+                    if p == self.rank:
+                        ptrs.append(self.region)
+                        continue
+                    buf = (ctypes.c_char * nb).from_buffer_copy(hb)
+                    out = ctypes.c_void_p()
+                    HIP.call("kml_ipc_open", "p p", ctypes.addressof(buf), ctypes.addressof(out))
+                    self.opened.append(out.value)
+                    ptrs.append(out.value)
+                torch.cuda.synchronize(self.device)
+            except Exception as e:   # a rank that cannot map a peer must not leave the others waiting
+                err = f"rank {self.rank}: {e!r}"[:300]
+            self._regions = (ctypes.c_void_p * self.world)(*(ptrs + [0] * (self.world - len(ptrs))))
+        errs: List[str] = [""] * self.world
+        dist.all_gather_object(errs, err, group=group)   # every rank has mapped every region (or not)
+        if any(errs):
+            self._release()
+            raise PeerCommError("peer all-reduce setup failed: " + "; ".join(e for e in errs if e))
 
     # ------------------------------------------------------------------ calls
     def pick_algo(self, t: torch.Tensor) -> str:
@@ -145,6 +152,45 @@ class PeerAllReduce:
             raise PeerCommError(f"peer all-reduce: {n} barrier wait(s) on rank {self.rank}/{self.world} timed out "
                                 f"after {self.timeout_s:g} s (a peer stopped calling); results since then are NaN")
 
+    def self_test(self, n: Optional[int] = None) -> bool:
+        """Collective: run both algorithms and both wires on rank-dependent integer patterns
+        (exact in bf16 and fp32) and compare with the closed-form sums.  True on every rank
+        only if every rank got exact results and no wait timed out."""
+        ok = True
+        try:
+            big = min(n or 4 << 20, self.cap // 4 - 64)
+            for numel, algo in ((4099, "oneshot"), (big, "twoshot")):
+                if numel < self.world * 8:
+                    continue
+                idx = torch.arange(numel, device=self.device)
+                base = (idx % 8).float()
+                want = base * float(self.world * (self.world + 1) // 2)
+                for wire in (torch.float32, torch.bfloat16):
+                    if not self.supports(base, algo, wire):
+                        continue
+                    for _ in range(3):          # both slot parities, then one more
+                        t = base * float(self.rank + 1)
+                        self.all_reduce_(t, 1.0, algo=algo, wire=wire)
+                        ok = ok and bool(torch.equal(t, want))
+            torch.cuda.synchronize(self.device)
+            ok = ok and self.errors() == 0
+        except Exception:
+            ok = False
+        flags: List[bool] = [False] * self.world
+        self.dist.all_gather_object(flags, ok, group=self.group)
+        return all(flags)
+
+    def _release(self):
+        for p in self.opened:
+            try:
+                HIP.call("kml_ipc_close", "p", p)
+            except Exception:
+                pass
+        self.opened = []
+        if self.region is not None:
+            HIP.call("kml_peer_free", "p p", self.region, self.ctrl)
+        self.region = self.ctrl = None
+
     def close(self):
         """Collective: unmap the peers' regions after everyone is done, then free our own."""
         if self.region is None:
@@ -157,6 +203,28 @@ class PeerAllReduce:
         self.dist.barrier(group=self.group)
         HIP.call("kml_peer_free", "p p", self.region, self.ctrl)
         self.region = self.ctrl = None
+
+
+def verified_peer(group=None, cap_bytes: int = DEFAULT_CAP, device: Optional[torch.device] = None,
+                  log=None) -> Optional["PeerAllReduce"]:
+    """Collective: a :class:`PeerAllReduce` that passed :meth:`PeerAllReduce.self_test` on every
+    rank, or None (every rank agrees) — callers then keep RCCL.  ``KUBEML_PEER_SELFTEST=0``
+    skips the test."""
+    try:
+        p = PeerAllReduce(group, cap_bytes=cap_bytes, device=device)
+    except PeerCommError as e:
+        if log:
+            log(f"peer all-reduce unavailable, using RCCL: {e}")
+        return None
+    if os.environ.get("KUBEML_PEER_SELFTEST", "1") == "0" or p.self_test():
+        return p
+    if log:
+        log("peer all-reduce failed its self-test on this node, using RCCL")
+    try:
+        p.close()
+    except Exception:
+        pass
+    return None
 
 
 def stream_copy(src: torch.Tensor, dst: torch.Tensor, nbytes: int, blocks: int, passes: int = 1):

@@ -114,6 +114,30 @@ def test_train_validate_history_infer(env):
     assert jid in [x.id for x in c.histories.list()]
 
 
+def test_allreduce_seconds_exported_while_a_two_worker_job_runs(env):
+    """K-AVG rounds of a 2-worker job are timed on the workers (sync_seconds per epoch) and
+    the PS exports them as kubeml_allreduce_seconds{jobid} while the job runs."""
+    import re
+    from kubeml_amd.control.http import call
+    srv, c, _ = env
+    req = TrainRequest(batch_size=32, epochs=6, dataset="mnist", lr=0.05, function_name="lenet",
+                       options=TrainOptions(default_parallelism=2, static_parallelism=True, validate_every=0, k=2,
+                                            goal_accuracy=100))
+    jid = c.networks.train(req)
+    pat = re.compile(r'kubeml_allreduce_seconds\{jobid="%s"\} ([0-9.e+-]+)' % jid)
+    seen, t0 = [], time.time()
+    while c.tasks.status(jid)["state"] == "running" and time.time() - t0 < 300:
+        m = call("GET", srv.url("metrics") + "/metrics")
+        m = m.decode() if isinstance(m, bytes) else str(m)
+        seen += [float(v) for v in pat.findall(m)]
+        time.sleep(0.02)
+    assert c.tasks.status(jid)["state"] == "finished"
+    ep = [json.loads(l) for l in c.logs(jid).decode().splitlines()
+          if l.startswith("{") and '"epoch finished"' in l]
+    assert ep and all(float(e.get("sync_seconds") or 0) > 0 for e in ep), ep
+    assert any(v > 0 for v in seen), seen
+
+
 def test_job_rest_surface_through_ps(env):
     """The TrainJob's own routes (reference ml/pkg/train/api.go) are served via the PS:
     /job/{id}/status while the job runs, 404 for an unknown job."""

@@ -755,7 +755,7 @@ def test_bn_relu_maxpool_matches_unfused(B, H, C):
     assert agree.float().mean() > 0.995
 
 
-@pytest.mark.parametrize("B,C,ld", [(256, 1000, 1000), (37, 10, 16), (130, 1000, 1008)])
+@pytest.mark.parametrize("B,C,ld", [(256, 1000, 1000), (37, 10, 16), (130, 1000, 1008), (600, 1000, 1000)])
 def test_ce_bwd_adds_bias_gradient(B, C, ld):
     """ce_bwd(dbias=...): same dlogits, and dbias += column sums of dlogits (the logits
     Linear's bias gradient, which that Linear then skips)."""
@@ -779,3 +779,31 @@ def test_ce_bwd_adds_bias_gradient(B, C, ld):
     db3 = torch.empty_like(db2)
     K.ce_bwd(logits, lab, ws, out3, classes=C, dbias=db3, accumulate=False)
     assert torch.equal(db2[:C], db3[:C])
+
+
+@pytest.mark.parametrize("B,C,K,grouped", [(256, 512, 1000, True), (256, 512, 1000, False), (96, 64, 24, True)])
+def test_wgrad_ones_column_bias_gradient(B, C, K, grouped):
+    """conv_wgrad / conv_bwd(dbias=...) of a Linear (1x1 conv on a 1x1 map): the bias
+    gradient comes out of the wgrad GEMM's extra ones column; dW is unchanged by it."""
+    from kubeml_amd.ops import kernels as K_
+    torch.manual_seed(11)
+    x = _bf(torch.randn(B, 1, 1, C, device=dev))
+    dy = _bf(torch.randn(B, 1, 1, K, device=dev))
+    w = _bf(torch.randn(K, 1, 1, C, device=dev) * 0.05)
+    want_db = dy.float().reshape(B, K).sum(0)
+    want_dw = (dy.float().reshape(B, K).t() @ x.float().reshape(B, C)).reshape(K, 1, 1, C)
+    dw = torch.full((K, 1, 1, C), float("nan"), device=dev)
+    db = torch.full((K,), float("nan"), device=dev)
+    if grouped:
+        dx = K_.conv_bwd(dy, w, x, dw, 1, 1, (1, 1), (0, 0), accumulate=False, dbias=db, bias_accumulate=False)
+        torch.testing.assert_close(dx.float().reshape(B, C), dy.float().reshape(B, K) @ w.float().reshape(K, C),
+                                   rtol=2e-2, atol=2e-2)
+    else:
+        K_.conv_wgrad(x, dy, dw, 1, 1, (1, 1), (0, 0), accumulate=False, dbias=db, bias_accumulate=False)
+    torch.testing.assert_close(db, want_db, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(dw, want_dw, rtol=1e-5, atol=1e-4)
+    # accumulate mode adds
+    db2 = torch.full((K,), 0.5, device=dev)
+    dw2 = torch.zeros_like(dw)
+    K_.conv_wgrad(x, dy, dw2, 1, 1, (1, 1), (0, 0), accumulate=True, dbias=db2, bias_accumulate=True)
+    torch.testing.assert_close(db2, want_db + 0.5, rtol=1e-5, atol=1e-4)

@@ -162,8 +162,17 @@ def _run(rank, world, port, q, late):
         if not torch.allclose(t, _expect(world, 777, 900, dev, torch.float32, 1.0 / world), rtol=0, atol=1e-6):
             bad.append(("comm", 777))
         comm.check()
+        if not ar.self_test():
+            bad.append(("self_test",))
         errs = ar.errors()
         ar.close()
+        # the verified factory (what make_train_step uses) agrees on both ranks
+        from kubeml_amd.parallel.peer import verified_peer
+        vp = verified_peer(None, cap_bytes=64 << 20, device=dev)
+        if vp is None:
+            bad.append(("verified_peer", None))
+        else:
+            vp.close()
         q.put((rank, bad, errs, None))
     except Exception as e:  # report instead of hanging the parent
         import traceback

@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "interference.json"))
     ap.add_argument("--plan-out", default=None)
     ap.add_argument("--skip-plans", action="store_true")
+    ap.add_argument("--wires", default="fp32",
+                    help="wire dtypes the plan choice may use (fp32 keeps the gradient sums fp32 end to end; "
+                         "'fp32,bf16' also ranks the bf16 wire)")
     a = ap.parse_args()
 
     import torch
@@ -237,6 +240,9 @@ def main():
                 bf = min(f32, key=f32.get)
                 if cands[bf] <= cands[best] * 1.03:
                     best = bf
+            allowed = {k: v for k, v in cands.items() if k.split(":")[2] in a.wires.split(",")}
+            if allowed and best not in allowed:
+                best = min(allowed, key=allowed.get)
             choice[str(N)] = best
             pred[str(N)] = {k: round(v, 4) for k, v in sorted(cands.items(), key=lambda kv: kv[1])}
     rows["predicted_ms"] = pred
@@ -247,7 +253,8 @@ def main():
     if a.plan_out:
         with open(a.plan_out, "w") as f:
             json.dump({"choice": choice, "predicted_ms": pred, "base_ms": rows["base_ms"],
-                       "link_gbs_assumed": a.link_gbs, "source": "tools/interference_probe.py"}, f, indent=1)
+                       "link_gbs_assumed": a.link_gbs, "wires_allowed": a.wires,
+                       "source": "tools/interference_probe.py"}, f, indent=1)
     log(choice=choice)
     dist.destroy_process_group()
 
