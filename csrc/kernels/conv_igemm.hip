@@ -117,6 +117,11 @@ struct ConvArgs {
   // rows of [sum(fold_c) | sumsq(fold_c)] (BN kernels see ordinary rows of the real
   // channels).  The WGRAD of an unrolled conv runs in the plain 3x3 form (prep_wgrad).
   int fold_c;
+  // g22: an unrolled conv whose 1x1-form weight W'[(p, n)][(q, c)] = w[n][tap(p, q)][c] is
+  // gathered by the FWD / DGRAD weight loaders straight from the 3x3 weight w (no unrolled
+  // copy per step): K = 4 Kq, C = 4 Cq in the 1x1 form, fd_gK / fd_gC divide by Kq / Cq.
+  int g22;
+  FastDiv fd_gK, fd_gC;
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
@@ -192,17 +197,31 @@ struct FwdA {  // im2col(X): LDS row = output pixel, K-contiguous over cin
   }
 };
 
+// 3x3 tap of the unrolled pair (output position p, input position q) on a 2x2 map
+__device__ __forceinline__ int tap22(int p, int q) { return ((q >> 1) - (p >> 1) + 1) * 3 + ((q & 1) - (p & 1) + 1); }
+
 template <int BK, bool TAPU>
 struct FwdB {  // W[n][tap][cin], K-contiguous
-  int base, koff;
+  int base, koff, p22;
   bool valid;
   __device__ void init(const ConvArgs& a, int n, int q) {
     valid = n < a.N;
-    base = (valid ? n : 0) * a.KH * a.KW * a.C;
+    const int nn = valid ? n : 0;
+    if (a.g22) {  // row n = (p, n') of the unrolled weight
+      p22 = fdiv(nn, a.fd_gK);
+      base = (nn - p22 * a.fd_gK.d) * 9 * a.fd_gC.d;
+    } else {
+      p22 = 0;
+      base = nn * a.KH * a.KW * a.C;
+    }
     koff = (q % (BK / 8)) * 8;
   }
   __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
     const int k = kb + koff;
+    if (a.g22) {  // column k = (q, c): w[n'][tap(p, q)][c]
+      const int q = fdiv(k, a.fd_gC), c = k - q * a.fd_gC.d;
+      return (valid && k < kend) ? a.w + base + tap22(p22, q) * a.fd_gC.d + c : a.zp;
+    }
     const int tap = TAPU ? fdiv(kb, a.fd_C) : fdiv(k, a.fd_C);
     const int c = k - tap * a.C;
     int r, s;
@@ -239,17 +258,30 @@ struct DgradA {  // dY gathered for input pixel m; K = (tap, cout); Kp % BK == 0
 
 template <int BK, int BN>
 struct DgradB {  // LDS row = k = (tap, cout), cols = cin; chunk = W[cout][tap][c..c+7]
-  int krow, c;
+  int krow, c, q22, c22;
   bool valid;
   __device__ void init(const ConvArgs& a, int n0, int q) {
     constexpr int CPR = BN / 8;
     krow = q / CPR;
     c = n0 + (q % CPR) * 8;
     valid = c < a.N;
+    if (a.g22) {  // column c = (q, c') of the unrolled weight
+      const int cc = valid ? c : 0;
+      q22 = fdiv(cc, a.fd_gC);
+      c22 = cc - q22 * a.fd_gC.d;
+    } else {
+      q22 = c22 = 0;
+    }
   }
   __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
     const int tap = fdiv(kb, a.fd_Kp);  // uniform
     const int n = kb - tap * a.Kp + krow;
+    if (a.g22) {  // 1x1 form (tap 0), row n = (p, n'): w[n'][tap(p, q)][c']
+      const bool ok = valid && kb + krow < kend && n < a.K;
+      const int nn = ok ? n : 0;
+      const int p = fdiv(nn, a.fd_gK);
+      return ok ? a.w + ((long long)(nn - p * a.fd_gK.d) * 9 + tap22(p, q22)) * a.fd_gC.d + c22 : a.zp;
+    }
     int r, s;
     tap_rs(a, tap, r, s);
     const bool ok = valid && kb + krow < kend && n < a.K;
@@ -1413,6 +1445,16 @@ const bf16_t* one_page() {
 
 }  // namespace
 
+namespace {
+// g22 needs the 1x1 form of an unrolled 3x3 conv: Cq = C / 4 a multiple of 8 (a 16-byte chunk
+// never straddles two input positions), Kq = K / 4
+bool g22_ok(int C, int K, int KH, int KW) { return KH == 1 && KW == 1 && C % 32 == 0 && K % 4 == 0; }
+void set_g22(ConvArgs& a, int g22, int C, int K) {
+  a.g22 = g22 ? 1 : 0;
+  if (a.g22) { a.fd_gK = make_fd(K / 4); a.fd_gC = make_fd(C / 4); }
+}
+}  // namespace
+
 KML_API int kml_conv_tap_window(int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
                                 int* out4) {
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
@@ -1432,8 +1474,9 @@ KML_API int kml_conv_effective_splits(int Kd, int bk, int splits) {
 KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* stats, int stats_part,
                          int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int relu,
                          int bm, int bn, int bk, int splits, int variant, float* slab, unsigned* counters,
-                         float* grp_out, unsigned* grp_cnt, int grp_tiles, int fold_c, hipStream_t s) {
+                         float* grp_out, unsigned* grp_cnt, int grp_tiles, int fold_c, int g22, hipStream_t s) {
   if (grp_out && (!stats || !stats_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
+  if (g22 && !g22_ok(C, K, KH, KW)) return (int)hipErrorInvalidValue;
   if (fold_c && (grp_out || K % fold_c || (stats && !stats_part))) return (int)hipErrorInvalidValue;
   if (C % 8) return (int)hipErrorInvalidValue;
   if (variant == 3) {  // direct: bk carries the wave count; needs 32-aligned taps
@@ -1441,6 +1484,7 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
     a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
     a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
+    set_g22(a, g22, C, K);
     a.zp = zero_page();
     a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
     a.splits = 1; a.kchunk = a.Kd;
@@ -1451,6 +1495,7 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
   a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
   a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
+  set_g22(a, g22, C, K);
   a.zp = zero_page();
   a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
@@ -1465,8 +1510,9 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
                const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W, int C, int K,
                int KH, int KW, int sh, int sw, int ph, int pw, int bk, int splits, int variant, float* slab,
-               unsigned* counters, int fold_c, int bnf_mask_out) {
+               unsigned* counters, int fold_c, int bnf_mask_out, int g22) {
   if (C % 8 || K % 8) return (int)hipErrorInvalidValue;
+  if (g22 && (variant == 3 || !g22_ok(C, K, KH, KW))) return (int)hipErrorInvalidValue;
   if (grp_out && (!bnf_part || !grp_cnt || grp_tiles < 1)) return (int)hipErrorInvalidValue;
   if (bnf_mask_out && !bnf_part) return (int)hipErrorInvalidValue;
   if (fold_c && (grp_out || C % fold_c)) return (int)hipErrorInvalidValue;
@@ -1480,6 +1526,7 @@ int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt,
   a.bnf_y = bnf_y; a.bnf_c = bnf_c; a.bnf_mean = bnf_mean; a.bnf_rstd = bnf_rstd; a.bnf_part = bnf_part;
   a.bnf_mask_out = bnf_mask_out;
   a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
+  set_g22(a, g22, C, K);
   a.M = B * H * W; a.N = C; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * a.Kp;
   if (!a.zp) return (int)hipErrorInvalidSymbol;
   if (direct) {
@@ -1531,13 +1578,13 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
                               int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk, int wsplits,
                               int wvariant, int fold_c, int bnf_mask_out, float* wslab, unsigned* wcounters,
-                              int waccumulate, float* wbias, int wbias_acc, hipStream_t s) {
+                              int waccumulate, float* wbias, int wbias_acc, int g22, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
   int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
                      grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
-                     fold_c, bnf_mask_out);
+                     fold_c, bnf_mask_out, g22);
   if (e) return e;
   e = prep_wgrad(aw, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, wslab,
                  wcounters, wbias, wbias_acc);
@@ -1598,11 +1645,11 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
                            float* bnf_part, float* grp_out, unsigned* grp_cnt, int grp_tiles, int B, int H, int W,
                            int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn, int bk,
                            int splits, int variant, float* slab, unsigned* counters, int fold_c, int bnf_mask_out,
-                           hipStream_t s) {
+                           int g22, hipStream_t s) {
   ConvArgs a;
   const int e = prep_dgrad(a, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
                            grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, slab, counters,
-                           fold_c, bnf_mask_out);
+                           fold_c, bnf_mask_out, g22);
   if (e) return e;
   if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
   if (variant) bk = 64;

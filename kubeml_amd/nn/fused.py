@@ -143,6 +143,11 @@ def unrolled_for(conv, x):
     if not K.unrolled22(x.shape[1], x.shape[2], kh, kw, conv.stride, conv.padding):
         return None
     w = shadow_of(conv.weight)
+    if _U22_GATHER and w.shape[3] % 8 == 0 and K.bwd_plans(
+            x.shape, w.shape[0], kh, kw, conv.stride, conv.padding, unroll=True)[0][4] != K.DIRECT:
+        # the kernels gather the unrolled weight from w: no copy to make or keep fresh
+        object.__setattr__(conv, "_kml_wu", K.GATHER22)
+        return K.GATHER22
     buf = _wu_buf(conv, w)
     if not getattr(conv, "_kml_wu_fresh", False):
         object.__setattr__(conv, "_kml_wants_wu", True)
@@ -150,6 +155,9 @@ def unrolled_for(conv, x):
     object.__setattr__(conv, "_kml_wu_fresh", False)   # one forward per refresh
     object.__setattr__(conv, "_kml_wu", buf)           # for this forward's backward
     return buf
+
+
+_U22_GATHER = os.environ.get("KUBEML_U22_GATHER", "1") != "0"
 
 
 def refresh_transposed(convs):

@@ -281,11 +281,33 @@ def unroll22_reference(w):
     return wu.reshape(4 * K, 1, 1, 4 * C)
 
 
+class _Gather22:
+    """``wu=GATHER22``: run an unrolled conv in its 1x1 form WITHOUT a materialised unrolled
+    weight — the FWD / DGRAD weight loaders gather W'[(p, n)][(q, c)] = w[n][tap(p, q)][c]
+    straight from the 3x3 weight (no k_unroll22_multi pass per step).  Not for the direct
+    (transposed-weight) dgrad variant."""
+
+    def __repr__(self):
+        return "GATHER22"
+
+
+GATHER22 = _Gather22()
+
+
+def _g22_weight_ok(w, K1, C1):
+    """The 3x3 weight of a gathered 1x1-form conv of K1 = 4K outputs, C1 = 4C inputs."""
+    return tuple(w.shape) == (K1 // 4, 3, 3, C1 // 4) and K1 % 4 == 0 and C1 % 32 == 0
+
+
 def _check_wu(x_shape, w, wu, KH, KW, stride, pad):
     B, H, W, C = x_shape
     if not unrolled22(H, W, KH, KW, stride, pad):
         raise ValueError("wu given for a conv that is not unrolled (3x3/s1/p1 on 2x2)")
     K = w.shape[0]
+    if wu is GATHER22:
+        if C % 8:
+            raise ValueError("gathered unrolled conv: Cin must be a multiple of 8")
+        return B, C, K
     _chk(wu, BF16, "wu", 4)
     if tuple(wu.shape) != (4 * K, 1, 1, 4 * C):
         raise ValueError(f"unrolled weight shape {tuple(wu.shape)} != {(4 * K, 1, 1, 4 * C)}")
@@ -293,13 +315,14 @@ def _check_wu(x_shape, w, wu, KH, KW, stride, pad):
 
 
 def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False,
-             wu=None, _fold=0):
+             wu=None, _fold=0, _g22=False):
     """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats).
 
     stats: fp32 [2*Cout] accumulated with atomics, or with ``stats_part`` a [G, 2*Cout]
     buffer of per-wave partial rows (``G = conv_stats_rows(M, plan)``, see
     :func:`conv_fwd_plan`) that :func:`bn_apply` sums — no zeroing, no atomics.
-    wu: unrolled weight (:func:`unrolled22`): the conv runs as its dense 1x1 form."""
+    wu: unrolled weight (:func:`unrolled22`): the conv runs as its dense 1x1 form
+    (``GATHER22``: gathered from ``w`` by the kernel)."""
     _chk(x, BF16, "x", 4)
     _chk(w, BF16, "w", 4)
     if wu is not None:
@@ -309,12 +332,16 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
         if out is not None and tuple(out.shape) != (B, 2, 2, K):
             raise ValueError("out shape mismatch")
         o = None if out is None else out.view(B, 1, 1, 4 * K)
-        y = conv_fwd(x.view(B, 1, 1, 4 * C), wu, 1, 1, (1, 1), (0, 0), bias=bias, stats=stats, relu=relu, out=o,
-                     cfg=cfg, stats_part=stats_part, _fold=K)
+        g = wu is GATHER22
+        y = conv_fwd(x.view(B, 1, 1, 4 * C), w if g else wu, 1, 1, (1, 1), (0, 0), bias=bias, stats=stats, relu=relu,
+                     out=o, cfg=cfg, stats_part=stats_part, _fold=K, _g22=g)
         return y.view(B, 2, 2, K)
     B, H, W, C = x.shape
-    K = w.shape[0]
-    if tuple(w.shape[1:]) != (KH, KW, C):
+    K = 4 * w.shape[0] if _g22 else w.shape[0]
+    if _g22:
+        if (KH, KW) != (1, 1) or not _g22_weight_ok(w, K, C):
+            raise ValueError(f"gathered unrolled weight {tuple(w.shape)} does not match the 1x1 form {K}x{C}")
+    elif tuple(w.shape[1:]) != (KH, KW, C):
         raise ValueError(f"weight shape {tuple(w.shape)} does not match KH={KH} KW={KW} Cin={C}")
     if C % 8:
         raise ValueError("Cin must be a multiple of 8 (pad channels)")
@@ -341,17 +368,17 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
             rows, grp, gcnt, tpg = _stats_ws(x.device, M, K, (bm, bn, bk, splits, variant), stats)
     if _fold and grp is not None:
         raise ValueError("folded statistics cannot be group-reduced")
-    sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i i s"
+    sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i i i s"
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, int(_fold),
-                 _s())
+                 int(_g22), _s())
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
     HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
              sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt), tpg,
-             int(_fold), _s())
+             int(_fold), int(_g22), _s())
     return out
 
 
@@ -385,7 +412,7 @@ def _u22_views(B, C, K, dy=None, x=None, addend=None, bnf=None):
 
 
 def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=None, bnf=None, wt=None, wu=None,
-               _fold=0, bnf_mask=False):
+               _fold=0, bnf_mask=False, _g22=False):
     """dx = conv input gradient (+ addend, the fused residual-gradient sum).
 
     bnf = (y or None, c, mean, rstd) of the BatchNorm that consumes dx: the epilogue also
@@ -399,19 +426,23 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         B, C, K = _check_wu(in_shape, w, wu, KH, KW, stride, pad)
         dy1, _, add1, bnf1 = _u22_views(B, C, K, dy=dy, addend=addend, bnf=bnf)
         o = None if out is None else out.view(B, 1, 1, 4 * C)
-        r = conv_dgrad(dy1, wu, (B, 1, 1, 4 * C), 1, 1, (1, 1), (0, 0), out=o, addend=add1, cfg=cfg, bnf=bnf1, wt=wt,
-                       _fold=C, bnf_mask=bnf_mask)
+        g = wu is GATHER22
+        r = conv_dgrad(dy1, w if g else wu, (B, 1, 1, 4 * C), 1, 1, (1, 1), (0, 0), out=o, addend=add1, cfg=cfg,
+                       bnf=bnf1, wt=wt, _fold=C, bnf_mask=bnf_mask, _g22=g)
         if bnf is not None:
             return r[0].view(B, 2, 2, C), r[1]
         return r.view(B, 2, 2, C)
     B, H, W, C = in_shape
-    K = w.shape[0]
+    K = dy.shape[3] if _g22 else w.shape[0]
     sh, sw = stride
     ph, pw = pad
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
     if tuple(dy.shape) != (B, OH, OW, K):
         raise ValueError(f"dy shape {tuple(dy.shape)} != {(B, OH, OW, K)}")
-    if tuple(w.shape) != (K, KH, KW, C):
+    if _g22:
+        if (KH, KW) != (1, 1) or not _g22_weight_ok(w, K, C):
+            raise ValueError(f"gathered unrolled weight {tuple(w.shape)} does not match the 1x1 form {K}x{C}")
+    elif tuple(w.shape) != (K, KH, KW, C):
         raise ValueError(f"weight shape {tuple(w.shape)} != {(K, KH, KW, C)}")
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
@@ -428,6 +459,8 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan, _fold)
     slab = cnt = None
     if variant == DIRECT:
+        if _g22:
+            raise ValueError("the direct dgrad variant needs a materialised unrolled weight (not GATHER22)")
         # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
         wt = _direct_wt(w, wt)
         splits = 1
@@ -435,10 +468,10 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         wt = None
         splits = effective_splits(ntap * _cdiv(K, bk) * bk, bk, splits)
         slab, cnt = _splitk_ws(dy.device, M, C, bm, bn, splits)
-    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p i i s",
+    HIP.call("kml_conv_dgrad", "p p p p p p p p p p p p i i i i i i i i i i i i i i i i i p p i i i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt),
-             int(_fold), int(bool(bnf_mask) and bnf is not None), _s())
+             int(_fold), int(bool(bnf_mask) and bnf is not None), int(_g22), _s())
     return (out, (part, G)) if bnf is not None else out
 
 
@@ -541,11 +574,12 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         raise ValueError("conv_bwd shape mismatch")
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
-    fold = 0
+    fold, g22 = 0, False
     if wu is not None:
         _check_wu(x.shape, w, wu, KH, KW, stride, pad)
         dy, x, addend, bnf = _u22_views(B, C, K, dy=dy, x=x, addend=addend, bnf=bnf)
-        w, fold, accumulate = wu, C, False
+        g22 = wu is GATHER22
+        w, fold, accumulate = (w if g22 else wu), C, False
         H = W = OH = OW = 1
         KH = KW = sh = sw = 1
         ph = pw = 0
@@ -561,7 +595,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, accumulate=accumulate, dbias=dbias,
                    bias_accumulate=bias_accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
-                       bnf_mask=bnf_mask)
+                       bnf_mask=bnf_mask, _g22=g22)
         if not fold:
             return r
         if bnf is not None:
@@ -575,6 +609,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan, fold)
     slab = cnt = None
     if variant == DIRECT:
+        if g22:
+            raise ValueError("the direct dgrad variant needs a materialised unrolled weight (not GATHER22)")
         wt = _direct_wt(w, wt)
         dsplits = 1
     else:
@@ -585,12 +621,12 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     _chk_dbias(dbias, K, KH, KW, stride, pad)
     wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan, dbias is not None)
     HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i s",
+             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i i s",
              _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
              _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
              _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
              int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _p(dbias),
-             int(bool(bias_accumulate)), _s())
+             int(bool(bias_accumulate)), int(g22), _s())
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out

@@ -3,6 +3,10 @@
 set -o pipefail
 out=gpurun_out/r3meas
 mkdir -p $out
+for v in 1 0 1 0; do
+  KUBEML_U22_GATHER=$v timeout -k 10 200 python bench.py --steps 300 --warmup 20 --e2e off --no-epoch > $out/ab_g$v.json 2> $out/ab.err || { tail -5 $out/ab.err; exit 1; }
+  echo "gather=$v $(python -c "import json;d=json.load(open('$out/ab_g$v.json'));print(d['ms_per_step'])")"
+done
 timeout -k 10 500 python -u tools/convergence_check.py --steps 1200 --out $out/convergence.json > $out/convergence.log 2>&1 || { tail -20 $out/convergence.log; exit 1; }
 tail -1 $out/convergence.log | cut -c1-400
 timeout -k 10 500 python -u tools/bench_e2e.py --epochs 4 --validate --trace $out/e2e_trace > $out/e2e.json 2> $out/e2e.err || { tail -20 $out/e2e.err; exit 1; }

@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/r3perf2
 mkdir -p $out
-timeout -k 10 400 python -u -m pytest tests/test_determinism_gpu.py tests/test_engine_gpu.py tests/test_kernels_gpu.py tests/test_models_gpu.py tests/test_peer_gpu.py -x -q --timeout 200 --timeout-method thread -k "determinism or bitwise or memset or one_update or first_update or overlap_matches or plans_on_one or unrolled or ce_bwd or conv or wgrad or linear or resnet or peer" > $out/tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_determinism_gpu.py tests/test_engine_gpu.py tests/test_kernels_gpu.py tests/test_models_gpu.py tests/test_peer_gpu.py -x -q --timeout 200 --timeout-method thread -k "determinism or bitwise or memset or one_update or first_update or overlap_matches or plans_on_one or unrolled or ce_bwd or conv or wgrad or linear or resnet or peer or gathered" > $out/tests.log 2>&1
 rc=$?; tail -5 $out/tests.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 200 python bench.py --steps 200 --warmup 10 --e2e off > $out/bench.json 2> $out/bench.err || { tail -5 $out/bench.err; exit 1; }
 cut -c1-300 $out/bench.json

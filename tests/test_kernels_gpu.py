@@ -807,3 +807,33 @@ def test_wgrad_ones_column_bias_gradient(B, C, K, grouped):
     dw2 = torch.zeros_like(dw)
     K_.conv_wgrad(x, dy, dw2, 1, 1, (1, 1), (0, 0), accumulate=True, dbias=db2, bias_accumulate=True)
     torch.testing.assert_close(db2, want_db + 0.5, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,C,Kc", [(64, 256, 256), (32, 128, 256), (8, 64, 32)])
+def test_gathered_unrolled_weight_matches_materialised(B, C, Kc):
+    """wu=GATHER22: the FWD / DGRAD loaders gather the unrolled weight straight from the 3x3
+    weight — bitwise the same results as the materialised [4K,1,1,4C] copy, for the forward
+    (with folded BN partial rows), the dgrad and the grouped dgrad+wgrad launch."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(3)
+    x = _bf(torch.randn(B, 2, 2, C, device=dev))
+    w = _bf(torch.randn(Kc, 3, 3, C, device=dev) * 0.05)
+    dy = _bf(torch.randn(B, 2, 2, Kc, device=dev))
+    wu = K.unrolled_weight(w)
+    args = (3, 3, (1, 1), (1, 1))
+    Gu = K.conv_fwd_stats_rows(x.shape, Kc, *args, unroll=True)
+    s1 = torch.empty(Gu * 2 * Kc, device=dev)
+    s2 = torch.empty(Gu * 2 * Kc, device=dev)
+    y1 = K.conv_fwd(x, w, *args, stats=s1, stats_part=True, wu=wu)
+    y2 = K.conv_fwd(x, w, *args, stats=s2, stats_part=True, wu=K.GATHER22)
+    assert torch.equal(y1, y2) and torch.equal(s1, s2)
+    plan = K.bwd_plans(x.shape, Kc, *args, unroll=True)[0]
+    if plan[4] != K.DIRECT:
+        d1 = K.conv_dgrad(dy, w, x.shape, *args, wu=wu)
+        d2 = K.conv_dgrad(dy, w, x.shape, *args, wu=K.GATHER22)
+        assert torch.equal(d1, d2)
+        g1 = torch.empty((4 * Kc, 1, 1, 4 * C), device=dev)
+        g2 = torch.empty_like(g1)
+        e1 = K.conv_bwd(dy, w, x, g1, *args, wu=wu)
+        e2 = K.conv_bwd(dy, w, x, g2, *args, wu=K.GATHER22)
+        assert torch.equal(e1, e2) and torch.equal(g1, g2)
