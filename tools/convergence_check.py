@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def make_task(n, g, dev, templates):
+def make_task(n, g, dev, templates, noise=40.0, label_noise=0.0):
     import torch
     cls = torch.randint(0, 10, (n,), device=dev, generator=g)
     contrast = 0.6 + 0.8 * torch.rand(n, 1, 1, 1, device=dev, generator=g)
@@ -40,8 +40,12 @@ def make_task(n, g, dev, templates):
     rows = (sy.view(n, 1) + torch.arange(32, device=dev).view(1, 32))  # [n, 32]
     cols = (sx.view(n, 1) + torch.arange(32, device=dev).view(1, 32))
     img = img[torch.arange(n, device=dev).view(n, 1, 1), rows.view(n, 32, 1), cols.view(n, 1, 32)]
-    img = img + 40.0 * torch.randn(img.shape, device=dev, generator=g)
-    return img.clamp(0, 255).round().to(torch.uint8).contiguous(), cls
+    img = img + noise * torch.randn(img.shape, device=dev, generator=g)
+    labels = cls.clone()
+    if label_noise > 0:   # training labels only: a fraction replaced by uniform random classes
+        flip = torch.rand(n, device=dev, generator=g) < label_noise
+        labels[flip] = torch.randint(0, 10, (int(flip.sum()),), device=dev, generator=g)
+    return img.clamp(0, 255).round().to(torch.uint8).contiguous(), labels
 
 
 def main():
@@ -53,6 +57,11 @@ def main():
     ap.add_argument("--n-train", type=int, default=25600)
     ap.add_argument("--n-test", type=int, default=5120)
     ap.add_argument("--log-every", type=int, default=25)
+    ap.add_argument("--eval-every", type=int, default=200, help="validation accuracy of both paths every N steps")
+    ap.add_argument("--noise", type=float, default=70.0, help="per-pixel Gaussian noise (uint8 units)")
+    ap.add_argument("--mix", type=float, default=0.75,
+                    help="share of a template common to every class (higher: classes overlap more)")
+    ap.add_argument("--label-noise", type=float, default=0.2, help="fraction of random training labels")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "convergence.json"))
     a = ap.parse_args()
 
@@ -68,10 +77,11 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(2024)
     # low-frequency colour templates (8x8 random field upsampled to 38x38)
-    base = torch.rand(10, 3, 8, 8, device=dev, generator=g) * 255.0
+    common = torch.rand(1, 3, 8, 8, device=dev, generator=g) * 255.0
+    base = a.mix * common + (1.0 - a.mix) * torch.rand(10, 3, 8, 8, device=dev, generator=g) * 255.0
     templates = F.interpolate(base, size=(38, 38), mode="bilinear", align_corners=False).permute(0, 2, 3, 1)
-    xtr, ytr = make_task(a.n_train, g, dev, templates)
-    xte, yte = make_task(a.n_test, g, dev, templates)
+    xtr, ytr = make_task(a.n_train, g, dev, templates, a.noise, a.label_noise)
+    xte, yte = make_task(a.n_test, g, dev, templates, a.noise, 0.0)
     B = a.batch
 
     torch.manual_seed(7)
@@ -111,7 +121,7 @@ def main():
         model.train()
         return 100.0 * correct / tot, loss_sum / tot
 
-    curve = []
+    curve, val_curve = [], []
     t0 = time.time()
     for s in range(a.steps):
         K.augment(xtr, ytr, ctr, B, out=xb, labels_out=yb, train=True)
@@ -127,10 +137,17 @@ def main():
         if s % a.log_every == 0 or s == a.steps - 1:
             curve.append({"step": s, "ours": round(float(lo), 4), "stock_fp32": round(float(lr_), 4)})
             print(json.dumps(curve[-1]), flush=True)
+        if a.eval_every and (s + 1) % a.eval_every == 0 and s + 1 < a.steps:
+            ao, _ = evaluate(ours, False)
+            ar, _ = evaluate(ref, True)
+            val_curve.append({"step": s + 1, "ours_acc": round(ao, 2), "stock_fp32_acc": round(ar, 2)})
+            print(json.dumps(val_curve[-1]), flush=True)
     acc_o, vl_o = evaluate(ours, False)
     acc_r, vl_r = evaluate(ref, True)
     epochs = a.steps * B / a.n_train
-    res = {"task": "synthetic learnable CIFAR-shaped (10 class templates, shift, contrast, noise)",
+    val_curve.append({"step": a.steps, "ours_acc": round(acc_o, 2), "stock_fp32_acc": round(acc_r, 2)})
+    res = {"task": (f"synthetic learnable CIFAR-shaped (10 overlapping class templates, mix {a.mix}, shift, "
+                    f"contrast, noise {a.noise}, {100 * a.label_noise:.0f}% random training labels)"),
            "model": "resnet34 (ImageNet stem, 1000-class head)", "batch": B, "steps": a.steps,
            "epochs": round(epochs, 2), "optimizer": f"SGD lr={a.lr} momentum={a.momentum} wd=1e-4",
            "ours": {"path": "kubeml_amd bf16 HIP kernels, fp32 master, graphed step",
@@ -138,11 +155,11 @@ def main():
            "stock_fp32": {"path": "torch fp32 NCHW (MIOpen/hipBLASLt), torch.optim.SGD",
                           "final_val_acc": round(acc_r, 2), "final_val_loss": round(vl_r, 4)},
            "acc_gap_points": round(acc_o - acc_r, 2), "wall_s": round(time.time() - t0, 1),
-           "curve": curve}
+           "val_curve": val_curve, "curve": curve}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k != "curve"}), flush=True)
+    print(json.dumps({k: v for k, v in res.items() if k not in ("curve", "val_curve")}), flush=True)
     if not all(math.isfinite(c["ours"]) for c in curve):
         sys.exit(1)
 
