@@ -433,7 +433,7 @@ __device__ __forceinline__ int row_off(const ConvArgs& a, int col) {
 }
 __device__ __forceinline__ int sq_off(const ConvArgs& a) { return a.fold_c ? a.fold_c : a.N; }
 
-template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false>
+template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false, bool STAGE_ALL = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
                                               int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -555,7 +555,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     constexpr int BMT = SINGLE ? WM : 2 * WM, BNT = SINGLE ? WN : 2 * WN;
     // Large tiles stage the bf16 output through LDS (past the 16-byte split-K flag word) and
     // write it back as 16-byte row chunks instead of one 2-byte store per element.
-    constexpr bool STAGE_OK = !SINGLE && BMT * BNT >= 8192;
+    constexpr bool STAGE_OK = !SINGLE && (STAGE_ALL || BMT * BNT >= 8192);
     constexpr int LDO = BNT + 8;  // padded LDS row (bf16 elements)
     constexpr int RED_OFF = 16 + (STAGE_OK ? BMT * LDO * 2 : 0);
     const bool stage = STAGE_OK && flag != nullptr && (a.N % 8) == 0;
@@ -1171,6 +1171,221 @@ __global__ void k_weight_transpose(const bf16_t* __restrict__ w, bf16_t* __restr
   }
 }
 
+// =====================================================================================
+// Variant 4: halo-patch forward for 3x3 / stride 1 / pad 1 convolutions on small maps.
+//
+// The implicit-GEMM kernels above stage im2col(X) tiles: every input pixel passes through
+// LDS once per filter tap (9x the activation bytes), plus a weight panel per M-tile.  On
+// ResNet-34's 8x8 / 4x4 layers that traffic, not the MFMA, bounds them (47-55 MB through
+// the CU's L2->LDS path per call, profiles/resnet34_bench_r3.md).  Here a block owns IMG
+// whole images: their zero-padded (HW+2)^2 x C patches are staged into LDS ONCE and the 9
+// taps are LDS address offsets; the weights never touch LDS — each lane streams its MFMA B
+// fragments (16 B = 8 consecutive k of one output channel, K-contiguous KRSC) straight from
+// L2 into registers, D K-steps ahead.  Per block: IMG*(HW)^2*C*2 activation bytes + a BN x 9C
+// weight slice (shared by the two waves of a column through L1), instead of
+// 9*BM*C*2 + BN*9C*2 through LDS.
+//
+// Waves: 2x2, each (BM/2) x (BN/2) of v_mfma_f32_16x16x32_bf16 fragments.  Patch pixels are
+// C*2-byte rows of 16-byte chunks, chunk XOR (pixel & SWZ): a fragment read (16 rows x 4
+// chunks) touches every bank group once for consecutive pixels.  The epilogue is the shared
+// conv_epilogue (BN statistics partial rows per M-tile, bias/ReLU, bf16 store).
+// =====================================================================================
+template <int C, int HW, int IMG, int BN, int D>
+struct HaloFwd {
+  static constexpr int HP = HW + 2;              // padded patch side
+  static constexpr int CH = C / 8;               // 16-byte chunks per pixel
+  // patch row pitch (pixels) and chunk swizzle, chosen with tools/lds_banks.py's model of
+  // ds_read_b128 lane groups over every (tap, fragment, k-chunk) read of the main loop:
+  // pitch 16 on 8x8 maps is conflict-free at C = 64; pixel*13 on 4x4 maps (pitch 8) leaves
+  // 1/3 of the reads 2-way instead of all of them with the natural pitch.
+  static constexpr int PITCH0 = HW == 8 ? 16 : 8;
+  static constexpr int PITCH = IMG * HP * PITCH0 * C * 2 <= 96 * 1024 ? PITCH0 : HP;
+  static constexpr int IMGPIX = HP * PITCH;      // patch pixels per image (incl. unused pitch)
+  static constexpr int PIX = IMG * IMGPIX;
+  static constexpr int SWZ = CH >= 16 ? 15 : 7;  // chunk swizzle mask
+  static constexpr int BM = IMG * HW * HW;
+  static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  static constexpr int KS = 9 * C / 32;          // 32-deep K-steps (tap-major, cin-minor)
+  static constexpr int WCH = 9 * CH;             // 16-byte chunks per weight row
+  static constexpr int SMEM_PATCH = PIX * C * 2;
+  static constexpr int SMEM_W = BN * 9 * C * 2;  // the block's whole weight slice
+  // weights staged in LDS with the patch when both fit (coalesced 1 KiB wave loads, 4x fewer
+  // L2 requests than per-fragment row segments); otherwise streamed into registers
+  static constexpr bool WLDS = SMEM_PATCH + SMEM_W <= 128 * 1024;
+  static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
+  static constexpr int SMEM_MAIN = SMEM_PATCH + (WLDS ? SMEM_W : 0);
+  static constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __device__ __forceinline__ static int swz(int pix) {
+    const int h = (HW == 8) ? (C == 64 ? pix : pix * 9) : pix * 13;
+    return h & SWZ;
+  }
+  static_assert(BM % 32 == 0 && BN % 32 == 0 && C % 32 == 0, "halo tile shape");
+  static_assert(SMEM <= 160 * 1024, "halo patch exceeds LDS");
+};
+
+template <int C, int HW, int IMG, int BN, int D>
+__global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
+  using P = HaloFwd<C, HW, IMG, BN, D>;
+  constexpr int MR = P::MR, NR = P::NR, KS = P::KS, CH = P::CH, HP = P::HP, PITCH = P::PITCH;
+  constexpr bool WL = P::WLDS;
+  __shared__ __attribute__((aligned(16))) char smem[P::SMEM];
+  char* const swt = smem + P::SMEM_PATCH;  // weight slice [BN][9C] (WLDS)
+  const Blk bk = xcd_blk();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int m0 = bk.y * P::BM, n0 = bk.x * BN, img0 = bk.y * IMG;
+
+  // weights first (register stream: D K-steps of B fragments; LDS: the whole contiguous
+  // [n0, n0+BN) x 9C slice), in flight while the patch loads are issued
+  const bf16_t* wp[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+    wp[j] = a.w + (long long)(n0 + wn * P::WN + j * 16 + (lane & 15)) * (9 * C) + 8 * (lane >> 4);
+  constexpr int DD = WL ? 1 : D;
+  bf16x8_t bq[DD][NR];
+  constexpr int WCHUNKS = BN * P::WCH;
+  constexpr int WPER = WL ? (WCHUNKS + 255) / 256 : 1;
+  uint4 wv[WPER];
+  if constexpr (WL) {
+    const bf16_t* wsrc = a.w + (long long)n0 * (9 * C);
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+      const int q = tid + u * 256;
+      wv[u] = ld16(q < WCHUNKS ? wsrc + q * 8 : a.zp);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < DD; ++d)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bq[d][j] = *reinterpret_cast<const bf16x8_t*>(wp[j] + d * 32);
+  }
+
+  // zero-padded patches of images img0 .. img0+IMG-1 (images past B read the zero page)
+  constexpr int CHUNKS = IMG * HP * HP * CH;
+  constexpr int PER = (CHUNKS + 255) / 256;
+  uint4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = tid + u * 256;
+    const int qq = q < CHUNKS ? q : 0;
+    const int pix = qq / CH, ch = qq - pix * CH;
+    const int im = pix / (HP * HP), rem = pix - im * (HP * HP);
+    const int ih = rem / HP - 1, iw = rem - (rem / HP) * HP - 1;
+    const bool in = q < CHUNKS && (unsigned)ih < (unsigned)HW && (unsigned)iw < (unsigned)HW && img0 + im < a.B;
+    v[u] = ld16(in ? a.x + (((long long)(img0 + im) * HW + ih) * HW + iw) * C + ch * 8 : a.zp);
+  }
+  if constexpr (WL) {
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+      const int q = tid + u * 256;
+      if (q < WCHUNKS) {
+        const int n = q / P::WCH, c = q - n * P::WCH;
+        *reinterpret_cast<uint4*>(swt + (n * P::WCH + (c ^ (n & P::SWZ))) * 16) = wv[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = tid + u * 256;
+    if (q < CHUNKS) {
+      const int pix = q / CH, ch = q - pix * CH;
+      const int im = pix / (HP * HP), rem = pix - im * (HP * HP);
+      const int lp = im * P::IMGPIX + (rem / HP) * PITCH + (rem - (rem / HP) * HP);
+      *reinterpret_cast<uint4*>(smem + (lp * CH + (ch ^ P::swz(lp))) * 16) = v[u];
+    }
+  }
+  __syncthreads();
+
+  // patch pixel of tap (0,0) for each A row this lane feeds
+  int abase[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int r = wm * P::WM + i * 16 + (lane & 15);
+    const int im = r / (HW * HW), p = r - im * (HW * HW);
+    abase[i] = im * P::IMGPIX + (p / HW) * PITCH + (p % HW);
+  }
+  // weight-slice row of each B fragment this lane feeds (WLDS)
+  int brow[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) brow[j] = wn * P::WN + j * 16 + (lane & 15);
+  auto read_ab = [&](int ks, bf16x8_t (&af)[MR], bf16x8_t (&bf)[NR]) {
+    const int tap = ks / (C / 32);
+    const int toff = (tap / 3) * PITCH + (tap % 3);
+    const int chunk = (ks % (C / 32)) * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int pix = abase[i] + toff;
+      af[i] = *reinterpret_cast<const bf16x8_t*>(smem + (pix * CH + (chunk ^ P::swz(pix))) * 16);
+    }
+    if constexpr (WL) {
+      const int wc = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bf[j] = *reinterpret_cast<const bf16x8_t*>(swt + (brow[j] * P::WCH + (wc ^ (brow[j] & P::SWZ))) * 16);
+    }
+  };
+
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // LDS fragments one K-step ahead (the MFMAs of step ks never wait on its LDS reads)
+  bf16x8_t af[2][MR], bl[2][NR];
+  read_ab(0, af[0], bl[0]);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (ks + 1 < KS) read_ab(ks + 1, af[(ks + 1) & 1], bl[(ks + 1) & 1]);
+    bf16x8_t bf[NR];
+    if constexpr (WL) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bf[j] = bl[ks & 1][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bf[j] = bq[ks % DD][j];
+      if (ks + DD < KS) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) bq[ks % DD][j] = *reinterpret_cast<const bf16x8_t*>(wp[j] + (ks + DD) * 32);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();  // LDS is reused by the epilogue
+  conv_epilogue<FWD, MR, NR, P::WM, P::WN, false, true>(a, acc, m0, n0, wm, wn, lane, tid, 0, 0,
+                                                        reinterpret_cast<unsigned*>(smem));
+}
+
+template <int C, int HW, int IMG, int BN>
+int launch_halo(const ConvArgs& a, hipStream_t s) {
+  using P = HaloFwd<C, HW, IMG, BN, 1>;
+  constexpr int D = P::NR >= 4 ? 4 : (P::NR == 2 ? 8 : 12);
+  dim3 grid(a.N / BN, (a.M + P::BM - 1) / P::BM, 1);
+  hipLaunchKernelGGL((k_conv_halo<C, HW, IMG, BN, D>), grid, dim3(256), 0, s, a);
+  KML_LAUNCH_CHECK();
+}
+
+// bm = pixels per block (IMG whole images), bn = output channels per block
+bool halo_shape_ok(int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, int bm, int bn) {
+  return KH == 3 && KW == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && H == W && bn > 0 && K % bn == 0 &&
+         bm % (H * W) == 0;
+}
+
+int dispatch_halo(const ConvArgs& a, int bm, int bn, hipStream_t s) {
+#define KML_H(Cv, HWv, BMv, BNv)                                                   \
+  if (a.C == Cv && a.H == HWv && bm == BMv && bn == BNv)                           \
+    return launch_halo<Cv, HWv, BMv / (HWv * HWv), BNv>(a, s);
+  KML_H(64, 8, 64, 64) KML_H(64, 8, 128, 64) KML_H(64, 8, 64, 32)
+  KML_H(128, 4, 64, 32) KML_H(128, 4, 64, 64) KML_H(128, 4, 128, 32) KML_H(128, 4, 64, 128) KML_H(128, 4, 128, 64)
+  KML_H(256, 4, 64, 32) KML_H(256, 4, 64, 64) KML_H(256, 8, 64, 32) KML_H(256, 8, 64, 64)
+  KML_H(512, 4, 64, 32) KML_H(512, 4, 64, 64)
+#undef KML_H
+  return (int)hipErrorInvalidValue;
+}
+
 template <int MODE>
 int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
 #define KML_T(BMv, BNv)                                                  \
@@ -1490,6 +1705,17 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     a.splits = 1; a.kchunk = a.Kd;
     if (!a.zp) return (int)hipErrorInvalidSymbol;
     return dispatch_direct<FWD>(a, bm, bn, bk, s);
+  }
+  if (variant == 4) {  // halo patch: bm = pixels per block (whole images), bn = channels per block
+    if (g22 || fold_c || !halo_shape_ok(H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn)) return (int)hipErrorInvalidValue;
+    ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+    a.zp = zero_page();
+    a.M = B * a.OH * a.OW; a.N = K; a.Kd = 9 * C;
+    a.splits = 1; a.kchunk = a.Kd;
+    if (!a.zp) return (int)hipErrorInvalidSymbol;
+    return dispatch_halo(a, bm, bn, s);
   }
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);

@@ -355,7 +355,8 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
         assert bias.numel() >= K
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
-    bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg)
+    bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg,
+                                                geom=None if _g22 else (H, W, KH, KW, stride, pad))
     rows, grp, gcnt, tpg = stats, None, None, 0
     if stats is not None:
         _chk(stats, F32, "stats")
@@ -369,6 +370,10 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     if _fold and grp is not None:
         raise ValueError("folded statistics cannot be group-reduced")
     sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i i i s"
+    if variant == HALO:
+        HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
+                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, HALO, 0, 0, _p(grp), _p(gcnt), tpg, 0, 0, _s())
+        return out
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, int(_fold),
@@ -382,12 +387,49 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     return out
 
 
-def conv_fwd_plan(C, M, K, Kd, cfg=None):
-    """The (bm, bn, bk, splits, variant) conv_fwd will run for this shape."""
+def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
+    """The (bm, bn, bk, splits, variant) conv_fwd will run for this shape.  ``geom`` =
+    (H, W, KH, KW, stride, pad) lets an eligible conv take the halo-patch kernel
+    (:func:`halo_plan`); without it (or when ineligible) a HALO plan falls back."""
+    if cfg is None and geom is not None:
+        hp = halo_plan(C, K, *geom)
+        if hp is not None:
+            return hp
     plan = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
+    if plan[4] == HALO and (geom is None or not halo_ok(C, K, *geom, plan[0], plan[1])):
+        plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == DIRECT and C % 32:
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     return plan
+
+
+HALO = 4  # cfg variant id of the halo-patch forward (3x3/s1/p1 on small maps): bm = pixels, bn = channels
+# (C, H) -> (bm, bn): the halo tiles the kernel is instantiated for, first = default
+_HALO_TILES = {(64, 8): [(64, 32), (64, 64), (128, 64)],
+               (128, 4): [(64, 32), (64, 64), (128, 32), (64, 128), (128, 64)],
+               (256, 8): [(64, 64), (64, 32)], (256, 4): [(64, 32), (64, 64)],
+               (512, 4): [(64, 32), (64, 64)]}
+_HALO_ON = os.environ.get("KUBEML_CONV_HALO", "1") != "0"
+
+
+def halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
+    """Is (bm, bn) an instantiated halo tile for this conv?"""
+    return ((KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1) and H == W and
+            (bm, bn) in _HALO_TILES.get((C, H), ()) and K % bn == 0)
+
+
+def halo_plan(C, K, H, W, KH, KW, stride, pad):
+    """Default halo-patch plan for an eligible forward conv, or None (``KUBEML_CONV_HALO=0``
+    disables it; ``KUBEML_HALO_TILE=bm,bn`` picks another instantiated tile)."""
+    if not _HALO_ON:
+        return None
+    tiles = _HALO_TILES.get((C, H), ())
+    env = os.environ.get("KUBEML_HALO_TILE")
+    cands = ([tuple(int(v) for v in env.split(","))] if env else []) + list(tiles)
+    for bm, bn in cands:
+        if halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn):
+            return (bm, bn, 0, 1, HALO)
+    return None
 
 
 def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False):
@@ -401,7 +443,7 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False)
     OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
-    return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg))
+    return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg, geom=(H, W, KH, KW, stride, pad)))
 
 
 def _u22_views(B, C, K, dy=None, x=None, addend=None, bnf=None):

@@ -362,6 +362,43 @@ def test_conv_direct_variant(shape, tile):
     assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
 
 
+HALO_CASES = [(4, 8, 64, 64), (3, 8, 64, 128), (6, 4, 128, 128), (5, 4, 128, 256), (2, 8, 256, 64),
+              (3, 4, 256, 64), (2, 4, 512, 64)]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_variant(case):
+    """Halo-patch forward (variant 4: whole zero-padded images staged in LDS once, weights
+    streamed into MFMA registers) for every instantiated tile: output (+bias/ReLU), atomic
+    statistics and per-M-tile partial rows vs fp32 torch; batches that do not fill the last
+    block's images exercise the zero-page tail."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co = case
+    torch.manual_seed(11)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * (1.0 / (9 * Ci) ** 0.5))
+    bias = torch.randn(Co, device=dev)
+    pre = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, padding=1)
+    tiles = [t for t in K._HALO_TILES[(Ci, H)] if Co % t[1] == 0]
+    assert tiles and K.halo_plan(Ci, Co, H, H, 3, 3, (1, 1), (1, 1)) is not None
+    for bm, bn in tiles:
+        cfg = (bm, bn, 0, 1, K.HALO)
+        st = torch.zeros(2 * Co, device=dev)
+        y = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), bias=bias, stats=st, relu=True, cfg=cfg)
+        yr = F.relu(pre)
+        assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2, (bm, bn)
+        assert _rel(st[:Co], yr.sum((0, 2, 3))) < 2e-2, (bm, bn)
+        G = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, (1, 1), (1, 1), cfg=cfg)
+        assert G == -(-B * H * H // bm)
+        buf = torch.full((G * 2 * Co + 256,), float("nan"), device=dev)
+        y2 = K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=buf[:G * 2 * Co], stats_part=True, cfg=cfg)
+        assert torch.isnan(buf[G * 2 * Co:]).all() and not torch.isnan(buf[:G * 2 * Co]).any()
+        yf = (pre - bias.view(1, -1, 1, 1))
+        assert _rel(y2.permute(0, 3, 1, 2), yf) < 1e-2, (bm, bn)
+        rows = buf[:G * 2 * Co].view(G, 2, Co).sum(0)
+        assert _rel(rows[0], yf.sum((0, 2, 3))) < 2e-2 and _rel(rows[1], (yf * yf).sum((0, 2, 3))) < 2e-2
+
+
 @pytest.mark.parametrize("cfg", [(32, 32, 64, 1, 0), (64, 32, 64, 2, 1), (128, 64, 64, 1, 2), (32, 32, 4, 1, 3),
                                  (64, 64, 32, 4, 0)])
 def test_conv_partial_stats_into_bn_apply(cfg):
