@@ -1190,10 +1190,15 @@ __global__ void k_weight_transpose(const bf16_t* __restrict__ w, bf16_t* __restr
 // chunks) touches every bank group once for consecutive pixels.  The epilogue is the shared
 // conv_epilogue (BN statistics partial rows per M-tile, bias/ReLU, bf16 store).
 // =====================================================================================
-template <int C, int HW, int IMG, int BN, int D>
-struct HaloFwd {
+// MODE = FWD : A = patch of x (C = Cin channels), B[n = cout][k = (tap, cin)] = w rows.
+// MODE = DGRAD: A = patch of dy (C = Cout channels), B[n = cin][k = (tap', cout)] =
+//               w[cout][8 - tap'][cin] (stride 1 / pad 1: dX is the correlation of the padded dY
+//               with the flipped filter).  Its weight slice is staged K-strided ([k][BN], one
+//               16-byte chunk = 8 cin of one (cout, tap)) and read with ds_read_b64_tr_b16.
+template <int MODE, int C, int HW, int IMG, int BN, int D>
+struct HaloBody {
   static constexpr int HP = HW + 2;              // padded patch side
-  static constexpr int CH = C / 8;               // 16-byte chunks per pixel
+  static constexpr int CH = C / 8;               // 16-byte chunks per patch pixel
   // patch row pitch (pixels) and chunk swizzle, chosen with tools/lds_banks.py's model of
   // ds_read_b128 lane groups over every (tap, fragment, k-chunk) read of the main loop:
   // pitch 16 on 8x8 maps is conflict-free at C = 64; pixel*13 on 4x4 maps (pitch 8) leaves
@@ -1205,13 +1210,13 @@ struct HaloFwd {
   static constexpr int SWZ = CH >= 16 ? 15 : 7;  // chunk swizzle mask
   static constexpr int BM = IMG * HW * HW;
   static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
-  static constexpr int KS = 9 * C / 32;          // 32-deep K-steps (tap-major, cin-minor)
-  static constexpr int WCH = 9 * CH;             // 16-byte chunks per weight row
+  static constexpr int KS = 9 * C / 32;          // 32-deep K-steps (tap-major, channel-minor)
+  static constexpr int WCH = 9 * CH;             // FWD: 16-byte chunks per weight row
   static constexpr int SMEM_PATCH = PIX * C * 2;
   static constexpr int SMEM_W = BN * 9 * C * 2;  // the block's whole weight slice
-  // weights staged in LDS with the patch when both fit (coalesced 1 KiB wave loads, 4x fewer
-  // L2 requests than per-fragment row segments); otherwise streamed into registers
-  static constexpr bool WLDS = SMEM_PATCH + SMEM_W <= 128 * 1024;
+  // weights staged in LDS with the patch when both fit (coalesced loads, 4x fewer L2 requests
+  // than per-fragment row segments); otherwise (FWD only) streamed into registers
+  static constexpr bool WLDS = MODE == DGRAD || SMEM_PATCH + SMEM_W <= 128 * 1024;
   static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
   static constexpr int SMEM_MAIN = SMEM_PATCH + (WLDS ? SMEM_W : 0);
   static constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
@@ -1219,38 +1224,48 @@ struct HaloFwd {
     const int h = (HW == 8) ? (C == 64 ? pix : pix * 9) : pix * 13;
     return h & SWZ;
   }
+  static_assert(MODE == FWD || MODE == DGRAD, "halo: fwd / dgrad");
   static_assert(BM % 32 == 0 && BN % 32 == 0 && C % 32 == 0, "halo tile shape");
-  static_assert(SMEM <= 160 * 1024, "halo patch exceeds LDS");
+  static_assert(MODE == FWD || BN == 32 || BN == 64, "dgrad halo: K-strided tile of 32 or 64 columns");
+  static_assert(SMEM <= 160 * 1024, "halo working set exceeds LDS");
+  static constexpr int THREADS = 256;
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem);
 };
 
-template <int C, int HW, int IMG, int BN, int D>
-__global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
-  using P = HaloFwd<C, HW, IMG, BN, D>;
+template <int MODE, int C, int HW, int IMG, int BN, int D>
+__device__ __forceinline__ void HaloBody<MODE, C, HW, IMG, BN, D>::run(const ConvArgs& a, const Blk& bk, char* smem) {
+  using P = HaloBody<MODE, C, HW, IMG, BN, D>;
   constexpr int MR = P::MR, NR = P::NR, KS = P::KS, CH = P::CH, HP = P::HP, PITCH = P::PITCH;
   constexpr bool WL = P::WLDS;
-  __shared__ __attribute__((aligned(16))) char smem[P::SMEM];
-  char* const swt = smem + P::SMEM_PATCH;  // weight slice [BN][9C] (WLDS)
-  const Blk bk = xcd_blk();
+  char* const swt = smem + P::SMEM_PATCH;  // weight slice (WLDS)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int m0 = bk.y * P::BM, n0 = bk.x * BN, img0 = bk.y * IMG;
+  const bf16_t* const src = (MODE == FWD) ? a.x : a.dy;   // patch source, C channels
 
-  // weights first (register stream: D K-steps of B fragments; LDS: the whole contiguous
-  // [n0, n0+BN) x 9C slice), in flight while the patch loads are issued
+  // weights first (FWD register stream: D K-steps of B fragments; otherwise the block's whole
+  // slice), in flight while the patch loads are issued
   const bf16_t* wp[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j)
     wp[j] = a.w + (long long)(n0 + wn * P::WN + j * 16 + (lane & 15)) * (9 * C) + 8 * (lane >> 4);
   constexpr int DD = WL ? 1 : D;
   bf16x8_t bq[DD][NR];
-  constexpr int WCHUNKS = BN * P::WCH;
+  constexpr int WCHUNKS = BN * 9 * C / 8;
   constexpr int WPER = WL ? (WCHUNKS + 255) / 256 : 1;
   uint4 wv[WPER];
   if constexpr (WL) {
-    const bf16_t* wsrc = a.w + (long long)n0 * (9 * C);
 #pragma unroll
     for (int u = 0; u < WPER; ++u) {
       const int q = tid + u * 256;
-      wv[u] = ld16(q < WCHUNKS ? wsrc + q * 8 : a.zp);
+      const int qq = q < WCHUNKS ? q : 0;
+      const bf16_t* p;
+      if constexpr (MODE == FWD) {  // contiguous [n0, n0+BN) x 9C slice
+        p = a.w + (long long)n0 * (9 * C) + qq * 8;
+      } else {                      // chunk q = (row (cout, tap), cin chunk): w[cout][tap][n0 + 8c ..]
+        const int row = qq / (BN / 8), c = qq - row * (BN / 8);
+        p = a.w + (long long)row * a.C + n0 + c * 8;
+      }
+      wv[u] = ld16(q < WCHUNKS ? p : a.zp);
     }
   } else {
 #pragma unroll
@@ -1271,15 +1286,22 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
     const int im = pix / (HP * HP), rem = pix - im * (HP * HP);
     const int ih = rem / HP - 1, iw = rem - (rem / HP) * HP - 1;
     const bool in = q < CHUNKS && (unsigned)ih < (unsigned)HW && (unsigned)iw < (unsigned)HW && img0 + im < a.B;
-    v[u] = ld16(in ? a.x + (((long long)(img0 + im) * HW + ih) * HW + iw) * C + ch * 8 : a.zp);
+    v[u] = ld16(in ? src + (((long long)(img0 + im) * HW + ih) * HW + iw) * C + ch * 8 : a.zp);
   }
   if constexpr (WL) {
 #pragma unroll
     for (int u = 0; u < WPER; ++u) {
       const int q = tid + u * 256;
       if (q < WCHUNKS) {
-        const int n = q / P::WCH, c = q - n * P::WCH;
-        *reinterpret_cast<uint4*>(swt + (n * P::WCH + (c ^ (n & P::SWZ))) * 16) = wv[u];
+        if constexpr (MODE == FWD) {
+          const int n = q / P::WCH, c = q - n * P::WCH;
+          *reinterpret_cast<uint4*>(swt + (n * P::WCH + (c ^ (n & P::SWZ))) * 16) = wv[u];
+        } else {  // LDS row k = (8 - tap) * C + cout, K-strided swizzled chunk
+          const int row = q / (BN / 8), c = q - row * (BN / 8);
+          const int cout = row / 9, tap = row - cout * 9;
+          const int k = (8 - tap) * C + cout;
+          *reinterpret_cast<uint4*>(swt + (k * BN + ((c ^ swz_ks<BN>(k)) << 3)) * 2) = wv[u];
+        }
       }
     }
   }
@@ -1303,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
     const int im = r / (HW * HW), p = r - im * (HW * HW);
     abase[i] = im * P::IMGPIX + (p / HW) * PITCH + (p % HW);
   }
-  // weight-slice row of each B fragment this lane feeds (WLDS)
+  // FWD weight-slice row of each B fragment this lane feeds (WLDS)
   int brow[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) brow[j] = wn * P::WN + j * 16 + (lane & 15);
@@ -1316,11 +1338,15 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
       const int pix = abase[i] + toff;
       af[i] = *reinterpret_cast<const bf16x8_t*>(smem + (pix * CH + (chunk ^ P::swz(pix))) * 16);
     }
-    if constexpr (WL) {
+    if constexpr (WL && MODE == FWD) {
       const int wc = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int j = 0; j < NR; ++j)
         bf[j] = *reinterpret_cast<const bf16x8_t*>(swt + (brow[j] * P::WCH + (wc ^ (brow[j] & P::SWZ))) * 16);
+    } else if constexpr (MODE == DGRAD) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bf[j] = frag_kstrided<BN>(reinterpret_cast<const bf16_t*>(swt), wn * P::WN + j * 16, ks, lane);
     }
   };
 
@@ -1355,16 +1381,23 @@ __global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[j], acc[i][j], 0, 0, 0);
   }
   __syncthreads();  // LDS is reused by the epilogue
-  conv_epilogue<FWD, MR, NR, P::WM, P::WN, false, true>(a, acc, m0, n0, wm, wn, lane, tid, 0, 0,
-                                                        reinterpret_cast<unsigned*>(smem));
+  conv_epilogue<MODE, MR, NR, P::WM, P::WN, false, true>(a, acc, m0, n0, wm, wn, lane, tid, 0, 0,
+                                                         reinterpret_cast<unsigned*>(smem));
 }
 
-template <int C, int HW, int IMG, int BN>
+template <int MODE, int C, int HW, int IMG, int BN, int D>
+__global__ __launch_bounds__(256) void k_conv_halo(ConvArgs a) {
+  using Body = HaloBody<MODE, C, HW, IMG, BN, D>;
+  __shared__ __attribute__((aligned(16))) char smem[Body::SMEM];
+  Body::run(a, xcd_blk(), smem);
+}
+
+template <int MODE, int C, int HW, int IMG, int BN>
 int launch_halo(const ConvArgs& a, hipStream_t s) {
-  using P = HaloFwd<C, HW, IMG, BN, 1>;
+  using P = HaloBody<MODE, C, HW, IMG, BN, 1>;
   constexpr int D = P::NR >= 4 ? 4 : (P::NR == 2 ? 8 : 12);
   dim3 grid(a.N / BN, (a.M + P::BM - 1) / P::BM, 1);
-  hipLaunchKernelGGL((k_conv_halo<C, HW, IMG, BN, D>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_conv_halo<MODE, C, HW, IMG, BN, D>), grid, dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();
 }
 
@@ -1374,14 +1407,22 @@ bool halo_shape_ok(int H, int W, int C, int K, int KH, int KW, int sh, int sw, i
          bm % (H * W) == 0;
 }
 
+// FWD: a.C = patch channels (Cin), N = Cout.  DGRAD: a.K = patch channels (Cout), N = Cin.
+template <int MODE>
 int dispatch_halo(const ConvArgs& a, int bm, int bn, hipStream_t s) {
+  const int cp = MODE == FWD ? a.C : a.K;
 #define KML_H(Cv, HWv, BMv, BNv)                                                   \
-  if (a.C == Cv && a.H == HWv && bm == BMv && bn == BNv)                           \
-    return launch_halo<Cv, HWv, BMv / (HWv * HWv), BNv>(a, s);
-  KML_H(64, 8, 64, 64) KML_H(64, 8, 128, 64) KML_H(64, 8, 64, 32)
-  KML_H(128, 4, 64, 32) KML_H(128, 4, 64, 64) KML_H(128, 4, 128, 32) KML_H(128, 4, 64, 128) KML_H(128, 4, 128, 64)
-  KML_H(256, 4, 64, 32) KML_H(256, 4, 64, 64) KML_H(256, 8, 64, 32) KML_H(256, 8, 64, 64)
-  KML_H(512, 4, 64, 32) KML_H(512, 4, 64, 64)
+  if (cp == Cv && a.H == HWv && bm == BMv && bn == BNv)                            \
+    return launch_halo<MODE, Cv, HWv, BMv / (HWv * HWv), BNv>(a, s);
+  if constexpr (MODE == FWD) {
+    KML_H(64, 8, 64, 64) KML_H(64, 8, 128, 64) KML_H(64, 8, 64, 32)
+    KML_H(128, 4, 64, 32) KML_H(128, 4, 64, 64) KML_H(128, 4, 128, 32) KML_H(128, 4, 64, 128) KML_H(128, 4, 128, 64)
+    KML_H(256, 4, 64, 32) KML_H(256, 4, 64, 64) KML_H(256, 8, 64, 32) KML_H(256, 8, 64, 64)
+    KML_H(512, 4, 64, 32) KML_H(512, 4, 64, 64)
+  } else {
+    KML_H(64, 8, 64, 32) KML_H(64, 8, 64, 64) KML_H(64, 8, 128, 64)
+    KML_H(128, 4, 64, 32)
+  }
 #undef KML_H
   return (int)hipErrorInvalidValue;
 }
@@ -1506,7 +1547,14 @@ using DgDi3216 = DirectBody<DGRAD, 2, 1, 4, 4>;
 using DgDi6432 = DirectBody<DGRAD, 4, 2, 4, 2>;
 using WgIg3232 = IgemmBody<WGRAD, 32, 32, 64, true>;
 using WgIg6432 = IgemmBody<WGRAD, 64, 32, 64, true>;
+// halo dgrad bodies (variant 4): the plan's bk slot carries Cout * 16 + H (the body's geometry)
+using DgHa64x8 = HaloBody<DGRAD, 64, 8, 1, 32, 1>;
+using DgHa128x4 = HaloBody<DGRAD, 128, 4, 4, 32, 1>;
 #define KML_PAIR_LIST(X)                                   \
+  X(4, 64, 32, 1032, DgHa64x8, 64, 32, WgIg3232, 32, 32)   \
+  X(4, 64, 32, 1032, DgHa64x8, 64, 32, WgIg6432, 64, 32)   \
+  X(4, 64, 32, 2052, DgHa128x4, 64, 32, WgIg3232, 32, 32)  \
+  X(4, 64, 32, 2052, DgHa128x4, 64, 32, WgIg6432, 64, 32)  \
   X(0, 32, 64, 64, DgIg3264, 32, 64, WgIg3232, 32, 32)     \
   X(0, 32, 64, 64, DgIg3264, 32, 64, WgIg6432, 64, 32)     \
   X(0, 32, 32, 64, DgIg3232, 32, 32, WgIg3232, 32, 32)     \
@@ -1715,7 +1763,7 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     a.M = B * a.OH * a.OW; a.N = K; a.Kd = 9 * C;
     a.splits = 1; a.kchunk = a.Kd;
     if (!a.zp) return (int)hipErrorInvalidSymbol;
-    return dispatch_halo(a, bm, bn, s);
+    return dispatch_halo<FWD>(a, bm, bn, s);
   }
   if (variant) bk = 64;
   ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
@@ -1807,6 +1855,9 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                               int waccumulate, float* wbias, int wbias_acc, int g22, hipStream_t s) {
   const int which = pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
   if (!which) return (int)hipErrorInvalidValue;
+  if (dvariant == 4 && (g22 || fold_c || dsplits != 1 || dbk != K * 16 + H ||
+                        !halo_shape_ok(H, W, K, C, KH, KW, sh, sw, ph, pw, dbm, dbn)))
+    return (int)hipErrorInvalidValue;
   ConvArgs ad, aw;
   int e = prep_dgrad(ad, dy, w, wt, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
                      grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
@@ -1878,6 +1929,11 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
                            fold_c, bnf_mask_out, g22);
   if (e) return e;
   if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
+  if (variant == 4) {  // halo patch of dy (Cout channels), flipped-filter slice of Cin columns
+    if (g22 || fold_c || a.splits != 1 || !halo_shape_ok(H, W, K, C, KH, KW, sh, sw, ph, pw, bm, bn))
+      return (int)hipErrorInvalidValue;
+    return dispatch_halo<DGRAD>(a, bm, bn, s);
+  }
   if (variant) bk = 64;
   return dispatch<DGRAD>(a, bm, bn, bk, variant, s);
 }

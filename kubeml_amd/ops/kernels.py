@@ -418,6 +418,28 @@ def halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
             (bm, bn) in _HALO_TILES.get((C, H), ()) and K % bn == 0)
 
 
+# dgrad halo tiles, keyed by (Cout = the dy patch's channels, H): (bm, bn) with bn over Cin
+_HALO_DG_TILES = {(64, 8): [(64, 32), (64, 64), (128, 64)], (128, 4): [(64, 32)]}
+_HALO_DG_ON = os.environ.get("KUBEML_DGRAD_HALO", "0") == "1"   # opt-in: measured slower in the step (profiles/r3/halo_dgrad.md)
+
+
+def halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
+    """Is (bm, bn) an instantiated halo dgrad tile for this conv (C = Cin, K = Cout)?"""
+    return ((KH, KW) == (3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1) and H == W and
+            (bm, bn) in _HALO_DG_TILES.get((K, H), ()) and C % bn == 0)
+
+
+def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
+    """Default halo-patch dgrad plan (patch of dy, flipped-filter weight slice in LDS) for an
+    eligible conv, or None (``KUBEML_DGRAD_HALO=0``)."""
+    if not _HALO_DG_ON:
+        return None
+    for bm, bn in _HALO_DG_TILES.get((K, H), ()):
+        if halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn):
+            return (bm, bn, K * 16 + H, 1, HALO)   # bk slot: the body's geometry (grouped pairs)
+    return None
+
+
 def halo_plan(C, K, H, W, KH, KW, stride, pad):
     """Default halo-patch plan for an eligible forward conv, or None (``KUBEML_CONV_HALO=0``
     disables it; ``KUBEML_HALO_TILE=bm,bn`` picks another instantiated tile)."""
@@ -496,11 +518,16 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M = B * H * W
     ntap = (r1 - r0) * (s1 - s0)
-    bm, bn, bk, splits, variant = _norm_cfg(cfg or plan_conv("dgrad", M, C, ntap * K))
+    hp = None if (cfg is not None or _g22) else halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad)
+    bm, bn, bk, splits, variant = _norm_cfg(cfg or hp or plan_conv("dgrad", M, C, ntap * K))
+    if variant == HALO and (_g22 or not halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn)):
+        bm, bn, bk, splits, variant = _norm_cfg(plan_conv("dgrad", M, C, ntap * K))
     plan = (bm, bn, bk, splits, variant)
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan, _fold)
     slab = cnt = None
-    if variant == DIRECT:
+    if variant == HALO:
+        wt, splits, bk = None, 1, 0
+    elif variant == DIRECT:
         if _g22:
             raise ValueError("the direct dgrad variant needs a materialised unrolled weight (not GATHER22)")
         # k-contiguous transposed weight copy, then the LDS-free kernel (bk = wave count)
@@ -569,6 +596,9 @@ def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None, unroll=Fal
     ntap = (r1 - r0) * (s1 - s0)
     if dcfg is None and wcfg is None:
         dcfg, wcfg = _TUNED_PAIR.get((B * H * W, C, ntap * K, K, ntap * C, B * OH * OW), (None, None))
+        hp = halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad)
+        if hp is not None:
+            dcfg = hp
     dplan = _norm_cfg(dcfg or plan_conv("dgrad", B * H * W, C, ntap * K))
     wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
     return dplan, wplan, _PAIR_ON and conv_pair_supported(dplan, wplan)
@@ -650,7 +680,9 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         assert addend.shape == out.shape
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan, fold)
     slab = cnt = None
-    if variant == DIRECT:
+    if variant == HALO:
+        wt, dsplits = None, 1
+    elif variant == DIRECT:
         if g22:
             raise ValueError("the direct dgrad variant needs a materialised unrolled weight (not GATHER22)")
         wt = _direct_wt(w, wt)

@@ -399,6 +399,48 @@ def test_conv_halo_variant(case):
         assert _rel(rows[0], yf.sum((0, 2, 3))) < 2e-2 and _rel(rows[1], (yf * yf).sum((0, 2, 3))) < 2e-2
 
 
+@pytest.mark.parametrize("case", [(4, 8, 64, 64), (3, 8, 128, 64), (6, 4, 128, 128), (5, 4, 256, 128)])
+def test_conv_halo_dgrad(case):
+    """Halo-patch dgrad (variant 4: padded dy patch in LDS, flipped-filter weight slice read
+    with transposing LDS reads): dx (+ residual addend) vs fp32 torch, and the consumer-BN
+    fusion (masked dz + dgamma/dbeta partial rows) vs the implicit-GEMM plan."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co = case
+    torch.manual_seed(12)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * (1.0 / (9 * Ci) ** 0.5))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1)
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    add = _bf(torch.randn(B, H, H, Ci, device=dev))
+    # the step's grouped backward (halo dgrad + wgrad in one launch when instantiated)
+    dplan, wplan, grouped = K.bwd_plans(x.shape, Co, 3, 3, (1, 1), (1, 1))
+    assert dplan[4] == K.HALO
+    dw = torch.full((Co, 3, 3, Ci), float("nan"), device=dev)
+    dx = K.conv_bwd(dyn, w, x, dw, 3, 3, (1, 1), (1, 1), addend=add, accumulate=False)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2, grouped
+    assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < 1e-2, grouped
+    c = _bf(torch.randn(B, H, H, Ci, device=dev))
+    yb = _bf(torch.randn(B, H, H, Ci, device=dev))
+    mean, rstd = torch.randn(Ci, device=dev) * 0.1, torch.rand(Ci, device=dev) + 0.5
+    tiles = [t for t in K._HALO_DG_TILES[(Co, H)] if Ci % t[1] == 0]
+    assert tiles and K.halo_dgrad_plan(Ci, Co, H, H, 3, 3, (1, 1), (1, 1)) is not None
+    base = K.plan_conv("dgrad", B * H * H, Ci, 9 * Co)
+    r_ref = K.conv_dgrad(dyn, w, x.shape, 3, 3, (1, 1), (1, 1), cfg=base, bnf=(yb, c, mean, rstd), bnf_mask=True)
+    for bm, bn in tiles:
+        cfg = (bm, bn, 0, 1, K.HALO)
+        dx = K.conv_dgrad(dyn, w, x.shape, 3, 3, (1, 1), (1, 1), addend=add, cfg=cfg)
+        assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2, (bm, bn)
+        r = K.conv_dgrad(dyn, w, x.shape, 3, 3, (1, 1), (1, 1), cfg=cfg, bnf=(yb, c, mean, rstd), bnf_mask=True)
+        assert _rel(r[0], r_ref[0]) < 1e-2, (bm, bn)
+        (p1, g1), (p0, g0) = r[1], r_ref[1]
+        assert g1 == -(-B * H * H // bm)
+        assert _rel(p1.view(g1, 2 * Ci).sum(0), p0.view(g0, 2 * Ci).sum(0)) < 2e-2, (bm, bn)
+
+
 @pytest.mark.parametrize("cfg", [(32, 32, 64, 1, 0), (64, 32, 64, 2, 1), (128, 64, 64, 1, 2), (32, 32, 4, 1, 3),
                                  (64, 64, 32, 4, 0)])
 def test_conv_partial_stats_into_bn_apply(cfg):
