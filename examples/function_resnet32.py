@@ -8,7 +8,6 @@ from torch.optim import SGD
 
 from kubeml import KubeModel
 from kubeml_amd.models.resnet import resnet32
-from kubeml_amd.nn import cross_entropy
 from kubeml_amd.sdk.vision import CIFAR10_MEAN, CIFAR10_STD, ImageDataset, prepare
 
 
@@ -31,7 +30,7 @@ class KubeResnet(KubeModel):
 
     def validate(self, batch, batch_index) -> Tuple[float, float]:
         x, y = prepare(batch, self._dataset, train=False)
-        loss, correct = cross_entropy(self(x), y, return_correct=True)
+        correct, loss = self.evaluate(x, y)  # graph-replayed eval forward on the GPU
         return correct * 100 / self.batch_size, loss
 
     def infer(self, data):

@@ -19,7 +19,6 @@ from torch.optim import SGD
 
 from kubeml import KubeModel
 from kubeml_amd.models.resnet import resnet50
-from kubeml_amd.nn import cross_entropy
 from kubeml_amd.sdk.vision import IMAGENET_MEAN, IMAGENET_STD, ImageDataset, prepare
 
 
@@ -43,7 +42,7 @@ class KubeResnet50(KubeModel):
 
     def validate(self, batch, batch_index) -> Tuple[float, float]:
         x, y = prepare(batch, self._dataset, train=False)
-        loss, correct = cross_entropy(self(x), y, return_correct=True)
+        correct, loss = self.evaluate(x, y)  # graph-replayed eval forward on the GPU
         return correct * 100 / self.batch_size, loss
 
     def infer(self, data):

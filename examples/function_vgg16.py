@@ -9,7 +9,6 @@ from torch.optim import Adam
 
 from kubeml import KubeModel
 from kubeml_amd.models.vgg import vgg16
-from kubeml_amd.nn import cross_entropy
 from kubeml_amd.sdk.vision import ImageDataset, prepare
 
 CIFAR100_MEAN = (0.5070751592371323, 0.48654887331495095, 0.4409178433670343)
@@ -34,7 +33,7 @@ class KubeVGG(KubeModel):
 
     def validate(self, batch, batch_index) -> Tuple[float, float]:
         x, y = prepare(batch, self._dataset, train=False)
-        loss, correct = cross_entropy(self(x), y, return_correct=True)
+        correct, loss = self.evaluate(x, y)  # graph-replayed eval forward on the GPU
         return correct * 100 / self.batch_size, loss
 
     def infer(self, data):

@@ -139,8 +139,13 @@ class KubeDataset(data.Dataset, ABC):
         try:
             st = self._streamers.get(split)
             if st is None:
-                from .loader import SplitStreamer
-                st = SplitStreamer(self._store, self.dataset, split, device)
+                import os
+                from .loader import ResidentSplit, SplitStreamer
+                budget = float(os.environ.get("KUBEML_RESIDENT_MB", "8192")) * 2**20
+                if ResidentSplit.nbytes(self._store, self.dataset, split) <= budget:
+                    st = ResidentSplit(self._store, self.dataset, split, device)   # once per job
+                else:
+                    st = SplitStreamer(self._store, self.dataset, split, device)
                 self._streamers[split] = st
             st.plan(doc_ranges, batch_size)
         except (RuntimeError, TypeError):

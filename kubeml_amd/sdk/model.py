@@ -534,6 +534,46 @@ class KubeModel(ABC):
             self._synced_steps += 1
         return loss
 
+    def evaluate(self, x, y, loss_fn=None):
+        """Eval-mode forward + loss + correct count for one validation batch -> (correct,
+        loss) as device tensors.  On the GPU the first call per batch shape captures the
+        forward into a hipGraph that later calls replay: a validation pass is then one replay
+        per batch instead of ~80 host-issued launches (host-bound at the reference's batch
+        sizes).  Weights and BN running statistics are read in place, so every replay sees
+        the current model."""
+        from ..nn import cross_entropy
+        loss_fn = loss_fn or cross_entropy
+
+        def fwd(xx, yy):
+            out = self._network(xx)
+            if loss_fn is cross_entropy:
+                return loss_fn(out, yy, return_correct=True)[::-1]
+            loss = loss_fn(out, yy)
+            return (out.argmax(1) == yy).sum(), loss
+
+        if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
+            return fwd(x, y)
+        key = ("eval", tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(loss_fn))
+        g = self._graphs.get(key)
+        if g is None:
+            if len(self._graphs) >= self.MAX_GRAPHS:
+                self._graphs.pop(next(iter(self._graphs)))
+            xs, ys = x.clone(), y.clone()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                fwd(xs, ys)                       # warm-up: plans, workspaces, lazy buffers
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                outs = fwd(xs, ys)
+            g = self._graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
+        g["x"].copy_(x, non_blocking=True)
+        g["y"].copy_(y, non_blocking=True)
+        g["graph"].replay()
+        correct, loss = g["out"]
+        return correct.clone(), loss.clone()
+
     # ---- user hooks (network.py:463-476) --------------------------------------------------
     def configure_optimizers(self) -> torch.optim.Optimizer:
         pass

@@ -130,6 +130,9 @@ def events() -> List[dict]:
         return list(_events)
 
 
+_FLUSHES = 0
+
+
 def flush(directory: Optional[str] = None, clear: bool = True) -> Optional[str]:
     """Write collected events; returns the file path (None if nothing recorded)."""
     try:
@@ -149,7 +152,10 @@ def flush(directory: Optional[str] = None, clear: bool = True) -> Optional[str]:
     meta = [{"name": "process_name", "ph": "M", "pid": os.getpid(), "args": {"name": name}}]
     meta += [{"name": "thread_name", "ph": "M", "pid": os.getpid(), "tid": tid, "args": {"name": tr}}
              for tr, tid in _TRACKS.items()]
-    path = os.path.join(directory, f"{name}-pid{os.getpid()}.json")
+    # one file per flush (workers flush after every task): earlier tasks' spans are kept
+    global _FLUSHES
+    _FLUSHES += 1
+    path = os.path.join(directory, f"{name}-pid{os.getpid()}-{_FLUSHES:04d}.json")
     with open(path, "w") as f:
         json.dump({"traceEvents": meta + evs, "displayTimeUnit": "ms"}, f)
     return path

@@ -49,3 +49,29 @@ def test_stream_matches_load_docs(tmp_path):
     s.plan([(2, 3)], 64)
     xb, yb = s.next()
     assert np.array_equal(xb.cpu().numpy(), x[128:192])
+
+
+@pytest.mark.parametrize("budget_mb", ["8192", "0"])
+def test_dataset_resident_or_streamed_matches_load_docs(tmp_path, monkeypatch, budget_mb):
+    """KubeDataset's GPU path: a split within KUBEML_RESIDENT_MB is uploaded once and served
+    as views (ResidentSplit); a larger one streams through pinned memory (SplitStreamer).
+    Both hand out byte-exact batches in plan order."""
+    from kubeml_amd.sdk.loader import ResidentSplit, SplitStreamer
+    st, x, y = _store(tmp_path)
+    monkeypatch.setenv("KUBEML_RESIDENT_MB", budget_mb)
+
+    class DS:
+        from kubeml_amd.sdk.dataset import KubeDataset as _K
+        _plan_stream = _K._plan_stream
+        _stream_ok = lambda self, d: True
+
+    ds = DS()
+    ds._store, ds.dataset, ds._streamers = st, "ds", {}
+    assert ds._plan_stream("train", [(0, 3), (3, 16)], 128, dev)
+    s = ds._streamers["train"]
+    assert isinstance(s, ResidentSplit if budget_mb != "0" else SplitStreamer)
+    ref_x, ref_y = st.load_docs("ds", "train", 0, 3)
+    xb, yb = s.next()
+    assert np.array_equal(xb.cpu().numpy(), ref_x[:128]) and np.array_equal(yb.cpu().numpy(), ref_y[:128])
+    xb, yb = s.next()
+    assert np.array_equal(xb.cpu().numpy(), ref_x[128:192])     # round boundary: ragged batch

@@ -161,3 +161,20 @@ def test_native_merger_sum():
     xs = [torch.randn(300000) for _ in range(3)]
     got = _native_reduce(xs, "sum")
     assert torch.allclose(got, xs[0] + xs[1] + xs[2], atol=1e-5)
+
+
+def test_evaluate_eager_matches_manual():
+    """KubeModel.evaluate on a CPU worker: eager eval forward -> (correct count, mean CE loss)."""
+    import types
+    import torch
+    import torch.nn.functional as F
+    from kubeml_amd.sdk.model import KubeModel
+    torch.manual_seed(0)
+    net = torch.nn.Linear(12, 5)
+    stub = types.SimpleNamespace(device=torch.device("cpu"), _network=net, _graphs={}, MAX_GRAPHS=8)
+    x, y = torch.randn(9, 12), torch.randint(0, 5, (9,))
+    with torch.no_grad():
+        correct, loss = KubeModel.evaluate(stub, x, y)
+        out = net(x)
+    assert int(correct) == int((out.argmax(1) == y).sum())
+    assert abs(float(loss) - float(F.cross_entropy(out, y))) < 1e-5
