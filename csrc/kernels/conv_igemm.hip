@@ -1427,6 +1427,127 @@ int dispatch_halo(const ConvArgs& a, int bm, int bn, hipStream_t s) {
   return (int)hipErrorInvalidValue;
 }
 
+// =====================================================================================
+// Variant 5: one-shot panels for single-tap forward GEMMs with a short K (1x1-form convs:
+// ResNet-34's unrolled 2x2-map layer3 convs, K = 4C = 1024, and layer4's centre-tap convs
+// on 1x1 maps, K = 512).  The implicit-GEMM pipelines keep 2-3 BK=64 stages in flight per
+// block, so a K = 1024 panel pair is 16 dependent round trips; here every byte of the block's
+// A (BM x K) and B (BN x K) panels is requested at once by LDS-DMA (global_load_lds, no VGPR
+// staging; the chunk swizzle is applied on the per-lane SOURCE address because the DMA image
+// is lane-linear), one wait, one barrier, then the MFMA loop runs out of LDS.  Rows are
+// 2K-byte pitched, so the swizzle is chunk ^ (row & 15) (conflict-free ds_read_b128 over a
+// fragment's 16 rows x 4 chunks).  The unrolled convs' B rows are gathered from the 3x3
+// weight (g22) per 16-byte chunk.
+// =====================================================================================
+template <int BM, int BN, int KD>
+struct OneShotBody {
+  static constexpr int CPR = KD / 8;                    // 16-byte chunks per panel row
+  static constexpr int A_BYTES = BM * KD * 2, B_BYTES = BN * KD * 2;
+  static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  static constexpr int NIA = BM * CPR / 64, NIB = BN * CPR / 64;  // 1 KiB DMA instructions per panel
+  static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
+  static constexpr int SMEM = A_BYTES + B_BYTES > SMEM_EPI ? A_BYTES + B_BYTES : SMEM_EPI;
+  static constexpr int THREADS = 256;
+  static_assert(CPR % 16 == 0 && NIA % 4 == 0 && NIB % 4 == 0, "one-shot panel shape");
+  static_assert(SMEM <= 160 * 1024, "one-shot panels exceed LDS");
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+    const int m0 = bk.y * BM, n0 = bk.x * BN;
+    const int tapoff = (a.r0 * a.KW + a.s0) * a.C;
+#pragma unroll
+    for (int j = 0; j < NIA / 4; ++j) {
+      const int u = j * 4 + wave;
+      const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
+      const int m = m0 + row;
+      const bf16_t* src = m < a.M ? a.x + (long long)m * a.C + lc * 8 : a.zp;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(smem + u * 1024),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NIB / 4; ++j) {
+      const int u = j * 4 + wave;
+      const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
+      const int n = n0 + row, k = lc * 8;
+      const bf16_t* src = a.zp;
+      if (n < a.N) {
+        if (a.g22) {  // W'[(p, n')][(q, c)] = w[n'][tap(p, q)][c]
+          const int p = fdiv(n, a.fd_gK), q = fdiv(k, a.fd_gC);
+          src = a.w + ((long long)(n - p * a.fd_gK.d) * 9 + tap22(p, q)) * a.fd_gC.d + (k - q * a.fd_gC.d);
+        } else {
+          src = a.w + (long long)n * a.KH * a.KW * a.C + tapoff + k;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(smem + A_BYTES + u * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* sA = smem;
+    const char* sB = smem + A_BYTES;
+    auto rd = [&](const char* base, int row, int ks) {
+      const int c = 4 * ks + (lane >> 4);
+      return *reinterpret_cast<const bf16x8_t*>(base + (row * CPR + (c ^ (row & 15))) * 16);
+    };
+    f32x4_t acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int KS = KD / 32;
+    bf16x8_t af[2][MR], bf[2][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i) af[0][i] = rd(sA, wm * WM + i * 16 + (lane & 15), 0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) bf[0][j] = rd(sB, wn * WN + j * 16 + (lane & 15), 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i) af[(ks + 1) & 1][i] = rd(sA, wm * WM + i * 16 + (lane & 15), ks + 1);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) bf[(ks + 1) & 1][j] = rd(sB, wn * WN + j * 16 + (lane & 15), ks + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[ks & 1][j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // LDS is reused by the epilogue
+    conv_epilogue<FWD, MR, NR, WM, WN, false, true>(a, acc, m0, n0, wm, wn, lane, tid, 0, 0,
+                                                    reinterpret_cast<unsigned*>(smem));
+  }
+};
+
+template <int BM, int BN, int KD>
+__global__ __launch_bounds__(256) void k_conv_oneshot(ConvArgs a) {
+  using Body = OneShotBody<BM, BN, KD>;
+  __shared__ __attribute__((aligned(1024))) char smem[Body::SMEM];
+  Body::run(a, xcd_blk(), smem);
+}
+
+// single-tap forward whose A rows are contiguous C-element rows: 1x1 maps (centre tap) or
+// a 1x1 / stride-1 / pad-0 conv
+bool oneshot_shape_ok(const ConvArgs& a) {
+  const bool one_tap = (a.r1 - a.r0) == 1 && (a.s1 - a.s0) == 1;
+  const bool rows = (a.H * a.W == 1 && a.OH * a.OW == 1) ||
+                    (a.KH == 1 && a.KW == 1 && a.sh == 1 && a.sw == 1 && a.ph == 0 && a.pw == 0);
+  return one_tap && rows && a.Kd == a.C;
+}
+
+int dispatch_oneshot(const ConvArgs& a, int bm, int bn, hipStream_t s) {
+  dim3 grid((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, 1);
+#define KML_O(BMv, BNv, KDv)                                                          \
+  if (bm == BMv && bn == BNv && a.Kd == KDv) {                                        \
+    hipLaunchKernelGGL((k_conv_oneshot<BMv, BNv, KDv>), grid, dim3(256), 0, s, a);     \
+    KML_LAUNCH_CHECK();                                                               \
+  }
+  KML_O(32, 32, 512) KML_O(32, 32, 1024) KML_O(32, 64, 512) KML_O(64, 32, 512) KML_O(32, 32, 256)
+  KML_O(32, 64, 256) KML_O(64, 64, 256)
+#undef KML_O
+  return (int)hipErrorInvalidValue;
+}
+
 template <int MODE>
 int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
 #define KML_T(BMv, BNv)                                                  \
@@ -1753,6 +1874,18 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     a.splits = 1; a.kchunk = a.Kd;
     if (!a.zp) return (int)hipErrorInvalidSymbol;
     return dispatch_direct<FWD>(a, bm, bn, bk, s);
+  }
+  if (variant == 5) {  // one-shot panels: single-tap, contiguous A rows, short K
+    ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles; a.fold_c = fold_c;
+    set_g22(a, g22, C, K);
+    a.zp = zero_page();
+    a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
+    a.splits = 1; a.kchunk = a.Kd;
+    if (!a.zp) return (int)hipErrorInvalidSymbol;
+    if (!oneshot_shape_ok(a)) return (int)hipErrorInvalidValue;
+    return dispatch_oneshot(a, bm, bn, s);
   }
   if (variant == 4) {  // halo patch: bm = pixels per block (whole images), bn = channels per block
     if (g22 || fold_c || !halo_shape_ok(H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn)) return (int)hipErrorInvalidValue;

@@ -355,8 +355,7 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
         assert bias.numel() >= K
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
-    bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg,
-                                                geom=None if _g22 else (H, W, KH, KW, stride, pad))
+    bm, bn, bk, splits, variant = conv_fwd_plan(C, M, K, Kd, cfg, geom=(H, W, KH, KW, stride, pad))
     rows, grp, gcnt, tpg = stats, None, None, 0
     if stats is not None:
         _chk(stats, F32, "stats")
@@ -373,6 +372,11 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     if variant == HALO:
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, HALO, 0, 0, _p(grp), _p(gcnt), tpg, 0, 0, _s())
+        return out
+    if variant == ONESHOT:
+        HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
+                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, ONESHOT, 0, 0, _p(grp), _p(gcnt), tpg,
+                 int(_fold), int(_g22), _s())
         return out
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
@@ -392,11 +396,13 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
     (H, W, KH, KW, stride, pad) lets an eligible conv take the halo-patch kernel
     (:func:`halo_plan`); without it (or when ineligible) a HALO plan falls back."""
     if cfg is None and geom is not None:
-        hp = halo_plan(C, K, *geom)
+        hp = halo_plan(C, K, *geom) or oneshot_plan(C, K, Kd, *geom)
         if hp is not None:
             return hp
     plan = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
     if plan[4] == HALO and (geom is None or not halo_ok(C, K, *geom, plan[0], plan[1])):
+        plan = _norm_cfg(default_plan("fwd", M, K, Kd))
+    if plan[4] == ONESHOT and (geom is None or not oneshot_ok(C, K, Kd, *geom, plan[0], plan[1])):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == DIRECT and C % 32:
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
@@ -440,6 +446,34 @@ def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
     return None
 
 
+ONESHOT = 5  # cfg variant id of the one-shot panel forward (single-tap convs, K in _ONESHOT_TILES)
+_ONESHOT_TILES = {512: [(32, 32), (32, 64), (64, 32)], 1024: [(32, 32)], 256: [(32, 32), (32, 64), (64, 64)]}
+_ONESHOT_ON = os.environ.get("KUBEML_CONV_ONESHOT", "1") != "0"
+
+
+def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
+    """Single-tap forward with contiguous A rows and an instantiated (bm, bn, Kd) panel pair."""
+    if Kd != C or (bm, bn) not in _ONESHOT_TILES.get(Kd, ()):
+        return False
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    rows = (H * W == 1 and OH * OW == 1) or ((KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0))
+    return (r1 - r0) == 1 and (s1 - s0) == 1 and rows
+
+
+def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad):
+    """Default one-shot panel plan for an eligible forward conv, or None
+    (``KUBEML_CONV_ONESHOT=0`` disables it; ``KUBEML_ONESHOT_TILE=bm,bn`` picks a tile)."""
+    if not _ONESHOT_ON:
+        return None
+    env = os.environ.get("KUBEML_ONESHOT_TILE")
+    cands = ([tuple(int(v) for v in env.split(","))] if env else []) + list(_ONESHOT_TILES.get(Kd, ()))
+    for bm, bn in cands:
+        if oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn):
+            return (bm, bn, 0, 1, ONESHOT)
+    return None
+
+
 def halo_plan(C, K, H, W, KH, KW, stride, pad):
     """Default halo-patch plan for an eligible forward conv, or None (``KUBEML_CONV_HALO=0``
     disables it; ``KUBEML_HALO_TILE=bm,bn`` picks another instantiated tile)."""
@@ -461,7 +495,7 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False)
     if unroll:
         if not unrolled22(H, W, KH, KW, stride, pad):
             raise ValueError("conv is not unrolled")
-        return 4 * conv_stats_rows(B, conv_fwd_plan(4 * C, B, 4 * K, 4 * C, cfg))
+        return 4 * conv_stats_rows(B, conv_fwd_plan(4 * C, B, 4 * K, 4 * C, cfg, geom=(1, 1, 1, 1, (1, 1), (0, 0))))
     OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C

@@ -400,11 +400,12 @@ def test_conv_halo_variant(case):
 
 
 @pytest.mark.parametrize("case", [(4, 8, 64, 64), (3, 8, 128, 64), (6, 4, 128, 128), (5, 4, 256, 128)])
-def test_conv_halo_dgrad(case):
+def test_conv_halo_dgrad(case, monkeypatch):
     """Halo-patch dgrad (variant 4: padded dy patch in LDS, flipped-filter weight slice read
     with transposing LDS reads): dx (+ residual addend) vs fp32 torch, and the consumer-BN
     fusion (masked dz + dgamma/dbeta partial rows) vs the implicit-GEMM plan."""
     from kubeml_amd.ops import kernels as K
+    monkeypatch.setattr(K, "_HALO_DG_ON", True)      # opt-in in the step (profiles/r3/halo_dgrad.md)
     B, H, Ci, Co = case
     torch.manual_seed(12)
     x = _bf(torch.randn(B, H, H, Ci, device=dev))
@@ -916,3 +917,53 @@ def test_gathered_unrolled_weight_matches_materialised(B, C, Kc):
         e1 = K.conv_bwd(dy, w, x, g1, *args, wu=wu)
         e2 = K.conv_bwd(dy, w, x, g2, *args, wu=K.GATHER22)
         assert torch.equal(e1, e2) and torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("shape", [(40, 1, 1, 512, 512, 3, 1, 1), (37, 1, 1, 512, 96, 1, 1, 0),
+                                   (30, 2, 2, 256, 256, 1, 1, 0), (33, 1, 1, 256, 64, 1, 1, 0)])
+def test_conv_oneshot_variant(shape):
+    """One-shot panel forward (variant 5, LDS-DMA of the whole K panels): single-tap convs
+    (centre tap on 1x1 maps, 1x1/s1) vs fp32 torch, with bias/ReLU/atomic statistics and the
+    per-M-tile partial rows; M and N tails included."""
+    from kubeml_amd.ops import kernels as K
+    B, H, W, Ci, Co, k, s, p = shape
+    torch.manual_seed(13)
+    x = _bf(torch.randn(B, H, W, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * (1.0 / Ci ** 0.5))
+    bias = torch.randn(Co, device=dev)
+    pre = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, stride=s, padding=p)
+    tiles = [t for t in K._ONESHOT_TILES[Ci]]
+    assert K.oneshot_plan(Ci, Co, Ci, H, W, k, k, (s, s), (p, p)) is not None
+    for bm, bn in tiles:
+        cfg = (bm, bn, 0, 1, K.ONESHOT)
+        st = torch.zeros(2 * Co, device=dev)
+        y = K.conv_fwd(x, w, k, k, (s, s), (p, p), bias=bias, stats=st, relu=True, cfg=cfg)
+        yr = F.relu(pre)
+        assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2, (bm, bn)
+        assert _rel(st[:Co], yr.sum((0, 2, 3))) < 2e-2, (bm, bn)
+        G = K.conv_fwd_stats_rows(x.shape, Co, k, k, (s, s), (p, p), cfg=cfg)
+        buf = torch.full((G * 2 * Co + 256,), float("nan"), device=dev)
+        y2 = K.conv_fwd(x, w, k, k, (s, s), (p, p), stats=buf[:G * 2 * Co], stats_part=True, cfg=cfg)
+        assert torch.isnan(buf[G * 2 * Co:]).all() and not torch.isnan(buf[:G * 2 * Co]).any()
+        yf = pre - bias.view(1, -1, 1, 1)
+        assert _rel(y2.permute(0, 3, 1, 2), yf) < 1e-2
+        assert _rel(buf[:G * 2 * Co].view(G, 2, Co).sum(0)[0], yf.sum((0, 2, 3))) < 2e-2
+
+
+def test_conv_oneshot_unrolled_gather():
+    """Unrolled 2x2-map conv (1x1 form, K = 4C = 1024) on the one-shot kernel with the B rows
+    gathered from the 3x3 weight (GATHER22): equals the 3x3 conv, folded statistics included."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(14)
+    B, C, Co = 24, 256, 256
+    x = _bf(torch.randn(B, 2, 2, C, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5))
+    args = (3, 3, (1, 1), (1, 1))
+    assert K.conv_fwd_plan(4 * C, B, 4 * Co, 4 * C, geom=(1, 1, 1, 1, (1, 1), (0, 0)))[4] == K.ONESHOT
+    G = K.conv_fwd_stats_rows(x.shape, Co, *args, unroll=True)
+    st = torch.empty(G * 2 * Co, device=dev)
+    y = K.conv_fwd(x, w, *args, stats=st, stats_part=True, wu=K.GATHER22)
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    rows = st.view(G, 2, Co).sum(0)
+    assert _rel(rows[0], yr.sum((0, 2, 3))) < 2e-2 and _rel(rows[1], (yr * yr).sum((0, 2, 3))) < 2e-2

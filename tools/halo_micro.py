@@ -19,6 +19,7 @@ from conv_micro import gtime
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--oneshot", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda")
     B = a.batch
@@ -40,5 +41,30 @@ def main():
               flush=True)
 
 
+
+
+def oneshot_main():
+    """One-shot panel kernel (variant 5) vs the tuned plan: layer3's unrolled 2x2 convs
+    (1x1 form, weight gathered from the 3x3 weight) and layer4's centre-tap convs."""
+    dev = torch.device("cuda")
+    B = 256
+    for name, (H, C, Co, unroll) in {"layer3_unrolled": (2, 256, 256, True), "layer4": (1, 512, 512, False)}.items():
+        x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, 3, 3, C, device=dev) * 0.05).to(torch.bfloat16)
+        M, N, Kd = (B, 4 * Co, 4 * C) if unroll else (B, Co, C)
+        base = K.plan_conv("fwd", M, N, Kd)
+        rows = {}
+        for cfg in [base] + [(bm, bn, 0, 1, K.ONESHOT) for bm, bn in K._ONESHOT_TILES[Kd]]:
+            G = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, (1, 1), (1, 1), cfg=cfg, unroll=unroll)
+            st = torch.empty(G * 2 * Co, device=dev)
+            kw = dict(wu=K.GATHER22) if unroll else {}
+            t = gtime(lambda: K.conv_fwd(x, w, 3, 3, (1, 1), (1, 1), stats=st, stats_part=True, cfg=cfg, **kw))
+            rows[str(tuple(cfg))] = round(t, 2)
+        print(json.dumps({"layer": name, "M": M, "N": N, "K": Kd, "us": rows}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--oneshot" in sys.argv:
+        oneshot_main()
+    else:
+        main()
