@@ -1519,6 +1519,145 @@ struct OneShotBody {
   }
 };
 
+// One-shot backward bodies for the same single-tap convs.  K-strided operands (the dgrad
+// weight W'[k][c] read along k for a fixed c; both wgrad operands, read along the pixel axis)
+// are staged as [K rows][R cols] tiles with the K-strided XOR swizzle (swz_ks, applied on the
+// DMA source address) and read with ds_read_b64_tr_b16 (frag_kstrided).
+//   DGRAD: dX[m][c] = sum_k dY[m][k] W'[k][c]   (A = dY rows, K = Cout)
+//   WGRAD: dW'[k][c] = sum_m dY[m][k] X[m][c]   (K = pixels; both panels K-strided)
+template <int MODE, int BM, int BN, int KD>
+struct OneShotBwdBody {
+  static_assert(MODE == DGRAD || MODE == WGRAD, "one-shot backward: dgrad / wgrad");
+  static constexpr bool A_KC = MODE == DGRAD;             // A K-contiguous (dY rows) or K-strided
+  static constexpr int A_BYTES = BM * KD * 2, B_BYTES = BN * KD * 2;
+  static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  static constexpr int NIA = A_BYTES / 1024, NIB = B_BYTES / 1024;
+  static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
+  static constexpr int SMEM = A_BYTES + B_BYTES > SMEM_EPI ? A_BYTES + B_BYTES : SMEM_EPI;
+  static constexpr int THREADS = 256;
+  static_assert(NIA % 4 == 0 && NIB % 4 == 0 && (KD / 8) % 16 == 0, "one-shot panel shape");
+  static_assert((BM == 32 || BM == 64) && (BN == 32 || BN == 64), "K-strided tiles of 32 / 64 columns");
+  static_assert(SMEM <= 160 * 1024, "one-shot panels exceed LDS");
+
+  // one 16-byte chunk of a K-strided [KD][R] tile: DMA slot L -> (k row, logical chunk)
+  template <int R>
+  __device__ __forceinline__ static void ks_slot(int L, int& k, int& lc) {
+    k = L / (R / 8);
+    lc = (L % (R / 8)) ^ swz_ks<R>(k);
+  }
+
+  __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+    const int m0 = bk.y * BM, n0 = bk.x * BN;
+    const int tapoff = (a.r0 * a.KW + a.s0) * a.C;
+    char* const sA = smem;
+    char* const sB = smem + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < NIA / 4; ++j) {
+      const int u = j * 4 + wave, L = u * 64 + lane;
+      const bf16_t* src;
+      if constexpr (MODE == DGRAD) {  // dY rows [BM][KD], chunk ^ (row & 15)
+        const int row = L / (KD / 8), lc = (L % (KD / 8)) ^ (row & 15), m = m0 + row;
+        src = m < a.M ? a.dy + (long long)m * a.K + lc * 8 : a.zp;
+      } else {                        // dY as [KD pixels][BM out-channels]
+        int k, lc;
+        ks_slot<BM>(L, k, lc);
+        const int col = m0 + lc * 8;
+        src = (k < a.Kd && col < a.M) ? a.dy + (long long)k * a.K + col : a.zp;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(sA + u * 1024),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NIB / 4; ++j) {
+      const int u = j * 4 + wave, L = u * 64 + lane;
+      int k, lc;
+      ks_slot<BN>(L, k, lc);
+      const int col = n0 + lc * 8;
+      const bf16_t* src = a.zp;
+      if constexpr (MODE == DGRAD) {  // W'[k][col]: k = output channel, col = input channel
+        if (k < a.K && col < a.N) {
+          if (a.g22) {
+            const int p = fdiv(k, a.fd_gK), q = fdiv(col, a.fd_gC);
+            src = a.w + ((long long)(k - p * a.fd_gK.d) * 9 + tap22(p, q)) * a.fd_gC.d + (col - q * a.fd_gC.d);
+          } else {
+            src = a.w + (long long)k * a.KH * a.KW * a.C + tapoff + col;
+          }
+        }
+      } else {                        // X as [KD pixels][BN in-channels]
+        if (k < a.Kd && col < a.N) src = a.x + (long long)k * a.C + col;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(sB + u * 1024),
+                                       16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    auto rdA = [&](int i, int ks) -> bf16x8_t {
+      if constexpr (A_KC) {
+        const int row = wm * WM + i * 16 + (lane & 15), c = 4 * ks + (lane >> 4);
+        return *reinterpret_cast<const bf16x8_t*>(sA + (row * (KD / 8) + (c ^ (row & 15))) * 16);
+      } else {
+        return frag_kstrided<BM>(reinterpret_cast<const bf16_t*>(sA), wm * WM + i * 16, ks, lane);
+      }
+    };
+    auto rdB = [&](int j, int ks) -> bf16x8_t {
+      return frag_kstrided<BN>(reinterpret_cast<const bf16_t*>(sB), wn * WN + j * 16, ks, lane);
+    };
+    f32x4_t acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int KS = KD / 32;
+    bf16x8_t af[2][MR], bf[2][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i) af[0][i] = rdA(i, 0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) bf[0][j] = rdB(j, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i) af[(ks + 1) & 1][i] = rdA(i, ks + 1);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) bf[(ks + 1) & 1][j] = rdB(j, ks + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[ks & 1][j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // LDS is reused by the epilogue
+    conv_epilogue<MODE, MR, NR, WM, WN, false, true>(a, acc, m0, n0, wm, wn, lane, tid, 0, 0,
+                                                     reinterpret_cast<unsigned*>(smem));
+  }
+};
+
+template <int MODE, int BM, int BN, int KD>
+__global__ __launch_bounds__(256) void k_conv_oneshot_bwd(ConvArgs a) {
+  using Body = OneShotBwdBody<MODE, BM, BN, KD>;
+  __shared__ __attribute__((aligned(1024))) char smem[Body::SMEM];
+  Body::run(a, xcd_blk(), smem);
+}
+
+template <int MODE>
+int dispatch_oneshot_bwd(const ConvArgs& a, int bm, int bn, hipStream_t s) {
+  dim3 grid((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, 1);
+#define KML_OB(BMv, BNv, KDv)                                                              \
+  if (bm == BMv && bn == BNv && a.Kd == KDv) {                                             \
+    hipLaunchKernelGGL((k_conv_oneshot_bwd<MODE, BMv, BNv, KDv>), grid, dim3(256), 0, s, a); \
+    KML_LAUNCH_CHECK();                                                                    \
+  }
+  if constexpr (MODE == DGRAD) {
+    KML_OB(32, 32, 1024) KML_OB(32, 32, 512) KML_OB(32, 64, 512)
+  } else {
+    KML_OB(32, 32, 256) KML_OB(64, 32, 256) KML_OB(32, 64, 256) KML_OB(64, 64, 256)
+  }
+#undef KML_OB
+  return (int)hipErrorInvalidValue;
+}
+
 template <int BM, int BN, int KD>
 __global__ __launch_bounds__(256) void k_conv_oneshot(ConvArgs a) {
   using Body = OneShotBody<BM, BN, KD>;
@@ -2062,6 +2201,13 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
                            fold_c, bnf_mask_out, g22);
   if (e) return e;
   if (variant == 3) return dispatch_direct<DGRAD>(a, bm, bn, bk, s);
+  if (variant == 5) {  // one-shot panels (single tap, contiguous dY rows, K = Cout)
+    const bool one_tap = (a.r1 - a.r0) == 1 && (a.s1 - a.s0) == 1;
+    const bool rows = (H * W == 1 && a.OH * a.OW == 1) || (KH == 1 && KW == 1 && sh == 1 && sw == 1 && !ph && !pw);
+    if (!one_tap || !rows || a.splits != 1) return (int)hipErrorInvalidValue;
+    a.Kd = K;
+    return dispatch_oneshot_bwd<DGRAD>(a, bm, bn, s);
+  }
   if (variant == 4) {  // halo patch of dy (Cout channels), flipped-filter slice of Cin columns
     if (g22 || fold_c || a.splits != 1 || !halo_shape_ok(H, W, K, C, KH, KW, sh, sw, ph, pw, bm, bn))
       return (int)hipErrorInvalidValue;
@@ -2086,6 +2232,12 @@ KML_API int kml_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, int B, 
   const int e = prep_wgrad(a, x, dy, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, splits, variant, accumulate,
                            slab, counters, dbias, bias_acc);
   if (e) return e;
+  if (variant == 5) {  // one-shot panels: single tap, K = pixels, no split-K, no bias column
+    const bool one_tap = (a.r1 - a.r0) == 1 && (a.s1 - a.s0) == 1;
+    const bool rows = (H * W == 1 && a.OH * a.OW == 1) || (KH == 1 && KW == 1 && sh == 1 && sw == 1 && !ph && !pw);
+    if (!one_tap || !rows || dbias || a.splits != 1) return (int)hipErrorInvalidValue;
+    return dispatch_oneshot_bwd<WGRAD>(a, bm, bn, s);
+  }
   if (variant) bk = 64;
   return dispatch<WGRAD>(a, bm, bn, bk, variant, s);
 }

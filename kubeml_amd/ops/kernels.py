@@ -474,6 +474,28 @@ def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad):
     return None
 
 
+# opt-in: as two launches the one-shot dgrad + wgrad lose to the grouped implicit-GEMM pair
+# (1.376 vs 1.353 ms/step, profiles/r3/oneshot.md)
+_ONESHOT_BWD_ON = os.environ.get("KUBEML_BWD_ONESHOT", "0") == "1"
+_ONESHOT_DG_TILES = {1024: (32, 32), 512: (32, 32)}   # keyed by the dgrad K (= Cout)
+_ONESHOT_WG_TILES = {256: (32, 32)}                    # keyed by the wgrad K (= pixels)
+
+
+def oneshot_bwd_plans(C, K, B, H, W, KH, KW, stride, pad):
+    """(dgrad plan or None, wgrad plan or None) of the one-shot backward bodies for a
+    single-tap conv with contiguous rows (``KUBEML_BWD_ONESHOT=0`` disables both)."""
+    if not _ONESHOT_BWD_ON or C % 32 or K % 32:
+        return None, None
+    r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
+    rows = (H * W == 1 and OH * OW == 1) or ((KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0))
+    if not ((r1 - r0) == 1 and (s1 - s0) == 1 and rows):
+        return None, None
+    d = _ONESHOT_DG_TILES.get(K)
+    w = _ONESHOT_WG_TILES.get(B * OH * OW)
+    return ((d[0], d[1], 0, 1, ONESHOT) if d else None), ((w[0], w[1], 0, 1, ONESHOT) if w else None)
+
+
 def halo_plan(C, K, H, W, KH, KW, stride, pad):
     """Default halo-patch plan for an eligible forward conv, or None (``KUBEML_CONV_HALO=0``
     disables it; ``KUBEML_HALO_TILE=bm,bn`` picks another instantiated tile)."""
@@ -559,7 +581,7 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     plan = (bm, bn, bk, splits, variant)
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan, _fold)
     slab = cnt = None
-    if variant == HALO:
+    if variant in (HALO, ONESHOT):
         wt, splits, bk = None, 1, 0
     elif variant == DIRECT:
         if _g22:
@@ -633,6 +655,8 @@ def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None, unroll=Fal
         hp = halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad)
         if hp is not None:
             dcfg = hp
+        od, ow = oneshot_bwd_plans(C, K, B, H, W, KH, KW, stride, pad)
+        dcfg, wcfg = od or dcfg, ow or wcfg
     dplan = _norm_cfg(dcfg or plan_conv("dgrad", B * H * W, C, ntap * K))
     wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
     return dplan, wplan, _PAIR_ON and conv_pair_supported(dplan, wplan)
@@ -714,7 +738,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         assert addend.shape == out.shape
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, dplan, fold)
     slab = cnt = None
-    if variant == HALO:
+    if variant in (HALO, ONESHOT):
         wt, dsplits = None, 1
     elif variant == DIRECT:
         if g22:

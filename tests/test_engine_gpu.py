@@ -170,7 +170,8 @@ def test_bench_reports_the_framework_epoch():
     storage upload, `kubeml train` with validation every epoch (experiments/e2e.py)."""
     d = _bench("--steps", "10", "--warmup", "2", "--e2e", "on", timeout=900)
     assert d.get("e2e_error") is None, d.get("e2e_error")
-    assert d["e2e_epoch_time_s"] > 0 and len(d["e2e_epoch_wall_s"]) == 3
+    assert d["e2e_epoch_time_s"] > 0 and len(d["e2e_epoch_wall_s"]) == 4 and d["e2e_warmup_epochs"] == 2
+    assert d["e2e_total_s"] >= sum(d["e2e_epoch_wall_s"]) - 1e-3
     assert d["e2e_train_task_img_s"] > 0 and d["e2e_vs_bench_step_rate"] > 0
 
 

@@ -967,3 +967,38 @@ def test_conv_oneshot_unrolled_gather():
     assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
     rows = st.view(G, 2, Co).sum(0)
     assert _rel(rows[0], yr.sum((0, 2, 3))) < 2e-2 and _rel(rows[1], (yr * yr).sum((0, 2, 3))) < 2e-2
+
+
+@pytest.mark.parametrize("unroll", [False, True])
+def test_conv_oneshot_backward(unroll, monkeypatch):
+    """One-shot dgrad / wgrad bodies (K-strided panels by LDS-DMA, transposing reads) on the
+    batch-256 single-tap convs they are planned for: layer4's centre-tap 3x3 on 1x1 maps and
+    layer3's unrolled 2x2 convs (1x1 form, gathered weight, folded BN partials) vs fp32 torch."""
+    from kubeml_amd.ops import kernels as K
+    monkeypatch.setattr(K, "_ONESHOT_BWD_ON", True)     # opt-in in the step
+    torch.manual_seed(15)
+    B, H, C, Co = (256, 2, 256, 256) if unroll else (256, 1, 512, 512)
+    x = _bf(torch.randn(B, H, H, C, device=dev))
+    w = _bf(torch.randn(Co, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1)
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    add = _bf(torch.randn(B, H, H, C, device=dev))
+    dplan, wplan, _ = K.bwd_plans(x.shape, Co, 3, 3, (1, 1), (1, 1), unroll=unroll)
+    assert dplan[4] == K.ONESHOT and wplan[4] == K.ONESHOT
+    if unroll:
+        dw = torch.full((4 * Co, 1, 1, 4 * C), float("nan"), device=dev)
+        dx = K.conv_bwd(dyn, w, x, dw, 3, 3, (1, 1), (1, 1), addend=add, wu=K.GATHER22)
+        dw3 = torch.zeros(Co, 3, 3, C, device=dev)
+        K.fold22_multi([(dw, dw3, False)])
+    else:
+        dw3 = torch.full((Co, 3, 3, C), float("nan"), device=dev)
+        dx = K.conv_bwd(dyn, w, x, dw3, 3, 3, (1, 1), (1, 1), addend=add, accumulate=False)
+        # on a 1x1 map only the centre tap has a gradient (the others see padding only)
+        dw3 = dw3[:, 1:2, 1:2, :]
+    gref = wr.grad if unroll else wr.grad[:, :, 1:2, 1:2]
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
+    assert _rel(dw3.permute(0, 3, 1, 2), gref) < 1e-2
