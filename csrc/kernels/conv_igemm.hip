@@ -122,6 +122,15 @@ struct ConvArgs {
   // copy per step): K = 4 Kq, C = 4 Cq in the 1x1 form, fd_gK / fd_gC divide by Kq / Cq.
   int g22;
   FastDiv fd_gK, fd_gC;
+  // FWD halo with the INPUT's BatchNorm + ReLU applied while the patch is staged (ibn_rows set):
+  // the producer conv's partial statistics rows [ibn_G][2C] are summed in the prologue (same order
+  // as the BN apply kernel), the interior patch chunks are normalised in registers, and the blocks
+  // of N-tile 0 write the normalised map to ibn_y (the activation the backward keeps)
+  const float* ibn_rows; int ibn_G; long long ibn_M;
+  const float* ibn_gamma; const float* ibn_beta;
+  float* ibn_mean; float* ibn_rstd; float* ibn_rmean; float* ibn_rvar;
+  float ibn_eps, ibn_mom;
+  bf16_t* ibn_y;
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
 };
 
@@ -1218,7 +1227,8 @@ struct HaloBody {
   // than per-fragment row segments); otherwise (FWD only) streamed into registers
   static constexpr bool WLDS = MODE == DGRAD || SMEM_PATCH + SMEM_W <= 128 * 1024;
   static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
-  static constexpr int SMEM_MAIN = SMEM_PATCH + (WLDS ? SMEM_W : 0);
+  static constexpr int SMEM_BN = MODE == FWD ? (4 * C + 4 * 256) * 4 : 0;  // scale, shift, sums, scratch
+  static constexpr int SMEM_MAIN = SMEM_PATCH + (WLDS ? SMEM_W : 0) + SMEM_BN;
   static constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __device__ __forceinline__ static int swz(int pix) {
     const int h = (HW == 8) ? (C == 64 ? pix : pix * 9) : pix * 13;
@@ -1301,6 +1311,88 @@ __device__ __forceinline__ void HaloBody<MODE, C, HW, IMG, BN, D>::run(const Con
           const int cout = row / 9, tap = row - cout * 9;
           const int k = (8 - tap) * C + cout;
           *reinterpret_cast<uint4*>(swt + (k * BN + ((c ^ swz_ks<BN>(k)) << 3)) * 2) = wv[u];
+        }
+      }
+    }
+  }
+  if constexpr (MODE == FWD) {
+    if (a.ibn_rows) {  // the input's BatchNorm (training statistics) + ReLU, applied here
+      float* bsc = reinterpret_cast<float*>(smem + P::SMEM_MAIN - P::SMEM_BN);
+      float* bsf = bsc + C;
+      float* sums = bsf + C;
+      float4* scratch = reinterpret_cast<float4*>(sums + 2 * C);
+      constexpr int Q = 2 * C / 4, S = 256 / Q;  // float4 columns of a row, row slices
+      const int q = tid % Q, sl = tid / Q;
+      float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (sl < S) {  // rows sl, sl + S, ... in order (the BN apply kernel's summation order)
+        const float4* p4 = reinterpret_cast<const float4*>(a.ibn_rows) + q;
+        for (int g = sl; g < a.ibn_G; g += 16 * S) {
+          float4 rv[16];
+#pragma unroll
+          for (int uu = 0; uu < 16; ++uu) rv[uu] = p4[(long long)min(g + uu * S, a.ibn_G - 1) * Q];
+#pragma unroll
+          for (int uu = 0; uu < 16; ++uu) {
+            const bool in = g + uu * S < a.ibn_G;
+            acc4.x += in ? rv[uu].x : 0.f; acc4.y += in ? rv[uu].y : 0.f;
+            acc4.z += in ? rv[uu].z : 0.f; acc4.w += in ? rv[uu].w : 0.f;
+          }
+        }
+      }
+      scratch[tid] = acc4;
+      __syncthreads();
+      if (tid < Q) {
+        float4 t4 = scratch[tid];
+        for (int k = 1; k < S; ++k) {
+          const float4 w4 = scratch[k * Q + tid];
+          t4.x += w4.x; t4.y += w4.y; t4.z += w4.z; t4.w += w4.w;
+        }
+        reinterpret_cast<float4*>(sums)[tid] = t4;
+      }
+      __syncthreads();
+      for (int c = tid; c < C; c += 256) {
+        const float mean = sums[c] / (float)a.ibn_M;
+        const float var = fmaxf(sums[C + c] / (float)a.ibn_M - mean * mean, 0.f);
+        const float rstd = rsqrtf(var + a.ibn_eps);
+        const float g = a.ibn_gamma ? a.ibn_gamma[c] : 1.f, bb = a.ibn_beta ? a.ibn_beta[c] : 0.f;
+        bsc[c] = g * rstd;
+        bsf[c] = bb - mean * g * rstd;
+        if (bk.x == 0 && bk.y == 0) {
+          if (a.ibn_mean) { a.ibn_mean[c] = mean; a.ibn_rstd[c] = rstd; }
+          if (a.ibn_rmean) {
+            const float unb = a.ibn_M > 1 ? var * (float)a.ibn_M / (float)(a.ibn_M - 1) : var;
+            a.ibn_rmean[c] = (1.f - a.ibn_mom) * a.ibn_rmean[c] + a.ibn_mom * mean;
+            a.ibn_rvar[c] = (1.f - a.ibn_mom) * a.ibn_rvar[c] + a.ibn_mom * unb;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int q2 = tid + u * 256;
+        if (q2 < CHUNKS) {
+          const int pix = q2 / CH, ch = q2 - pix * CH;
+          const int im = pix / (HP * HP), rem = pix - im * (HP * HP);
+          const int ih = rem / HP - 1, iw = rem - (rem / HP) * HP - 1;
+          if ((unsigned)ih < (unsigned)HW && (unsigned)iw < (unsigned)HW && img0 + im < a.B) {
+            float f[8];
+            const unsigned* wv32 = reinterpret_cast<const unsigned*>(&v[u]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              f[2 * k] = bf2f((bf16_t)(wv32[k] & 0xffffu));
+              f[2 * k + 1] = bf2f((bf16_t)(wv32[k] >> 16));
+            }
+            unsigned o32[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int c0 = ch * 8 + 2 * k;
+              const float lo = fmaxf(f[2 * k] * bsc[c0] + bsf[c0], 0.f);
+              const float hi = fmaxf(f[2 * k + 1] * bsc[c0 + 1] + bsf[c0 + 1], 0.f);
+              o32[k] = pack_bf2(lo, hi);
+            }
+            v[u] = make_uint4(o32[0], o32[1], o32[2], o32[3]);
+            if (bk.x == 0)
+              *reinterpret_cast<uint4*>(a.ibn_y + (((long long)(img0 + im) * HW + ih) * HW + iw) * C + ch * 8) = v[u];
+          }
         }
       }
     }
@@ -1687,6 +1779,104 @@ int dispatch_oneshot(const ConvArgs& a, int bm, int bn, hipStream_t s) {
   return (int)hipErrorInvalidValue;
 }
 
+// =====================================================================================
+// Variant 6: the ImageNet stem (7x7 / stride 2 / pad 3, Cin padded to 8) as a halo-patch
+// kernel: one block per image stages the zero-padded (HW+6)^2 x 8 patch (one 16-byte chunk per
+// pixel) and the whole 64 x 392 weight (K padded to 416 = 13 K-steps with zero rows) in LDS
+// once; a 32-deep K-step is 4 taps x 8 channels, so each lane's A fragment is ONE patch pixel
+// (tap 4 ks + lane/16 of its output pixel).  The implicit-GEMM pipeline re-read every input
+// pixel once per tap (49x) through LDS.
+// =====================================================================================
+template <int HW>
+struct StemBody {
+  static constexpr int HP = HW + 6, OHW = HW / 2, BM = OHW * OHW, BN = 64;
+  // K padded to 416 (13 K-steps); weight rows pitched at 56 chunks so the chunk ^ (n & 7)
+  // swizzle stays inside the row (chunks 49..55 hold zeros / are never read)
+  static constexpr int KP = 416, KSTEPS = KP / 32, WCH = 56;
+  static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  static constexpr int SMEM_PATCH = HP * HP * 16, SMEM_W = BN * WCH * 16;
+  static constexpr int SMEM_EPI = 16 + 2 * BN * 4;
+  static constexpr int SMEM = SMEM_PATCH + SMEM_W > SMEM_EPI ? SMEM_PATCH + SMEM_W : SMEM_EPI;
+  static_assert(SMEM <= 160 * 1024, "stem patch exceeds LDS");
+};
+
+template <int HW>
+__global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a) {
+  using P = StemBody<HW>;
+  constexpr int HP = P::HP, OHW = P::OHW, MR = P::MR, NR = P::NR;
+  __shared__ __attribute__((aligned(16))) char smem[P::SMEM];
+  char* const swt = smem + P::SMEM_PATCH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int img = (int)blockIdx.x, m0 = img * P::BM;
+  // weights [64][392] -> LDS rows of 56 chunks (chunks 49..55 zero), chunk ^ (n & 7)
+  constexpr int WCHUNKS = P::BN * P::WCH;
+  constexpr int WPER = (WCHUNKS + 255) / 256;
+  uint4 wv[WPER];
+#pragma unroll
+  for (int u = 0; u < WPER; ++u) {
+    const int q = tid + u * 256, n = q / P::WCH, c = q - n * P::WCH;
+    wv[u] = ld16(q < WCHUNKS && c < 49 ? a.w + (long long)n * 392 + c * 8 : a.zp);
+  }
+  constexpr int PCH = HP * HP;
+  constexpr int PER = (PCH + 255) / 256;
+  uint4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = tid + u * 256;
+    const int ih = q / HP - 3, iw = q - (q / HP) * HP - 3;
+    const bool in = q < PCH && (unsigned)ih < (unsigned)HW && (unsigned)iw < (unsigned)HW && img < a.B;
+    v[u] = ld16(in ? a.x + (((long long)img * HW + ih) * HW + iw) * 8 : a.zp);
+  }
+#pragma unroll
+  for (int u = 0; u < WPER; ++u) {
+    const int q = tid + u * 256, n = q / P::WCH, c = q - n * P::WCH;
+    if (q < WCHUNKS) *reinterpret_cast<uint4*>(swt + (n * P::WCH + (c ^ (n & 7))) * 16) = wv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = tid + u * 256;
+    if (q < PCH) *reinterpret_cast<uint4*>(smem + q * 16) = v[u];
+  }
+  __syncthreads();
+  int pbase[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int r = wm * P::WM + i * 16 + (lane & 15);
+    pbase[i] = (2 * (r / OHW)) * HP + 2 * (r % OHW);
+  }
+  int brow[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) brow[j] = wn * P::WN + j * 16 + (lane & 15);
+  auto rd = [&](int ks, bf16x8_t (&af)[MR], bf16x8_t (&bf)[NR]) {
+    const int tap = min(4 * ks + (lane >> 4), 48);  // taps 49..51 meet zero weights
+    const int toff = (tap / 7) * HP + (tap % 7);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(smem + (pbase[i] + toff) * 16);
+    const int wc = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8_t*>(swt + (brow[j] * P::WCH + (wc ^ (brow[j] & 7))) * 16);
+  };
+  f32x4_t acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t af[2][MR], bf[2][NR];
+  rd(0, af[0], bf[0]);
+#pragma unroll
+  for (int ks = 0; ks < P::KSTEPS; ++ks) {
+    if (ks + 1 < P::KSTEPS) rd(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[ks & 1][j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  conv_epilogue<FWD, MR, NR, P::WM, P::WN>(a, acc, m0, 0, wm, wn, lane, tid, 0, 0, reinterpret_cast<unsigned*>(smem));
+}
+
 template <int MODE>
 int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
 #define KML_T(BMv, BNv)                                                  \
@@ -2014,6 +2204,20 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     if (!a.zp) return (int)hipErrorInvalidSymbol;
     return dispatch_direct<FWD>(a, bm, bn, bk, s);
   }
+  if (variant == 6) {  // stem halo: 7x7 / s2 / p3, Cin 8, Cout 64, one image per block
+    if (g22 || fold_c || C != 8 || K != 64 || KH != 7 || KW != 7 || sh != 2 || sw != 2 || ph != 3 || pw != 3 ||
+        H != W || H != 32)
+      return (int)hipErrorInvalidValue;
+    ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+    a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+    a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+    a.zp = zero_page();
+    a.M = B * a.OH * a.OW; a.N = K; a.Kd = 392;
+    a.splits = 1; a.kchunk = a.Kd;
+    if (!a.zp) return (int)hipErrorInvalidSymbol;
+    hipLaunchKernelGGL((k_conv_stem<32>), dim3(B), dim3(256), 0, s, a);
+    KML_LAUNCH_CHECK();
+  }
   if (variant == 5) {  // one-shot panels: single-tap, contiguous A rows, short K
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
     a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
@@ -2049,6 +2253,31 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
   a.slab = slab; a.counters = counters;
   return dispatch<FWD>(a, bm, bn, bk, variant, s);
+}
+
+// Halo forward (variant 4) of a conv whose INPUT is the raw output of another conv: that
+// conv's BatchNorm (training statistics from its partial rows) + ReLU is applied while the
+// patch is staged; the normalised input is written to ibn_y, the statistics to mean / rstd and
+// the running buffers updated — the BN apply launch between the two convs disappears.
+KML_API int kml_conv_fwd_bnin(const bf16_t* x, const bf16_t* w, bf16_t* y, float* stats, int stats_part, int B,
+                              int H, int W, int C, int K, int bm, int bn, float* grp_out, unsigned* grp_cnt,
+                              int grp_tiles, const float* ibn_rows, int ibn_G, const float* gamma, const float* beta,
+                              float* mean, float* rstd, float* rmean, float* rvar, float eps, float momentum,
+                              bf16_t* ibn_y, hipStream_t s) {
+  if (!ibn_rows || ibn_G < 1 || !ibn_y || !halo_shape_ok(H, W, C, K, 3, 3, 1, 1, 1, 1, bm, bn) || 2 * C > 1024 ||
+      (256 % (2 * C / 4)) != 0)
+    return (int)hipErrorInvalidValue;
+  ConvArgs a = make_args(B, H, W, C, K, 3, 3, 1, 1, 1, 1);
+  a.x = x; a.w = w; a.out = y; a.stats = stats; a.stats_part = stats_part;
+  a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+  a.zp = zero_page();
+  a.M = B * H * W; a.N = K; a.Kd = 9 * C;
+  a.splits = 1; a.kchunk = a.Kd;
+  a.ibn_rows = ibn_rows; a.ibn_G = ibn_G; a.ibn_M = (long long)B * H * W;
+  a.ibn_gamma = gamma; a.ibn_beta = beta; a.ibn_mean = mean; a.ibn_rstd = rstd; a.ibn_rmean = rmean;
+  a.ibn_rvar = rvar; a.ibn_eps = eps; a.ibn_mom = momentum; a.ibn_y = ibn_y;
+  if (!a.zp) return (int)hipErrorInvalidSymbol;
+  return dispatch_halo<FWD>(a, bm, bn, s);
 }
 
 namespace {

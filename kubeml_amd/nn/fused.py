@@ -209,8 +209,55 @@ class BNRegistry:
         self.bns = list(bns)
 
 
+# KUBEML_BN_FOLD=0: every BatchNorm of a BasicBlock runs its own apply kernel (no folding of
+# bn1 + ReLU into conv2's halo patch staging, see BlockFn.forward)
+_BN_FOLD = os.environ.get("KUBEML_BN_FOLD", "1") != "0"
+# group-reduce the folded BN's statistics rows in the producing conv (<= 16 rows for the consumer);
+# off: measured slower (1.354 vs 1.333 ms/step) and the ungrouped fold is bit-identical to the
+# unfolded BN apply (tests/test_models_gpu.py::test_resnet34_bn_fold_matches_unfolded)
+_FOLD_GROUP = os.environ.get("KUBEML_BN_FOLD_GROUP", "0") == "1"
+
+
 class ConvBNUnit:
     """Stateless executor for (conv module, bn module, relu)."""
+
+    @staticmethod
+    def conv_rows(x, conv, group=False):
+        """Training conv with per-tile BN partial statistics rows (no BN applied):
+        (c, rows, G).  group: reduce the rows to <= 16 in the producing launch (for a
+        consumer whose every block sums them: the BN-folding halo conv)."""
+        from ..ops import kernels as K
+        w = shadow_of(conv.weight)
+        kh, kw = conv.kernel_size
+        K_out = w.shape[0]
+        G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, group=group)
+        stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True, stats_group=group)
+        return c, stats, G
+
+    @staticmethod
+    def forward_folded(c_in, rows_in, G_in, bn_in, x_in, conv, bn, relu: bool, res: Optional[torch.Tensor]):
+        """conv(relu(bn_in(c_in))) with bn_in applied inside the conv's patch staging
+        (ops.kernels.conv_fwd_bnin), then this unit's own BN.  Returns (y, saved of the bn_in
+        unit, saved of this unit)."""
+        from ..ops import kernels as K
+        C = c_in.shape[-1]
+        y_in = torch.empty_like(c_in)
+        mean_in = torch.empty(C, dtype=torch.float32, device=c_in.device)
+        rstd_in = torch.empty_like(mean_in)
+        w = shadow_of(conv.weight)
+        K_out = w.shape[0]
+        G = K.conv_fwd_stats_rows(c_in.shape, K_out, 3, 3, (1, 1), (1, 1))
+        stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=c_in.device)
+        c = K.conv_fwd_bnin(c_in, w, rows_in, G_in, master_of(bn_in.weight), master_of(bn_in.bias), mean_in, rstd_in,
+                            bn_in.running_mean, bn_in.running_var, bn_in.eps,
+                            bn_in.momentum if bn_in.momentum is not None else 0.1, y_in, stats=stats, stats_part=True)
+        mean = torch.empty(K_out, dtype=torch.float32, device=c_in.device)
+        rstd = torch.empty_like(mean)
+        y = K.bn_apply(c, stats, master_of(bn.weight), master_of(bn.bias), res=res, save_mean=mean, save_rstd=rstd,
+                       run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
+                       momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
+        return y, (x_in, c_in, y_in, mean_in, rstd_in), (y_in, c, y if relu else None, mean, rstd)
 
     @staticmethod
     def forward(x, conv, bn, relu: bool, res: Optional[torch.Tensor], training: bool):
@@ -292,20 +339,28 @@ class BlockFn(Function):
     @staticmethod
     def forward(ctx, x, block, *params):
         training = True
-        saved = []
+        plan = block._kml_plan
+        saved = [None] * len(plan)
+        fold = _fold_unit(x, plan)      # index of a main unit whose BN + ReLU the next conv applies
         h = x
         short = None
-        for conv, bn, relu, role in block._kml_plan:
+        pending = None
+        for i, (conv, bn, relu, role) in enumerate(plan):
             if role == "short":
-                short, s = ConvBNUnit.forward(x, conv, bn, relu, None, training)
-                saved.append(s)
+                short, saved[i] = ConvBNUnit.forward(x, conv, bn, relu, None, training)
+            elif i == fold:
+                c, rows, G = ConvBNUnit.conv_rows(h, conv, group=_FOLD_GROUP)
+                pending = (i, h, c, rows, G, bn)
+            elif pending is not None:   # the conv right after the folded unit ("last": + residual)
+                j, x_in, c_in, rows, G, bn_in = pending
+                res = (short if short is not None else x) if role == "last" else None
+                h, saved[j], saved[i] = ConvBNUnit.forward_folded(c_in, rows, G, bn_in, x_in, conv, bn, relu, res)
+                pending = None
             elif role == "last":
                 res = short if short is not None else x
-                h, s = ConvBNUnit.forward(h, conv, bn, relu, res, training)
-                saved.append(s)
+                h, saved[i] = ConvBNUnit.forward(h, conv, bn, relu, res, training)
             else:
-                h, s = ConvBNUnit.forward(h, conv, bn, relu, None, training)
-                saved.append(s)
+                h, saved[i] = ConvBNUnit.forward(h, conv, bn, relu, None, training)
         ctx.block = block
         ctx.saved = saved
         # the next block's first dgrad produces this block's output gradient; it can emit
@@ -363,6 +418,29 @@ class BlockFn(Function):
         ctx.saved = None
         object.__setattr__(block, "_kml_last_saved", None)
         return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+def _fold_unit(x, plan):
+    """Index of the BasicBlock's first unit when its BN + ReLU can run inside the second conv's
+    halo patch staging (training, GPU, 3x3/s1 halo-eligible second conv), else None."""
+    from ..ops import kernels as K
+    if not (_BN_FOLD and x.is_cuda):
+        return None
+    mains = [i for i, u in enumerate(plan) if u[3] != "short"]
+    if len(mains) != 2:
+        return None
+    i1, i2 = mains
+    conv1, _, relu1, _ = plan[i1]
+    conv2 = plan[i2][0]
+    if not relu1 or conv2.kernel_size != (3, 3) or tuple(conv2.stride) != (1, 1) or tuple(conv2.padding) != (1, 1):
+        return None
+    B, H, W, _ = x.shape
+    kh, kw = conv1.kernel_size
+    OH, OW = K.out_hw(H, W, kh, kw, conv1.stride[0], conv1.stride[1], conv1.padding[0], conv1.padding[1])
+    shape1 = (B, OH, OW, shadow_of(conv1.weight).shape[0])
+    if K.unrolled22(H, W, kh, kw, conv1.stride, conv1.padding):
+        return None
+    return i1 if K.bnin_ok(shape1, shadow_of(conv2.weight).shape[0], 3, 3, (1, 1), (1, 1)) else None
 
 
 def block_params(block) -> List[torch.nn.Parameter]:

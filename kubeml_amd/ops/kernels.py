@@ -193,27 +193,32 @@ _GRP_MIN = int(os.environ.get("KUBEML_BN_GROUP_MIN", "0"))
 _GRP_ROWS = 16
 
 
-def _stats_layout(M, cfg):
-    """(per-wave rows G, M-tiles per group or 0, rows the consumer reads)."""
+def _stats_layout(M, cfg, group=False):
+    """(per-wave rows G, M-tiles per group or 0, rows the consumer reads).  group: reduce
+    to at most _GRP_ROWS rows regardless of KUBEML_BN_GROUP_MIN (a consumer whose every
+    block reads all rows, e.g. the BN-folding halo conv)."""
     bm = _norm_cfg(cfg)[0]
     tiles = _cdiv(M, bm)
     # one row per M tile (the epilogue sums the tile's wave row-bands; tail tiles included)
     G = tiles
-    if _GRP_MIN <= 0 or G <= _GRP_MIN:
+    if group:
+        if G <= _GRP_ROWS:
+            return G, 0, G
+    elif _GRP_MIN <= 0 or G <= _GRP_MIN:
         return G, 0, G
     tpg = _cdiv(tiles, _GRP_ROWS)
     return G, tpg, _cdiv(tiles, tpg)
 
 
-def conv_stats_rows(M, cfg):
+def conv_stats_rows(M, cfg, group=False):
     """Rows of the partial-statistics buffer a conv epilogue hands to the BN kernel for a
     plan: one per M-tile, or one per M-tile group when group-reduced."""
-    return _stats_layout(M, cfg)[2]
+    return _stats_layout(M, cfg, group)[2]
 
 
-def _stats_ws(device, M, N, cfg, out):
+def _stats_ws(device, M, N, cfg, out, group=False):
     """(rows buffer the epilogue writes, group output or None, tickets, tiles per group)."""
-    G, tpg, ng = _stats_layout(M, cfg)
+    G, tpg, ng = _stats_layout(M, cfg, group)
     if not tpg:
         return out, None, None, 0
     bn = _norm_cfg(cfg)[1]
@@ -315,7 +320,7 @@ def _check_wu(x_shape, w, wu, KH, KW, stride, pad):
 
 
 def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=None, cfg=None, stats_part=False,
-             wu=None, _fold=0, _g22=False):
+             wu=None, _fold=0, _g22=False, stats_group=False):
     """y[B,OH,OW,Cout] = conv(x[B,H,W,Cin], w[Cout,KH,KW,Cin]) (+bias, ReLU; BN stats).
 
     stats: fp32 [2*Cout] accumulated with atomics, or with ``stats_part`` a [G, 2*Cout]
@@ -359,19 +364,23 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     rows, grp, gcnt, tpg = stats, None, None, 0
     if stats is not None:
         _chk(stats, F32, "stats")
-        need = 2 * K * (conv_stats_rows(M, (bm, bn, bk, splits, variant)) if stats_part else 1)
+        need = 2 * K * (conv_stats_rows(M, (bm, bn, bk, splits, variant), stats_group) if stats_part else 1)
         if _fold and (not stats_part or K % _fold):
             raise ValueError("folded statistics need stats_part and K % fold == 0")
         if stats.numel() < need:
             raise ValueError(f"stats buffer has {stats.numel()} floats, needs {need}")
         if stats_part:
-            rows, grp, gcnt, tpg = _stats_ws(x.device, M, K, (bm, bn, bk, splits, variant), stats)
+            rows, grp, gcnt, tpg = _stats_ws(x.device, M, K, (bm, bn, bk, splits, variant), stats, stats_group)
     if _fold and grp is not None:
         raise ValueError("folded statistics cannot be group-reduced")
     sig = "p p p p p i i i i i i i i i i i i i i i i i i p p p p i i i s"
     if variant == HALO:
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, HALO, 0, 0, _p(grp), _p(gcnt), tpg, 0, 0, _s())
+        return out
+    if variant == STEM:
+        HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
+                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, STEM, 0, 0, _p(grp), _p(gcnt), tpg, 0, 0, _s())
         return out
     if variant == ONESHOT:
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
@@ -396,13 +405,15 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
     (H, W, KH, KW, stride, pad) lets an eligible conv take the halo-patch kernel
     (:func:`halo_plan`); without it (or when ineligible) a HALO plan falls back."""
     if cfg is None and geom is not None:
-        hp = halo_plan(C, K, *geom) or oneshot_plan(C, K, Kd, *geom)
+        hp = halo_plan(C, K, *geom) or oneshot_plan(C, K, Kd, *geom) or stem_plan(C, K, *geom)
         if hp is not None:
             return hp
     plan = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
     if plan[4] == HALO and (geom is None or not halo_ok(C, K, *geom, plan[0], plan[1])):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == ONESHOT and (geom is None or not oneshot_ok(C, K, Kd, *geom, plan[0], plan[1])):
+        plan = _norm_cfg(default_plan("fwd", M, K, Kd))
+    if plan[4] == STEM and (geom is None or stem_plan(C, K, *geom, force=True) is None):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == DIRECT and C % 32:
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
@@ -444,6 +455,19 @@ def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
         if halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn):
             return (bm, bn, K * 16 + H, 1, HALO)   # bk slot: the body's geometry (grouped pairs)
     return None
+
+
+STEM = 6  # cfg variant id of the stem halo kernel (7x7/s2/p3, Cin 8, Cout 64, 32x32 input): bm = one image
+_STEM_ON = os.environ.get("KUBEML_CONV_STEM", "1") != "0"
+
+
+def stem_plan(C, K, H, W, KH, KW, stride, pad, force=False):
+    """(256, 64, 0, 1, STEM) for the ResNet ImageNet stem on 32x32 images, else None."""
+    if not (_STEM_ON or force):
+        return None
+    if (C, K, H, W, KH, KW, tuple(stride), tuple(pad)) != (8, 64, 32, 32, 7, 7, (2, 2), (3, 3)):
+        return None
+    return (256, 64, 0, 1, STEM)
 
 
 ONESHOT = 5  # cfg variant id of the one-shot panel forward (single-tap convs, K in _ONESHOT_TILES)
@@ -510,7 +534,7 @@ def halo_plan(C, K, H, W, KH, KW, stride, pad):
     return None
 
 
-def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False):
+def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False, group=False):
     """G of the partial-statistics buffer conv_fwd(stats_part=True) needs for this conv
     (``unroll``: the conv runs with its unrolled weight, 4 folded rows per M-tile)."""
     B, H, W, C = x_shape
@@ -521,7 +545,55 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False)
     OH, OW = out_hw(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
     M, Kd = B * OH * OW, (r1 - r0) * (s1 - s0) * C
-    return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg, geom=(H, W, KH, KW, stride, pad)))
+    return conv_stats_rows(M, conv_fwd_plan(C, M, K, Kd, cfg, geom=(H, W, KH, KW, stride, pad)), group)
+
+
+def bnin_ok(x_shape, K, KH, KW, stride, pad) -> bool:
+    """Can this forward conv apply its input's BatchNorm + ReLU while staging (conv_fwd_bnin)?"""
+    B, H, W, C = x_shape
+    return (_BNIN_ON and halo_plan(C, K, H, W, KH, KW, stride, pad) is not None and 2 * C <= 1024 and
+            256 % (C // 2) == 0)
+
+
+_BNIN_ON = os.environ.get("KUBEML_BN_FOLD", "1") != "0"
+
+
+def conv_fwd_bnin(c_in, w, rows, G, gamma, beta, save_mean, save_rstd, run_mean, run_var, eps, momentum, y_in,
+                  stats=None, stats_part=True, stats_group=False, out=None):
+    """out = conv3x3(relu(bn(c_in))) on the halo kernel with the BatchNorm applied while the patch
+    is staged: ``rows``/``G`` are the producer's partial statistics rows, the normalised input is
+    written to ``y_in`` (every element, by the N-tile-0 blocks), ``save_mean``/``save_rstd`` and
+    the running buffers are updated as bn_apply would.  ``stats`` as in :func:`conv_fwd` (the
+    output's own BN partial rows)."""
+    _chk(c_in, BF16, "c_in", 4)
+    _chk(w, BF16, "w", 4)
+    _chk(y_in, BF16, "y_in", 4)
+    B, H, W, C = c_in.shape
+    K = w.shape[0]
+    if tuple(w.shape) != (K, 3, 3, C) or tuple(y_in.shape) != tuple(c_in.shape):
+        raise ValueError("conv_fwd_bnin: 3x3 weight over c_in's channels and a y_in like c_in")
+    plan = halo_plan(C, K, H, W, 3, 3, (1, 1), (1, 1))
+    if plan is None or not bnin_ok(c_in.shape, K, 3, 3, (1, 1), (1, 1)):
+        raise ValueError("conv_fwd_bnin: conv is not halo-eligible")
+    bm, bn = plan[0], plan[1]
+    if out is None:
+        out = torch.empty((B, H, W, K), dtype=BF16, device=c_in.device)
+    srows, grp, gcnt, tpg = stats, None, None, 0
+    if stats is not None:
+        _chk(stats, F32, "stats")
+        need = 2 * K * (conv_stats_rows(B * H * W, plan, stats_group) if stats_part else 1)
+        if stats.numel() < need:
+            raise ValueError(f"stats buffer has {stats.numel()} floats, needs {need}")
+        if stats_part:
+            srows, grp, gcnt, tpg = _stats_ws(c_in.device, B * H * W, K, plan, stats, stats_group)
+    _chk(rows, F32, "rows")
+    if rows.numel() < G * 2 * C:
+        raise ValueError("conv_fwd_bnin: partial rows smaller than G x 2C")
+    HIP.call("kml_conv_fwd_bnin", "p p p p i i i i i i i i p p i p i p p p p p p f f p s",
+             _p(c_in), _p(w), _p(out), _p(srows), int(stats_part), B, H, W, C, K, bm, bn, _p(grp), _p(gcnt), tpg,
+             _p(rows), int(G), _p(gamma), _p(beta), _p(save_mean), _p(save_rstd), _p(run_mean), _p(run_var),
+             float(eps), float(momentum), _p(y_in), _s())
+    return out
 
 
 def _u22_views(B, C, K, dy=None, x=None, addend=None, bnf=None):

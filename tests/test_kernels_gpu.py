@@ -1002,3 +1002,72 @@ def test_conv_oneshot_backward(unroll, monkeypatch):
     gref = wr.grad if unroll else wr.grad[:, :, 1:2, 1:2]
     assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
     assert _rel(dw3.permute(0, 3, 1, 2), gref) < 1e-2
+
+
+def test_conv_stem_variant():
+    """Stem halo kernel (variant 6: 7x7/s2/p3 on a 32x32 image, Cin 3 padded to 8, one image per
+    block) vs fp32 torch: output, atomic statistics and one partial row per image."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(16)
+    B = 5
+    x = torch.zeros(B, 32, 32, 8, device=dev)
+    x[..., :3] = torch.randn(B, 32, 32, 3, device=dev)
+    x = _bf(x)
+    w = torch.zeros(64, 7, 7, 8, device=dev)
+    w[..., :3] = torch.randn(64, 7, 7, 3, device=dev) * 0.1
+    w = _bf(w)
+    cfg = K.conv_fwd_plan(8, B * 256, 64, 392, geom=(32, 32, 7, 7, (2, 2), (3, 3)))
+    assert cfg[4] == K.STEM
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2, padding=3)
+    st = torch.zeros(128, device=dev)
+    y = K.conv_fwd(x, w, 7, 7, (2, 2), (3, 3), stats=st, cfg=cfg)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    assert _rel(st[:64], yr.sum((0, 2, 3))) < 2e-2 and _rel(st[64:], (yr * yr).sum((0, 2, 3))) < 2e-2
+    G = K.conv_fwd_stats_rows(x.shape, 64, 7, 7, (2, 2), (3, 3))
+    assert G == B
+    buf = torch.full((G * 128 + 64,), float("nan"), device=dev)
+    y2 = K.conv_fwd(x, w, 7, 7, (2, 2), (3, 3), stats=buf[:G * 128], stats_part=True)
+    assert torch.equal(y, y2) and torch.isnan(buf[G * 128:]).all()
+    assert _rel(buf[:G * 128].view(G, 2, 64).sum(0)[0], yr.sum((0, 2, 3))) < 2e-2
+
+
+@pytest.mark.parametrize("case", [(8, 8, 64, 64), (12, 4, 128, 128)])
+def test_conv_fwd_bnin_matches_bn_then_conv(case):
+    """conv_fwd_bnin (the input's BN + ReLU applied while the halo patch is staged) vs
+    bn_apply followed by the halo conv: normalised input, saved statistics, running buffers
+    and the conv output (+ its partial rows); the producer's rows group-reduced or not."""
+    from kubeml_amd.ops import kernels as K
+    B, H, C, Co = case
+    torch.manual_seed(17)
+    x = _bf(torch.randn(B, H, H, C, device=dev))
+    w1 = _bf(torch.randn(C, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5))
+    w2 = _bf(torch.randn(Co, 3, 3, C, device=dev) * (1.0 / (9 * C) ** 0.5))
+    g, b = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+    for group in (False, True):
+        G1 = K.conv_fwd_stats_rows(x.shape, C, 3, 3, (1, 1), (1, 1), group=group)
+        rows = torch.empty(G1 * 2 * C, device=dev)
+        c1 = K.conv_fwd(x, w1, 3, 3, (1, 1), (1, 1), stats=rows, stats_part=True, stats_group=group)
+        # reference: BN apply kernel, then the conv
+        m0, r0 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        rm0, rv0 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y0 = K.bn_apply(c1, rows, g, b, save_mean=m0, save_rstd=r0, run_mean=rm0, run_var=rv0, relu=True,
+                        stats_rows=G1)
+        o0 = K.conv_fwd(y0, w2, 3, 3, (1, 1), (1, 1))
+        # folded
+        m1, r1 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        rm1, rv1 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        y1 = torch.full_like(c1, float("nan"))
+        G2 = K.conv_fwd_stats_rows(c1.shape, Co, 3, 3, (1, 1), (1, 1))
+        st2 = torch.empty(G2 * 2 * Co, device=dev)
+        o1 = K.conv_fwd_bnin(c1, w2, rows, G1, g, b, m1, r1, rm1, rv1, 1e-5, 0.1, y1, stats=st2)
+        torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(r1, r0, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(rm1, rm0, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(rv1, rv0, rtol=1e-5, atol=1e-6)
+        assert not torch.isnan(y1.float()).any(), group
+        assert _rel(y1, y0) < 1e-2, (group, _rel(y1, y0))
+        if not group:   # same rows, same summation order and arithmetic as the BN apply kernel
+            assert torch.equal(y1, y0) and torch.equal(m1, m0) and torch.equal(r1, r0)
+        assert _rel(o1, o0) < 1e-2, (group, _rel(o1, o0))
+        of = o1.float().reshape(-1, Co)
+        assert _rel(st2.view(G2, 2, Co).sum(0)[0], of.sum(0)) < 2e-2

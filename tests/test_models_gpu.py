@@ -296,3 +296,38 @@ def test_resnet_fused_stem_matches_unfused_stem():
     (pr * R.permute(0, 3, 1, 2)).sum().backward()
     assert _rel(p1.permute(0, 3, 1, 2), pr) < 2e-2
     assert _rel(g1, gam.grad) < 5e-2 and _rel(b1, bet.grad) < 5e-2
+
+
+def test_resnet34_bn_fold_matches_unfolded():
+    """BasicBlock bn1 + ReLU applied inside conv2's halo patch staging (KUBEML_BN_FOLD path,
+    kernels.conv_fwd_bnin) vs a separate BN apply: logits, loss, every gradient, the folded BNs'
+    running statistics — bit-identical forward (same rows, same summation order)."""
+    from kubeml_amd.models.resnet import resnet34
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.nn import fused
+    torch.manual_seed(0)
+    x = torch.randn(64, 32, 32, 8, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 1000, (64,), device=dev)
+    res = []
+    old = fused._BN_FOLD, fused._FOLD_GROUP
+    try:
+        for fold, group in ((False, False), (True, False)):
+            fused._BN_FOLD, fused._FOLD_GROUP = fold, group
+            torch.manual_seed(3)
+            m = resnet34(1000).to(dev)
+            sp = flatten_module(m)
+            m.train()
+            sp.zero_grad()
+            out = m(x)
+            loss = cross_entropy(out, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((out.float(), float(loss), sp.grad.clone(), m.layer1[0].bn1.running_var.clone(),
+                        m.layer2[1].bn1.running_mean.clone()))
+    finally:
+        fused._BN_FOLD, fused._FOLD_GROUP = old
+    (o0, l0, g0, rv0, rm0), (o1, l1, g1, rv1, rm1) = res
+    # the rows are summed in the BN apply kernel's own order and arithmetic: bit-identical
+    assert torch.equal(o1, o0), _rel(o1, o0)
+    assert l1 == l0 and torch.equal(rv1, rv0) and torch.equal(rm1, rm0)
+    assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
