@@ -1252,6 +1252,20 @@ __device__ __forceinline__ void HaloBody<MODE, C, HW, IMG, BN, D>::run(const Con
   const int m0 = bk.y * P::BM, n0 = bk.x * BN, img0 = bk.y * IMG;
   const bf16_t* const src = (MODE == FWD) ? a.x : a.dy;   // patch source, C channels
 
+  // folded input BN: the first 16 statistics rows of this thread's slice are requested before
+  // anything else, so their round trip overlaps the weight / patch loads (vmcnt retires in
+  // issue order: rows issued after the patch would wait for it)
+  constexpr int BQ = 2 * C / 4, BS = 256 / BQ;   // float4 columns of a statistics row, row slices
+  float4 brow_early[16];
+  const bool bnin = MODE == FWD && a.ibn_rows != nullptr;
+  if constexpr (MODE == FWD) {
+    if (bnin && tid / BQ < BS) {
+      const float4* p4 = reinterpret_cast<const float4*>(a.ibn_rows) + tid % BQ;
+#pragma unroll
+      for (int uu = 0; uu < 16; ++uu) brow_early[uu] = p4[(long long)min(tid / BQ + uu * BS, a.ibn_G - 1) * BQ];
+    }
+  }
+
   // weights first (FWD register stream: D K-steps of B fragments; otherwise the block's whole
   // slice), in flight while the patch loads are issued
   const bf16_t* wp[NR];
@@ -1321,12 +1335,18 @@ __device__ __forceinline__ void HaloBody<MODE, C, HW, IMG, BN, D>::run(const Con
       float* bsf = bsc + C;
       float* sums = bsf + C;
       float4* scratch = reinterpret_cast<float4*>(sums + 2 * C);
-      constexpr int Q = 2 * C / 4, S = 256 / Q;  // float4 columns of a row, row slices
+      constexpr int Q = BQ, S = BS;
       const int q = tid % Q, sl = tid / Q;
       float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
       if (sl < S) {  // rows sl, sl + S, ... in order (the BN apply kernel's summation order)
         const float4* p4 = reinterpret_cast<const float4*>(a.ibn_rows) + q;
-        for (int g = sl; g < a.ibn_G; g += 16 * S) {
+#pragma unroll
+        for (int uu = 0; uu < 16; ++uu) {
+          const bool in = sl + uu * S < a.ibn_G;
+          acc4.x += in ? brow_early[uu].x : 0.f; acc4.y += in ? brow_early[uu].y : 0.f;
+          acc4.z += in ? brow_early[uu].z : 0.f; acc4.w += in ? brow_early[uu].w : 0.f;
+        }
+        for (int g = sl + 16 * S; g < a.ibn_G; g += 16 * S) {
           float4 rv[16];
 #pragma unroll
           for (int uu = 0; uu < 16; ++uu) rv[uu] = p4[(long long)min(g + uu * S, a.ibn_G - 1) * Q];
