@@ -88,13 +88,32 @@ def _free_port():
     return p
 
 
+def _visible_gpus():
+    """GPUs this process may use, without touching HIP: the *_VISIBLE_DEVICES lists, else the
+    KFD topology's GPU nodes (simd_count > 0).  None when neither can be read."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(base):
+            with open(os.path.join(base, node, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            n += int(props.get("simd_count", "0")) > 0
+        return n
+    except OSError:
+        return None
+
+
 def relaunch(args):
-    """--gpus N > 1 outside torchrun: start N ranks as a child torch.distributed.run (the
-    parent never initialises the GPU; device_count() does not) and exit with its code."""
+    """--gpus N > 1 outside torchrun: start N ranks as a child torch.distributed.run and exit
+    with its code.  The parent never loads HIP: it counts GPUs from the visible-devices
+    variables or the KFD topology (sysfs)."""
     if not args.cpu_smoke:
-        import torch
-        have = torch.cuda.device_count()
-        if have < args.gpus:
+        have = _visible_gpus()
+        if have is not None and have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) visible "
                   f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', '<unset>')})", file=sys.stderr)
             sys.exit(2)
