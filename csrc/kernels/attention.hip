@@ -30,6 +30,9 @@
 // fused QKV projection output / dQKV gradient buffers are used in place.
 #include "kml_common.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
@@ -47,6 +50,8 @@ struct AttnArgs {
   const float* ctr;    // [seed, step] (device) for attention dropout, or null
   unsigned salt;
   float pdrop;         // dropout probability (0: off)
+  int xcd;             // XCD-aware block order (attn_blk); 0: plain grid order (A/B switch)
+  unsigned char* keep; // dropout keep bits written by the forward, read by the backward (Drop), or null
 };
 
 __device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
@@ -58,6 +63,12 @@ __device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
 // per-kernel dropout state.  One 32-bit hash per (q, key pair): its low 16 bits decide the
 // even key, the high 16 bits the odd one (threshold p * 2^16) — half the hashing of one hash
 // per element, and the inner loops always visit keys in aligned pairs.
+//
+// The forward also stores the decisions as a bit mask (AttnArgs::keep), so the backward
+// kernels read 1 bit per probability instead of re-hashing (the hash is most of their
+// vector-ALU work): u64 word (bh, key tile kb, query q) at byte ((bh*nkb + kb)*Lp + q)*8,
+// Lp = 64*nkb; bit 16g + 4t + i = key kb*64 + 16t + 4g + i — the 16 keys a forward lane
+// holds (lane group g, S-tile t, element i) are one u16 at byte 2g.
 struct Drop {
   unsigned k0, k1, thr;
   float sc;
@@ -66,6 +77,7 @@ struct Drop {
   __device__ void init(const AttnArgs& a, int bh) {
     on = a.ctr != nullptr && a.pdrop > 0.f;
     LP = (unsigned)(a.L + 1) >> 1;
+    sc = 1.f;
     if (on) {
       k0 = (unsigned)a.ctr[0] ^ a.salt;
       k1 = (unsigned)a.ctr[1] * 0x632BE5ABu ^ (unsigned)bh * 0x5851F42Du;
@@ -73,15 +85,45 @@ struct Drop {
       sc = 1.f / (1.f - a.pdrop);
     }
   }
-  // keep factors of keys (key, key + 1), key even
-  __device__ __forceinline__ void keep2(int q, int key, float& z0, float& z1) const {
+  // keep bits of keys kbase + 16t + i (bit 4t + i), kbase = kb*64 + 4g
+  __device__ __forceinline__ unsigned bits16(int q, int kbase) const {
+    unsigned bits = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {
+        const unsigned h = ahash(k0, k1, (unsigned)q * LP + ((unsigned)(kbase + 16 * t + i) >> 1));
+        bits |= ((h & 0xFFFFu) >= thr ? 1u : 0u) << (4 * t + i);
+        bits |= (h >= (thr << 16) ? 1u : 0u) << (4 * t + i + 1);
+      }
+    return bits;
+  }
+  // all-ones / zero mask of one (q, key)
+  __device__ __forceinline__ int keep1(int q, int key) const {
     const unsigned h = ahash(k0, k1, (unsigned)q * LP + ((unsigned)key >> 1));
-    z0 = (h & 0xFFFFu) >= thr ? sc : 0.f;
-    z1 = (h >> 16) >= thr ? sc : 0.f;
+    return ((key & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr ? -1 : 0;
   }
 };
 
+// bit j of w as an all-ones / zero mask (v_bfe_i32)
+__device__ __forceinline__ int bitmask(unsigned w, int j) { return __builtin_amdgcn_sbfe((int)w, j, 1); }
+__device__ __forceinline__ float fmask(float x, int m) { return __int_as_float(__float_as_int(x) & m); }
+
 __device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+// XCD-aware block order.  Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share
+// one), so with the plain (tile, b*h) grid the 8 tiles of one head land on 8 different L2s
+// and each XCD fetches that head's K/V (or Q/dO) again.  Renumbered so each XCD runs a
+// contiguous range of ids, tile fastest: the tiles of one head share one L2.
+__device__ __forceinline__ void attn_blk(const AttnArgs& a, int& xt, int& bh) {
+  const int gx = (int)gridDim.x, nwg = gx * (int)gridDim.y;
+  const int lin = (int)blockIdx.y * gx + (int)blockIdx.x;
+  if (!a.xcd) { xt = (int)blockIdx.x; bh = (int)blockIdx.y; return; }
+  const int q = nwg >> 3, r = nwg & 7, x = lin & 7, k = lin >> 3;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  bh = id / gx;
+  xt = id - bh * gx;
+}
 
 struct TileRegs { uint4 v[2]; };
 
@@ -148,13 +190,21 @@ __device__ __forceinline__ void store4(bf16_t* p, const f32x4_t& v, float s) {
 }
 
 // ------------------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
+// OCC: waves per SIMD the register budget is sized for (launch bounds); selectable at run
+// time (attn_occ) so the occupancy / register trade is measured, not assumed
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
+  // K/V double-buffered (40 KB: 4 blocks per CU, the VGPR occupancy): one barrier per key
+  // tile, and the register-staged next tile is stored after this tile's MFMAs, a whole tile
+  // after its global loads were issued
   __shared__ __attribute__((aligned(16))) char sQ[8192];
-  __shared__ __attribute__((aligned(16))) char sK[8192];
-  __shared__ __attribute__((aligned(16))) char sV[8192];
+  __shared__ __attribute__((aligned(16))) char sK2[2][8192];
+  __shared__ __attribute__((aligned(16))) char sV2[2][8192];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int L = a.L, q0 = blockIdx.x * 64;
+  int xt, bh;
+  attn_blk(a, xt, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int L = a.L, q0 = xt * 64;
   const bf16_t* Qb = a.q + (long long)b * L * a.ldq + h * 64;
   const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
   const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
@@ -168,6 +218,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   tile_load(rk, Kb, a.ldk, 0, L, tid);
   tile_load(rv, Vb, a.ldv, 0, L, tid);
   tile_store(sQ, rq, tid);
+  tile_store(sK2[0], rk, tid);
+  tile_store(sV2[0], rv, tid);
+  const int nkb = (L + 63) / 64;
+  if (nkb > 1) {
+    tile_load(rk, Kb, a.ldk, 64, L, tid);
+    tile_load(rv, Vb, a.ldv, 64, L, tid);
+  }
   __syncthreads();
   const bf16x8_t qf0 = frag_rows(sQ, 16 * w, 0, lane), qf1 = frag_rows(sQ, 16 * w, 1, lane);
 
@@ -176,16 +233,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) acc[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nkb = (L + 63) / 64;
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();
-    tile_store(sK, rk, tid);
-    tile_store(sV, rv, tid);
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      tile_load(rk, Kb, a.ldk, (kb + 1) * 64, L, tid);
-      tile_load(rv, Vb, a.ldv, (kb + 1) * 64, L, tid);
-    }
+    const char* sK = sK2[kb & 1];
+    const char* sV = sV2[kb & 1];
     f32x4_t s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -193,49 +243,64 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       s[t] = MFMA16(frag_rows(sK, 16 * t, 0, lane), qf0, s[t]);
       s[t] = MFMA16(frag_rows(sK, 16 * t, 1, lane), qf1, s[t]);
     }
+    // bias or key tail: scale + bias + mask every score; otherwise the max of the raw scores
+    // (scale > 0) and one fma per probability below
+    const bool gen = bias != nullptr || kb * 64 + 64 > L;
     float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kb * 64 + 16 * t + 4 * g + i;
-        float v = s[t][i] * sl2;
-        if (bias && key < L) v += bias[key] * LOG2E;
-        if (key >= L) v = -INFINITY;
-        s[t][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m2, mx);
-    const bool dead = mn == -INFINITY;
-    const float alpha = dead ? 1.f : fexp2(m2 - mn);
-    float ps = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = dead ? 0.f : fexp2(s[t][i] - mn);
-        s[t][i] = p;
-        ps += p;
-      }
-    ps += __shfl_xor(ps, 16, 64);
-    ps += __shfl_xor(ps, 32, 64);
-    lsum = lsum * alpha + ps;
-    m2 = mn;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) acc[d] *= alpha;
-    if (drop.on) {
-      const int qq = q0 + 16 * w + (lane & 15);
+    if (gen) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          float z0, z1;
-          drop.keep2(qq, kb * 64 + 16 * t + 4 * g + i, z0, z1);
-          s[t][i] *= z0;
-          s[t][i + 1] *= z1;
+        for (int i = 0; i < 4; ++i) {
+          const int key = kb * 64 + 16 * t + 4 * g + i;
+          float v = s[t][i] * sl2;
+          if (bias && key < L) v += bias[key] * LOG2E;
+          if (key >= L) v = -INFINITY;
+          s[t][i] = v;
+          mx = fmaxf(mx, v);
         }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+      mx *= sl2;
+    }
+    // lazy rescale: the running max m2 moves only when a score exceeds it by 8 (P <= 2^8,
+    // exact in fp32, the same relative precision in bf16) — most tiles skip the shuffles and
+    // the accumulator scaling.  The four lanes of a query column always agree on m2.
+    if (__any(mx > m2 + 8.f)) {
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m2, mx);
+      const float alpha = mn == -INFINITY ? 1.f : fexp2(m2 - mn);
+      lsum *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) acc[d] *= alpha;
+      m2 = mn;
+    }
+    const float off = m2 == -INFINITY ? 0.f : m2;
+    if (gen) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[t][i] = fexp2(s[t][i] - off);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[t][i] = fexp2(fmaf(s[t][i], sl2, -off));
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) lsum += (s[t][0] + s[t][1]) + (s[t][2] + s[t][3]);
+    if (drop.on) {   // zero the dropped probabilities (1/(1-p) is applied to O at the end)
+      const int qq = q0 + 16 * w + (lane & 15);
+      const unsigned bits = drop.bits16(qq, kb * 64 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[t][i] = fmask(s[t][i], bitmask(bits, 4 * t + i));
+      if (a.keep && qq < L)
+        *reinterpret_cast<unsigned short*>(a.keep + (((long long)bh * nkb + kb) * (nkb * 64) + qq) * 8 + 2 * g) =
+            (unsigned short)bits;
     }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
 #pragma unroll
@@ -243,10 +308,21 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       acc[d] = MFMA16(frag_tr(sV, 16 * d, 0, lane), p0, acc[d]);
       acc[d] = MFMA16(frag_tr(sV, 16 * d, 1, lane), p1, acc[d]);
     }
+    if (kb + 1 < nkb) {   // buffer (kb+1)&1 last held tile kb-1: every wave left it at the last barrier
+      tile_store(sK2[(kb + 1) & 1], rk, tid);
+      tile_store(sV2[(kb + 1) & 1], rv, tid);
+      if (kb + 2 < nkb) {
+        tile_load(rk, Kb, a.ldk, (kb + 2) * 64, L, tid);
+        tile_load(rv, Vb, a.ldv, (kb + 2) * 64, L, tid);
+      }
+      __syncthreads();
+    }
   }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
   const int q = q0 + 16 * w + (lane & 15);
   if (q < L) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? drop.sc / lsum : 0.f;
     bf16_t* op = a.out + (long long)(b * L + q) * a.ldout + h * 64;
 #pragma unroll
     for (int d = 0; d < 4; ++d) store4(op + 16 * d + 4 * g, acc[d], inv);
@@ -255,13 +331,16 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dQ (+D)
-__global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char sK[8192];
-  __shared__ __attribute__((aligned(16))) char sV[8192];
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sK2[2][8192];   // K/V double-buffered (k_attn_fwd)
+  __shared__ __attribute__((aligned(16))) char sV2[2][8192];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  int xt, bh;
+  attn_blk(a, xt, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
   const int L = a.L;
-  const int q = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const int q = xt * 64 + 16 * w + (lane & 15);
   const bool qok = q < L;
   const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
   const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
@@ -298,15 +377,25 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   tile_load(rk, Kb, a.ldk, 0, L, tid);
   tile_load(rv, Vb, a.ldv, 0, L, tid);
   const int nkb = (L + 63) / 64;
+  tile_store(sK2[0], rk, tid);
+  tile_store(sV2[0], rv, tid);
+  if (nkb > 1) {
+    tile_load(rk, Kb, a.ldk, 64, L, tid);
+    tile_load(rv, Vb, a.ldv, 64, L, tid);
+  }
+  __syncthreads();
+  // this lane's u16 of the stored keep bits for key tile kb (Drop), prefetched with K/V
+  const bool kbits = drop.on && a.keep != nullptr;
+  const unsigned short* kp16 =
+      reinterpret_cast<const unsigned short*>(a.keep + ((long long)bh * nkb * (nkb * 64) + (qok ? q : 0)) * 8 + 2 * g);
+  const long long kstride = (long long)nkb * 64 * 4;   // u16 units per key tile
+  unsigned knext = kbits ? kp16[0] : 0xFFFFu;
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();
-    tile_store(sK, rk, tid);
-    tile_store(sV, rv, tid);
-    __syncthreads();
-    if (kb + 1 < nkb) {
-      tile_load(rk, Kb, a.ldk, (kb + 1) * 64, L, tid);
-      tile_load(rv, Vb, a.ldv, (kb + 1) * 64, L, tid);
-    }
+    const char* sK = sK2[kb & 1];
+    const char* sV = sV2[kb & 1];
+    unsigned bits = knext;
+    if (kbits && kb + 1 < nkb) knext = kp16[(kb + 1) * kstride];
+    if (drop.on && !kbits) bits = drop.bits16(q, kb * 64 + 4 * g);
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -317,26 +406,38 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
       dp[t] = MFMA16(frag_rows(sV, 16 * t, 0, lane), df0, dp[t]);
       dp[t] = MFMA16(frag_rows(sV, 16 * t, 1, lane), df1, dp[t]);
     }
+    // dS = P (.) (dP (.) Z/(1-p) - D); bias / key tail only on the general path
+    const bool gen = bias != nullptr || kb * 64 + 64 > L;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; i += 2) {
+      for (int i = 0; i < 4; ++i) {
         const int key = kb * 64 + 16 * t + 4 * g + i;
-        float z0 = 1.f, z1 = 1.f;
-        if (drop.on) drop.keep2(q, key, z0, z1);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          float v = s[t][i + e] * sl2;
-          if (bias && key + e < L) v += bias[key + e] * LOG2E;
-          const float p = key + e < L ? fexp2(v - lse) : 0.f;
-          s[t][i + e] = p * (dp[t][i + e] * (e ? z1 : z0) - D);
+        float p = 0.f;
+        if (gen) {
+          float v = s[t][i] * sl2;
+          if (bias && key < L) v += bias[key] * LOG2E;
+          if (key < L) p = fexp2(v - lse);
+        } else {
+          p = fexp2(fmaf(s[t][i], sl2, -lse));
         }
+        const float dpz = drop.on ? fmask(dp[t][i], bitmask(bits, 4 * t + i)) : dp[t][i];
+        s[t][i] = p * fmaf(dpz, drop.sc, -D);
       }
     const bf16x8_t d0 = pack_p(s[0], s[1]), d1 = pack_p(s[2], s[3]);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       acc[d] = MFMA16(frag_tr(sK, 16 * d, 0, lane), d0, acc[d]);
       acc[d] = MFMA16(frag_tr(sK, 16 * d, 1, lane), d1, acc[d]);
+    }
+    if (kb + 1 < nkb) {
+      tile_store(sK2[(kb + 1) & 1], rk, tid);
+      tile_store(sV2[(kb + 1) & 1], rv, tid);
+      if (kb + 2 < nkb) {
+        tile_load(rk, Kb, a.ldk, (kb + 2) * 64, L, tid);
+        tile_load(rv, Vb, a.ldv, (kb + 2) * 64, L, tid);
+      }
+      __syncthreads();
     }
   }
   if (qok) {
@@ -347,14 +448,19 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dK, dV
-__global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char sQ[8192];
-  __shared__ __attribute__((aligned(16))) char sO[8192];  // dO tile
-  __shared__ float sL[64], sD[64];
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
+  // double-buffered like k_attn_fwd: Q, dO, LSE, D and the keep bits of a query tile
+  __shared__ __attribute__((aligned(16))) char sQ2[2][8192];
+  __shared__ __attribute__((aligned(16))) char sO2[2][8192];  // dO tile
+  __shared__ float sL2[2][64], sD2[2][64];
+  __shared__ __attribute__((aligned(16))) unsigned sM2[2][128];   // keep bits: 64 u64 words
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  int xt, bh;
+  attn_blk(a, xt, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
   const int L = a.L;
-  const int key = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const int key = xt * 64 + 16 * w + (lane & 15);
   const bool kok = key < L;
   const bf16_t* Qb = a.q + (long long)b * L * a.ldq + h * 64;
   const bf16_t* Ob = a.dout + (long long)b * L * a.lddo + h * 64;
@@ -370,31 +476,42 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
   f32x4_t adk[4], adv[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) { adk[d] = f32x4_t{0.f, 0.f, 0.f, 0.f}; adv[d] = adk[d]; }
-  TileRegs rq, ro;
-  tile_load(rq, Qb, a.ldq, 0, L, tid);
-  tile_load(ro, Ob, a.lddo, 0, L, tid);
-  float pl = 0.f, pd = 0.f;
-  if (tid < 64) {
-    pl = tid < L ? a.lse[(long long)bh * L + tid] : INFINITY;
-    pd = tid < L ? a.dsum[(long long)bh * L + tid] : 0.f;
-  }
   const int nqb = (L + 63) / 64;
-  for (int qb = 0; qb < nqb; ++qb) {
-    __syncthreads();
-    tile_store(sQ, rq, tid);
-    tile_store(sO, ro, tid);
-    if (tid < 64) { sL[tid] = pl; sD[tid] = pd; }
-    __syncthreads();
-    if (qb + 1 < nqb) {
-      const int nq0 = (qb + 1) * 64;
-      tile_load(rq, Qb, a.ldq, nq0, L, tid);
-      tile_load(ro, Ob, a.lddo, nq0, L, tid);
-      if (tid < 64) {
-        const int qq = nq0 + tid;
-        pl = qq < L ? a.lse[(long long)bh * L + qq] : INFINITY;
-        pd = qq < L ? a.dsum[(long long)bh * L + qq] : 0.f;
-      }
+  // stored keep bits (Drop): the 512-byte tile of words (q = qb*64.., this key tile) is
+  // staged in LDS; this lane's key sits at bit kbit of each word
+  const bool kbits = drop.on && a.keep != nullptr;
+  const uint4* kw = reinterpret_cast<const uint4*>(a.keep + ((long long)bh * nqb + xt) * (nqb * 64) * 8);
+  const int kl = 16 * w + (lane & 15), kbit = 16 * ((kl >> 2) & 3) + 4 * (kl >> 4) + (kl & 3);
+  TileRegs rq, ro;
+  float pl = 0.f, pd = 0.f;
+  uint4 mnext = make_uint4(0, 0, 0, 0);
+  auto fetch = [&](int qbn) {
+    const int nq0 = qbn * 64;
+    tile_load(rq, Qb, a.ldq, nq0, L, tid);
+    tile_load(ro, Ob, a.lddo, nq0, L, tid);
+    if (tid < 64) {
+      const int qq = nq0 + tid;
+      pl = qq < L ? a.lse[(long long)bh * L + qq] : INFINITY;
+      pd = qq < L ? a.dsum[(long long)bh * L + qq] : 0.f;
     }
+    if (kbits && tid < 32) mnext = kw[qbn * 32 + tid];
+  };
+  auto stage = [&](int j) {
+    tile_store(sQ2[j], rq, tid);
+    tile_store(sO2[j], ro, tid);
+    if (tid < 64) { sL2[j][tid] = pl; sD2[j][tid] = pd; }
+    if (kbits && tid < 32) reinterpret_cast<uint4*>(sM2[j])[tid] = mnext;
+  };
+  fetch(0);
+  stage(0);
+  if (nqb > 1) fetch(1);
+  __syncthreads();
+  for (int qb = 0; qb < nqb; ++qb) {
+    const char* sQ = sQ2[qb & 1];
+    const char* sO = sO2[qb & 1];
+    const float* sL = sL2[qb & 1];
+    const float* sD = sD2[qb & 1];
+    const unsigned* sM = sM2[qb & 1];
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -411,15 +528,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * t + 4 * g + i;
-        const float p = fexp2(s[t][i] * sl2 + kb2 - sL[r]);
-        float z = 1.f;
-        if (drop.on) {   // this lane's key pairs with the neighbour lane's key (key ^ 1)
-          float z0, z1;
-          drop.keep2(qb * 64 + r, key & ~1, z0, z1);
-          z = (key & 1) ? z1 : z0;
-        }
-        s[t][i] = p * z;
-        dp[t][i] = p * (dp[t][i] * z - sD[r]);
+        const float p = fexp2(fmaf(s[t][i], sl2, kb2 - sL[r]));
+        int m = -1;
+        if (kbits) m = bitmask(sM[2 * r + (kbit >> 5)], kbit & 31);
+        else if (drop.on) m = drop.keep1(qb * 64 + r, key);
+        // dV takes P (.) Z (1/(1-p) applied at the store), dS = P (.) (dP (.) Z/(1-p) - D)
+        s[t][i] = fmask(p, m);
+        dp[t][i] = p * fmaf(fmask(dp[t][i], m), drop.sc, -sD[r]);
       }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
     const bf16x8_t d0 = pack_p(dp[0], dp[1]), d1 = pack_p(dp[2], dp[3]);
@@ -430,6 +545,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
       adk[d] = MFMA16(frag_tr(sQ, 16 * d, 0, lane), d0, adk[d]);
       adk[d] = MFMA16(frag_tr(sQ, 16 * d, 1, lane), d1, adk[d]);
     }
+    if (qb + 1 < nqb) {   // buffer (qb+1)&1 last held tile qb-1: every wave left it at the last barrier
+      stage((qb + 1) & 1);
+      if (qb + 2 < nqb) fetch(qb + 2);
+      __syncthreads();
+    }
   }
   if (kok) {
     bf16_t* kp = a.dk + (long long)(b * L + key) * a.lddk + h * 64;
@@ -437,37 +557,58 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkv(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       store4(kp + 16 * d + 4 * g, adk[d], a.scale);
-      store4(vp + 16 * d + 4 * g, adv[d], 1.f);
+      store4(vp + 16 * d + 4 * g, adv[d], drop.sc);
     }
   }
 }
 
 bool aligned16(const void* p) { return (((unsigned long long)p) & 15ull) == 0; }
 
+// KUBEML_ATTN_OCC="dq,dkv" waves per SIMD of the backward kernels (default 4,2: dq fits 128
+// VGPRs without spills, dkv needs ~220; the forward always runs at 4 with 120)
+const int* attn_occ() {
+  static int occ[2] = {4, 2};
+  static const bool init = [] {
+    if (const char* e = std::getenv("KUBEML_ATTN_OCC")) std::sscanf(e, "%d,%d", &occ[0], &occ[1]);
+    return true;
+  }();
+  (void)init;
+  return occ;
+}
+
+int xcd_order() {
+  static const int on = [] { const char* e = std::getenv("KUBEML_ATTN_XCD"); return e ? std::atoi(e) : 1; }();
+  return on;
+}
+
 }  // namespace
 
 // q/k/v/out: token-major [B*L, ld*] bf16, head h at column 64h (head_dim must be 64)
-// ctr/salt/pdrop: attention-probability dropout (ctr null or pdrop 0: none)
+// ctr/salt/pdrop: attention-probability dropout (ctr null or pdrop 0: none); keep: null or a
+// [B*H, nkb, 64*nkb] u64 buffer (nkb = ceil(L/64)) that receives the keep bits (Drop)
 KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* out, float* lse,
                          const float* bias, int ldq, int ldk, int ldv, int ldout, int B, int H, int L, float scale,
-                         const float* ctr, int salt, float pdrop, hipStream_t s) {
+                         const float* ctr, int salt, float pdrop, unsigned char* keep, hipStream_t s) {
   if (L <= 0 || B <= 0 || H <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldout % 4) return (int)hipErrorInvalidValue;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v)) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = q; a.k = k; a.v = v; a.out = out; a.lse = lse; a.bias = bias;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldout = ldout;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
-  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop;
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = xcd_order(); a.keep = keep;
   if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_attn_fwd, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
+  const dim3 grid((L + 63) / 64, B * H);
+  hipLaunchKernelGGL(k_attn_fwd<4>, grid, dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();
 }
 
-// dq/dk/dv may point into one fused [B*L, 3*H*64] buffer (ld = 3*H*64); dsum: [B*H*L] fp32 scratch
+// dq/dk/dv may point into one fused [B*L, 3*H*64] buffer (ld = 3*H*64); dsum: [B*H*L] fp32 scratch;
+// keep: the forward's keep bits (read instead of re-hashing), or null
 KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                          const float* lse, float* dsum, const float* bias, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                          int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv, int B, int H,
-                         int L, float scale, const float* ctr, int salt, float pdrop, hipStream_t s) {
+                         int L, float scale, const float* ctr, int salt, float pdrop, const unsigned char* keep,
+                         hipStream_t s) {
   if (L <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
@@ -475,9 +616,13 @@ KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   a.bias = bias; a.dq = dq; a.dk = dk; a.dv = dv;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
-  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop;
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = xcd_order();
+  a.keep = const_cast<unsigned char*>(keep);
   if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_attn_bwd_dq, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_attn_bwd_dkv, dim3((L + 63) / 64, B * H), dim3(256), 0, s, a);
+  const dim3 grid((L + 63) / 64, B * H);
+  if (attn_occ()[0] == 3) hipLaunchKernelGGL(k_attn_bwd_dq<3>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_attn_bwd_dq<4>, grid, dim3(256), 0, s, a);
+  if (attn_occ()[1] == 3) hipLaunchKernelGGL(k_attn_bwd_dkv<3>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_attn_bwd_dkv<2>, grid, dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();
 }

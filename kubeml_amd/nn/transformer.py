@@ -179,8 +179,9 @@ class _AttnFn(Function):
         from ..ops import transformer as T
         D = H * 64
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
-        out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias, drop=drop)
-        ctx.save = (qkv, out, lse, bias)
+        keep = T.attn_keep_buffer(B, H, L, qkv.device) if drop is not None and drop[2] > 0.0 else None
+        out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias, drop=drop, keep=keep)
+        ctx.save = (qkv, out, lse, bias, keep)
         ctx.dims = (B, H, L)
         ctx.drop = drop
         return out
@@ -188,12 +189,12 @@ class _AttnFn(Function):
     @staticmethod
     def backward(ctx, dout):
         from ..ops import transformer as T
-        qkv, out, lse, bias = ctx.save
+        qkv, out, lse, bias, keep = ctx.save
         B, H, L = ctx.dims
         D = H * 64
         dqkv = torch.empty_like(qkv)
         T.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, _bf(dout).contiguous(), lse, B, H, L, bias=bias,
-                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=ctx.drop)
+                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=ctx.drop, keep=keep)
         ctx.save = None
         return dqkv, None, None, None, None, None
 

@@ -37,10 +37,28 @@ def _drop_args(drop):
     return ctr.data_ptr(), int(salt) & 0x7FFFFFFF, float(p)
 
 
-def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None, drop=None):
+def attn_keep_buffer(B, H, L, device):
+    """Buffer for the attention-dropout keep bits the forward writes and the backward reads
+    (attention.hip ``Drop``): one u64 word per (b*h, key tile, query), queries padded to
+    whole 64-row tiles — B*H*L^2/8 bytes, 12.6 MB per BERT-base layer at L = 512."""
+    nkb = (L + 63) // 64
+    return torch.empty(B * H * nkb * nkb * 64 * 8, dtype=torch.uint8, device=device)
+
+
+def _keep_arg(keep, B, H, L, drop):
+    if keep is None or drop is None or drop[2] <= 0.0:
+        return 0
+    nkb = (L + 63) // 64
+    if keep.dtype != torch.uint8 or not keep.is_cuda or keep.numel() < B * H * nkb * nkb * 512:
+        raise ValueError("keep must be a GPU uint8 buffer from attn_keep_buffer(B, H, L)")
+    return keep.data_ptr()
+
+
+def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None, drop=None, keep=None):
     """q/k/v: [B*L, ld] bf16 views with head h at columns 64h..64h+63 (may be column
-    slices of one fused QKV buffer).  drop: (ctr, salt, p) attention-probability dropout.
-    Returns (out [B*L, H*64], lse [B*H, L])."""
+    slices of one fused QKV buffer).  drop: (ctr, salt, p) attention-probability dropout;
+    keep: optional :func:`attn_keep_buffer` that receives the dropout keep bits, so
+    :func:`attn_bwd` reads them instead of re-hashing.  Returns (out [B*L, H*64], lse [B*H, L])."""
     for n, t in (("q", q), ("k", k), ("v", v)):
         _chk_view(t, n)
         if t.shape[0] != B * L or t.shape[1] < H * 64:
@@ -54,13 +72,16 @@ def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None, drop=None):
     lse = torch.empty((B * H, L), dtype=F32, device=q.device)
     scale = 1.0 / math.sqrt(64) if scale is None else scale
     c, salt, pd = _drop_args(drop)
-    HIP.call("kml_attn_fwd", "p p p p p p i i i i i i i f p i f s", _p(q), _p(k), _p(v), _p(out), _p(lse), _p(bias),
-             q.stride(0), k.stride(0), v.stride(0), out.stride(0), B, H, L, float(scale), c, salt, pd, _s())
+    HIP.call("kml_attn_fwd", "p p p p p p i i i i i i i f p i f p s", _p(q), _p(k), _p(v), _p(out), _p(lse),
+             _p(bias), q.stride(0), k.stride(0), v.stride(0), out.stride(0), B, H, L, float(scale), c, salt, pd,
+             _keep_arg(keep, B, H, L, drop), _s())
     return out, lse
 
 
-def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=None, scale=None, drop=None):
-    """Gradients of attention; dq/dk/dv may be column views of one [B*L, 3*H*64] buffer."""
+def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=None, scale=None, drop=None,
+             keep=None):
+    """Gradients of attention; dq/dk/dv may be column views of one [B*L, 3*H*64] buffer.
+    keep: the keep-bit buffer the forward filled (same drop), or None to re-hash the mask."""
     dev = q.device
     if dq is None:
         dq = torch.empty((B * L, H * 64), dtype=BF16, device=dev)
@@ -77,10 +98,10 @@ def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=Non
     dsum = torch.empty((B * H, L), dtype=F32, device=dev)
     scale = 1.0 / math.sqrt(64) if scale is None else scale
     c, salt, pd = _drop_args(drop)
-    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f p i f s",
+    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f p i f p s",
              _p(q), _p(k), _p(v), _p(o), _p(dout), _p(lse), _p(dsum), _p(bias), _p(dq), _p(dk), _p(dv),
              q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
-             dv.stride(0), B, H, L, float(scale), c, salt, pd, _s())
+             dv.stride(0), B, H, L, float(scale), c, salt, pd, _keep_arg(keep, B, H, L, drop), _s())
     return dq, dk, dv
 
 

@@ -237,3 +237,34 @@ def test_gelu_bwd_with_bias_colsum(M, N):
     want = torch.full((N,), 0.5, device=dev)
     K.colsum_(ref, want)
     assert _rel(db, want) < 1e-5
+
+
+@pytest.mark.parametrize("L", [64, 300])
+def test_attention_keep_bits_match_hash(L):
+    """The dropout keep bits the forward stores (attention.hip Drop) decode to the Python
+    replica of the hashed mask, and the backward that reads them is bit-identical to the
+    backward that re-hashes the mask."""
+    import numpy as np
+    from kubeml_amd.ops import transformer as T
+    torch.manual_seed(9)
+    B, H, p = 2, 2, 0.25
+    D = H * 64
+    qkv = (torch.randn(B * L, 3 * D, device="cuda") * 0.5).to(torch.bfloat16)
+    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+    ctr = torch.tensor([11.0, 3.0], device="cuda")
+    drop = (ctr, 7919 * 3, p)
+    kbuf = T.attn_keep_buffer(B, H, L, "cuda")
+    out, lse = T.attn_fwd(q, k, v, B, H, L, drop=drop, keep=kbuf)
+    nkb = (L + 63) // 64
+    w = kbuf.cpu().numpy().view(np.uint64).reshape(B * H, nkb, nkb * 64)
+    key = np.arange(L)
+    kl = key % 64
+    bit = (16 * ((kl // 4) % 4) + 4 * (kl // 16) + kl % 4).astype(np.uint64)
+    got = (w[:, (key // 64)[None, :], np.arange(L)[:, None]] >> bit[None, None, :]) & np.uint64(1)
+    ref = (_attn_keep(11, 3, 7919 * 3, B, H, L, p) != 0).numpy().reshape(B * H, L, L)
+    assert np.array_equal(got.astype(bool), ref)
+    dout = torch.randn(B * L, D, device="cuda").to(torch.bfloat16)
+    g1 = T.attn_bwd(q, k, v, out, dout, lse, B, H, L, drop=drop, keep=kbuf)
+    g2 = T.attn_bwd(q, k, v, out, dout, lse, B, H, L, drop=drop)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
