@@ -7,8 +7,12 @@ batch 256, SGD(lr, weight_decay=1e-4), synchronous gradient all-reduce every ste
 (north-star config 2: K=1), bf16 compute with fp32 master weights.
 
 The step is the framework's own: :func:`kubeml_amd.engine.dp.make_train_step`, the
-builder ``KubeModel.step`` uses on resident workers (stage-split backward, overlapped
-RCCL all-reduce of the flat gradient buffer, fused SGD, one hipGraph replay per step).
+builder ``KubeModel.step`` uses on resident workers (forward, backward, fused SGD, one
+hipGraph replay per step).  With N > 1 the gradient exchange is the measured comm plan
+(``kubeml_amd/parallel/comm_plan.json``; default ``peer:shard:fp32``: the fp32 gradient is
+reduce-scattered straight out of the peers' HBM over xGMI, each rank applies SGD to its 1/N
+of the master inside that kernel, and the bf16 weights are all-gathered — all inside the
+captured step).  At N = 1 no collective runs (``config.sync`` says so).
 
 Data: synthetic CIFAR-10-shaped uint8 images resident in HBM (no network for the
 real dataset); every step runs the full on-device augmentation (random crop 32/pad 4,
@@ -292,11 +296,12 @@ def main():
     last_loss = float(loss.item())
     if getattr(step, "peer", None) is not None:
         step.peer.check()          # a timed-out peer barrier poisons the sums: fail loudly
+    space.sync_master()            # sharded update: complete the fp32 master (no-op otherwise)
     in_sync = None
     if comm:
         # every rank must hold identical weights after K all-reduced steps (checks that the
         # graph-replayed collectives really ran)
-        cs = space.master.double().abs().sum().view(1)
+        cs = (space.master.double().abs().sum() + space.shadow.double().abs().sum()).view(1)
         lo, hi = cs.clone(), cs.clone()
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
@@ -325,7 +330,9 @@ def main():
             "data": "synthetic (CIFAR-10-shaped uint8 in HBM, on-device crop/flip/normalize), random-init weights",
             "config": {"model": "resnet34 (torchvision, ImageNet stem, 1000-class head)", "global_batch": B * world,
                        "per_worker_batch": B, "seq_len": None, "image": "32x32x3", "parallelism": f"dp{world}",
-                       "optimizer": "SGD lr=%g wd=1e-4" % args.lr, "sync": "gradient all-reduce every step (K=1)",
+                       "optimizer": "SGD lr=%g wd=1e-4" % args.lr,
+                       "sync": ("gradient exchange every step (K=1): " + plan.tag()) if plan is not None
+                       else "none (N=1: no collective in the step)",
                        "graph": not args.no_graph,
                        "overlap_segments": bool(comm and len(step.segments) > 1),
                        "graph_comm": bool(getattr(step, "graph_comm", graph_comm) and comm), "bucket_mb": args.bucket_mb,

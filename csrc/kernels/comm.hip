@@ -326,6 +326,143 @@ __global__ __launch_bounds__(PC_BLOCK) void k_pc_ag(float* __restrict__ out, PcP
   pc_finish_call(ctrl, 2u);
 }
 
+// ---- sharded data-parallel update (ZeRO-1 over peer memory) ------------------------------
+// Every rank's flat fp32 gradient, fp32 master and bf16 shadow are IPC-exportable hipMalloc
+// buffers that every peer maps; nothing is staged.  Chunk q = elements [q*C, min((q+1)C, n)),
+// C a multiple of 64, updated by rank q alone:
+//   rs   barrier(seq+1); rank r sums chunk r of the P gradients in rank order (fp32, read in
+//        place over xGMI) and either applies SGD to its master / momentum chunk and writes its
+//        bf16 shadow chunk (fused), or stores the sum into its own gradient chunk (any optimizer
+//        then runs on the chunk range)
+//   ag   barrier(seq+2); rank r copies chunk q of peer q's bf16 shadow into its own, q != r
+//   gm   barrier(seq+1); rank r copies chunk q of peer q's fp32 master (K-AVG, checkpoint, epoch
+//        end: the only times a full fp32 master is read)
+// Link bytes per rank per step: 4(P-1)/P n (gradient) + 2(P-1)/P n (shadow) — the fp32-exact
+// gradient at 3/4 of an fp32 all-reduce, and 1/P of the optimizer pass.
+// Reuse is safe single-buffered: a rank rewrites its gradient (next backward) only after its ag
+// barrier, which every peer enters after its rs reads finished; it rewrites its shadow chunk
+// only after the next rs barrier, which every peer enters after its ag reads finished.  The
+// buffers are written with plain stores by ordinary kernels: the kernel boundary before the
+// publishing launch writes the XCD L2s back, and peers read with system-scope loads.
+struct ZsPeers {
+  const char* flags[PC_MAX_RANKS];   // every rank's barrier region
+  const char* data[PC_MAX_RANKS];    // every rank's gradient / shadow / master buffer
+};
+
+template <int P, bool SGD>
+__global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region, unsigned* ctrl, int rank,
+                                                    long long lo, long long hi, float* __restrict__ own_grad,
+                                                    float* __restrict__ master, float* __restrict__ mom,
+                                                    bf16_t* __restrict__ shadow, const float* __restrict__ lr_ptr,
+                                                    float wd, float momentum, float dampening, int nesterov,
+                                                    const float* __restrict__ first_ptr, float grad_scale,
+                                                    float* __restrict__ adv_ctr, float adv_batch, float adv_n,
+                                                    unsigned long long limit) {
+  if (adv_ctr && blockIdx.x == 0 && threadIdx.x == 0) {  // data-sampler counter (see k_sgd)
+    adv_ctr[1] += 1.f;
+    float st = adv_ctr[2] + adv_batch;
+    if (st >= adv_n) st -= adv_n;
+    adv_ctr[2] = st;
+  }
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PcPeers fl;
+#pragma unroll
+  for (int p = 0; p < P; ++p) fl.region[p] = peers.flags[p];
+  const bool ok = pc_barrier(fl, region, ctrl, rank, P, seq + 1u, limit);
+  const long long nv = (hi - lo) >> 2;  // fp32x4 vectors of this rank's chunk
+  __amdgpu_buffer_rsrc_t rs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(peers.data[p] + lo * 4, (hi - lo) * 4);
+  float lr = 0.f;
+  int first = 0;
+  if constexpr (SGD) {
+    lr = *lr_ptr;
+    first = first_ptr ? (*first_ptr != 0.f) : 0;
+  }
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < nv; v += stride) {
+    float acc[4];
+    if (ok) {
+      uint4 w[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) w[p] = ld_sys16(rs[p], v * 16);
+      Wire<false>::unpack(w[0], acc);
+#pragma unroll
+      for (int p = 1; p < P; ++p) {
+        float x[4];
+        Wire<false>::unpack(w[p], x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += x[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_nanf("");
+    }
+    const long long e = lo + v * 4;
+    if constexpr (SGD) {
+      const float4 W = *reinterpret_cast<const float4*>(master + e);
+      float wv[4] = {W.x, W.y, W.z, W.w}, mv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (mom) {
+        const float4 M = *reinterpret_cast<const float4*>(mom + e);
+        mv[0] = M.x, mv[1] = M.y, mv[2] = M.z, mv[3] = M.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // the k_sgd recurrence, op for op
+        float d = acc[k] * grad_scale + wd * wv[k];
+        if (mom) {
+          mv[k] = first ? d : momentum * mv[k] + (1.f - dampening) * d;
+          d = nesterov ? d + momentum * mv[k] : mv[k];
+        }
+        wv[k] -= lr * d;
+      }
+      *reinterpret_cast<float4*>(master + e) = make_float4(wv[0], wv[1], wv[2], wv[3]);
+      if (mom) *reinterpret_cast<float4*>(mom + e) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      uint2 s;
+      s.x = pack_bf2(wv[0], wv[1]);
+      s.y = pack_bf2(wv[2], wv[3]);
+      *reinterpret_cast<uint2*>(shadow + e) = s;
+    } else {
+      *reinterpret_cast<float4*>(own_grad + e) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+  }
+}
+
+// all-gather of chunks: chunk q of peer q's buffer -> own buffer, q != rank (16-byte vectors;
+// `ve` elements per vector, `esz` bytes per element).  Barrier `bar` of the call; `finish` =
+// barriers this call passes (the last launch of a call advances the sequence).
+template <int P>
+__global__ __launch_bounds__(PC_BLOCK) void k_zs_gather(ZsPeers peers, char* region, unsigned* ctrl, int rank,
+                                                        char* __restrict__ own, long long n, long long chunk, int esz,
+                                                        unsigned bar, unsigned finish, unsigned long long limit) {
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PcPeers fl;
+#pragma unroll
+  for (int p = 0; p < P; ++p) fl.region[p] = peers.flags[p];
+  const bool ok = pc_barrier(fl, region, ctrl, rank, P, seq + bar, limit);
+  const long long cv = chunk * esz / 16;  // vectors per (full) chunk
+  const long long total = (long long)(P - 1) * cv;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < total; j += stride) {
+    int q = (int)(j / cv);
+    const long long v = j - (long long)q * cv;
+    q += (q >= rank);
+    const long long off = (long long)q * chunk * esz + v * 16;  // byte offset in the buffer
+    if (off >= n * esz) continue;                                // the last chunk is short
+    uint4 w;
+    if (ok) {
+      w = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int p = 0; p < P; ++p)  // uniform-index select keeps the descriptors in SGPRs
+        if (p == q) w = ld_sys16(pc_rsrc(peers.data[p] + (long long)p * chunk * esz, chunk * esz), v * 16);
+    } else {
+      const unsigned nan = esz == 2 ? 0x7FC07FC0u : 0x7FC00000u;
+      w = make_uint4(nan, nan, nan, nan);
+    }
+    *reinterpret_cast<uint4*>(own + off) = w;
+  }
+  if (finish) pc_finish_call(ctrl, finish);
+}
+
 // side-stream HBM streamer for the interference probe: `passes` copies of n 16-byte vectors
 __global__ __launch_bounds__(PC_BLOCK) void k_stream_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                           long long n, int passes) {
@@ -464,6 +601,112 @@ KML_API int kml_peer_allreduce(const float* in, float* out, const void* const* r
                                            reinterpret_cast<unsigned*>(ctrl), rank, cap, n, scale, algo, max_blocks,
                                            limit, s);
   return (int)e;
+}
+
+// ---- sharded update (ZeRO-1) entry points ------------------------------------------------
+// IPC-exportable buffer (hipMalloc base, zeroed): a flat gradient / master / shadow peers map
+KML_API int kml_ipc_alloc(long long bytes, void** out) {
+  *out = nullptr;
+  if (bytes <= 0) return (int)hipErrorInvalidValue;
+  hipError_t e = hipMalloc(out, (size_t)bytes);
+  if (e == hipSuccess) e = hipMemset(*out, 0, (size_t)bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess && *out) {
+    (void)hipFree(*out);
+    *out = nullptr;
+  }
+  return (int)e;
+}
+
+KML_API int kml_ipc_free(void* p) { return (int)(p ? hipFree(p) : hipSuccess); }
+
+namespace {
+bool zs_peers(ZsPeers& zp, const void* const* flags, const void* const* data, int world) {
+  zp = {};
+  for (int p = 0; p < world; ++p) {
+    if (!flags[p] || !data[p]) return false;
+    zp.flags[p] = reinterpret_cast<const char*>(flags[p]);
+    zp.data[p] = reinterpret_cast<const char*>(data[p]);
+  }
+  return true;
+}
+unsigned long long zs_limit(double timeout_s) {
+  const double ticks = timeout_s * 1.0e8;
+  return ticks > 1.8e19 ? ~0ull : (unsigned long long)ticks;
+}
+unsigned zs_grid(long long items, int max_blocks) {
+  long long g = (items + PC_BLOCK - 1) / PC_BLOCK;
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+}  // namespace
+
+// reduce-scatter of the flat fp32 gradients: rank's chunk [lo, hi) summed over the group in rank
+// order.  fused_sgd: the sum goes straight into the SGD update of master / mom (may be null) and
+// the bf16 shadow chunk (lr, first flag on device; advance counter as k_sgd); else it is stored
+// into the own gradient chunk.  grads[world] / flags[world]: every rank's buffers as mapped here.
+KML_API int kml_zs_reduce_scatter(const void* const* flags, const void* const* grads, void* region, void* ctrl,
+                                  int rank, int world, long long lo, long long hi, int fused_sgd, float* master,
+                                  float* mom, bf16_t* shadow, const float* lr_ptr, float wd, float momentum,
+                                  float dampening, int nesterov, const float* first_ptr, float grad_scale,
+                                  float* adv_ctr, float adv_batch, float adv_n, int max_blocks, double timeout_s,
+                                  hipStream_t s) {
+  ZsPeers zp;
+  if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || lo < 0 || hi < lo || (lo & 3) ||
+      (hi & 3) || max_blocks < 1 || !(timeout_s > 0.0) || !zs_peers(zp, flags, grads, world) ||
+      zp.flags[rank] != region || (fused_sgd && (!master || !shadow || !lr_ptr)))
+    return (int)hipErrorInvalidValue;
+  float* own = const_cast<float*>(reinterpret_cast<const float*>(grads[rank]));
+  const unsigned g = zs_grid((hi - lo) / 4, max_blocks);
+  const unsigned long long lim = zs_limit(timeout_s);
+  switch (world) {
+#define ZS_CASE(P)                                                                                                   \
+  case P:                                                                                                            \
+    if (fused_sgd)                                                                                                   \
+      hipLaunchKernelGGL((k_zs_rs<P, true>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),     \
+                         reinterpret_cast<unsigned*>(ctrl), rank, lo, hi, own, master, mom, shadow, lr_ptr, wd,      \
+                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim);      \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_zs_rs<P, false>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),    \
+                         reinterpret_cast<unsigned*>(ctrl), rank, lo, hi, own, master, mom, shadow, lr_ptr, wd,      \
+                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim);      \
+    break;
+    ZS_CASE(1) ZS_CASE(2) ZS_CASE(3) ZS_CASE(4) ZS_CASE(5) ZS_CASE(6) ZS_CASE(7) ZS_CASE(8)
+#undef ZS_CASE
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  KML_LAUNCH_CHECK();
+}
+
+// all-gather of chunks (n elements of esz = 2 or 4 bytes, chunk elements per rank, chunk*esz a
+// multiple of 16): barrier `bar` (2 after a reduce-scatter of the same call, 1 standalone);
+// `finish` barriers close the call.
+KML_API int kml_zs_all_gather(const void* const* flags, const void* const* bufs, void* region, void* ctrl, int rank,
+                              int world, long long n, long long chunk, int esz, int bar, int finish, int max_blocks,
+                              double timeout_s, hipStream_t s) {
+  ZsPeers zp;
+  if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || n < 0 || chunk <= 0 ||
+      (esz != 2 && esz != 4) || (chunk * esz) % 16 || chunk * world < n || bar < 1 || finish < 0 ||
+      max_blocks < 1 || !(timeout_s > 0.0) || !zs_peers(zp, flags, bufs, world) || zp.flags[rank] != region)
+    return (int)hipErrorInvalidValue;
+  char* own = const_cast<char*>(reinterpret_cast<const char*>(bufs[rank]));
+  const unsigned g = zs_grid((long long)(world - 1) * chunk * esz / 16, max_blocks);
+  const unsigned long long lim = zs_limit(timeout_s);
+  switch (world) {
+#define ZS_CASE(P)                                                                                                   \
+  case P:                                                                                                            \
+    hipLaunchKernelGGL((k_zs_gather<P>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),         \
+                       reinterpret_cast<unsigned*>(ctrl), rank, own, n, chunk, esz, (unsigned)bar, (unsigned)finish,  \
+                       lim);                                                                                         \
+    break;
+    ZS_CASE(1) ZS_CASE(2) ZS_CASE(3) ZS_CASE(4) ZS_CASE(5) ZS_CASE(6) ZS_CASE(7) ZS_CASE(8)
+#undef ZS_CASE
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  KML_LAUNCH_CHECK();
 }
 
 // device wall-clock stamp (100 MHz ticks) into buf[idx]: brackets the collectives inside a

@@ -30,6 +30,7 @@ class Config:
     host: str = "127.0.0.1"
     num_gpus: int = -1            # -1: autodetect (torch.cuda.device_count), 0: CPU workers
     num_cpu_workers: int = 2      # worker processes when no GPU is present
+    workers_per_gpu: int = 1      # >1 packs several workers on each GPU (reference get_gpu: func_id % devices)
     max_parallelism: int = -1     # clamp for the elastic policy (-1: number of workers)
     dtype: str = "bf16"
     bucket_mb: float = 64.0       # gradient all-reduce bucket (xGMI: few, large collectives)
@@ -57,6 +58,7 @@ class Config:
             "scheduler_port": "KUBEML_SCHEDULER_PORT", "ps_port": "KUBEML_PS_PORT",
             "storage_port": "KUBEML_STORAGE_PORT", "metrics_port": "KUBEML_METRICS_PORT",
             "host": "KUBEML_HOST", "num_gpus": "KUBEML_NUM_GPUS", "num_cpu_workers": "KUBEML_NUM_CPU_WORKERS",
+            "workers_per_gpu": "KUBEML_WORKERS_PER_GPU",
             "max_parallelism": "KUBEML_MAX_PARALLELISM", "dtype": "KUBEML_DTYPE", "bucket_mb": "KUBEML_BUCKET_MB",
             "fault": "KUBEML_FAULT",
         }
@@ -78,8 +80,8 @@ class Config:
         return p
 
 
-def detect_workers(cfg: Config) -> tuple:
-    """(n_workers, use_gpu) for this node: one worker per MI355X, else CPU workers."""
+def physical_gpus(cfg: Config) -> int:
+    """GPUs on this node (``num_gpus``, else counted without initialising HIP)."""
     n = cfg.num_gpus
     if n < 0:
         try:
@@ -87,6 +89,14 @@ def detect_workers(cfg: Config) -> tuple:
             n = torch.cuda.device_count()
         except Exception:
             n = 0
+    return max(0, n)
+
+
+def detect_workers(cfg: Config) -> tuple:
+    """(n_workers, use_gpu) for this node: ``workers_per_gpu`` workers per MI355X (one by
+    default), else CPU workers.  Worker slot s runs on GPU ``s % gpus`` (reference
+    python/kubeml/kubeml/util.py:13-34, ``func_id % device_count``)."""
+    n = physical_gpus(cfg)
     if n > 0:
-        return n, True
+        return n * max(1, cfg.workers_per_gpu), True
     return max(1, cfg.num_cpu_workers), False

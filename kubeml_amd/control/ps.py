@@ -97,8 +97,9 @@ class ParameterServer:
     def __init__(self, store_dir: str, n_workers: int, use_gpu: bool, metrics: Optional[Metrics] = None,
                  scheduler=None, max_parallelism: int = -1, freeze_parallelism: bool = False,
                  worker_env: Optional[Dict[str, str]] = None, task_timeout: float = 3600.0,
-                 worker_threads: int = 1):
+                 worker_threads: int = 1, n_gpus: Optional[int] = None):
         self.store_dir = store_dir
+        self.n_gpus = n_gpus          # physical GPUs: slot s runs on GPU s % n_gpus
         self.inventory = Inventory(n_workers, use_gpu)
         self.use_gpu = use_gpu
         self.metrics = metrics or Metrics()
@@ -142,7 +143,7 @@ class ParameterServer:
             with self._lock:
                 self.alloc[job.id] = ids
         pool = WorkerPool(len(ids), self.use_gpu, self.store_dir, gpu_ids=ids, env=self.worker_env,
-                          timeout=self.task_timeout, threads=self.worker_threads)
+                          timeout=self.task_timeout, threads=self.worker_threads, n_gpus=self.n_gpus)
         return pool.start()
 
     # ------------------------------------------------------------------ API (ps/api.go)
@@ -241,7 +242,7 @@ class ParameterServer:
                 ids = self.inventory.acquire(1)
                 self._infer_ids = ids
                 self._infer_pool = WorkerPool(1, self.use_gpu, self.store_dir, gpu_ids=ids, env=self.worker_env,
-                                              timeout=self.task_timeout).start()
+                                              timeout=self.task_timeout, n_gpus=self.n_gpus).start()
                 self.metrics.task_started("inference")
             msg = {"op": "task", "kind": "infer", "job": f"infer-{req.model_id}", "function": fn,
                    "code_path": self.functions.code_path(fn), "N": 1, "K": -1, "batch_size": hist.task.batch_size,

@@ -16,7 +16,7 @@ import signal
 import threading
 from typing import Dict, Optional
 
-from ..config import Config, detect_workers
+from ..config import Config, detect_workers, physical_gpus
 from ..metrics import Metrics
 from ..store import service as storage_service
 from ..store.shards import ShardStore
@@ -52,7 +52,8 @@ class KubeMLServer:
         self.ps = ParameterServer(self.cfg.store_dir, n, gpu, metrics=self.metrics, scheduler=self.scheduler,
                                   max_parallelism=max_p,
                                   freeze_parallelism=self.cfg.debug_env or self.cfg.limit_parallelism,
-                                  worker_env=worker_env, task_timeout=task_timeout, worker_threads=worker_threads)
+                                  worker_env=worker_env, task_timeout=task_timeout, worker_threads=worker_threads,
+                                  n_gpus=(physical_gpus(self.cfg) or None) if gpu else None)
         self.scheduler.ps = self.ps
         self.controller = Controller(self.cfg.store_dir, self.scheduler, self.ps, shards=self.shards)
         self.servers: Dict[str, Server] = {}

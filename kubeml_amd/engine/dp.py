@@ -60,7 +60,23 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             every T-th step (``step.comm_seconds()``; exported as kubeml_allreduce_seconds)
     """
     comm = world > 1 or force_comm
-    if plan is not None:
+    shard = None
+    if plan is not None and plan.schedule == "shard":
+        on_gpu = comm and torch.cuda.is_available() and space.grad.is_cuda
+        if on_gpu:
+            from ..parallel.peer import PeerShard, verified_shard
+            shard = peer if isinstance(peer, PeerShard) and peer.space is space and peer.region is not None else None
+            if shard is None:
+                shard = verified_shard(space, group, log=_log.warning)     # collective over group
+        if shard is None:
+            # no IPC buffers / self-test failed (every rank alike) / CPU group: exact all-reduce
+            from ..parallel.plan import CommPlan
+            plan = CommPlan("peer" if on_gpu else "rccl", "end" if on_gpu else "overlap", "fp32", plan.max_blocks,
+                            source=f"{plan.source} (shard unavailable)")
+        peer = shard
+        if shard is not None:
+            overlap = False                   # the update is one collective after the backward
+    if plan is not None and shard is None:
         overlap = plan.schedule == "overlap"
         comm_dtype = plan.wire_dtype
         if plan.backend == "peer" and comm and peer is None and torch.cuda.is_available() and space.grad.is_cuda:
@@ -150,6 +166,31 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             backward_loss(loss)
             space.finish_grads()
             return loss
+    shard_step = on_replay = None
+    if shard is not None:
+        blocks = plan.max_blocks
+        fused_sgd = getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges()
+        if not (fused_sgd or getattr(optimizer, "supports_ranges", lambda: False)()):
+            raise ValueError("the shard plan needs a fused optimizer over one flat space")
+
+        def shard_step():
+            space.finish_grads()
+            if fused_sgd:           # reduce-scatter + SGD + shadow chunk in one pass
+                shard.reduce_scatter(optimizer, advance=fold, max_blocks=blocks)
+            else:
+                shard.reduce_scatter(None, max_blocks=blocks)
+                optimizer.set_grad_scale(scale)
+                optimizer.step_range(shard.lo, shard.hi, max_blocks=blocks)
+                if fold is not None:
+                    from ..ops import kernels as K
+                    K.advance_counter_(*fold)
+            shard.all_gather_shadow(max_blocks=blocks)
+            if post is not None:
+                post()
+
+        def on_replay():
+            space._master_stale = True
+
     optimizer.set_grad_scale(scale)
     return GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
@@ -157,4 +198,5 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             state_tensors=train_state_tensors(model, space, optimizer, extra_state),
                             segment_opt=seg_opt, opt_finish=opt_finish, peer=peer,
                             schedule=plan.schedule if plan is not None else "overlap",
-                            peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing)
+                            peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing,
+                            shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1))

@@ -144,7 +144,8 @@ class GraphedTrainStep:
                  state_tensors: Sequence[torch.Tensor] = (), comm_dtype=torch.float32,
                  segment_opt: Optional[Sequence[Callable[[], None]]] = None,
                  opt_finish: Optional[Callable[[], None]] = None, peer=None, schedule: str = "overlap",
-                 peer_blocks: int = 256, comm_timing: int = 0):
+                 peer_blocks: int = 256, comm_timing: int = 0, shard_step: Optional[Callable[[], None]] = None,
+                 on_replay: Optional[Callable[[], None]] = None, world: Optional[int] = None):
         if segments is None:
             if fwd_bwd is None:
                 raise ValueError("need fwd_bwd or segments")
@@ -156,7 +157,12 @@ class GraphedTrainStep:
             raise ValueError("segment_grads must have one entry per segment")
         self.opt_step = opt_step
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        # world: ranks of THIS step's gradient exchange.  Given explicitly by make_train_step: a
+        # local step (world 1) of a process that belongs to a larger default group must not
+        # reduce over that group
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = int(world)
         # force_comm: issue the collectives even on a 1-rank group (exercises RCCL next to
         # the captured graphs on a single-GPU box)
         self.comm = self.world > 1 or (force_comm and dist.is_available() and dist.is_initialized())
@@ -181,10 +187,16 @@ class GraphedTrainStep:
         # peer backend (parallel/peer.py): plain kernels, so the collectives always live in
         # the step's one graph; "end" = one all-reduce per view after the whole backward on
         # the compute stream, "overlap" = per segment on a side stream (block-capped)
-        if schedule not in ("end", "overlap"):
-            raise ValueError("schedule must be 'end' or 'overlap'")
+        if schedule not in ("end", "overlap", "shard"):
+            raise ValueError("schedule must be 'end', 'overlap' or 'shard'")
+        if schedule == "shard" and shard_step is None:
+            raise ValueError("the shard schedule needs shard_step (reduce-scatter, update, all-gather)")
         self.peer = peer if self.comm else None
         self.schedule = schedule
+        # shard: the optimizer is part of the collective (parallel/peer.py PeerShard) — with the
+        # collectives on, shard_step replaces opt_step; the local warm-up still runs opt_step
+        self.shard_step = shard_step if self.comm else None
+        self.on_replay = on_replay      # host bookkeeping after every replay (e.g. master now sharded)
         self.peer_blocks = int(peer_blocks)
         self._peer_side = None
         if self.peer is not None and self.segment_opt is not None:
@@ -281,7 +293,7 @@ class GraphedTrainStep:
     def _issue(self, k):
         """Async all-reduce of the gradients finished by segment k (bf16-compressed with
         ``comm_dtype=torch.bfloat16``: the widening back runs in :meth:`_finish_comm`)."""
-        if not (self.comm and self._comm_on):
+        if not (self.comm and self._comm_on) or self.shard_step is not None:
             return []
         views = list(self._views(k))
         if not views:
@@ -342,7 +354,13 @@ class GraphedTrainStep:
                 loss = out
             works += self._issue(k)
         self._finish_comm(works)
-        self.opt_step()
+        if self.shard_step is not None and self._comm_on:
+            dev = self._dev
+            self._stamp(0, dev)
+            self.shard_step()
+            self._stamp(1, dev)
+        else:
+            self.opt_step()
         return loss
 
     def _debug_fork(self):
@@ -392,7 +410,7 @@ class GraphedTrainStep:
     def prime_comm(self):
         """One eager all-reduce of every gradient view (sets up RCCL connections before
         the first capture).  Call on ALL ranks at the same point."""
-        if not self.comm or self.peer is not None:
+        if not self.comm or self.peer is not None or self.shard_step is not None:
             return
         for k in range(len(self.segments)):
             for v in self._views(k):
@@ -421,7 +439,7 @@ class GraphedTrainStep:
         # capture; "thread_local" keeps its (uncaptured) queries from invalidating the
         # capture.  Nothing on this thread makes an unsafe call inside a capture.
         mode = "thread_local" if self.comm else "global"
-        if self.comm and trace.enabled():
+        if self.comm and trace.enabled() and self.shard_step is None:
             self.graph_comm = False   # keep the collectives outside the graph so they can be timed
         captured_all = False
         if not self.comm or self.graph_comm:
@@ -432,8 +450,10 @@ class GraphedTrainStep:
                 self.g_all, self.g_seg, self.g_opt = g, [], None
                 captured_all = True
             except RuntimeError as e:
-                if not self.comm:
+                if not self.comm or self.shard_step is not None:
                     raise
+                import traceback
+                traceback.print_exc()
                 # the collectives would not capture on this RCCL/driver build: every rank hits
                 # the same op, so all fall back together to per-segment graphs with eager
                 # collectives between the replays
@@ -463,6 +483,8 @@ class GraphedTrainStep:
         self.captured = True
 
     def __call__(self):
+        if self.on_replay is not None:
+            self.on_replay()
         if not self.captured:
             self.loss = self._body()
             return self.loss

@@ -98,11 +98,27 @@ class FlatParamSpace:
         self.n_i64 = len(self.i64_buffers)
         self.count_idx = self.i64_off + self.n_i64
         self.state_numel = -(-(self.count_idx + 1) // ALIGN) * ALIGN
-        self.state = torch.zeros(self.state_numel, dtype=torch.float32, device=self.device)
+        # GPU: state / grad / shadow each at the base of an IPC-exportable allocation, so the
+        # peers of a data-parallel group can read them in place (parallel/peer.py PeerShard)
+        bufs = None
+        if self.device.type == "cuda" and with_shadow:
+            from ..parallel.peer import ipc_zeros
+            bufs = (ipc_zeros(self.state_numel, torch.float32, self.device),
+                    ipc_zeros(self.numel, torch.float32, self.device),
+                    ipc_zeros(self.numel, torch.bfloat16, self.device))
+            if any(b is None for b in bufs):
+                bufs = None
+        self.ipc = bufs is not None
+        if bufs is None:
+            bufs = (torch.zeros(self.state_numel, dtype=torch.float32, device=self.device),
+                    torch.zeros(self.numel, dtype=torch.float32, device=self.device),
+                    torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device) if with_shadow else None)
+        self.state, self.grad, self.shadow = bufs
         self.master = self.state[:self.numel]
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-        self.shadow = (torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device)
-                       if with_shadow else None)
+        # sharded (ZeRO-1) update: the fp32 master is complete only on this rank's chunk until
+        # master_sync (the shard transport's gather) runs; see sync_master()
+        self.master_sync = None
+        self._master_stale = False
         with torch.no_grad():
             for p, (shape, view, n), (o, _) in zip(self.params, specs, self.offsets):
                 st = self.master[o:o + n].view(shape)
@@ -161,6 +177,14 @@ class FlatParamSpace:
         return self.i64_arena
 
     # ------------------------------------------------------------------ utilities
+    def sync_master(self):
+        """Complete a sharded fp32 master (collective over the shard group; no-op when every
+        chunk is current).  Call before anything reads the full master: K-AVG, checkpoints,
+        checksums."""
+        if self._master_stale and self.master_sync is not None:
+            self.master_sync()
+        self._master_stale = False
+
     def refresh_shadow(self):
         """bf16 shadow := master (after init, load_state_dict, K-AVG averaging)."""
         if self.shadow is None:

@@ -201,7 +201,7 @@ class SGD(FusedOptimizer):
         return len(spaces) == 1 and not loose
 
     @torch.no_grad()
-    def step_range(self, start: int, end: int):
+    def step_range(self, start: int, end: int, max_blocks: int = 0):
         """The fused step restricted to flat elements [start, end): the gradients of a
         finished backward stage are applied while earlier stages still run backward.  The
         first-step flag stays set until :meth:`finish_ranges` (every range of the step
@@ -222,7 +222,7 @@ class SGD(FusedOptimizer):
                None if sp.shadow is None else sp.shadow[start:end], g["lr"], wd=g["weight_decay"],
                momentum=g["momentum"], dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
                grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first,
-               max_blocks=_RANGE_BLOCKS)
+               max_blocks=max_blocks or _RANGE_BLOCKS)
 
     @torch.no_grad()
     def finish_ranges(self):
@@ -315,6 +315,30 @@ class Adam(FusedOptimizer):
         if loose:
             _torch_adam(loose, g, self.state, self._grad_scale, self.decoupled)
         return loss
+
+    def supports_ranges(self) -> bool:
+        spaces, loose = self._flat_groups()
+        return len(spaces) == 1 and not loose and spaces[0][0].device.type == "cuda"
+
+    @torch.no_grad()
+    def step_range(self, start: int, end: int, max_blocks: int = 0):
+        """The fused step over flat elements [start, end) only (a sharded update: this rank
+        owns that chunk of the master and its moments); advances the step counter."""
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        spaces, loose = self._flat_groups()
+        if len(spaces) != 1 or loose:
+            raise ValueError("step_range needs all parameters in one flat space")
+        sp = spaces[0][0]
+        self._step_host += 1
+        from ..ops import kernels as K
+        st = self._step_dev_inc(sp.device)
+        bufs = self._bufs(sp, ["exp_avg", "exp_avg_sq"])
+        if end > start:
+            K.adam_(sp.master[start:end], sp.grad[start:end], bufs["exp_avg"][start:end],
+                    bufs["exp_avg_sq"][start:end], None if sp.shadow is None else sp.shadow[start:end], g["lr"], 0.0,
+                    b1, b2, g["eps"], g["weight_decay"], self.decoupled, self._grad_scale,
+                    lr_dev=self.lr_tensor(sp.device), step_dev=st)
 
     def _step_dev_inc(self, device):
         from ..ops import kernels as K

@@ -97,9 +97,17 @@ _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "avg": "AVG"}
 
 
 class TorchComm(Comm):
-    """torch.distributed group (RCCL over xGMI on MI355X, gloo on CPU)."""
+    """torch.distributed group (RCCL over xGMI on MI355X, gloo on CPU).
 
-    def __init__(self, group=None, ranks: Optional[List[int]] = None, parent: "TorchComm" = None):
+    ``peer_data=True`` (GPU workers bootstrapped over gloo — e.g. several workers packed on one
+    GPU, which RCCL refuses): the data plane is the peer-memory transport.  fp32 CUDA sums,
+    averages and broadcasts go through a :class:`~kubeml_amd.parallel.peer.PeerAllReduce` grown
+    on demand to the largest tensor seen (growing is collective; every member reduces the same
+    sizes in the same order, so they grow together); other CUDA dtypes bounce through host
+    memory over gloo."""
+
+    def __init__(self, group=None, ranks: Optional[List[int]] = None, parent: "TorchComm" = None,
+                 peer_data: bool = False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -109,7 +117,8 @@ class TorchComm(Comm):
         self.world = len(self.ranks)
         self._subs: Dict[int, "TorchComm"] = {}
         self._parent = parent
-        self.peer = None          # small/large fp32 reductions (enable_peer)
+        self.peer_data = peer_data
+        self.peer = None          # small/large fp32 reductions (enable_peer / peer_data)
         self.grad_peer = None     # the train step's gradient all-reduce (engine/dp.py, plan "peer")
 
     @property
@@ -128,25 +137,89 @@ class TorchComm(Comm):
 
     def check(self):
         """Raise :class:`~kubeml_amd.parallel.peer.PeerCommError` if a peer all-reduce of
-        this group (or of its sub-groups) timed out; synchronises the device."""
-        for p in (self.peer, self.grad_peer):
-            if p is not None:
+        this group (or of its sub-groups) timed out; synchronises the device.  A poisoned
+        transport is dropped first (its results are NaN for good): the next collective that
+        needs one builds a fresh one, collectively."""
+        err = None
+        for name in ("peer", "grad_peer"):
+            p = getattr(self, name)
+            if p is None:
+                continue
+            try:
                 p.check()
+            except Exception as e:
+                err = err or e
+                self._drop(name)
         for c in self._subs.values():
-            c.check()
+            try:
+                c.check()
+            except Exception as e:
+                err = err or e
+        if err is not None:
+            raise err
+
+    def _drop(self, name):
+        """Unmap and free a transport WITHOUT a group barrier (its group may be broken)."""
+        p = getattr(self, name)
+        setattr(self, name, None)
+        if p is not None:
+            try:
+                p._release()
+            except Exception:
+                pass
+
+    def drop_peers(self):
+        """Forget every peer transport of this group and its sub-groups (non-collective)."""
+        for name in ("peer", "grad_peer"):
+            self._drop(name)
+        for c in self._subs.values():
+            c.drop_peers()
+
+    def _peer_for(self, t, need_algo="auto"):
+        """The peer transport for ``t`` (grown collectively when ``t`` no longer fits), or None."""
+        if self.peer is not None and self.peer.supports(t):
+            return self.peer
+        if not (self.peer_data and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+            return None
+        from .peer import DEFAULT_CAP, PeerAllReduce, slot_bytes
+        cap = max(DEFAULT_CAP, slot_bytes(t.numel(), self.world, "twoshot"), slot_bytes(t.numel(), self.world, "oneshot"))
+        if self.peer is not None:
+            cap = max(cap, self.peer.cap)
+            self.peer.close()
+        self.peer = PeerAllReduce(self.group, cap_bytes=cap, device=t.device)
+        return self.peer
+
+    def _host_bounce(self, t, fn):
+        """gloo collective on a host copy of a CUDA tensor (peer_data mode, non-fp32 dtypes)."""
+        h = t.detach().cpu()
+        fn(h)
+        t.copy_(h)
+        return t
 
     def all_reduce_(self, t, op="sum"):
         if self.world == 1:
             return t
-        if self.peer is not None and op in ("sum", "avg") and self.peer.supports(t):
-            return self.peer.all_reduce_(t, 1.0 / self.world if op == "avg" else 1.0)
+        if op in ("sum", "avg"):
+            peer = self._peer_for(t)
+            if peer is not None:
+                return peer.all_reduce_(t, 1.0 / self.world if op == "avg" else 1.0)
         o = getattr(self.dist.ReduceOp, _OPS[op])
+        if self.peer_data and t.is_cuda:
+            return self._host_bounce(t, lambda h: self.dist.all_reduce(h, op=o, group=self.group))
         self.dist.all_reduce(t, op=o, group=self.group)
         return t
 
     def broadcast_(self, t, src=0):
         if self.world == 1:
             return t
+        if self.peer_data and t.is_cuda:
+            peer = self._peer_for(t) if t.dtype == torch.float32 and t.is_contiguous() else None
+            if peer is not None:
+                # broadcast = sum with zeros from every other rank: exact (x + 0 = x)
+                if self.rank != src:
+                    t.zero_()
+                return peer.all_reduce_(t, 1.0)
+            return self._host_bounce(t, lambda h: self.dist.broadcast(h, src=self.ranks[src], group=self.group))
         self.dist.broadcast(t, src=self.ranks[src], group=self.group)
         return t
 
@@ -176,7 +249,7 @@ class TorchComm(Comm):
         if c is None:
             ranks = self.ranks[:parallelism]
             g = self.dist.new_group(ranks=ranks)  # every world rank must call this, in order
-            c = TorchComm(g, ranks, parent=self)
+            c = TorchComm(g, ranks, parent=self, peer_data=self.peer_data)
             self._subs[parallelism] = c
         return c
 

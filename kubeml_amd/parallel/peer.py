@@ -227,6 +227,272 @@ def verified_peer(group=None, cap_bytes: int = DEFAULT_CAP, device: Optional[tor
     return None
 
 
+# ---------------------------------------------------------------------------------------------
+# IPC-exportable device buffers and the sharded (ZeRO-1) update
+# ---------------------------------------------------------------------------------------------
+class _IpcBlock:
+    """One hipMalloc allocation (an IPC handle covers it from its base) exposed to torch through
+    ``__cuda_array_interface__``; freed when the last tensor viewing it dies."""
+
+    def __init__(self, nbytes: int, device: torch.device):
+        out = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            HIP.call("kml_ipc_alloc", "l p", int(nbytes), ctypes.addressof(out))
+        self.ptr, self.nbytes, self.device = out.value, int(nbytes), device
+        self.__cuda_array_interface__ = {"shape": (self.nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 2}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                HIP.raw("kml_ipc_free", self.ptr)
+        except Exception:
+            pass
+        self.ptr = None
+
+
+_IPC_OK = None
+
+
+def ipc_zeros(numel: int, dtype: torch.dtype, device) -> Optional[torch.Tensor]:
+    """Zeroed device tensor at the base of its own hipMalloc allocation (so peers can map it with
+    an IPC handle), or None where this torch build cannot wrap foreign device memory."""
+    global _IPC_OK
+    if _IPC_OK is False or os.environ.get("KUBEML_IPC_FLAT", "1") == "0":
+        return None
+    device = torch.device(device)
+    esz = torch.tensor([], dtype=dtype).element_size()
+    try:
+        blk = _IpcBlock(max(16, numel * esz), device)
+        t = torch.as_tensor(blk, device=device)
+        if t.data_ptr() != blk.ptr or t.device != device:
+            raise RuntimeError("foreign device memory not wrapped in place")
+        _IPC_OK = True
+        return t[:numel * esz].view(dtype)
+    except Exception as e:   # pragma: no cover - depends on the torch build
+        if _IPC_OK is None:
+            import logging
+            logging.getLogger("kubeml.peer").warning("IPC flat buffers unavailable (%r): the sharded "
+                                                     "update falls back to the all-reduce plans", e)
+        _IPC_OK = False
+        return None
+
+
+def _handle_of(ptr: int) -> bytes:
+    nb = HIP.raw("kml_ipc_handle_bytes")
+    h = (ctypes.c_char * nb)()
+    HIP.call("kml_ipc_get_handle", "p p", ptr, ctypes.addressof(h))
+    return bytes(h)
+
+
+class PeerShard:
+    """ZeRO-1 data-parallel update of one flat parameter space over a one-node group.
+
+    Every rank's fp32 gradient, fp32 master (the head of ``space.state``) and bf16 shadow are
+    IPC buffers (:func:`ipc_zeros`); every rank maps every peer's.  One step is two launches
+    (``csrc/kernels/comm.hip`` k_zs_rs / k_zs_gather): rank r reduces chunk r of the P gradients
+    in rank order straight from the peers' HBM (fp32, exact sums, no staging copy) and applies
+    the optimizer to its 1/P of the master — fused into the same pass for SGD — then every rank
+    gathers the peers' freshly written bf16 shadow chunks, which are the weights the next forward
+    reads.  The fp32 master is complete only on its owner's chunk; :meth:`gather_master` (one
+    launch) completes it where the full master is read: K-AVG rounds, checkpoints, epoch ends.
+
+    Link bytes per rank and step: 4(P-1)/P n + 2(P-1)/P n — an fp32-exact gradient at 3/4 of an
+    fp32 all-reduce, with 1/P of the optimizer pass instead of all of it on every rank.
+    Construction is collective over ``group``; failures are loud like :class:`PeerAllReduce`.
+    Reference counterpart: the job's fp32 merge + average (ml/pkg/model/parallelSGD.go:26-54)."""
+
+    def __init__(self, space, group=None, timeout_s: float = DEFAULT_TIMEOUT_S):
+        import torch.distributed as dist
+        self.dist, self.group, self.space = dist, group, space
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > PeerAllReduce.MAX_RANKS:
+            raise ValueError(f"sharded update supports up to {PeerAllReduce.MAX_RANKS} ranks (one node)")
+        if not getattr(space, "ipc", False):
+            raise PeerCommError("sharded update needs IPC flat buffers (nn/flat.py, KUBEML_IPC_FLAT)")
+        self.timeout_s = float(timeout_s)
+        self.device = space.device
+        self.n = int(space.numel)
+        self.chunk = -(-self.n // (self.world * 64)) * 64
+        self.lo = min(self.n, self.rank * self.chunk)
+        self.hi = min(self.n, self.lo + self.chunk)
+        self.opened: List[int] = []
+        self.region = self.ctrl = None
+        err = ""
+        with torch.cuda.device(self.device):
+            region, ctrl = ctypes.c_void_p(), ctypes.c_void_p()
+            HIP.call("kml_peer_alloc", "l p p", 16, ctypes.addressof(region), ctypes.addressof(ctrl))
+            self.region, self.ctrl = region.value, ctrl.value
+            mine = [self.region, space.grad.data_ptr(), space.shadow.data_ptr(), space.state.data_ptr()]
+            hs = [_handle_of(p) for p in mine]
+            allh: List[list] = [None] * self.world
+            dist.all_gather_object(allh, hs, group=group)
+            cols: List[list] = [[0] * self.world for _ in range(4)]
+            try:
+                for p in range(self.world):
+                    for k in range(4):
+                        if p == self.rank:
+                            cols[k][p] = mine[k]
+                            continue
+                        nb = len(allh[p][k])
+                        buf = (ctypes.c_char * nb).from_buffer_copy(allh[p][k])
+                        out = ctypes.c_void_p()
+                        HIP.call("kml_ipc_open", "p p", ctypes.addressof(buf), ctypes.addressof(out))
+                        self.opened.append(out.value)
+                        cols[k][p] = out.value
+                torch.cuda.synchronize(self.device)
+            except Exception as e:
+                err = f"rank {self.rank}: {e!r}"[:300]
+            arr = ctypes.c_void_p * self.world
+            self._flags, self._grads, self._shadows, self._states = (arr(*c) for c in cols)
+        errs: List[str] = [""] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        if any(errs):
+            self._release()
+            raise PeerCommError("sharded update setup failed: " + "; ".join(e for e in errs if e))
+        space.master_sync = self.gather_master
+
+    # ------------------------------------------------------------------ the step
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def reduce_scatter(self, optimizer=None, advance=None, max_blocks: int = 256):
+        """Chunk ``[lo, hi)`` := sum over ranks.  With a fused-SGD ``optimizer`` the sum is
+        applied at once (master, momentum, shadow of the chunk; 1/P folded in); else it lands in
+        the own gradient chunk for :meth:`update_range`."""
+        sp = self.space
+        if self.region is None:
+            raise PeerCommError("sharded update used after close()")
+        fused = optimizer is not None
+        mom = first = lr = None
+        wd = momentum = dampening = 0.0
+        nesterov = 0
+        if fused:
+            g = optimizer.param_groups[0]
+            wd, momentum, dampening, nesterov = g["weight_decay"], g["momentum"], g["dampening"], int(g["nesterov"])
+            lr = optimizer.lr_tensor(sp.device)
+            if momentum != 0:
+                mom = optimizer._bufs(sp, ["momentum"])["momentum"]
+                first = optimizer.first_tensor(sp.device)
+        ctr, ab, an = advance if advance is not None else (None, 0.0, 0.0)
+        HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d s",
+                 ctypes.addressof(self._flags), ctypes.addressof(self._grads), self.region, self.ctrl, self.rank,
+                 self.world, self.lo, self.hi, int(fused), sp.master.data_ptr() if fused else None,
+                 mom.data_ptr() if mom is not None else None, sp.shadow.data_ptr() if fused else None,
+                 lr.data_ptr() if lr is not None else None, float(wd), float(momentum), float(dampening), nesterov,
+                 first.data_ptr() if first is not None else None, 1.0 / self.world,
+                 ctr.data_ptr() if ctr is not None else None, float(ab), float(an), int(max_blocks),
+                 self.timeout_s, self._stream())
+        if first is not None:
+            from ..ops import kernels as K
+            K.fill_(first, 0.0)
+
+    def all_gather_shadow(self, max_blocks: int = 256):
+        """Every rank's shadow := the owners' freshly updated chunks (closes the step's call)."""
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d s", ctypes.addressof(self._flags),
+                 ctypes.addressof(self._shadows), self.region, self.ctrl, self.rank, self.world, self.n,
+                 self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, self._stream())
+        self.space._master_stale = True
+
+    def gather_master(self, max_blocks: int = 256):
+        """Collective: complete the fp32 master from the owners' chunks (one barrier)."""
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d s", ctypes.addressof(self._flags),
+                 ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
+                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, self._stream())
+        self.space._master_stale = False
+
+    # ------------------------------------------------------------------ health
+    def errors(self) -> int:
+        if self.ctrl is None:
+            return 0
+        out = ctypes.c_uint(0)
+        HIP.call("kml_peer_errors", "p p", self.ctrl, ctypes.addressof(out))
+        return int(out.value)
+
+    def check(self):
+        n = self.errors()
+        if n:
+            raise PeerCommError(f"sharded update: {n} barrier wait(s) on rank {self.rank}/{self.world} timed out "
+                                f"after {self.timeout_s:g} s (a peer stopped calling); results since then are NaN")
+
+    def self_test(self) -> bool:
+        """Collective: reduce-scatter / gather the space's own buffers on rank-dependent integer
+        patterns (exact in fp32 and bf16), compare with the closed forms, restore the buffers.
+        True on every rank only if every rank was exact and no wait timed out."""
+        sp = self.space
+        ok = True
+        saved = [t.clone() for t in (sp.grad, sp.shadow, sp.state)]
+        try:
+            idx = torch.arange(self.n, device=self.device)
+            base = (idx % 8).float()
+            sp.grad.copy_(base * float(self.rank + 1))
+            self.reduce_scatter()
+            tri = float(self.world * (self.world + 1) // 2)
+            ok = ok and bool(torch.equal(sp.grad[self.lo:self.hi], base[self.lo:self.hi] * tri))
+            owner = torch.div(idx, self.chunk, rounding_mode="floor").float()
+            sp.shadow.copy_(((owner == self.rank).float() * (base + owner)).to(torch.bfloat16))
+            self.all_gather_shadow()
+            ok = ok and bool(torch.equal(sp.shadow.float(), base + owner))
+            sp.master.copy_((owner == self.rank).float() * (base * 3 + owner))
+            self.gather_master()
+            ok = ok and bool(torch.equal(sp.master, base * 3 + owner))
+            torch.cuda.synchronize(self.device)
+            ok = ok and self.errors() == 0
+        except Exception:
+            ok = False
+        finally:
+            for t, s in zip((sp.grad, sp.shadow, sp.state), saved):
+                t.copy_(s)
+            sp._master_stale = False
+            torch.cuda.synchronize(self.device)
+        flags: List[bool] = [False] * self.world
+        self.dist.all_gather_object(flags, ok, group=self.group)
+        return all(flags)
+
+    def _release(self):
+        for p in self.opened:
+            try:
+                HIP.call("kml_ipc_close", "p", p)
+            except Exception:
+                pass
+        self.opened = []
+        if self.region is not None:
+            HIP.call("kml_peer_free", "p p", self.region, self.ctrl)
+        self.region = self.ctrl = None
+        if getattr(self.space, "master_sync", None) == self.gather_master:
+            self.space.master_sync = None
+
+    def close(self):
+        """Collective over the group: unmap the peers' buffers once everyone is done."""
+        if self.region is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self.dist.barrier(group=self.group)
+        self._release()
+        self.dist.barrier(group=self.group)
+
+
+def verified_shard(space, group=None, log=None) -> Optional[PeerShard]:
+    """Collective: a :class:`PeerShard` that passed its self-test on every rank, or None on every
+    rank (callers then use the all-reduce plans).  ``KUBEML_PEER_SELFTEST=0`` skips the test."""
+    try:
+        p = PeerShard(space, group)
+    except PeerCommError as e:
+        if log:
+            log(f"sharded update unavailable: {e}")
+        return None
+    if os.environ.get("KUBEML_PEER_SELFTEST", "1") == "0" or p.self_test():
+        return p
+    if log:
+        log("sharded update failed its self-test on this node")
+    try:
+        p.close()
+    except Exception:
+        pass
+    return None
+
+
 def stream_copy(src: torch.Tensor, dst: torch.Tensor, nbytes: int, blocks: int, passes: int = 1):
     """Interference-probe streamer: ``passes`` copies of ``nbytes`` on ``blocks`` workgroups."""
     HIP.call("kml_stream_copy", "p p l i i s", src.data_ptr(), dst.data_ptr(), int(nbytes), int(blocks), int(passes),

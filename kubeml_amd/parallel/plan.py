@@ -8,7 +8,11 @@ gradient all-reduce:
   ``"rccl"`` — RCCL over xGMI through ``torch.distributed``.
 * ``schedule`` ``"end"`` — one all-reduce of the whole flat gradient after the backward, on
   the compute stream with the whole chip; ``"overlap"`` — one all-reduce per backward stage
-  on a side stream while the next stage's backward runs.
+  on a side stream while the next stage's backward runs; ``"shard"`` (peer only) — ZeRO-1:
+  reduce-scatter of the fp32 gradient read in place from the peers, the optimizer on this
+  rank's 1/P of the master (fused into the reduce for SGD), all-gather of the bf16 shadow
+  (:class:`~kubeml_amd.parallel.peer.PeerShard`; the wire field is ignored: fp32 gradient,
+  bf16 weights, which is what the forward computes with anyway).
 * ``wire``     fp32, or bf16 (half the link bytes; the sum accumulates in fp32).
 * ``max_blocks`` the grid cap of every peer launch (the CUs the collective may hold).
 
@@ -48,8 +52,10 @@ class CommPlan:
     def __post_init__(self):
         if self.backend not in ("peer", "rccl"):
             raise ValueError(f"backend must be peer or rccl, not {self.backend!r}")
-        if self.schedule not in ("end", "overlap"):
-            raise ValueError(f"schedule must be end or overlap, not {self.schedule!r}")
+        if self.schedule not in ("end", "overlap", "shard"):
+            raise ValueError(f"schedule must be end, overlap or shard, not {self.schedule!r}")
+        if self.schedule == "shard" and self.backend != "peer":
+            raise ValueError("the shard schedule runs on the peer backend")
         if self.wire not in _WIRES:
             raise ValueError(f"wire must be fp32 or bf16, not {self.wire!r}")
         self.max_blocks = max(1, int(self.max_blocks))

@@ -43,11 +43,18 @@ def free_port() -> int:
 class WorkerPool:
     def __init__(self, n: int, use_gpu: bool, store_dir: str, gpu_ids: Optional[List[int]] = None,
                  timeout: float = 600.0, env: Optional[Dict[str, str]] = None, grace: float = 5.0,
-                 threads: int = 1, stall_timeout: Optional[float] = None):
+                 threads: int = 1, stall_timeout: Optional[float] = None, n_gpus: Optional[int] = None):
         self.n = n
         self.use_gpu = use_gpu
         self.store_dir = store_dir
         self.gpu_ids = list(gpu_ids) if gpu_ids is not None else list(range(n))
+        # slot -> GPU (several slots may share one GPU: reference get_gpu = func_id % devices)
+        self.n_gpus = n_gpus
+        self.devices = [g % n_gpus for g in self.gpu_ids] if (use_gpu and n_gpus) else list(self.gpu_ids)
+        # the data plane of the pool's group: RCCL when every rank has its own GPU; gloo
+        # bootstrap + the peer-memory transport when ranks share a GPU (RCCL refuses that)
+        self.comm_mode = os.environ.get("KUBEML_WORKER_COMM") or (
+            "gloo" if not use_gpu else "nccl" if len(set(self.devices)) == len(self.devices) else "gloo+peer")
         self.timeout = timeout
         self.grace = grace
         self.env = dict(env or {})
@@ -67,7 +74,8 @@ class WorkerPool:
         port = free_port()
         env = {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
                "TORCH_NCCL_ASYNC_ERROR_HANDLING": os.environ.get("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1"), **self.env}
-        opts = {"use_gpu": self.use_gpu, "gpu_ids": self.gpu_ids, "store_dir": self.store_dir, "port": port,
+        opts = {"use_gpu": self.use_gpu, "gpu_ids": self.devices, "comm": self.comm_mode,
+                "store_dir": self.store_dir, "port": port,
                 "timeout": float(os.environ.get("KUBEML_COLLECTIVE_TIMEOUT", self.timeout)), "env": env,
                 "threads": self.threads}
         # one progress counter per rank, bumped by the worker (shared memory, no locking)

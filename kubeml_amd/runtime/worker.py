@@ -141,14 +141,17 @@ class Worker:
             torch.set_num_threads(max(1, int(self.opts.get("threads", 1))))
         if self.world > 1:
             import torch.distributed as dist
+            mode = self.opts.get("comm") or ("nccl" if self.use_gpu else "gloo")
+            if mode not in ("nccl", "gloo", "gloo+peer"):
+                raise ValueError(f"worker comm mode {mode!r}: nccl | gloo | gloo+peer")
             kw = {}
-            if self.use_gpu:
+            if mode == "nccl":
                 kw["device_id"] = self.device
-            dist.init_process_group("nccl" if self.use_gpu else "gloo",
+            dist.init_process_group("nccl" if mode == "nccl" else "gloo",
                                     init_method=f"tcp://127.0.0.1:{self.opts['port']}", rank=self.rank,
                                     world_size=self.world, timeout=timedelta(seconds=self.opts.get("timeout", 600)),
                                     **kw)
-            self.comm = TorchComm()
+            self.comm = TorchComm(peer_data=(mode == "gloo+peer" and self.use_gpu))
             self.comm.prepare_subgroups(self.world)
             if self.use_gpu and os.environ.get("KUBEML_PEER", os.environ.get("KUBEML_ONESHOT", "0")) == "1":
                 # fp32 reductions over the world group (K-AVG rounds, BN statistics, counts) go

@@ -83,7 +83,9 @@ class KubeModel(ABC):
         self.optimizer = None
         self.epoch = None
         self._averager = ModelAverager(network)
-        self._graphs: Dict[tuple, dict] = {}
+        self._graphs: Dict[tuple, dict] = {}       # train steps (engine/dp.py), by batch shape + comm
+        self._eval_graphs: Dict[tuple, dict] = {}  # eval forwards (evaluate)
+        self._shards: Dict[int, Any] = {}         # id(comm) -> PeerShard of this model's flat space
         self._flat = None
         self._sync_mode = "local"      # "grad": self.step all-reduces gradients (K=1 fast path)
         self._grad_comm = None
@@ -171,6 +173,7 @@ class KubeModel(ABC):
             opt = old
         elif old is not None and opt is not old:
             self._graphs.clear()  # graphs captured the old optimizer's step
+            self._shards.clear()  # (a shard's fused update reads the optimizer's state too)
         self.optimizer = opt
         if opt is not None and hasattr(opt, "set_grad_scale"):
             opt.set_grad_scale(1.0)
@@ -298,6 +301,8 @@ class KubeModel(ABC):
             for r in range(rounds):
                 fault.point("round", rank=fid, epoch=self.epoch, round=r, task="train", job=self.args._job_id)
                 _progress()
+                if r == full_rounds and self._flat is not None:
+                    self._flat.sync_master()   # sharded update -> local rounds read the whole master
                 participate = r < len(intervals)
                 self._sync_mode = "grad" if (grad_ok and r < full_rounds) else "local"
                 self._synced_steps = 0
@@ -342,6 +347,8 @@ class KubeModel(ABC):
                 with trace.span("average_flush"):
                     self._async_averager.flush_(comm)          # every worker ends on the same model
                 self.sync_seconds += time.perf_counter() - t0
+            if self._flat is not None:
+                self._flat.sync_master()       # collective over the shard group (no-op if current)
             if grad_rounds:
                 # in-graph gradient all-reduce time (device stamps sampled by the step)
                 cs = [g["step"].comm_seconds() for k, g in self._graphs.items() if k[5]]
@@ -515,14 +522,20 @@ class KubeModel(ABC):
             if comm is not None:
                 from ..parallel.plan import choose_plan
                 plan = choose_plan(comm.world, self._flat.grad.numel() * 4)
-                peer = getattr(comm, "grad_peer", None) if plan.backend == "peer" else None
+                peer = self._reusable_peer(comm, plan)
             st = make_train_step(self._network, self._flat, self.optimizer, loss_fn, xs, ys,
                                  group=comm.group if comm is not None else None,
                                  world=comm.world if comm is not None else 1,
                                  graph_comm=os.environ.get("KUBEML_GRAPH_COMM", "1") != "0",
                                  plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0)
+            self.logger.info("train step graph: batch %s, comm %s, plan %s, transport %s", tuple(x.shape),
+                             comm.world if comm is not None else 1, plan.tag() if plan is not None else None,
+                             type(st.peer).__name__ if st.peer is not None else None)
             if st.peer is not None and comm is not None:
-                comm.grad_peer = st.peer          # one gradient transport per group, reused
+                if st.schedule == "shard":
+                    self._shards[id(comm)] = st.peer       # bound to this model's flat buffers
+                else:
+                    comm.grad_peer = st.peer          # one gradient transport per group, reused
             from ..runtime.worker import busy
             with busy():                          # capture + warm-up can take seconds
                 st.capture()
@@ -533,6 +546,24 @@ class KubeModel(ABC):
         if grad:
             self._synced_steps += 1
         return loss
+
+    def _reusable_peer(self, comm, plan):
+        """The transport a new train-step graph may reuse: the shard of this model's space on
+        ``comm``, or the group's gradient all-reduce if its slots fit this gradient and wire
+        (one that does not is closed — collectively: every rank sees the same sizes)."""
+        if plan.backend != "peer":
+            return None
+        if plan.schedule == "shard":
+            sh = self._shards.get(id(comm))
+            return sh if sh is not None and sh.region is not None else None
+        gp = getattr(comm, "grad_peer", None)
+        if gp is None or gp.region is None:
+            return None
+        if gp.supports(self._flat.grad, "twoshot", plan.wire_dtype):
+            return gp
+        gp.close()
+        comm.grad_peer = None
+        return None
 
     def evaluate(self, x, y, loss_fn=None):
         """Eval-mode forward + loss + correct count for one validation batch -> (correct,
@@ -554,10 +585,10 @@ class KubeModel(ABC):
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
             return fwd(x, y)
         key = ("eval", tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(loss_fn))
-        g = self._graphs.get(key)
+        g = self._eval_graphs.get(key)
         if g is None:
-            if len(self._graphs) >= self.MAX_GRAPHS:
-                self._graphs.pop(next(iter(self._graphs)))
+            if len(self._eval_graphs) >= self.MAX_GRAPHS:
+                self._eval_graphs.pop(next(iter(self._eval_graphs)))
             xs, ys = x.clone(), y.clone()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -567,7 +598,7 @@ class KubeModel(ABC):
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 outs = fwd(xs, ys)
-            g = self._graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
+            g = self._eval_graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
         g["graph"].replay()

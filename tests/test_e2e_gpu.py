@@ -113,3 +113,103 @@ def test_bert_mlm_function_on_gpu_worker(tmp_path):
     assert len(h.train_loss) == 2 and all(np.isfinite(h.train_loss))
     assert h.train_loss[0] > 5.0                   # ~ln(30522) at random init
     assert len(h.accuracy) == 2 and all(0 <= a <= 100 for a in h.accuracy)
+
+
+def _packed_server(tmp_path, workers, policy=None):
+    """A server whose ``workers`` worker slots all run on the box's one GPU (reference packing,
+    ``func_id % device_count``): the pool bootstraps over gloo and moves data through the
+    peer-memory transport, since RCCL refuses two ranks on one device."""
+    from kubeml_amd.config import Config
+    from kubeml_amd.control.server import KubeMLServer
+    cfg = Config()
+    cfg.store_dir = str(tmp_path / "store")
+    cfg.num_gpus = 1
+    return KubeMLServer(cfg, n_workers=workers, use_gpu=True, task_timeout=600, policy=policy).start(
+        ports={k_: 0 for k_ in ("controller", "scheduler", "ps", "storage", "metrics")})
+
+
+def _cifar_like(n=1280, nte=256, seed=3):
+    rng = np.random.default_rng(seed)
+    return {"xtr": rng.integers(0, 256, (n, 32, 32, 3), dtype=np.uint8),
+            "ytr": rng.integers(0, 10, n).astype(np.int64),
+            "xte": rng.integers(0, 256, (nte, 32, 32, 3), dtype=np.uint8),
+            "yte": rng.integers(0, 10, nte).astype(np.int64)}
+
+
+def _run_job(c, tmp_path, k, parallelism, static=True, epochs=2, batch=128):
+    import json
+    from kubeml_amd.api.types import TrainOptions, TrainRequest
+    jid = c.networks.train(TrainRequest(batch_size=batch, epochs=epochs, dataset="cifar10", lr=0.05,
+                                        function_name="resnet34",
+                                        options=TrainOptions(default_parallelism=parallelism,
+                                                             static_parallelism=static, validate_every=1, k=k)))
+    t0 = time.time()
+    while c.tasks.status(jid)["state"] == "running":
+        assert time.time() - t0 < 600
+        time.sleep(0.5)
+    st = c.tasks.status(jid)
+    assert st["state"] == "finished", (st, c.logs(jid).decode()[-3000:])
+    logs = [json.loads(l) for l in c.logs(jid).decode().splitlines() if l.startswith("{")]
+    return jid, c.histories.get(jid).data, [l for l in logs if l.get("msg") == "epoch finished"]
+
+
+def _same_model(ep):
+    ck = list(ep["checksums"].values())
+    ends = [v[1] for v in ck]
+    return max(ends) - min(ends) <= 1e-6 * max(1.0, abs(ends[0]))
+
+
+def test_two_workers_share_one_gpu_grad_sync_and_kavg(tmp_path):
+    """``kubeml train --parallelism 2`` with both workers on the one GPU: K = 1 runs as the
+    in-graph gradient sync (the comm plan's transport over peer memory), K = 4 as K-AVG
+    rounds over the peer all-reduce; both keep the two workers on one model."""
+    from kubeml_amd.client import KubemlClient
+    srv = _packed_server(tmp_path, 2)
+    try:
+        assert srv.ps.n_gpus == 1 and srv.ps.inventory.n == 2
+        c = KubemlClient(srv.url())
+        arrs = _cifar_like()
+        paths = {}
+        for key, v in arrs.items():
+            paths[key] = str(tmp_path / f"{key}.npy")
+            np.save(paths[key], v)
+        c.datasets.create("cifar10", paths["xtr"], paths["ytr"], paths["xte"], paths["yte"])
+        c.functions.create("resnet34", os.path.join(ROOT, "examples", "function_resnet34.py"))
+        for k, mode in ((1, "grad-allreduce"), (4, "kavg")):
+            _, h, eps = _run_job(c, tmp_path, k, 2)
+            assert h.parallelism == [2.0, 2.0] and all(np.isfinite(h.train_loss)), h
+            assert all(m == mode for m in h.sync_mode), h.sync_mode
+            assert all(len(e["checksums"]) == 2 and _same_model(e) for e in eps), eps
+    finally:
+        srv.stop()
+
+
+def test_elastic_one_two_one_on_one_gpu(tmp_path):
+    """Scripted elastic resize P = 1 -> 2 -> 1 with two workers on one GPU: the worker joining
+    at P = 2 starts from rank 0's model (epoch-start broadcast over the peer transport) and both
+    end the epoch on one model."""
+    from kubeml_amd.client import KubemlClient
+    srv = _packed_server(tmp_path, 2, policy="scripted:1,2,1")
+    try:
+        c = KubemlClient(srv.url())
+        arrs = _cifar_like(seed=4)
+        paths = {}
+        for key, v in arrs.items():
+            paths[key] = str(tmp_path / f"{key}.npy")
+            np.save(paths[key], v)
+        c.datasets.create("cifar10", paths["xtr"], paths["ytr"], paths["xte"], paths["yte"])
+        c.functions.create("resnet34", os.path.join(ROOT, "examples", "function_resnet34.py"))
+        _, h, eps = _run_job(c, tmp_path, 1, 1, static=False, epochs=3)
+        assert h.parallelism == [1.0, 2.0, 1.0], h.parallelism
+        assert [len(e["checksums"]) for e in eps] == [1, 2, 1]
+        prev_end = None
+        for e in eps:
+            ck = list(e["checksums"].values())
+            starts = [v[0] for v in ck]
+            assert max(starts) - min(starts) <= 1e-9 * max(1.0, abs(starts[0])), e["checksums"]
+            if prev_end is not None:
+                assert abs(starts[0] - prev_end) <= 1e-6 * max(1.0, abs(prev_end)), (starts, prev_end)
+            assert _same_model(e), e["checksums"]
+            prev_end = ck[0][1]
+    finally:
+        srv.stop()
