@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--force-comm", action="store_true",
                     help="run the RCCL all-reduce path even with one rank (single-GPU rehearsal of dp>1)")
     ap.add_argument("--graph-comm", choices=["on", "off"], default="on",
-                    help="capture the overlapped all-reduces inside the step's hipGraph (KUBEML_GRAPH_COMM=0: off)")
+                    help="capture the RCCL all-reduces inside the step's hipGraph (off: eager between segment graphs)")
     ap.add_argument("--no-epoch", action="store_true", help="skip the measured epoch after the timed steps")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="gradient all-reduce precision (bf16 = compressed, half the xGMI bytes)")
@@ -245,7 +245,7 @@ def main():
     opt = SGD(model.parameters(), lr=args.lr, weight_decay=1e-4)
 
     overlap = args.overlap == "on" or (args.overlap == "auto" and comm)
-    graph_comm = args.graph_comm == "on" and os.environ.get("KUBEML_GRAPH_COMM", "1") != "0"
+    graph_comm = args.graph_comm == "on"
     plan = None
     if comm:
         from kubeml_amd.parallel.plan import choose_plan

@@ -12,7 +12,8 @@
 //
 // Attention-probability dropout (HF BERT attention_probs_dropout_prob): keep mask
 // Z[b,h,q,key] = half16(hash(seed ^ salt, step, b, h, q, key / 2), key & 1) >= p * 2^16,
-// recomputed in all three kernels (nothing stored; one hash per key pair).  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
+// hashed once by the forward (one hash per key pair), which stores the decisions as a bit mask
+// (1 bit per probability, AttnArgs::keep) that both backward kernels read.  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
 // the undropped probabilities; backward: dV = (P (.) Z/(1-p))^T dO, dP = (dO V^T) (.) Z/(1-p),
 // dS = P (.) (dP - D) with D = rowsum(dO (.) O) (unchanged by the mask).
 //

@@ -385,7 +385,8 @@ __global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region,
     if (ok) {
       uint4 w[P];
 #pragma unroll
-      for (int p = 0; p < P; ++p) w[p] = ld_sys16(rs[p], v * 16);
+      for (int p = 0; p < P; ++p)  // own gradient: local bytes, plain (L2-cached) loads
+        w[p] = p == rank ? *reinterpret_cast<const uint4*>(own_grad + lo + v * 4) : ld_sys16(rs[p], v * 16);
       Wire<false>::unpack(w[0], acc);
 #pragma unroll
       for (int p = 1; p < P; ++p) {

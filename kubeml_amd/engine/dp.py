@@ -38,18 +38,18 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     post(): runs after the optimizer
     advance: (ctr, batch, n) -- advance the on-device data counter after the optimizer
             (``ops.kernels.advance_counter_``); folded into the fused SGD launch when the
-            optimizer can (``fuse_advance``; ``KUBEML_ADV_IN_OPT=0`` keeps it a separate launch)
+            optimizer can (``fuse_advance``)
     world:  ranks in ``group``; > 1 adds the gradient all-reduce (SUM) and sets the
             optimizer's gradient scale to 1/world
     overlap: split backward at ``model.stages()`` (if the model has them) so each
             stage's gradients are all-reduced while the next stage's backward runs
     comm_dtype: torch.bfloat16 all-reduces bf16-rounded gradients (half the bytes; see
-            :class:`GraphedTrainStep`); None = ``KUBEML_COMM_DTYPE`` (``bf16`` or fp32, default)
+            :class:`GraphedTrainStep`); None = fp32
     opt_overlap: apply the optimizer per backward stage on a side stream as soon as the
             stage's gradients are final (after its all-reduce when world > 1), overlapping the
             bandwidth-bound update with the rest of the latency-bound backward; needs a model
             with stages, an optimizer with ``step_range`` and the whole step in one graph.
-            None = ``KUBEML_OPT_OVERLAP`` (default OFF: on one MI355X the concurrent
+            None = off (on one MI355X the concurrent
             side-stream update slows the backward's latency-bound kernel stream, ResNet-34
             1.40 -> 1.73-1.81 ms/step whatever its grid; profiles/launch_fusion_r2.md)
     plan:   a :class:`kubeml_amd.parallel.plan.CommPlan` (transport, schedule, wire, block cap);
@@ -88,8 +88,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         if plan.backend != "peer":
             peer = None
     if comm_dtype is None:
-        comm_dtype = torch.bfloat16 if os.environ.get("KUBEML_COMM_DTYPE", "fp32").lower() in (
-            "bf16", "bfloat16") else torch.float32
+        comm_dtype = torch.float32
     from ..nn import backward_loss
     scale = 1.0 / max(world, 1)
 
@@ -106,13 +105,10 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
 
     segs = seg_grads = seg_opt = opt_finish = None
     staged_ok = hasattr(model, "stages") and hasattr(model, "stage_params")
-    if opt_overlap is None:
-        opt_overlap = os.environ.get("KUBEML_OPT_OVERLAP", "0") == "1"
     opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm) and peer is None
                        and getattr(optimizer, "supports_ranges", lambda: False)())
     if advance is not None:
-        fused = (not opt_overlap and os.environ.get("KUBEML_ADV_IN_OPT", "1") != "0"
-                 and getattr(optimizer, "fuse_advance", lambda *a: False)(*advance))
+        fused = (not opt_overlap and getattr(optimizer, "fuse_advance", lambda *a: False)(*advance))
         if fused:
             fold = tuple(advance)
         else:

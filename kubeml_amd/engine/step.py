@@ -90,11 +90,6 @@ def _widen(lp, v):
         v.reshape(-1).copy_(lp)
 
 
-import os as _os
-
-_DEBUG_FORK = _os.environ.get("KUBEML_DEBUG_FORK", "0") == "1"
-
-
 class _SideJoin:
     """'Work' handle of a side-stream collective: waiting joins the side stream into the
     current one (a graph join edge when captured)."""
@@ -224,11 +219,8 @@ class GraphedTrainStep:
     # ------------------------------------------------------------------ pieces
     @staticmethod
     def _run(fn):
-        """Run a forward/backward callable with conv wgrads on the side stream (joined
-        before returning, so a captured segment ends with all branches merged)."""
-        from ..nn.fused import wgrad_overlap
-        with wgrad_overlap():
-            return fn()
+        """Run one forward/backward segment callable."""
+        return fn()
 
     def _views(self, k):
         for t in self.segment_grads[k]:
@@ -345,8 +337,6 @@ class GraphedTrainStep:
     def _body(self):
         if self.segment_opt is not None:
             return self._body_opt_overlap()
-        if _DEBUG_FORK and torch.cuda.is_available():
-            self._debug_fork()
         loss, works = None, []
         for k, seg in enumerate(self.segments):
             out = self._run(seg)
@@ -362,19 +352,6 @@ class GraphedTrainStep:
         else:
             self.opt_step()
         return loss
-
-    def _debug_fork(self):
-        """KUBEML_DEBUG_FORK=1: one empty side-stream branch per step (fork + tiny kernel +
-        join) — measures what a multi-stream graph costs by itself."""
-        from ..ops import kernels as K
-        if self._opt_side is None:
-            self._opt_side = torch.cuda.Stream()
-            self._fork_buf = torch.zeros(64, device="cuda")
-        cur = torch.cuda.current_stream()
-        self._opt_side.wait_stream(cur)
-        with torch.cuda.stream(self._opt_side):
-            K.fill_(self._fork_buf, 1.0)
-        cur.wait_stream(self._opt_side)
 
     def _body_opt_overlap(self):
         """Per-segment update on a side stream: after segment k's backward (and its

@@ -222,7 +222,7 @@ class _StemFn(torch.autograd.Function):
     """conv1 -> bn1 -> ReLU -> max-pool of the training forward.  BN-apply, ReLU and the pool
     run as ONE pass (``bn_relu_maxpool``: the full-resolution normalised map is never
     written); backward folds the ReLU mask into the gather max-pool backward, so the BN
-    backward reads dz and the conv output only.  ``KUBEML_STEM_FUSE=0``: unfused path."""
+    backward reads dz and the conv output only.  ``_STEM_FUSE = False``: unfused path (tests)."""
 
     @staticmethod
     def forward(ctx, x, net, *params):
@@ -262,7 +262,7 @@ class _StemFn(torch.autograd.Function):
         return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
-_STEM_FUSE = __import__("os").environ.get("KUBEML_STEM_FUSE", "1") != "0"
+_STEM_FUSE = True
 
 
 def resnet18(num_classes=1000, **kw):

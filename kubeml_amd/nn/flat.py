@@ -55,6 +55,8 @@ def _storage_spec(p: torch.nn.Parameter):
 class FlatParamSpace:
     """Owns the flat buffers for a list of parameters (all on one device)."""
 
+    full_zero = False     # tests: memset the whole gradient every step (the reference behaviour)
+
     def __init__(self, params: Iterable[torch.nn.Parameter], device=None, reverse: bool = True,
                  with_shadow: Optional[bool] = None, buffers=None):
         """buffers: optional list of (module, name) of floating-point module buffers to
@@ -228,7 +230,7 @@ class FlatParamSpace:
         at the cost of zeroing only what an add-only producer will accumulate into."""
         if self.device.type != "cuda":
             self.grad.zero_()
-        elif not self._zeroed_once or os.environ.get("KUBEML_FULL_ZERO") == "1":
+        elif not self._zeroed_once or self.full_zero:
             from ..ops import kernels as K
             K.memset_(self.grad)          # first step: learn which producers overwrite
             self._zeroed_once = True
@@ -282,8 +284,6 @@ class FlatParamSpace:
 
     def _run_folds(self, run):
         from ..ops import kernels as K
-        from .fused import join_wgrad
-        join_wgrad()          # side-stream wgrads (KUBEML_WGRAD_SIDE) wrote the scratch
         K.fold22_multi([(g, dw, acc) for _, g, dw, acc in run])
 
     def finish_grads(self, params=None):

@@ -29,55 +29,9 @@ import os
 
 from .flat import grad_out, grad_out_pair, master_of, shadow_of
 
-# KUBEML_BN_FUSE=0: every BN backward runs its own dgamma/dbeta reduction instead of
-# taking partial rows from the dgrad epilogue that produced its input gradient
-_BN_FUSE = os.environ.get("KUBEML_BN_FUSE", "1") != "0"
-
-
-class _WgradSide:
-    """Side stream for conv weight gradients (see :func:`wgrad_overlap`)."""
-    stream = None
-    pending = False
-
-
-class wgrad_overlap:
-    """Run every conv wgrad of the enclosed backward on a side stream.
-
-    The dgrad chain (BN backward -> dgrad -> next BN backward ...) is the critical path
-    of backward; each unit's wgrad only feeds the gradient buffer.  Forking it onto a
-    second stream lets the two independent small GEMMs share the CUs (a captured graph
-    keeps the fork as parallel branches that run on separate hardware queues).  On exit
-    the main stream waits for the side stream, so everything after the block (all-reduce,
-    optimizer) sees finished gradients.
-
-    Opt-in (``KUBEML_WGRAD_SIDE=1``): measured on ResNet-34 b256 (1x MI355X) the
-    cross-queue dependency per unit costs more than the overlap gains (1.96 -> 2.2-2.4
-    ms/step with 36 forks per step), so the default keeps one stream.
-    """
-
-    _stream_cache = {}
-
-    def __enter__(self):
-        self.prev = _WgradSide.stream
-        if torch.cuda.is_available() and os.environ.get("KUBEML_WGRAD_SIDE", "0") == "1":
-            dev = torch.cuda.current_device()
-            s = self._stream_cache.get(dev)
-            if s is None:
-                s = self._stream_cache[dev] = torch.cuda.Stream()
-            _WgradSide.stream = s
-        return self
-
-    def __exit__(self, *exc):
-        join_wgrad()
-        _WgradSide.stream = self.prev
-        return False
-
-
-def join_wgrad():
-    """Make the current stream wait for outstanding side-stream wgrads."""
-    if _WgradSide.stream is not None and _WgradSide.pending:
-        torch.cuda.current_stream().wait_stream(_WgradSide.stream)
-        _WgradSide.pending = False
+# every BN backward takes its dgamma/dbeta partial rows from the dgrad epilogue that produced
+# its input gradient (False: its own reduction pass; tests compare the two)
+_BN_FUSE = True
 
 
 def _wg_buf(conv, x):
@@ -102,22 +56,10 @@ def _wgrad_target(conv, x, unroll):
 def _wgrad(x, dc, conv, unroll=False):
     from ..ops import kernels as K
     kh, kw = conv.kernel_size
-    side = _WgradSide.stream
     dw, acc = _wgrad_target(conv, x, unroll)
-    if side is None:
-        K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
-        if unroll:
-            conv.weight._kml_flat.defer_fold22(conv.weight, dw)
-        return
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
-    # the allocator must not hand these blocks to the main stream before the side reads them
-    x.record_stream(side)
-    dc.record_stream(side)
-    _WgradSide.pending = True
+    K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
     if unroll:
-        conv.weight._kml_flat.defer_fold22(conv.weight, dw)   # runs after join_wgrad()
+        conv.weight._kml_flat.defer_fold22(conv.weight, dw)
 
 
 def _wu_buf(conv, w):
@@ -157,7 +99,7 @@ def unrolled_for(conv, x):
     return buf
 
 
-_U22_GATHER = os.environ.get("KUBEML_U22_GATHER", "1") != "0"
+_U22_GATHER = True    # unrolled 2x2 convs read the 3x3 weight through a gather (no materialised copy)
 
 
 def refresh_transposed(convs):
@@ -209,13 +151,13 @@ class BNRegistry:
         self.bns = list(bns)
 
 
-# KUBEML_BN_FOLD=0: every BatchNorm of a BasicBlock runs its own apply kernel (no folding of
-# bn1 + ReLU into conv2's halo patch staging, see BlockFn.forward)
-_BN_FOLD = os.environ.get("KUBEML_BN_FOLD", "1") != "0"
+# bn1 + ReLU of a BasicBlock folded into conv2's halo patch staging (BlockFn.forward); False:
+# every BatchNorm runs its own apply kernel (tests compare the two)
+_BN_FOLD = True
 # group-reduce the folded BN's statistics rows in the producing conv (<= 16 rows for the consumer);
 # off: measured slower (1.354 vs 1.333 ms/step) and the ungrouped fold is bit-identical to the
 # unfolded BN apply (tests/test_models_gpu.py::test_resnet34_bn_fold_matches_unfolded)
-_FOLD_GROUP = os.environ.get("KUBEML_BN_FOLD_GROUP", "0") == "1"
+_FOLD_GROUP = False
 
 
 class ConvBNUnit:
@@ -304,7 +246,7 @@ class ConvBNUnit:
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
         wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
         object.__setattr__(conv, "_kml_wu", None)
-        if need_dx and _WgradSide.stream is None:
+        if need_dx:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
             w = shadow_of(conv.weight)
             wt = getattr(conv, "_kml_wt", None)

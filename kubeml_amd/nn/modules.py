@@ -40,22 +40,13 @@ def _on_gpu(x):
 # 256/128-tile LDS-DMA MFMA kernel of csrc/kernels/gemm.hip (ops/gemm.py): bias and erf-GELU
 # in the forward epilogue, the weight gradient accumulated in fp32 straight into the flat
 # gradient storage (split-K with agent atomics).  Small-M layers and fused-ReLU heads stay on
-# the implicit-GEMM conv kernels.  KUBEML_LINEAR_BLAS=1 routes the large ones to hipBLASLt
-# instead (A/B comparison only; not used by default).
-_LIN_BLAS = os.environ.get("KUBEML_LINEAR_BLAS", "0")
+# the implicit-GEMM conv kernels.
 
 
 def _linear_route(M, ip, op, act):
-    """'blas' (hipBLASLt, opt-in), 'gemm' (gemm.hip) or 'conv' (implicit-GEMM kernels)."""
+    """'gemm' (gemm.hip) or 'conv' (implicit-GEMM kernels)."""
     big = M >= 2048 and ip >= 256 and op >= 256 and act != 1
-    if big and _LIN_BLAS == "1" and act == 0:
-        return "blas"
     return "gemm" if big else "conv"
-
-
-def _blas_wgrad_(dw, dy, x):
-    """dw[op, ip] (fp32) += dy[M, op]^T @ x[M, ip] on hipBLASLt (KUBEML_LINEAR_BLAS=1 only)."""
-    torch.addmm(dw, dy.t(), x, out_dtype=torch.float32, out=dw)
 
 
 class _PadChannelsFn(Function):
@@ -181,9 +172,6 @@ class _LinearFn(Function):
             w2 = shadow_of(weight).view(op, ip)
             pre = torch.empty((B, op), dtype=torch.bfloat16, device=x2.device) if act == 2 else None
             y = G.linear_fwd(x2, w2, None if bias is None else master_of(bias), act=1 if act == 2 else 0, pre=pre)
-        elif route == "blas":
-            w2 = shadow_of(weight).view(op, ip)
-            y = torch.mm(x2, w2.t()) if bias is None else torch.addmm(shadow_of(bias), x2, w2.t())
         else:
             if act == 2:
                 raise ValueError("fused GELU needs the large-linear GEMM path")
@@ -247,10 +235,6 @@ class _LinearFn(Function):
                 dx = G.linear_dgrad(dy, w2, addend=addend)
                 addend = None
             G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x)
-        elif ctx.route == "blas":
-            if ctx.needs_input_grad[0]:
-                dx = torch.mm(dy, shadow_of(mod.weight).view(op, ip))
-            _blas_wgrad_(dw4.view(op, ip), dy, ctx.x)
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
@@ -533,7 +517,7 @@ class _CEFn(Function):
         return d, None, None, None, None
 
 
-_CE_BIAS_FUSE = __import__("os").environ.get("KUBEML_CE_BIAS_FUSE", "1") != "0"
+_CE_BIAS_FUSE = True    # the head's bias gradient comes out of the cross-entropy backward
 
 
 def cross_entropy(logits, labels, ignore_index=-100, return_correct=False, classes=None):

@@ -27,9 +27,9 @@ def _bf(x):
     return x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
 
 
-# KUBEML_RES_FUSE=0: residual gradients summed by autograd (a separate add) instead of the
-# consuming Linear's dgrad epilogue
-_RES_FUSE = __import__("os").environ.get("KUBEML_RES_FUSE", "1") != "0"
+# residual gradients summed in the consuming Linear's dgrad epilogue (False: by autograd, a
+# separate add; tests compare the two)
+_RES_FUSE = True
 
 
 # ====================================================================================== LayerNorm
@@ -77,7 +77,7 @@ class LayerNorm(tnn.LayerNorm):
     """LayerNorm over the last dim; ``forward(x, residual, dropout)`` normalises
     ``dropout(x) + residual``.  On the GPU in training the dropout runs inside the LayerNorm
     kernels (same counter-hash mask as :class:`Dropout`): no separate dropout pass forward
-    or backward (``KUBEML_LN_DROP_FUSE=0`` keeps it separate)."""
+    or backward (``_LN_DROP_FUSE = False`` keeps it separate)."""
 
     def forward(self, x, residual=None, dropout=None):
         drop, sep = None, False
@@ -97,7 +97,7 @@ class LayerNorm(tnn.LayerNorm):
         return _LNFn.apply(x2, self.weight, self.bias, self, r2, drop, sep).view(shp)
 
 
-_LN_DROP_FUSE = __import__("os").environ.get("KUBEML_LN_DROP_FUSE", "1") != "0"
+_LN_DROP_FUSE = True
 
 
 class _GELUFn(Function):

@@ -124,19 +124,7 @@ def plan_conv(mode, M, N, Kd):
     3 = direct LDS-free kernel (fwd/dgrad; bk = waves splitting K, splits = 1)."""
     cfg = _TUNED.get((mode, M, N, Kd))
     cfg = cfg if cfg is not None else default_plan(mode, M, N, Kd)
-    cfg = list(tuple(cfg) + (0,) * (5 - len(cfg)))
-    if _DBG_NOGLDS:
-        cfg[4] = 0
-    if _DBG_NOSPLIT and mode != "wgrad":
-        cfg[3] = 1
-    if _DBG_NOSPLIT_W and mode == "wgrad":
-        cfg[3] = 1
-    return tuple(cfg)
-
-
-_DBG_NOGLDS = os.environ.get("KUBEML_CONV_NOGLDS") == "1"
-_DBG_NOSPLIT = os.environ.get("KUBEML_CONV_NOSPLIT") == "1"
-_DBG_NOSPLIT_W = os.environ.get("KUBEML_CONV_NOSPLIT_W") == "1"
+    return tuple(tuple(cfg) + (0,) * (5 - len(cfg)))
 
 
 def _norm_cfg(cfg):
@@ -186,17 +174,18 @@ DIRECT = 3  # cfg variant id of the LDS-free wave-split-K kernel (fwd / dgrad)
 
 # Partial BN rows above this count are group-reduced inside the producing conv (the last
 # block of every group of M-tiles sums its group's rows): the consumer BN kernel, whose every
-# block otherwise re-reads all rows from L2, then reads at most 16 rows.  Opt-in
-# (KUBEML_BN_GROUP_MIN=N): on ResNet-34/b256 the ticket hand-off in every producer block costs
-# more than the consumer saves (1.720 ms/step off vs 1.758-1.782 at N = 64..512).
-_GRP_MIN = int(os.environ.get("KUBEML_BN_GROUP_MIN", "0"))
+# block otherwise re-reads all rows from L2, then reads at most 16 rows.  Off (0) for plain
+# consumers: on ResNet-34/b256 the ticket hand-off in every producer block costs more than the
+# consumer saves (1.720 ms/step off vs 1.758-1.782 at 64..512 rows); consumers whose every block
+# reads all rows ask for it (``group=True``).
+_GRP_MIN = 0
 _GRP_ROWS = 16
 
 
 def _stats_layout(M, cfg, group=False):
     """(per-wave rows G, M-tiles per group or 0, rows the consumer reads).  group: reduce
-    to at most _GRP_ROWS rows regardless of KUBEML_BN_GROUP_MIN (a consumer whose every
-    block reads all rows, e.g. the BN-folding halo conv)."""
+    to at most _GRP_ROWS rows regardless of _GRP_MIN (a consumer whose every block reads all
+    rows, e.g. the BN-folding halo conv)."""
     bm = _norm_cfg(cfg)[0]
     tiles = _cdiv(M, bm)
     # one row per M tile (the epilogue sums the tile's wave row-bands; tail tiles included)
@@ -235,11 +224,7 @@ def unrolled22(H, W, KH, KW, stride, pad) -> bool:
     the im2col FLOPs (ResNet-34/18 layer3 at 32x32 input, 2x2 maps).  BN statistics fold the
     4 positions back onto the K channels in the epilogue (``fold_c``) and the weight
     gradient scatters back onto the 3x3 taps (``u_k0/u_c0``)."""
-    return (H, W, KH, KW) == (2, 2, 3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1) and \
-        _UNROLL_ON
-
-
-_UNROLL_ON = os.environ.get("KUBEML_CONV_UNROLL", "1") != "0"
+    return (H, W, KH, KW) == (2, 2, 3, 3) and tuple(stride) == (1, 1) and tuple(pad) == (1, 1)
 
 
 def unroll22_multi(ws, wus):
@@ -426,7 +411,6 @@ _HALO_TILES = {(64, 8): [(64, 32), (64, 64), (128, 64)],
                (128, 4): [(64, 32), (64, 64), (128, 32), (64, 128), (128, 64)],
                (256, 8): [(64, 64), (64, 32)], (256, 4): [(64, 32), (64, 64)],
                (512, 4): [(64, 32), (64, 64)]}
-_HALO_ON = os.environ.get("KUBEML_CONV_HALO", "1") != "0"
 
 
 def halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
@@ -437,7 +421,7 @@ def halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
 
 # dgrad halo tiles, keyed by (Cout = the dy patch's channels, H): (bm, bn) with bn over Cin
 _HALO_DG_TILES = {(64, 8): [(64, 32), (64, 64), (128, 64)], (128, 4): [(64, 32)]}
-_HALO_DG_ON = os.environ.get("KUBEML_DGRAD_HALO", "0") == "1"   # opt-in: measured slower in the step (profiles/r3/halo_dgrad.md)
+_HALO_DG_ON = False   # tests / micro-benchmarks only: measured slower in the step (profiles/r3/halo_dgrad.md)
 
 
 def halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
@@ -447,8 +431,8 @@ def halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn) -> bool:
 
 
 def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
-    """Default halo-patch dgrad plan (patch of dy, flipped-filter weight slice in LDS) for an
-    eligible conv, or None (``KUBEML_DGRAD_HALO=0``)."""
+    """Halo-patch dgrad plan (patch of dy, flipped-filter weight slice in LDS) for an eligible
+    conv when ``_HALO_DG_ON``, else None."""
     if not _HALO_DG_ON:
         return None
     for bm, bn in _HALO_DG_TILES.get((K, H), ()):
@@ -458,13 +442,8 @@ def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
 
 
 STEM = 6  # cfg variant id of the stem halo kernel (7x7/s2/p3, Cin 8, Cout 64, 32x32 input): bm = one image
-_STEM_ON = os.environ.get("KUBEML_CONV_STEM", "1") != "0"
-
-
 def stem_plan(C, K, H, W, KH, KW, stride, pad, force=False):
     """(256, 64, 0, 1, STEM) for the ResNet ImageNet stem on 32x32 images, else None."""
-    if not (_STEM_ON or force):
-        return None
     if (C, K, H, W, KH, KW, tuple(stride), tuple(pad)) != (8, 64, 32, 32, 7, 7, (2, 2), (3, 3)):
         return None
     return (256, 64, 0, 1, STEM)
@@ -472,7 +451,6 @@ def stem_plan(C, K, H, W, KH, KW, stride, pad, force=False):
 
 ONESHOT = 5  # cfg variant id of the one-shot panel forward (single-tap convs, K in _ONESHOT_TILES)
 _ONESHOT_TILES = {512: [(32, 32), (32, 64), (64, 32)], 1024: [(32, 32)], 256: [(32, 32), (32, 64), (64, 64)]}
-_ONESHOT_ON = os.environ.get("KUBEML_CONV_ONESHOT", "1") != "0"
 
 
 def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
@@ -486,28 +464,23 @@ def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
 
 
 def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad):
-    """Default one-shot panel plan for an eligible forward conv, or None
-    (``KUBEML_CONV_ONESHOT=0`` disables it; ``KUBEML_ONESHOT_TILE=bm,bn`` picks a tile)."""
-    if not _ONESHOT_ON:
-        return None
-    env = os.environ.get("KUBEML_ONESHOT_TILE")
-    cands = ([tuple(int(v) for v in env.split(","))] if env else []) + list(_ONESHOT_TILES.get(Kd, ()))
-    for bm, bn in cands:
+    """Default one-shot panel plan for an eligible forward conv, or None."""
+    for bm, bn in _ONESHOT_TILES.get(Kd, ()):
         if oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn):
             return (bm, bn, 0, 1, ONESHOT)
     return None
 
 
-# opt-in: as two launches the one-shot dgrad + wgrad lose to the grouped implicit-GEMM pair
-# (1.376 vs 1.353 ms/step, profiles/r3/oneshot.md)
-_ONESHOT_BWD_ON = os.environ.get("KUBEML_BWD_ONESHOT", "0") == "1"
+# tests / micro-benchmarks only: as two launches the one-shot dgrad + wgrad lose to the grouped
+# implicit-GEMM pair (1.376 vs 1.353 ms/step, profiles/r3/oneshot.md)
+_ONESHOT_BWD_ON = False
 _ONESHOT_DG_TILES = {1024: (32, 32), 512: (32, 32)}   # keyed by the dgrad K (= Cout)
 _ONESHOT_WG_TILES = {256: (32, 32)}                    # keyed by the wgrad K (= pixels)
 
 
 def oneshot_bwd_plans(C, K, B, H, W, KH, KW, stride, pad):
     """(dgrad plan or None, wgrad plan or None) of the one-shot backward bodies for a
-    single-tap conv with contiguous rows (``KUBEML_BWD_ONESHOT=0`` disables both)."""
+    single-tap conv with contiguous rows (only when ``_ONESHOT_BWD_ON``)."""
     if not _ONESHOT_BWD_ON or C % 32 or K % 32:
         return None, None
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, stride[0], stride[1], pad[0], pad[1])
@@ -521,14 +494,8 @@ def oneshot_bwd_plans(C, K, B, H, W, KH, KW, stride, pad):
 
 
 def halo_plan(C, K, H, W, KH, KW, stride, pad):
-    """Default halo-patch plan for an eligible forward conv, or None (``KUBEML_CONV_HALO=0``
-    disables it; ``KUBEML_HALO_TILE=bm,bn`` picks another instantiated tile)."""
-    if not _HALO_ON:
-        return None
-    tiles = _HALO_TILES.get((C, H), ())
-    env = os.environ.get("KUBEML_HALO_TILE")
-    cands = ([tuple(int(v) for v in env.split(","))] if env else []) + list(tiles)
-    for bm, bn in cands:
+    """Default halo-patch plan for an eligible forward conv, or None."""
+    for bm, bn in _HALO_TILES.get((C, H), ()):
         if halo_ok(C, K, H, W, KH, KW, stride, pad, bm, bn):
             return (bm, bn, 0, 1, HALO)
     return None
@@ -555,7 +522,7 @@ def bnin_ok(x_shape, K, KH, KW, stride, pad) -> bool:
             256 % (C // 2) == 0)
 
 
-_BNIN_ON = os.environ.get("KUBEML_BN_FOLD", "1") != "0"
+_BNIN_ON = True
 
 
 def conv_fwd_bnin(c_in, w, rows, G, gamma, beta, save_mean, save_rstd, run_mean, run_var, eps, momentum, y_in,
@@ -731,11 +698,10 @@ def bwd_plans(in_shape, K, KH, KW, stride, pad, dcfg=None, wcfg=None, unroll=Fal
         dcfg, wcfg = od or dcfg, ow or wcfg
     dplan = _norm_cfg(dcfg or plan_conv("dgrad", B * H * W, C, ntap * K))
     wplan = _norm_cfg(wcfg or plan_conv("wgrad", K, ntap * C, B * OH * OW))
-    return dplan, wplan, _PAIR_ON and conv_pair_supported(dplan, wplan)
+    return dplan, wplan, conv_pair_supported(dplan, wplan)
 
 
 _PAIR_OK: dict = {}
-_PAIR_ON = os.environ.get("KUBEML_CONV_PAIR", "1") != "0"
 
 
 def conv_pair_supported(dcfg, wcfg) -> bool:
@@ -989,8 +955,8 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
 
 # BN-backward dgamma/dbeta reduction: "fused" (default) = per-block partials, summed in
 # a fixed order by the apply kernel (deterministic, no atomics / fences); "ticket" = the
-# in-kernel last-arriver reduce; "atomic" = fp32 atomics.  KUBEML_BN_REDUCE selects.
-_BN_REDUCE = os.environ.get("KUBEML_BN_REDUCE", "fused")
+# in-kernel last-arriver reduce; "atomic" = fp32 atomics (tests and tools/bn_micro.py compare).
+_BN_REDUCE = "fused"
 
 
 def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None, accumulate=True):

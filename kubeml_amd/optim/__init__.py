@@ -235,7 +235,7 @@ class SGD(FusedOptimizer):
         self._first = False
 
 # grid cap of a range update (it runs beside the backward on a side stream)
-_RANGE_BLOCKS = int(__import__("os").environ.get("KUBEML_OPT_OVERLAP_BLOCKS", "64"))
+_RANGE_BLOCKS = 64
 
 
 def _sgd_range_cpu(sp, start, end, g, mom, first, grad_scale):

@@ -39,8 +39,8 @@ import torch
 from .._native import HIP
 from ..api.errors import MergeError
 
-DEFAULT_CAP = int(float(os.environ.get("KUBEML_PEER_MB", os.environ.get("KUBEML_ONESHOT_MB", "8"))) * 2**20)
-ONESHOT_MAX_BYTES = int(os.environ.get("KUBEML_ONESHOT_MAX_KB", "512")) * 1024
+DEFAULT_CAP = int(float(os.environ.get("KUBEML_PEER_MB", "8")) * 2**20)
+ONESHOT_MAX_BYTES = 512 * 1024    # one-shot (latency-optimal) up to here, two-shot above
 DEFAULT_TIMEOUT_S = float(os.environ.get("KUBEML_PEER_TIMEOUT_S", "60"))
 ALGOS = {"oneshot": 0, "twoshot": 1}
 

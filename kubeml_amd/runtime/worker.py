@@ -153,7 +153,7 @@ class Worker:
                                     **kw)
             self.comm = TorchComm(peer_data=(mode == "gloo+peer" and self.use_gpu))
             self.comm.prepare_subgroups(self.world)
-            if self.use_gpu and os.environ.get("KUBEML_PEER", os.environ.get("KUBEML_ONESHOT", "0")) == "1":
+            if self.use_gpu and os.environ.get("KUBEML_PEER", "0") == "1":
                 # fp32 reductions over the world group (K-AVG rounds, BN statistics, counts) go
                 # through the peer-memory all-reduce over xGMI instead of RCCL
                 self.comm.enable_peer()

@@ -141,12 +141,16 @@ class SplitStreamer:
 
 
 class ResidentSplit:
-    """A whole split resident in HBM for the job (CIFAR-10 is 150 MB of a
-    GPU's 288 GB).  Uploaded once, in pinned chunks, when the job first plans the split; a
-    minibatch is then a view of it.  Nothing is copied while training steps run — a copy
-    beside the step's latency-bound dispatches slows every one of them (the framework-path
-    step ran 1.46-1.51 ms with per-batch H2D against 1.38 ms without,
-    profiles/e2e_r3.md).  Same interface as :class:`SplitStreamer`."""
+    """This rank's rows of a split resident in HBM for the job (CIFAR-10 is
+    150 MB of a GPU's 288 GB).  A minibatch is a view of the resident rows; nothing is copied
+    while training steps run — a copy beside the step's latency-bound dispatches slows every
+    one of them (the framework-path step ran 1.46-1.51 ms with per-batch H2D against 1.38 ms
+    without, profiles/e2e_r3.md).  Same interface as :class:`SplitStreamer`.
+
+    Only the rows a rank reads are uploaded: its ``split_minibatches`` shard (reference
+    python/kubeml/kubeml/network.py:263-264), i.e. 1/N of the split on each of N workers.  When
+    an elastic resize moves the shard outside the resident window, the window is re-uploaded
+    for the new shard (pinned chunks, synchronously, at the task start)."""
 
     def __init__(self, store, dataset: str, split: str, device: torch.device, chunk_rows: int = 8192):
         self.data_view, self.label_view = store.open(dataset, split)
@@ -154,22 +158,38 @@ class ResidentSplit:
         if arr.dtype not in _NP2TORCH:
             raise TypeError(f"unsupported dtype {arr.dtype}")
         self.n = int(arr.shape[0])
+        self.split = split
         self.device = device
-        dt = _NP2TORCH[arr.dtype]
-        self.x = torch.empty(tuple(arr.shape), dtype=dt, device=device)
-        with trace.span("h2d_resident", split=split, rows=self.n):
-            pin = torch.empty((min(chunk_rows, max(self.n, 1)),) + tuple(arr.shape[1:]), dtype=dt, pin_memory=True)
-            pn = pin.numpy()
-            stream = torch.cuda.current_stream(device)
-            for s in range(0, self.n, chunk_rows):
-                e = min(self.n, s + chunk_rows)
-                pn[:e - s] = arr[s:e]
-                self.x[s:e].copy_(pin[:e - s], non_blocking=True)
-                stream.synchronize()                     # the pinned chunk is reused
+        self.chunk_rows = int(chunk_rows)
+        self.dtype = _NP2TORCH[arr.dtype]
+        self.x = None
+        self.w0 = self.w1 = 0                  # resident rows [w0, w1) of the split
+        self.uploaded_rows = 0                 # rows moved host -> HBM so far (tests / metrics)
         lab = np.ascontiguousarray(self.label_view.arr).reshape(-1).astype(np.int64)
         self.labels = torch.from_numpy(lab).to(device)
         self.batches: List[Tuple[int, int]] = []
         self.pos = 0
+
+    def _upload(self, r0: int, r1: int):
+        arr = self.data_view.arr
+        x = torch.empty((r1 - r0,) + tuple(arr.shape[1:]), dtype=self.dtype, device=self.device)
+        with trace.span("h2d_resident", split=self.split, rows=r1 - r0):
+            cr = min(self.chunk_rows, max(r1 - r0, 1))
+            pins = [torch.empty((cr,) + tuple(arr.shape[1:]), dtype=self.dtype, pin_memory=True) for _ in range(2)]
+            done = [None, None]
+            stream = torch.cuda.current_stream(self.device)
+            for k, s in enumerate(range(r0, r1, cr)):
+                e = min(r1, s + cr)
+                b = k % 2
+                if done[b] is not None:
+                    done[b].synchronize()          # this pinned buffer's previous copy has landed
+                pins[b].numpy()[:e - s] = arr[s:e]  # host fill overlaps the other buffer's H2D
+                x[s - r0:e - r0].copy_(pins[b][:e - s], non_blocking=True)
+                done[b] = torch.cuda.Event()
+                done[b].record(stream)
+            stream.synchronize()
+        self.x, self.w0, self.w1 = x, r0, r1
+        self.uploaded_rows += r1 - r0
 
     @staticmethod
     def nbytes(store, dataset: str, split: str) -> int:
@@ -178,12 +198,17 @@ class ResidentSplit:
 
     def plan(self, doc_ranges: Sequence[Tuple[int, int]], batch_size: int, subset: int = 64):
         self.batches, self.pos = [], 0
+        lo, hi = self.n, 0
         for d0, d1 in doc_ranges:
             r0, r1 = d0 * subset, min(d1 * subset, self.n)
+            if r1 > r0:
+                lo, hi = min(lo, r0), max(hi, r1)
             for s in range(r0, r1, batch_size):
                 self.batches.append((s, min(batch_size, r1 - s)))
+        if hi > lo and (self.x is None or lo < self.w0 or hi > self.w1):
+            self._upload(lo, hi)
 
     def next(self):
         r0, nr = self.batches[self.pos]
         self.pos += 1
-        return self.x[r0:r0 + nr], self.labels[r0:r0 + nr]
+        return self.x[r0 - self.w0:r0 - self.w0 + nr], self.labels[r0:r0 + nr]

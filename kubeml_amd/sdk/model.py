@@ -514,6 +514,17 @@ class KubeModel(ABC):
                id(comm) if comm is not None else None)
         g = self._graphs.get(key)
         if g is None:
+            g = self._build_step(key, x, y, loss_fn, comm)
+        g["x"].copy_(x, non_blocking=True)
+        g["y"].copy_(y, non_blocking=True)
+        loss = g["step"]()
+        if grad:
+            self._synced_steps += 1
+        return loss
+
+    def _build_step(self, key, x, y, loss_fn, comm):
+        """Build and capture the train-step graph for one batch shape (+ comm group)."""
+        with trace.span("step_graph", shape=str(tuple(x.shape)), comm=comm.world if comm is not None else 1):
             from ..engine.dp import make_train_step
             if len(self._graphs) >= self.MAX_GRAPHS:
                 self._graphs.pop(next(iter(self._graphs)))
@@ -526,7 +537,6 @@ class KubeModel(ABC):
             st = make_train_step(self._network, self._flat, self.optimizer, loss_fn, xs, ys,
                                  group=comm.group if comm is not None else None,
                                  world=comm.world if comm is not None else 1,
-                                 graph_comm=os.environ.get("KUBEML_GRAPH_COMM", "1") != "0",
                                  plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0)
             self.logger.info("train step graph: batch %s, comm %s, plan %s, transport %s", tuple(x.shape),
                              comm.world if comm is not None else 1, plan.tag() if plan is not None else None,
@@ -537,15 +547,10 @@ class KubeModel(ABC):
                 else:
                     comm.grad_peer = st.peer          # one gradient transport per group, reused
             from ..runtime.worker import busy
-            with busy():                          # capture + warm-up can take seconds
+            with busy(), trace.span("capture"):   # capture + warm-up can take seconds
                 st.capture()
             g = self._graphs[key] = {"x": xs, "y": ys, "step": st}
-        g["x"].copy_(x, non_blocking=True)
-        g["y"].copy_(y, non_blocking=True)
-        loss = g["step"]()
-        if grad:
-            self._synced_steps += 1
-        return loss
+            return g
 
     def _reusable_peer(self, comm, plan):
         """The transport a new train-step graph may reuse: the shard of this model's space on
@@ -589,6 +594,8 @@ class KubeModel(ABC):
         if g is None:
             if len(self._eval_graphs) >= self.MAX_GRAPHS:
                 self._eval_graphs.pop(next(iter(self._eval_graphs)))
+            _sp = trace.span("eval_graph", shape=str(tuple(x.shape)))
+            _sp.__enter__()
             xs, ys = x.clone(), y.clone()
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -599,6 +606,7 @@ class KubeModel(ABC):
             with torch.cuda.graph(graph):
                 outs = fwd(xs, ys)
             g = self._eval_graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
+            _sp.__exit__(None, None, None)
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
         g["graph"].replay()

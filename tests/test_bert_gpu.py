@@ -84,7 +84,7 @@ def test_bert_tiny_graphed_adam_learns():
 @pytest.mark.parametrize("dropout", [0.0, 0.1])
 def test_bert_fused_residual_and_bias_gradients_match_unfused(dropout):
     """Residual-gradient sums in the dgrad epilogue and the out-projection / FFN2 bias
-    gradients summed inside the LayerNorm backward (KUBEML_RES_FUSE, default on) give the
+    gradients summed inside the LayerNorm backward (_RES_FUSE, default on) give the
     same loss and gradients as autograd adds + column-sum kernels (same dropout masks)."""
     from kubeml_amd.models.bert import bert_tiny_mlm
     from kubeml_amd.nn import flatten_module

@@ -50,13 +50,13 @@ def test_two_identical_runs_are_bitwise_equal():
 def test_gradient_buffer_is_not_memset_every_step():
     """After the first step only add-only producers' regions are zeroed (ResNet-34 has none:
     every gradient is stored by its producer), and the result equals a full-zero run."""
-    import os
+    from kubeml_amd.nn.flat import FlatParamSpace
     s1, g1, _ = _run(steps=3)
-    os.environ["KUBEML_FULL_ZERO"] = "1"
+    FlatParamSpace.full_zero = True
     try:
         s2, g2, _ = _run(steps=3)
     finally:
-        del os.environ["KUBEML_FULL_ZERO"]
+        FlatParamSpace.full_zero = False
     assert torch.equal(g1, g2) and torch.equal(s1, s2)
     from kubeml_amd.models.resnet import resnet34
     from kubeml_amd.nn import flatten_module

@@ -75,3 +75,30 @@ def test_dataset_resident_or_streamed_matches_load_docs(tmp_path, monkeypatch, b
     assert np.array_equal(xb.cpu().numpy(), ref_x[:128]) and np.array_equal(yb.cpu().numpy(), ref_y[:128])
     xb, yb = s.next()
     assert np.array_equal(xb.cpu().numpy(), ref_x[128:192])     # round boundary: ragged batch
+
+
+def test_resident_split_holds_only_the_ranks_shard(tmp_path):
+    """Each of N workers uploads its own split_minibatches shard, not the whole split (reference
+    network.py:263-264); an elastic resize that moves the shard re-uploads just the new one."""
+    from kubeml_amd.sdk.loader import ResidentSplit
+    from kubeml_amd.sdk.util import split_minibatches
+    st, x, y = _store(tmp_path)
+    docs = st.num_docs("ds", "train")
+    for world in (2, 4):
+        for rank in range(world):
+            s = ResidentSplit(st, "ds", "train", dev)
+            sh = split_minibatches(range(docs), world)[rank]
+            s.plan([(d, d + 2) for d in range(sh.start, sh.stop, 2)], 128)
+            r0, r1 = sh.start * 64, min(sh.stop * 64, x.shape[0])
+            assert (s.w0, s.w1) == (r0, r1) and s.uploaded_rows == r1 - r0 < x.shape[0] // world + 64
+            xb, yb = s.next()
+            n = min(128, r1 - r0)
+            assert np.array_equal(xb.cpu().numpy(), x[r0:r0 + n]) and np.array_equal(yb.cpu().numpy(), y[r0:r0 + n])
+    s = ResidentSplit(st, "ds", "train", dev)
+    s.plan([(0, 4)], 64)
+    s.plan([(1, 3)], 64)                       # inside the window: nothing moves
+    assert s.uploaded_rows == 256
+    s.plan([(8, 12)], 64)                      # resize moved the shard: new window only
+    assert (s.w0, s.w1) == (512, 768) and s.uploaded_rows == 512
+    xb, _ = s.next()
+    assert np.array_equal(xb.cpu().numpy(), x[512:576])

@@ -247,7 +247,7 @@ def test_resnet32_cifar_learns_on_gpu():
 
 
 def test_resnet_fused_stem_matches_unfused_stem():
-    """KUBEML_STEM_FUSE path (one BN->ReLU->max-pool pass, ReLU mask folded into the pool
+    """_STEM_FUSE path (one BN->ReLU->max-pool pass, ReLU mask folded into the pool
     backward) vs the unfused BN-apply + max-pool pair and an fp32 torch stem, on the stem
     alone (conv1 -> bn1 -> ReLU -> max-pool -> fixed random readout): output, running stats
     and the conv1 / bn1 gradients."""
@@ -299,7 +299,7 @@ def test_resnet_fused_stem_matches_unfused_stem():
 
 
 def test_resnet34_bn_fold_matches_unfolded():
-    """BasicBlock bn1 + ReLU applied inside conv2's halo patch staging (KUBEML_BN_FOLD path,
+    """BasicBlock bn1 + ReLU applied inside conv2's halo patch staging (_BN_FOLD path,
     kernels.conv_fwd_bnin) vs a separate BN apply: logits, loss, every gradient, the folded BNs'
     running statistics — bit-identical forward (same rows, same summation order)."""
     from kubeml_amd.models.resnet import resnet34
