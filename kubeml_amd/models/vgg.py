@@ -10,8 +10,15 @@ checkpoints interoperate.  Two heads:
 * ``head="cifar"`` (default for the CIFAR configs) — 512→4096→4096→classes, as in the
   pytorch-cifar100 recipe the reference cites (function_vgg11.py:14-15).
 
-Activations are NHWC bf16 on the GPU; Conv→BN→ReLU triples run as conv (MFMA
-implicit GEMM with BN-statistics epilogue) + one fused BN-apply+ReLU kernel.
+Activations are NHWC bf16 on the GPU.  In GPU training the Conv→BN→ReLU units between two
+max-pools run as one fused autograd node (nn/fused.py ``BlockFn``, the ResNet blocks'
+executor): conv (MFMA implicit GEMM, +bias) with the BN statistics in its epilogue, one
+BN-apply+ReLU pass; backward: BN backward, then dgrad + wgrad as one grouped launch whose dgrad
+epilogue already emits the next BatchNorm's dgamma/dbeta partial rows.  The classifier's
+Linear+ReLU pairs run with the ReLU in the GEMM epilogue.  The classifier's
+dropout is the in-tree counter-hash kernel (nn/transformer.py ``Dropout``: the mask is a hash of
+(seed, step, layer salt, index), recomputed in the backward, nothing stored); its step counter
+advances once per training forward on the device, so a replayed hipGraph draws a new mask.
 """
 from __future__ import annotations
 
@@ -20,7 +27,39 @@ from typing import List, Union
 import torch
 import torch.nn as tnn
 
+from ..nn.fused import BlockFn, block_params, refresh_transposed
 from ..nn.modules import BatchNorm2d, Conv2d, Flatten, Linear, MaxPool2d, ReLU, to_nhwc
+from ..nn.transformer import Dropout, RNGState
+
+
+class _Stage:
+    """Conv→BN→ReLU units between two max-pools (plain holder: the modules stay registered under
+    ``features`` with torchvision's names); ``BlockFn`` runs the plan."""
+
+    def __init__(self, units):
+        self._kml_plan = [(conv, bn, True, "main") for conv, bn in units]
+
+
+def _segments(features: tnn.Sequential):
+    """[(stage | None, pool | None)]: the fused stages and the max-pools of a BN feature stack, or
+    None when the stack is not made of Conv→BN→ReLU units and pools."""
+    mods = list(features)
+    segs, units, i = [], [], 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, Conv2d) and i + 2 < len(mods) and isinstance(mods[i + 1], BatchNorm2d) and \
+                isinstance(mods[i + 2], ReLU):
+            units.append((m, mods[i + 1]))
+            i += 3
+        elif isinstance(m, MaxPool2d):
+            segs.append((_Stage(units) if units else None, m))
+            units = []
+            i += 1
+        else:
+            return None
+    if units:
+        segs.append((_Stage(units), None))
+    return segs
 
 CFGS = {
     "vgg11": [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
@@ -69,10 +108,12 @@ class VGG(tnn.Module):
             self.avgpool = None
             fin = 512
         self.flatten = Flatten()
+        self.rng = RNGState(seed=17)
         self.classifier = tnn.Sequential(
-            Linear(fin, 4096), ReLU(True), tnn.Dropout(dropout),
-            Linear(4096, 4096), ReLU(True), tnn.Dropout(dropout),
+            Linear(fin, 4096, fused_relu=True), ReLU(True), Dropout(dropout, rng=self.rng),
+            Linear(4096, 4096, fused_relu=True), ReLU(True), Dropout(dropout, rng=self.rng),
             Linear(4096, num_classes))
+        object.__setattr__(self, "_kml_segments", _segments(self.features) if batch_norm else None)
         for m in self.modules():
             if isinstance(m, Conv2d):
                 tnn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
@@ -98,13 +139,44 @@ class VGG(tnn.Module):
             i += 1
         return x
 
+    def _features_fused(self, x):
+        from ..ops import kernels as K
+        sp = getattr(self, "_kml_flat", None)
+        if sp is not None and sp.i64_buffers:
+            K.add_i64_(sp.i64_arena_now())     # every BN's num_batches_tracked, one launch
+        else:
+            for m in self.features:
+                if isinstance(m, BatchNorm2d):
+                    K.add_i64_(m.num_batches_tracked)
+        convs = getattr(self, "_kml_convs", None)
+        if convs is None:
+            convs = [m for m in self.features if isinstance(m, Conv2d)]
+            object.__setattr__(self, "_kml_convs", convs)
+        refresh_transposed(convs)
+        for stage, pool in self._kml_segments:
+            if stage is not None:
+                x = BlockFn.apply(x, stage, *block_params(stage))
+            if pool is not None:
+                x = pool(x)
+        return x
+
     def forward(self, x):
+        fused = x.is_cuda and self.training and torch.is_grad_enabled() and self._kml_segments is not None
+        if self.training and x.is_cuda:
+            self.rng.advance(x.device)      # a fresh dropout mask per step (device counter)
         x = to_nhwc(x, 8)
-        x = self._features(x)
+        x = self._features_fused(x) if fused else self._features(x)
         if self.avgpool is not None:
             x = self.avgpool(x)
         x = self.flatten(x)
-        return self.classifier(x)
+        if not x.is_cuda:
+            return self.classifier(x)
+        mods = list(self.classifier)
+        for i, m in enumerate(mods):
+            if isinstance(m, ReLU) and i > 0 and getattr(mods[i - 1], "fused_relu", False):
+                continue                      # already applied in the Linear's epilogue
+            x = m(x)
+        return x
 
 
 def vgg11(num_classes: int = 1000, batch_norm: bool = False, head: str = "imagenet", **kw) -> VGG:

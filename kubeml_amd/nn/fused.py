@@ -160,6 +160,19 @@ _BN_FOLD = True
 _FOLD_GROUP = False
 
 
+def _conv_bias(conv):
+    """fp32 storage of a conv's bias (VGG), or None.
+
+    Its gradient is never produced: in front of a training-mode BatchNorm a per-channel bias
+    has an identically zero gradient — the BN backward output dc = a (dy - mean(dy) - xhat
+    mean(dy xhat)) sums to a (sum dy - sum dy - mean(dy xhat) sum xhat) = 0 per channel because
+    sum xhat = 0 — so the region stays zero (FlatParamSpace.finish_grads zeroes regions nobody
+    wrote) instead of column-summing rounding noise.  The forward still adds it, so batch and
+    running statistics (and eval outputs, checkpoints) match torch's conv(+bias) -> BN."""
+    b = getattr(conv, "bias", None)
+    return master_of(b) if b is not None else None
+
+
 class ConvBNUnit:
     """Stateless executor for (conv module, bn module, relu)."""
 
@@ -174,7 +187,8 @@ class ConvBNUnit:
         K_out = w.shape[0]
         G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, group=group)
         stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
-        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True, stats_group=group)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=_conv_bias(conv), stats=stats, stats_part=True,
+                       stats_group=group)
         return c, stats, G
 
     @staticmethod
@@ -207,14 +221,15 @@ class ConvBNUnit:
         w = shadow_of(conv.weight)
         kh, kw = conv.kernel_size
         gamma, beta = master_of(bn.weight), master_of(bn.bias)
+        bias = _conv_bias(conv)
         if training:
             # per-wave partial statistics from the conv epilogue (plain stores, every row
             # written: no zeroing, no atomics); bn_apply sums them in its prologue
             K_out = w.shape[0]
-            wu = unrolled_for(conv, x)
+            wu = unrolled_for(conv, x) if bias is None else None   # the 1x1 form has no bias epilogue
             G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, unroll=wu is not None)
             stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
-            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True, wu=wu)
+            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=bias, stats=stats, stats_part=True, wu=wu)
             C = c.shape[-1]
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             rstd = torch.empty_like(mean)
@@ -222,7 +237,7 @@ class ConvBNUnit:
                            run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
                            momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
             return y, (x, c, y if relu else None, mean, rstd)
-        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=bias)
         y = K.bn_apply(c, None, gamma, beta, res=res, run_mean=bn.running_mean, run_var=bn.running_var,
                        eps=bn.eps, relu=relu, training=False)
         return y, None
@@ -374,6 +389,8 @@ def _fold_unit(x, plan):
     i1, i2 = mains
     conv1, _, relu1, _ = plan[i1]
     conv2 = plan[i2][0]
+    if getattr(conv1, "bias", None) is not None or getattr(conv2, "bias", None) is not None:
+        return None          # the BN-folding halo conv has no bias epilogue
     if not relu1 or conv2.kernel_size != (3, 3) or tuple(conv2.stride) != (1, 1) or tuple(conv2.padding) != (1, 1):
         return None
     B, H, W, _ = x.shape

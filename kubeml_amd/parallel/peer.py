@@ -278,6 +278,16 @@ def ipc_zeros(numel: int, dtype: torch.dtype, device) -> Optional[torch.Tensor]:
         return None
 
 
+def _device_ident(device) -> tuple:
+    """Identity of the physical GPU behind ``device`` (PCI location), comparable across processes."""
+    import socket
+    props = torch.cuda.get_device_properties(device)
+    pci = tuple(getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if all(v is None for v in pci):
+        pci = (torch.device(device).index, os.environ.get("HIP_VISIBLE_DEVICES"), os.environ.get("ROCR_VISIBLE_DEVICES"))
+    return (socket.gethostname(),) + pci
+
+
 def _handle_of(ptr: int) -> bytes:
     nb = HIP.raw("kml_ipc_handle_bytes")
     h = (ctypes.c_char * nb)()
@@ -327,7 +337,11 @@ class PeerShard:
             mine = [self.region, space.grad.data_ptr(), space.shadow.data_ptr(), space.state.data_ptr()]
             hs = [_handle_of(p) for p in mine]
             allh: List[list] = [None] * self.world
-            dist.all_gather_object(allh, hs, group=group)
+            dist.all_gather_object(allh, (hs, _device_ident(self.device)), group=group)
+            # ranks sharing one GPU (packed workers, tests): a barrier must not occupy every CU
+            # while a peer still needs them to reach it -> one-block wait launches (split)
+            self.packed = len({a[1] for a in allh}) < self.world
+            allh = [a[0] for a in allh]
             cols: List[list] = [[0] * self.world for _ in range(4)]
             try:
                 for p in range(self.world):
@@ -376,30 +390,30 @@ class PeerShard:
                 mom = optimizer._bufs(sp, ["momentum"])["momentum"]
                 first = optimizer.first_tensor(sp.device)
         ctr, ab, an = advance if advance is not None else (None, 0.0, 0.0)
-        HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d s",
+        HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d i s",
                  ctypes.addressof(self._flags), ctypes.addressof(self._grads), self.region, self.ctrl, self.rank,
                  self.world, self.lo, self.hi, int(fused), sp.master.data_ptr() if fused else None,
                  mom.data_ptr() if mom is not None else None, sp.shadow.data_ptr() if fused else None,
                  lr.data_ptr() if lr is not None else None, float(wd), float(momentum), float(dampening), nesterov,
                  first.data_ptr() if first is not None else None, 1.0 / self.world,
                  ctr.data_ptr() if ctr is not None else None, float(ab), float(an), int(max_blocks),
-                 self.timeout_s, self._stream())
+                 self.timeout_s, int(self.packed), self._stream())
         if first is not None:
             from ..ops import kernels as K
             K.fill_(first, 0.0)
 
     def all_gather_shadow(self, max_blocks: int = 256):
         """Every rank's shadow := the owners' freshly updated chunks (closes the step's call)."""
-        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d s", ctypes.addressof(self._flags),
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i s", ctypes.addressof(self._flags),
                  ctypes.addressof(self._shadows), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, self._stream())
+                 self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, int(self.packed), self._stream())
         self.space._master_stale = True
 
     def gather_master(self, max_blocks: int = 256):
         """Collective: complete the fp32 master from the owners' chunks (one barrier)."""
-        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d s", ctypes.addressof(self._flags),
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i s", ctypes.addressof(self._flags),
                  ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, self._stream())
+                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, int(self.packed), self._stream())
         self.space._master_stale = False
 
     # ------------------------------------------------------------------ health

@@ -160,6 +160,11 @@ class Worker:
         else:
             self.comm = LocalComm()
         self.store = ShardStore(self.store_dir)
+        # a resident worker starts warm (the reference's Fission pool keeps pre-specialised
+        # containers): the first ``torch.optim`` construction of a user function imports
+        # torch._dynamo, ~1.4 s that would otherwise land inside the job's first epoch
+        with busy():
+            import torch._dynamo  # noqa: F401
 
     # ------------------------------------------------------------------ ops
     def handle(self, msg: Dict[str, Any]) -> Dict[str, Any]:

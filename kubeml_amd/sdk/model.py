@@ -263,7 +263,8 @@ class KubeModel(ABC):
 
     # ---- train (network.py:252-310, K-AVG) ------------------------------------------------
     def _train(self) -> float:
-        self._on_train_start()
+        with trace.span("train_start"):
+            self._on_train_start()
         comm = self._comm()
         N, fid, K = self.args._N, self.args._func_id, self.args._K
         num_docs = self._dataset.num_docs
@@ -272,7 +273,8 @@ class KubeModel(ABC):
             self._averager.broadcast_(comm, 0)
         ctx = current_task()
         if ctx is not None and os.environ.get("KUBEML_CHECKSUMS", "1") != "0":
-            ctx.extra["start_checksum"] = self.model_checksum()
+            with trace.span("checksum"):
+                ctx.extra["start_checksum"] = self.model_checksum()
         splits = split_minibatches(range(num_docs), N)
         assigned = splits[fid]
         per = max(get_subset_period(K, self.batch_size, assigned), 1)
@@ -292,8 +294,9 @@ class KubeModel(ABC):
             self._prime_grad_sync()
         self.logger.debug("subsets per iteration %d, rounds %d, grad-sync %s", per, rounds, grad_ok)
         # every minibatch of this task queued on the pinned stream (GPU, batch-hook datasets)
-        self._dataset._plan_stream("train", [(i, min(assigned.stop, i + per)) for i in intervals],
-                                   self.batch_size, self.device)
+        with trace.span("plan_stream"):
+            self._dataset._plan_stream("train", [(i, min(assigned.stop, i + per)) for i in intervals],
+                                       self.batch_size, self.device)
         loss_host, loss_dev, num_iterations = 0.0, None, 0
         self.sync_seconds = 0.0
         grad_rounds = 0
@@ -365,7 +368,8 @@ class KubeModel(ABC):
             self._dataset._stream_end()
         self._on_train_end()
         if loss_dev is not None:
-            loss_host += float(loss_dev.item())
+            with trace.span("loss_sync"):          # waits for the queued steps to finish
+                loss_host += float(loss_dev.item())
         self.grad_rounds = grad_rounds
         if ctx is not None and os.environ.get("KUBEML_CHECKSUMS", "1") != "0":
             ctx.extra["end_checksum"] = self.model_checksum()

@@ -168,6 +168,10 @@ def candidates(mode, M, N, Kd, cin, cout, ntap):
     """Every (bm, bn, bk, splits, variant) plan worth timing for one conv GEMM."""
     cands = []
     split_opts = [1, 2, 4, 8, 16] if mode != "wgrad" else [1, 2, 4, 8, 16, 32, 64]
+    if mode != "wgrad" and M * N >= 256 * 256 * 64:
+        split_opts = [1, 2]                 # thousands of output tiles: split-K only adds traffic
+    elif mode == "wgrad" and Kd >= 32768:
+        split_opts = [4, 8, 16, 32, 64]    # long reductions: never one block per tile
     for bm, bn in TILES:
         if bm > max(32, -(-M // 32) * 32) or bn > max(32, -(-N // 32) * 32):
             continue
@@ -187,6 +191,15 @@ def candidates(mode, M, N, Kd, cin, cout, ntap):
     return cands
 
 
+def save(args, table):
+    out = {"model": "resnet34+bert_base" if args.bert else args.model, "batch": args.batch, "arch": "gfx950",
+           "entries": sorted(table.values(), key=lambda e: (e["mode"], -e["M"]))}
+    tmp = args.out + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(out, f, indent=1)
+    os.replace(tmp, args.out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet34")
@@ -197,6 +210,7 @@ def main():
     ap.add_argument("--fresh", action="store_true", help="ignore existing entries (re-measure every shape)")
     ap.add_argument("--pairs", action="store_true", help="tune grouped dgrad+wgrad launches (conv layers)")
     ap.add_argument("--size", type=int, default=32, help="input image size of the CNN (224 for ImageNet shapes)")
+    ap.add_argument("--max-seconds", type=float, default=0, help="stop (table saved) after this long")
     args = ap.parse_args()
     dev = torch.device("cuda")
     if args.bert:
@@ -268,6 +282,12 @@ def main():
             table[key] = entry
             report.append(entry)
             print(json.dumps(entry), flush=True)
+            save(args, table)                     # incremental: a cut-off run keeps its shapes
+            if args.max_seconds and time.time() - t_start > args.max_seconds:
+                break
+        if args.max_seconds and time.time() - t_start > args.max_seconds:
+            print(json.dumps({"stopped": "max-seconds"}), flush=True)
+            break
     out = {"model": "resnet34+bert_base" if args.bert else args.model, "batch": args.batch, "arch": "gfx950",
            "entries": sorted(table.values(), key=lambda e: (e["mode"], -e["M"]))}
     with open(args.out, "w") as f:
