@@ -166,11 +166,13 @@ __device__ bool pc_barrier(const PcPeers& peers, const char* region, unsigned* c
 }
 
 // the last block of a call's final launch advances the barrier sequence and the call count
-__device__ void pc_finish_call(unsigned* ctrl, unsigned barriers) {
+// (and, when timing, stamps the collective's end)
+__device__ void pc_finish_call(unsigned* ctrl, unsigned barriers, unsigned long long* stamp = nullptr) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned t = __hip_atomic_fetch_add(ctrl + C_TICKET, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
+      if (stamp) *stamp = __builtin_amdgcn_s_memrealtime();
       __hip_atomic_store(ctrl + C_TICKET, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned s = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned c = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -349,6 +351,26 @@ struct ZsPeers {
   const char* data[PC_MAX_RANKS];    // every rank's gradient / shadow / master buffer
 };
 
+// Ranks that share one GPU (packed workers) must not spin in every block of a work kernel while
+// a peer still needs CUs to reach the barrier: there the barrier is a one-block launch of its
+// own (k_zs_wait) and the work kernel that follows only reads the poison flag (`split`).
+__device__ __forceinline__ bool zs_enter(const ZsPeers& peers, char* region, unsigned* ctrl, int rank, int world,
+                                         unsigned target, unsigned long long limit, int split) {
+  if (split) return __hip_atomic_load(ctrl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  PcPeers fl;
+  for (int p = 0; p < world; ++p) fl.region[p] = peers.flags[p];
+  return pc_barrier(fl, region, ctrl, rank, world, target, limit);
+}
+
+__global__ __launch_bounds__(64) void k_zs_wait(ZsPeers peers, char* region, unsigned* ctrl, int rank, int world,
+                                                unsigned bar, unsigned long long limit, unsigned long long* stamp) {
+  if (stamp && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();  // collective start (timing)
+  const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  PcPeers fl;
+  for (int p = 0; p < world; ++p) fl.region[p] = peers.flags[p];
+  (void)pc_barrier(fl, region, ctrl, rank, world, seq + bar, limit);
+}
+
 template <int P, bool SGD>
 __global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region, unsigned* ctrl, int rank,
                                                     long long lo, long long hi, float* __restrict__ own_grad,
@@ -357,7 +379,7 @@ __global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region,
                                                     float wd, float momentum, float dampening, int nesterov,
                                                     const float* __restrict__ first_ptr, float grad_scale,
                                                     float* __restrict__ adv_ctr, float adv_batch, float adv_n,
-                                                    unsigned long long limit) {
+                                                    unsigned long long limit, int split) {
   if (adv_ctr && blockIdx.x == 0 && threadIdx.x == 0) {  // data-sampler counter (see k_sgd)
     adv_ctr[1] += 1.f;
     float st = adv_ctr[2] + adv_batch;
@@ -365,10 +387,7 @@ __global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region,
     adv_ctr[2] = st;
   }
   const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  PcPeers fl;
-#pragma unroll
-  for (int p = 0; p < P; ++p) fl.region[p] = peers.flags[p];
-  const bool ok = pc_barrier(fl, region, ctrl, rank, P, seq + 1u, limit);
+  const bool ok = zs_enter(peers, region, ctrl, rank, P, seq + 1u, limit, split);
   const long long nv = (hi - lo) >> 2;  // fp32x4 vectors of this rank's chunk
   __amdgpu_buffer_rsrc_t rs[P];
 #pragma unroll
@@ -434,12 +453,10 @@ __global__ __launch_bounds__(PC_BLOCK) void k_zs_rs(ZsPeers peers, char* region,
 template <int P>
 __global__ __launch_bounds__(PC_BLOCK) void k_zs_gather(ZsPeers peers, char* region, unsigned* ctrl, int rank,
                                                         char* __restrict__ own, long long n, long long chunk, int esz,
-                                                        unsigned bar, unsigned finish, unsigned long long limit) {
+                                                        unsigned bar, unsigned finish, unsigned long long limit,
+                                                        int split, unsigned long long* stamp) {
   const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  PcPeers fl;
-#pragma unroll
-  for (int p = 0; p < P; ++p) fl.region[p] = peers.flags[p];
-  const bool ok = pc_barrier(fl, region, ctrl, rank, P, seq + bar, limit);
+  const bool ok = zs_enter(peers, region, ctrl, rank, P, seq + bar, limit, split);
   const long long cv = chunk * esz / 16;  // vectors per (full) chunk
   const long long total = (long long)(P - 1) * cv;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -461,7 +478,7 @@ __global__ __launch_bounds__(PC_BLOCK) void k_zs_gather(ZsPeers peers, char* reg
     }
     *reinterpret_cast<uint4*>(own + off) = w;
   }
-  if (finish) pc_finish_call(ctrl, finish);
+  if (finish) pc_finish_call(ctrl, finish, stamp);
 }
 
 // side-stream HBM streamer for the interference probe: `passes` copies of n 16-byte vectors
@@ -652,7 +669,7 @@ KML_API int kml_zs_reduce_scatter(const void* const* flags, const void* const* g
                                   float* mom, bf16_t* shadow, const float* lr_ptr, float wd, float momentum,
                                   float dampening, int nesterov, const float* first_ptr, float grad_scale,
                                   float* adv_ctr, float adv_batch, float adv_n, int max_blocks, double timeout_s,
-                                  hipStream_t s) {
+                                  int split, unsigned long long* stamp, hipStream_t s) {
   ZsPeers zp;
   if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || lo < 0 || hi < lo || (lo & 3) ||
       (hi & 3) || max_blocks < 1 || !(timeout_s > 0.0) || !zs_peers(zp, flags, grads, world) ||
@@ -661,17 +678,22 @@ KML_API int kml_zs_reduce_scatter(const void* const* flags, const void* const* g
   float* own = const_cast<float*>(reinterpret_cast<const float*>(grads[rank]));
   const unsigned g = zs_grid((hi - lo) / 4, max_blocks);
   const unsigned long long lim = zs_limit(timeout_s);
+  if (split)
+    hipLaunchKernelGGL(k_zs_wait, dim3(1), dim3(64), 0, s, zp, reinterpret_cast<char*>(region),
+                       reinterpret_cast<unsigned*>(ctrl), rank, world, 1u, lim, stamp);
   switch (world) {
 #define ZS_CASE(P)                                                                                                   \
   case P:                                                                                                            \
     if (fused_sgd)                                                                                                   \
       hipLaunchKernelGGL((k_zs_rs<P, true>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),     \
                          reinterpret_cast<unsigned*>(ctrl), rank, lo, hi, own, master, mom, shadow, lr_ptr, wd,      \
-                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim);      \
+                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim,       \
+                         split);                                                                                     \
     else                                                                                                             \
       hipLaunchKernelGGL((k_zs_rs<P, false>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),    \
                          reinterpret_cast<unsigned*>(ctrl), rank, lo, hi, own, master, mom, shadow, lr_ptr, wd,      \
-                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim);      \
+                         momentum, dampening, nesterov, first_ptr, grad_scale, adv_ctr, adv_batch, adv_n, lim,       \
+                         split);                                                                                     \
     break;
     ZS_CASE(1) ZS_CASE(2) ZS_CASE(3) ZS_CASE(4) ZS_CASE(5) ZS_CASE(6) ZS_CASE(7) ZS_CASE(8)
 #undef ZS_CASE
@@ -686,7 +708,7 @@ KML_API int kml_zs_reduce_scatter(const void* const* flags, const void* const* g
 // `finish` barriers close the call.
 KML_API int kml_zs_all_gather(const void* const* flags, const void* const* bufs, void* region, void* ctrl, int rank,
                               int world, long long n, long long chunk, int esz, int bar, int finish, int max_blocks,
-                              double timeout_s, hipStream_t s) {
+                              double timeout_s, int split, unsigned long long* stamp, hipStream_t s) {
   ZsPeers zp;
   if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || n < 0 || chunk <= 0 ||
       (esz != 2 && esz != 4) || (chunk * esz) % 16 || chunk * world < n || bar < 1 || finish < 0 ||
@@ -695,12 +717,15 @@ KML_API int kml_zs_all_gather(const void* const* flags, const void* const* bufs,
   char* own = const_cast<char*>(reinterpret_cast<const char*>(bufs[rank]));
   const unsigned g = zs_grid((long long)(world - 1) * chunk * esz / 16, max_blocks);
   const unsigned long long lim = zs_limit(timeout_s);
+  if (split)
+    hipLaunchKernelGGL(k_zs_wait, dim3(1), dim3(64), 0, s, zp, reinterpret_cast<char*>(region),
+                       reinterpret_cast<unsigned*>(ctrl), rank, world, (unsigned)bar, lim, nullptr);
   switch (world) {
 #define ZS_CASE(P)                                                                                                   \
   case P:                                                                                                            \
     hipLaunchKernelGGL((k_zs_gather<P>), dim3(g), dim3(PC_BLOCK), 0, s, zp, reinterpret_cast<char*>(region),         \
                        reinterpret_cast<unsigned*>(ctrl), rank, own, n, chunk, esz, (unsigned)bar, (unsigned)finish,  \
-                       lim);                                                                                         \
+                       lim, split, stamp);                                                                           \
     break;
     ZS_CASE(1) ZS_CASE(2) ZS_CASE(3) ZS_CASE(4) ZS_CASE(5) ZS_CASE(6) ZS_CASE(7) ZS_CASE(8)
 #undef ZS_CASE

@@ -169,18 +169,22 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
         if not (fused_sgd or getattr(optimizer, "supports_ranges", lambda: False)()):
             raise ValueError("the shard plan needs a fused optimizer over one flat space")
 
-        def shard_step():
+        def shard_step(stamps=None):
+            """stamps: int64[2] device buffer (timing) — start / end of the collective."""
+            s0 = s1 = None
+            if stamps is not None:
+                s0, s1 = stamps.data_ptr(), stamps.data_ptr() + 8
             space.finish_grads()
             if fused_sgd:           # reduce-scatter + SGD + shadow chunk in one pass
-                shard.reduce_scatter(optimizer, advance=fold, max_blocks=blocks)
+                shard.reduce_scatter(optimizer, advance=fold, max_blocks=blocks, stamp=s0)
             else:
-                shard.reduce_scatter(None, max_blocks=blocks)
+                shard.reduce_scatter(None, max_blocks=blocks, stamp=s0)
                 optimizer.set_grad_scale(scale)
                 optimizer.step_range(shard.lo, shard.hi, max_blocks=blocks)
                 if fold is not None:
                     from ..ops import kernels as K
                     K.advance_counter_(*fold)
-            shard.all_gather_shadow(max_blocks=blocks)
+            shard.all_gather_shadow(max_blocks=blocks, stamp=s1)
             if post is not None:
                 post()
 

@@ -345,10 +345,7 @@ class GraphedTrainStep:
             works += self._issue(k)
         self._finish_comm(works)
         if self.shard_step is not None and self._comm_on:
-            dev = self._dev
-            self._stamp(0, dev)
-            self.shard_step()
-            self._stamp(1, dev)
+            self.shard_step(stamps=self._stamps)     # the collective's own launches stamp it
         else:
             self.opt_step()
         return loss

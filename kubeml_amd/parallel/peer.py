@@ -338,9 +338,12 @@ class PeerShard:
             hs = [_handle_of(p) for p in mine]
             allh: List[list] = [None] * self.world
             dist.all_gather_object(allh, (hs, _device_ident(self.device)), group=group)
-            # ranks sharing one GPU (packed workers, tests): a barrier must not occupy every CU
-            # while a peer still needs them to reach it -> one-block wait launches (split)
+            # the barrier is a one-block launch of its own and the work kernels behind it never
+            # spin (split): they run at full grid like any streaming kernel, with no per-block
+            # fence, and ranks that share one GPU (packed workers, tests) cannot fill the CUs a
+            # peer still needs to reach the barrier
             self.packed = len({a[1] for a in allh}) < self.world
+            self.split = True
             allh = [a[0] for a in allh]
             cols: List[list] = [[0] * self.world for _ in range(4)]
             try:
@@ -371,10 +374,11 @@ class PeerShard:
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def reduce_scatter(self, optimizer=None, advance=None, max_blocks: int = 256):
+    def reduce_scatter(self, optimizer=None, advance=None, max_blocks: int = 256, stamp: Optional[int] = None):
         """Chunk ``[lo, hi)`` := sum over ranks.  With a fused-SGD ``optimizer`` the sum is
         applied at once (master, momentum, shadow of the chunk; 1/P folded in); else it lands in
-        the own gradient chunk for :meth:`update_range`."""
+        the own gradient chunk for :meth:`update_range`.  ``stamp``: device address of an int64 the
+        barrier launch stamps (100 MHz wall clock) when timing the step's collectives."""
         sp = self.space
         if self.region is None:
             raise PeerCommError("sharded update used after close()")
@@ -390,30 +394,31 @@ class PeerShard:
                 mom = optimizer._bufs(sp, ["momentum"])["momentum"]
                 first = optimizer.first_tensor(sp.device)
         ctr, ab, an = advance if advance is not None else (None, 0.0, 0.0)
-        HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d i s",
+        HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d i p s",
                  ctypes.addressof(self._flags), ctypes.addressof(self._grads), self.region, self.ctrl, self.rank,
                  self.world, self.lo, self.hi, int(fused), sp.master.data_ptr() if fused else None,
                  mom.data_ptr() if mom is not None else None, sp.shadow.data_ptr() if fused else None,
                  lr.data_ptr() if lr is not None else None, float(wd), float(momentum), float(dampening), nesterov,
                  first.data_ptr() if first is not None else None, 1.0 / self.world,
                  ctr.data_ptr() if ctr is not None else None, float(ab), float(an), int(max_blocks),
-                 self.timeout_s, int(self.packed), self._stream())
+                 self.timeout_s, int(self.split), stamp, self._stream())
         if first is not None:
             from ..ops import kernels as K
             K.fill_(first, 0.0)
 
-    def all_gather_shadow(self, max_blocks: int = 256):
-        """Every rank's shadow := the owners' freshly updated chunks (closes the step's call)."""
-        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i s", ctypes.addressof(self._flags),
+    def all_gather_shadow(self, max_blocks: int = 256, stamp: Optional[int] = None):
+        """Every rank's shadow := the owners' freshly updated chunks (closes the step's call;
+        ``stamp``: its last block stamps the collective's end)."""
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
                  ctypes.addressof(self._shadows), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, int(self.packed), self._stream())
+                 self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, int(self.split), stamp, self._stream())
         self.space._master_stale = True
 
     def gather_master(self, max_blocks: int = 256):
         """Collective: complete the fp32 master from the owners' chunks (one barrier)."""
-        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i s", ctypes.addressof(self._flags),
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
                  ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, int(self.packed), self._stream())
+                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
         self.space._master_stale = False
 
     # ------------------------------------------------------------------ health
