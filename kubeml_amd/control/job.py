@@ -119,6 +119,7 @@ class TrainJob:
         self.log = JobLogger(store_dir, self.id)
         self.ckpt = ckpt_path(store_dir, self.id)
         self.have_ckpt = False
+        self.ckpt_epoch = None                # epoch of the last checkpoint confirmed on disk
         self.thread: Optional[threading.Thread] = None
         self.images_per_second = 0.0
         self.last_sync_seconds = 0.0
@@ -211,7 +212,7 @@ class TrainJob:
         if self.resume_from:
             self._resume()
         else:
-            self._checkpoint()
+            self._checkpoint(wait=True)   # the recovery base: confirmed on disk before epoch 1
         return layers
 
     def _resume(self):
@@ -241,10 +242,16 @@ class TrainJob:
         epoch's critical path); ``wait`` = the file is on disk when this returns."""
         rep = self.pool.call(0, {"op": "checkpoint", "job": self.id, "path": self.ckpt, "epoch": self.epoch,
                                  "extra": {"history": self.history.to_dict()}, "wait": bool(wait)})
-        if rep.get("ok"):
-            self.have_ckpt = True
-        else:
+        if rep.get("previous_error"):
+            self.log.warn("background checkpoint write failed", error=rep["previous_error"],
+                          durable_epoch=rep.get("durable_epoch"))
+        if not rep.get("ok"):
             self.log.warn("checkpoint failed", error=rep.get("error"))
+        # have_ckpt = some checkpoint is CONFIRMED on disk (a waited write, or an earlier
+        # background write that completed); a restore then reads the last good file
+        if rep.get("durable_epoch") is not None:
+            self.have_ckpt = True
+        self.ckpt_epoch = rep.get("durable_epoch")
 
     def _train_epoch(self) -> float:
         """One epoch with recovery: a lost worker → rebuild the pool on the survivors,

@@ -242,17 +242,26 @@ class Worker:
         if self.ckpt is None:
             self.ckpt = AsyncCheckpointer()
         try:
-            path = self.ckpt.save(km.network, msg["path"], job_id=msg["job"], epoch=int(msg.get("epoch", 0)),
+            prev = self.ckpt.save(km.network, msg["path"], job_id=msg["job"], epoch=int(msg.get("epoch", 0)),
                                   extra=msg.get("extra"))
             if msg.get("wait"):
                 self.ckpt.wait()
         except Exception as e:
-            return {"ok": False, "error": f"checkpoint failed: {e!r}", "code": 500}
-        return {"ok": True, "result": path}
+            return {"ok": False, "error": f"checkpoint failed: {e!r}", "code": 500,
+                    "durable_epoch": self.ckpt.durable_epoch}
+        rep = {"ok": True, "result": msg["path"], "durable_epoch": self.ckpt.durable_epoch}
+        if prev is not None:
+            rep["previous_error"] = repr(prev)
+        return rep
 
     def _flush_checkpoint(self):
+        """Wait for the background write.  A failed write is not fatal here: the file
+        on disk is still the last good checkpoint (writes rename into place)."""
         if self.ckpt is not None:
-            self.ckpt.wait()
+            e = self.ckpt.wait(raise_error=False)
+            if e is not None:
+                log.warning("checkpoint write failed (%r); the checkpoint of epoch %s stays current",
+                            e, self.ckpt.durable_epoch)
 
     def _release(self, job):
         self._flush_checkpoint()

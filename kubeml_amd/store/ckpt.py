@@ -76,6 +76,8 @@ class AsyncCheckpointer:
         self._pinned: Dict[str, torch.Tensor] = {}
         self.error: Optional[BaseException] = None
         self.writes = 0
+        self.durable_epoch: Optional[int] = None   # epoch of the last write confirmed on disk
+        self._writing_epoch: Optional[int] = None
 
     def _snapshot(self, module: torch.nn.Module) -> Dict[str, torch.Tensor]:
         sd = module.state_dict()
@@ -95,9 +97,13 @@ class AsyncCheckpointer:
         return out
 
     def save(self, module: torch.nn.Module, path: str, job_id: str = "", epoch: int = 0,
-             extra: Optional[dict] = None) -> str:
+             extra: Optional[dict] = None) -> Optional[BaseException]:
+        """Snapshot ``module`` now and write it in the background.  Returns the error of
+        the PREVIOUS background write, if it failed (this snapshot is still taken and
+        written: a failed epoch-``e`` write never costs the epoch-``e+1`` checkpoint, and
+        the file at ``path`` stays the last good one because writes rename into place)."""
         import threading
-        self.wait()
+        prev = self._join()
         sd = self._snapshot(module)
         meta = {"format": FORMAT, "jobId": job_id, "epoch": str(epoch), "keys": "{jobId}:{name}"}
         side = {"jobId": job_id, "epoch": epoch, "tensors": len(sd), **(extra or {})}
@@ -111,20 +117,29 @@ class AsyncCheckpointer:
                 os.replace(tmp, path)
                 write_json(path + ".json", side)
                 self.writes += 1
-            except BaseException as e:  # surfaced by the next wait()
+                self.durable_epoch = epoch
+            except BaseException as e:  # surfaced by the next save() / wait()
                 self.error = e
+        self._writing_epoch = epoch
         self._thread = threading.Thread(target=write, name="kubeml-ckpt", daemon=True)
         self._thread.start()
-        return path
+        return prev
 
-    def wait(self):
-        """Block until the last write is on disk; re-raise a failed write."""
+    def _join(self) -> Optional[BaseException]:
         t, self._thread = self._thread, None
         if t is not None:
             t.join()
-        if self.error is not None:
-            e, self.error = self.error, None
+        e, self.error = self.error, None
+        return e
+
+    def wait(self, raise_error: bool = True) -> Optional[BaseException]:
+        """Block until the last write is on disk; a failed write is re-raised (or, with
+        ``raise_error=False``, returned — the file on disk is then the previous good
+        checkpoint, ``durable_epoch`` says which)."""
+        e = self._join()
+        if e is not None and raise_error:
             raise e
+        return e
 
 
 def load_state(path: str) -> Dict[str, torch.Tensor]:

@@ -68,6 +68,37 @@ def test_checkpoint_roundtrip_and_reference_keys(tmp_path):
     assert "j1:conv1.weight/2" in reference_keys("j1", a, func_id=2)
 
 
+def test_async_checkpoint_failure_keeps_last_good_file(tmp_path, monkeypatch):
+    """A failed background write is reported by the next save() (which still takes and
+    writes its own snapshot), and the file on disk stays the last confirmed epoch."""
+    import safetensors.torch as st
+    from kubeml_amd.store.ckpt import AsyncCheckpointer, load_state, metadata
+    m = torch.nn.Linear(4, 3)
+    path = str(tmp_path / "j.safetensors")
+    ck = AsyncCheckpointer()
+    assert ck.save(m, path, job_id="j", epoch=0) is None
+    ck.wait()
+    assert ck.durable_epoch == 0 and metadata(path)["epoch"] == "0"
+    real = st.save_file
+
+    def boom(*a, **k):
+        raise OSError("disk full")
+    monkeypatch.setattr(st, "save_file", boom)
+    with torch.no_grad():
+        m.weight.add_(1.0)
+    assert ck.save(m, path, job_id="j", epoch=1) is None
+    assert isinstance(ck.wait(raise_error=False), OSError)
+    assert ck.durable_epoch == 0 and metadata(path)["epoch"] == "0"   # old file intact
+    monkeypatch.setattr(st, "save_file", boom)
+    ck.save(m, path, job_id="j", epoch=2)                              # fails in background
+    monkeypatch.setattr(st, "save_file", real)
+    prev = ck.save(m, path, job_id="j", epoch=3)                       # reports it, still writes
+    assert isinstance(prev, OSError)
+    ck.wait()
+    assert ck.durable_epoch == 3 and metadata(path)["epoch"] == "3"
+    assert torch.equal(load_state(path)["weight"], m.weight.detach())
+
+
 def test_history_and_function_stores(tmp_path):
     from kubeml_amd.api.errors import KubeMLException
     from kubeml_amd.api.types import History, JobHistory, TrainRequest

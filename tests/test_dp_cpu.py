@@ -192,3 +192,71 @@ def test_comm_plan_parse_and_choice(tmp_path, monkeypatch):
     assert choose_plan(8, 1 << 20, table=table).tag() == "rccl:overlap:fp32"
     assert choose_plan(8, 1 << 20, override="peer:end:bf16:128", table=table).tag() == "peer:end:bf16:128"
     assert CommPlan().tag() == "peer:end:fp32:256"
+
+
+def test_shipped_plan_table_is_exact_fp32():
+    """The shipped table never picks a lossy wire by default (bf16 is opt-in)."""
+    from kubeml_amd.parallel.plan import choose_plan
+    for n in (2, 4, 8):
+        assert choose_plan(n, 1 << 24).wire == "fp32"
+
+
+class _FakePeer:
+    def __init__(self, poisoned=False, fits=True):
+        self.poisoned, self.fits, self.released, self.closed = poisoned, fits, False, False
+        self.region = object()
+
+    def check(self):
+        if self.poisoned:
+            from kubeml_amd.parallel.peer import PeerCommError
+            raise PeerCommError("barrier timeout")
+
+    def supports(self, *a):
+        return self.fits
+
+    def _release(self):
+        self.released = True
+
+    def close(self):
+        self.closed = True
+
+
+def _bare_comm():
+    from kubeml_amd.parallel.comm import TorchComm
+    c = TorchComm.__new__(TorchComm)
+    c.rank, c.world, c._subs, c.peer_data = 0, 2, {}, True
+    c.peer = c.grad_peer = None
+    return c
+
+
+def test_poisoned_peer_is_dropped_and_the_next_job_recovers():
+    """A barrier timeout poisons a transport for good; ``check()`` raises once, drops it
+    (unmapped without a group barrier), and the following job's check passes — the next
+    collective then builds a fresh transport instead of reusing the NaN one."""
+    from kubeml_amd.parallel.peer import PeerCommError
+    c = _bare_comm()
+    sub = _bare_comm()
+    c._subs[2] = sub
+    bad, good = _FakePeer(poisoned=True), _FakePeer()
+    c.peer, sub.grad_peer = good, bad
+    with pytest.raises(PeerCommError):
+        c.check()
+    assert sub.grad_peer is None and bad.released and c.peer is good and not good.released
+    c.check()                                     # next job: clean
+
+
+def test_grad_peer_reused_only_if_it_fits():
+    """A cached gradient transport is reused only when its slots fit this model's gradient
+    at this wire; otherwise it is closed and a new one is built."""
+    from kubeml_amd.parallel.plan import parse_plan
+    from kubeml_amd.sdk.model import KubeModel
+    km = KubeModel.__new__(KubeModel)
+    km._flat = type("S", (), {"grad": torch.zeros(8)})()
+    km._shards = {}
+    c = _bare_comm()
+    plan = parse_plan("peer:end:fp32:256")
+    c.grad_peer = fit = _FakePeer(fits=True)
+    assert km._reusable_peer(c, plan) is fit and c.grad_peer is fit
+    c.grad_peer = small = _FakePeer(fits=False)
+    assert km._reusable_peer(c, plan) is None and small.closed and c.grad_peer is None
+    assert km._reusable_peer(c, parse_plan("rccl:end:fp32")) is None
