@@ -11,8 +11,8 @@
 //           key tile; both recompute P from the saved LSE — no atomics, deterministic.
 //
 // Attention-probability dropout (HF BERT attention_probs_dropout_prob): keep mask
-// Z[b,h,q,key] = half16(hash(seed ^ salt, step, b, h, q, key / 2), key & 1) >= p * 2^16,
-// hashed once by the forward (one hash per key pair), which stores the decisions as a bit mask
+// Z[b,h,q,key] = half16(word(seed ^ salt, step, b, h, q, key / 2), key & 1) >= p * 2^16
+// (word: Drop below), hashed once by the forward, which stores the decisions as a bit mask
 // (1 bit per probability, AttnArgs::keep) that both backward kernels read.  Forward: O = softmax(S) (.) Z/(1-p) @ V, the row normaliser from
 // the undropped probabilities; backward: dV = (P (.) Z/(1-p))^T dO, dP = (dO V^T) (.) Z/(1-p),
 // dS = P (.) (dP - D) with D = rowsum(dO (.) O) (unchanged by the mask).
@@ -61,15 +61,23 @@ __device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
   return h;
 }
 
-// per-kernel dropout state.  One 32-bit hash per (q, key pair): its low 16 bits decide the
-// even key, the high 16 bits the odd one (threshold p * 2^16) — half the hashing of one hash
-// per element, and the inner loops always visit keys in aligned pairs.
+// per-kernel dropout state.  One 32-bit word per (q, key pair): its low 16 bits decide the
+// even key, the high 16 bits the odd one (threshold p * 2^16).  The words of the 16 keys a
+// forward lane holds (query q, keys kbase + 16t + i, kbase = kb*64 + 4g) come from ONE full
+// hash of (q, kbase) followed by a one-multiply finaliser per pair: word(off) =
+// fmix1(ahash(q*LP + kbase/2) + off * golden), off = 8t + i/2 — 11 multiplies per lane per
+// key tile instead of 24 (the hash was a quarter of the forward's vector-ALU work).
 //
 // The forward also stores the decisions as a bit mask (AttnArgs::keep), so the backward
 // kernels read 1 bit per probability instead of re-hashing (the hash is most of their
 // vector-ALU work): u64 word (bh, key tile kb, query q) at byte ((bh*nkb + kb)*Lp + q)*8,
 // Lp = 64*nkb; bit 16g + 4t + i = key kb*64 + 16t + 4g + i — the 16 keys a forward lane
 // holds (lane group g, S-tile t, element i) are one u16 at byte 2g.
+__device__ __forceinline__ unsigned fmix1(unsigned x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15;
+  return x;
+}
+
 struct Drop {
   unsigned k0, k1, thr;
   float sc;
@@ -88,12 +96,13 @@ struct Drop {
   }
   // keep bits of keys kbase + 16t + i (bit 4t + i), kbase = kb*64 + 4g
   __device__ __forceinline__ unsigned bits16(int q, int kbase) const {
+    const unsigned h0 = ahash(k0, k1, (unsigned)q * LP + ((unsigned)kbase >> 1));
     unsigned bits = 0;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 4; i += 2) {
-        const unsigned h = ahash(k0, k1, (unsigned)q * LP + ((unsigned)(kbase + 16 * t + i) >> 1));
+        const unsigned h = fmix1(h0 + (unsigned)(8 * t + i / 2) * 0x9E3779B9u);
         bits |= ((h & 0xFFFFu) >= thr ? 1u : 0u) << (4 * t + i);
         bits |= (h >= (thr << 16) ? 1u : 0u) << (4 * t + i + 1);
       }
@@ -101,7 +110,9 @@ struct Drop {
   }
   // all-ones / zero mask of one (q, key)
   __device__ __forceinline__ int keep1(int q, int key) const {
-    const unsigned h = ahash(k0, k1, (unsigned)q * LP + ((unsigned)key >> 1));
+    const int kbase = (key & ~63) + 4 * ((key & 15) >> 2);
+    const unsigned h0 = ahash(k0, k1, (unsigned)q * LP + ((unsigned)kbase >> 1));
+    const unsigned h = fmix1(h0 + (unsigned)((key >> 1) - (kbase >> 1)) * 0x9E3779B9u);
     return ((key & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr ? -1 : 0;
   }
 };
@@ -454,8 +465,11 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
   // double-buffered like k_attn_fwd: Q, dO, LSE, D and the keep bits of a query tile
   __shared__ __attribute__((aligned(16))) char sQ2[2][8192];
   __shared__ __attribute__((aligned(16))) char sO2[2][8192];  // dO tile
-  __shared__ float sL2[2][64], sD2[2][64];
-  __shared__ __attribute__((aligned(16))) unsigned sM2[2][128];   // keep bits: 64 u64 words
+  __shared__ __attribute__((aligned(16))) float sL2[2][64];
+  __shared__ __attribute__((aligned(16))) float sD2[2][64];
+  // keep bits: the tile's 64 u64 words as two planes of 32-bit halves, sM2[j][half][q], so a
+  // lane's four queries 16t + 4g + i are one ds_read_b128 (like LSE and D)
+  __shared__ __attribute__((aligned(16))) unsigned sM2[2][2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   int xt, bh;
   attn_blk(a, xt, bh);
@@ -501,7 +515,10 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
     tile_store(sQ2[j], rq, tid);
     tile_store(sO2[j], ro, tid);
     if (tid < 64) { sL2[j][tid] = pl; sD2[j][tid] = pd; }
-    if (kbits && tid < 32) reinterpret_cast<uint4*>(sM2[j])[tid] = mnext;
+    if (kbits && tid < 32) {   // words 2tid, 2tid+1 = (mnext.x, .y), (mnext.z, .w)
+      *reinterpret_cast<uint2*>(&sM2[j][0][2 * tid]) = make_uint2(mnext.x, mnext.z);
+      *reinterpret_cast<uint2*>(&sM2[j][1][2 * tid]) = make_uint2(mnext.y, mnext.w);
+    }
   };
   fetch(0);
   stage(0);
@@ -512,7 +529,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
     const char* sO = sO2[qb & 1];
     const float* sL = sL2[qb & 1];
     const float* sD = sD2[qb & 1];
-    const unsigned* sM = sM2[qb & 1];
+    const unsigned* sM = sM2[qb & 1][kbit >> 5];
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -525,18 +542,24 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
     }
     // s[t][i] = S[q = 16t + 4g + i][key]
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const float4 l4 = *reinterpret_cast<const float4*>(sL + 16 * t + 4 * g);
+      const float4 d4 = *reinterpret_cast<const float4*>(sD + 16 * t + 4 * g);
+      const uint4 m4 = kbits ? *reinterpret_cast<const uint4*>(sM + 16 * t + 4 * g) : make_uint4(0, 0, 0, 0);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+      const unsigned mv[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * t + 4 * g + i;
-        const float p = fexp2(fmaf(s[t][i], sl2, kb2 - sL[r]));
+        const float p = fexp2(fmaf(s[t][i], sl2, kb2 - lv[i]));
         int m = -1;
-        if (kbits) m = bitmask(sM[2 * r + (kbit >> 5)], kbit & 31);
+        if (kbits) m = bitmask(mv[i], kbit & 31);
         else if (drop.on) m = drop.keep1(qb * 64 + r, key);
         // dV takes P (.) Z (1/(1-p) applied at the store), dS = P (.) (dP (.) Z/(1-p) - D)
         s[t][i] = fmask(p, m);
-        dp[t][i] = p * fmaf(fmask(dp[t][i], m), drop.sc, -sD[r]);
+        dp[t][i] = p * fmaf(fmask(dp[t][i], m), drop.sc, -dv[i]);
       }
+    }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
     const bf16x8_t d0 = pack_p(dp[0], dp[1]), d1 = pack_p(dp[2], dp[3]);
 #pragma unroll

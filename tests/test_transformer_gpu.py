@@ -137,7 +137,10 @@ def _attn_keep(seed, step, salt, B, H, L, p):
     keep = np.zeros((B, H, L, L), dtype=np.float32)
     q = np.arange(L, dtype=np.uint64).reshape(L, 1)
     key = np.arange(L, dtype=np.uint64).reshape(1, L)
-    c = (q * np.uint64((L + 1) // 2) + (key >> np.uint64(1))) & M   # one hash per key pair
+    # one full hash per (q, kbase = 64*kb + 4*g), then a one-multiply finaliser per key pair
+    kbase = (key & ~np.uint64(63)) + np.uint64(4) * ((key & np.uint64(15)) >> np.uint64(2))
+    c = (q * np.uint64((L + 1) // 2) + (kbase >> np.uint64(1))) & M
+    off = (key >> np.uint64(1)) - (kbase >> np.uint64(1))
     for b in range(B):
         for h in range(H):
             bh = np.uint64(b * H + h)
@@ -148,6 +151,10 @@ def _attn_keep(seed, step, salt, B, H, L, p):
             hh = mul(hh, 0x2C1B3C6D)
             hh ^= hh >> np.uint64(12)
             hh = mul(hh, 0x297A2D39)
+            hh ^= hh >> np.uint64(15)
+            hh = (hh + mul(off, 0x9E3779B9)) & M
+            hh ^= hh >> np.uint64(16)
+            hh = mul(hh, 0x7FEB352D)
             hh ^= hh >> np.uint64(15)
             half = np.where((key & np.uint64(1)) == 1, hh >> np.uint64(16), hh & np.uint64(0xFFFF))
             keep[b, h] = np.where(half >= thr, 1.0 / (1.0 - p), 0.0)
