@@ -442,7 +442,115 @@ __device__ __forceinline__ int row_off(const ConvArgs& a, int col) {
 }
 __device__ __forceinline__ int sq_off(const ConvArgs& a) { return a.fold_c ? a.fold_c : a.N; }
 
-template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false, bool STAGE_ALL = false>
+// DGRAD epilogue through LDS rows, for tiles whose output merges an addend and/or feeds the
+// consumer BN's partial sums.  The per-element path gathers addend / y / c with 2-byte
+// loads (one wave instruction = 4 rows x 32 B, address-unit bound): on ResNet-50's 56x56
+// 1x1 dgrads that epilogue took ~5x the GEMM.  Here the fp32 tile is staged in LDS (column
+// chunk XOR-swizzled by (row >> 2) & 3 so a fragment store's 4 rows x 16 columns hit 64
+// distinct banks), then each thread owns one 8-channel chunk column and walks the tile's
+// rows with 16-byte loads and stores: v = acc + addend, bf16 round, the consumer BN's
+// masked dz and dz * xhat sums.  Partial rows: a shuffle butterfly over the lanes of a
+// chunk column, then a fixed-order sum of the 4 waves — deterministic, one row per M-tile
+// as in the per-element path.
+template <int BMT, int BNT, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                              int wn, int lane, int tid, unsigned* flag) {
+  constexpr int CPR = BNT / 8, RSTEP = 256 / CPR;
+  static_assert(BNT % 64 == 0 && 64 % CPR == 0, "row pass: 64-column multiples");
+  float* sF = reinterpret_cast<float*>(reinterpret_cast<char*>(flag) + 16);
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = wm * WM + i * 16 + fq * 4 + e, c = wn * WN + j * 16 + fr;
+        sF[r * BNT + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
+      }
+  __syncthreads();
+  const int cc = tid % CPR, r0 = tid / CPR;
+  const int col0 = n0 + cc * 8;
+  const bool cok = col0 < a.N;
+  const bool bnf = a.bnf_part != nullptr;
+  float mean[8], rstd[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { mean[k] = 0.f; rstd[k] = 0.f; s1[k] = 0.f; s2[k] = 0.f; }
+  if (bnf && cok) {
+    const int bc0 = a.fold_c ? col0 % a.fold_c : col0;  // 8 channels never straddle a fold group
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { mean[k] = a.bnf_mean[bc0 + k]; rstd[k] = a.bnf_rstd[bc0 + k]; }
+  }
+  for (int r = r0; r < BMT; r += RSTEP) {
+    const int row = m0 + r;
+    if (row >= a.M || !cok) continue;
+    const float* src = sF + r * BNT + ((cc * 8) ^ (((r >> 2) & 3) << 4));
+    const float4 p0 = *reinterpret_cast<const float4*>(src), p1 = *reinterpret_cast<const float4*>(src + 4);
+    float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    const long long idx = (long long)row * a.N + col0;
+    if (a.addend) {
+      const uint4 ad = ld16(a.addend + idx);
+      const unsigned aw[4] = {ad.x, ad.y, ad.z, ad.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[2 * k] += lo_bf(aw[k]); v[2 * k + 1] += hi_bf(aw[k]); }
+    }
+    unsigned ow[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ow[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+    if (bnf) {
+      const uint4 cv = ld16(a.bnf_c + idx);
+      const uint4 yv = a.bnf_y ? ld16(a.bnf_y + idx) : make_uint4(0, 0, 0, 0);
+      const unsigned cw[4] = {cv.x, cv.y, cv.z, cv.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float dz0 = lo_bf(ow[k]), dz1 = hi_bf(ow[k]);
+        if (a.bnf_y) {
+          const bool k0 = lo_bf(yw[k]) > 0.f, k1 = hi_bf(yw[k]) > 0.f;
+          if (!k0) dz0 = 0.f;
+          if (!k1) dz1 = 0.f;
+          if (a.bnf_mask_out) ow[k] &= (k0 ? 0x0000ffffu : 0u) | (k1 ? 0xffff0000u : 0u);
+        }
+        const float x0 = (lo_bf(cw[k]) - mean[2 * k]) * rstd[2 * k];
+        const float x1 = (hi_bf(cw[k]) - mean[2 * k + 1]) * rstd[2 * k + 1];
+        s1[2 * k] += dz0; s2[2 * k] += dz0 * x0;
+        s1[2 * k + 1] += dz1; s2[2 * k + 1] += dz1 * x1;
+      }
+    }
+    *reinterpret_cast<uint4*>(a.out + idx) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+  if (!bnf) return;
+#pragma unroll
+  for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += __shfl_xor(s1[k], off, 64);
+      s2[k] += __shfl_xor(s2[k], off, 64);
+    }
+  __syncthreads();  // staging reads done: the tile area is reused as [4 waves][CPR][16]
+  const int wave = tid >> 6;
+  if (lane < CPR) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sF[(wave * CPR + lane) * 16 + k] = s1[k];
+      sF[(wave * CPR + lane) * 16 + 8 + k] = s2[k];
+    }
+  }
+  __syncthreads();
+  float* rows = a.bnf_part;
+  const bool sc1_rows = a.grp_out != nullptr;
+  const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
+  for (int q = tid; q < 2 * BNT; q += 256) {
+    const int half = q / BNT, cl = q - half * BNT, col = n0 + cl;
+    if (col >= a.N) continue;
+    const int c8 = cl >> 3, k = (cl & 7) + 8 * half;
+    const float sum = ((sF[(0 * CPR + c8) * 16 + k] + sF[(1 * CPR + c8) * 16 + k]) +
+                       sF[(2 * CPR + c8) * 16 + k]) + sF[(3 * CPR + c8) * 16 + k];
+    store_row(rows + rrow + row_off(a, col) + (half ? sq_off(a) : 0), sum, sc1_rows);
+  }
+  if (a.grp_out) group_reduce_rows<BMT, BNT, 1, false>(a, rows, m0, n0, tid, flag);
+}
+
+template <int MODE, int MR, int NR, int WM, int WN, bool SINGLE = false, bool STAGE_ALL = false, int LDSB = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
                                               int wn, int lane, int tid, int tile, int bz, unsigned* flag) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -562,6 +670,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     // (entered after a block barrier: the main loops end with one, so LDS is free here)
     // tile geometry: 2x2 waves (SINGLE: one live wave owns the whole tile)
     constexpr int BMT = SINGLE ? WM : 2 * WM, BNT = SINGLE ? WN : 2 * WN;
+    constexpr bool ROWPASS = MODE == DGRAD && !SINGLE && BNT % 64 == 0 && BMT * BNT >= 4096 &&
+                             LDSB >= 16 + BMT * BNT * 4;
+    if constexpr (ROWPASS) {
+      if (a.addend || a.bnf_part) {
+        dgrad_rowpass<BMT, BNT, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, flag);
+        return;
+      }
+    }
     // Large tiles stage the bf16 output through LDS (past the 16-byte split-K flag word) and
     // write it back as 16-byte row chunks instead of one 2-byte store per element.
     constexpr bool STAGE_OK = !SINGLE && (STAGE_ALL || BMT * BNT >= 8192);
@@ -794,8 +910,9 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const Con
     }
   }
 
-  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * bk.gx + tile_n, bk.z,
-                                      reinterpret_cast<unsigned*>(smem));
+  conv_epilogue<MODE, MR, NR, WM, WN, false, false, SMEM>(a, acc, m0, n0, wm, wn, lane, tid,
+                                                          tile_m * bk.gx + tile_n, bk.z,
+                                                          reinterpret_cast<unsigned*>(smem));
 }
 
 template <int MODE, int BM, int BN, int BK, bool TAPU>
@@ -972,8 +1089,9 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  conv_epilogue<MODE, MR, NR, WM, WN>(a, acc, m0, n0, wm, wn, lane, tid, tile_m * bk.gx + tile_n, bk.z,
-                                      reinterpret_cast<unsigned*>(smem));
+  conv_epilogue<MODE, MR, NR, WM, WN, false, false, SMEM>(a, acc, m0, n0, wm, wn, lane, tid,
+                                                          tile_m * bk.gx + tile_n, bk.z,
+                                                          reinterpret_cast<unsigned*>(smem));
 }
 
 // XCD-aware tile order (CDNA guide T1): blocks b and b+8 share an XCD (round-robin

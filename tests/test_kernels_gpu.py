@@ -481,16 +481,21 @@ def test_bn_stats_partial_rows(M, C):
     assert _rel(s[:C], xf.sum(0)) < 1e-4 and _rel(s[C:], (xf * xf).sum(0)) < 1e-4
 
 
-@pytest.mark.parametrize("cfg", [(32, 32, 64, 1, 0), (64, 32, 64, 2, 1), (32, 32, 4, 1, 3), (64, 64, 32, 4, 0)])
-def test_dgrad_emits_consumer_bn_partials(cfg):
+@pytest.mark.parametrize("cfg,Ci,with_add", [
+    ((32, 32, 64, 1, 0), 64, True), ((64, 32, 64, 2, 1), 64, True), ((32, 32, 4, 1, 3), 64, True),
+    ((64, 64, 32, 4, 0), 64, True),
+    # 64-column tiles run the LDS row-pass epilogue (16-byte addend / y / c rows)
+    ((64, 64, 32, 1, 0), 192, True), ((64, 64, 32, 1, 0), 192, False), ((64, 64, 64, 1, 0), 64, False),
+    ((64, 128, 64, 1, 1), 192, True), ((64, 128, 64, 1, 1), 64, False)])
+def test_dgrad_emits_consumer_bn_partials(cfg, Ci, with_add):
     """conv_dgrad(bnf=...) writes the dgamma/dbeta partial rows of the BN that consumes dX;
     bn_bwd(partial=...) then equals the unfused bn_bwd."""
     from kubeml_amd.ops import kernels as K
     torch.manual_seed(7)
-    B, H, W, Ci, Co = 6, 5, 5, 64, 96
+    B, H, W, Co = 6, 5, 5, 96
     dy = _bf(torch.randn(B, H, W, Co, device=dev))
     w = _bf(torch.randn(Co, 3, 3, Ci, device=dev) * 0.05)
-    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    add = _bf(torch.randn(B, H, W, Ci, device=dev)) if with_add else None
     c = _bf(torch.randn(B, H, W, Ci, device=dev))            # the consumer BN's input
     ybn = _bf(torch.randn(B, H, W, Ci, device=dev))          # its ReLU output (sign pattern)
     mean, rstd = torch.randn(Ci, device=dev), torch.rand(Ci, device=dev) + 0.5
@@ -505,6 +510,10 @@ def test_dgrad_emits_consumer_bn_partials(cfg):
     r1 = K.bn_bwd(dx1, ybn, c, mean, rstd, g, dg1, db1, partial=partial)
     assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
     assert _rel(r1, r0) < 1e-2
+    xr = torch.zeros(B, Ci, H, W, device=dev, requires_grad=True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1) + (add.float() if add is not None else 0.0)
+    assert _rel(dx1, ref) < 1e-2
     # bnf_mask: the dgrad writes dz = dX * [y > 0] itself; the BN backward then runs without
     # y (no mask, y never read) and gives the same dx / dres / dgamma / dbeta
     dz, partial2 = K.conv_dgrad(dy, w, (B, H, W, Ci), 3, 3, (1, 1), (1, 1), addend=add, cfg=cfg,
