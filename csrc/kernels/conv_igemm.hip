@@ -132,6 +132,13 @@ struct ConvArgs {
   float ibn_eps, ibn_mom;
   bf16_t* ibn_y;
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
+  // Stride-2 DGRAD by parity class (kml_conv_dgrad_s2): this launch computes the input pixels
+  // (ih, iw) = (2i + pa, 2j + pe) only — GEMM row m = (b, i, j) over an Hc x Wc grid — with
+  // only the taps of matching parity (r = r0 + tstep * tr, tstep = 2), so none of the 3/4 of
+  // (pixel, tap) pairs a stride-2 dgrad gathers from the zero page is computed.  rowbase: the
+  // class's first row in the consumer-BN partial-row buffer.
+  int par, pa, pe, tstep, rowbase;
+  FastDiv fd_Wc, fd_Hc;
 };
 
 // Block coordinates of one conv tile: kernels pass blockIdx; the grouped backward kernel
@@ -163,8 +170,8 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cas
 
 __device__ __forceinline__ void tap_rs(const ConvArgs& a, int tap, int& r, int& s) {
   const int tr = fdiv(tap, a.fd_nts);
-  r = a.r0 + tr;
-  s = a.s0 + (tap - tr * a.fd_nts.d);
+  r = a.r0 + tr * a.tstep;
+  s = a.s0 + (tap - tr * a.fd_nts.d) * a.tstep;
 }
 
 // ---------------------------------------------------------------------------------
@@ -246,10 +253,17 @@ struct DgradA {  // dY gathered for input pixel m; K = (tap, cout); Kp % BK == 0
   __device__ void init(const ConvArgs& a, int m, int q) {
     valid = m < a.M;
     const int mm = valid ? m : 0;
-    const int t = fdiv(mm, a.fd_W);
-    iw = mm - t * a.W;
-    b = fdiv(t, a.fd_H);
-    ih = t - b * a.H;
+    if (a.par) {  // parity class: row = (b, i, j) -> pixel (2i + pa, 2j + pe)
+      const int t = fdiv(mm, a.fd_Wc);
+      iw = 2 * (mm - t * a.fd_Wc.d) + a.pe;
+      b = fdiv(t, a.fd_Hc);
+      ih = 2 * (t - b * a.fd_Hc.d) + a.pa;
+    } else {
+      const int t = fdiv(mm, a.fd_W);
+      iw = mm - t * a.W;
+      b = fdiv(t, a.fd_H);
+      ih = t - b * a.H;
+    }
     koff = (q % (BK / 8)) * 8;
   }
   __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
@@ -442,6 +456,14 @@ __device__ __forceinline__ int row_off(const ConvArgs& a, int col) {
 }
 __device__ __forceinline__ int sq_off(const ConvArgs& a) { return a.fold_c ? a.fold_c : a.N; }
 
+// Output pixel row of GEMM row `row` (identity except in a stride-2 parity-class DGRAD).
+__device__ __forceinline__ long long prow(const ConvArgs& a, int row) {
+  if (!a.par) return row;
+  const int t = fdiv(row, a.fd_Wc), j = row - t * a.fd_Wc.d;
+  const int b = fdiv(t, a.fd_Hc), i = t - b * a.fd_Hc.d;
+  return ((long long)b * a.H + 2 * i + a.pa) * a.W + 2 * j + a.pe;
+}
+
 // DGRAD epilogue through LDS rows, for tiles whose output merges an addend and/or feeds the
 // consumer BN's partial sums.  The per-element path gathers addend / y / c with 2-byte
 // loads (one wave instruction = 4 rows x 32 B, address-unit bound): on ResNet-50's 56x56
@@ -487,7 +509,7 @@ __device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[
     const float* src = sF + r * BNT + ((cc * 8) ^ (((r >> 2) & 3) << 4));
     const float4 p0 = *reinterpret_cast<const float4*>(src), p1 = *reinterpret_cast<const float4*>(src + 4);
     float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-    const long long idx = (long long)row * a.N + col0;
+    const long long idx = prow(a, row) * a.N + col0;
     if (a.addend) {
       const uint4 ad = ld16(a.addend + idx);
       const unsigned aw[4] = {ad.x, ad.y, ad.z, ad.w};
@@ -538,7 +560,7 @@ __device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[
   __syncthreads();
   float* rows = a.bnf_part;
   const bool sc1_rows = a.grp_out != nullptr;
-  const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
+  const long long rrow = (long long)(a.rowbase + m0 / BMT) * 2 * a.N;
   for (int q = tid; q < 2 * BNT; q += 256) {
     const int half = q / BNT, cl = q - half * BNT, col = n0 + cl;
     if (col >= a.N) continue;
@@ -691,7 +713,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     // the BN kernel (every block of which reads all rows) reads half as many.
     float* rows = (MODE == DGRAD) ? a.bnf_part : ((a.stats && a.stats_part) ? a.stats : nullptr);
     const bool sc1_rows = a.grp_out != nullptr;
-    const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
+    const long long rrow = (long long)(a.rowbase + m0 / BMT) * 2 * a.N;
     const int ldc = a.N;
     float k1[NR], k2[NR];
 #pragma unroll
@@ -710,10 +732,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
           if (row < a.M && cok) {
             float v = acc[i][j][e] + bv;
             if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
-            if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
+            const long long orow = MODE == DGRAD ? prow(a, row) : (long long)row;
+            if (MODE == DGRAD && a.addend) v += bf2f(a.addend[orow * ldc + col]);
             bf16_t vb = f2bf(v);
             if (MODE == DGRAD && a.bnf_part) {  // consumer BN's dbeta / dgamma partials
-              const long long idx = (long long)row * ldc + col;
+              const long long idx = orow * ldc + col;
               float dz = bf2f(vb);
               if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) {
                 dz = 0.f;
@@ -727,7 +750,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
               s2 += v * v;
             }
             if (stage) sout[(row - m0) * LDO + (col - n0)] = vb;
-            else a.out[(long long)row * ldc + col] = vb;
+            else a.out[orow * ldc + col] = vb;
           }
         }
       if ((MODE == DGRAD && a.bnf_part) || (MODE == FWD && a.stats)) {
@@ -769,7 +792,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
           const int r = q / CPR, c8 = (q - r * CPR) * 8;
           const int row = m0 + r, col = n0 + c8;
           if (row < a.M && col < a.N)
-            *reinterpret_cast<uint4*>(a.out + (long long)row * ldc + col) =
+            *reinterpret_cast<uint4*>(a.out + (MODE == DGRAD ? prow(a, row) : (long long)row) * ldc + col) =
                 *reinterpret_cast<const uint4*>(sout + r * LDO + c8);
         }
       }
@@ -2015,6 +2038,122 @@ __global__ __launch_bounds__(256) void k_conv_stem(ConvArgs a) {
   conv_epilogue<FWD, MR, NR, P::WM, P::WN>(a, acc, m0, 0, wm, wn, lane, tid, 0, 0, reinterpret_cast<unsigned*>(smem));
 }
 
+// Variant 6 on ImageNet-size images: the same patch-in-LDS im2col, tiled by PAIRS OF OUTPUT
+// ROWS (GEMM rows m0 = tile * 2 * OW.., contiguous, so the FWD epilogue and its BN partial
+// rows are unchanged).  A tile reads a 9 x (2 * OW + 6) input patch (the 7 tap rows of two
+// stride-2 output rows); every A fragment is one 16-byte LDS read at (patch pixel, tap) —
+// no im2col staging — and the 64 x 392 weight matrix stays in LDS for the whole launch:
+// persistent blocks (one per CU) walk tiles b, b + grid, ..., the next tile's patch loaded
+// into registers while this tile's MFMAs run.  (The general implicit GEMM gathers 392 K per
+// row through 16-byte chunks that are 5/8 zero channels and re-stages the weights per tile.)
+template <int OW>
+struct StemRowsBody {
+  static constexpr int WIN = 2 * OW, PW = WIN + 6, PH = 9, BM = 2 * OW, BN = 64;
+  static constexpr int KP = 416, KSTEPS = KP / 32, WCH = 56;
+  static constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
+  static constexpr int PCH = PH * PW;
+  static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
+  static constexpr int SMEM_PATCH0 = PCH * 16;
+  static constexpr int SMEM_PATCH = ((SMEM_PATCH0 > SMEM_EPI ? SMEM_PATCH0 : SMEM_EPI) + 1023) / 1024 * 1024;
+  static constexpr int SMEM_W = BN * WCH * 16;
+  static constexpr int SMEM = SMEM_PATCH + SMEM_W;
+  static_assert(WM % 16 == 0, "two output rows must split into 16-row wave fragments");
+  static_assert(SMEM <= 160 * 1024, "stem row-pair patch exceeds LDS");
+};
+
+template <int OW>
+__global__ __launch_bounds__(256) void k_conv_stem_rows(ConvArgs a) {
+  using P = StemRowsBody<OW>;
+  constexpr int PW = P::PW, MR = P::MR, NR = P::NR, PER = (P::PCH + 255) / 256;
+  __shared__ __attribute__((aligned(1024))) char smem[P::SMEM];
+  char* const swt = smem + P::SMEM_PATCH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int tiles_per_img = a.OH / 2, T = a.B * tiles_per_img;
+  {  // weights [64][392] -> LDS rows of 56 chunks (49..55 zero), chunk ^ (n & 7)
+    constexpr int WCHUNKS = P::BN * P::WCH;
+    for (int q = tid; q < WCHUNKS; q += 256) {
+      const int n = q / P::WCH, c = q - n * P::WCH;
+      *reinterpret_cast<uint4*>(swt + (n * P::WCH + (c ^ (n & 7))) * 16) =
+          ld16(c < 49 ? a.w + (long long)n * 392 + c * 8 : a.zp);
+    }
+  }
+  uint4 v[PER];
+  auto load_patch = [&](int tile) {
+    const int img = tile / tiles_per_img, ih0 = 2 * 2 * (tile - img * tiles_per_img) - 3;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int q = tid + u * 256;
+      const int pr = q / PW, ih = ih0 + pr, iw = q - pr * PW - 3;
+      const bool in = q < P::PCH && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      v[u] = ld16(in ? a.x + (((long long)img * a.H + ih) * a.W + iw) * 8 : a.zp);
+    }
+  };
+  auto store_patch = [&]() {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int q = tid + u * 256;
+      if (q < P::PCH) *reinterpret_cast<uint4*>(smem + q * 16) = v[u];
+    }
+  };
+  int tile = (int)blockIdx.x;
+  if (tile >= T) return;
+  load_patch(tile);
+  store_patch();
+  int pbase[MR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int r = wm * P::WM + i * 16 + (lane & 15);
+    pbase[i] = (2 * (r / OW)) * PW + 2 * (r % OW);
+  }
+  int brow[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) brow[j] = wn * P::WN + j * 16 + (lane & 15);
+  auto rd = [&](int ks, bf16x8_t (&af)[MR], bf16x8_t (&bf)[NR]) {
+    const int tap = min(4 * ks + (lane >> 4), 48);  // taps 49..51 meet zero weights
+    const int toff = (tap / 7) * PW + (tap % 7);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(smem + (pbase[i] + toff) * 16);
+    const int wc = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8_t*>(swt + (brow[j] * P::WCH + (wc ^ (brow[j] & 7))) * 16);
+  };
+  __syncthreads();
+  for (;;) {
+    const int next = tile + (int)gridDim.x;
+    if (next < T) load_patch(next);  // in flight during this tile's MFMAs
+    f32x4_t acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t af[2][MR], bf[2][NR];
+    rd(0, af[0], bf[0]);
+#pragma unroll
+    for (int ks = 0; ks < P::KSTEPS; ++ks) {
+      if (ks + 1 < P::KSTEPS) rd(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bf[ks & 1][j], acc[i][j], 0, 0, 0);
+    }
+    // raw barriers (LDS ordering only): __syncthreads would also drain the vector-memory
+    // counter, i.e. wait for this tile's output stores before the next tile may start
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // patch reads done: the epilogue stages its output over the patch
+    conv_epilogue<FWD, MR, NR, P::WM, P::WN>(a, acc, tile * P::BM, 0, wm, wn, lane, tid, 0, 0,
+                                             reinterpret_cast<unsigned*>(smem));
+    if (next >= T) break;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // epilogue LDS reads done
+    store_patch();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    tile = next;
+  }
+}
+
 template <int MODE>
 int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
 #define KML_T(BMv, BNv)                                                  \
@@ -2073,6 +2212,7 @@ ConvArgs make_args(int B, int H, int W, int C, int K, int KH, int KW, int sh, in
   a.fd_sh = make_fd(sh);
   a.fd_sw = make_fd(sw);
   a.fd_Kp = make_fd(1);
+  a.tstep = 1;
   return a;
 }
 
@@ -2342,10 +2482,24 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
     if (!a.zp) return (int)hipErrorInvalidSymbol;
     return dispatch_direct<FWD>(a, bm, bn, bk, s);
   }
-  if (variant == 6) {  // stem halo: 7x7 / s2 / p3, Cin 8, Cout 64, one image per block
+  if (variant == 6) {  // stem halo: 7x7 / s2 / p3, Cin 8, Cout 64; 32x32: one image per block,
+                       // 224x224: persistent blocks over output row pairs
     if (g22 || fold_c || C != 8 || K != 64 || KH != 7 || KW != 7 || sh != 2 || sw != 2 || ph != 3 || pw != 3 ||
-        H != W || H != 32)
+        H != W || (H != 32 && H != 224))
       return (int)hipErrorInvalidValue;
+    if (H == 224) {
+      if (bm != 224) return (int)hipErrorInvalidValue;
+      ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
+      a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
+      a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
+      a.zp = zero_page();
+      a.M = B * a.OH * a.OW; a.N = K; a.Kd = 392;
+      a.splits = 1; a.kchunk = a.Kd;
+      if (!a.zp) return (int)hipErrorInvalidSymbol;
+      const int T = B * (a.OH / 2);
+      hipLaunchKernelGGL((k_conv_stem_rows<112>), dim3(T < 256 ? T : 256), dim3(256), 0, s, a);
+      KML_LAUNCH_CHECK();
+    }
     ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
     a.x = x; a.w = w; a.out = y; a.bias = bias; a.stats = stats; a.stats_part = stats_part; a.relu = relu;
     a.grp_out = grp_out; a.grp_cnt = grp_cnt; a.grp_tiles = grp_tiles;
@@ -2582,6 +2736,55 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
   }
   if (variant) bk = 64;
   return dispatch<DGRAD>(a, bm, bn, bk, variant, s);
+}
+
+// Stride-2 DGRAD as four parity classes (ConvArgs::par): class (pa, pe) computes the input
+// pixels (2i + pa, 2j + pe) from the taps of matching parity only — 1/4 of the gathered
+// (pixel, tap) pairs of the plain stride-2 dgrad are non-zero, and a class with no taps
+// (1x1/s2: three of four) runs the epilogue alone (addend / zeros, consumer-BN partials).
+// Plain igemm / glds variants, no split-K, no group reduction; bnf_part holds the classes'
+// partial rows back to back (kml_conv_dgrad_s2_rows).
+KML_API int kml_conv_dgrad_s2_rows(int B, int H, int W, int bm) {
+  int rows = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int pa = c >> 1, pe = c & 1;
+    const long long Mc = (long long)B * ((H - pa + 1) / 2) * ((W - pe + 1) / 2);
+    rows += (int)((Mc + bm - 1) / bm);
+  }
+  return rows;
+}
+
+KML_API int kml_conv_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend,
+                              const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
+                              float* bnf_part, int B, int H, int W, int C, int K, int KH, int KW, int ph, int pw,
+                              int bm, int bn, int bk, int variant, int bnf_mask_out, hipStream_t s) {
+  if (variant != 0 && variant != 1 && variant != 2) return (int)hipErrorInvalidValue;
+  ConvArgs a0;
+  int e = prep_dgrad(a0, dy, w, nullptr, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, nullptr, nullptr, 0,
+                     B, H, W, C, K, KH, KW, 2, 2, ph, pw, bk, 1, variant, nullptr, nullptr, 0, bnf_mask_out, 0);
+  if (e) return e;
+  if (variant) bk = 64;
+  int rowbase = 0;
+  for (int c = 0; c < 4; ++c) {
+    ConvArgs a = a0;
+    a.par = 1; a.pa = c >> 1; a.pe = c & 1; a.tstep = 2;
+    const int Hc = (H - a.pa + 1) / 2, Wc = (W - a.pe + 1) / 2;
+    a.fd_Hc = make_fd(Hc > 0 ? Hc : 1); a.fd_Wc = make_fd(Wc > 0 ? Wc : 1);
+    a.M = B * Hc * Wc;
+    if (a.M <= 0) continue;
+    a.r0 = (a.pa + ph) & 1; a.s0 = (a.pe + pw) & 1;
+    const int nr = a.r0 < KH ? (KH - a.r0 + 1) / 2 : 0, ns = a.s0 < KW ? (KW - a.s0 + 1) / 2 : 0;
+    a.r1 = a.r0 + 2 * nr; a.s1 = a.s0 + 2 * ns;
+    a.fd_nts = make_fd(ns > 0 ? ns : 1);
+    a.Kd = nr * ns * a.Kp;
+    a.kchunk = a.Kd > 0 ? (a.Kd + bk - 1) / bk * bk : bk;
+    a.splits = 1;
+    a.rowbase = rowbase;
+    rowbase += (a.M + bm - 1) / bm;
+    e = dispatch<DGRAD>(a, bm, bn, bk, variant, s);
+    if (e) return e;
+  }
+  return 0;
 }
 
 KML_API int kml_weight_transpose(const bf16_t* w, bf16_t* wt, int K, int KH, int KW, int C, hipStream_t s) {

@@ -441,12 +441,18 @@ def halo_dgrad_plan(C, K, H, W, KH, KW, stride, pad):
     return None
 
 
-STEM = 6  # cfg variant id of the stem halo kernel (7x7/s2/p3, Cin 8, Cout 64, 32x32 input): bm = one image
+STEM = 6  # cfg variant id of the stem patch kernel (7x7/s2/p3, Cin 8, Cout 64; 32x32 or 224x224 input)
 def stem_plan(C, K, H, W, KH, KW, stride, pad, force=False):
-    """(256, 64, 0, 1, STEM) for the ResNet ImageNet stem on 32x32 images, else None."""
-    if (C, K, H, W, KH, KW, tuple(stride), tuple(pad)) != (8, 64, 32, 32, 7, 7, (2, 2), (3, 3)):
+    """The ResNet ImageNet stem (7x7/s2/p3, Cin padded to 8, 64 out) as the patch-in-LDS
+    kernel: (256, 64, 0, 1, STEM) on 32x32 images (one image per block), (224, 64, 0, 1,
+    STEM) on 224x224 (persistent blocks over output row pairs, bm = 2 output rows), else None."""
+    if (C, K, KH, KW, tuple(stride), tuple(pad)) != (8, 64, 7, 7, (2, 2), (3, 3)) or H != W:
         return None
-    return (256, 64, 0, 1, STEM)
+    if H == 32:
+        return (256, 64, 0, 1, STEM)
+    if H == 224:
+        return (224, 64, 0, 1, STEM)
+    return None
 
 
 ONESHOT = 5  # cfg variant id of the one-shot panel forward (single-tap convs, K in _ONESHOT_TILES)
@@ -618,6 +624,19 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     if variant == HALO and (_g22 or not halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn)):
         bm, bn, bk, splits, variant = _norm_cfg(plan_conv("dgrad", M, C, ntap * K))
     plan = (bm, bn, bk, splits, variant)
+    if s2_parity_ok(B, H, W, stride, variant, _g22, _fold):
+        part, G = None, 0
+        by = bc = bmean = brstd = None
+        if bnf is not None:
+            by, bc, bmean, brstd = bnf
+            if bc.shape != out.shape or (by is not None and by.shape != out.shape):
+                raise ValueError("bnf tensors must match the dgrad output shape")
+            G = HIP.fn("kml_conv_dgrad_s2_rows", "i i i i")(B, H, W, bm)
+            part = torch.empty(G * 2 * C, dtype=F32, device=out.device)
+        HIP.call("kml_conv_dgrad_s2", "p p p p p p p p p i i i i i i i i i i i i i i s",
+                 _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(part), B, H, W, C, K,
+                 KH, KW, ph, pw, bm, bn, bk, variant, int(bool(bnf_mask) and bnf is not None), _s())
+        return (out, (part, G)) if bnf is not None else out
     by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan, _fold)
     slab = cnt = None
     if variant in (HALO, ONESHOT):
@@ -637,6 +656,17 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
              _p(gcnt), tpg, B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant, _p(slab), _p(cnt),
              int(_fold), int(bool(bnf_mask) and bnf is not None), int(_g22), _s())
     return (out, (part, G)) if bnf is not None else out
+
+
+# Stride-2 dgrads of the large-map convs run as four parity-class launches
+# (kml_conv_dgrad_s2): 1/4 of the (pixel, tap) pairs of a stride-2 dgrad are non-zero.  Off
+# for small maps (ResNet-34/CIFAR), where four launches cost more than the skipped zeros.
+_S2_PARITY_MIN_ROWS = 20000
+
+
+def s2_parity_ok(B, H, W, stride, variant, g22=False, fold=0) -> bool:
+    return (tuple(stride) == (2, 2) and variant in (0, 1, 2) and not g22 and not fold
+            and B * H * W >= _S2_PARITY_MIN_ROWS)
 
 
 def _bnf_ws(bnf, out, M, C, plan, fold=0):
@@ -757,6 +787,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
+    if grouped and s2_parity_ok(B, H, W, stride, dplan[4], g22, fold):
+        grouped = False
     if dbias is not None and wu is not None:
         raise ValueError("conv_bwd: dbias needs a 1x1 conv")
     if not grouped:

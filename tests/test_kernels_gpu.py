@@ -1038,6 +1038,38 @@ def test_conv_stem_variant():
     assert _rel(buf[:G * 128].view(G, 2, 64).sum(0)[0], yr.sum((0, 2, 3))) < 2e-2
 
 
+@pytest.mark.parametrize("B", [3, 300])
+def test_conv_stem_rows_224(B):
+    """ImageNet-size stem (variant 6 on 224x224: persistent blocks over output row pairs,
+    weights resident in LDS) vs fp32 torch: output and one partial statistics row per row
+    pair.  B = 300 has more tiles (16800) than blocks, so blocks loop and prefetch."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(18)
+    x = torch.zeros(B, 224, 224, 8, device=dev)
+    x[..., :3] = torch.randn(B, 224, 224, 3, device=dev)
+    x = _bf(x)
+    w = torch.zeros(64, 7, 7, 8, device=dev)
+    w[..., :3] = torch.randn(64, 7, 7, 3, device=dev) * 0.1
+    w = _bf(w)
+    M = B * 112 * 112
+    cfg = K.conv_fwd_plan(8, M, 64, 392, geom=(224, 224, 7, 7, (2, 2), (3, 3)))
+    assert cfg[4] == K.STEM and cfg[0] == 224
+    G = K.conv_fwd_stats_rows(x.shape, 64, 7, 7, (2, 2), (3, 3))
+    assert G == B * 56
+    buf = torch.full((G * 128 + 64,), float("nan"), device=dev)
+    y = K.conv_fwd(x, w, 7, 7, (2, 2), (3, 3), stats=buf[:G * 128], stats_part=True)
+    torch.cuda.synchronize()
+    assert torch.isnan(buf[G * 128:]).all() and not torch.isnan(buf[:G * 128]).any()
+    for b0 in sorted({0, B // 2, B - 1}):
+        yr = F.conv2d(x[b0:b0 + 1].float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), stride=2, padding=3)
+        assert _rel(y[b0:b0 + 1].permute(0, 3, 1, 2), yr) < 1e-2
+        rows = buf[:G * 128].view(B, 56, 2, 64)[b0]
+        assert _rel(rows[:, 0].sum(0), yr.sum((0, 2, 3))) < 2e-2
+        assert _rel(rows[:, 1].sum(0), (yr * yr).sum((0, 2, 3))) < 2e-2
+        # one row per output row pair: row t covers output rows 2t, 2t+1
+        assert _rel(rows[7, 0], yr[0, :, 14:16].sum((1, 2))) < 2e-2
+
+
 @pytest.mark.parametrize("case", [(8, 8, 64, 64), (12, 4, 128, 128)])
 def test_conv_fwd_bnin_matches_bn_then_conv(case):
     """conv_fwd_bnin (the input's BN + ReLU applied while the halo patch is staged) vs
@@ -1078,3 +1110,43 @@ def test_conv_fwd_bnin_matches_bn_then_conv(case):
         assert _rel(o1, o0) < 1e-2, (group, _rel(o1, o0))
         of = o1.float().reshape(-1, Co)
         assert _rel(st2.view(G2, 2, Co).sum(0)[0], of.sum(0)) < 2e-2
+
+
+@pytest.mark.parametrize("shape", [(8, 56, 56, 64, 64, 3, 1), (8, 57, 57, 64, 128, 3, 1), (8, 56, 56, 128, 64, 1, 0),
+                                   (8, 57, 56, 64, 64, 1, 0)])
+@pytest.mark.parametrize("cfg", [(64, 64, 32, 1, 0), (64, 64, 64, 1, 0), (64, 128, 64, 1, 1)])
+def test_stride2_dgrad_parity_classes(shape, cfg, monkeypatch):
+    """Stride-2 dgrad as four parity-class launches == the plain stride-2 dgrad (bit-exact dX,
+    same consumer-BN dgamma/dbeta) and the fp32 torch reference; with and without addend."""
+    from kubeml_amd.ops import kernels as K
+    B, H, W, Ci, Co, k, p = shape
+    assert K.s2_parity_ok(B, H, W, (2, 2), cfg[4])
+    torch.manual_seed(11)
+    OH, OW = K.out_hw(H, W, k, k, 2, 2, p, p)
+    dy = _bf(torch.randn(B, OH, OW, Co, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * 0.05)
+    add = _bf(torch.randn(B, H, W, Ci, device=dev))
+    c = _bf(torch.randn(B, H, W, Ci, device=dev))
+    ybn = _bf(torch.randn(B, H, W, Ci, device=dev))
+    mean, rstd = torch.randn(Ci, device=dev), torch.rand(Ci, device=dev) + 0.5
+    g = torch.rand(Ci, device=dev) + 0.5
+    for addend in (add, None):
+        for mask in (False, True):
+            dx1, part1 = K.conv_dgrad(dy, w, (B, H, W, Ci), k, k, (2, 2), (p, p), addend=addend, cfg=cfg,
+                                      bnf=(ybn, c, mean, rstd), bnf_mask=mask)
+            monkeypatch.setattr(K, "_S2_PARITY_MIN_ROWS", 1 << 40)
+            dx0, part0 = K.conv_dgrad(dy, w, (B, H, W, Ci), k, k, (2, 2), (p, p), addend=addend, cfg=cfg,
+                                      bnf=(ybn, c, mean, rstd), bnf_mask=mask)
+            monkeypatch.setattr(K, "_S2_PARITY_MIN_ROWS", 20000)
+            torch.cuda.synchronize()
+            assert torch.equal(dx1, dx0)
+            dg0, db0 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+            dg1, db1 = torch.zeros(Ci, device=dev), torch.zeros(Ci, device=dev)
+            yy = None if mask else ybn
+            K.bn_bwd(dx0, yy, c, mean, rstd, g, dg0, db0, partial=part0)
+            K.bn_bwd(dx1, yy, c, mean, rstd, g, dg1, db1, partial=part1)
+            assert _rel(db1, db0) < 1e-4 and _rel(dg1, dg0) < 1e-4
+    xr = torch.zeros(B, Ci, H, W, device=dev, requires_grad=True)
+    F.conv2d(xr, w.float().permute(0, 3, 1, 2), stride=2, padding=p).backward(dy.float().permute(0, 3, 1, 2))
+    dx = K.conv_dgrad(dy, w, (B, H, W, Ci), k, k, (2, 2), (p, p), cfg=cfg)
+    assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
