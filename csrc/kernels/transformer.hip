@@ -108,6 +108,12 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, co
 // ------------------------------------------------------------------------------ LayerNorm bwd
 // dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat));  dx (+)= into dx (accumulate flag)
 // dgamma/dbeta: per-block partials [gridDim][2N], then k_colreduce sums them in block order.
+// One wave per row, NV = ceil(N / 256) register vectors per operand (compile time: a 768-wide
+// BERT row holds 3, not the 8 of the widest shape), and the wave's NEXT row (row + 4) is
+// loaded while this one is reduced and stored — the per-row chain (loads -> two wave
+// reductions -> stores) otherwise leaves one row in flight per wave.  Same per-element
+// arithmetic and per-wave row order as the one-row version: bit-identical results.
+template <int NV>
 __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ xin,
                                                 const float* __restrict__ mean, const float* __restrict__ rstd,
                                                 const float* __restrict__ gamma, bf16_t* __restrict__ dx,
@@ -116,29 +122,54 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
                                                 const float* __restrict__ dctr, unsigned dsalt, float dp,
                                                 int with_in) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nv = N / 256 + ((N % 256) > 0);
-  float pg[MAXV][4], pb[MAXV][4], pi[MAXV][4];  // pi: column sums of the input gradient (part_in)
+  float pg[NV][4], pb[NV][4], pi[NV][4];  // pi: column sums of the input gradient (part_in)
+  float gm[NV][4];
 #pragma unroll
-  for (int u = 0; u < MAXV; ++u)
+  for (int u = 0; u < NV; ++u) {
+    const int c = (u * 64 + lane) * 4;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { pg[u][k] = 0.f; pb[u][k] = 0.f; pi[u][k] = 0.f; }
+    for (int k = 0; k < 4; ++k) {
+      pg[u][k] = 0.f; pb[u][k] = 0.f; pi[u][k] = 0.f;
+      gm[u][k] = c < N ? gamma[c + k] : 0.f;
+    }
+  }
   const long long r0 = (long long)blockIdx.x * rows_per_block;
   const long long r1 = min(M, r0 + rows_per_block);
-  for (long long row = r0 + wv; row < r1; row += 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[MAXV][4], gd[MAXV][4];
+  uint2 dv[NV], xv[NV], av[NV];
+  float mu = 0.f, rs = 0.f;
+  auto load = [&](long long row) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = (u * 64 + lane) * 4;
+      if (c < N) {
+        dv[u] = *reinterpret_cast<const uint2*>(dy + row * N + c);
+        xv[u] = *reinterpret_cast<const uint2*>(xin + row * N + c);
+        if (dx_add) av[u] = *reinterpret_cast<const uint2*>(dx_add + row * N + c);
+      }
+    }
+    mu = mean[row];
+    rs = rstd[row];
+  };
+  long long row = r0 + wv;
+  if (row < r1) load(row);
+  for (; row < r1; row += 4) {
+    uint2 d_cur[NV], x_cur[NV], a_cur[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) { d_cur[u] = dv[u]; x_cur[u] = xv[u]; a_cur[u] = av[u]; }
+    const float mu_c = mu, rs_c = rs;
+    if (row + 4 < r1) load(row + 4);  // next row of this wave, in flight during this one
+    float xh[NV][4], gd[NV][4];
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int u = 0; u < MAXV; ++u) {
+    for (int u = 0; u < NV; ++u) {
       const int c = (u * 64 + lane) * 4;
-      if (u < nv && c < N) {
-        float d[4], xv[4];
-        ld4(dy + row * N + c, d);
-        ld4(xin + row * N + c, xv);
+      if (c < N) {
+        const float d[4] = {lo_bf(d_cur[u].x), hi_bf(d_cur[u].x), lo_bf(d_cur[u].y), hi_bf(d_cur[u].y)};
+        const float xf[4] = {lo_bf(x_cur[u].x), hi_bf(x_cur[u].x), lo_bf(x_cur[u].y), hi_bf(x_cur[u].y)};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          xh[u][k] = (xv[k] - mu) * rs;
-          gd[u][k] = d[k] * gamma[c + k];
+          xh[u][k] = (xf[k] - mu_c) * rs_c;
+          gd[u][k] = d[k] * gm[u][k];
           a1 += gd[u][k];
           a2 += gd[u][k] * xh[u][k];
           pg[u][k] += d[k] * xh[u][k];
@@ -149,15 +180,14 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
     a1 = wave_sum(a1) / N;
     a2 = wave_sum(a2) / N;
 #pragma unroll
-    for (int u = 0; u < MAXV; ++u) {
+    for (int u = 0; u < NV; ++u) {
       const int c = (u * 64 + lane) * 4;
-      if (u < nv && c < N) {
+      if (c < N) {
         float o[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = rs * (gd[u][k] - a1 - xh[u][k] * a2);
+        for (int k = 0; k < 4; ++k) o[k] = rs_c * (gd[u][k] - a1 - xh[u][k] * a2);
         if (dx_add) {
-          float e[4];
-          ld4(dx_add + row * N + c, e);
+          const float e[4] = {lo_bf(a_cur[u].x), hi_bf(a_cur[u].x), lo_bf(a_cur[u].y), hi_bf(a_cur[u].y)};
 #pragma unroll
           for (int k = 0; k < 4; ++k) o[k] += e[k];
         }
@@ -179,9 +209,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
   // block partials: reduce the 4 waves in LDS, then one row of 2N floats per block
   __shared__ float red[4][2 * 2048];
 #pragma unroll
-  for (int u = 0; u < MAXV; ++u) {
+  for (int u = 0; u < NV; ++u) {
     const int c = (u * 64 + lane) * 4;
-    if (u < nv && c < N)
+    if (c < N)
 #pragma unroll
       for (int k = 0; k < 4; ++k) { red[wv][c + k] = pg[u][k]; red[wv][N + c + k] = pb[u][k]; }
   }
@@ -192,9 +222,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(const bf16_t* __restrict__ dy, c
   if (with_in) {  // third segment, through the same LDS (uniform branch)
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < MAXV; ++u) {
+    for (int u = 0; u < NV; ++u) {
       const int c = (u * 64 + lane) * 4;
-      if (u < nv && c < N)
+      if (c < N)
 #pragma unroll
         for (int k = 0; k < 4; ++k) red[wv][c + k] = pi[u][k];
     }
@@ -463,8 +493,13 @@ KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, c
   // dbias_in (optional): += column sums of the input gradient (dx_drop, else dx) — the bias
   // gradient of the Linear feeding this LayerNorm; partials in ws after the [g][2N] block
   const int with_in = dbias_in ? 1 : 0;
-  hipLaunchKernelGGL(k_ln_bwd, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, rpb,
-                     dx_drop, dctr, dsalt, dp, with_in);
+  const int nv = (N + 255) / 256;
+#define KML_LNB(NVv)                                                                                              \
+  if (nv == NVv)                                                                                                  \
+    hipLaunchKernelGGL(k_ln_bwd<NVv>, dim3(g), dim3(256), 0, s, dy, xin, mean, rstd, gamma, dx, dx_add, ws, M, N, \
+                       rpb, dx_drop, dctr, dsalt, dp, with_in);
+  KML_LNB(1) KML_LNB(2) KML_LNB(3) KML_LNB(4) KML_LNB(5) KML_LNB(6) KML_LNB(7) KML_LNB(8)
+#undef KML_LNB
   const int W = (2 + with_in) * N;
   hipLaunchKernelGGL(k_colreduce, dim3((W + 63) / 64), dim3(256), 0, s, ws, g, W, N, dgamma, dbeta, N, dbias_in);
   KML_LAUNCH_CHECK();

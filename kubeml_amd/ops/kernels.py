@@ -390,7 +390,9 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
     (H, W, KH, KW, stride, pad) lets an eligible conv take the halo-patch kernel
     (:func:`halo_plan`); without it (or when ineligible) a HALO plan falls back."""
     if cfg is None and geom is not None:
-        hp = halo_plan(C, K, *geom) or oneshot_plan(C, K, Kd, *geom) or stem_plan(C, K, *geom)
+        OH, OW = out_hw(geom[0], geom[1], geom[2], geom[3], geom[4][0], geom[4][1], geom[5][0], geom[5][1])
+        B = M // max(OH * OW, 1)
+        hp = halo_plan(C, K, *geom) or oneshot_plan(C, K, Kd, *geom, B=B) or stem_plan(C, K, *geom)
         if hp is not None:
             return hp
     plan = _norm_cfg(cfg or plan_conv("fwd", M, K, Kd))
@@ -469,8 +471,16 @@ def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
     return (r1 - r0) == 1 and (s1 - s0) == 1 and rows
 
 
-def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad):
+# Large maps with K >= 512 take the tuned implicit GEMM instead: the one-shot panels (one
+# block per CU at K = 1024, 32x32 tiles) run ResNet-50's 14x14 / 28x28 1x1 convs at ~95-135
+# TF/s against 290-380 for the tuned tiles; at K = 256 the panels still win (56x56 maps).
+_ONESHOT_MAX_ROWS_LONG_K = 4096
+
+
+def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad, B=0):
     """Default one-shot panel plan for an eligible forward conv, or None."""
+    if Kd >= 512 and B * H * W > _ONESHOT_MAX_ROWS_LONG_K:
+        return None
     for bm, bn in _ONESHOT_TILES.get(Kd, ()):
         if oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn):
             return (bm, bn, 0, 1, ONESHOT)
