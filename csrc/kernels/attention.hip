@@ -202,8 +202,8 @@ __device__ __forceinline__ void store4(bf16_t* p, const f32x4_t& v, float s) {
 }
 
 // ------------------------------------------------------------------------------ forward
-// OCC: waves per SIMD the register budget is sized for (launch bounds); selectable at run
-// time (attn_occ) so the occupancy / register trade is measured, not assumed
+// OCC: waves per SIMD the register budget is sized for (launch bounds; the occupancy /
+// register trade of each kernel was measured, profiles/bert_base_r3.md)
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
   // K/V double-buffered (40 KB: 4 blocks per CU, the VGPR occupancy): one barrier per key
@@ -588,23 +588,6 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
 
 bool aligned16(const void* p) { return (((unsigned long long)p) & 15ull) == 0; }
 
-// KUBEML_ATTN_OCC="dq,dkv" waves per SIMD of the backward kernels (default 4,2: dq fits 128
-// VGPRs without spills, dkv needs ~220; the forward always runs at 4 with 120)
-const int* attn_occ() {
-  static int occ[2] = {4, 2};
-  static const bool init = [] {
-    if (const char* e = std::getenv("KUBEML_ATTN_OCC")) std::sscanf(e, "%d,%d", &occ[0], &occ[1]);
-    return true;
-  }();
-  (void)init;
-  return occ;
-}
-
-int xcd_order() {
-  static const int on = [] { const char* e = std::getenv("KUBEML_ATTN_XCD"); return e ? std::atoi(e) : 1; }();
-  return on;
-}
-
 }  // namespace
 
 // q/k/v/out: token-major [B*L, ld*] bf16, head h at column 64h (head_dim must be 64)
@@ -619,7 +602,7 @@ KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
   a.q = q; a.k = k; a.v = v; a.out = out; a.lse = lse; a.bias = bias;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldout = ldout;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
-  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = xcd_order(); a.keep = keep;
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = 1; a.keep = keep;
   if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
   const dim3 grid((L + 63) / 64, B * H);
   hipLaunchKernelGGL(k_attn_fwd<4>, grid, dim3(256), 0, s, a);
@@ -640,13 +623,13 @@ KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   a.bias = bias; a.dq = dq; a.dk = dk; a.dv = dv;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
   a.B = B; a.H = H; a.L = L; a.scale = scale;
-  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = xcd_order();
+  a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = 1;
   a.keep = const_cast<unsigned char*>(keep);
   if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
   const dim3 grid((L + 63) / 64, B * H);
-  if (attn_occ()[0] == 3) hipLaunchKernelGGL(k_attn_bwd_dq<3>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_attn_bwd_dq<4>, grid, dim3(256), 0, s, a);
-  if (attn_occ()[1] == 3) hipLaunchKernelGGL(k_attn_bwd_dkv<3>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(k_attn_bwd_dkv<2>, grid, dim3(256), 0, s, a);
+  // occupancy from the register budgets (profiles/bert_base_r3.md): dQ at 4 waves per SIMD
+  // (124 VGPRs, no spills), dKV at 2 (~211 VGPRs; 3 spills and doubles its time)
+  hipLaunchKernelGGL(k_attn_bwd_dq<4>, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_attn_bwd_dkv<2>, grid, dim3(256), 0, s, a);
   KML_LAUNCH_CHECK();
 }

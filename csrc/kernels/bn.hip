@@ -823,17 +823,6 @@ static int pick_v(long long n8, int vmax) {
   while (r < v && r < vmax) r *= 2;
   return r;
 }
-// Every block of an apply kernel sums all G partial rows first: with many rows, fewer and
-// fuller blocks (twice the chunks per thread) halve that L2 traffic.  Threshold from
-// KUBEML_BN_ROWS_WIDEN (rows; 0 = off), read once.
-static int rows_widen_v(int V, int G, int vmax) {
-  static int thr = -1;
-  if (thr < 0) {
-    const char* e = getenv("KUBEML_BN_ROWS_WIDEN");
-    thr = e ? atoi(e) : 0;
-  }
-  return (thr > 0 && G >= thr && V * 2 <= vmax) ? V * 2 : V;
-}
 static unsigned v_grid(long long n8, int V) {
   long long g = (n8 + (long long)TPB * V - 1) / ((long long)TPB * V);
   if (g > 1024) g = 1024;
@@ -1137,7 +1126,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
                                 hipStream_t s) {
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = rows_widen_v(pick_v(n8, 4), G, 4);
+    const int V = pick_v(n8, 4);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
 #define KML_BWD_V(VV)                                                                                          \
@@ -1188,7 +1177,7 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
   if (mode == 0 && stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = rows_widen_v(pick_v(n8, 8), mode == 0 ? stats_rows : 0, 8);
+    const int V = pick_v(n8, 8);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
 #define KML_AP_V(VV)                                                                                           \

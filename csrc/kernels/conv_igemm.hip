@@ -134,11 +134,11 @@ struct ConvArgs {
   FastDiv fd_C, fd_nts, fd_OW, fd_OH, fd_W, fd_H, fd_Kp, fd_sh, fd_sw;
   // Stride-2 DGRAD by parity class (kml_conv_dgrad_s2): this launch computes the input pixels
   // (ih, iw) = (2i + pa, 2j + pe) only — GEMM row m = (b, i, j) over an Hc x Wc grid — with
-  // only the taps of matching parity (r = r0 + tstep * tr, tstep = 2), so none of the 3/4 of
-  // (pixel, tap) pairs a stride-2 dgrad gathers from the zero page is computed.  rowbase: the
-  // class's first row in the consumer-BN partial-row buffer.
-  int par, pa, pe, tstep, rowbase;
-  FastDiv fd_Wc, fd_Hc;
+  // only the taps of matching parity (r = r0 + 2 tr, tap_rs2), so none of the 3/4 of
+  // (pixel, tap) pairs a stride-2 dgrad gathers from the zero page is computed.
+  // par: bit 0 = parity class, bit 1 = pa, bit 2 = pe (fd_W / fd_H then divide by the class
+  // grid Wc / Hc; bnf_part points at the class's first partial row).
+  int par;
 };
 
 // Block coordinates of one conv tile: kernels pass blockIdx; the grouped backward kernel
@@ -170,8 +170,14 @@ __device__ __forceinline__ uint4 ld16(const bf16_t* p) { return *reinterpret_cas
 
 __device__ __forceinline__ void tap_rs(const ConvArgs& a, int tap, int& r, int& s) {
   const int tr = fdiv(tap, a.fd_nts);
-  r = a.r0 + tr * a.tstep;
-  s = a.s0 + (tap - tr * a.fd_nts.d) * a.tstep;
+  r = a.r0 + tr;
+  s = a.s0 + (tap - tr * a.fd_nts.d);
+}
+// taps of one stride-2 parity class: every second row / column of the filter
+__device__ __forceinline__ void tap_rs2(const ConvArgs& a, int tap, int& r, int& s) {
+  const int tr = fdiv(tap, a.fd_nts);
+  r = a.r0 + 2 * tr;
+  s = a.s0 + 2 * (tap - tr * a.fd_nts.d);
 }
 
 // ---------------------------------------------------------------------------------
@@ -253,17 +259,10 @@ struct DgradA {  // dY gathered for input pixel m; K = (tap, cout); Kp % BK == 0
   __device__ void init(const ConvArgs& a, int m, int q) {
     valid = m < a.M;
     const int mm = valid ? m : 0;
-    if (a.par) {  // parity class: row = (b, i, j) -> pixel (2i + pa, 2j + pe)
-      const int t = fdiv(mm, a.fd_Wc);
-      iw = 2 * (mm - t * a.fd_Wc.d) + a.pe;
-      b = fdiv(t, a.fd_Hc);
-      ih = 2 * (t - b * a.fd_Hc.d) + a.pa;
-    } else {
-      const int t = fdiv(mm, a.fd_W);
-      iw = mm - t * a.W;
-      b = fdiv(t, a.fd_H);
-      ih = t - b * a.H;
-    }
+    const int t = fdiv(mm, a.fd_W);
+    iw = mm - t * a.W;
+    b = fdiv(t, a.fd_H);
+    ih = t - b * a.H;
     koff = (q % (BK / 8)) * 8;
   }
   __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
@@ -271,6 +270,36 @@ struct DgradA {  // dY gathered for input pixel m; K = (tap, cout); Kp % BK == 0
     const int n = kb - tap * a.Kp + koff;
     int r, s;
     tap_rs(a, tap, r, s);
+    const int th = ih + a.ph - r, tw = iw + a.pw - s;
+    const int oh = fdiv(th < 0 ? 0 : th, a.fd_sh), ow = fdiv(tw < 0 ? 0 : tw, a.fd_sw);
+    const bool ok = valid && kb + koff < kend && n < a.K && th >= 0 && tw >= 0 && oh * a.sh == th &&
+                    ow * a.sw == tw && oh < a.OH && ow < a.OW;
+    return ok ? a.dy + ((b * a.OH + oh) * a.OW + ow) * a.K + n : a.zp;
+  }
+};
+
+template <int BK>
+// Stride-2 parity-class dgrad operands (kml_conv_dgrad_s2): GEMM row m = (b, i, j) is the input
+// pixel (2i + pa, 2j + pe) and the taps are those of matching parity (tap_rs2).  Selected by
+// the DGRAD bodies' TAPU = false instantiation (a plain DGRAD K-tile always sits in one tap,
+// so TAPU = false is otherwise never launched for DGRAD): the plain kernels keep their code.
+struct DgradAP {  // dY gathered for parity-class pixel m
+  int b, ih, iw, koff;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int m, int q) {
+    valid = m < a.M;
+    const int mm = valid ? m : 0;
+    const int t = fdiv(mm, a.fd_W);  // fd_W / fd_H hold the class grid Wc / Hc here
+    iw = 2 * (mm - t * a.fd_W.d) + ((a.par >> 2) & 1);
+    b = fdiv(t, a.fd_H);
+    ih = 2 * (t - b * a.fd_H.d) + ((a.par >> 1) & 1);
+    koff = (q % (BK / 8)) * 8;
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int tap = fdiv(kb, a.fd_Kp);  // uniform
+    const int n = kb - tap * a.Kp + koff;
+    int r, s;
+    tap_rs2(a, tap, r, s);
     const int th = ih + a.ph - r, tw = iw + a.pw - s;
     const int oh = fdiv(th < 0 ? 0 : th, a.fd_sh), ow = fdiv(tw < 0 ? 0 : tw, a.fd_sw);
     const bool ok = valid && kb + koff < kend && n < a.K && th >= 0 && tw >= 0 && oh * a.sh == th &&
@@ -307,6 +336,39 @@ struct DgradB {  // LDS row = k = (tap, cout), cols = cin; chunk = W[cout][tap][
     }
     int r, s;
     tap_rs(a, tap, r, s);
+    const bool ok = valid && kb + krow < kend && n < a.K;
+    return ok ? a.w + ((n * a.KH + r) * a.KW + s) * a.C + c : a.zp;
+  }
+};
+
+template <int BK, int BN>
+struct DgradBP {  // DgradB over one parity class's taps (tap_rs2; no unrolled-weight gather)  // LDS row = k = (tap, cout), cols = cin; chunk = W[cout][tap][c..c+7]
+  int krow, c, q22, c22;
+  bool valid;
+  __device__ void init(const ConvArgs& a, int n0, int q) {
+    constexpr int CPR = BN / 8;
+    krow = q / CPR;
+    c = n0 + (q % CPR) * 8;
+    valid = c < a.N;
+    if (a.g22) {  // column c = (q, c') of the unrolled weight
+      const int cc = valid ? c : 0;
+      q22 = fdiv(cc, a.fd_gC);
+      c22 = cc - q22 * a.fd_gC.d;
+    } else {
+      q22 = c22 = 0;
+    }
+  }
+  __device__ const bf16_t* ptr(const ConvArgs& a, int kb, int kend) const {
+    const int tap = fdiv(kb, a.fd_Kp);  // uniform
+    const int n = kb - tap * a.Kp + krow;
+    if (a.g22) {  // 1x1 form (tap 0), row n = (p, n'): w[n'][tap(p, q)][c']
+      const bool ok = valid && kb + krow < kend && n < a.K;
+      const int nn = ok ? n : 0;
+      const int p = fdiv(nn, a.fd_gK);
+      return ok ? a.w + ((long long)(nn - p * a.fd_gK.d) * 9 + tap22(p, q22)) * a.fd_gC.d + c22 : a.zp;
+    }
+    int r, s;
+    tap_rs2(a, tap, r, s);
     const bool ok = valid && kb + krow < kend && n < a.K;
     return ok ? a.w + ((n * a.KH + r) * a.KW + s) * a.C + c : a.zp;
   }
@@ -456,12 +518,13 @@ __device__ __forceinline__ int row_off(const ConvArgs& a, int col) {
 }
 __device__ __forceinline__ int sq_off(const ConvArgs& a) { return a.fold_c ? a.fold_c : a.N; }
 
-// Output pixel row of GEMM row `row` (identity except in a stride-2 parity-class DGRAD).
+// Output pixel row of GEMM row `row` (identity except in a stride-2 parity-class DGRAD, which
+// always runs the row-pass epilogue below: the per-element epilogue stays free of the remap).
 __device__ __forceinline__ long long prow(const ConvArgs& a, int row) {
   if (!a.par) return row;
-  const int t = fdiv(row, a.fd_Wc), j = row - t * a.fd_Wc.d;
-  const int b = fdiv(t, a.fd_Hc), i = t - b * a.fd_Hc.d;
-  return ((long long)b * a.H + 2 * i + a.pa) * a.W + 2 * j + a.pe;
+  const int t = fdiv(row, a.fd_W), j = row - t * a.fd_W.d;
+  const int b = fdiv(t, a.fd_H), i = t - b * a.fd_H.d;
+  return ((long long)b * a.H + 2 * i + ((a.par >> 1) & 1)) * a.W + 2 * j + ((a.par >> 2) & 1);
 }
 
 // DGRAD epilogue through LDS rows, for tiles whose output merges an addend and/or feeds the
@@ -560,7 +623,7 @@ __device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[
   __syncthreads();
   float* rows = a.bnf_part;
   const bool sc1_rows = a.grp_out != nullptr;
-  const long long rrow = (long long)(a.rowbase + m0 / BMT) * 2 * a.N;
+  const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
   for (int q = tid; q < 2 * BNT; q += 256) {
     const int half = q / BNT, cl = q - half * BNT, col = n0 + cl;
     if (col >= a.N) continue;
@@ -713,7 +776,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
     // the BN kernel (every block of which reads all rows) reads half as many.
     float* rows = (MODE == DGRAD) ? a.bnf_part : ((a.stats && a.stats_part) ? a.stats : nullptr);
     const bool sc1_rows = a.grp_out != nullptr;
-    const long long rrow = (long long)(a.rowbase + m0 / BMT) * 2 * a.N;
+    const long long rrow = (long long)(m0 / BMT) * 2 * a.N;
     const int ldc = a.N;
     float k1[NR], k2[NR];
 #pragma unroll
@@ -732,11 +795,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
           if (row < a.M && cok) {
             float v = acc[i][j][e] + bv;
             if (MODE == FWD && a.relu) v = fmaxf(v, 0.f);
-            const long long orow = MODE == DGRAD ? prow(a, row) : (long long)row;
-            if (MODE == DGRAD && a.addend) v += bf2f(a.addend[orow * ldc + col]);
+            if (MODE == DGRAD && a.addend) v += bf2f(a.addend[(long long)row * ldc + col]);
             bf16_t vb = f2bf(v);
             if (MODE == DGRAD && a.bnf_part) {  // consumer BN's dbeta / dgamma partials
-              const long long idx = orow * ldc + col;
+              const long long idx = (long long)row * ldc + col;
               float dz = bf2f(vb);
               if (a.bnf_y && !(bf2f(a.bnf_y[idx]) > 0.f)) {
                 dz = 0.f;
@@ -750,7 +812,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
               s2 += v * v;
             }
             if (stage) sout[(row - m0) * LDO + (col - n0)] = vb;
-            else a.out[orow * ldc + col] = vb;
+            else a.out[(long long)row * ldc + col] = vb;
           }
         }
       if ((MODE == DGRAD && a.bnf_part) || (MODE == FWD && a.stats)) {
@@ -792,7 +854,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
           const int r = q / CPR, c8 = (q - r * CPR) * 8;
           const int row = m0 + r, col = n0 + c8;
           if (row < a.M && col < a.N)
-            *reinterpret_cast<uint4*>(a.out + (MODE == DGRAD ? prow(a, row) : (long long)row) * ldc + col) =
+            *reinterpret_cast<uint4*>(a.out + (long long)row * ldc + col) =
                 *reinterpret_cast<const uint4*>(sout + r * LDO + c8);
         }
       }
@@ -835,9 +897,11 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const Con
 
   // ---- per-thread chunk generators ----
   using GA = typename std::conditional<MODE == FWD, FwdA<BK, TAPU>,
-             typename std::conditional<MODE == DGRAD, DgradA<BK>, WgradA<BK, BM>>::type>::type;
+             typename std::conditional<MODE == DGRAD, typename std::conditional<TAPU, DgradA<BK>, DgradAP<BK>>::type,
+                                       WgradA<BK, BM>>::type>::type;
   using GB = typename std::conditional<MODE == FWD, FwdB<BK, TAPU>,
-             typename std::conditional<MODE == DGRAD, DgradB<BK, BN>, WgradB<BK, BN>>::type>::type;
+             typename std::conditional<MODE == DGRAD, typename std::conditional<TAPU, DgradB<BK, BN>, DgradBP<BK, BN>>::type,
+                                       WgradB<BK, BN>>::type>::type;
   GA ga[PA];
   GB gb[PB];
   int offA[PA], offB[PB];
@@ -1029,9 +1093,11 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   using GA = typename std::conditional<MODE == FWD, FwdA<BK, TAPU>,
-             typename std::conditional<MODE == DGRAD, DgradA<BK>, WgradA<BK, BM>>::type>::type;
+             typename std::conditional<MODE == DGRAD, typename std::conditional<TAPU, DgradA<BK>, DgradAP<BK>>::type,
+                                       WgradA<BK, BM>>::type>::type;
   using GB = typename std::conditional<MODE == FWD, FwdB<BK, TAPU>,
-             typename std::conditional<MODE == DGRAD, DgradB<BK, BN>, WgradB<BK, BN>>::type>::type;
+             typename std::conditional<MODE == DGRAD, typename std::conditional<TAPU, DgradB<BK, BN>, DgradBP<BK, BN>>::type,
+                                       WgradB<BK, BN>>::type>::type;
   GA ga[NA];
   GB gb[NB];
   // Generators are addressed like the register-staged kernel: K-contiguous ones take
@@ -2173,6 +2239,28 @@ int dispatch(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t
   return (int)hipErrorInvalidValue;
 }
 
+// Parity-class DGRAD launches (kml_conv_dgrad_s2): the TAPU = false DGRAD bodies (DgradAP /
+// DgradBP), for the tiles whose epilogue is the row pass (kml_conv_dgrad_s2_ok).
+int dispatch_par(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStream_t s) {
+  dim3 grid((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, 1);
+#define KML_P(BMv, BNv, BKv)                                                                             \
+  if (variant == 0 && bm == BMv && bn == BNv && bk == BKv) {                                             \
+    hipLaunchKernelGGL((k_conv_igemm<DGRAD, BMv, BNv, BKv, false>), grid, dim3(256), 0, s, a);           \
+    return (int)hipGetLastError();                                                                       \
+  }
+#define KML_PG(BMv, BNv, Sv, Vv)                                                                         \
+  if (variant == Vv && bm == BMv && bn == BNv) {                                                         \
+    hipLaunchKernelGGL((k_conv_glds<DGRAD, BMv, BNv, Sv, false>), grid, dim3(256), 0, s, a);             \
+    return (int)hipGetLastError();                                                                       \
+  }
+  KML_P(64, 64, 32) KML_P(64, 64, 64) KML_P(64, 128, 64) KML_P(128, 64, 64) KML_P(128, 128, 64)
+  KML_PG(64, 64, 3, 1) KML_PG(64, 128, 3, 1) KML_PG(128, 64, 3, 1) KML_PG(128, 128, 3, 1)
+  KML_PG(64, 64, 4, 2) KML_PG(64, 128, 4, 2) KML_PG(128, 64, 4, 2)
+#undef KML_P
+#undef KML_PG
+  return (int)hipErrorInvalidValue;
+}
+
 FastDiv make_fd(int d) {
   FastDiv f;
   f.d = d < 1 ? 1 : d;
@@ -2212,7 +2300,6 @@ ConvArgs make_args(int B, int H, int W, int C, int K, int KH, int KW, int sh, in
   a.fd_sh = make_fd(sh);
   a.fd_sw = make_fd(sw);
   a.fd_Kp = make_fd(1);
-  a.tstep = 1;
   return a;
 }
 
@@ -2744,6 +2831,34 @@ KML_API int kml_conv_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, 
 // (1x1/s2: three of four) runs the epilogue alone (addend / zeros, consumer-BN partials).
 // Plain igemm / glds variants, no split-K, no group reduction; bnf_part holds the classes'
 // partial rows back to back (kml_conv_dgrad_s2_rows).
+// Host mirror of conv_epilogue's ROWPASS condition for a DGRAD plan (Body::SMEM formulas of
+// IgemmBody / GldsBody): the parity-class launches need the row-pass epilogue.
+static bool s2_rowpass_ok(int bm, int bn, int bk, int variant) {
+  if (bn % 64 || bm * bn < 4096) return false;
+  long long smem;
+  if (variant == 1 || variant == 2) {
+    smem = (long long)(variant == 1 ? 3 : 4) * (bm + bn) * 64 * 2;
+  } else {
+    const long long ta = (long long)bm * (bk + PADK);
+    const long long tb = (bn == 32 || bn == 64 || bn == 128) ? (long long)bk * bn : (long long)bk * (bn + PADR);
+    smem = 2 * (ta + tb) * 2;
+  }
+  return smem >= 16 + (long long)bm * bn * 4;
+}
+
+KML_API int kml_conv_dgrad_s2_ok(int bm, int bn, int bk, int variant) {
+  // the instantiations of dispatch_par (all of which take the row pass)
+  bool listed = false;
+  if (variant == 0)
+    listed = (bm == 64 && bn == 64 && (bk == 32 || bk == 64)) ||
+             (bk == 64 && ((bm == 64 && bn == 128) || (bm == 128 && bn == 64) || (bm == 128 && bn == 128)));
+  else if (variant == 1)
+    listed = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
+  else if (variant == 2)
+    listed = (bm == 64 && (bn == 64 || bn == 128)) || (bm == 128 && bn == 64);
+  return listed && s2_rowpass_ok(bm, bn, variant ? 64 : bk, variant) ? 1 : 0;
+}
+
 KML_API int kml_conv_dgrad_s2_rows(int B, int H, int W, int bm) {
   int rows = 0;
   for (int c = 0; c < 4; ++c) {
@@ -2758,7 +2873,7 @@ KML_API int kml_conv_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, con
                               const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
                               float* bnf_part, int B, int H, int W, int C, int K, int KH, int KW, int ph, int pw,
                               int bm, int bn, int bk, int variant, int bnf_mask_out, hipStream_t s) {
-  if (variant != 0 && variant != 1 && variant != 2) return (int)hipErrorInvalidValue;
+  if (!kml_conv_dgrad_s2_ok(bm, bn, bk, variant) || (!addend && !bnf_part)) return (int)hipErrorInvalidValue;
   ConvArgs a0;
   int e = prep_dgrad(a0, dy, w, nullptr, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, nullptr, nullptr, 0,
                      B, H, W, C, K, KH, KW, 2, 2, ph, pw, bk, 1, variant, nullptr, nullptr, 0, bnf_mask_out, 0);
@@ -2767,21 +2882,22 @@ KML_API int kml_conv_dgrad_s2(const bf16_t* dy, const bf16_t* w, bf16_t* dx, con
   int rowbase = 0;
   for (int c = 0; c < 4; ++c) {
     ConvArgs a = a0;
-    a.par = 1; a.pa = c >> 1; a.pe = c & 1; a.tstep = 2;
-    const int Hc = (H - a.pa + 1) / 2, Wc = (W - a.pe + 1) / 2;
-    a.fd_Hc = make_fd(Hc > 0 ? Hc : 1); a.fd_Wc = make_fd(Wc > 0 ? Wc : 1);
+    const int pa = c >> 1, pe = c & 1;
+    a.par = 1 | (pa << 1) | (pe << 2);
+    const int Hc = (H - pa + 1) / 2, Wc = (W - pe + 1) / 2;
+    a.fd_H = make_fd(Hc > 0 ? Hc : 1); a.fd_W = make_fd(Wc > 0 ? Wc : 1);
     a.M = B * Hc * Wc;
     if (a.M <= 0) continue;
-    a.r0 = (a.pa + ph) & 1; a.s0 = (a.pe + pw) & 1;
+    a.r0 = (pa + ph) & 1; a.s0 = (pe + pw) & 1;
     const int nr = a.r0 < KH ? (KH - a.r0 + 1) / 2 : 0, ns = a.s0 < KW ? (KW - a.s0 + 1) / 2 : 0;
     a.r1 = a.r0 + 2 * nr; a.s1 = a.s0 + 2 * ns;
     a.fd_nts = make_fd(ns > 0 ? ns : 1);
     a.Kd = nr * ns * a.Kp;
     a.kchunk = a.Kd > 0 ? (a.Kd + bk - 1) / bk * bk : bk;
     a.splits = 1;
-    a.rowbase = rowbase;
+    if (bnf_part) a.bnf_part = bnf_part + (long long)rowbase * 2 * C;
     rowbase += (a.M + bm - 1) / bm;
-    e = dispatch<DGRAD>(a, bm, bn, bk, variant, s);
+    e = dispatch_par(a, bm, bn, bk, variant, s);
     if (e) return e;
   }
   return 0;

@@ -634,7 +634,7 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     if variant == HALO and (_g22 or not halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn)):
         bm, bn, bk, splits, variant = _norm_cfg(plan_conv("dgrad", M, C, ntap * K))
     plan = (bm, bn, bk, splits, variant)
-    if s2_parity_ok(B, H, W, stride, variant, _g22, _fold):
+    if s2_parity_ok(B, H, W, stride, plan, _g22, _fold, operands=addend is not None or bnf is not None):
         part, G = None, 0
         by = bc = bmean = brstd = None
         if bnf is not None:
@@ -674,9 +674,21 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
 _S2_PARITY_MIN_ROWS = 20000
 
 
-def s2_parity_ok(B, H, W, stride, variant, g22=False, fold=0) -> bool:
-    return (tuple(stride) == (2, 2) and variant in (0, 1, 2) and not g22 and not fold
-            and B * H * W >= _S2_PARITY_MIN_ROWS)
+_S2_OK: dict = {}
+
+
+def s2_parity_ok(B, H, W, stride, plan, g22=False, fold=0, operands=True) -> bool:
+    """True when a stride-2 dgrad runs as parity classes: large map, a plain igemm / glds plan
+    whose tile takes the row-pass epilogue, and an addend or consumer-BN operand."""
+    bm, bn, bk, _, variant = plan
+    if not (tuple(stride) == (2, 2) and variant in (0, 1, 2) and not g22 and not fold and operands
+            and B * H * W >= _S2_PARITY_MIN_ROWS):
+        return False
+    key = (bm, bn, bk, variant)
+    ok = _S2_OK.get(key)
+    if ok is None:
+        ok = _S2_OK[key] = bool(HIP.fn("kml_conv_dgrad_s2_ok", "i i i i")(bm, bn, bk, variant))
+    return ok
 
 
 def _bnf_ws(bnf, out, M, C, plan, fold=0):
@@ -797,7 +809,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
-    if grouped and s2_parity_ok(B, H, W, stride, dplan[4], g22, fold):
+    if grouped and s2_parity_ok(B, H, W, stride, dplan, g22, fold, operands=addend is not None or bnf is not None):
         grouped = False
     if dbias is not None and wu is not None:
         raise ValueError("conv_bwd: dbias needs a 1x1 conv")

@@ -1120,7 +1120,7 @@ def test_stride2_dgrad_parity_classes(shape, cfg, monkeypatch):
     same consumer-BN dgamma/dbeta) and the fp32 torch reference; with and without addend."""
     from kubeml_amd.ops import kernels as K
     B, H, W, Ci, Co, k, p = shape
-    assert K.s2_parity_ok(B, H, W, (2, 2), cfg[4])
+    assert K.s2_parity_ok(B, H, W, (2, 2), cfg)
     torch.manual_seed(11)
     OH, OW = K.out_hw(H, W, k, k, 2, 2, p, p)
     dy = _bf(torch.randn(B, OH, OW, Co, device=dev))
