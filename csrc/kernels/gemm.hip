@@ -38,6 +38,10 @@ namespace {
 typedef __attribute__((ext_vector_type(4))) short v4s_t;
 
 constexpr int GEMM_ADD_C2 = 3;  // act code: C = bf16(bf16(A B) + c2)
+// act code (k_gemm8 dgrad only): C = bf16(bf16(A B) * gelu'(c2)) — the FFN's GELU backward in
+// the epilogue of the dgrad that produced d(activation), c2 = the saved pre-activation; the
+// column sums of C (the FFN1 bias gradient) go to colpart[M / 256][N] (one row per M-tile)
+constexpr int GEMM_GELU_BWD = 4;
 
 struct GemmArgs {
   const bf16_t* a;
@@ -52,6 +56,7 @@ struct GemmArgs {
   int act;             // 0 none, 1 erf-GELU
   float beta;
   int kchunk;          // split-K slice length (multiple of 64)
+  float* colpart;      // GEMM_GELU_BWD: per-M-tile column sums of the output
 };
 
 constexpr int BK = 64;
@@ -656,6 +661,8 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       __syncthreads();
     };
     // LDS tile -> 16-byte row-contiguous global stores (512 B per half-wave)
+    const bool gbwd = g.act == GEMM_GELU_BWD;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // GELU_BWD: this thread's 8 columns
     auto store = [&](bf16_t* dst) {
 #pragma unroll 2
       for (int it = 0; it < 16; ++it) {
@@ -664,6 +671,18 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
         uint4 v = *reinterpret_cast<const uint4*>(smem + row * 512 + ((ch ^ (row & 15)) << 4));
         const int m = m0 + row, n = n0 + ch * 8;
         if (m < g.M && n < g.N) {
+          if (gbwd) {  // d(pre) = bf16(bf16(d act) * gelu'(pre)), as k_gelu_bwd_colsum
+            const uint4 pv = *reinterpret_cast<const uint4*>(g.c2 + (long long)m * g.ldc + n);
+            const unsigned dw[4] = {v.x, v.y, v.z, v.w}, pw[4] = {pv.x, pv.y, pv.z, pv.w};
+            unsigned ow[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              ow[k] = pack_bf2(lo_bf(dw[k]) * kml_gelu_grad(lo_bf(pw[k])), hi_bf(dw[k]) * kml_gelu_grad(hi_bf(pw[k])));
+              csum[2 * k] += lo_bf(ow[k]);
+              csum[2 * k + 1] += hi_bf(ow[k]);
+            }
+            v = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          }
           if (g.act == GEMM_ADD_C2) {  // + bf16 addend (the staged tile is already bf16-rounded)
             const uint4 ad = *reinterpret_cast<const uint4*>(g.c2 + (long long)m * g.ldc + n);
             v.x = pack_bf2(lo_bf(v.x) + lo_bf(ad.x), hi_bf(v.x) + hi_bf(ad.x));
@@ -676,12 +695,25 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       }
       __syncthreads();
     };
-    if (g.c2 && g.act != GEMM_ADD_C2) {   // pre-activation copy first: the accumulators stay live across it
+    if (g.c2 && g.act != GEMM_ADD_C2 && !gbwd) {   // pre-activation copy first: the accumulators stay live across it
       stage(false);
       store(g.c2);
     }
     stage(g.act == 1);
     store(static_cast<bf16_t*>(g.c));
+    if (gbwd) {  // column sums: 16 threads (tid >> 5) share each 8-column chunk; fixed order
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[tid * 8 + k] = csum[k];
+      __syncthreads();
+      if (tid < 256) {
+        const int ch = tid >> 3, k = tid & 7, n = n0 + tid;
+        float sum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += red[((r << 5) + ch) * 8 + k];
+        if (n < g.N) g.colpart[(long long)(m0 / 256) * g.N + n] = sum;
+      }
+    }
   }
 }
 
@@ -773,8 +805,9 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   GemmArgs g;
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
-  g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K;
+  g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K; g.colpart = nullptr;
   if (M <= 0 || N <= 0) return 0;
+  if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
   if (layout == 0 && out == 1) return by_tile<true, true, 1>(g, tile, 1, s);
   if (layout == 0 && out == 2) return by_tile<true, true, 2>(g, tile, splits, s);
@@ -783,6 +816,21 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   if (layout == 2 && out == 1) return by_tile<false, false, 1>(g, tile, 1, s);
   if (layout == 2 && out == 2) return by_tile<false, false, 2>(g, tile, splits, s);
   return (int)hipErrorInvalidValue;
+}
+
+// dgrad (layout 1, 256x256 phase tile) with the GELU backward of the layer that produced its
+// operand's forward input in the epilogue: c = bf16(bf16(dy W) * gelu'(pre)), colpart[M/256][N]
+// = per-M-tile column sums of c (summed in order by the caller: the FFN1 bias gradient).
+KML_API int kml_gemm_dgrad_gelu(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, bf16_t* c,
+                                long long ldc, const bf16_t* pre, float* colpart, const bf16_t* zp, int M, int N,
+                                int K, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (N % 8 || ldc % 8 || !pre || !colpart) return (int)hipErrorInvalidValue;
+  GemmArgs g;
+  g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(pre); g.bias = nullptr; g.zp = zp;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.act = GEMM_GELU_BWD; g.beta = 0.f; g.kchunk = K; g.colpart = colpart;
+  return launch8<true, false, 0>(g, 1, s);
 }
 
 // Deterministic split-K weight gradient: dw[M][N] = beta * dw + sum_k A^T B (layout 2), each
@@ -796,7 +844,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   GemmArgs g;
   g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = N;
-  g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K;
+  g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K; g.colpart = nullptr;
   splits = splits < 1 ? 1 : splits;
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;

@@ -53,6 +53,9 @@ class BertLayer(tnn.Module):
         # alone: that Linear's bias gradient is summed inside the LayerNorm backward
         object.__setattr__(self.attention.ln, "_kml_in_linear", self.attention.out)
         object.__setattr__(self.output.LayerNorm, "_kml_in_linear", self.output.dense)
+        # FFN2 is the only consumer of FFN1's GELU output: FFN2's dgrad applies the GELU
+        # backward (and sums FFN1's bias gradient) in its epilogue (nn/modules.py)
+        object.__setattr__(self.output.dense, "_kml_gelu_producer", self.intermediate.dense)
 
     def forward(self, h, B: int, L: int, bias=None):
         # hidden dropout runs inside the LayerNorm kernels (LN(dropout(a) + h))

@@ -181,6 +181,17 @@ class _LinearFn(Function):
         ctx.mod, ctx.x, ctx.has_bias, ctx.act = mod, x2, bias is not None, act
         ctx.y = y if act == 1 else None
         ctx.pre = pre
+        # GELU hand-off (models/bert.py): a Linear declared as this one's sole consumer runs
+        # the GELU backward in its dgrad epilogue; it finds the pre-activation here
+        if pre is not None:
+            object.__setattr__(mod, "_kml_gelu_pre", (y.data_ptr(), pre))
+        ctx.gelu = None
+        prod = getattr(mod, "_kml_gelu_producer", None)
+        if prod is not None and route == "gemm":
+            hand = getattr(prod, "_kml_gelu_pre", None)
+            if hand is not None and hand[0] == x2.data_ptr():
+                ctx.gelu = (prod, hand[1])
+                object.__setattr__(prod, "_kml_gelu_pre", None)
         ctx.keep_pad = keep_pad
         if op != mod.out_features and not keep_pad:
             y = y[:, :mod.out_features].contiguous()
@@ -201,9 +212,13 @@ class _LinearFn(Function):
         if ctx.act == 1:
             dy = K.relu_bwd(dy, ctx.y)
         elif ctx.act == 2:
-            from ..ops import transformer as T
-            # the bias gradient comes out of the GELU backward pass (no column-sum pass)
-            dy = T.gelu_bwd(dy, ctx.pre, dbias=grad_storage_of(mod.bias) if ctx.has_bias else None)
+            if getattr(mod, "_kml_gelu_done", False):
+                # the consumer's dgrad already applied the GELU backward and summed the bias
+                object.__setattr__(mod, "_kml_gelu_done", False)
+            else:
+                from ..ops import transformer as T
+                # the bias gradient comes out of the GELU backward pass (no column-sum pass)
+                dy = T.gelu_bwd(dy, ctx.pre, dbias=grad_storage_of(mod.bias) if ctx.has_bias else None)
             bias_done = ctx.has_bias
         dy4 = dy.view(B, 1, 1, op)
         x4 = ctx.x.view(B, 1, 1, ip)
@@ -232,7 +247,15 @@ class _LinearFn(Function):
             from ..ops import gemm as G
             w2 = shadow_of(mod.weight).view(op, ip)
             if ctx.needs_input_grad[0]:
-                dx = G.linear_dgrad(dy, w2, addend=addend)
+                dx = None
+                if ctx.gelu is not None and addend is None and _GELU_FUSE:
+                    prod, pre = ctx.gelu
+                    dx = G.linear_dgrad_gelu(dy, w2, pre,
+                                             dbias=grad_storage_of(prod.bias) if prod.bias is not None else None)
+                    if dx is not None:
+                        object.__setattr__(prod, "_kml_gelu_done", True)
+                if dx is None:
+                    dx = G.linear_dgrad(dy, w2, addend=addend)
                 addend = None
             G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x)
         elif ctx.needs_input_grad[0]:
@@ -249,8 +272,12 @@ class _LinearFn(Function):
                 K.colsum_(dy, grad_storage_of(mod.bias))
         if addend is not None and dx is not None:
             dx = K.add_bf16(dx, addend)
-        ctx.x = ctx.y = ctx.pre = None
+        ctx.x = ctx.y = ctx.pre = ctx.gelu = None
         return dx, None, None, None, None, None
+
+
+# FFN1 -> FFN2: FFN2's dgrad epilogue applies FFN1's GELU backward (ops.gemm.linear_dgrad_gelu)
+_GELU_FUSE = True
 
 
 class Linear(tnn.Module):

@@ -175,6 +175,30 @@ def linear_dgrad(dy, w, addend=None):
     return dx
 
 
+def linear_dgrad_gelu(dy, w, pre, dbias=None):
+    """dx = bf16(bf16(dy @ w) * gelu'(pre)) in the dgrad epilogue — the GELU backward of the
+    layer whose output this linear consumed (FFN1 -> FFN2), and ``dbias`` (fp32) += column
+    sums of dx (FFN1's bias gradient).  Only for shapes whose plan is the 256x256 phase tile
+    without split-K; returns None otherwise (the caller runs the separate GELU backward)."""
+    T, op = dy.shape
+    ip = w.shape[1]
+    tile, splits = plan(1, T, ip, op)
+    if TILES.get(tuple(tile)) != 6 or splits != 1 or ip % 8 or tuple(pre.shape) != (T, ip):
+        return None
+    _check(dy, BF16, "dy")
+    _check(w, BF16, "w")
+    _check(pre, BF16, "pre")
+    dx = torch.empty((T, ip), dtype=BF16, device=dy.device)
+    colpart = torch.empty((_cdiv(T, 256), ip), dtype=F32, device=dy.device)
+    HIP.call("kml_gemm_dgrad_gelu", "p l p l p l p p p i i i s", dy.data_ptr(), int(op), w.data_ptr(), int(ip),
+             dx.data_ptr(), int(ip), pre.data_ptr(), colpart.data_ptr(), _zp(dy.device).data_ptr(), int(T), int(ip),
+             int(op), stream_ptr())
+    if dbias is not None:
+        from . import kernels as KK
+        KK.slab_sum_add_(colpart, dbias)
+    return dx
+
+
 def linear_wgrad_(dw, dy, x):
     """dw[op, ip] (fp32) += dy[T, op]^T @ x[T, ip]."""
     T, op = dy.shape

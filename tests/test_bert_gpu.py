@@ -113,3 +113,56 @@ def test_bert_fused_residual_and_bias_gradients_match_unfused(dropout):
     for n in p0:
         if n.endswith("bias"):
             assert _rel(p1[n], p0[n]) < 1e-2, (n, _rel(p1[n], p0[n]))
+
+
+def test_bert_ffn_gelu_backward_in_dgrad_epilogue_matches_unfused(monkeypatch):
+    """FFN2's dgrad applying FFN1's GELU backward and summing FFN1's bias gradient in its
+    epilogue (modules._GELU_FUSE, the 256x256 phase tile) == the separate GELU backward pass:
+    same loss, the same weight gradients, bias gradients to fp32 summation order."""
+    from kubeml_amd.models.bert import bert_tiny_mlm
+    from kubeml_amd.nn import flatten_module
+    from kubeml_amd.nn import modules as MO
+    from kubeml_amd.nn import transformer as TR
+    from kubeml_amd.ops import gemm as G
+    orig = G.plan
+
+    def plan(layout, M, N, K):   # force the phase tile on the tiny model's FFN2 dgrad
+        if layout == 1 and N % 256 == 0 and N > K:
+            return (256, 256, 8), 1
+        return orig(layout, M, N, K)
+    monkeypatch.setattr(G, "plan", plan)
+    calls = []
+    real = G.linear_dgrad_gelu
+
+    def spy(*a, **k):
+        r = real(*a, **k)
+        calls.append(r is not None)
+        return r
+    monkeypatch.setattr(G, "linear_dgrad_gelu", spy)
+    # large enough for the gemm.hip route of every Linear (>= 2048 tokens, >= 256 features)
+    ids, tt, pos, lab, mask = _data(16, 128, 20, 1000, seed=4)
+    out = []
+    old = MO._GELU_FUSE
+    try:
+        for fuse in (False, True):
+            MO._GELU_FUSE = fuse
+            torch.manual_seed(0)
+            TR.Dropout._salt = 0
+            m = bert_tiny_mlm(dropout=0.1, hidden=256, inter=1024, heads=4).to(dev)
+            sp = flatten_module(m)
+            m.train()
+            sp.zero_grad()
+            loss = m(ids.to(dev), tt.to(dev), mask.to(dev), pos.to(dev), lab.to(dev))
+            loss.backward()
+            torch.cuda.synchronize()
+            out.append((float(loss), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    finally:
+        MO._GELU_FUSE = old
+    assert calls and all(calls), calls
+    (l0, p0), (l1, p1) = out
+    assert l1 == l0
+    for n in p0:
+        if n.endswith("bias") or "embeddings" in n:   # fp32 order / atomic scatter-adds
+            assert _rel(p1[n], p0[n]) < 1e-3, (n, _rel(p1[n], p0[n]))
+        else:
+            assert torch.equal(p1[n], p0[n]), n
