@@ -544,6 +544,15 @@ KML_API int kml_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* x, bf16_t* dx, f
   KML_LAUNCH_CHECK();
 }
 
+// out[c] += sum_g part[g][c] for part [G][N] fp32 (fixed row order; k_colreduce: 64 columns x
+// 4 row slices per block) — e.g. the per-M-tile column sums of a GEMM epilogue
+KML_API int kml_colreduce_add(const float* part, int G, int N, float* out, hipStream_t s) {
+  if (G < 1 || N < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_colreduce, dim3((N + 63) / 64), dim3(256), 0, s, part, G, N, N, out, (float*)nullptr, 0,
+                     (float*)nullptr);
+  KML_LAUNCH_CHECK();
+}
+
 KML_API int kml_dropout(const bf16_t* x, bf16_t* y, const float* ctr, unsigned salt, float p, long long n,
                         hipStream_t s) {
   if (n % 8 || p < 0.f || p >= 1.f) return (int)hipErrorInvalidValue;

@@ -194,8 +194,9 @@ def linear_dgrad_gelu(dy, w, pre, dbias=None):
              dx.data_ptr(), int(ip), pre.data_ptr(), colpart.data_ptr(), _zp(dy.device).data_ptr(), int(T), int(ip),
              int(op), stream_ptr())
     if dbias is not None:
-        from . import kernels as KK
-        KK.slab_sum_add_(colpart, dbias)
+        _check(dbias, F32, "dbias")
+        HIP.call("kml_colreduce_add", "p i i p s", colpart.data_ptr(), int(colpart.shape[0]), int(ip),
+                 dbias.data_ptr(), stream_ptr())
     return dx
 
 

@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r4
 mkdir -p $out
-timeout -k 10 400 python -u -m pytest tests/test_bert_gpu.py tests/test_transformer_gpu.py -x -q --timeout 120 --timeout-method thread > $out/r23_tests.log 2>&1 || { tail -30 $out/r23_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_bert_gpu.py tests/test_transformer_gpu.py tests/test_kernels_gpu.py -k "bert or attention or layernorm or ln or gelu or adam or sgd or optim" -x -q --timeout 120 --timeout-method thread > $out/r23_tests.log 2>&1 || { tail -30 $out/r23_tests.log; exit 1; }
 tail -1 $out/r23_tests.log
 timeout -k 10 300 python -u tools/bench_bert.py > $out/bert_r23.json 2> $out/bert_r23.err || { tail -20 $out/bert_r23.err; exit 1; }
 python -c "import json;d=json.load(open('$out/bert_r23.json'));print('bert', d['value'], d['ms_per_step'])"
