@@ -1,0 +1,10 @@
+#!/bin/bash
+# full GPU suite at HEAD + driver smoke
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r4
+mkdir -p $out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/gpu_suite.log 2>&1 || { tail -40 $out/gpu_suite.log; exit 1; }
+tail -3 $out/gpu_suite.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
