@@ -224,8 +224,12 @@ class _LinearFn(Function):
         x4 = ctx.x.view(B, 1, 1, ip)
         if ctx.route == "conv":          # implicit-GEMM wgrad: stores or adds, deterministic
             dwst, wacc = grad_out(mod.weight)
-        else:                            # gemm.hip / hipBLASLt wgrad: adds
-            dwst, wacc = grad_storage_of(mod.weight), True
+        else:
+            from ..ops import gemm as G
+            if G.wgrad_can_store(op, ip, B):   # slab split-K / one pass: stores the first write
+                dwst, wacc = grad_out(mod.weight)
+            else:                              # fp32-atomic split-K: adds only
+                dwst, wacc = grad_storage_of(mod.weight), True
         dw4 = dwst.view(op, 1, 1, ip)
         # implicit-GEMM route: the bias gradient is one more column of the wgrad GEMM (a ones
         # column in its input operand) — no column-sum pass
@@ -257,7 +261,7 @@ class _LinearFn(Function):
                 if dx is None:
                     dx = G.linear_dgrad(dy, w2, addend=addend)
                 addend = None
-            G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x)
+            G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x, accumulate=wacc)
         elif ctx.needs_input_grad[0]:
             # dgrad + wgrad as one grouped launch
             w = shadow_of(mod.weight).view(op, 1, 1, ip)

@@ -200,8 +200,17 @@ def linear_dgrad_gelu(dy, w, pre, dbias=None):
     return dx
 
 
-def linear_wgrad_(dw, dy, x):
-    """dw[op, ip] (fp32) += dy[T, op]^T @ x[T, ip]."""
+def wgrad_can_store(op, ip, T) -> bool:
+    """True if linear_wgrad_ for this shape can overwrite dw (slab split-K or a single pass:
+    dw = 0 * dw + ...); False for the fp32-atomic split-K form, which only adds."""
+    tile, splits = plan(2, op, ip, T)
+    return len(tile) == 4 or splits <= 1
+
+
+def linear_wgrad_(dw, dy, x, accumulate=True):
+    """dw[op, ip] (fp32) += dy[T, op]^T @ x[T, ip]; ``accumulate=False`` overwrites dw (the
+    first gradient write of a step: the region needs no zeroing, and the reduce never reads
+    it) — only where :func:`wgrad_can_store`."""
     T, op = dy.shape
     ip = x.shape[1]
     if tuple(dw.shape) != (op, ip) or x.shape[0] != T:
@@ -209,7 +218,10 @@ def linear_wgrad_(dw, dy, x):
     if not dw.is_contiguous():
         raise ValueError("linear_wgrad_: dw must be contiguous")
     tile, splits = plan(2, op, ip, T)
+    beta = 1.0 if accumulate else 0.0
     if len(tile) == 4:    # (BM, BN, stages, "slab"): deterministic slab split-K
-        return wgrad_splitk_(dw, dy, op, x, ip, op, ip, T, beta=1.0, tile=tile[:3], splits=splits)
-    gemm(dy, op, x, ip, dw, ip, op, ip, T, 2, 2 if splits > 1 else 1, beta=1.0, tile=tile, splits=splits)
+        return wgrad_splitk_(dw, dy, op, x, ip, op, ip, T, beta=beta, tile=tile[:3], splits=splits)
+    if splits > 1 and not accumulate:
+        raise ValueError("linear_wgrad_: the atomic split-K form only accumulates")
+    gemm(dy, op, x, ip, dw, ip, op, ip, T, 2, 2 if splits > 1 else 1, beta=beta, tile=tile, splits=splits)
     return dw
