@@ -50,6 +50,8 @@ __device__ __forceinline__ void drop4(float* v, long long e, const float* ctr, u
 
 // ------------------------------------------------------------------------------ LayerNorm fwd
 // y = LN(x [+ res]) * g + b ; sum_out (optional) = x + res (the LN input, kept for backward)
+// One wave per row; NV = ceil(N / 256) register vectors (compile time: 3 for a 768-wide row).
+template <int NV>
 __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 bf16_t* __restrict__ y, bf16_t* __restrict__ sum_out,
@@ -60,20 +62,25 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, co
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const bf16_t* xr = x + row * N;
-  const int nv = N / 256 + ((N % 256) > 0);
-  float v[MAXV][4];
+  float v[NV][4];
+  uint2 rv[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {  // all loads first
+    const int c = (u * 64 + lane) * 4;
+    if (c < N) {
+      const uint2 xv = *reinterpret_cast<const uint2*>(xr + c);
+      v[u][0] = lo_bf(xv.x); v[u][1] = hi_bf(xv.x); v[u][2] = lo_bf(xv.y); v[u][3] = hi_bf(xv.y);
+      if (res) rv[u] = *reinterpret_cast<const uint2*>(res + row * N + c);
+    }
+  }
   float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < MAXV; ++u) {
+  for (int u = 0; u < NV; ++u) {
     const int c = (u * 64 + lane) * 4;
-    if (u < nv && c < N) {
-      ld4(xr + c, v[u]);
+    if (c < N) {
       if (dctr) drop4(v[u], row * N + c, dctr, dsalt, dp);  // x = dropout(x), as k_dropout
       if (res) {
-        float r[4];
-        ld4(res + row * N + c, r);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[u][k] += r[k];
+        v[u][0] += lo_bf(rv[u].x); v[u][1] += hi_bf(rv[u].x); v[u][2] += lo_bf(rv[u].y); v[u][3] += hi_bf(rv[u].y);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) s += v[u][k];
@@ -83,18 +90,18 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const bf16_t* __restrict__ x, co
   const float mu = s / N;
   float q = 0.f;
 #pragma unroll
-  for (int u = 0; u < MAXV; ++u) {
+  for (int u = 0; u < NV; ++u) {
     const int c = (u * 64 + lane) * 4;
-    if (u < nv && c < N)
+    if (c < N)
 #pragma unroll
       for (int k = 0; k < 4; ++k) { const float d = v[u][k] - mu; q += d * d; }
   }
   q = wave_sum(q);
   const float rs = rsqrtf(q / N + eps);
 #pragma unroll
-  for (int u = 0; u < MAXV; ++u) {
+  for (int u = 0; u < NV; ++u) {
     const int c = (u * 64 + lane) * 4;
-    if (u < nv && c < N) {
+    if (c < N) {
       if (sum_out) st4(sum_out + row * N + c, v[u]);
       float o[4];
 #pragma unroll
@@ -468,8 +475,13 @@ KML_API int kml_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, c
                        unsigned dsalt, float dp, hipStream_t s) {
   if (N % 4 || N > 64 * 4 * MAXV) return (int)hipErrorInvalidValue;
   if (dctr && (dp < 0.f || dp >= 1.f)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ln_fwd, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, res, gamma, beta, y, sum_out, mean,
-                     rstd, M, N, eps, dctr, dsalt, dp);
+  const int nv = (N + 255) / 256;
+#define KML_LNF(NVv)                                                                                           \
+  if (nv == NVv)                                                                                               \
+    hipLaunchKernelGGL(k_ln_fwd<NVv>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, res, gamma, beta, y, \
+                       sum_out, mean, rstd, M, N, eps, dctr, dsalt, dp);
+  KML_LNF(1) KML_LNF(2) KML_LNF(3) KML_LNF(4) KML_LNF(5) KML_LNF(6) KML_LNF(7) KML_LNF(8)
+#undef KML_LNF
   KML_LAUNCH_CHECK();
 }
 
