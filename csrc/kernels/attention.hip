@@ -53,40 +53,7 @@ struct AttnArgs {
   float pdrop;         // dropout probability (0: off)
   int xcd;             // XCD-aware block order (attn_blk); 0: plain grid order (A/B switch)
   unsigned char* keep; // dropout keep bits written by the forward, read by the backward (Drop), or null
-  // backward (optional): per-64-row-tile column sums of the bf16 dQ | dK | dV it stores,
-  // [B * ceil(L/64)][3 * H * 64] — the bias gradient of the fused QKV Linear without a
-  // column-sum pass over the [B*L, 3*H*64] gradient (one row per (batch, row tile))
-  float* colpart;
 };
-
-// Column sums of the 64 x 64 bf16 tile a backward block stores: lane (row 16w + (lane & 15),
-// columns 16d + 4g + e) -> butterfly over the 16 rows of the wave, the 4 waves through LDS
-// (fixed order), one row of 64 floats at dst.  vals = the values exactly as stored (bf16).
-__device__ __forceinline__ void tile_colsum(const f32x4_t (&acc)[4], float sc, bool ok, int lane, int w,
-                                            float (*red)[64], float* dst) {
-  const int g = lane >> 4;
-  float cs[4][4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float v = ok ? __uint_as_float(((unsigned)f2bf(acc[d][e] * sc)) << 16) : 0.f;
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      cs[d][e] = v;
-    }
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[w][16 * d + 4 * g + e] = cs[d][e];
-  }
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < 64) dst[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-}
 
 __device__ __forceinline__ unsigned ahash(unsigned a, unsigned b, unsigned c) {
   unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ c * 0xC2B2AE3Du;
@@ -490,12 +457,6 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) store4(op + 16 * d + 4 * g, acc[d], a.scale);
   }
-  if (a.colpart) {
-    __shared__ float red[4][64];
-    const int nqb = (L + 63) / 64;
-    tile_colsum(acc, a.scale, qok, lane, w, red,
-                a.colpart + (long long)(b * nqb + xt) * (3 * a.H * 64) + h * 64);
-  }
 }
 
 // ------------------------------------------------------------------------------ backward: dK, dV
@@ -623,13 +584,6 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
       store4(vp + 16 * d + 4 * g, adv[d], drop.sc);
     }
   }
-  if (a.colpart) {
-    __shared__ float red[4][64];
-    float* row = a.colpart + (long long)(b * nqb + xt) * (3 * a.H * 64);
-    tile_colsum(adk, a.scale, kok, lane, w, red, row + (a.H + h) * 64);
-    __syncthreads();
-    tile_colsum(adv, drop.sc, kok, lane, w, red, row + (2 * a.H + h) * 64);
-  }
 }
 
 bool aligned16(const void* p) { return (((unsigned long long)p) & 15ull) == 0; }
@@ -661,11 +615,10 @@ KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
                          const float* lse, float* dsum, const float* bias, bf16_t* dq, bf16_t* dk, bf16_t* dv,
                          int ldq, int ldk, int ldv, int ldo, int lddo, int lddq, int lddk, int lddv, int B, int H,
                          int L, float scale, const float* ctr, int salt, float pdrop, const unsigned char* keep,
-                         float* colpart, hipStream_t s) {
+                         hipStream_t s) {
   if (L <= 0 || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 8 || lddo % 8 || lddq % 4 || lddk % 4 || lddv % 4)
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
-  a.colpart = colpart;
   a.q = q; a.k = k; a.v = v; a.o = o; a.dout = dout; a.lse = const_cast<float*>(lse); a.dsum = dsum;
   a.bias = bias; a.dq = dq; a.dk = dk; a.dv = dv;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;

@@ -175,12 +175,9 @@ class Dropout(tnn.Module):
 # ====================================================================================== attention
 class _AttnFn(Function):
     @staticmethod
-    def forward(ctx, qkv, B, H, L, bias, drop=None, qkv_lin=None):
+    def forward(ctx, qkv, B, H, L, bias, drop=None):
         from ..ops import transformer as T
         D = H * 64
-        # qkv_lin: the Linear that produced qkv (its only consumer is this node): the
-        # backward kernels sum its bias gradient (column sums of dqkv) as they store dqkv
-        ctx.qkv_lin = qkv_lin
         q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
         keep = T.attn_keep_buffer(B, H, L, qkv.device) if drop is not None and drop[2] > 0.0 else None
         out, lse = T.attn_fwd(q, k, v, B, H, L, bias=bias, drop=drop, keep=keep)
@@ -196,21 +193,10 @@ class _AttnFn(Function):
         B, H, L = ctx.dims
         D = H * 64
         dqkv = torch.empty_like(qkv)
-        lin, colpart = ctx.qkv_lin, None
-        if lin is not None and lin.bias is not None and _QKV_BIAS_FUSE and qkv.shape[1] == 3 * D:
-            colpart = torch.empty((B * (-(-L // 64)), 3 * D), dtype=torch.float32, device=qkv.device)
         T.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, _bf(dout).contiguous(), lse, B, H, L, bias=bias,
-                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=ctx.drop, keep=keep,
-                   colpart=colpart)
-        if colpart is not None:
-            T.colreduce_add_(colpart, grad_storage_of(lin.bias))
-            object.__setattr__(lin, "_kml_bias_done", True)   # the Linear's backward skips its column sum
-        ctx.save = ctx.qkv_lin = None
-        return dqkv, None, None, None, None, None, None
-
-
-# the fused QKV Linear's bias gradient from the attention backward kernels (no column-sum pass)
-_QKV_BIAS_FUSE = True
+                   dq=dqkv[:, :D], dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=ctx.drop, keep=keep)
+        ctx.save = None
+        return dqkv, None, None, None, None, None
 
 
 def attention_reference(qkv, B, H, L, bias=None, keep=None):
@@ -294,7 +280,7 @@ class SelfAttention(tnn.Module):
             drop = None
             if self.training and self.attn_dropout > 0:
                 drop = (self.rng.tensor(x.device), self.salt, self.attn_dropout)
-            ctx = _AttnFn.apply(qkv.contiguous(), B, self.heads, L, bias, drop, self.qkv)
+            ctx = _AttnFn.apply(qkv.contiguous(), B, self.heads, L, bias, drop)
         return self.out(ctx)
 
 

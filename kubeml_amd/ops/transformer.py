@@ -79,11 +79,9 @@ def attn_fwd(q, k, v, B, H, L, bias=None, out=None, scale=None, drop=None, keep=
 
 
 def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=None, scale=None, drop=None,
-             keep=None, colpart=None):
+             keep=None):
     """Gradients of attention; dq/dk/dv may be column views of one [B*L, 3*H*64] buffer.
-    keep: the keep-bit buffer the forward filled (same drop), or None to re-hash the mask.
-    colpart: optional fp32 [B * ceil(L/64), 3*H*64] that receives per-row-tile column sums of
-    the stored dQ | dK | dV (the fused QKV Linear's bias gradient, summed by the caller)."""
+    keep: the keep-bit buffer the forward filled (same drop), or None to re-hash the mask."""
     dev = q.device
     if dq is None:
         dq = torch.empty((B * L, H * 64), dtype=BF16, device=dev)
@@ -100,22 +98,11 @@ def attn_bwd(q, k, v, o, dout, lse, B, H, L, bias=None, dq=None, dk=None, dv=Non
     dsum = torch.empty((B * H, L), dtype=F32, device=dev)
     scale = 1.0 / math.sqrt(64) if scale is None else scale
     c, salt, pd = _drop_args(drop)
-    if colpart is not None and (colpart.dtype != F32 or colpart.numel() != B * (-(-L // 64)) * 3 * H * 64
-                                or not colpart.is_contiguous()):
-        raise ValueError("colpart must be a contiguous fp32 [B * ceil(L/64), 3*H*64] tensor")
-    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f p i f p p s",
+    HIP.call("kml_attn_bwd", "p p p p p p p p p p p i i i i i i i i i i i f p i f p s",
              _p(q), _p(k), _p(v), _p(o), _p(dout), _p(lse), _p(dsum), _p(bias), _p(dq), _p(dk), _p(dv),
              q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
-             dv.stride(0), B, H, L, float(scale), c, salt, pd, _keep_arg(keep, B, H, L, drop), _p(colpart), _s())
+             dv.stride(0), B, H, L, float(scale), c, salt, pd, _keep_arg(keep, B, H, L, drop), _s())
     return dq, dk, dv
-
-
-def colreduce_add_(part, out):
-    """out (fp32 [N]) += part.sum(0) for part fp32 [G, N], rows summed in order."""
-    if part.dtype != F32 or out.dtype != F32 or part.shape[-1] != out.numel():
-        raise ValueError("colreduce_add_: fp32 [G, N] part and [N] out")
-    HIP.call("kml_colreduce_add", "p i i p s", _p(part), int(part.shape[0]), int(part.shape[1]), _p(out), _s())
-    return out
 
 
 def ln_fwd(x, gamma, beta, res=None, eps=1e-12, keep_sum=True, drop=None):

@@ -166,51 +166,3 @@ def test_bert_ffn_gelu_backward_in_dgrad_epilogue_matches_unfused(monkeypatch):
             assert _rel(p1[n], p0[n]) < 1e-3, (n, _rel(p1[n], p0[n]))
         else:
             assert torch.equal(p1[n], p0[n]), n
-
-
-def test_attention_backward_column_sums_equal_qkv_bias_gradient():
-    """attn_bwd(colpart=...) rows sum to the column sums of the stored dQ | dK | dV (the QKV
-    Linear's bias gradient), and the model with the fusion matches the one without."""
-    from kubeml_amd.models.bert import bert_tiny_mlm
-    from kubeml_amd.nn import flatten_module
-    from kubeml_amd.nn import transformer as TR
-    from kubeml_amd.ops import transformer as T
-    torch.manual_seed(5)
-    B, H, L = 2, 2, 100
-    D = H * 64
-    qkv = (torch.randn(B * L, 3 * D, device=dev) * 0.5).to(torch.bfloat16)
-    dout = torch.randn(B * L, D, device=dev).to(torch.bfloat16)
-    ctr = torch.tensor([3.0, 1.0], device=dev)
-    drop = (ctr, 7919, 0.1)
-    keep = T.attn_keep_buffer(B, H, L, dev)
-    out, lse = T.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], B, H, L, drop=drop, keep=keep)
-    dqkv = torch.empty_like(qkv)
-    colpart = torch.full((B * 2, 3 * D), float("nan"), device=dev)
-    T.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], out, dout, lse, B, H, L, dq=dqkv[:, :D],
-               dk=dqkv[:, D:2 * D], dv=dqkv[:, 2 * D:], drop=drop, keep=keep, colpart=colpart)
-    torch.cuda.synchronize()
-    assert not torch.isnan(colpart).any()
-    ref = dqkv.float().sum(0)
-    assert _rel(colpart.sum(0), ref) < 1e-5, _rel(colpart.sum(0), ref)
-    grads = []
-    old = TR._QKV_BIAS_FUSE
-    ids, tt, pos, lab, mask = _data(2, 128, 20, 1000, seed=6)
-    try:
-        for fuse in (False, True):
-            TR._QKV_BIAS_FUSE = fuse
-            torch.manual_seed(0)
-            TR.Dropout._salt = 0
-            m = bert_tiny_mlm(dropout=0.1).to(dev)
-            sp = flatten_module(m)
-            m.train()
-            sp.zero_grad()
-            m(ids.to(dev), tt.to(dev), mask.to(dev), pos.to(dev), lab.to(dev)).backward()
-            torch.cuda.synchronize()
-            grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
-    finally:
-        TR._QKV_BIAS_FUSE = old
-    for n in grads[0]:
-        if "qkv.bias" in n:
-            assert _rel(grads[1][n], grads[0][n]) < 1e-3, n
-        elif "embeddings" not in n:
-            assert torch.equal(grads[1][n], grads[0][n]), n
