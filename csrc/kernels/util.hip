@@ -178,6 +178,20 @@ __global__ void k_add_i64(long long* __restrict__ p, long long v, int n) {
   if (i < n) p[i] += v;
 }
 
+// flat row index of (batch b, position pos[b][j]) in a [B*L] token-major tensor: out = b*L + pos
+__global__ void k_row_index(const long long* __restrict__ pos, long long* __restrict__ out, int P, long long L,
+                            int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (long long)(i / P) * L + pos[i];
+}
+
+KML_API int kml_row_index(const long long* pos, long long* out, int B, int P, long long L, hipStream_t s) {
+  const int n = B * P;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_row_index, dim3((n + 255) / 256), dim3(256), 0, s, pos, out, P, L, n);
+  KML_LAUNCH_CHECK();
+}
+
 KML_API int kml_add_i64(long long* p, long long v, int n, hipStream_t s) {
   hipLaunchKernelGGL(k_add_i64, dim3((n + 255) / 256), dim3(256), 0, s, p, v, n);
   KML_LAUNCH_CHECK();

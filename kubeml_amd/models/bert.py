@@ -156,9 +156,11 @@ class BertForMaskedLM(tnn.Module):
             self.rng.advance(ids.device)
         h = self.bert(ids, token_type_ids, attention_mask)
         if mlm_positions is not None:
-            P = mlm_positions.shape[1]
-            base = (torch.arange(B, device=ids.device) * L).view(B, 1)
-            idx = (mlm_positions + base).reshape(-1).contiguous()
+            if ids.is_cuda:
+                from ..ops import kernels as K
+                idx = K.row_index(mlm_positions, L)      # one kernel (no arange / mul / add)
+            else:
+                idx = (mlm_positions + (torch.arange(B, device=ids.device) * L).view(B, 1)).reshape(-1)
             h = gather_rows(h, idx)
         t = self.cls.predictions.transform
         z = t.LayerNorm(t.dense(h, act="gelu"))
@@ -204,8 +206,8 @@ class BertForMaskedLM(tnn.Module):
             for lay in groups[-1]:
                 h = lay(h, B, L, bias)
             if mlm_positions is not None:
-                base = (torch.arange(B, device=ids.device) * L).view(B, 1)
-                h = gather_rows(h, (mlm_positions + base).reshape(-1).contiguous())
+                from ..ops import kernels as K
+                h = gather_rows(h, K.row_index(mlm_positions, L))
             t = self.cls.predictions.transform
             z = t.LayerNorm(t.dense(h, act="gelu"))
             return cross_entropy(self.cls.predictions.decoder(z, keep_pad=True), labels.reshape(-1),

@@ -1340,6 +1340,17 @@ def slab_sum_add_(part, dst):
     return dst
 
 
+def row_index(pos, L):
+    """int64 [B*P]: b * L + pos[b, j] (flat token rows of per-sequence positions), one launch."""
+    if pos.dtype != torch.int64 or pos.dim() != 2:
+        raise TypeError("row_index: int64 [B, P] positions")
+    pos = pos.contiguous()
+    B, P = pos.shape
+    out = torch.empty(B * P, dtype=torch.int64, device=pos.device)
+    HIP.call("kml_row_index", "p p i i l s", _p(pos), _p(out), B, P, int(L), _s())
+    return out
+
+
 def add_i64_(t, v=1):
     HIP.call("kml_add_i64", "p l i s", _p(t), int(v), t.numel(), _s())
 
