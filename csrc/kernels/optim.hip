@@ -269,6 +269,62 @@ __global__ void k_kavg_finish(float* __restrict__ state, long long n_params, lon
   }
 }
 
+// Staleness-1 K-AVG (parallel/kavg.py AsyncModelAverager), two passes per round instead of six:
+// launch: flat := x, snap := x (one read, two writes; flat then goes into the async SUM);
+// apply:  x := x + (flat / world - snap), the bf16 shadow of the parameter range refreshed in
+// the same pass (same arithmetic order as the torch div / sub / add it replaces).
+__global__ void k_kavg_snap(const float* __restrict__ x, float* __restrict__ flat, float* __restrict__ snap,
+                            long long n) {
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<float4*>(flat)[i] = v;
+    reinterpret_cast<float4*>(snap)[i] = v;
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    flat[i] = x[i];
+    snap[i] = x[i];
+  }
+}
+
+__global__ void k_kavg_async_apply(float* __restrict__ x, const float* __restrict__ flat,
+                                   const float* __restrict__ snap, bf16_t* __restrict__ shadow, float world,
+                                   long long n, long long n_params) {
+  const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<float4*>(x)[i];
+    const float4 f = reinterpret_cast<const float4*>(flat)[i], sn = reinterpret_cast<const float4*>(snap)[i];
+    v.x += f.x / world - sn.x; v.y += f.y / world - sn.y; v.z += f.z / world - sn.z; v.w += f.w / world - sn.w;
+    reinterpret_cast<float4*>(x)[i] = v;
+    if (shadow && 4 * i + 3 < n_params) {
+      uint2 sh;
+      sh.x = pack_bf2(v.x, v.y);
+      sh.y = pack_bf2(v.z, v.w);
+      reinterpret_cast<uint2*>(shadow)[i] = sh;
+    } else if (shadow) {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int k = 0; k < 4; ++k)
+        if (4 * i + k < n_params) shadow[4 * i + k] = f2bf(vv[k]);
+    }
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    x[i] += flat[i] / world - snap[i];
+    if (shadow && i < n_params) shadow[i] = f2bf(x[i]);
+  }
+}
+
+KML_API int kml_kavg_snap(const float* x, float* flat, float* snap, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_kavg_snap, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, x, flat, snap, n);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_kavg_async_apply(float* x, const float* flat, const float* snap, bf16_t* shadow, float world,
+                                 long long n, long long n_params, hipStream_t s) {
+  hipLaunchKernelGGL(k_kavg_async_apply, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, x, flat, snap,
+                     shadow, world, n, n_params);
+  KML_LAUNCH_CHECK();
+}
+
 KML_API int kml_kavg_pack(float* state, const long long* i64, long long i64_off, int n_i64, long long count_idx,
                           int participate, hipStream_t s) {
   const int n = n_i64 > 1 ? n_i64 : 1;

@@ -1297,6 +1297,28 @@ def kavg_finish_(state, n_params, count_idx, shadow, i64, i64_off, n_i64):
              int(i64_off), int(n_i64), _s())
 
 
+def kavg_snap_(x, flat, snap):
+    """flat := x and snap := x (fp32, one pass): the staleness-1 K-AVG round launch."""
+    for t, n in ((x, "x"), (flat, "flat"), (snap, "snap")):
+        _chk(t, F32, n)
+    if not (x.numel() == flat.numel() == snap.numel()):
+        raise ValueError("kavg_snap_: size mismatch")
+    HIP.call("kml_kavg_snap", "p p p l s", _p(x), _p(flat), _p(snap), x.numel(), _s())
+
+
+def kavg_async_apply_(x, flat, snap, shadow, world, n_params):
+    """x += flat / world - snap (the in-flight average replaces the stale base), the bf16
+    shadow of x[:n_params] refreshed in the same pass."""
+    for t, n in ((x, "x"), (flat, "flat"), (snap, "snap")):
+        _chk(t, F32, n)
+    if not (x.numel() == flat.numel() == snap.numel()) or n_params > x.numel():
+        raise ValueError("kavg_async_apply_: size mismatch")
+    if shadow is not None and (shadow.dtype != BF16 or shadow.numel() < n_params):
+        raise ValueError("kavg_async_apply_: shadow must be bf16 covering the parameters")
+    HIP.call("kml_kavg_async_apply", "p p p p f l l s", _p(x), _p(flat), _p(snap), _p(shadow), float(world),
+             x.numel(), int(n_params), _s())
+
+
 # --------------------------------------------------------------------------------------
 # data
 # --------------------------------------------------------------------------------------

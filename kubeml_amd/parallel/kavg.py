@@ -225,6 +225,7 @@ class AsyncModelAverager(ModelAverager):
         super().__init__(module)
         self._pending = None      # (work | None, send, snap, tensors)
         self.rounds_overlapped = 0
+        self._bufs = None         # (flat, snap) reused across rounds (flat-space GPU path)
 
     def _tensors(self):
         sp = self._space()
@@ -256,8 +257,17 @@ class AsyncModelAverager(ModelAverager):
         t0 = time.perf_counter()
         ts, sp = self._tensors()
         self._apply_pending(comm, ts, sp)
-        flat = torch.cat([t.reshape(-1).float() for t in ts]) if len(ts) > 1 else ts[0].detach().clone()
-        snap = flat.clone()
+        if sp is not None and ts[0].is_cuda:
+            # one fused pass (ops.kernels.kavg_snap_) into two round buffers kept across rounds
+            x = ts[0]
+            if self._bufs is None or self._bufs[0].numel() != x.numel():
+                self._bufs = (torch.empty_like(x), torch.empty_like(x))
+            flat, snap = self._bufs
+            from ..ops import kernels as K
+            K.kavg_snap_(x, flat, snap)
+        else:
+            flat = torch.cat([t.reshape(-1).float() for t in ts]) if len(ts) > 1 else ts[0].detach().clone()
+            snap = flat.clone()
         work = self._launch(comm, flat)
         self._pending = (work, flat, snap)
         self.rounds_overlapped += 1
@@ -271,6 +281,13 @@ class AsyncModelAverager(ModelAverager):
         self._pending = None
         if work is not None:
             work.wait()
+        if sp is not None and ts[0].is_cuda and len(ts) == 1:
+            # x <- x + (avg - snap) with the shadow refresh, one pass (same arithmetic order)
+            from ..ops import kernels as K
+            K.kavg_async_apply_(ts[0], flat, snap, sp.shadow, comm.world, sp.numel if sp.shadow is not None else 0)
+            for p in sp.params:
+                p._kml_shadow_version = p._version
+            return
         # x <- avg + (x - snap), per tensor of the flat layout
         flat.div_(comm.world).sub_(snap)
         off = 0

@@ -1150,3 +1150,24 @@ def test_stride2_dgrad_parity_classes(shape, cfg, monkeypatch):
     F.conv2d(xr, w.float().permute(0, 3, 1, 2), stride=2, padding=p).backward(dy.float().permute(0, 3, 1, 2))
     dx = K.conv_dgrad(dy, w, (B, H, W, Ci), k, k, (2, 2), (p, p), cfg=cfg)
     assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("n,n_params", [(4099, 4096), (1 << 20, (1 << 20) - 40)])
+def test_kavg_async_snap_and_apply_match_torch(n, n_params):
+    """Fused staleness-1 K-AVG passes == the torch ops they replace (flat / snap copies;
+    x + (flat / world - snap)), bit for bit, and the shadow is bf16(x) over the parameters."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(19)
+    x = torch.randn(n, device=dev)
+    flat, snap = torch.empty_like(x), torch.empty_like(x)
+    K.kavg_snap_(x, flat, snap)
+    assert torch.equal(flat, x) and torch.equal(snap, x)
+    flat.mul_(3.0).add_(torch.randn_like(x))          # the "all-reduced" sum
+    x2 = x + torch.randn_like(x) * 0.01                # local progress since the snapshot
+    ref = x2.clone()
+    ref.add_(flat.clone().div_(3).sub_(snap))
+    shadow = torch.zeros(n_params, dtype=torch.bfloat16, device=dev)
+    K.kavg_async_apply_(x2, flat, snap, shadow, 3, n_params)
+    torch.cuda.synchronize()
+    assert torch.equal(x2, ref)
+    assert torch.equal(shadow, ref[:n_params].to(torch.bfloat16))
