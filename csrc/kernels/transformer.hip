@@ -278,6 +278,26 @@ __global__ void k_gelu_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
   }
 }
 
+// 16-byte rows of 8 elements, two independent loads in flight per thread (the GELU pass
+// after a library GEMM writes the pre-activation: 2 x 100 MB for BERT-base's FFN1)
+__global__ void k_gelu_fwd8(const uint4* __restrict__ x, uint4* __restrict__ y, long long n8) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += 2 * stride) {
+    const bool two = i + stride < n8;
+    const uint4 a = x[i];
+    const uint4 b = two ? x[i + stride] : a;
+    auto g = [](uint4 v) {
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+      unsigned o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack_bf2(gelu(lo_bf(w[k])), gelu(hi_bf(w[k])));
+      return make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    y[i] = g(a);
+    if (two) y[i + stride] = g(b);
+  }
+}
+
 __global__ void k_gelu_bwd(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, bf16_t* __restrict__ dx,
                            long long n4) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -519,7 +539,11 @@ KML_API int kml_ln_bwd(const bf16_t* dy, const bf16_t* xin, const float* mean, c
 
 KML_API int kml_gelu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_gelu_fwd, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, x, y, n / 4);
+  if (n % 8 == 0 && (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0)
+    hipLaunchKernelGGL(k_gelu_fwd8, dim3(kml_stream_grid(n / 16, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(x), reinterpret_cast<uint4*>(y), n / 8);
+  else
+    hipLaunchKernelGGL(k_gelu_fwd, dim3(kml_stream_grid(n / 4, 256)), dim3(256), 0, s, x, y, n / 4);
   KML_LAUNCH_CHECK();
 }
 

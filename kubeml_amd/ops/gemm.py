@@ -20,12 +20,23 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5,
          (256, 256, 8): 6}  # (BM, BN[, stages])
-_TUNE_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_TUNE_FILE = os.environ.get("KUBEML_GEMM_TUNING_FILE") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _TUNED: dict = {}
 if os.path.exists(_TUNE_FILE) and os.environ.get("KUBEML_GEMM_TUNING", "1") != "0":
     with open(_TUNE_FILE) as f:
         for e in json.load(f).get("entries", []):
             _TUNED[(e["layout"], e["M"], e["N"], e["K"])] = (tuple(e["tile"]), int(e.get("splits", 1)))
+
+# A table entry with tile ["blas"] runs that forward / dgrad GEMM on hipBLASLt (torch.mm /
+# addmm) — only where the GEMM is plain (bias or a C addend, no fused activation) and the
+# library kernel measured faster inside the step.
+BLAS = ("blas",)
+
+
+def _blas(layout, M, N, K) -> bool:
+    t = _TUNED.get((layout, M, N, K))
+    return t is not None and t[0] == BLAS
 
 _ZP = {}
 
@@ -59,7 +70,7 @@ def plan(layout: int, M: int, N: int, K: int):
     general choice — 128x128 two-stage tiles (two blocks per CU hide each other's
     prologue / epilogue), split-K when the output tiles cannot fill 256 CUs."""
     t = _TUNED.get((layout, M, N, K))
-    if t is not None:
+    if t is not None and t[0] != BLAS:
         return t
     tile = (128, 128, 2)
     tiles = _cdiv(M, 128) * _cdiv(N, 128)
@@ -143,6 +154,16 @@ def linear_fwd(x, w, bias=None, act=0, pre=None):
     if w.shape[1] != ip:
         raise ValueError(f"linear_fwd: x {tuple(x.shape)} vs w {tuple(w.shape)}")
     y = torch.empty((T, op), dtype=BF16, device=x.device)
+    if _blas(0, T, op, ip) and (act == 0 and pre is None or act == 1 and pre is not None):
+        # act 1 (erf-GELU, pre-activation kept): the library GEMM writes pre, one pass applies GELU
+        z = y if act == 0 else pre
+        if bias is None:
+            torch.mm(x, w.t(), out=z)
+        else:
+            torch.addmm(bias[:op].to(BF16), x, w.t(), out=z)
+        if act == 1:
+            HIP.call("kml_gelu_fwd", "p p l s", pre.data_ptr(), y.data_ptr(), pre.numel(), stream_ptr())
+        return y
     gemm(x, ip, w, ip, y, op, T, op, ip, 0, 0, bias=bias, act=act, c2=pre)
     return y
 
@@ -159,6 +180,9 @@ def linear_dgrad(dy, w, addend=None):
         raise ValueError(f"linear_dgrad: dy {tuple(dy.shape)} vs w {tuple(w.shape)}")
     if addend is not None and (tuple(addend.shape) != (T, ip) or not addend.is_contiguous()):
         raise ValueError("linear_dgrad: addend must be a contiguous [T, ip] tensor")
+    if _blas(1, T, ip, op):
+        # the addend is a fresh residual gradient owned by this call: accumulate into it
+        return torch.mm(dy, w) if addend is None else addend.addmm_(dy, w)
     dx = torch.empty((T, ip), dtype=BF16, device=dy.device)
     tile, splits = plan(1, T, ip, op)
     if splits > 1:
