@@ -124,7 +124,7 @@ def main():
                "masked_per_seq": P, "layers": a.layers, "optimizer": "fused AdamW", "dtype": "bf16",
                "data": "synthetic tokens, random init", "graph": not a.no_graph, "overlap_segments": len(segs),
                "loss_first_last": [round(first, 4), round(float(loss.detach()), 4)],
-               "gemm": "csrc/kernels/gemm.hip"}
+               "gemm": "gemm.hip (wgrad, FFN2 dgrad + GELU backward) / hipBLASLt (plain fwd, dgrad: gemm_tuning.json)"}
         if in_sync is not None:
             out["ranks_in_sync"] = in_sync
         print(json.dumps(out), flush=True)
