@@ -287,14 +287,22 @@ __global__ void k_kavg_snap(const float* __restrict__ x, float* __restrict__ fla
   }
 }
 
+// x + (flat / world - snap) rounded exactly as the torch ops it replaces (flat.div_(world):
+// a multiply by the fp32 reciprocal, computed once on the host; no contraction into an FMA)
+__device__ __forceinline__ float kavg_step(float x, float f, float sn, float inv) {
+#pragma clang fp contract(off)
+  return x + (f * inv - sn);
+}
+
 __global__ void k_kavg_async_apply(float* __restrict__ x, const float* __restrict__ flat,
-                                   const float* __restrict__ snap, bf16_t* __restrict__ shadow, float world,
+                                   const float* __restrict__ snap, bf16_t* __restrict__ shadow, float inv,
                                    long long n, long long n_params) {
   const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 v = reinterpret_cast<float4*>(x)[i];
     const float4 f = reinterpret_cast<const float4*>(flat)[i], sn = reinterpret_cast<const float4*>(snap)[i];
-    v.x += f.x / world - sn.x; v.y += f.y / world - sn.y; v.z += f.z / world - sn.z; v.w += f.w / world - sn.w;
+    v.x = kavg_step(v.x, f.x, sn.x, inv); v.y = kavg_step(v.y, f.y, sn.y, inv);
+    v.z = kavg_step(v.z, f.z, sn.z, inv); v.w = kavg_step(v.w, f.w, sn.w, inv);
     reinterpret_cast<float4*>(x)[i] = v;
     if (shadow && 4 * i + 3 < n_params) {
       uint2 sh;
@@ -308,7 +316,7 @@ __global__ void k_kavg_async_apply(float* __restrict__ x, const float* __restric
     }
   }
   for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    x[i] += flat[i] / world - snap[i];
+    x[i] = kavg_step(x[i], flat[i], snap[i], inv);
     if (shadow && i < n_params) shadow[i] = f2bf(x[i]);
   }
 }
@@ -321,7 +329,7 @@ KML_API int kml_kavg_snap(const float* x, float* flat, float* snap, long long n,
 KML_API int kml_kavg_async_apply(float* x, const float* flat, const float* snap, bf16_t* shadow, float world,
                                  long long n, long long n_params, hipStream_t s) {
   hipLaunchKernelGGL(k_kavg_async_apply, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, x, flat, snap,
-                     shadow, world, n, n_params);
+                     shadow, 1.0f / world, n, n_params);
   KML_LAUNCH_CHECK();
 }
 

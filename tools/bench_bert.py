@@ -3,7 +3,9 @@ bench — see bench.py).  Synthetic token batches of the real shape (there is no
 for a corpus), random-init BERT-base (109.5 M params), fused AdamW, bf16 compute, fp32
 master weights, hidden + attention-probability dropout 0.1, 76 masked positions per
 512-token sequence (Google BERT's max_predictions_per_seq), whole step captured as one
-hipGraph.  Every large GEMM runs on csrc/kernels/gemm.hip (no vendor BLAS).
+hipGraph.  Weight gradients and the GELU-fused FFN2 dgrad run on csrc/kernels/gemm.hip; the
+plain forward / dgrad GEMMs (bias or residual addend only) run on hipBLASLt where
+``gemm_tuning.json`` says the library measured faster inside the step.
 
 Data parallel (config 5: 8 workers): ``--gpus N`` launches N ranks (one per GPU,
 torch.distributed over RCCL/xGMI) unless already under torchrun; backward is split into
