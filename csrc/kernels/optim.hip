@@ -272,7 +272,7 @@ __global__ void k_kavg_finish(float* __restrict__ state, long long n_params, lon
 // Staleness-1 K-AVG (parallel/kavg.py AsyncModelAverager), two passes per round instead of six:
 // launch: flat := x, snap := x (one read, two writes; flat then goes into the async SUM);
 // apply:  x := x + (flat / world - snap), the bf16 shadow of the parameter range refreshed in
-// the same pass (same arithmetic order as the torch div / sub / add it replaces).
+// the same pass (same operation order as the torch div / sub / add it replaces).
 __global__ void k_kavg_snap(const float* __restrict__ x, float* __restrict__ flat, float* __restrict__ snap,
                             long long n) {
   const long long n4 = n >> 2, stride = (long long)gridDim.x * blockDim.x;
@@ -287,8 +287,8 @@ __global__ void k_kavg_snap(const float* __restrict__ x, float* __restrict__ fla
   }
 }
 
-// x + (flat / world - snap) rounded exactly as the torch ops it replaces (flat.div_(world):
-// a multiply by the fp32 reciprocal, computed once on the host; no contraction into an FMA)
+// x + (flat / world - snap): a multiply by the fp32 reciprocal (computed once on the host), then
+// the subtraction and the addition, each rounded on its own (no contraction into an FMA)
 __device__ __forceinline__ float kavg_step(float x, float f, float sn, float inv) {
 #pragma clang fp contract(off)
   return x + (f * inv - sn);
