@@ -677,6 +677,43 @@ _S2_PARITY_MIN_ROWS = 20000
 _S2_OK: dict = {}
 
 
+# 1x1 / stride-1 / pad-0 conv weight gradients are plain GEMMs (dw[K][C] = dy^T x over the
+# pixels).  ``wgrad_gemm.json`` maps (pixels, K, C) to the GEMM that measured faster than the
+# implicit-GEMM wgrad inside the step (tools/wgrad_1x1.py): ["blas"] (hipBLASLt, fp32 out,
+# beta 1) or ["slab", BM, BN, stages, splits] (gemm.hip's deterministic slab split-K).
+_WGRAD_GEMM_FILE = os.environ.get("KUBEML_WGRAD_GEMM_FILE") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "wgrad_gemm.json")
+_WGRAD_GEMM: dict = {}
+if os.path.exists(_WGRAD_GEMM_FILE):
+    with open(_WGRAD_GEMM_FILE) as _f:
+        for _e in json.load(_f).get("entries", []):
+            _WGRAD_GEMM[(int(_e["P"]), int(_e["K"]), int(_e["C"]))] = tuple(_e["route"])
+
+
+def wgrad_gemm_route(x_shape, K, KH, KW, stride, pad, dbias=None):
+    """The table's GEMM route for this conv's weight gradient, or None (implicit-GEMM wgrad)."""
+    if not _WGRAD_GEMM or dbias is not None or (KH, KW) != (1, 1) or tuple(stride) != (1, 1) or tuple(pad) != (0, 0):
+        return None
+    B, H, W, C = x_shape
+    return _WGRAD_GEMM.get((B * H * W, K, C))
+
+
+def _wgrad_gemm(route, x, dy, dw, accumulate):
+    B, H, W, C = x.shape
+    K, P = dy.shape[3], B * H * W
+    x2, dy2, dw2 = x.reshape(P, C), dy.reshape(P, K), dw.view(K, C)
+    if route[0] == "blas":
+        if accumulate:
+            torch.addmm(dw2, dy2.t(), x2, out_dtype=F32, out=dw2)
+        else:
+            torch.mm(dy2.t(), x2, out_dtype=F32, out=dw2)
+        return dw
+    from . import gemm as G
+    _, bm, bn, st, splits = route
+    G.wgrad_splitk_(dw2, dy2, K, x2, C, K, C, P, beta=1.0 if accumulate else 0.0, tile=(bm, bn, st), splits=splits)
+    return dw
+
+
 def s2_parity_ok(B, H, W, stride, plan, g22=False, fold=0, operands=True) -> bool:
     """True when a stride-2 dgrad runs as parity classes: large map, a plain igemm / glds plan
     whose tile takes the row-pass epilogue, and an addend or consumer-BN operand."""
@@ -809,13 +846,16 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     ntap = (r1 - r0) * (s1 - s0)
     M = B * H * W
     dplan, wplan, grouped = bwd_plans(x.shape, K, KH, KW, stride, pad, dcfg, wcfg)
+    wroute = None if (wcfg is not None or wu is not None) else wgrad_gemm_route(x.shape, K, KH, KW, stride, pad, dbias)
+    if wroute is not None:
+        grouped = False
     if grouped and s2_parity_ok(B, H, W, stride, dplan, g22, fold, operands=addend is not None or bnf is not None):
         grouped = False
     if dbias is not None and wu is not None:
         raise ValueError("conv_bwd: dbias needs a 1x1 conv")
     if not grouped:
-        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=wplan, accumulate=accumulate, dbias=dbias,
-                   bias_accumulate=bias_accumulate)
+        conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None if wroute is not None else wplan, accumulate=accumulate,
+                   dbias=dbias, bias_accumulate=bias_accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
                        bnf_mask=bnf_mask, _g22=g22)
         if not fold:
@@ -928,6 +968,9 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulat
     OH, OW = out_hw(H, W, KH, KW, sh, sw, ph, pw)
     if tuple(dy.shape) != (B, OH, OW, K) or tuple(dw.shape) != (K, KH, KW, C):
         raise ValueError("wgrad shape mismatch")
+    route = None if cfg is not None else wgrad_gemm_route(x.shape, K, KH, KW, stride, pad, dbias)
+    if route is not None:
+        return _wgrad_gemm(route, x, dy, dw, accumulate)
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
     bm, bn, bk, splits, variant = cfg

@@ -3,7 +3,7 @@ set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r4
 mkdir -p $out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "kavg or gelu" > $out/r35_kavg.log 2>&1 || { tail -30 $out/r35_kavg.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "kavg or gelu or conv1x1_wgrad" > $out/r35_kavg.log 2>&1 || { tail -30 $out/r35_kavg.log; exit 1; }
 tail -1 $out/r35_kavg.log
 timeout -k 10 120 python tools/diag/kavg_bits.py
 timeout -k 10 300 python -u tools/bench_bert.py > $out/bert_r35.json 2> $out/bert_r35.err || { tail -20 $out/bert_r35.err; exit 1; }

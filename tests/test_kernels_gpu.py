@@ -1173,3 +1173,27 @@ def test_kavg_async_snap_and_apply_match_torch(n, n_params):
     torch.cuda.synchronize()
     torch.testing.assert_close(x2, ref, rtol=1e-6, atol=1e-6)
     assert torch.equal(shadow, x2[:n_params].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("route", [("blas",), ("slab", 128, 128, 2, 16)])
+def test_conv1x1_wgrad_gemm_routes(monkeypatch, route):
+    """1x1/s1 conv weight gradient on a GEMM route (wgrad_gemm.json): hipBLASLt or the slab
+    split-K kernel, stored and accumulated, alone and through conv_bwd (which then runs the
+    dgrad on its own) — against fp32 torch."""
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(23)
+    B, H, W, C, Co = 8, 14, 14, 64, 128
+    monkeypatch.setitem(K._WGRAD_GEMM, (B * H * W, Co, C), route)
+    x = torch.randn(B, H, W, C, device=dev).to(torch.bfloat16)
+    dy = torch.randn(B, H, W, Co, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
+    ref = (dy.reshape(-1, Co).double().t() @ x.reshape(-1, C).double()).view(Co, 1, 1, C)
+    dw = torch.full((Co, 1, 1, C), 7.0, device=dev)
+    K.conv_wgrad(x, dy, dw, 1, 1, (1, 1), (0, 0), accumulate=False)
+    assert _rel(dw, ref) < 1e-5
+    K.conv_wgrad(x, dy, dw, 1, 1, (1, 1), (0, 0), accumulate=True)
+    assert _rel(dw, 2 * ref) < 1e-5
+    dw2 = torch.zeros_like(dw)
+    dx = K.conv_bwd(dy, w, x, dw2, 1, 1, (1, 1), (0, 0))
+    assert _rel(dw2, ref) < 1e-5
+    assert _rel(dx, dy.float() @ w.view(Co, C).float()) < 1e-2
