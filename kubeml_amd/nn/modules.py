@@ -171,7 +171,8 @@ class _LinearFn(Function):
             from ..ops import gemm as G
             w2 = shadow_of(weight).view(op, ip)
             pre = torch.empty((B, op), dtype=torch.bfloat16, device=x2.device) if act == 2 else None
-            y = G.linear_fwd(x2, w2, None if bias is None else master_of(bias), act=1 if act == 2 else 0, pre=pre)
+            y = G.linear_fwd(x2, w2, None if bias is None else master_of(bias), act=1 if act == 2 else 0, pre=pre,
+                             bias16=None if bias is None else shadow_of(bias))
         else:
             if act == 2:
                 raise ValueError("fused GELU needs the large-linear GEMM path")

@@ -147,8 +147,10 @@ def wgrad_splitk_(dw, a, lda, b, ldb, M, N, K, beta=1.0, tile=(256, 256, 8), spl
     return dw
 
 
-def linear_fwd(x, w, bias=None, act=0, pre=None):
-    """y[T, op] = act(x[T, ip] @ w[op, ip]^T + bias); ``pre`` receives the pre-activation."""
+def linear_fwd(x, w, bias=None, act=0, pre=None, bias16=None):
+    """y[T, op] = act(x[T, ip] @ w[op, ip]^T + bias); ``pre`` receives the pre-activation.
+    bias16: the bias's bf16 shadow, used by the library route (whose epilogue takes a bias of
+    the output type) instead of a conversion per call."""
     T, ip = x.shape
     op = w.shape[0]
     if w.shape[1] != ip:
@@ -160,7 +162,8 @@ def linear_fwd(x, w, bias=None, act=0, pre=None):
         if bias is None:
             torch.mm(x, w.t(), out=z)
         else:
-            torch.addmm(bias[:op].to(BF16), x, w.t(), out=z)
+            b16 = bias16[:op] if bias16 is not None else bias[:op].to(BF16)
+            torch.addmm(b16, x, w.t(), out=z)
         if act == 1:
             HIP.call("kml_gelu_fwd", "p p l s", pre.data_ptr(), y.data_ptr(), pre.numel(), stream_ptr())
         return y
