@@ -710,7 +710,8 @@ def _wgrad_gemm(route, x, dy, dw, accumulate):
         return dw
     from . import gemm as G
     _, bm, bn, st, splits = route
-    G.wgrad_splitk_(dw2, dy2, K, x2, C, K, C, P, beta=1.0 if accumulate else 0.0, tile=(bm, bn, st), splits=splits)
+    G.wgrad_splitk_(dw2, dy2, K, x2, C, K, C, P, beta=1.0 if accumulate else 0.0,
+                    tile=(bm, bn, st) if st else (bm, bn), splits=splits)
     return dw
 
 

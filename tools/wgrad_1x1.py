@@ -22,7 +22,37 @@ SHAPES = [(401408, 64, 64), (401408, 64, 256), (401408, 256, 64), (401408, 128, 
           (6272, 512, 2048), (6272, 2048, 512)]
 
 
+def sweep():
+    """--sweep: slab split-K tile x splits grid per shape; prints the best route per shape."""
+    dev = torch.device("cuda")
+    grid = {401408: [64, 96, 128, 192, 256], 100352: [32, 48, 64, 96, 128], 25088: [12, 16, 24, 32, 48],
+            6272: [2, 3, 4, 6, 8]}
+    for P, Co, Ci in SHAPES:
+        B = 128
+        x2 = torch.randn(P, Ci, device=dev).to(torch.bfloat16)
+        dy2 = torch.randn(P, Co, device=dev).to(torch.bfloat16)
+        dw2 = torch.zeros(Co, Ci, device=dev)
+        hw = int(round((P // B) ** 0.5))
+        N = 4
+        conv = timed(lambda: [K.conv_wgrad(x2.view(B, hw, hw, Ci), dy2.view(B, hw, hw, Co), dw2.view(Co, 1, 1, Ci),
+                                           1, 1, (1, 1), (0, 0), cfg=K.plan_conv("wgrad", Co, Ci, P)) for _ in range(N)], N)
+        best = ("conv", conv)
+        res = {"P": P, "Cout": Co, "Cin": Ci, "conv_us": round(conv, 2)}
+        for tile in [(128, 128, 2), (256, 128), (128, 256), (256, 256, 8)]:
+            for sp in grid[P]:
+                t = timed(lambda: [G.wgrad_splitk_(dw2, dy2, Co, x2, Ci, Co, Ci, P, beta=0.0, tile=tile, splits=sp)
+                                   for _ in range(N)], N)
+                res[f"{'x'.join(map(str, tile))}/{sp}"] = round(t, 2)
+                if t < best[1]:
+                    best = (["slab", tile[0], tile[1], tile[2] if len(tile) > 2 else 0, sp], t)
+        res["best"] = best[0]
+        res["best_us"] = round(best[1], 2)
+        print(json.dumps(res), flush=True)
+
+
 def main():
+    if "--sweep" in sys.argv:
+        return sweep()
     dev = torch.device("cuda")
     for P, Co, Ci in SHAPES:
         torch.manual_seed(0)
