@@ -25,8 +25,12 @@ SHAPES = [(401408, 64, 64), (401408, 64, 256), (401408, 256, 64), (401408, 128, 
 def sweep():
     """--sweep: slab split-K tile x splits grid per shape; prints the best route per shape."""
     dev = torch.device("cuda")
-    grid = {401408: [64, 96, 128, 192, 256], 100352: [32, 48, 64, 96, 128], 25088: [12, 16, 24, 32, 48],
-            6272: [2, 3, 4, 6, 8]}
+    grid = {401408: [64, 96, 128, 192, 256, 384, 512], 100352: [32, 48, 64, 96, 128], 25088: [12, 16, 24, 32, 48],
+            6272: [2, 3, 4, 6, 8, 12, 16]}
+    if "--tiles" in sys.argv:    # the 128x128 two-stage tile only (it won every shape of the full sweep)
+        tiles = [(128, 128, 2)]
+    else:
+        tiles = [(128, 128, 2), (256, 128), (128, 256), (256, 256, 8)]
     for P, Co, Ci in SHAPES:
         B = 128
         x2 = torch.randn(P, Ci, device=dev).to(torch.bfloat16)
@@ -38,7 +42,7 @@ def sweep():
                                            1, 1, (1, 1), (0, 0), cfg=K.plan_conv("wgrad", Co, Ci, P)) for _ in range(N)], N)
         best = ("conv", conv)
         res = {"P": P, "Cout": Co, "Cin": Ci, "conv_us": round(conv, 2)}
-        for tile in [(128, 128, 2), (256, 128), (128, 256), (256, 256, 8)]:
+        for tile in tiles:
             for sp in grid[P]:
                 t = timed(lambda: [G.wgrad_splitk_(dw2, dy2, Co, x2, Ci, Co, Ci, P, beta=0.0, tile=tile, splits=sp)
                                    for _ in range(N)], N)
