@@ -29,12 +29,30 @@ This replaces the reference's per-iteration HTTP fan-out + Redis weight round-tr
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Callable, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 from ..utils import trace
+
+
+@contextlib.contextmanager
+def capture_graph(g, **kw):
+    """torch.cuda.graph with the cyclic garbage collected first and the collector paused for the
+    capture: a collection inside the capture can free an earlier step's graph, events or
+    library handles, and those destroy calls invalidate a global-mode capture."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def train_state_tensors(module=None, space=None, optimizer=None, extra: Sequence[torch.Tensor] = ()):
@@ -419,7 +437,7 @@ class GraphedTrainStep:
         if not self.comm or self.graph_comm:
             try:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, capture_error_mode=mode):
+                with capture_graph(g, capture_error_mode=mode):
                     self.loss = self._body()
                 self.g_all, self.g_seg, self.g_opt = g, [], None
                 captured_all = True
@@ -444,13 +462,13 @@ class GraphedTrainStep:
             self.g_seg = []
             for k, seg in enumerate(self.segments):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
+                with capture_graph(g, pool=pool, capture_error_mode=mode):
                     out = self._run(seg)
                 if k == 0:
                     self.loss = out
                 self.g_seg.append(g)
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt, pool=pool, capture_error_mode=mode):
+            with capture_graph(self.g_opt, pool=pool, capture_error_mode=mode):
                 self.opt_step()
             self.g_all = None
         torch.cuda.synchronize()

@@ -607,7 +607,8 @@ class KubeModel(ABC):
                 fwd(xs, ys)                       # warm-up: plans, workspaces, lazy buffers
             torch.cuda.current_stream(self.device).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            from ..engine.step import capture_graph
+            with capture_graph(graph):
                 outs = fwd(xs, ys)
             g = self._eval_graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
             _sp.__exit__(None, None, None)
