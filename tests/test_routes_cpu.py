@@ -1,0 +1,42 @@
+"""Measured-table routing (no GPU needed): which GEMM runs a linear / 1x1-conv product.
+
+ops/gemm_tuning.json entries with tile ["blas"] send a plain forward / dgrad to hipBLASLt;
+ops/wgrad_gemm.json sends a 1x1 / stride-1 conv weight gradient to gemm.hip's slab split-K.
+Everything not in a table stays on the hand-written kernels."""
+import json
+import os
+
+from kubeml_amd.ops import gemm as G
+from kubeml_amd.ops import kernels as K
+
+OPS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kubeml_amd", "ops")
+
+
+def test_library_entries_are_plain_bert_shapes_only():
+    d = json.load(open(os.path.join(OPS, "gemm_tuning.json")))
+    blas = [(e["layout"], e["M"], e["N"], e["K"]) for e in d["entries"] if e["tile"] == ["blas"]]
+    assert blas, "the shipped table routes BERT-base's plain GEMMs to the library"
+    assert all(layout in (0, 1) for layout, *_ in blas)          # never a weight gradient
+    # FFN2's dgrad keeps the hand-written kernel: its epilogue applies FFN1's GELU backward
+    assert (1, 16384, 3072, 768) not in blas
+    for key in blas:
+        assert G._blas(*key)
+        tile, _ = G.plan(*key)                 # kernel callers never see the library tile
+        assert tile != G.BLAS
+    assert not G._blas(0, 4096, 3072, 768)     # shapes outside the table: hand-written
+
+
+def test_wgrad_gemm_route_only_for_plain_1x1():
+    d = json.load(open(os.path.join(OPS, "wgrad_gemm.json")))
+    assert d["entries"]
+    e = d["entries"][0]
+    B = 128
+    hw = int(round((e["P"] // B) ** 0.5))
+    shape = (B, hw, hw, e["C"])
+    assert K.wgrad_gemm_route(shape, e["K"], 1, 1, (1, 1), (0, 0)) == tuple(e["route"])
+    assert K.wgrad_gemm_route(shape, e["K"], 3, 3, (1, 1), (1, 1)) is None       # not a GEMM
+    assert K.wgrad_gemm_route(shape, e["K"], 1, 1, (2, 2), (0, 0)) is None       # strided
+    assert K.wgrad_gemm_route(shape, e["K"], 1, 1, (1, 1), (0, 0), dbias=object()) is None
+    assert K.wgrad_gemm_route((B, hw, hw, e["C"] + 8), e["K"], 1, 1, (1, 1), (0, 0)) is None
+    for r in d["entries"]:
+        assert r["route"][0] in ("blas", "slab")
