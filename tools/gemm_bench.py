@@ -80,7 +80,7 @@ def main():
             if layout == 2:   # deterministic slab split-K (kml_gemm_wgrad_splitk)
                 tiles = -(-M // tile[0]) * -(-N // tile[1])
                 base = max(1, round(256 / tiles))
-                for s in sorted({max(1, base // 2), base, base * 2}):
+                for s in sorted({max(1, base // 2), base, base * 2, base * 4, base * 8}):
                     if K // s >= 256:
                         cands.append((tile + ("slab",), s))
 
