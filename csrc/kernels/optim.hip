@@ -290,8 +290,11 @@ __global__ void k_kavg_snap(const float* __restrict__ x, float* __restrict__ fla
 // x + (flat / world - snap): a multiply by the fp32 reciprocal (computed once on the host), then
 // the subtraction and the addition, each rounded on its own (no contraction into an FMA)
 __device__ __forceinline__ float kavg_step(float x, float f, float sn, float inv) {
-#pragma clang fp contract(off)
-  return x + (f * inv - sn);
+  // the build's -ffp-contract=fast ignores contract pragmas: an empty asm on the product keeps
+  // it a rounded value of its own, so the subtraction is not fused into an FMA
+  float q = f * inv;
+  asm volatile("" : "+v"(q));
+  return x + (q - sn);
 }
 
 __global__ void k_kavg_async_apply(float* __restrict__ x, const float* __restrict__ flat,

@@ -1155,9 +1155,9 @@ def test_stride2_dgrad_parity_classes(shape, cfg, monkeypatch):
 @pytest.mark.parametrize("n,n_params", [(4099, 4096), (1 << 20, (1 << 20) - 40)])
 def test_kavg_async_snap_and_apply_match_torch(n, n_params):
     """Fused staleness-1 K-AVG passes == the torch ops they replace: the flat / snap copies bit
-    for bit; x + (flat / world - snap) to within one fp32 rounding (torch's scalar division
-    and this kernel may round the quotient differently); the shadow is exactly bf16(x) over
-    the parameters."""
+    for bit; x + (flat / world - snap) to within one fp32 rounding (torch divides by a scalar
+    as a multiply by the fp32 reciprocal; the kernel keeps that product rounded on its own, no
+    FMA); the shadow is exactly bf16(x) over the parameters."""
     from kubeml_amd.ops import kernels as K
     torch.manual_seed(19)
     x = torch.randn(n, device=dev)
