@@ -222,7 +222,8 @@ def main():
 
     B = args.batch
     n_local = CIFAR_TRAIN // world          # split_minibatches gives every rank ~1/N of the docs
-    n_val = -(-CIFAR_TEST // world)
+    # the 10,000-image test set split over the ranks exactly (the ranks' shares sum to 10,000)
+    n_val = CIFAR_TEST // world + (rank < CIFAR_TEST % world)
 
     # synthetic CIFAR-10 shards resident in HBM (each rank its own shard)
     g = torch.Generator(device=dev).manual_seed(rank)
@@ -397,29 +398,41 @@ def measure_epoch(args, model, space, step, averager, cm, comm, world, dev, time
     B = args.batch
     steps = math.ceil(n_local / B)
     n_val = vdata.shape[0]
-    vsteps = math.ceil(n_val / B)
+    vsteps = n_val // B                     # full validation batches ...
+    vtail = n_val - vsteps * B              # ... and the partial last one (10,000 = 39 x 256 + 16)
     vctr = torch.zeros(3, dtype=torch.float32, device=dev)
     acc = torch.zeros(2, dtype=torch.float64, device=dev)    # [correct, count]
+    xt = torch.empty((max(vtail, 1),) + tuple(xbuf.shape[1:]), dtype=xbuf.dtype, device=dev)
+    yt = torch.empty((max(vtail, 1),), dtype=ybuf.dtype, device=dev)
 
-    def val_batch():
-        K.augment(vdata, vlabels, vctr, B, out=xbuf, labels_out=ybuf, pad=0, flip=False, train=False)
-        K.advance_counter_(vctr, B, n_val)
+    def val_batch(nb, xb, yb):
+        K.augment(vdata, vlabels, vctr, nb, out=xb, labels_out=yb, pad=0, flip=False, train=False)
+        K.advance_counter_(vctr, nb, n_val)
         with torch.no_grad():
-            loss, correct = cross_entropy(model(xbuf), ybuf, return_correct=True)
+            loss, correct = cross_entropy(model(xb), yb, return_correct=True)
         acc[0] += correct
-        acc[1] += B
-    # eval forward as one graph too (captured once, outside the timed region; BN in eval mode)
+        acc[1] += nb
+    full = (lambda: val_batch(B, xbuf, ybuf))
+    tail = (lambda: val_batch(vtail, xt, yt)) if vtail else None
+    # eval forwards as graphs too (captured once, outside the timed region; BN in eval mode)
     model.eval()
-    vgraph = None
+    vgraph = tgraph = None
     if not args.no_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            val_batch()
-        torch.cuda.current_stream().wait_stream(s)
-        vgraph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(vgraph):
-            val_batch()
+        graphs = []
+        for fn in (full, tail):
+            if fn is None:
+                graphs.append(None)
+                continue
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fn()
+            torch.cuda.current_stream().wait_stream(s)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                fn()
+            graphs.append(gr)
+        vgraph, tgraph = graphs
     model.train()
     acc.zero_()
     vctr.zero_()
@@ -435,7 +448,12 @@ def measure_epoch(args, model, space, step, averager, cm, comm, world, dev, time
             if vgraph is not None:
                 vgraph.replay()
             else:
-                val_batch()
+                full()
+        if tail is not None:
+            if tgraph is not None:
+                tgraph.replay()
+            else:
+                tail()
         model.train()
         if comm:
             dist.all_reduce(acc)
@@ -444,6 +462,7 @@ def measure_epoch(args, model, space, step, averager, cm, comm, world, dev, time
     t_val, _ = timed(validate)
     return {"epoch_time_s": round(t_train + t_val, 4), "epoch_train_s": round(t_train, 4),
             "epoch_val_s": round(t_val, 4), "epoch_steps_per_rank": steps, "val_images": int(acc[1].item()),
+            "val_batches_per_rank": vsteps + (1 if vtail else 0),
             "epoch_measured": True}
 
 

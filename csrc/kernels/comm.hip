@@ -735,6 +735,21 @@ KML_API int kml_zs_all_gather(const void* const* flags, const void* const* bufs,
   KML_LAUNCH_CHECK();
 }
 
+// standalone barrier `bar` past the current sequence (one-block launch).  gather_master closes
+// with it (all-gather with finish = 2, then bar = 0): no rank leaves the call — and overwrites
+// its own master chunk with a local step, a broadcast or a restore — while a peer may still be
+// reading that chunk over xGMI.
+KML_API int kml_zs_barrier(const void* const* flags, void* region, void* ctrl, int rank, int world, int bar,
+                           double timeout_s, hipStream_t s) {
+  ZsPeers zp;
+  if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || bar < 0 || !(timeout_s > 0.0) ||
+      !zs_peers(zp, flags, flags, world) || zp.flags[rank] != region)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_zs_wait, dim3(1), dim3(64), 0, s, zp, reinterpret_cast<char*>(region),
+                     reinterpret_cast<unsigned*>(ctrl), rank, world, (unsigned)bar, zs_limit(timeout_s), nullptr);
+  KML_LAUNCH_CHECK();
+}
+
 // device wall-clock stamp (100 MHz ticks) into buf[idx]: brackets the collectives inside a
 // captured step so their time is known without events or a host sync
 __global__ void k_stamp(unsigned long long* buf, int idx) {

@@ -63,7 +63,14 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     shard = None
     if plan is not None and plan.schedule == "shard":
         on_gpu = comm and torch.cuda.is_available() and space.grad.is_cuda
-        if on_gpu:
+        # the optimizer's capability is checked BEFORE the collective setup (the same answer on
+        # every rank), so an optimizer that cannot update one flat range falls back like a node
+        # without IPC buffers instead of failing after the self-test
+        can_shard = ((getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges())
+                     or getattr(optimizer, "supports_shard_range", lambda: False)())
+        if on_gpu and not can_shard:
+            _log.warning("shard plan: the optimizer cannot update one flat range; using the all-reduce plan")
+        if on_gpu and can_shard:
             from ..parallel.peer import PeerShard, verified_shard
             shard = peer if isinstance(peer, PeerShard) and peer.space is space and peer.region is not None else None
             if shard is None:
@@ -166,8 +173,6 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     if shard is not None:
         blocks = plan.max_blocks
         fused_sgd = getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges()
-        if not (fused_sgd or getattr(optimizer, "supports_ranges", lambda: False)()):
-            raise ValueError("the shard plan needs a fused optimizer over one flat space")
 
         def shard_step(stamps=None):
             """stamps: int64[2] device buffer (timing) — start / end of the collective."""

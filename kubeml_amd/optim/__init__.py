@@ -200,6 +200,10 @@ class SGD(FusedOptimizer):
         spaces, loose = self._flat_groups()
         return len(spaces) == 1 and not loose
 
+    def supports_shard_range(self) -> bool:
+        """One :meth:`step_range` per step over this rank's chunk (engine/dp.py shard plan)."""
+        return self.supports_ranges()
+
     @torch.no_grad()
     def step_range(self, start: int, end: int, max_blocks: int = 0):
         """The fused step restricted to flat elements [start, end): the gradients of a
@@ -317,6 +321,13 @@ class Adam(FusedOptimizer):
         return loss
 
     def supports_ranges(self) -> bool:
+        """False: a per-backward-stage update (opt_overlap) would advance the bias-correction
+        step once per stage; Adam has no finish_ranges.  The sharded update uses
+        :meth:`supports_shard_range` (one range per step)."""
+        return False
+
+    def supports_shard_range(self) -> bool:
+        """One :meth:`step_range` per step over this rank's chunk (engine/dp.py shard plan)."""
         spaces, loose = self._flat_groups()
         return len(spaces) == 1 and not loose and spaces[0][0].device.type == "cuda"
 

@@ -319,8 +319,9 @@ class PeerShard:
         self.world = dist.get_world_size(group)
         if self.world > PeerAllReduce.MAX_RANKS:
             raise ValueError(f"sharded update supports up to {PeerAllReduce.MAX_RANKS} ranks (one node)")
-        if not getattr(space, "ipc", False):
-            raise PeerCommError("sharded update needs IPC flat buffers (nn/flat.py, KUBEML_IPC_FLAT)")
+        # whether this rank's flat buffers are IPC-exportable is agreed collectively below: a
+        # rank that bailed out here alone would leave its peers blocked in all_gather_object
+        ipc_ok = bool(getattr(space, "ipc", False))
         self.timeout_s = float(timeout_s)
         self.device = space.device
         self.n = int(space.numel)
@@ -331,13 +332,20 @@ class PeerShard:
         self.region = self.ctrl = None
         err = ""
         with torch.cuda.device(self.device):
-            region, ctrl = ctypes.c_void_p(), ctypes.c_void_p()
-            HIP.call("kml_peer_alloc", "l p p", 16, ctypes.addressof(region), ctypes.addressof(ctrl))
-            self.region, self.ctrl = region.value, ctrl.value
-            mine = [self.region, space.grad.data_ptr(), space.shadow.data_ptr(), space.state.data_ptr()]
-            hs = [_handle_of(p) for p in mine]
+            hs = None
+            if ipc_ok:
+                region, ctrl = ctypes.c_void_p(), ctypes.c_void_p()
+                HIP.call("kml_peer_alloc", "l p p", 16, ctypes.addressof(region), ctypes.addressof(ctrl))
+                self.region, self.ctrl = region.value, ctrl.value
+                mine = [self.region, space.grad.data_ptr(), space.shadow.data_ptr(), space.state.data_ptr()]
+                hs = [_handle_of(p) for p in mine]
             allh: List[list] = [None] * self.world
             dist.all_gather_object(allh, (hs, _device_ident(self.device)), group=group)
+            if any(a[0] is None for a in allh):
+                self._release()
+                bad = [r for r, a in enumerate(allh) if a[0] is None]
+                raise PeerCommError(f"sharded update needs IPC flat buffers on every rank (nn/flat.py, "
+                                    f"KUBEML_IPC_FLAT); ranks {bad} have none")
             # the barrier is a one-block launch of its own and the work kernels behind it never
             # spin (split): they run at full grid like any streaming kernel, with no per-block
             # fence, and ranks that share one GPU (packed workers, tests) cannot fill the CUs a
@@ -415,10 +423,15 @@ class PeerShard:
         self.space._master_stale = True
 
     def gather_master(self, max_blocks: int = 256):
-        """Collective: complete the fp32 master from the owners' chunks (one barrier)."""
+        """Collective: complete the fp32 master from the owners' chunks.  Entry barrier, gather,
+        then an exit barrier: callers overwrite their own master chunk right after this (tail
+        local rounds, the next epoch's broadcast, the self-test restore), which must not happen
+        while a slower peer is still reading that chunk."""
         HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
                  ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 4, 1, 1, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
+                 self.chunk, 4, 1, 2, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
+        HIP.call("kml_zs_barrier", "p p p i i i d s", ctypes.addressof(self._flags), self.region, self.ctrl,
+                 self.rank, self.world, 0, self.timeout_s, self._stream())
         self.space._master_stale = False
 
     # ------------------------------------------------------------------ health

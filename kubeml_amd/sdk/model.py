@@ -173,10 +173,29 @@ class KubeModel(ABC):
             opt = old
         elif old is not None and opt is not old:
             self._graphs.clear()  # graphs captured the old optimizer's step
-            self._shards.clear()  # (a shard's fused update reads the optimizer's state too)
+            self._drop_shards()   # (a shard's fused update reads the optimizer's state too)
         self.optimizer = opt
         if opt is not None and hasattr(opt, "set_grad_scale"):
             opt.set_grad_scale(1.0)
+
+    def _drop_shards(self):
+        """Close the sharded-update transports of this model (collective: every worker runs the
+        same function code, so every rank changes its optimizer at the same point).  Unmaps the
+        peers' buffers and frees the barrier region instead of leaking them; a master left
+        sharded by the last step is completed first."""
+        if self._shards and self._flat is not None:
+            self._flat.sync_master()
+        for sh in list(self._shards.values()):
+            try:
+                sh.close()
+            except Exception:
+                try:
+                    sh._release()
+                except Exception:
+                    pass
+        self._shards.clear()
+        if self._flat is not None and getattr(self._flat, "master_sync", None) is not None:
+            self._flat.master_sync = None
 
     def _reset_optimizer_state(self):
         """Reference behaviour at every K-AVG round (network.py:121-128)."""
