@@ -823,6 +823,15 @@ static int pick_v(long long n8, int vmax) {
   while (r < v && r < vmax) r *= 2;
   return r;
 }
+// lower bound on V from the environment (tuning experiments: fewer, fuller blocks re-read the
+// partial rows fewer times); 1 = the default pick
+static int env_vmin(const char* name) {
+  const char* v = getenv(name);
+  const int r = v ? atoi(v) : 1;
+  return r == 2 || r == 4 || r == 8 ? r : 1;
+}
+static int vmin_fwd() { static const int v = env_vmin("KUBEML_BN_VMIN_FWD"); return v; }
+static int vmin_bwd() { static const int v = env_vmin("KUBEML_BN_VMIN_BWD"); return v < 4 ? v : 4; }
 static unsigned v_grid(long long n8, int V) {
   long long g = (n8 + (long long)TPB * V - 1) / ((long long)TPB * V);
   if (g > 1024) g = 1024;
@@ -1126,7 +1135,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
                                 hipStream_t s) {
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = pick_v(n8, 4);
+    const int V = max(pick_v(n8, 4), vmin_bwd());
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
 #define KML_BWD_V(VV)                                                                                          \
@@ -1177,7 +1186,7 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
   if (mode == 0 && stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = pick_v(n8, 8);
+    const int V = max(pick_v(n8, 8), stats_rows > 0 ? vmin_fwd() : 1);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
 #define KML_AP_V(VV)                                                                                           \

@@ -132,6 +132,10 @@ class ResNet(tnn.Module):
         blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
         for prev, b in zip([None] + blocks[:-1], blocks):
             object.__setattr__(b, "_kml_prev_ref", weakref.ref(prev) if prev is not None else None)
+        # forward fusion chain: a block may leave its output BN to the next block's first conv
+        for b, nxt in zip(blocks, blocks[1:] + [None]):
+            object.__setattr__(b, "_kml_next_ref", weakref.ref(nxt) if nxt is not None else None)
+        object.__setattr__(self, "_kml_blocks", blocks)
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -145,10 +149,26 @@ class ResNet(tnn.Module):
 
     def forward(self, x):
         """x: NHWC bf16 (channels padded to 8) on GPU, or NCHW float (converted)."""
-        x = self._head(x)
-        x = self.layer4(self.layer3(x))
+        with self._chain(x):
+            x = self._head(x)
+            x = self.layer4(self.layer3(x))
         x = self.avgpool(x)
         return self.fc(x)
+
+    def _chain(self, x):
+        """Training forward on the GPU: blocks may hand their output BN to the next block's
+        first conv (nn/fused.py cross-block fold); every deferred output is applied by the end."""
+        import contextlib
+        if x.is_cuda and self.training and torch.is_grad_enabled():
+            from ..nn.fused import chain
+            return chain(self._kml_blocks)
+        return contextlib.nullcontext()
+
+    def _chained(self, layer):
+        def run(h):
+            with self._chain(h):
+                return layer(h)
+        return run
 
     def _head(self, x):
         return self.layer2(self._stem_l1(x))
@@ -178,7 +198,8 @@ class ResNet(tnn.Module):
         the flat buffer, so each stage's gradients are one contiguous range.  Backward runs
         the stages in reverse, so the all-reduce that nothing can hide (the first stage's)
         carries only the stem + layer1 gradients (~1 % of ResNet-34's 87 MB)."""
-        return [self._stem_l1, self.layer2, self.layer3, lambda h: self.fc(self.avgpool(self.layer4(h)))]
+        return [self._chained(self._stem_l1), self._chained(self.layer2), self._chained(self.layer3),
+                lambda h: self.fc(self.avgpool(self._chained(self.layer4)(h)))]
 
     def stage_params(self):
         """Parameters owned by each stage of :meth:`stages`."""

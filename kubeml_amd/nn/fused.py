@@ -32,6 +32,11 @@ from .flat import grad_out, grad_out_pair, master_of, shadow_of
 # every BN backward takes its dgamma/dbeta partial rows from the dgrad epilogue that produced
 # its input gradient (False: its own reduction pass; tests compare the two)
 _BN_FUSE = True
+# ... and, where the conv's backward pair has a BN-folded instantiation (ops.kernels.bnb_ok), may
+# run inside that pair's dz staging instead of its own launch.  Opt-in (KUBEML_BNB_FOLD=1): exact,
+# but every block of the pair re-reads the partial rows from the other XCDs' writes, and the
+# ResNet-34 step measured 1.423 vs 1.331 ms/step without it (profiles/r5/bn_fold_ab.md)
+_BNB_FOLD = os.environ.get("KUBEML_BNB_FOLD", "0") == "1"
 
 
 def _wg_buf(conv, x):
@@ -185,6 +190,12 @@ class ConvBNUnit:
         w = shadow_of(conv.weight)
         kh, kw = conv.kernel_size
         K_out = w.shape[0]
+        wu = unrolled_for(conv, x) if _conv_bias(conv) is None else None
+        if wu is not None:    # the unrolled 1x1 form writes folded rows (never group-reduced)
+            G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, unroll=True)
+            stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
+            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, stats=stats, stats_part=True, wu=wu)
+            return c, stats, G
         G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, group=group)
         stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
         c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=_conv_bias(conv), stats=stats, stats_part=True,
@@ -192,10 +203,13 @@ class ConvBNUnit:
         return c, stats, G
 
     @staticmethod
-    def forward_folded(c_in, rows_in, G_in, bn_in, x_in, conv, bn, relu: bool, res: Optional[torch.Tensor]):
+    def forward_folded(c_in, rows_in, G_in, bn_in, x_in, conv, bn, relu: bool, res: Optional[torch.Tensor],
+                       defer: bool = False):
         """conv(relu(bn_in(c_in))) with bn_in applied inside the conv's patch staging
         (ops.kernels.conv_fwd_bnin), then this unit's own BN.  Returns (y, saved of the bn_in
-        unit, saved of this unit)."""
+        unit, saved of this unit).  defer: this unit's BN is NOT applied — y, mean and rstd are
+        empty buffers that the next block's first conv fills (:class:`PendingBN`), returned as the
+        4th element."""
         from ..ops import kernels as K
         C = c_in.shape[-1]
         y_in = torch.empty_like(c_in)
@@ -203,17 +217,41 @@ class ConvBNUnit:
         rstd_in = torch.empty_like(mean_in)
         w = shadow_of(conv.weight)
         K_out = w.shape[0]
-        G = K.conv_fwd_stats_rows(c_in.shape, K_out, 3, 3, (1, 1), (1, 1))
+        unrolled_for(conv, c_in)      # marks this forward's form (unrolled 2x2: GATHER22) for the backward
+        G = K.bnin_stats_rows(c_in.shape, K_out)
         stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=c_in.device)
         c = K.conv_fwd_bnin(c_in, w, rows_in, G_in, master_of(bn_in.weight), master_of(bn_in.bias), mean_in, rstd_in,
                             bn_in.running_mean, bn_in.running_var, bn_in.eps,
                             bn_in.momentum if bn_in.momentum is not None else 0.1, y_in, stats=stats, stats_part=True)
         mean = torch.empty(K_out, dtype=torch.float32, device=c_in.device)
         rstd = torch.empty_like(mean)
+        if defer:
+            y = torch.empty_like(c)
+            pend = PendingBN(y, c, stats, G, bn, res, mean, rstd, relu)
+            return y, (x_in, c_in, y_in, mean_in, rstd_in), (y_in, c, y if relu else None, mean, rstd), pend
         y = K.bn_apply(c, stats, master_of(bn.weight), master_of(bn.bias), res=res, save_mean=mean, save_rstd=rstd,
                        run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
                        momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
         return y, (x_in, c_in, y_in, mean_in, rstd_in), (y_in, c, y if relu else None, mean, rstd)
+
+    @staticmethod
+    def conv_rows_pending(pend, h, conv):
+        """conv_rows(h, conv) where h is the EMPTY output of the previous block (``pend``): the
+        previous block's last BN (+ residual + ReLU) is applied while this conv stages its input
+        (ops.kernels.conv_fwd_bnin with res), which also writes h, the BN's saved mean / rstd and
+        its running statistics.  Returns (c, rows, G) like conv_rows."""
+        from ..ops import kernels as K
+        bn = pend.bn
+        w = shadow_of(conv.weight)
+        K_out = w.shape[0]
+        unrolled_for(conv, h)         # this forward's form of conv (unrolled 2x2: GATHER22) for the backward
+        G = K.bnin_stats_rows(h.shape, K_out)
+        stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=h.device)
+        c = K.conv_fwd_bnin(pend.c, w, pend.rows, pend.G, master_of(bn.weight), master_of(bn.bias), pend.mean,
+                            pend.rstd, bn.running_mean, bn.running_var, bn.eps,
+                            bn.momentum if bn.momentum is not None else 0.1, h, stats=stats, stats_part=True,
+                            res=pend.res)
+        return c, stats, G
 
     @staticmethod
     def forward(x, conv, bn, relu: bool, res: Optional[torch.Tensor], training: bool):
@@ -252,14 +290,28 @@ class ConvBNUnit:
         here, its mask applied to dx, and the partials returned."""
         from ..ops import kernels as K
         x, c, y, mean, rstd = saved
-        dres = torch.empty_like(dy) if want_dres else None
-        dg, db, acc = grad_out_pair(bn.weight, bn.bias)
-        dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
-                      dg, db, dres=dres, partial=partial, accumulate=acc)
         kh, kw = conv.kernel_size
+        dg, db, acc = grad_out_pair(bn.weight, bn.bias)
+        wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
         dx, part_out = None, None
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
-        wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
+        if (_BNB_FOLD and partial is not None and need_dx and x.is_cuda and
+                K.bnb_ok(x.shape, c.shape[-1], kh, kw, conv.stride, conv.padding, partial[1], unroll=wu is not None)):
+            # the BN backward runs inside the conv pair's dz staging: no BN launch, and the
+            # residual gradient IS dy (the upstream dgrad already applied this BN's ReLU mask)
+            object.__setattr__(conv, "_kml_wu", None)
+            w = shadow_of(conv.weight)
+            dw, wacc = _wgrad_target(conv, x, wu is not None)
+            bnb = (c, partial[0], partial[1], mean, rstd, master_of(bn.weight), dg, db, acc)
+            r = K.conv_bwd(dy, w, x, dw, kh, kw, conv.stride, conv.padding, addend=addend, bnf=bnf, wu=wu,
+                           bnf_mask=True, accumulate=wacc, bnb=bnb)
+            if wu is not None:
+                conv.weight._kml_flat.defer_fold22(conv.weight, dw)
+            dx, part_out = r if bnf is not None else (r, None)
+            return dx, (dy if want_dres else None), part_out
+        dres = torch.empty_like(dy) if want_dres else None
+        dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
+                      dg, db, dres=dres, partial=partial, accumulate=acc)
         object.__setattr__(conv, "_kml_wu", None)
         if need_dx:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
@@ -284,6 +336,69 @@ class ConvBNUnit:
         return dx, dres, part_out
 
 
+class PendingBN:
+    """A residual block's output BN (+ residual + ReLU) left unapplied for the next block's first
+    conv to apply while staging its input (cross-block fold, :func:`_defer_target`).  ``y`` is
+    the block output buffer, still empty; :meth:`materialize` is the fallback (one BN apply)."""
+    __slots__ = ("y", "c", "rows", "G", "bn", "res", "mean", "rstd", "relu")
+
+    def __init__(self, y, c, rows, G, bn, res, mean, rstd, relu):
+        self.y, self.c, self.rows, self.G, self.bn = y, c, rows, G, bn
+        self.res, self.mean, self.rstd, self.relu = res, mean, rstd, relu
+
+    def materialize(self):
+        from ..ops import kernels as K
+        bn = self.bn
+        K.bn_apply(self.c, self.rows, master_of(bn.weight), master_of(bn.bias), y=self.y, res=self.res,
+                   save_mean=self.mean, save_rstd=self.rstd, run_mean=bn.running_mean, run_var=bn.running_var,
+                   eps=bn.eps, momentum=bn.momentum if bn.momentum is not None else 0.1, relu=self.relu,
+                   stats_rows=self.G)
+
+
+# cross-block fold: a BasicBlock's output BN + residual + ReLU is applied by the next block's first
+# conv (halo / one-shot BN-in staging) instead of its own launch.  Only inside a model forward that
+# drives the chain (``chain()``: ResNet.forward), so a block called on its own never defers.
+_CROSS_FOLD = os.environ.get("KUBEML_CROSS_FOLD", "1") != "0"
+_CHAIN = [0]
+
+
+class chain:
+    """Context of a model forward whose blocks may defer their output BN to the next block."""
+
+    def __init__(self, blocks):
+        self.blocks = blocks
+
+    def __enter__(self):
+        _CHAIN[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _CHAIN[0] -= 1
+        for b in self.blocks:   # safety: a deferred output nobody consumed is applied here
+            pend = getattr(b, "_kml_pend_in", None)
+            if pend is not None:
+                object.__setattr__(b, "_kml_pend_in", None)
+                pend.materialize()
+        return False
+
+
+def _defer_target(block, out_shape):
+    """The next block if it will apply this block's output BN in its first conv, else None."""
+    if not (_CROSS_FOLD and _BN_FOLD and _CHAIN[0] > 0):
+        return None
+    ref = getattr(block, "_kml_next_ref", None)
+    nxt = ref() if ref is not None else None
+    if nxt is None or not nxt.training or any(u[3] == "short" for u in nxt._kml_plan):
+        return None
+    from ..ops import kernels as K
+    if _fold_unit_shape(out_shape, nxt._kml_plan) is None:
+        return None
+    conv1 = nxt._kml_plan[0][0]
+    if conv1.kernel_size != (3, 3) or tuple(conv1.stride) != (1, 1) or tuple(conv1.padding) != (1, 1):
+        return None
+    return nxt if K.bnin_ok(out_shape, shadow_of(conv1.weight).shape[0], 3, 3, (1, 1), (1, 1)) else None
+
+
 class BlockFn(Function):
     """Autograd node for a residual block described by a ``plan`` of units.
 
@@ -299,6 +414,12 @@ class BlockFn(Function):
         plan = block._kml_plan
         saved = [None] * len(plan)
         fold = _fold_unit(x, plan)      # index of a main unit whose BN + ReLU the next conv applies
+        # the previous block's output BN, deferred to this block's first conv (x is still empty)
+        pend_in = getattr(block, "_kml_pend_in", None)
+        object.__setattr__(block, "_kml_pend_in", None)
+        if pend_in is not None and (pend_in.y.data_ptr() != x.data_ptr() or fold != 0):
+            pend_in.materialize()
+            pend_in = None
         h = x
         short = None
         pending = None
@@ -306,12 +427,20 @@ class BlockFn(Function):
             if role == "short":
                 short, saved[i] = ConvBNUnit.forward(x, conv, bn, relu, None, training)
             elif i == fold:
-                c, rows, G = ConvBNUnit.conv_rows(h, conv, group=_FOLD_GROUP)
+                if pend_in is not None:
+                    c, rows, G = ConvBNUnit.conv_rows_pending(pend_in, h, conv)
+                    pend_in = None
+                else:
+                    c, rows, G = ConvBNUnit.conv_rows(h, conv, group=_FOLD_GROUP)
                 pending = (i, h, c, rows, G, bn)
             elif pending is not None:   # the conv right after the folded unit ("last": + residual)
                 j, x_in, c_in, rows, G, bn_in = pending
                 res = (short if short is not None else x) if role == "last" else None
-                h, saved[j], saved[i] = ConvBNUnit.forward_folded(c_in, rows, G, bn_in, x_in, conv, bn, relu, res)
+                nxt = _defer_target(block, (x.shape[0],) + _out_hw_c(c_in.shape, conv)) if role == "last" else None
+                r = ConvBNUnit.forward_folded(c_in, rows, G, bn_in, x_in, conv, bn, relu, res, defer=nxt is not None)
+                h, saved[j], saved[i] = r[:3]
+                if nxt is not None:
+                    object.__setattr__(nxt, "_kml_pend_in", r[3])
                 pending = None
             elif role == "last":
                 res = short if short is not None else x
@@ -377,11 +506,22 @@ class BlockFn(Function):
         return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
+def _out_hw_c(c_in_shape, conv):
+    """(OH, OW, Cout) of a 3x3 / s1 / p1 conv on a c_in_shape input (shape-preserving)."""
+    return (c_in_shape[1], c_in_shape[2], shadow_of(conv.weight).shape[0])
+
+
 def _fold_unit(x, plan):
     """Index of the BasicBlock's first unit when its BN + ReLU can run inside the second conv's
     halo patch staging (training, GPU, 3x3/s1 halo-eligible second conv), else None."""
-    from ..ops import kernels as K
     if not (_BN_FOLD and x.is_cuda):
+        return None
+    return _fold_unit_shape(tuple(x.shape), plan)
+
+
+def _fold_unit_shape(xshape, plan):
+    from ..ops import kernels as K
+    if not _BN_FOLD:
         return None
     mains = [i for i, u in enumerate(plan) if u[3] != "short"]
     if len(mains) != 2:
@@ -393,13 +533,18 @@ def _fold_unit(x, plan):
         return None          # the BN-folding halo conv has no bias epilogue
     if not relu1 or conv2.kernel_size != (3, 3) or tuple(conv2.stride) != (1, 1) or tuple(conv2.padding) != (1, 1):
         return None
-    B, H, W, _ = x.shape
+    B, H, W, _ = xshape
     kh, kw = conv1.kernel_size
     OH, OW = K.out_hw(H, W, kh, kw, conv1.stride[0], conv1.stride[1], conv1.padding[0], conv1.padding[1])
     shape1 = (B, OH, OW, shadow_of(conv1.weight).shape[0])
-    if K.unrolled22(H, W, kh, kw, conv1.stride, conv1.padding):
+    if K.unrolled22(H, W, kh, kw, conv1.stride, conv1.padding) and not _FOLD_UNROLLED:
         return None
     return i1 if K.bnin_ok(shape1, shadow_of(conv2.weight).shape[0], 3, 3, (1, 1), (1, 1)) else None
+
+
+# the folded conv1 may itself run unrolled (2x2 maps: its folded statistics rows feed the one-shot
+# BN-in conv2 like any rows); False: layer3's blocks keep their separate bn1 apply (tests)
+_FOLD_UNROLLED = True
 
 
 def block_params(block) -> List[torch.nn.Parameter]:
