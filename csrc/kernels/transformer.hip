@@ -631,3 +631,73 @@ KML_API int kml_scatter_rows(const bf16_t* src, const long long* idx, bf16_t* ds
                      accumulate);
   KML_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------------------------------
+// BERT masked-LM batch preparation on the device (Google BERT's recipe): per sequence, P of
+// the L positions are chosen uniformly without replacement (the P largest keys of a hash of
+// (seed, step, token), ties broken by position), listed in increasing order; each chosen token
+// becomes [MASK] with probability 0.8, a uniformly random token with 0.1, and stays with 0.1.
+// One block per sequence: keys in LDS, rank = count of larger keys (O(L^2 / threads)), slot =
+// count of chosen positions before it.  ctr = [seed, step] (fp32, the RNGState layout); with a
+// ticket the last block to finish advances ctr[1] (every block read it first), so a captured
+// step draws a fresh mask at every replay.  Replaces the eager topk / sort / rand / where /
+// scatter chain of the reference-style function (examples/function_bert.py).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mlm_mask(const long long* __restrict__ ids, long long* __restrict__ xout,
+                                                  long long* __restrict__ pos, long long* __restrict__ lab,
+                                                  float* __restrict__ ctr, unsigned* __restrict__ ticket, int L, int P,
+                                                  long long mask_id, long long vocab) {
+  __shared__ unsigned key[2048];
+  __shared__ unsigned char sel[2048];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const unsigned seed = (unsigned)ctr[0], step = (unsigned)ctr[1];
+  const long long* row = ids + (long long)b * L;
+  for (int l = tid; l < L; l += 256) key[l] = hash3(seed ^ 0x6D61736Bu, step, (unsigned)(b * L + l));
+  __syncthreads();
+  for (int l = tid; l < L; l += 256) {
+    const unsigned k = key[l];
+    int rank = 0;
+    for (int j = 0; j < L; ++j) {
+      const unsigned kj = key[j];
+      rank += (kj > k) || (kj == k && j < l);
+    }
+    sel[l] = rank < P ? 1 : 0;
+  }
+  __syncthreads();
+  for (int l = tid; l < L; l += 256) {
+    const long long t = row[l];
+    long long o = t;
+    if (sel[l]) {
+      int slot = 0;
+      for (int j = 0; j < l; ++j) slot += sel[j];
+      const unsigned r = hash3(seed ^ 0x72706C63u, step, (unsigned)(b * P + slot));
+      const float u = (float)(r >> 8) * (1.0f / 16777216.0f);
+      if (u < 0.8f) o = mask_id;
+      else if (u < 0.9f) o = (long long)(hash3(seed ^ 0x746F6B6Eu, step, (unsigned)(b * P + slot)) % (unsigned)vocab);
+      pos[(long long)b * P + slot] = l;
+      lab[(long long)b * P + slot] = t;
+    }
+    xout[(long long)b * L + l] = o;
+  }
+  if (ticket) {
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      const unsigned t = atomicAdd(ticket, 1u);
+      if (t == gridDim.x - 1) {
+        ctr[1] = (float)(step + 1u);
+        atomicExch(ticket, 0u);
+      }
+    }
+  }
+}
+
+// ids / xout [B][L], pos / lab [B][P] int64; L <= 2048, 1 <= P <= L.  ticket: null = the step
+// counter is not advanced (a fixed evaluation mask)
+KML_API int kml_mlm_mask(const long long* ids, long long* xout, long long* pos, long long* lab, float* ctr,
+                         unsigned* ticket, int B, int L, int P, long long mask_id, long long vocab, hipStream_t s) {
+  if (B < 1 || L < 1 || L > 2048 || P < 1 || P > L || vocab < 1 || !ids || !xout || !pos || !lab || !ctr)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_mlm_mask, dim3(B), dim3(256), 0, s, ids, xout, pos, lab, ctr, ticket, L, P, mask_id, vocab);
+  KML_LAUNCH_CHECK();
+}

@@ -12,6 +12,13 @@ predicted; of those 80 % become [MASK], 10 % a random token, 10 % stay.
 Model: HuggingFace-layout BertForMaskedLM (kubeml_amd/models/bert.py) on the hand-written
 MFMA GEMM / flash-attention kernels; optimizer AdamW (fused single launch on the GPU).
 Validation reports masked-token accuracy (%) and MLM loss.
+
+GPU path: masking (one HIP kernel, ``kernels.mlm_mask``: a fresh mask per replay from a device
+counter), forward, loss, backward and AdamW of a batch are ONE hipGraph replay
+(``self.step(..., forward=...)``); validation is a captured eval forward with a fixed mask.
+Train with ``kubeml train -f bert --K 1 --grad-sync`` for synchronous data parallelism with
+persistent Adam moments (the reference semantics — an optimizer rebuilt every round — would
+make every AdamW step a first step).  CPU workers run the same recipe with stock torch ops.
 """
 from typing import Tuple
 
@@ -56,10 +63,35 @@ def mask_tokens(ids: torch.Tensor, gen: torch.Generator):
     return x, pos.contiguous(), lab.contiguous()
 
 
+def _preds(L):
+    return min(MAX_PREDS, max(1, int(round(L * MASK_FRAC))))
+
+
 class KubeBert(KubeModel):
     def __init__(self, network, dataset):
         super().__init__(network, dataset, gpu=True)
         self._gen = None
+        self._ctr = {}     # "train" / "val" -> device [seed, step] of the masking kernel
+
+        # captured with the step / eval graphs, so created once (their identity keys the graphs)
+        def fwd_train(net, ids, seg):
+            from kubeml_amd.ops import kernels as K
+            x, pos, lab = K.mlm_mask(ids, self._counter("train"), _preds(ids.shape[1]), MASK_ID, VOCAB)
+            return net(x, mlm_positions=pos, labels=lab)
+
+        def fwd_val(net, ids, seg):
+            from kubeml_amd.ops import kernels as K
+            x, pos, lab = K.mlm_mask(ids, self._counter("val"), _preds(ids.shape[1]), MASK_ID, VOCAB, advance=False)
+            loss, correct = net(x, mlm_positions=pos, labels=lab, return_correct=True)
+            return correct, loss
+        self._fwd_train, self._fwd_val = fwd_train, fwd_val
+
+    def _counter(self, split):
+        t = self._ctr.get(split)
+        if t is None or t.device != self.device:
+            seed = 1 + self.args._func_id + (7919 if split == "val" else 0)
+            t = self._ctr[split] = torch.tensor([float(seed), 0.0], dtype=torch.float32, device=self.device)
+        return t
 
     def _generator(self):
         if self._gen is None or self._gen.device != self.device:
@@ -70,16 +102,21 @@ class KubeBert(KubeModel):
         return AdamW(self.parameters(), lr=self.lr, weight_decay=0.01)
 
     def train(self, batch, batch_index) -> float:
-        ids, _ = batch
+        ids, seg = batch
+        if ids.is_cuda:
+            return self.step(ids, seg, forward=self._fwd_train)   # device loss: read back once per task
         x, pos, lab = mask_tokens(ids, self._generator())
         self.optimizer.zero_grad()
         loss = self(x, mlm_positions=pos, labels=lab)
         loss.backward()
         self.optimizer.step()
-        return loss.detach()   # device tensor: read back once per task
+        return loss.detach()
 
     def validate(self, batch, batch_index) -> Tuple[float, float]:
-        ids, _ = batch
+        ids, seg = batch
+        if ids.is_cuda:
+            correct, loss = self.evaluate(ids, seg, forward=self._fwd_val)
+            return correct * 100 / (ids.shape[0] * _preds(ids.shape[1])), loss
         x, pos, lab = mask_tokens(ids, self._generator())
         loss, correct = self(x, mlm_positions=pos, labels=lab, return_correct=True)
         return correct * 100 / lab.numel(), loss

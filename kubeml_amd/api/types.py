@@ -59,7 +59,12 @@ class TrainOptions(_Json):
     k: int = -1
     goal_accuracy: float = 100.0
     resume_from: str = ""   # extension: continue a finished/failed job from its checkpoint
-    _OMIT_EMPTY = ("resume_from",)
+    # extension: "grad" = K=1 rounds as synchronous data parallelism with PERSISTENT optimizer
+    # state (Adam moments, momentum carry across rounds).  A deliberate departure from the
+    # reference, which rebuilds the optimizer every round (network.py:208-217) — with Adam
+    # that makes every step a first step.  "" = the reference semantics.
+    sync: str = ""
+    _OMIT_EMPTY = ("resume_from", "sync")
 
 
 @dataclass

@@ -68,7 +68,7 @@ def cmd_train(a):
                        function_name=a.function,
                        options=TrainOptions(default_parallelism=a.parallelism, static_parallelism=a.static,
                                             validate_every=a.validate_every, k=K, goal_accuracy=a.goal_accuracy,
-                                            resume_from=a.resume or ""))
+                                            resume_from=a.resume or "", sync="grad" if a.grad_sync else ""))
     # validateTrainRequest (train.go:150-172)
     if not (0 < req.batch_size <= MAX_BATCH):
         raise KubeMLException(f"batch size must be between 1 and {MAX_BATCH}", 400)
@@ -76,6 +76,8 @@ def cmd_train(a):
         raise KubeMLException("epochs must be positive", 400)
     if req.lr <= 0:
         raise KubeMLException("learning rate must be positive", 400)
+    if req.options.sync == "grad" and req.options.k != 1:
+        raise KubeMLException("--grad-sync runs K = 1 rounds: pass --K 1", 400)
     c.datasets.get(req.dataset)
     if not any(f["name"] == req.function_name for f in c.functions.list()):
         raise KubeMLException(f"function {req.function_name} does not exist", 404)
@@ -248,6 +250,9 @@ def build_parser() -> argparse.ArgumentParser:
     t.add_argument("--goal-accuracy", type=float, default=100.0)
     t.add_argument("--wait", action="store_true", help="block until the job ends, print its history")
     t.add_argument("--resume", default=None, help="continue from the checkpoint/history of this job id")
+    t.add_argument("--grad-sync", action="store_true",
+                   help="K=1 as synchronous data parallelism with persistent optimizer state (any fused "
+                        "optimizer, e.g. AdamW); default: the reference's per-round optimizer reset")
     t.set_defaults(fn=cmd_train)
 
     d = sub.add_parser("dataset", help="manage datasets").add_subparsers(dest="sub", required=True)

@@ -95,9 +95,12 @@ class TrainJob:
         self.req = task.request
         opts = self.req.options
         self.static = bool(opts.static_parallelism)
+        # capture the workers' graphs during initialisation (KUBEML_WARM=0: inside epoch 1)
+        self.warm = os.environ.get("KUBEML_WARM", "1") != "0"
         self.validate_every = int(opts.validate_every)
         self.goal_accuracy = float(opts.goal_accuracy)
         self.K = int(opts.k)
+        self.sync = str(getattr(opts, "sync", "") or "")
         self.code_path = code_path
         self.store_dir = store_dir
         self.pool_factory = pool_factory
@@ -167,6 +170,8 @@ class TrainJob:
         m = {"op": "task", "kind": kind, "job": self.id, "function": self.req.function_name,
              "code_path": self.code_path, "N": self.parallelism, "K": self.K, "batch_size": self.req.batch_size,
              "lr": self.req.lr, "epoch": self.epoch}
+        if self.sync:
+            m["sync"] = self.sync
         m.update(kw)
         return m
 
@@ -213,7 +218,26 @@ class TrainJob:
             self._resume()
         else:
             self._checkpoint(wait=True)   # the recovery base: confirmed on disk before epoch 1
+        self._warm()
         return layers
+
+    def _warm(self):
+        """Part of initialisation (before the clock starts, as init is in job.go:173-183): every
+        worker of the first epoch captures the train-step and eval graphs of its batch shapes
+        (KubeModel._warm; no update is applied).  Best effort: a failure only costs the
+        capture time inside epoch 1."""
+        if not self.warm:
+            return
+        try:
+            P = self.parallelism
+            res = self._fanout("warm", list(range(P)), N=P, restore=self._pending_restore)
+            bad = {r: v.get("error") for r, v in res.items() if not v.get("ok")}
+            if bad:
+                self.log.warn("warm-up failed on some workers", errors=bad)
+            else:
+                self.log.info("workers warm", shapes={str(r): v.get("result") for r, v in sorted(res.items())})
+        except Exception as e:
+            self.log.warn("warm-up skipped", error=repr(e))
 
     def _resume(self):
         """Continue job ``resume_from``: its checkpoint becomes this job's starting model

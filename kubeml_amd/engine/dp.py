@@ -31,7 +31,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
                     extra_state: Sequence[torch.Tensor] = (), comm_dtype=None,
                     opt_overlap: Optional[bool] = None, advance=None, plan=None, peer=None,
-                    comm_timing: int = 0) -> GraphedTrainStep:
+                    comm_timing: int = 0, forward: Optional[Callable] = None) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
     pre():  runs first inside the step (e.g. on-device augmentation into ``x``)
@@ -58,6 +58,9 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             creates one sized for the flat gradient — collective over ``group``.
     comm_timing: T > 0 stamps the collectives on the device every step and samples their time
             every T-th step (``step.comm_seconds()``; exported as kubeml_allreduce_seconds)
+    forward: ``forward(model, x, y) -> loss`` in place of ``loss_fn(model(x), y)`` (models whose
+            call takes more than the batch, e.g. BERT MLM with its positions and labels, or a
+            step that prepares its batch on the device first); the step is then not stage-split
     """
     comm = world > 1 or force_comm
     shard = None
@@ -111,7 +114,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             post()
 
     segs = seg_grads = seg_opt = opt_finish = None
-    staged_ok = hasattr(model, "stages") and hasattr(model, "stage_params")
+    staged_ok = forward is None and hasattr(model, "stages") and hasattr(model, "stage_params")
     opt_overlap = bool(opt_overlap and staged_ok and use_graph and (graph_comm or not comm) and peer is None
                        and getattr(optimizer, "supports_ranges", lambda: False)())
     if advance is not None:
@@ -165,7 +168,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             if pre is not None:
                 pre()
             space.zero_grad()
-            loss = loss_fn(model(x), y)
+            loss = forward(model, x, y) if forward is not None else loss_fn(model(x), y)
             backward_loss(loss)
             space.finish_grads()
             return loss

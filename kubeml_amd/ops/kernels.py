@@ -1557,6 +1557,24 @@ def row_index(pos, L):
     return out
 
 
+def mlm_mask(ids, ctr, P, mask_id=103, vocab=30522, advance=True, out=None):
+    """BERT MLM masking on the device (kml_mlm_mask): ids [B, L] int64 -> (masked ids [B, L],
+    positions [B, P] ascending, labels [B, P]); P positions per sequence chosen uniformly without
+    replacement, 80 % -> mask_id, 10 % -> random token, 10 % kept.  ctr: the [seed, step] fp32
+    device tensor; advance: the kernel's last block bumps ctr[1] (fresh masks per replay)."""
+    _chk(ids, torch.int64, "ids", 2)
+    _chk(ctr, F32, "ctr")
+    B, L = ids.shape
+    if out is None:
+        out = (torch.empty_like(ids), torch.empty((B, P), dtype=torch.int64, device=ids.device),
+               torch.empty((B, P), dtype=torch.int64, device=ids.device))
+    x, pos, lab = out
+    tk = _COUNTERS.take(ids.device, 1) if advance else None
+    HIP.call("kml_mlm_mask", "p p p p p p i i i l l s", _p(ids), _p(x), _p(pos), _p(lab), _p(ctr), _p(tk), B, L,
+             int(P), int(mask_id), int(vocab), _s())
+    return x, pos, lab
+
+
 def add_i64_(t, v=1):
     HIP.call("kml_add_i64", "p l i s", _p(t), int(v), t.numel(), _s())
 

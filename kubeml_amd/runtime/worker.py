@@ -193,6 +193,7 @@ class Worker:
                           comm=self.comm.sub(P) if P > 1 else _local(), store=self.store,
                           store_dir=self.store_dir, device=self.device, checkpoint=msg.get("checkpoint"))
         ctx.extra["restore"] = msg.get("restore")
+        ctx.extra["sync"] = msg.get("sync", "")
         if msg.get("restore") or kind == "infer":
             self._flush_checkpoint()         # the file a restore / inference reads is complete
         token = set_task(ctx)

@@ -50,7 +50,8 @@ class _KubeArgs:
     """Task arguments of the current invocation (reference dataset.py:24-78)."""
 
     def __init__(self, job_id: str, N: int, K: int, task: str, func_id: int, epoch: int, lr: float = 0,
-                 batch_size: int = 0):
+                 batch_size: int = 0, sync: str = ""):
+        self._sync = sync          # extension: "grad" = persistent-state synchronous K=1 (TrainOptions.sync)
         self._job_id = job_id
         self._N = N
         self._K = K
@@ -66,7 +67,8 @@ class _KubeArgs:
         if ctx is None:
             from ..api.errors import InvalidArgsError
             raise InvalidArgsError(RuntimeError("no task context: invoke through a kubeml worker"))
-        return cls(ctx.job_id, ctx.N, ctx.K, ctx.task, ctx.func_id, ctx.epoch, ctx.lr, ctx.batch_size)
+        return cls(ctx.job_id, ctx.N, ctx.K, ctx.task, ctx.func_id, ctx.epoch, ctx.lr, ctx.batch_size,
+                   str(ctx.extra.get("sync", "") or ""))
 
 
 class _RowSpan:

@@ -91,6 +91,7 @@ class KubeModel(ABC):
         self._grad_comm = None
         self._synced_steps = 0
         self.sync_seconds = 0.0
+        self._dry = False              # job warm-up (_warm): step / evaluate capture only
         ctx = current_task()
         if ctx is not None:
             ctx.extra["kubemodel"] = self
@@ -140,6 +141,8 @@ class KubeModel(ABC):
             return {"loss": loss, "accuracy": acc, "length": length}
         if self.task == "infer":
             return {"predictions": self._infer()}
+        if self.task == "warm":
+            return {"warmed": self._warm()}
         raise KubeMLException(f"Task {self.task} not recognized", 400)
 
     # ---- init (network.py:174-189) --------------------------------------------------------
@@ -229,8 +232,13 @@ class KubeModel(ABC):
     def _on_train_end(self):
         pass
 
+    def _persistent(self) -> bool:
+        """TrainOptions.sync == "grad": optimizer state persists across K=1 rounds."""
+        return self.args is not None and getattr(self.args, "_sync", "") == "grad"
+
     def _on_iteration_start(self):
-        self._reset_optimizer_state()
+        if not self._persistent():
+            self._reset_optimizer_state()
 
     def _on_iteration_end(self):
         pass
@@ -278,6 +286,10 @@ class KubeModel(ABC):
             return False
         if self.device.type == "cuda" and getattr(comm, "group", "missing") == "missing":
             return False      # the captured collectives need a torch.distributed group
+        if self._persistent():
+            # persistent state: a gradient step on the averaged gradient IS the update of
+            # synchronous data parallelism for any optimizer (Adam / AdamW moments included)
+            return True
         return getattr(self.optimizer, "kind", None) == "sgd" or type(self.optimizer) is torch.optim.SGD
 
     # ---- train (network.py:252-310, K-AVG) ------------------------------------------------
@@ -325,6 +337,8 @@ class KubeModel(ABC):
                 _progress()
                 if r == full_rounds and self._flat is not None:
                     self._flat.sync_master()   # sharded update -> local rounds read the whole master
+                    if grad_ok and self._persistent():
+                        self._sync_optimizer_state(comm)
                 participate = r < len(intervals)
                 self._sync_mode = "grad" if (grad_ok and r < full_rounds) else "local"
                 self._synced_steps = 0
@@ -412,6 +426,26 @@ class KubeModel(ABC):
             tot += t.detach().double().abs().sum().cpu()
         return float(tot)
 
+    def _sync_optimizer_state(self, comm):
+        """Before ragged-tail local rounds of a persistent-state job: a sharded update (engine/dp.py
+        shard plan) kept the optimizer state current only on each rank's own chunk; every rank
+        zeroes the rest and one SUM all-reduce per state buffer gives all ranks the owners'
+        values (a no-op collective when the state is already replicated)."""
+        sh = self._shards.get(id(comm))
+        if sh is None or sh.region is None or self._flat is None or not hasattr(self.optimizer, "_bufs"):
+            return
+        names = list(getattr(self.optimizer, "_STATE_NAMES", ()) or ())
+        if not names:
+            return
+        bufs = self.optimizer._bufs(self._flat, names)
+        for name in names:
+            t = bufs[name]
+            if sh.lo > 0:
+                t[:sh.lo].zero_()
+            if sh.hi < t.numel():
+                t[sh.hi:].zero_()
+            comm.all_reduce_(t)
+
     def _allreduce_grads_eager(self):
         """Eager (CPU / no-graph) gradient average over the grad-sync group."""
         comm = self._grad_comm
@@ -435,6 +469,74 @@ class KubeModel(ABC):
         comm = self._grad_comm
         if self._flat is not None and comm is not None and self.device.type == "cuda":
             comm.all_reduce_(self._flat.grad)
+
+    # ---- job-initialisation warm-up (runs before the job's clock, like init) -----------------
+    def _warm(self) -> int:
+        """Capture, before the first epoch, the hipGraphs the job's epochs will replay: the
+        train step for every minibatch shape of this worker's first epoch, and the eval
+        forward for every validation batch shape.  The epoch's batches are planned exactly as
+        ``_train`` / ``_validate`` plan them (the resident split uploads the worker's shard to
+        HBM here, during initialisation), and each NEW batch shape runs the user's ``train`` /
+        ``validate`` once in *dry* mode: ``step`` / ``evaluate`` build and capture their graph
+        (capture never mutates training state: engine/step.py) but replay nothing, so the
+        model, the optimizer and the BN statistics are untouched.  The reference has no graphs
+        to build; its clock (ml/pkg/train/job.go:183) also starts after initialisation.
+        Returns the number of graphs captured."""
+        self._on_train_start()
+        if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
+            return 0
+        comm = self._comm()
+        N, fid, K = self.args._N, self.args._func_id, self.args._K
+        bs = self.batch_size
+        assigned = split_minibatches(range(self._dataset.num_docs), N)[fid]
+        per = max(get_subset_period(K, bs, assigned), 1)
+        intervals = [(i, min(assigned.stop, i + per)) for i in range(assigned.start, assigned.stop, per)]
+        grad_ok = self._grad_sync_ok(comm, K)
+        if grad_ok:
+            self._grad_comm = comm
+            self._prime_grad_sync()
+        done = 0
+        self._dry = True
+        try:
+            self._sync_mode = "grad" if grad_ok else "local"
+            seen = set()
+            streamed = self._dataset._plan_stream("train", intervals, bs, self.device)
+            # a resident / streamed split yields batches as device views (cheap to walk); a host
+            # loader only walks the first and the last interval (the shapes a ragged end adds)
+            scan = intervals if streamed else list(dict.fromkeys([intervals[0], intervals[-1]])) if intervals else []
+            for i, e in scan:
+                self._dataset._load_train_data(start=i, end=e)
+                for batch in self._batches():
+                    shape = tuple(getattr(batch[0], "shape", ())) if isinstance(batch, (tuple, list)) else None
+                    if shape in seen:
+                        continue
+                    seen.add(shape)
+                    self.train(self._batch_to_device(batch), 0)
+                    done += 1
+            self._dataset._stream_end()
+            self._sync_mode = "local"
+            if self._dataset.num_val_docs:
+                va = split_minibatches(range(self._dataset.num_val_docs), N)[fid]
+                seen = set()
+                self._network.eval()
+                with torch.no_grad():
+                    self._dataset._plan_stream("test", [(va.start, va.stop)], bs, self.device)
+                    self._dataset._load_validation_data(start=va.start, end=va.stop)
+                    for batch in self._batches():
+                        shape = tuple(getattr(batch[0], "shape", ())) if isinstance(batch, (tuple, list)) else None
+                        if shape in seen:
+                            continue
+                        seen.add(shape)
+                        self.validate(self._batch_to_device(batch), 0)
+                        done += 1
+                    self._dataset._stream_end()
+                self._network.train()
+        finally:
+            self._dry = False
+            self._sync_mode = "local"
+            self._grad_comm = None
+        torch.cuda.synchronize(self.device)
+        return done
 
     # ---- validation (network.py:320-360) --------------------------------------------------
     def _on_validation_start(self):
@@ -515,16 +617,19 @@ class KubeModel(ABC):
     PEER_CHECK_EVERY = int(os.environ.get("KUBEML_PEER_CHECK_EVERY", "16"))
     COMM_TIMING = int(os.environ.get("KUBEML_COMM_TIMING", "50"))   # sample the in-graph all-reduce every N steps
 
-    def step(self, x, y, loss_fn=None):
+    def step(self, x, y, loss_fn=None, forward=None):
         """forward + loss + backward + optimizer step for one batch; on the GPU the first
         call for a given batch shape captures a hipGraph (engine/dp.py) that later calls
         replay.  In a K=1 grad-sync round the gradients are all-reduced over the worker
-        group inside the step.  Returns the (device) loss tensor."""
+        group inside the step.  Returns the (device) loss tensor.  forward: optional
+        ``forward(network, x, y) -> loss`` replacing ``loss_fn(network(x), y)`` — e.g. on-device
+        batch preparation (masking) followed by a model call with extra arguments; it is part
+        of the captured graph, so it must be a function of x, y and device state only."""
         from ..nn import backward_loss, cross_entropy
         loss_fn = loss_fn or cross_entropy
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
             self.optimizer.zero_grad()
-            loss = loss_fn(self(x), y)
+            loss = forward(self._network, x, y) if forward is not None else loss_fn(self(x), y)
             loss.backward()
             if self._sync_mode == "grad":
                 self._allreduce_grads_eager()
@@ -533,11 +638,13 @@ class KubeModel(ABC):
             return loss
         grad = self._sync_mode == "grad"
         comm = self._grad_comm if grad else None
-        key = (tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(loss_fn), grad,
+        key = (tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(forward or loss_fn), grad,
                id(comm) if comm is not None else None)
         g = self._graphs.get(key)
         if g is None:
-            g = self._build_step(key, x, y, loss_fn, comm)
+            g = self._build_step(key, x, y, loss_fn, comm, forward)
+        if self._dry:                 # job warm-up: graph built and captured, nothing replayed
+            return torch.zeros((), dtype=torch.float32, device=x.device)
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
         loss = g["step"]()
@@ -545,7 +652,7 @@ class KubeModel(ABC):
             self._synced_steps += 1
         return loss
 
-    def _build_step(self, key, x, y, loss_fn, comm):
+    def _build_step(self, key, x, y, loss_fn, comm, forward=None):
         """Build and capture the train-step graph for one batch shape (+ comm group)."""
         with trace.span("step_graph", shape=str(tuple(x.shape)), comm=comm.world if comm is not None else 1):
             from ..engine.dp import make_train_step
@@ -560,7 +667,8 @@ class KubeModel(ABC):
             st = make_train_step(self._network, self._flat, self.optimizer, loss_fn, xs, ys,
                                  group=comm.group if comm is not None else None,
                                  world=comm.world if comm is not None else 1,
-                                 plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0)
+                                 plan=plan, peer=peer, comm_timing=self.COMM_TIMING if comm is not None else 0,
+                                 forward=forward)
             self.logger.info("train step graph: batch %s, comm %s, plan %s, transport %s", tuple(x.shape),
                              comm.world if comm is not None else 1, plan.tag() if plan is not None else None,
                              type(st.peer).__name__ if st.peer is not None else None)
@@ -593,17 +701,20 @@ class KubeModel(ABC):
         comm.grad_peer = None
         return None
 
-    def evaluate(self, x, y, loss_fn=None):
+    def evaluate(self, x, y, loss_fn=None, forward=None):
         """Eval-mode forward + loss + correct count for one validation batch -> (correct,
         loss) as device tensors.  On the GPU the first call per batch shape captures the
         forward into a hipGraph that later calls replay: a validation pass is then one replay
         per batch instead of ~80 host-issued launches (host-bound at the reference's batch
         sizes).  Weights and BN running statistics are read in place, so every replay sees
-        the current model."""
+        the current model.  forward: optional ``forward(network, x, y) -> (correct, loss)``
+        replacing the classifier default (captured like the default)."""
         from ..nn import cross_entropy
         loss_fn = loss_fn or cross_entropy
 
         def fwd(xx, yy):
+            if forward is not None:
+                return forward(self._network, xx, yy)
             out = self._network(xx)
             if loss_fn is cross_entropy:
                 return loss_fn(out, yy, return_correct=True)[::-1]
@@ -612,7 +723,7 @@ class KubeModel(ABC):
 
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
             return fwd(x, y)
-        key = ("eval", tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(loss_fn))
+        key = ("eval", tuple(x.shape), tuple(y.shape), x.dtype, y.dtype, id(forward or loss_fn))
         g = self._eval_graphs.get(key)
         if g is None:
             if len(self._eval_graphs) >= self.MAX_GRAPHS:
@@ -631,6 +742,9 @@ class KubeModel(ABC):
                 outs = fwd(xs, ys)
             g = self._eval_graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
             _sp.__exit__(None, None, None)
+        if self._dry:                 # job warm-up: captured, not replayed
+            z = torch.zeros((), dtype=torch.float32, device=x.device)
+            return z, z.clone()
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
         g["graph"].replay()

@@ -213,3 +213,46 @@ def test_elastic_one_two_one_on_one_gpu(tmp_path):
             prev_end = ck[0][1]
     finally:
         srv.stop()
+
+
+def test_bert_grad_sync_persistent_adamw_two_packed_workers(tmp_path):
+    """Config 5 as a framework workload: ``kubeml train -f bert --K 1 --grad-sync --parallelism 2``
+    with both workers packed on the one GPU.  K = 1 rounds run as the in-graph gradient exchange
+    (the comm plan's transport over peer memory) with the AdamW moments kept across rounds
+    (TrainOptions.sync = "grad"); masking, forward, backward and AdamW of a batch are one graph
+    replay.  Both workers must end every epoch on one model, and the loss must fall."""
+    import json
+    from kubeml_amd.api.types import TrainOptions, TrainRequest
+    from kubeml_amd.client import KubemlClient
+    srv = _packed_server(tmp_path, 2)
+    try:
+        c = KubemlClient(srv.url())
+        rng = np.random.default_rng(5)
+        L = 128
+        base = rng.integers(1000, 1100, (16, L))              # a tiny repeating corpus: learnable
+        arrs = {"xtr": np.tile(base, (8, 1)).astype(np.int64), "ytr": np.zeros(128, dtype=np.int64),
+                "xte": base[:16].astype(np.int64), "yte": np.zeros(16, dtype=np.int64)}
+        paths = {}
+        for key, v in arrs.items():
+            paths[key] = str(tmp_path / f"{key}.npy")
+            np.save(paths[key], v)
+        c.datasets.create("wiki_tokens", paths["xtr"], paths["ytr"], paths["xte"], paths["yte"])
+        c.functions.create("bert", os.path.join(ROOT, "examples", "function_bert.py"))
+        jid = c.networks.train(TrainRequest(batch_size=64, epochs=3, dataset="wiki_tokens", lr=3e-4,
+                                            function_name="bert",
+                                            options=TrainOptions(default_parallelism=2, static_parallelism=True,
+                                                                 validate_every=1, k=1, sync="grad")))
+        t0 = time.time()
+        while c.tasks.status(jid)["state"] == "running":
+            assert time.time() - t0 < 600
+            time.sleep(0.5)
+        st = c.tasks.status(jid)
+        assert st["state"] == "finished", (st, c.logs(jid).decode()[-3000:])
+        h = c.histories.get(jid).data
+        logs = [json.loads(l) for l in c.logs(jid).decode().splitlines() if l.startswith("{")]
+        eps = [l for l in logs if l.get("msg") == "epoch finished"]
+        assert all(m == "grad-allreduce" for m in h.sync_mode), h.sync_mode
+        assert all(len(e["checksums"]) == 2 and _same_model(e) for e in eps), eps
+        assert all(np.isfinite(h.train_loss)) and h.train_loss[-1] < h.train_loss[0], h.train_loss
+    finally:
+        srv.stop()

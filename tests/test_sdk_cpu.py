@@ -178,3 +178,41 @@ def test_evaluate_eager_matches_manual():
         out = net(x)
     assert int(correct) == int((out.argmax(1) == y).sum())
     assert abs(float(loss) - float(F.cross_entropy(out, y))) < 1e-5
+
+
+def test_grad_sync_option_keeps_optimizer_state_and_wire_compat():
+    """TrainOptions.sync = "grad" (``kubeml train --grad-sync``): omitted from the JSON when
+    unset (reference wire format unchanged), carried to the function as _KubeArgs._sync, and a
+    persistent-state job neither resets the optimizer at a round start nor limits the K = 1
+    gradient exchange to SGD."""
+    import types
+    from kubeml_amd.sdk.context import TaskContext, reset_task, set_task
+    from kubeml_amd.sdk.dataset import _KubeArgs
+    from kubeml_amd.sdk.model import KubeModel
+    assert "sync" not in json.loads(T.TrainOptions().to_json())
+    o = T.TrainOptions(k=1, sync="grad")
+    assert json.loads(o.to_json())["sync"] == "grad" and T.TrainOptions.from_json(o.to_json()) == o
+    ctx = TaskContext(task="train", N=2, K=1)
+    ctx.extra["sync"] = "grad"
+    tok = set_task(ctx)
+    try:
+        args = _KubeArgs.parse()
+    finally:
+        reset_task(tok)
+    assert args._sync == "grad"
+    resets = []
+    stub = types.SimpleNamespace(args=args, _reset_optimizer_state=lambda: resets.append(1))
+    stub._persistent = lambda: KubeModel._persistent(stub)
+    KubeModel._on_iteration_start(stub)
+    assert resets == []
+    stub.args = types.SimpleNamespace(_sync="")
+    KubeModel._on_iteration_start(stub)
+    assert resets == [1]
+    # any optimizer qualifies for the K = 1 exchange when the state persists
+    comm = types.SimpleNamespace(world=2, group=None)
+    opt = torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))])
+    m = types.SimpleNamespace(device=torch.device("cpu"), batch_size=64, optimizer=opt, args=args)
+    m._persistent = lambda: KubeModel._persistent(m)
+    assert KubeModel._grad_sync_ok(m, comm, 1)
+    m.args = types.SimpleNamespace(_sync="")
+    assert not KubeModel._grad_sync_ok(m, comm, 1)

@@ -275,3 +275,34 @@ def test_attention_keep_bits_match_hash(L):
     g2 = T.attn_bwd(q, k, v, out, dout, lse, B, H, L, drop=drop)
     for a, b in zip(g1, g2):
         assert torch.equal(a, b)
+
+
+def test_mlm_mask_kernel_recipe():
+    """kernels.mlm_mask (one HIP kernel) vs BERT's masking recipe: P distinct ascending positions
+    per sequence, labels = the original tokens there, the input changed only there, about
+    80 / 10 / 10 % [MASK] / random / kept; a fixed counter gives the same mask, an advancing one
+    a new mask per call."""
+    from kubeml_amd.ops import kernels as K
+    B, L, P, V, MASK = 64, 512, 76, 30522, 103
+    g = torch.Generator(device="cuda").manual_seed(0)
+    ids = torch.randint(1000, V, (B, L), device="cuda", generator=g)
+    ctr = torch.tensor([3.0, 0.0], device="cuda")
+    x, pos, lab = K.mlm_mask(ids, ctr, P, MASK, V, advance=False)
+    x2, pos2, lab2 = K.mlm_mask(ids, ctr, P, MASK, V, advance=True)
+    torch.cuda.synchronize()
+    assert torch.equal(pos, pos2) and torch.equal(x, x2) and float(ctr[1]) == 1.0
+    x3, pos3, _ = K.mlm_mask(ids, ctr, P, MASK, V)
+    assert not torch.equal(pos3, pos) and float(ctr[1]) == 2.0
+    assert bool((pos[:, 1:] > pos[:, :-1]).all()) and int(pos.min()) >= 0 and int(pos.max()) < L
+    assert torch.equal(lab, ids.gather(1, pos))
+    changed = x != ids
+    sel = torch.zeros_like(changed)
+    sel.scatter_(1, pos, True)
+    assert not bool((changed & ~sel).any())
+    xv = x.gather(1, pos)
+    frac_mask = float((xv == MASK).float().mean())
+    frac_keep = float((xv == lab).float().mean())
+    assert abs(frac_mask - 0.8) < 0.03 and abs(frac_keep - 0.1) < 0.03, (frac_mask, frac_keep)
+    # positions uniform over the sequence
+    hist = torch.bincount(pos.reshape(-1) // 64, minlength=8).float()
+    assert float(hist.max() / hist.min()) < 1.35, hist

@@ -1,7 +1,7 @@
 """BERT-base MLM training throughput on MI355X (north-star config 5; not the headline
 bench — see bench.py).  Synthetic token batches of the real shape (there is no network
-for a corpus), random-init BERT-base (109.5 M params), fused AdamW, bf16 compute, fp32
-master weights, hidden + attention-probability dropout 0.1, 76 masked positions per
+for a corpus), masked on the device every step (kml_mlm_mask, BERT's 80/10/10 recipe), random-init
+BERT-base (109.5 M params), fused AdamW, bf16 compute, fp32 master weights, hidden + attention-probability dropout 0.1, 76 masked positions per
 512-token sequence (Google BERT's max_predictions_per_seq), whole step captured as one
 hipGraph.  Weight gradients and the GELU-fused FFN2 dgrad run on csrc/kernels/gemm.hip; the
 plain forward / dgrad GEMMs (bias or residual addend only) run on hipBLASLt where
@@ -80,18 +80,24 @@ def main():
     opt.set_grad_scale(1.0 / world)
     B, L, P, V = a.batch, a.seq, a.preds, 30522
     g = torch.Generator(device=dev).manual_seed(1 + rank)
-    ids = torch.randint(0, V, (B, L), device=dev, generator=g)
+    raw = torch.randint(0, V, (B, L), device=dev, generator=g)      # the corpus batch (token ids)
     tt = torch.zeros(B, L, dtype=torch.int64, device=dev)
-    pos = torch.stack([torch.randperm(L, device=dev, generator=g)[:P].sort().values for _ in range(B)])
-    lab = torch.randint(0, V, (B, P), device=dev, generator=g)
+    from kubeml_amd.ops import kernels as K
+    ctr = torch.tensor([float(1 + rank), 0.0], dtype=torch.float32, device=dev)
+    ids, pos, lab = K.mlm_mask(raw, ctr, P, advance=False)           # static buffers of the step
+
+    def pre():
+        # every step masks its batch on the device (a fresh mask per replay), inside the timed region
+        K.mlm_mask(raw, ctr, P, out=(ids, pos, lab))
+        sp.zero_grad()
 
     fns, sparams = m.stages(ids, tt, None, pos, lab, n=3)
-    staged = StagedForwardBackward(fns, lambda out: out, lambda: ids, pre=sp.zero_grad)
+    staged = StagedForwardBackward(fns, lambda out: out, lambda: ids, pre=pre)
     segs = [staged.segment(k) for k in range(staged.n_segments)]
     seg_grads = [[sp.grad_view(sparams[len(sparams) - 1 - k])] for k in range(len(sparams))]
     step = GraphedTrainStep(None, opt.step, use_graph=not a.no_graph, warmup=1, segments=segs,
                             segment_grads=seg_grads, force_comm=a.force_comm, graph_comm=True,
-                            state_tensors=train_state_tensors(m, sp, opt, [m.rng.tensor(dev)]))
+                            state_tensors=train_state_tensors(m, sp, opt, [m.rng.tensor(dev), ctr]))
     if comm:
         step.prime_comm()
     step.capture()
@@ -123,7 +129,8 @@ def main():
     if rank == 0:
         out = {"metric": "BERT-base MLM training tokens/s (whole job)", "value": round(tok_s, 1), "unit": "tokens/s",
                "n_gpus": world, "ms_per_step": round(dt / a.steps * 1e3, 3), "batch_per_gpu": B, "seq": L,
-               "masked_per_seq": P, "layers": a.layers, "optimizer": "fused AdamW", "dtype": "bf16",
+               "masked_per_seq": P, "masking": "per step on the device (kml_mlm_mask), inside the timed region",
+               "layers": a.layers, "optimizer": "fused AdamW", "dtype": "bf16",
                "data": "synthetic tokens, random init", "graph": not a.no_graph, "overlap_segments": len(segs),
                "loss_first_last": [round(first, 4), round(float(loss.detach()), 4)],
                "gemm": "gemm.hip (wgrad, FFN2 dgrad + GELU backward) / hipBLASLt (plain fwd, dgrad: gemm_tuning.json)"}
