@@ -174,6 +174,8 @@ class PeerAllReduce:
                         ok = ok and bool(torch.equal(t, want))
             torch.cuda.synchronize(self.device)
             ok = ok and self.errors() == 0
+            from ..utils import fault
+            fault.point("shard_selftest", rank=self.rank)    # failure-path tests: this rank's check fails
         except Exception:
             ok = False
         flags: List[bool] = [False] * self.world
@@ -471,6 +473,8 @@ class PeerShard:
             ok = ok and bool(torch.equal(sp.master, base * 3 + owner))
             torch.cuda.synchronize(self.device)
             ok = ok and self.errors() == 0
+            from ..utils import fault
+            fault.point("shard_selftest", rank=self.rank)    # failure-path tests: this rank's check fails
         except Exception:
             ok = False
         finally:

@@ -256,3 +256,38 @@ def test_bert_grad_sync_persistent_adamw_two_packed_workers(tmp_path):
         assert all(np.isfinite(h.train_loss)) and h.train_loss[-1] < h.train_loss[0], h.train_loss
     finally:
         srv.stop()
+
+
+def test_gpu_worker_killed_mid_round_pool_rebuilds_and_job_finishes(tmp_path):
+    """Failure recovery on the GPU data plane: two packed workers (gloo bootstrap, peer-memory
+    all-reduce over IPC-mapped HBM), K = 2 K-AVG; rank 1 is killed in epoch 1, round 1 while the
+    peers hold each other's IPC mappings.  The job must detect the loss, shut the pool down (the
+    survivor's process and its peer mappings go with it), rebuild on the survivor, restore the
+    post-init checkpoint and finish every epoch with a history (ml/pkg/train/util.go:144-166)."""
+    from kubeml_amd.api.types import TrainOptions, TrainRequest
+    from kubeml_amd.client import KubemlClient
+    from kubeml_amd.config import Config
+    from kubeml_amd.control.server import KubeMLServer
+    cfg = Config()
+    cfg.store_dir = str(tmp_path / "store")
+    cfg.num_gpus = 1
+    srv = KubeMLServer(cfg, n_workers=2, use_gpu=True, task_timeout=600,
+                       worker_env={"KUBEML_FAULT": "kill:at=round:rank=1:epoch=1:round=1"}).start(
+        ports={k_: 0 for k_ in ("controller", "scheduler", "ps", "storage", "metrics")})
+    try:
+        c = KubemlClient(srv.url())
+        arrs = _cifar_like(seed=6)
+        paths = {}
+        for key, v in arrs.items():
+            paths[key] = str(tmp_path / f"{key}.npy")
+            np.save(paths[key], v)
+        c.datasets.create("cifar10", paths["xtr"], paths["ytr"], paths["xte"], paths["yte"])
+        c.functions.create("resnet34", os.path.join(ROOT, "examples", "function_resnet34.py"))
+        jid, h, eps = _run_job(c, tmp_path, 2, 2, epochs=2)
+        log = c.logs(jid).decode()
+        assert "recovering" in log and "epoch failed" in log, log[-3000:]
+        assert h.parallelism == [1.0, 1.0], h.parallelism
+        assert len(h.train_loss) == 2 and all(np.isfinite(h.train_loss))
+        assert len(h.accuracy) == 2
+    finally:
+        srv.stop()

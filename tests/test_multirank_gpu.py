@@ -187,3 +187,97 @@ def test_train_step_two_ranks_one_gpu():
 
 def test_train_step_four_ranks_one_gpu():
     _check(4, _spawn(4, [c for c in CASES if c[1] == "sgd"]))
+
+
+def _rank_master_race(rank, world, port, q):
+    """After a sharded step, rank 0 overwrites its own master chunk right after sync_master
+    while rank 1 enters sync_master late: the gather's exit barrier must keep rank 0's write
+    behind rank 1's read (gather_master had only an entry barrier)."""
+    import time
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kubeml_amd.engine.dp import make_train_step
+        from kubeml_amd.nn import cross_entropy
+        from kubeml_amd.parallel.plan import parse_plan
+        m, sp, opt = _model(dev, "sgd")
+        xs, ys = _batches(rank, 1, dev)
+        x, y = xs[0].clone(), ys[0].clone()
+        step = make_train_step(m, sp, opt, cross_entropy, x, y, plan=parse_plan("peer:shard:fp32:256"), world=world)
+        assert type(step.peer).__name__ == "PeerShard"
+        step.capture()
+        step()
+        torch.cuda.synchronize()
+        sh = step.peer
+        own = sp.master[sh.lo:sh.hi].clone()          # this rank's chunk is current before the gather
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank == 1:
+            time.sleep(0.3)                           # arrive late: rank 0 waits in the entry barrier
+        sp.sync_master()
+        if rank == 0:
+            sp.master[sh.lo:sh.hi].fill_(12345.0)    # a local step right after the collective
+        torch.cuda.synchronize()
+        chunk0 = None
+        if rank == 1:
+            c0 = (0, sh.chunk) if sh.chunk <= sp.numel else (0, sp.numel)
+            chunk0 = _digest(sp.master[c0[0]:min(c0[1], sp.numel)])
+        mine = _digest(own)
+        allv = [None] * world
+        dist.all_gather_object(allv, (mine, chunk0))
+        sh.check()
+        q.put((rank, {"own": allv, "errors": sh.errors()}, None))
+        sh.close()
+    except Exception as e:
+        import traceback
+        q.put((rank, None, repr(e) + traceback.format_exc()[-2500:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_sync_master_exit_barrier_protects_late_readers():
+    import torch.multiprocessing as mp
+    from kubeml_amd.runtime.pool import free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_rank_master_race, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=300) for _ in ps]
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    for rank, out, exc in res:
+        assert exc is None, (rank, exc)
+    out = {rank: o for rank, o, _ in res}
+    rank0_chunk_before, _ = out[1]["own"][0]
+    _, rank1_saw = out[1]["own"][1]
+    assert rank1_saw == rank0_chunk_before         # rank 1 gathered rank 0's chunk before the overwrite
+    assert out[0]["errors"] == 0 and out[1]["errors"] == 0
+
+
+def test_shard_selftest_failure_falls_back_to_allreduce():
+    """A failing ZeRO-1 self-test (fault-injected on rank 1) must leave EVERY rank on the exact
+    all-reduce plan — same update, identical ranks — instead of one rank diverging or hanging."""
+    old = os.environ.get("KUBEML_FAULT")
+    os.environ["KUBEML_FAULT"] = "raise:at=shard_selftest:rank=1"
+    try:
+        res = _spawn(2, [("peer:shard:fp32:256", "sgd", 3)])
+    finally:
+        if old is None:
+            os.environ.pop("KUBEML_FAULT", None)
+        else:
+            os.environ["KUBEML_FAULT"] = old
+    rs = [res[r]["peer:shard:fp32:256/sgd"] for r in range(2)]
+    assert all(r["transport"] == "PeerAllReduce" for r in rs), [r["transport"] for r in rs]
+    assert rs[0]["digests"] == rs[1]["digests"] and all(r["finite"] for r in rs)
+    assert rs[0]["rel"] <= 1e-5, rs[0]["rel"]
