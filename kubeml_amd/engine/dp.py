@@ -64,6 +64,14 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     """
     comm = world > 1 or force_comm
     shard = None
+    staged_shard = False
+    if plan is not None and plan.schedule == "shardov":
+        # per-stage shard steps need stage-contiguous gradient ranges and the fused SGD
+        staged_shard = (forward is None and hasattr(model, "stages") and hasattr(model, "stage_params") and
+                        getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges())
+        from ..parallel.plan import CommPlan
+        plan = CommPlan("peer", "shard", plan.wire, plan.max_blocks,
+                        source=plan.source + ("" if staged_shard else " (shardov -> shard: no stages / fused SGD)"))
     if plan is not None and plan.schedule == "shard":
         on_gpu = comm and torch.cuda.is_available() and space.grad.is_cuda
         # the optimizer's capability is checked BEFORE the collective setup (the same answer on
@@ -85,7 +93,9 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             source=f"{plan.source} (shard unavailable)")
         peer = shard
         if shard is not None:
-            overlap = False                   # the update is one collective after the backward
+            overlap = staged_shard            # one collective after the backward, or one per stage
+        else:
+            staged_shard = False
     if plan is not None and shard is None:
         overlap = plan.schedule == "overlap"
         comm_dtype = plan.wire_dtype
@@ -129,7 +139,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     user_post()
                 from ..ops import kernels as K
                 K.advance_counter_(*advance)
-    if (comm and overlap and staged_ok) or opt_overlap:
+    if (comm and overlap and staged_ok) or opt_overlap or staged_shard:
         from .staged import StagedForwardBackward
 
         def pre0():
@@ -172,10 +182,25 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             backward_loss(loss)
             space.finish_grads()
             return loss
-    shard_step = on_replay = None
+    shard_step = on_replay = seg_shard = None
     if shard is not None:
         blocks = plan.max_blocks
         fused_sgd = getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges()
+        if staged_shard:
+            # ownership cut per backward stage (every rank the same ranges): stage k's
+            # reduce-scatter + SGD + all-gather run on a side stream once its gradients are final
+            space.sync_master()
+            ranges = [space.range_of(ps) for ps in stage_of_seg]
+            order = sorted(range(len(ranges)), key=lambda k: ranges[k][0])
+            shard.set_stages([ranges[k] for k in order])
+            seg_of = {k: order.index(k) for k in range(len(ranges))}
+            nseg = len(ranges)
+
+            def _stage(k, stamps=None):
+                s0, s1 = stamps if stamps is not None else (None, None)
+                shard.stage_step(seg_of[k], optimizer, advance=fold, max_blocks=blocks, first_stage=k == 0,
+                                 last_stage=k == nseg - 1, stamps=None if stamps is None else (s0, s1))
+            seg_shard = [(lambda st=None, k=k: _stage(k, st)) for k in range(nseg)]
 
         def shard_step(stamps=None):
             """stamps: int64[2] device buffer (timing) — start / end of the collective."""
@@ -196,6 +221,12 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             if post is not None:
                 post()
 
+        if seg_shard is not None:
+            def shard_step(stamps=None):
+                """Staged layout: the per-stage collectives ran beside the backward."""
+                if post is not None:
+                    post()
+
         def on_replay():
             space._master_stale = True
 
@@ -207,4 +238,5 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             segment_opt=seg_opt, opt_finish=opt_finish, peer=peer,
                             schedule=plan.schedule if plan is not None else "overlap",
                             peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing,
-                            shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1))
+                            shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1),
+                            segment_shard=seg_shard)

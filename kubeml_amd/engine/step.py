@@ -158,7 +158,8 @@ class GraphedTrainStep:
                  segment_opt: Optional[Sequence[Callable[[], None]]] = None,
                  opt_finish: Optional[Callable[[], None]] = None, peer=None, schedule: str = "overlap",
                  peer_blocks: int = 256, comm_timing: int = 0, shard_step: Optional[Callable[[], None]] = None,
-                 on_replay: Optional[Callable[[], None]] = None, world: Optional[int] = None):
+                 on_replay: Optional[Callable[[], None]] = None, world: Optional[int] = None,
+                 segment_shard: Optional[Sequence[Callable]] = None):
         if segments is None:
             if fwd_bwd is None:
                 raise ValueError("need fwd_bwd or segments")
@@ -210,6 +211,12 @@ class GraphedTrainStep:
         # collectives on, shard_step replaces opt_step; the local warm-up still runs opt_step
         self.shard_step = shard_step if self.comm else None
         self.on_replay = on_replay      # host bookkeeping after every replay (e.g. master now sharded)
+        # staged shard ("shardov"): segment_shard[k](stamps) = stage k's reduce-scatter + SGD +
+        # all-gather, issued on a block-capped side stream right after segment k's backward
+        if segment_shard is not None and (shard_step is None or len(segment_shard) != len(self.segments)):
+            raise ValueError("segment_shard needs shard_step and one callable per segment")
+        self.segment_shard = list(segment_shard) if (segment_shard is not None and self.comm) else None
+        self._shard_side = None
         self.peer_blocks = int(peer_blocks)
         self._peer_side = None
         if self.peer is not None and self.segment_opt is not None:
@@ -355,6 +362,8 @@ class GraphedTrainStep:
     def _body(self):
         if self.segment_opt is not None:
             return self._body_opt_overlap()
+        if self.segment_shard is not None and self._comm_on:
+            return self._body_staged_shard()
         loss, works = None, []
         for k, seg in enumerate(self.segments):
             out = self._run(seg)
@@ -366,6 +375,31 @@ class GraphedTrainStep:
             self.shard_step(stamps=self._stamps)     # the collective's own launches stamp it
         else:
             self.opt_step()
+        return loss
+
+    def _body_staged_shard(self):
+        """Staged ZeRO-1 step: after segment k's backward its gradient range is final, and
+        stage k's reduce-scatter (peer reads over xGMI) + fused SGD + bf16 all-gather run on a
+        side stream while segment k+1 (the stage before it) runs backward.  Stage k's weights
+        are not read again this step, so updating them early is exact; the compute stream joins
+        the side stream before the step ends (the next forward reads every stage)."""
+        cur = torch.cuda.current_stream()
+        if self._shard_side is None:
+            self._shard_side = torch.cuda.Stream()
+        side = self._shard_side
+        loss = None
+        for k, seg in enumerate(self.segments):
+            out = self._run(seg)
+            if k == 0:
+                loss = out
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                if self._stamps is not None:
+                    self.segment_shard[k]((self._stamps.data_ptr(), self._stamps.data_ptr() + 8))
+                else:
+                    self.segment_shard[k](None)
+        cur.wait_stream(side)
+        self.shard_step(stamps=None)
         return loss
 
     def _body_opt_overlap(self):

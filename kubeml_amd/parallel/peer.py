@@ -330,6 +330,10 @@ class PeerShard:
         self.chunk = -(-self.n // (self.world * 64)) * 64
         self.lo = min(self.n, self.rank * self.chunk)
         self.hi = min(self.n, self.lo + self.chunk)
+        # ownership layout: segments (s0, s1, chunk); rank r owns [s0 + r chunk, s0 + (r+1) chunk)
+        # of each.  One segment = the whole space; set_stages() cuts it per backward stage
+        self.segments = [(0, self.n, self.chunk)]
+        self._seg_ptrs: List[tuple] = []
         self.opened: List[int] = []
         self.region = self.ctrl = None
         err = ""
@@ -389,6 +393,11 @@ class PeerShard:
         applied at once (master, momentum, shadow of the chunk; 1/P folded in); else it lands in
         the own gradient chunk for :meth:`update_range`.  ``stamp``: device address of an int64 the
         barrier launch stamps (100 MHz wall clock) when timing the step's collectives."""
+        if len(self.segments) != 1:
+            raise PeerCommError("staged layout: use stage_step()")
+        self._rs_call(self.lo, self.hi, optimizer, advance, max_blocks, stamp, clear_first=True)
+
+    def _rs_call(self, lo, hi, optimizer, advance, max_blocks, stamp, clear_first=True):
         sp = self.space
         if self.region is None:
             raise PeerCommError("sharded update used after close()")
@@ -406,13 +415,13 @@ class PeerShard:
         ctr, ab, an = advance if advance is not None else (None, 0.0, 0.0)
         HIP.call("kml_zs_reduce_scatter", "p p p p i i l l i p p p p f f f i p f p f f i d i p s",
                  ctypes.addressof(self._flags), ctypes.addressof(self._grads), self.region, self.ctrl, self.rank,
-                 self.world, self.lo, self.hi, int(fused), sp.master.data_ptr() if fused else None,
+                 self.world, int(lo), int(hi), int(fused), sp.master.data_ptr() if fused else None,
                  mom.data_ptr() if mom is not None else None, sp.shadow.data_ptr() if fused else None,
                  lr.data_ptr() if lr is not None else None, float(wd), float(momentum), float(dampening), nesterov,
                  first.data_ptr() if first is not None else None, 1.0 / self.world,
                  ctr.data_ptr() if ctr is not None else None, float(ab), float(an), int(max_blocks),
                  self.timeout_s, int(self.split), stamp, self._stream())
-        if first is not None:
+        if first is not None and clear_first:
             from ..ops import kernels as K
             K.fill_(first, 0.0)
 
@@ -424,14 +433,73 @@ class PeerShard:
                  self.chunk, 2, 2, 2, int(max_blocks), self.timeout_s, int(self.split), stamp, self._stream())
         self.space._master_stale = True
 
+    # ------------------------------------------------------------------ staged layout
+    def set_stages(self, ranges):
+        """Cut the ownership per backward stage: ``ranges`` = contiguous flat ranges tiling the
+        space; rank r then owns chunk r of EVERY range, so each stage's gradient can be
+        reduce-scattered, applied and all-gathered on its own (:meth:`stage_step`) while the
+        backward of the stages before it still runs.  Collective in effect (every rank must
+        pass the same ranges); the master must be complete (sync_master) before the switch."""
+        segs = []
+        for s0, s1 in ranges:
+            s0, s1 = int(s0), int(s1)
+            if s1 <= s0:
+                continue
+            if s0 % 8 or (s1 % 8 and s1 != self.n):
+                raise ValueError("stage ranges must start at multiples of 8 elements")
+            segs.append((s0, s1, -(-(s1 - s0) // (self.world * 64)) * 64))
+        if not segs or segs[0][0] != 0 or segs[-1][1] != self.n or any(a[1] != b[0] for a, b in zip(segs, segs[1:])):
+            raise ValueError("stage ranges must tile the flat space in order")
+        self.segments = segs
+        arr = ctypes.c_void_p * self.world
+        self._seg_ptrs = []
+        for s0, s1, ch in segs:
+            sh = arr(*[int(v) + 2 * s0 for v in self._shadows])
+            st = arr(*[int(v) + 4 * s0 for v in self._states])
+            self._seg_ptrs.append((sh, st))
+
+    def owned(self):
+        """[(lo, hi)] flat ranges whose master / optimizer state this rank keeps current."""
+        out = []
+        for s0, s1, ch in self.segments:
+            lo = min(s1, s0 + self.rank * ch)
+            out.append((lo, min(s1, lo + ch)))
+        return out
+
+    def stage_step(self, k: int, optimizer, advance=None, max_blocks: int = 256, first_stage: bool = True,
+                   last_stage: bool = True, stamps=None):
+        """Segment k of a staged layout: reduce-scatter + fused SGD on this rank's chunk of the
+        segment, then the bf16 shadow all-gather of the segment.  ``first_stage`` /
+        ``last_stage``: the first call of a step stamps the start, the last clears SGD's
+        first-step flag, advances the data counter and stamps the end."""
+        s0, s1, ch = self.segments[k]
+        lo = min(s1, s0 + self.rank * ch)
+        hi = min(s1, lo + ch)
+        self._rs_call(lo, hi, optimizer, advance if last_stage else None, max_blocks,
+                      stamps[0] if (stamps is not None and first_stage) else None, clear_first=last_stage)
+        sh, _ = self._seg_ptrs[k]
+        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
+                 ctypes.addressof(sh), self.region, self.ctrl, self.rank, self.world, s1 - s0, ch, 2, 2, 2,
+                 int(max_blocks), self.timeout_s, int(self.split),
+                 stamps[1] if (stamps is not None and last_stage) else None, self._stream())
+        self.space._master_stale = True
+
     def gather_master(self, max_blocks: int = 256):
         """Collective: complete the fp32 master from the owners' chunks.  Entry barrier, gather,
         then an exit barrier: callers overwrite their own master chunk right after this (tail
         local rounds, the next epoch's broadcast, the self-test restore), which must not happen
         while a slower peer is still reading that chunk."""
-        HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
-                 ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
-                 self.chunk, 4, 1, 2, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
+        if len(self.segments) == 1:
+            HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
+                     ctypes.addressof(self._states), self.region, self.ctrl, self.rank, self.world, self.n,
+                     self.chunk, 4, 1, 2, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
+        else:
+            last = len(self.segments) - 1
+            for k, (s0, s1, ch) in enumerate(self.segments):
+                _, st = self._seg_ptrs[k]
+                HIP.call("kml_zs_all_gather", "p p p p i i l l i i i i d i p s", ctypes.addressof(self._flags),
+                         ctypes.addressof(st), self.region, self.ctrl, self.rank, self.world, s1 - s0, ch, 4, 1,
+                         2 if k == last else 1, int(max_blocks), self.timeout_s, int(self.split), None, self._stream())
         HIP.call("kml_zs_barrier", "p p p i i i d s", ctypes.addressof(self._flags), self.region, self.ctrl,
                  self.rank, self.world, 0, self.timeout_s, self._stream())
         self.space._master_stale = False

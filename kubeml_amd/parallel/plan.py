@@ -12,7 +12,10 @@ gradient all-reduce:
   reduce-scatter of the fp32 gradient read in place from the peers, the optimizer on this
   rank's 1/P of the master (fused into the reduce for SGD), all-gather of the bf16 shadow
   (:class:`~kubeml_amd.parallel.peer.PeerShard`; the wire field is ignored: fp32 gradient,
-  bf16 weights, which is what the forward computes with anyway).
+  bf16 weights, which is what the forward computes with anyway); ``"shardov"`` — the same
+  per backward stage on a side stream: each stage's reduce-scatter + SGD + all-gather runs as
+  soon as its gradients are final, beside the backward of the stages before it (fused SGD,
+  models with ``stages()``; otherwise it runs as ``"shard"``).
 * ``wire``     fp32, or bf16 (half the link bytes; the sum accumulates in fp32).
 * ``max_blocks`` the grid cap of every peer launch (the CUs the collective may hold).
 
@@ -52,10 +55,10 @@ class CommPlan:
     def __post_init__(self):
         if self.backend not in ("peer", "rccl"):
             raise ValueError(f"backend must be peer or rccl, not {self.backend!r}")
-        if self.schedule not in ("end", "overlap", "shard"):
-            raise ValueError(f"schedule must be end, overlap or shard, not {self.schedule!r}")
-        if self.schedule == "shard" and self.backend != "peer":
-            raise ValueError("the shard schedule runs on the peer backend")
+        if self.schedule not in ("end", "overlap", "shard", "shardov"):
+            raise ValueError(f"schedule must be end, overlap, shard or shardov, not {self.schedule!r}")
+        if self.schedule in ("shard", "shardov") and self.backend != "peer":
+            raise ValueError("the shard schedules run on the peer backend")
         if self.wire not in _WIRES:
             raise ValueError(f"wire must be fp32 or bf16, not {self.wire!r}")
         self.max_blocks = max(1, int(self.max_blocks))

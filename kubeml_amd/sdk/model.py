@@ -438,12 +438,13 @@ class KubeModel(ABC):
         if not names:
             return
         bufs = self.optimizer._bufs(self._flat, names)
+        owned = sh.owned()
         for name in names:
             t = bufs[name]
-            if sh.lo > 0:
-                t[:sh.lo].zero_()
-            if sh.hi < t.numel():
-                t[sh.hi:].zero_()
+            keep = torch.zeros_like(t)
+            for lo, hi in owned:
+                keep[lo:hi].copy_(t[lo:hi])
+            t.copy_(keep)
             comm.all_reduce_(t)
 
     def _allreduce_grads_eager(self):

@@ -161,14 +161,15 @@ def _spawn(world, cases):
 
 
 CASES = [("peer:end:fp32:256", "sgd", 4), ("peer:end:bf16:256", "sgd", 4), ("peer:shard:fp32:256", "sgd", 4),
-         ("peer:shard:fp32:256", "sgdm", 3), ("peer:shard:fp32:256", "adamw", 3)]
+         ("peer:shard:fp32:256", "sgdm", 3), ("peer:shard:fp32:256", "adamw", 3),
+         ("peer:shardov:fp32:64", "sgd", 4), ("peer:shardov:fp32:64", "sgdm", 3)]
 
 
 def _check(world, res):
     for key in res[0]:
         spec = key.split("/")[0]
         rs = [res[r][key] for r in range(world)]
-        want = "PeerShard" if ":shard:" in spec else "PeerAllReduce"
+        want = "PeerShard" if ":shard" in spec else "PeerAllReduce"
         assert all(r["transport"] == want for r in rs), (key, [r["transport"] for r in rs])
         assert all(r["finite"] for r in rs), key
         # every rank holds bit-identical weights after the replays
@@ -187,6 +188,14 @@ def test_train_step_two_ranks_one_gpu():
 
 def test_train_step_four_ranks_one_gpu():
     _check(4, _spawn(4, [c for c in CASES if c[1] == "sgd"]))
+
+
+def test_staged_shard_plan_rides_the_backward_stages():
+    """peer:shardov: the step is split at the model's backward stages and each stage runs its
+    own reduce-scatter + SGD + all-gather on a side stream (ownership cut per stage)."""
+    res = _spawn(2, [("peer:shardov:fp32:64", "sgd", 2)])
+    r0 = res[0]["peer:shardov:fp32:64/sgd"]
+    assert r0["transport"] == "PeerShard" and r0["rel"] <= 1e-5
 
 
 def _rank_master_race(rank, world, port, q):
