@@ -5,6 +5,8 @@
 //   maxpool bwd : gather formulation (each input element sums the output gradients of
 //                 the windows that selected it) — no atomics, no zero-fill pass.
 //   global avgpool fwd/bwd (AdaptiveAvgPool2d(1)).
+//   option-A shortcut fwd/bwd (CIFAR ResNet, reference ml/experiments/kubeml/resnet32.py
+//                 LambdaLayer): stride-2 subsample + zero channel padding, 16-byte chunks.
 // Reference parity: nn.MaxPool2d(3,2,1) of the ResNet stem / nn.MaxPool2d(2) of LeNet
 // (function_lenet.py:25-31), AdaptiveAvgPool2d((1,1)) of torchvision resnet.
 #include "kml_common.h"
@@ -138,6 +140,40 @@ __global__ void k_gavg_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ d
   }
 }
 
+// option-A shortcut forward: y[b,oh,ow,:] = [0]*pad ++ x[b,2oh,2ow,:] ++ [0]*pad; one thread per
+// 8-channel output chunk (pad % 8 == 0 keeps every chunk wholly data or wholly zero)
+__global__ void k_shortcut_a_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B, int H, int W, int C,
+                                 int OH, int OW, int pad) {
+  const int Co8 = (C + 2 * pad) / 8;
+  const long long total = (long long)B * OH * OW * Co8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Co8) * 8 - pad;
+    const long long pix = i / Co8;
+    const int ow = (int)(pix % OW), oh = (int)((pix / OW) % OH), b = (int)(pix / ((long long)OW * OH));
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (c >= 0 && c < C) v = *reinterpret_cast<const uint4*>(x + (((long long)b * H + 2 * oh) * W + 2 * ow) * C + c);
+    reinterpret_cast<uint4*>(y)[i] = v;
+  }
+}
+
+// option-A shortcut backward: dx at even (h, w) takes the un-padded channels of dy, zero elsewhere
+__global__ void k_shortcut_a_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int B, int H, int W, int C,
+                                 int OH, int OW, int pad) {
+  const int C8 = C / 8, Co = C + 2 * pad;
+  const long long total = (long long)B * H * W * C8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const long long pix = i / C8;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), b = (int)(pix / ((long long)W * H));
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (!(h & 1) && !(w & 1))
+      v = *reinterpret_cast<const uint4*>(dy + (((long long)b * OH + (h >> 1)) * OW + (w >> 1)) * Co + pad + c);
+    reinterpret_cast<uint4*>(dx)[i] = v;
+  }
+}
+
 }  // namespace
 
 KML_API int kml_maxpool_fwd(const bf16_t* x, bf16_t* y, unsigned char* idx, int B, int H, int W, int C, int k,
@@ -170,5 +206,23 @@ KML_API int kml_gavgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int HW, int C,
   if (C % 8) return (int)hipErrorInvalidValue;
   long long total = (long long)B * HW * (C / 8);
   hipLaunchKernelGGL(k_gavg_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, dx, B, HW, C);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_shortcut_a_fwd(const bf16_t* x, bf16_t* y, int B, int H, int W, int C, int pad, hipStream_t st) {
+  if (C % 8 || pad % 8 || pad < 0) return (int)hipErrorInvalidValue;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const long long total = (long long)B * OH * OW * ((C + 2 * pad) / 8);
+  hipLaunchKernelGGL(k_shortcut_a_fwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, x, y, B, H, W, C, OH, OW,
+                     pad);
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_shortcut_a_bwd(const bf16_t* dy, bf16_t* dx, int B, int H, int W, int C, int pad, hipStream_t st) {
+  if (C % 8 || pad % 8 || pad < 0) return (int)hipErrorInvalidValue;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2;
+  const long long total = (long long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(k_shortcut_a_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, dx, B, H, W, C, OH, OW,
+                     pad);
   KML_LAUNCH_CHECK();
 }

@@ -302,14 +302,33 @@ def resnet50(num_classes=1000, **kw):
 # CIFAR ResNet (He et al. 2016, option-A identity shortcut) — reference resnet32.py
 # ---------------------------------------------------------------------------------------
 
+class _ShortcutAFn(torch.autograd.Function):
+    """Option-A shortcut on the GPU: one gather launch each way (pool.hip k_shortcut_a_*)."""
+
+    @staticmethod
+    def forward(ctx, x, pad):
+        from ..ops import kernels as K
+        ctx.shape, ctx.pad = tuple(x.shape), pad
+        return K.shortcut_a_fwd(x.contiguous(), pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        return K.shortcut_a_bwd(dy.contiguous(), ctx.shape, ctx.pad), None
+
+
 class _LambdaShortcut(tnn.Module):
-    """Option A: stride-2 subsample + zero-pad channels (parameter-free)."""
+    """Option A: stride-2 subsample + zero-pad channels (parameter-free) — reference
+    ml/experiments/kubeml/resnet32.py LambdaLayer.  bf16 CUDA tensors take the in-tree HIP
+    gather; CPU keeps the stock slice + ``F.pad`` it is checked against."""
 
     def __init__(self, planes):
         super().__init__()
         self.pad = planes // 4
 
     def forward(self, x):  # NHWC
+        if x.is_cuda and x.dtype == torch.bfloat16:
+            return _ShortcutAFn.apply(x, self.pad)
         y = x[:, ::2, ::2, :]
         return F.pad(y, (self.pad, self.pad)).contiguous()
 

@@ -1331,6 +1331,30 @@ def maxpool_bwd(dy, idx, in_shape, k, s, p, relu_out=None):
     return dx
 
 
+def shortcut_a_fwd(x, pad):
+    """Option-A shortcut (CIFAR ResNet): ``F.pad(x[:, ::2, ::2, :], (pad, pad))`` on NHWC bf16
+    in one gather launch.  Needs C % 8 == 0 and pad % 8 == 0."""
+    _chk(x, BF16, "x", 4)
+    B, H, W, C = x.shape
+    if C % 8 or pad % 8 or pad < 0:
+        raise ValueError(f"shortcut_a_fwd: C={C} and pad={pad} must be multiples of 8")
+    y = torch.empty((B, (H + 1) // 2, (W + 1) // 2, C + 2 * pad), dtype=BF16, device=x.device)
+    HIP.call("kml_shortcut_a_fwd", "p p i i i i i s", _p(x), _p(y), B, H, W, C, int(pad), _s())
+    return y
+
+
+def shortcut_a_bwd(dy, in_shape, pad):
+    """Backward of :func:`shortcut_a_fwd`: the un-padded channels of dy at even pixels, zeros
+    elsewhere (writes every element of dx — no zero-fill pass)."""
+    _chk(dy, BF16, "dy", 4)
+    B, H, W, C = in_shape
+    if tuple(dy.shape) != (B, (H + 1) // 2, (W + 1) // 2, C + 2 * pad):
+        raise ValueError("shortcut_a_bwd: dy does not match the input shape and pad")
+    dx = torch.empty((B, H, W, C), dtype=BF16, device=dy.device)
+    HIP.call("kml_shortcut_a_bwd", "p p i i i i i s", _p(dy), _p(dx), B, H, W, C, int(pad), _s())
+    return dx
+
+
 def bn_relu_maxpool(x, stats, gamma, beta, k, s, p, save_mean=None, save_rstd=None, run_mean=None, run_var=None,
                     eps=1e-5, momentum=0.1, stats_rows=0, counters=None):
     """Training BN (batch statistics from ``stats``: [stats_rows][2C] conv-epilogue partial

@@ -259,6 +259,28 @@ def test_resnet32_cifar_learns_on_gpu():
     assert all(v == v for v in losses) and losses[-1] < 0.8 * losses[0], losses
 
 
+@pytest.mark.parametrize("shape,pad", [((4, 32, 32, 16), 8), ((3, 16, 16, 32), 16), ((2, 7, 9, 8), 8)])
+def test_option_a_shortcut_kernel_matches_slice_pad(shape, pad):
+    """pool.hip k_shortcut_a_fwd/bwd vs the stock slice + F.pad and its autograd (exact:
+    pure data movement), including odd spatial sizes."""
+    from kubeml_amd.models.resnet import _LambdaShortcut
+    from kubeml_amd.ops import kernels as K
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=dev).to(torch.bfloat16)
+    sc = _LambdaShortcut(4 * pad)
+    xr = x.float().cpu().requires_grad_(True)
+    yr = F.pad(xr[:, ::2, ::2, :], (pad, pad))
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    xg = x.clone().requires_grad_(True)
+    y = sc(xg)
+    assert torch.equal(y.float().cpu(), yr.detach())
+    y.backward(dy.to(dev, torch.bfloat16))
+    assert torch.equal(xg.grad.float().cpu(), xr.grad.to(torch.bfloat16).float())
+    with pytest.raises(ValueError):
+        K.shortcut_a_fwd(x, 4)
+
+
 def test_resnet_fused_stem_matches_unfused_stem():
     """_STEM_FUSE path (one BN->ReLU->max-pool pass, ReLU mask folded into the pool
     backward) vs the unfused BN-apply + max-pool pair and an fp32 torch stem, on the stem
