@@ -186,17 +186,91 @@ __device__ __forceinline__ const char* slot_of(const char* region, unsigned call
   return region + PC_FLAGS_BYTES + (long long)(calls & 1u) * cap;
 }
 
+// ---- K-AVG rounds on the two-shot: the model average fused into the collective -------------
+// (parallel/kavg.py; reference merge ml/pkg/model/model.go:249-302, parallelSGD.go:26-54).  The
+// state buffer's count slot (each rank's participation, 0 or 1) is also published in a word of
+// the flags area per slot parity, so every block can form the divisor right after the call's
+// first barrier without waiting for the rank that owns the count slot's chunk: the sum is taken
+// in rank order like the payload, so every rank and every block gets the same divisor.  The
+// epilogue then stores x * (1 / max(count, 1)) below the count slot (the raw sum at and above
+// it, as the unfused all-reduce + kml_kavg_finish pair leaves them), refreshes the bf16 shadow of
+// the parameter range and floors the int64 counters back into their arena — the finish pass
+// over the whole state disappears.
+constexpr int PC_KAVG_WORD = 32;  // flags-area words 32 / 33 (flags[p] uses words 0..7)
+
+struct PcKavg {
+  long long count_idx = -1;  // < 0: not a K-AVG call
+  long long n_params = 0;    // shadow refreshed for [0, n_params)
+  bf16_t* shadow = nullptr;
+  long long* i64 = nullptr;  // int64 counters of [i64_off, i64_off + n_i64)
+  long long i64_off = 0;
+  int n_i64 = 0;
+  int shadow_aligned = 0;    // 8-byte aligned shadow: 4-element packed stores
+};
+
+__device__ __forceinline__ unsigned* kavg_word(const char* region, unsigned calls) {
+  return reinterpret_cast<unsigned*>(const_cast<char*>(region)) + PC_KAVG_WORD + (calls & 1u);
+}
+
+// after the call's first barrier: {1 / max(count, 1), count}, the count summed in rank order
+template <int P>
+__device__ float2 kavg_divisor(const PcPeers& peers, unsigned calls) {
+  __shared__ float2 sh;
+  if (threadIdx.x == 0) {
+    float c = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      c += __uint_as_float(
+          __hip_atomic_load(kavg_word(peers.region[p], calls), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    sh = make_float2(1.f / fmaxf(c, 1.f), c);
+  }
+  __syncthreads();
+  return sh;
+}
+
+// the K-AVG epilogue for 4 fp32 sums at element e (products rounded on their own: no FMA
+// contraction into the counters' +1e-3, matching kml_kavg_finish bit for bit)
+__device__ __forceinline__ void kavg_store(float* __restrict__ out, long long e, long long n, bool aligned,
+                                           const float (&x)[4], float inv, const PcKavg& k) {
+  float y[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y[j] = (e + j < k.count_idx) ? __fmul_rn(x[j], inv) : x[j];
+  store_out<4>(out, e, n, aligned, y, 1.f);
+  if (k.shadow && e < k.n_params) {
+    if (k.shadow_aligned && e + 4 <= k.n_params) {
+      uint2 sv;
+      sv.x = pack_bf2(y[0], y[1]);
+      sv.y = pack_bf2(y[2], y[3]);
+      *reinterpret_cast<uint2*>(k.shadow + e) = sv;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (e + j < k.n_params) k.shadow[e + j] = f2bf(y[j]);
+    }
+  }
+  if (k.i64) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long q = e + j - k.i64_off;
+      if (q >= 0 && q < k.n_i64) k.i64[q] = (long long)floorf(__fadd_rn(y[j], 1e-3f));
+    }
+  }
+}
+
 // in (n fp32) -> own slot as nvec wire vectors (zero padding beyond n)
 template <bool BF16>
 __global__ __launch_bounds__(PC_BLOCK) void k_pc_copyin(const float* __restrict__ in, char* __restrict__ region,
                                                         const unsigned* __restrict__ ctrl, long long cap, long long n,
-                                                        long long nvec, int aligned) {
+                                                        long long nvec, int aligned, long long count_idx = -1) {
   using W = Wire<BF16>;
   constexpr int VE = W::VE;
   const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // a poisoned rank publishes NaN, so a late peer reading this slot cannot sum stale bytes
   const bool poisoned = __hip_atomic_load(ctrl + C_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
   const auto r = pc_rsrc(slot_of(region, calls, cap), cap);
+  if (count_idx >= 0 && blockIdx.x == 0 && threadIdx.x == 0)  // K-AVG: this rank's count, per parity
+    __hip_atomic_store(kavg_word(region, calls), __float_as_uint(poisoned ? __builtin_nanf("") : in[count_idx]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long v = blockIdx.x * (long long)blockDim.x + threadIdx.x; v < nvec; v += stride) {
     float x[VE];
@@ -250,15 +324,19 @@ __global__ __launch_bounds__(PC_BLOCK) void k_pc_oneshot(float* __restrict__ out
 
 // two-shot, reduce-scatter: chunk `rank` (cv vectors) summed over the P slots in rank order,
 // published back into the own slot (write-through) and widened into out
-template <bool BF16, int P>
+template <bool BF16, int P, bool KAVG = false>
 __global__ __launch_bounds__(PC_BLOCK) void k_pc_rs(float* __restrict__ out, PcPeers peers, char* region,
                                                     unsigned* ctrl, int rank, long long cap, long long n, long long cv,
-                                                    float scale, int aligned, unsigned long long limit) {
+                                                    float scale, int aligned, unsigned long long limit,
+                                                    PcKavg kv = PcKavg{}) {
   using W = Wire<BF16>;
   constexpr int VE = W::VE;
+  static_assert(!KAVG || !BF16, "K-AVG rounds use the fp32 wire");
   const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool ok = pc_barrier(peers, region, ctrl, rank, P, seq + 1u, limit);
+  float inv = 1.f;
+  if constexpr (KAVG) inv = kavg_divisor<P>(peers, calls).x;
   __amdgpu_buffer_rsrc_t rs[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(slot_of(peers.region[p], calls, cap), cap);
@@ -288,20 +366,27 @@ __global__ __launch_bounds__(PC_BLOCK) void k_pc_rs(float* __restrict__ out, PcP
       for (int j = 0; j < VE; ++j) acc[j] = __builtin_nanf("");
       st_sys16(own, g * 16, W::pack(acc));  // peers gathering this chunk read NaN
     }
-    store_out<VE>(out, g * VE, n, aligned != 0, acc, scale);
+    if constexpr (KAVG)
+      kavg_store(out, g * VE, n, aligned != 0, acc, inv, kv);
+    else
+      store_out<VE>(out, g * VE, n, aligned != 0, acc, scale);
   }
 }
 
 // two-shot, all-gather: every chunk q != rank copied from peer q's slot (its reduced chunk)
-template <bool BF16, int P>
+template <bool BF16, int P, bool KAVG = false>
 __global__ __launch_bounds__(PC_BLOCK) void k_pc_ag(float* __restrict__ out, PcPeers peers, char* region,
                                                     unsigned* ctrl, int rank, long long cap, long long n, long long cv,
-                                                    float scale, int aligned, unsigned long long limit) {
+                                                    float scale, int aligned, unsigned long long limit,
+                                                    PcKavg kv = PcKavg{}) {
   using W = Wire<BF16>;
   constexpr int VE = W::VE;
+  static_assert(!KAVG || !BF16, "K-AVG rounds use the fp32 wire");
   const unsigned seq = __hip_atomic_load(ctrl + C_SEQ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned calls = __hip_atomic_load(ctrl + C_CALLS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool ok = pc_barrier(peers, region, ctrl, rank, P, seq + 2u, limit);
+  float inv = 1.f;
+  if constexpr (KAVG) inv = kavg_divisor<P>(peers, calls).x;
   __amdgpu_buffer_rsrc_t rs[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) rs[p] = pc_rsrc(slot_of(peers.region[p], calls, cap), cap);
@@ -323,7 +408,10 @@ __global__ __launch_bounds__(PC_BLOCK) void k_pc_ag(float* __restrict__ out, PcP
 #pragma unroll
       for (int jj = 0; jj < VE; ++jj) x[jj] = __builtin_nanf("");
     }
-    store_out<VE>(out, g * VE, n, aligned != 0, x, scale);
+    if constexpr (KAVG)
+      kavg_store(out, g * VE, n, aligned != 0, x, inv, kv);
+    else
+      store_out<VE>(out, g * VE, n, aligned != 0, x, scale);
   }
   pc_finish_call(ctrl, 2u);
 }
@@ -526,6 +614,28 @@ hipError_t launch_all(const float* in, float* out, const PcPeers& peers, char* r
   return hipGetLastError();
 }
 
+template <int P>
+hipError_t launch_kavg(float* state, const PcPeers& peers, char* region, unsigned* ctrl, int rank, long long cap,
+                       long long n, const PcKavg& kv, int max_blocks, unsigned long long limit, hipStream_t s) {
+  const int aligned = (((uintptr_t)state) & 15) == 0;
+  auto grid_for = [&](long long items) {
+    long long g = (items + PC_BLOCK - 1) / PC_BLOCK;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+  };
+  const long long cv = ((n + 3) / 4 + P - 1) / P;
+  const long long nvec = cv * P;
+  if (nvec * 16 > cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_pc_copyin<false>, dim3(grid_for(nvec)), dim3(PC_BLOCK), 0, s, state, region, ctrl, cap, n, nvec,
+                     aligned, kv.count_idx);
+  hipLaunchKernelGGL((k_pc_rs<false, P, true>), dim3(grid_for(cv)), dim3(PC_BLOCK), 0, s, state, peers, region, ctrl,
+                     rank, cap, n, cv, 1.f, aligned, limit, kv);
+  hipLaunchKernelGGL((k_pc_ag<false, P, true>), dim3(grid_for((long long)(P - 1) * cv)), dim3(PC_BLOCK), 0, s, state,
+                     peers, region, ctrl, rank, cap, n, cv, 1.f, aligned, limit, kv);
+  return hipGetLastError();
+}
+
 template <bool BF16>
 hipError_t launch_world(int world, const float* in, float* out, const PcPeers& peers, char* region, unsigned* ctrl,
                         int rank, long long cap, long long n, float scale, int algo, int max_blocks,
@@ -659,6 +769,45 @@ unsigned zs_grid(long long items, int max_blocks) {
   return (unsigned)g;
 }
 }  // namespace
+
+// One K-AVG round in place on the flat state buffer (after kml_kavg_pack): the two-shot SUM with
+// the average, the bf16 shadow refresh of [0, n_params) and the int64 counter unpack fused into
+// its epilogues (see PcKavg).  Same result as kml_peer_allreduce(two-shot, fp32) + kml_kavg_finish.
+KML_API int kml_peer_kavg(float* state, const void* const* regions, void* region, void* ctrl, int rank, int world,
+                          long long cap, long long n, long long count_idx, long long n_params, bf16_t* shadow,
+                          long long* i64, long long i64_off, int n_i64, int max_blocks, double timeout_s,
+                          hipStream_t s) {
+  if (world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || n <= 0 || cap % 16 || max_blocks < 1 ||
+      !(timeout_s > 0.0) || count_idx < 0 || count_idx >= n || n_params < 0 || n_params > count_idx ||
+      n_i64 < 0 || (n_i64 > 0 && (!i64 || i64_off < 0 || i64_off + n_i64 > count_idx)))
+    return (int)hipErrorInvalidValue;
+  PcPeers peers = {};
+  for (int p = 0; p < world; ++p) {
+    if (!regions[p]) return (int)hipErrorInvalidValue;
+    peers.region[p] = reinterpret_cast<const char*>(regions[p]);
+  }
+  if (peers.region[rank] != region) return (int)hipErrorInvalidValue;
+  PcKavg kv;
+  kv.count_idx = count_idx;
+  kv.n_params = shadow ? n_params : 0;
+  kv.shadow = shadow;
+  kv.i64 = n_i64 > 0 ? i64 : nullptr;
+  kv.i64_off = i64_off;
+  kv.n_i64 = n_i64;
+  kv.shadow_aligned = (((uintptr_t)shadow) & 7) == 0;
+  const unsigned long long limit = zs_limit(timeout_s);
+  switch (world) {
+#define PK_CASE(P) \
+  case P:          \
+    return (int)launch_kavg<P>(state, peers, reinterpret_cast<char*>(region), reinterpret_cast<unsigned*>(ctrl), rank, \
+                               cap, n, kv, max_blocks, limit, s);
+    PK_CASE(1) PK_CASE(2) PK_CASE(3) PK_CASE(4) PK_CASE(5) PK_CASE(6) PK_CASE(7) PK_CASE(8)
+#undef PK_CASE
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+}
+
 
 // reduce-scatter of the flat fp32 gradients: rank's chunk [lo, hi) summed over the group in rank
 // order.  fused_sgd: the sum goes straight into the SGD update of master / mom (may be null) and

@@ -18,6 +18,7 @@ Redis round-trips (network.py:424-461, model.go:135-181).
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Dict, List, Optional
 
@@ -120,6 +121,8 @@ class TorchComm(Comm):
         self.peer_data = peer_data
         self.peer = None          # small/large fp32 reductions (enable_peer / peer_data)
         self.grad_peer = None     # the train step's gradient all-reduce (engine/dp.py, plan "peer")
+        self.kavg_p = None        # fused K-AVG rounds over RCCL groups (kavg_peer)
+        self._kavg_off = False    # its self-test failed: K-AVG stays on the RCCL all-reduce
 
     @property
     def member(self) -> bool:
@@ -141,8 +144,8 @@ class TorchComm(Comm):
         transport is dropped first (its results are NaN for good): the next collective that
         needs one builds a fresh one, collectively."""
         err = None
-        for name in ("peer", "grad_peer"):
-            p = getattr(self, name)
+        for name in ("peer", "grad_peer", "kavg_p"):
+            p = getattr(self, name, None)
             if p is None:
                 continue
             try:
@@ -160,7 +163,7 @@ class TorchComm(Comm):
 
     def _drop(self, name):
         """Unmap and free a transport WITHOUT a group barrier (its group may be broken)."""
-        p = getattr(self, name)
+        p = getattr(self, name, None)
         setattr(self, name, None)
         if p is not None:
             try:
@@ -170,7 +173,7 @@ class TorchComm(Comm):
 
     def drop_peers(self):
         """Forget every peer transport of this group and its sub-groups (non-collective)."""
-        for name in ("peer", "grad_peer"):
+        for name in ("peer", "grad_peer", "kavg_p"):
             self._drop(name)
         for c in self._subs.values():
             c.drop_peers()
@@ -188,6 +191,32 @@ class TorchComm(Comm):
             self.peer.close()
         self.peer = PeerAllReduce(self.group, cap_bytes=cap, device=t.device)
         return self.peer
+
+    def kavg_peer(self, t):
+        """The peer transport for a fused K-AVG round over ``t`` (the flat fp32 state buffer):
+        the two-shot with the average, shadow refresh and counter unpack in its epilogues
+        (parallel/kavg.py), or None (all-reduce + ``kavg_finish_``).  peer_data groups use
+        their data-plane transport; RCCL groups build one sized for the state on first use —
+        collective: every member averages the same state in the same round — and keep it only
+        if its self-test (which includes a fused round) passes on every rank.
+        ``KUBEML_KAVG_PEER=0`` keeps RCCL."""
+        if self.world == 1 or not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+            return None
+        if self.peer_data:
+            p = self._peer_for(t)
+            return p if p is not None and p.supports_kavg(t) else None
+        if getattr(self, "_kavg_off", False) or os.environ.get("KUBEML_KAVG_PEER", "1") == "0":
+            return None
+        if getattr(self, "kavg_p", None) is not None and self.kavg_p.supports_kavg(t):
+            return self.kavg_p
+        from .peer import slot_bytes, verified_peer
+        if getattr(self, "kavg_p", None) is not None:
+            self.kavg_p.close()
+            self.kavg_p = None
+        self.kavg_p = verified_peer(self.group, cap_bytes=slot_bytes(t.numel(), self.world, "twoshot"),
+                                    device=t.device)
+        self._kavg_off = self.kavg_p is None
+        return self.kavg_p
 
     def _host_bounce(self, t, fn):
         """gloo collective on a host copy of a CUDA tensor (peer_data mode, non-fp32 dtypes)."""

@@ -17,6 +17,14 @@ slot).  A round is three launches on the compute stream and no host synchronisat
     kavg_finish  x *= 1/count (divisor read on device), bf16 shadow refreshed in the
                  same pass, counters floored back to int64
 
+On one node the all-reduce and the finish are ONE collective (``TorchComm.kavg_peer``, default
+on GPU groups, ``KUBEML_KAVG_PEER=0`` keeps RCCL): the peer-memory two-shot over IPC-mapped
+HBM (parallel/peer.py, comm.hip ``kml_peer_kavg``) reads 2 (P-1)/P of the state per rank over
+xGMI and applies the average, the shadow refresh and the counter unpack in its reduce-scatter
+and all-gather epilogues, so no extra pass over the 87 MB state follows the exchange.  The
+transport passes a self-test that includes a fused round before it is used; on failure every
+rank keeps the RCCL all-reduce + finish pair.
+
 Workers that ran out of data (uneven ``split_minibatches``) send zeros and a zero
 count, so the divisor is the number of contributing ranks, exactly like the
 reference's partial merge rounds (ml/pkg/train/job.go:380-431).  CPU workers (gloo /
@@ -37,6 +45,7 @@ class ModelAverager:
         self.module = module
         self.last_seconds = 0.0   # host time of the last average_ call (metrics)
         self.force = False        # run rounds on a 1-rank group too (single-GPU rehearsal)
+        self.fused_rounds = 0     # rounds that ran as one fused peer-memory collective
 
     def _all_reduce(self, comm: Comm, t: torch.Tensor):
         if comm.world == 1 and self.force and hasattr(comm, "dist"):
@@ -74,8 +83,15 @@ class ModelAverager:
         if not participate:
             K.memset_(sp.state)
         K.kavg_pack_(sp.state, arena, sp.i64_off, sp.n_i64, sp.count_idx, participate)
-        self._all_reduce(comm, sp.state)
-        K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
+        pk = comm.kavg_peer(sp.state) if hasattr(comm, "kavg_peer") and comm.world > 1 else None
+        if pk is not None:
+            # one fused round on the peer-memory two-shot (comm.hip kml_peer_kavg)
+            pk.kavg_(sp.state, sp.count_idx, sp.numel, sp.shadow, arena, sp.i64_off,
+                     sp.n_i64 if arena is not None else 0)
+            self.fused_rounds += 1
+        else:
+            self._all_reduce(comm, sp.state)
+            K.kavg_finish_(sp.state, sp.numel, sp.count_idx, sp.shadow, arena, sp.i64_off, sp.n_i64)
         self._average_other(comm, sp, participate)
         return -1
 

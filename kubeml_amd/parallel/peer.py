@@ -136,6 +136,58 @@ class PeerAllReduce:
                  self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
         return t
 
+    def supports_kavg(self, state: torch.Tensor) -> bool:
+        return self.supports(state, "twoshot", torch.float32)
+
+    def kavg_(self, state: torch.Tensor, count_idx: int, n_params: int = 0, shadow: Optional[torch.Tensor] = None,
+              i64: Optional[torch.Tensor] = None, i64_off: int = 0, n_i64: int = 0,
+              max_blocks: Optional[int] = None) -> torch.Tensor:
+        """One K-AVG round in place on the flat state buffer (after ``kavg_pack_``): the
+        two-shot sum with the average by the on-device count, the bf16 shadow refresh of
+        ``[0, n_params)`` and the int64 counter unpack in its epilogues (comm.hip
+        ``kml_peer_kavg``) — what ``all_reduce_`` + ``kavg_finish_`` do in two passes more."""
+        if self.region is None:
+            raise PeerCommError("peer all-reduce used after close()")
+        if not self.supports_kavg(state):
+            raise ValueError(f"peer K-AVG: contiguous fp32 state on {self.device} within {self.cap} slot bytes")
+        if shadow is not None and (shadow.dtype != torch.bfloat16 or shadow.numel() < n_params):
+            raise ValueError("peer K-AVG: shadow must be bf16 with n_params elements")
+        if n_i64 and (i64 is None or i64.dtype != torch.int64 or i64.numel() < n_i64):
+            raise ValueError("peer K-AVG: i64 arena must hold n_i64 int64 counters")
+        HIP.call("kml_peer_kavg", "p p p p i i l l l l p p l i i d s", state.data_ptr(),
+                 ctypes.addressof(self._regions), self.region, self.ctrl, self.rank, self.world, self.cap,
+                 state.numel(), int(count_idx), int(n_params), 0 if shadow is None else shadow.data_ptr(),
+                 0 if i64 is None else i64.data_ptr(), int(i64_off), int(n_i64), int(max_blocks or 256),
+                 self.timeout_s, torch.cuda.current_stream(self.device).cuda_stream)
+        return state
+
+    def _kavg_self_test(self) -> bool:
+        """Fused K-AVG round on a synthetic layout (integer patterns, one non-participating rank
+        when world > 2) against the closed form computed with the same fp32 operations."""
+        n = min(1 << 20, self.cap // 4 - 64)
+        n -= n % 4
+        if n < self.world * 64:
+            return True
+        count_idx, n_params, i64_off, n_i64 = n - 3, n - 67, n - 67, 40
+        idx = torch.arange(n, device=self.device)
+        base = (idx % 8).float()
+        part = [r for r in range(self.world) if not (self.world > 2 and r == self.world - 1)]
+        ok = True
+        for _ in range(3):                      # both slot parities, then one more
+            st = base * float(self.rank + 1) if self.rank in part else torch.zeros_like(base)
+            st[count_idx] = 1.0 if self.rank in part else 0.0
+            shadow = torch.empty(n_params, dtype=torch.bfloat16, device=self.device)
+            arena = torch.empty(n_i64, dtype=torch.int64, device=self.device)
+            self.kavg_(st, count_idx, n_params, shadow, arena, i64_off, n_i64)
+            tot = base * float(sum(r + 1 for r in part))
+            want = tot.clone()
+            inv = torch.tensor(1.0, device=self.device) / float(max(len(part), 1))
+            want[:count_idx] = tot[:count_idx] * inv
+            want[count_idx] = float(len(part))
+            ok = ok and bool(torch.equal(st, want)) and bool(torch.equal(shadow, want[:n_params].to(torch.bfloat16)))
+            ok = ok and bool(torch.equal(arena, torch.floor(want[i64_off:i64_off + n_i64] + 1e-3).long()))
+        return ok
+
     # ------------------------------------------------------------------ health
     def errors(self) -> int:
         """Timed-out barrier waits so far (non-zero: the group is poisoned, outputs are NaN)."""
@@ -172,6 +224,7 @@ class PeerAllReduce:
                         t = base * float(self.rank + 1)
                         self.all_reduce_(t, 1.0, algo=algo, wire=wire)
                         ok = ok and bool(torch.equal(t, want))
+            ok = self._kavg_self_test() and ok
             torch.cuda.synchronize(self.device)
             ok = ok and self.errors() == 0
             from ..utils import fault

@@ -208,3 +208,88 @@ def test_peer_allreduce_late_peer_fails_loudly():
     for rank, bad, errs, exc in _spawn(True):
         assert exc is None, (rank, exc)
         assert not bad, (rank, bad[:5])
+
+
+def _run_kavg(rank, world, port, q, peer_data):
+    """Fused K-AVG rounds (comm.hip kml_peer_kavg through ModelAverager) on a ResNet-18 flat
+    state against the unfused reference computed from every rank's pre-round state: the SUM in
+    rank order, times fp32 1/count below the count slot, the raw sum at and above it, bf16
+    shadow of the parameters, int64 counters floored.  Round 2 leaves the last rank out."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from kubeml_amd.models.resnet import resnet18
+        from kubeml_amd.nn import flatten_module
+        from kubeml_amd.parallel.comm import TorchComm
+        from kubeml_amd.parallel.kavg import ModelAverager
+        torch.manual_seed(10 + rank)                      # different models per rank
+        net = resnet18(10).to(dev)
+        sp = flatten_module(net)
+        arena = sp.i64_arena_now()
+        comm = TorchComm(peer_data=peer_data)
+        av = ModelAverager(net)
+        bad = []
+        for rnd in range(3):
+            arena.copy_(torch.arange(sp.n_i64, device=dev) + 5 * rank + rnd)
+            with torch.no_grad():
+                sp.state[:sp.i64_off].add_(0.01 * (rank + rnd))
+            part = not (rnd == 1 and rank == world - 1)
+            # every rank's contribution as kavg_pack builds it, gathered on the host
+            mine = sp.state.clone()
+            if not part:
+                mine.zero_()
+            mine[sp.i64_off:sp.i64_off + sp.n_i64] = arena.float() if part else 0.0
+            mine[sp.count_idx] = 1.0 if part else 0.0
+            allc = [None] * world
+            dist.all_gather_object(allc, mine.cpu())
+            av.average_(comm, participate=part)
+            torch.cuda.synchronize()
+            tot = allc[0].clone()
+            for r in range(1, world):
+                tot = tot + allc[r]
+            cnt = float(tot[sp.count_idx])
+            inv = torch.tensor(1.0) / max(cnt, 1.0)
+            want = tot.clone()
+            want[:sp.count_idx] = tot[:sp.count_idx] * inv
+            got = sp.state.cpu()
+            if not torch.equal(got, want):
+                bad.append(("state", rnd, float((got - want).abs().max())))
+            if not torch.equal(sp.shadow.cpu(), want[:sp.numel].to(torch.bfloat16)):
+                bad.append(("shadow", rnd))
+            wi = torch.floor(want[sp.i64_off:sp.i64_off + sp.n_i64] + 1e-3).long()
+            if not torch.equal(arena.cpu(), wi):
+                bad.append(("counters", rnd))
+        q.put((rank, bad, av.fused_rounds, None))
+        comm.check()
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, None, None, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("peer_data", [True, False])
+def test_fused_kavg_round_three_ranks_one_gpu(peer_data):
+    """peer_data=True: the packed workers' data-plane transport; False: the transport an RCCL
+    group builds for K-AVG on first use (verified_peer, self-test with a fused round)."""
+    import torch.multiprocessing as mp
+    from kubeml_amd.runtime.pool import free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    world = 3
+    ps = [ctx.Process(target=_run_kavg, args=(r, world, port, q, peer_data)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=150) for _ in ps]
+    for p in ps:
+        p.join(30)
+    for rank, bad, fused, exc in res:
+        assert exc is None, (rank, exc)
+        assert not bad, (rank, bad[:5])
+        assert fused == 3, (rank, fused)
