@@ -64,7 +64,10 @@ constexpr int NT = 512;
 
 template <int R>
 __device__ __forceinline__ int swz_ks(int r) {  // K-strided [64][R] chunk swizzle (R >= 128)
-  return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+  if constexpr (R == 192)  // 384-byte rows: flips inside aligned groups of 8 chunks (24 per row)
+    return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+  else
+    return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
 }
 
 __device__ __forceinline__ bf16x8_t frag_kc(const char* lds, int row0, int ks, int lane) {
@@ -359,9 +362,12 @@ __device__ __forceinline__ bf16x8_t frag_ks_asm(const char* lds, int row0, int l
   return f;
 }
 
+// R = 192 (the 256x192 phase tile's B operand): 12 instructions per slot, two on waves 0-5 and
+// none on waves 6-7 — see k_gemm8 for why the counted waits stay exact.
 template <int R, bool KC>
-struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (512/R rows / KiB)
-  static constexpr int NI = R / 128;
+struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (R / 8 16-byte chunks per k-row)
+  static constexpr int NTOT = R / 16;          // 1 KiB instructions per slot
+  static constexpr int NI = (NTOT + 7) / 8;    // per wave (the last waves may issue fewer)
   const bf16_t* base[NI];
   int lim[NI];
   bool ok[NI];
@@ -369,7 +375,7 @@ struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (512
   __device__ void init(const bf16_t* p, long long ld, int r0, int rows, int wave, int lane) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int u = wave * NI + j;
+      const int u = min(wave * NI + j, NTOT - 1);   // clamped: unused slots are never issued
       if constexpr (KC) {
         const int row = 16 * u + (lane >> 2);
         const int chunk = (lane & 3) ^ ((row >> 1) & 3);
@@ -377,9 +383,10 @@ struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (512
         base[j] = p + (long long)(ok[j] ? r0 + row : 0) * ld + chunk * 8;
         lim[j] = chunk * 8;
       } else {
-        constexpr int CPR = R / 8, RPI = 64 / CPR;
-        const int krow = RPI * u + lane / CPR;
-        const int chunk = (lane % CPR) ^ swz_ks<R>(krow);
+        constexpr int CPR = R / 8;
+        const int idx = 64 * u + lane;           // lane-linear 16-byte position in the slot
+        const int krow = idx / CPR;
+        const int chunk = (idx % CPR) ^ swz_ks<R>(krow);
         ok[j] = r0 + chunk * 8 < rows;
         base[j] = p + (long long)krow * ld + (ok[j] ? r0 + chunk * 8 : 0);
         lim[j] = krow;
@@ -390,6 +397,7 @@ struct Stager32 {  // BK = 32 slots: KC [R][32] (16 rows / KiB), KS [32][R] (512
   __device__ __forceinline__ void issue(char* lds, int kb, int kend, const bf16_t* zp, int wave) const {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
+      if (NTOT % 8 != 0 && wave * NI + j >= NTOT) break;   // wave-uniform
       const bool in = ok[j] && kb + lim[j] < kend;
       const bf16_t* src = in ? base[j] + (long long)kb * kstep : zp;
       __builtin_amdgcn_global_load_lds((const void*)src,
@@ -509,10 +517,12 @@ __global__ __launch_bounds__(NT) void k_gemm4(GemmArgs g) {
 // idle) LDS with a row-XOR swizzle, then 16-byte row-contiguous global stores (512 B per
 // half-wave): full cache lines instead of 16 rows x 32 B per store instruction.
 // ---------------------------------------------------------------------------------------
-template <bool A_KC, bool B_KC, int OUT>
+template <bool A_KC, bool B_KC, int OUT, int BN = 256>
 __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
-  constexpr int HT = 256 * 32 * 2;  // half-tile bytes
-  constexpr int MR = 8, NR = 4;     // wave tile 128 x 64
+  static_assert(BN == 256 || BN == 192, "k_gemm8: BN is 256 or 192");
+  constexpr int HT = 256 * 32 * 2;  // half-tile slot bytes (a 192-row B half-tile uses 12 of 16 KB)
+  constexpr int MR = 8, NR = BN / 64;  // wave tile 128 x (BN / 4)
+  constexpr int WN = BN / 4;
   __shared__ __attribute__((aligned(1024))) char smem[8 * HT];
 
   int tx, ty, tz;
@@ -520,13 +530,13 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int m0 = ty * 256, n0 = tx * 256;
+  const int m0 = ty * 256, n0 = tx * BN;
   const int kbeg = tz * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + 63) / 64 : 0;
 
   Stager32<256, A_KC> sa;
-  Stager32<256, B_KC> sb;
+  Stager32<BN, B_KC> sb;
   sa.init(g.a, g.lda, m0, g.M, wave, lane);
   sb.init(g.b, g.ldb, n0, g.N, wave, lane);
 
@@ -557,7 +567,7 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       if constexpr ((q & 1) == 0) {
 #pragma unroll
         for (int j = 0; j < NR; ++j)
-          bfr[j] = B_KC ? frag_kc64_asm(sB, wn * 64 + j * 16, lane) : frag_ks_asm<256>(sB, wn * 64 + j * 16, lane);
+          bfr[j] = B_KC ? frag_kc64_asm(sB, wn * WN + j * 16, lane) : frag_ks_asm<BN>(sB, wn * WN + j * 16, lane);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -566,7 +576,7 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       }
     };
     // LDS read instructions one L segment issues for phase q (B fragments on even q only)
-    constexpr int RA = A_KC ? 4 : 8, RB = B_KC ? 4 : 8;
+    constexpr int RA = A_KC ? 4 : 8, RB = B_KC ? NR : 2 * NR;
     // Phase P = 4u + q.  Group 0: L_P between barriers 2P and 2P+1, C_P between 2P+1 and
     // 2P+2; group 1 one barrier later.  L_P reads phase P+1's fragments; C_P's lgkmcnt
     // retires phase P's reads (issued in L_{P-1}) before barrier 2P+2 (group 0) / 2P+3
@@ -589,9 +599,15 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       // ---- C segment: retire phase P's fragment reads (issued in L_{P-1}); L_P's stay in flight
       constexpr int NREAD = RA + ((qn & 1) == 0 ? RB : 0);
+      static_assert(NREAD == 4 || NREAD == 7 || NREAD == 8 || NREAD == 10 || NREAD == 11 || NREAD == 12 ||
+                    NREAD >= 14, "k_gemm8: add the lgkmcnt for this read count");
       if constexpr (NREAD >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+      else if constexpr (NREAD == 14) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
       else if constexpr (NREAD == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+      else if constexpr (NREAD == 11) asm volatile("s_waitcnt lgkmcnt(11)" ::: "memory");
+      else if constexpr (NREAD == 10) asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
       else if constexpr (NREAD == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else if constexpr (NREAD == 7) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
@@ -630,13 +646,17 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
   }
 
   if constexpr (OUT != 0) {
-    gemm_epilogue<OUT, MR, NR, 128, 64>(g, acc, m0, n0, wm, wn, lane, tz);
+    gemm_epilogue<OUT, MR, NR, 128, WN>(g, acc, m0, n0, wm, wn, lane, tz);
   } else {
+    // staged tile [256][BN] bf16: row stride 2 BN bytes, 16-byte chunk ch of row r at ch ^ swz(r)
+    // (BN = 192: 24 chunks per row, the XOR stays inside aligned groups of 8)
+    constexpr int CPR = BN / 8;
+    auto stg = [](int row, int ch) { return row * (2 * BN) + ((ch ^ (BN == 256 ? (row & 15) : (row & 7))) << 4); };
     __syncthreads();
     float4 bias4[NR];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
       bias4[j] = (g.bias && n < g.N) ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // fp32 accumulators -> (+bias, act) bf16 -> swizzled LDS tile [256][256]
@@ -646,14 +666,14 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
         const int row = wm * 128 + i * 16 + (lane & 15);
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
-          const int col = wn * 64 + j * 16 + 4 * (lane >> 4);
+          const int col = wn * WN + j * 16 + 4 * (lane >> 4);
           float v0 = acc[i][j][0] + bias4[j].x, v1 = acc[i][j][1] + bias4[j].y;
           float v2 = acc[i][j][2] + bias4[j].z, v3 = acc[i][j][3] + bias4[j].w;
           if (act) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3); }
           uint2 p;
           p.x = pack_bf2(v0, v1);
           p.y = pack_bf2(v2, v3);
-          const int off = row * 512 + (((col >> 3) ^ (row & 15)) << 4) + ((col >> 2) & 1) * 8;
+          const int off = stg(row, col >> 3) + ((col >> 2) & 1) * 8;
           *reinterpret_cast<uint2*>(smem + off) = p;
         }
         __builtin_amdgcn_sched_barrier(0);   // one fragment row at a time: bounds the temporaries
@@ -665,13 +685,13 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // GELU_BWD: this thread's 8 columns
     auto store = [&](bf16_t* dst) {
 #pragma unroll 2
-      for (int it = 0; it < 16; ++it) {
+      for (int it = 0; it < 256 * CPR / NT; ++it) {
         const int idx = it * NT + tid;
-        const int row = idx >> 5, ch = idx & 31;
-        uint4 v = *reinterpret_cast<const uint4*>(smem + row * 512 + ((ch ^ (row & 15)) << 4));
+        const int row = idx / CPR, ch = idx % CPR;
+        uint4 v = *reinterpret_cast<const uint4*>(smem + stg(row, ch));
         const int m = m0 + row, n = n0 + ch * 8;
         if (m < g.M && n < g.N) {
-          if (gbwd) {  // d(pre) = bf16(bf16(d act) * gelu'(pre)), as k_gelu_bwd_colsum
+          if (BN == 256 && gbwd) {  // d(pre) = bf16(bf16(d act) * gelu'(pre)), as k_gelu_bwd_colsum
             const uint4 pv = *reinterpret_cast<const uint4*>(g.c2 + (long long)m * g.ldc + n);
             const unsigned dw[4] = {v.x, v.y, v.z, v.w}, pw[4] = {pv.x, pv.y, pv.z, pv.w};
             unsigned ow[4];
@@ -701,7 +721,7 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
     }
     stage(g.act == 1);
     store(static_cast<bf16_t*>(g.c));
-    if (gbwd) {  // column sums: 16 threads (tid >> 5) share each 8-column chunk; fixed order
+    if (BN == 256 && gbwd) {  // column sums: 16 threads (tid >> 5) share each 8-column chunk; fixed order
       float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
       for (int k = 0; k < 8; ++k) red[tid * 8 + k] = csum[k];
@@ -717,15 +737,16 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
   }
 }
 
-template <bool A_KC, bool B_KC, int OUT>
+template <bool A_KC, bool B_KC, int OUT, int BN = 256>
 int launch8(GemmArgs g, int splits, hipStream_t s) {
+  if (BN != 256 && g.act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;
   splits = splits < 1 ? 1 : splits;
   int chunk = (g.K + splits - 1) / splits;
   chunk = ((chunk + 63) / 64) * 64;
   g.kchunk = chunk > 0 ? chunk : 64;
   const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
-  dim3 grid((g.N + 255) / 256, (g.M + 255) / 256, z);
-  hipLaunchKernelGGL((k_gemm8<A_KC, B_KC, OUT>), grid, dim3(NT), 0, s, g);
+  dim3 grid((g.N + BN - 1) / BN, (g.M + 255) / 256, z);
+  hipLaunchKernelGGL((k_gemm8<A_KC, B_KC, OUT, BN>), grid, dim3(NT), 0, s, g);
   KML_LAUNCH_CHECK();
 }
 
@@ -763,6 +784,7 @@ int by_tile(const GemmArgs& g, int tile, int splits, hipStream_t s) {
     case 4: return launch<128, 128, A_KC, B_KC, OUT, 2>(g, splits, s);   // 2 stages: 2 blocks per CU
     case 5: return launch4<A_KC, B_KC, OUT>(g, splits, s);
     case 6: return launch8<A_KC, B_KC, OUT>(g, splits, s);
+    case 7: return launch8<A_KC, B_KC, OUT, 192>(g, splits, s);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -795,7 +817,9 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
 // out:    0 = bf16 (+bias, act, pre-act copy), 1 = fp32 beta, 2 = fp32 atomic (split-K)
 // tile:   0 = 256x256, 1 = 256x128, 2 = 128x256, 3 = 128x128 (BM x BN; 3-stage where LDS allows),
 //         4 = 128x128 with 2 stages (64 KB: two blocks per CU), 5 = 256x256 BK=32 4-slot ring,
-//         6 = 256x256 two-group phase schedule (k_gemm8)
+//         6 = 256x256 two-group phase schedule (k_gemm8), 7 = the same schedule on 256x192 tiles
+//         (BERT's N = 768 / 2304 / 3072 outputs split into 4 / 12 / 16 column tiles: with T = 16384
+//         tokens every launch is a whole number of waves over 256 CUs)
 // Host contract (checked by ops/gemm.py): N % 4 == 0, ldc % 4 == 0, K-contiguous leading
 // dimensions % 8 == 0, 16-byte aligned pointers; a zero page of >= 16 bytes.  Tile 6 with
 // bf16 output also needs N % 8 == 0 and ldc % 8 == 0 (16-byte staged stores).
@@ -849,7 +873,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;
   // the launcher rounds the K chunk up to the tile's K step: count the slices it produced
-  int step = (tile == 5 || tile == 6) ? 64 : BK;
+  int step = (tile == 5 || tile == 6 || tile == 7) ? 64 : BK;
   int chunk = ((K + splits - 1) / splits + step - 1) / step * step;
   const int z = K > 0 ? (K + chunk - 1) / chunk : 1;
   const long long n4 = (long long)M * N / 4;

@@ -19,7 +19,7 @@ from .._native import HIP, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5,
-         (256, 256, 8): 6}  # (BM, BN[, stages])
+         (256, 256, 8): 6, (256, 192, 8): 7}  # (BM, BN[, stages])
 _TUNE_FILE = os.environ.get("KUBEML_GEMM_TUNING_FILE") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _TUNED: dict = {}
@@ -114,7 +114,7 @@ def gemm(a, lda, b, ldb, c, ldc, M, N, K, layout, out, bias=None, act=0, c2=None
         return wgrad_splitk_(c, a, lda, b, ldb, M, N, K, beta=beta, tile=tile, splits=splits)
     if out != 2:
         splits = 1
-    if TILES[tuple(tile)] == 6 and out == 0 and (N % 8 or ldc % 8):
+    if TILES[tuple(tile)] in (6, 7) and out == 0 and (N % 8 or ldc % 8):
         raise ValueError("gemm: the 256x256 phase tile with bf16 output needs N and ldc % 8 == 0")
     HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", a.data_ptr(), int(lda), b.data_ptr(), int(ldb),
              c.data_ptr(), int(ldc), 0 if c2 is None else c2.data_ptr(), 0 if bias is None else bias.data_ptr(),

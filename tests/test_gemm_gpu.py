@@ -17,8 +17,8 @@ def _rand(*s, scale=1.0):
     return (torch.randn(*s, device=dev) * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128),
-                                  (128, 128, 2)])
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (256, 128), (128, 256),
+                                  (128, 128), (128, 128, 2)])
 @pytest.mark.parametrize("T,ip,op", [(512, 768, 2304), (200, 72, 136), (1216, 768, 1000)])
 def test_forward_bias_gelu(tile, T, ip, op):
     from kubeml_amd.ops import gemm as G
@@ -33,8 +33,8 @@ def test_forward_bias_gelu(tile, T, ip, op):
     assert _rel(y, torch.nn.functional.gelu(h)) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (128, 128)])
-@pytest.mark.parametrize("T,ip,op", [(512, 768, 3072), (200, 72, 136)])
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (128, 128)])
+@pytest.mark.parametrize("T,ip,op", [(512, 768, 3072), (200, 72, 136), (768, 2304, 768)])
 def test_dgrad(tile, T, ip, op):
     from kubeml_amd.ops import gemm as G
     torch.manual_seed(1)
@@ -45,7 +45,7 @@ def test_dgrad(tile, T, ip, op):
 
 
 @pytest.mark.parametrize("tile,splits", [((256, 256), 1), ((256, 256, 4), 1), ((256, 256, 4), 2), ((256, 256, 8), 1),
-                                         ((256, 256, 8), 3), ((128, 128), 1),
+                                         ((256, 256, 8), 3), ((256, 192, 8), 1), ((256, 192, 8), 3), ((128, 128), 1),
                                          ((256, 128), 4), ((128, 128), 3)])
 @pytest.mark.parametrize("T,ip,op", [(2048, 768, 768), (200, 72, 136)])
 def test_wgrad_accumulates(tile, splits, T, ip, op):
@@ -59,9 +59,10 @@ def test_wgrad_accumulates(tile, splits, T, ip, op):
     assert _rel(dw, ref) < 1e-4
 
 
+@pytest.mark.parametrize("tile", [(256, 256, 8), (256, 192, 8)])
 @pytest.mark.parametrize("layout", [0, 1, 2])
 @pytest.mark.parametrize("K", [8, 64, 96, 128, 320, 4096])
-def test_phase_tile_reduction_lengths(layout, K):
+def test_phase_tile_reduction_lengths(layout, K, tile):
     """k_gemm8's five-half-tiles-ahead DMA schedule and group stagger at every pipeline
     depth: a single partial K-tile up to a long reduction; ragged M / N edges."""
     from kubeml_amd.ops import gemm as G
@@ -70,19 +71,19 @@ def test_phase_tile_reduction_lengths(layout, K):
     if layout == 0:
         A, B = _rand(M, K), _rand(N, K, scale=0.05)
         C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        G.gemm(A, K, B, K, C, N, M, N, K, 0, 0, tile=(256, 256, 8), splits=1)
+        G.gemm(A, K, B, K, C, N, M, N, K, 0, 0, tile=tile, splits=1)
         ref = A.double() @ B.double().t()
         tol = 1e-2
     elif layout == 1:
         A, B = _rand(M, K), _rand(K, N, scale=0.05)
         C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
-        G.gemm(A, K, B, N, C, N, M, N, K, 1, 0, tile=(256, 256, 8), splits=1)
+        G.gemm(A, K, B, N, C, N, M, N, K, 1, 0, tile=tile, splits=1)
         ref = A.double() @ B.double()
         tol = 1e-2
     else:
         A, B = _rand(K, M), _rand(K, N)
         C = torch.zeros(M, N, device=dev)
-        G.gemm(A, M, B, N, C, N, M, N, K, 2, 1, beta=1.0, tile=(256, 256, 8), splits=1)
+        G.gemm(A, M, B, N, C, N, M, N, K, 2, 1, beta=1.0, tile=tile, splits=1)
         ref = A.double().t() @ B.double()
         tol = 1e-4
     assert _rel(C, ref) < tol
@@ -134,8 +135,8 @@ def test_linear_helpers_match_torch():
         G.linear_fwd(x, w[:, :700])
 
 
-@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128),
-                                  (128, 128, 2)])
+@pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (256, 128), (128, 256),
+                                  (128, 128), (128, 128, 2)])
 @pytest.mark.parametrize("T,ip,op", [(512, 768, 2304), (200, 72, 136)])
 def test_dgrad_plus_addend_equals_separate_add(tile, T, ip, op):
     """act=ADD_C2 (the transformer's residual-gradient sum fused into the dgrad epilogue):

@@ -69,7 +69,8 @@ def main():
             lda, ldb, out = M, N, 1
             ref = lambda: torch.addmm(C, A.t(), B, out_dtype=torch.float32)
         cands = []
-        for tile in ((256, 256), (256, 256, 4), (256, 256, 8), (256, 128), (128, 256), (128, 128), (128, 128, 2)):
+        for tile in ((256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (256, 128), (128, 256), (128, 128),
+                     (128, 128, 2)):
             tname = "x".join(str(v) for v in tile)
             if a.tiles != "all" and tname not in a.tiles.split(","):
                 continue
