@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--tile", default="256,256")
     ap.add_argument("--splits", type=int, default=1)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--torch", action="store_true", help="run torch.mm (hipBLASLt) on the same operands instead")
     a = ap.parse_args()
     from kubeml_amd.ops import gemm as G
     dev = torch.device("cuda", 0)
@@ -34,6 +35,14 @@ def main():
         A, B = torch.randn(K, M, device=dev).bfloat16(), torch.randn(K, N, device=dev).bfloat16()
         C, lda, ldb, out = torch.zeros(M, N, device=dev), M, N, (1 if a.splits == 1 else 2)
     for _ in range(a.reps):
+        if a.torch:
+            if a.layout == 0:
+                torch.mm(A, B.t(), out=C)
+            elif a.layout == 1:
+                torch.mm(A, B, out=C)
+            else:
+                torch.addmm(C, A.t(), B, out_dtype=torch.float32)
+            continue
         G.gemm(A, lda, B, ldb, C, N, M, N, K, a.layout, out, beta=1.0 if a.layout == 2 else 0.0, tile=tile,
                splits=a.splits)
     torch.cuda.synchronize()
