@@ -188,10 +188,13 @@ KML_API int kml_sgd(float* w, const float* g, float* mom, bf16_t* shadow, const 
   KML_LAUNCH_CHECK();
 }
 
+// max_blocks > 0 caps the grid (a range update on a side stream beside the backward, as kml_sgd)
 KML_API int kml_adam(float* w, const float* g, float* m, float* v, bf16_t* shadow, const float* lr_ptr,
                      const float* step_ptr, float lr, float step, float b1, float b2, float eps, float wd,
-                     int decoupled, float grad_scale, long long n, hipStream_t s) {
-  hipLaunchKernelGGL(k_adam, dim3(kml_stream_grid((n + 3) / 4, 256)), dim3(256), 0, s, w, g, m, v, shadow, lr_ptr,
+                     int decoupled, float grad_scale, long long n, int max_blocks, hipStream_t s) {
+  unsigned grid = kml_stream_grid((n + 3) / 4, 256);
+  if (max_blocks > 0 && grid > (unsigned)max_blocks) grid = (unsigned)max_blocks;
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, s, w, g, m, v, shadow, lr_ptr,
                      step_ptr, lr, step, b1, b2, eps, wd, decoupled, grad_scale, n);
   KML_LAUNCH_CHECK();
 }

@@ -167,7 +167,13 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             if tiles[0][0] != 0 or tiles[-1][1] != space.numel or any(
                     a[1] != b[0] for a, b in zip(tiles, tiles[1:])):
                 raise ValueError("stage ranges must tile the flat parameter space")
-            seg_opt = [(lambda s=s, e=e: optimizer.step_range(s, e)) for s, e in ranges]
+            def _seg_opt(k, s, e):
+                def run():
+                    if k == 0:
+                        optimizer.begin_ranges()    # Adam: the bias-correction step advances once
+                    optimizer.step_range(s, e, advance_step=False)
+                return run
+            seg_opt = [_seg_opt(k, s, e) for k, (s, e) in enumerate(ranges)]
 
             def opt_finish():
                 optimizer.finish_ranges()

@@ -1466,11 +1466,11 @@ def sgd_(w, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=Fa
 
 
 def adam_(w, g, m, v, shadow, lr, step, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, decoupled=False,
-          grad_scale=1.0, lr_dev=None, step_dev=None):
+          grad_scale=1.0, lr_dev=None, step_dev=None, max_blocks=0):
     n = w.numel()
-    HIP.call("kml_adam", "p p p p p p p f f f f f f i f l s", _p(w), _p(g), _p(m), _p(v), _p(shadow),
+    HIP.call("kml_adam", "p p p p p p p f f f f f f i f l i s", _p(w), _p(g), _p(m), _p(v), _p(shadow),
              _p(lr_dev), _p(step_dev), float(lr), float(step), float(b1), float(b2), float(eps), float(wd),
-             int(decoupled), float(grad_scale), n, _s())
+             int(decoupled), float(grad_scale), n, int(max_blocks), _s())
 
 
 def increment_(t, by=1.0):

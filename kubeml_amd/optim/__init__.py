@@ -118,6 +118,9 @@ class FusedOptimizer(torch.optim.Optimizer):
 
     _STATE_NAMES = ()
 
+    def begin_ranges(self):
+        """Start of a step applied through ``step_range`` calls (no-op unless overridden)."""
+
     def prepare(self):
         """Allocate every device state buffer now (not lazily inside a first step), so
         :meth:`state_tensors` is complete before a graph capture."""
@@ -205,11 +208,12 @@ class SGD(FusedOptimizer):
         return self.supports_ranges()
 
     @torch.no_grad()
-    def step_range(self, start: int, end: int, max_blocks: int = 0):
+    def step_range(self, start: int, end: int, max_blocks: int = 0, advance_step: bool = True):
         """The fused step restricted to flat elements [start, end): the gradients of a
         finished backward stage are applied while earlier stages still run backward.  The
         first-step flag stays set until :meth:`finish_ranges` (every range of the step
-        reads the same value); the union of one step's ranges must cover the space once."""
+        reads the same value); the union of one step's ranges must cover the space once.
+        advance_step: accepted for the ranged-step protocol (SGD keeps no step counter)."""
         g = self.param_groups[0]
         spaces, loose = self._flat_groups()
         if len(spaces) != 1 or loose:
@@ -321,10 +325,21 @@ class Adam(FusedOptimizer):
         return loss
 
     def supports_ranges(self) -> bool:
-        """False: a per-backward-stage update (opt_overlap) would advance the bias-correction
-        step once per stage; Adam has no finish_ranges.  The sharded update uses
-        :meth:`supports_shard_range` (one range per step)."""
-        return False
+        """Per-backward-stage updates (engine/dp.py ``opt_overlap``): :meth:`begin_ranges`
+        advances the bias-correction step once, then every stage's :meth:`step_range` runs with
+        ``advance_step=False``, so a step split into ranges equals one whole step."""
+        spaces, loose = self._flat_groups()
+        return len(spaces) == 1 and not loose and spaces[0][0].device.type == "cuda"
+
+    @torch.no_grad()
+    def begin_ranges(self):
+        """Start of a step applied as several ranges: advance the step counter once."""
+        spaces, _ = self._flat_groups()
+        self._step_host += 1
+        self._step_dev_inc(spaces[0][0].device)
+
+    def finish_ranges(self):
+        """End of a ranged step (nothing to clear: the counter advanced in begin_ranges)."""
 
     def supports_shard_range(self) -> bool:
         """One :meth:`step_range` per step over this rank's chunk (engine/dp.py shard plan)."""
@@ -332,24 +347,31 @@ class Adam(FusedOptimizer):
         return len(spaces) == 1 and not loose and spaces[0][0].device.type == "cuda"
 
     @torch.no_grad()
-    def step_range(self, start: int, end: int, max_blocks: int = 0):
-        """The fused step over flat elements [start, end) only (a sharded update: this rank
-        owns that chunk of the master and its moments); advances the step counter."""
+    def step_range(self, start: int, end: int, max_blocks: int = 0, advance_step: bool = True):
+        """The fused step over flat elements [start, end) only.  advance_step=True (a sharded
+        update: this rank owns that chunk of the master and its moments, one range per step)
+        advances the step counter; False (one of several stage ranges of a step, after
+        :meth:`begin_ranges`) reuses it."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         spaces, loose = self._flat_groups()
         if len(spaces) != 1 or loose:
             raise ValueError("step_range needs all parameters in one flat space")
         sp = spaces[0][0]
-        self._step_host += 1
         from ..ops import kernels as K
-        st = self._step_dev_inc(sp.device)
+        if advance_step:
+            self._step_host += 1
+            st = self._step_dev_inc(sp.device)
+        else:
+            st = self.step_tensor(sp.device)
+        sp.finish_grads_range(start, end)
         bufs = self._bufs(sp, ["exp_avg", "exp_avg_sq"])
         if end > start:
             K.adam_(sp.master[start:end], sp.grad[start:end], bufs["exp_avg"][start:end],
                     bufs["exp_avg_sq"][start:end], None if sp.shadow is None else sp.shadow[start:end], g["lr"], 0.0,
                     b1, b2, g["eps"], g["weight_decay"], self.decoupled, self._grad_scale,
-                    lr_dev=self.lr_tensor(sp.device), step_dev=st)
+                    lr_dev=self.lr_tensor(sp.device), step_dev=st,
+                    max_blocks=max_blocks or (0 if advance_step else _RANGE_BLOCKS))
 
     def _step_dev_inc(self, device):
         from ..ops import kernels as K

@@ -252,6 +252,49 @@ def test_graphed_optimizer_overlap_matches_end_of_step_update():
     assert torch.equal(spa.shadow, spa.master.to(torch.bfloat16))
 
 
+def _vgg_adam_run(overlap, steps=3):
+    from kubeml_amd.engine.dp import make_train_step
+    from kubeml_amd.models.vgg import vgg11_bn
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.optim import AdamW
+    torch.manual_seed(0)
+    net = vgg11_bn(100, dropout=0.0).to(dev)    # no dropout: the two capture paths warm up a
+    net.train()                                   # different number of times (device RNG counter)
+    sp = flatten_module(net)
+    opt = AdamW(net.parameters(), lr=1e-3, weight_decay=0.01)
+    w0 = sp.master.clone()
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = [torch.randn(32, 32, 32, 8, device=dev, generator=g).to(torch.bfloat16) for _ in range(steps)]
+    ys = [torch.randint(0, 100, (32,), device=dev, generator=g) for _ in range(steps)]
+    xb, yb = torch.empty_like(xs[0]), torch.empty_like(ys[0])
+    step = make_train_step(net, sp, opt, cross_entropy, xb, yb, opt_overlap=overlap)
+    step.capture()
+    losses = []
+    for x, y in zip(xs, ys):
+        xb.copy_(x)
+        yb.copy_(y)
+        losses.append(float(step()))
+    torch.cuda.synchronize()
+    return sp.master - w0, sp, opt, losses, step
+
+
+def test_graphed_adam_overlap_advances_the_step_once():
+    """make_train_step(opt_overlap=True) with AdamW on VGG's [features, classifier] stages: the
+    classifier's update runs on a side stream while the convolutions run backward.  The bias-
+    correction step advances once per step (begin_ranges), so three overlapped steps equal three
+    end-of-step updates (to split-K atomic-order noise) and the device counter reads 3."""
+    ua, spa, oa, la, sa = _vgg_adam_run(True)
+    ub, spb, ob, lb, sb = _vgg_adam_run(False)
+    assert sa.segment_opt is not None and sb.segment_opt is None
+    assert float(oa.step_tensor(dev)) == float(ob.step_tensor(dev)) == 3.0
+    assert float(ub.abs().max()) > 1e-5
+    rel = float((ua - ub).norm() / ub.norm())
+    assert rel <= 1e-4, rel
+    for p, q in zip(la, lb):
+        assert abs(p - q) <= 1e-3 * max(1.0, abs(q)), (la, lb)
+    assert torch.equal(spa.shadow, spa.master.to(torch.bfloat16))
+
+
 def test_bench_peer_plans_rehearsal():
     """The peer transport inside the captured step (1-rank group: copy-in, reduce-scatter and
     all-gather kernels run; the link does not): end of step and overlapped with a block cap,

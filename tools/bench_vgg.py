@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--images", type=int, default=50000)
     ap.add_argument("--opt", choices=["adam", "sgd"], default="adam")
     ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--opt-overlap", choices=["on", "off"], default="off",
+                    help="per-stage optimizer on a side stream (classifier update beside the conv backward)")
     a = ap.parse_args()
     import torch
     from kubeml_amd.engine.dp import make_train_step
@@ -47,7 +49,7 @@ def main():
                                                                          weight_decay=5e-4)
     step = make_train_step(model, space, opt, cross_entropy, xbuf, ybuf,
                            pre=lambda: K.augment(data, labels, ctr, B, out=xbuf, labels_out=ybuf, train=True),
-                           advance=(ctr, B, a.images), extra_state=[ctr])
+                           advance=(ctr, B, a.images), extra_state=[ctr], opt_overlap=a.opt_overlap == "on")
     step.capture()
     for _ in range(a.warmup):
         loss = step()
@@ -62,6 +64,7 @@ def main():
     print(json.dumps({"metric": "VGG-16-BN CIFAR-100 training images/s (1 GPU, graphed step)",
                       "value": round(B * a.steps / dt, 1), "unit": "images/s", "ms_per_step": round(ms, 4),
                       "batch": B, "optimizer": a.opt, "steps": a.steps, "warmup": a.warmup,
+                      "opt_overlap": bool(getattr(step, "segment_opt", None)),
                       "loss_first_last": [round(l0, 4), round(float(loss), 4)],
                       "data": "synthetic CIFAR-100-shaped uint8 in HBM, on-device crop/flip/normalise; random init"}),
           flush=True)
