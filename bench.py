@@ -342,6 +342,7 @@ def main():
                        "comm_plan_source": plan.source if plan is not None else None,
                        "comm_transport": (("peer" if getattr(step, "peer", None) is not None else "rccl")
                                           if comm else None),
+                       "sgd_rider": getattr(step, "ride_plan", None),
                        "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }

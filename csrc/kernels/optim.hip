@@ -16,6 +16,7 @@
 // Optimizer-state reset at every K-AVG round (reference network.py:121-128) is a
 // hipMemsetAsync of the state buffers (kml_memset).
 #include "kml_common.h"
+#include "kml_sgd.h"
 
 namespace {
 
@@ -36,45 +37,8 @@ __global__ void k_sgd(float* __restrict__ w, const float* __restrict__ g, float*
   // first step after a reset (torch: momentum buffer := d, no dampening).  The flag lives
   // in device memory so a graph-captured step follows reset_state() between replays.
   const int first = first_ptr ? (*first_ptr != 0.f) : first_host;
-  const long long n4 = n >> 2;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 W = reinterpret_cast<float4*>(w)[i];
-    const float4 G = reinterpret_cast<const float4*>(g)[i];
-    float wv[4] = {W.x, W.y, W.z, W.w}, gv[4] = {G.x, G.y, G.z, G.w};
-    float mv[4] = {0, 0, 0, 0};
-    if (mom && momentum != 0.f) {
-      const float4 Mv = reinterpret_cast<float4*>(mom)[i];
-      mv[0] = Mv.x; mv[1] = Mv.y; mv[2] = Mv.z; mv[3] = Mv.w;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float d = gv[k] * grad_scale + wd * wv[k];
-      if (mom && momentum != 0.f) {
-        mv[k] = first ? d : momentum * mv[k] + (1.f - dampening) * d;
-        d = nesterov ? d + momentum * mv[k] : mv[k];
-      }
-      wv[k] -= lr * d;
-    }
-    reinterpret_cast<float4*>(w)[i] = make_float4(wv[0], wv[1], wv[2], wv[3]);
-    if (mom && momentum != 0.f) reinterpret_cast<float4*>(mom)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    if (shadow) {
-      uint2 s;
-      s.x = pack_bf2(wv[0], wv[1]);
-      s.y = pack_bf2(wv[2], wv[3]);
-      reinterpret_cast<uint2*>(shadow)[i] = s;
-    }
-  }
-  // scalar tail
-  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    float d = g[i] * grad_scale + wd * w[i];
-    if (mom && momentum != 0.f) {
-      mom[i] = first ? d : momentum * mom[i] + (1.f - dampening) * d;
-      d = nesterov ? d + momentum * mom[i] : mom[i];
-    }
-    w[i] -= lr * d;
-    if (shadow) shadow[i] = f2bf(w[i]);
-  }
+  kml_sgd_range(w, g, mom, shadow, lr, wd, momentum, dampening, nesterov, first, grad_scale, n,
+                blockIdx.x * (long long)blockDim.x + threadIdx.x, (long long)gridDim.x * blockDim.x);
 }
 
 __global__ void k_adam(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ m,

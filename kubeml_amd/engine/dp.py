@@ -31,6 +31,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     bucket_mb: float = 0.0, force_comm: bool = False, warmup: int = 1,
                     extra_state: Sequence[torch.Tensor] = (), comm_dtype=None,
                     opt_overlap: Optional[bool] = None, advance=None, plan=None, peer=None,
+                    ride: Optional[bool] = None,
                     comm_timing: int = 0, forward: Optional[Callable] = None) -> GraphedTrainStep:
     """Build (not capture) the train step on static input buffers ``x``/``y``.
 
@@ -58,6 +59,12 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             creates one sized for the flat gradient — collective over ``group``.
     comm_timing: T > 0 stamps the collectives on the device every step and samples their time
             every T-th step (``step.comm_seconds()``; exported as kubeml_allreduce_seconds)
+    ride:   apply the SGD update of the parameters ``model.ride_plan()`` names (ResNet: layer4 + fc)
+            in extra blocks of the grouped conv-backward launches of its host convs (layer3), where
+            the memory-bound update streams beside latency-bound conv tiles in the same launch (no
+            second queue); the end-of-step launch then covers the rest.  One GPU, no collective,
+            fused SGD.  None = ``KUBEML_RIDE`` (default on: ResNet-34 1.330 -> 1.320 ms/step over six
+            alternating runs on two boxes, bit-identical weights; profiles/r5/sgd_rider.md).
     forward: ``forward(model, x, y) -> loss`` in place of ``loss_fn(model(x), y)`` (models whose
             call takes more than the batch, e.g. BERT MLM with its positions and labels, or a
             step that prepares its batch on the device first); the step is then not stage-split
@@ -188,6 +195,13 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             backward_loss(loss)
             space.finish_grads()
             return loss
+    if ride is None:
+        ride = os.environ.get("KUBEML_RIDE", "1") == "1"
+    riding = bool(ride and fwd_bwd is not None and not comm and shard is None and seg_opt is None
+                  and forward is None and hasattr(model, "ride_plan") and getattr(optimizer, "kind", None) == "sgd"
+                  and optimizer.supports_ranges() and space.grad.is_cuda and bool(model.ride_plan()))
+    if riding:
+        fwd_bwd, opt_step = _ride(model, space, optimizer, fwd_bwd, post, lambda: fold, scale)
     shard_step = on_replay = seg_shard = None
     if shard is not None:
         blocks = plan.max_blocks
@@ -237,7 +251,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
             space._master_stale = True
 
     optimizer.set_grad_scale(scale)
-    return GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
+    step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
                             graph_comm=graph_comm, comm_dtype=comm_dtype,
                             state_tensors=train_state_tensors(model, space, optimizer, extra_state),
@@ -246,3 +260,83 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing,
                             shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1),
                             segment_shard=seg_shard)
+    step.ride_plan = (os.environ.get("KUBEML_RIDE_PLAN") or "4f:321") if riding else None
+    return step
+
+
+def _ride(model, space, optimizer, fwd_bwd, post, get_fold, scale):
+    """make_train_step's ``ride``: SgdRider slices of each ride group armed on its host convs for
+    the duration of the step's backward; the end-of-step SGD covers the remaining ranges."""
+    from ..ops import kernels as K
+    g = optimizer.param_groups[0]
+    dev = space.grad.device
+    mom = optimizer._bufs(space, ["momentum"])["momentum"] if g["momentum"] != 0 else None
+    first = optimizer.first_tensor(dev) if mom is not None else None
+    lr = optimizer.lr_tensor(dev)
+    blocks = int(os.environ.get("KUBEML_RIDE_BLOCKS", "512"))   # measured: 32 / 64 lose, 512-1024 best
+    riders, covered, seen = [], [], set()       # riders: (group, SgdRider)
+    groups = model.ride_plan()
+    holder = {}                                 # this step's take(): set below
+
+    def take_for(j):
+        return lambda: holder["take"](j)
+    for gi, (params, hosts) in enumerate(groups):
+        lo, hi = space.range_of(params)
+        if hi <= lo or not hosts or any(id(h) in seen for h in hosts):
+            raise ValueError("ride plan: each group needs parameters and host convs of its own")
+        seen.update(id(h) for h in hosts)
+        covered.append((lo, hi))
+        n = len(hosts)
+        cuts = [lo + ((hi - lo) * i // n) // 64 * 64 for i in range(n)] + [hi]
+        for i, (conv, a, b) in enumerate(zip(hosts, cuts, cuts[1:])):
+            r = None if b <= a else K.SgdRider(
+                space.master[a:b], space.grad[a:b], None if mom is None else mom[a:b],
+                None if space.shadow is None else space.shadow[a:b], lr, first, g["weight_decay"], g["momentum"],
+                g["dampening"], g["nesterov"], scale, blocks)
+            riders.append((gi, r))
+            object.__setattr__(conv, "_kml_rider", take_for(len(riders) - 1))
+    covered.sort()
+    if any(a[1] > b[0] for a, b in zip(covered, covered[1:])):
+        raise ValueError("ride plan: groups overlap in the flat layout")
+    rest, pos = [], 0
+    for a, b in covered:
+        if a > pos:
+            rest.append((pos, a))
+        pos = b
+    if pos < space.numel:
+        rest.append((pos, space.numel))
+    state = {"active": False, "fired": set(), "taken": set()}
+
+    def _rider_take_impl(j):
+        gi, r = riders[j]
+        if not state["active"] or r is None or j in state["taken"]:
+            return None
+        if gi not in state["fired"]:
+            space.finish_grads(groups[gi][0])   # e.g. layer3's deferred folds, one launch, here
+            state["fired"].add(gi)
+        state["taken"].add(j)
+        return r
+    holder["take"] = _rider_take_impl
+
+    def ride_fwd_bwd():
+        state["active"], state["fired"], state["taken"] = True, set(), set()
+        try:
+            return fwd_bwd()
+        finally:
+            state["active"] = False
+
+    def ride_opt_step():
+        optimizer.set_grad_scale(scale)
+        # a host conv whose backward did not run (or took another path) leaves its slice to here
+        for j, (gi, r) in enumerate(riders):
+            if r is not None and j not in state["taken"]:
+                r.run_alone()
+        for k, (a, b) in enumerate(rest):
+            optimizer.step_range(a, b, max_blocks=2048, advance=get_fold() if k == len(rest) - 1 else None)
+        if not rest and get_fold() is not None:
+            K.advance_counter_(*get_fold())
+        optimizer.finish_ranges()
+        if post is not None:
+            post()
+    return ride_fwd_bwd, ride_opt_step
+

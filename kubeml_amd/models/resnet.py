@@ -201,6 +201,29 @@ class ResNet(tnn.Module):
         return [self._chained(self._stem_l1), self._chained(self.layer2), self._chained(self.layer3),
                 lambda h: self.fc(self.avgpool(self._chained(self.layer4)(h)))]
 
+    def ride_plan(self):
+        """[(parameters, host convs), ...] for engine/dp.py ``ride``: each group's SGD update runs
+        in extra blocks of its host convs' grouped backward launches, which all run after the
+        group's gradients are final (backward order: fc, layer4, layer3, layer2, layer1).
+        ``KUBEML_RIDE_PLAN`` = groups separated by ``;``, each ``<layers>:<host layers>`` with
+        ``f`` for fc: "4f:3;3:21" rides layer4 + fc on layer3's convs and layer3 on layer2's and
+        layer1's.  Layer3's 3x3 convs run unrolled; their deferred gradient fold runs when the
+        first layer-2 host takes its slice (the same single fold launch, earlier)."""
+        import os
+        spec = os.environ.get("KUBEML_RIDE_PLAN")
+        if spec is None:
+            # measured on ResNet-34 / CIFAR (BasicBlock); other depths ride only when asked
+            if not isinstance(self.layer1[0], BasicBlock):
+                return []
+            spec = "4f:321"
+        groups = []
+        for part in filter(None, spec.split(";")):
+            own, host = part.split(":")
+            ps = [p for d in own for p in (self.fc if d == "f" else getattr(self, f"layer{d}")).parameters()]
+            hosts = [m for d in host for m in getattr(self, f"layer{d}").modules() if isinstance(m, M.Conv2d)]
+            groups.append((ps, hosts))
+        return groups
+
     def stage_params(self):
         """Parameters owned by each stage of :meth:`stages`."""
         later = ("layer2.", "layer3.", "layer4.", "fc.")

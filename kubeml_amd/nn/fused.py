@@ -304,7 +304,7 @@ class ConvBNUnit:
             dw, wacc = _wgrad_target(conv, x, wu is not None)
             bnb = (c, partial[0], partial[1], mean, rstd, master_of(bn.weight), dg, db, acc)
             r = K.conv_bwd(dy, w, x, dw, kh, kw, conv.stride, conv.padding, addend=addend, bnf=bnf, wu=wu,
-                           bnf_mask=True, accumulate=wacc, bnb=bnb)
+                           bnf_mask=True, accumulate=wacc, bnb=bnb, rider=_take_rider(conv))
             if wu is not None:
                 conv.weight._kml_flat.defer_fold22(conv.weight, dw)
             dx, part_out = r if bnf is not None else (r, None)
@@ -322,18 +322,29 @@ class ConvBNUnit:
                 object.__setattr__(conv, "_kml_wants_wt", True)   # batched by refresh_transposed()
             dw, acc = _wgrad_target(conv, x, wu is not None)
             r = K.conv_bwd(dc, w, x, dw, kh, kw, conv.stride, conv.padding,
-                           addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True, accumulate=acc)
+                           addend=addend, bnf=bnf, wt=wt, wu=wu, bnf_mask=True, accumulate=acc,
+                           rider=_take_rider(conv))
             if wu is not None:
                 conv.weight._kml_flat.defer_fold22(conv.weight, dw)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out
         _wgrad(x, dc, conv, unroll=wu is not None)
+        rider = _take_rider(conv)
+        if rider is not None:
+            rider.run_alone()
         if need_dx:
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
                              addend=addend, bnf=bnf, wu=wu, bnf_mask=True)
             dx, part_out = r if bnf is not None else (r, None)
         return dx, dres, part_out
+
+
+def _take_rider(conv):
+    """The optimizer-update rider armed on this conv for the current backward (engine/dp.py
+    ``ride``: a callable returning an ``ops.kernels.SgdRider`` or None), else None."""
+    r = getattr(conv, "_kml_rider", None)
+    return r() if r is not None else None
 
 
 class PendingBN:

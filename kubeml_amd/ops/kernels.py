@@ -922,7 +922,7 @@ def bnb_ok(x_shape, K, KH, KW, stride, pad, G, unroll=False) -> bool:
 
 
 def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None,
-             bnf_mask=False, accumulate=True, dbias=None, bias_accumulate=True, bnb=None):
+             bnf_mask=False, accumulate=True, dbias=None, bias_accumulate=True, bnb=None, rider=None):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
     :func:`conv_dgrad`) and ``dw += wgrad`` (``accumulate=False``: ``dw = wgrad``).  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
@@ -935,7 +935,9 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     dbias: as in :func:`conv_wgrad` (1x1/s1/p0 convs).
     bnb = (c, part, G, mean, rstd, gamma, dgamma, dbeta, acc): ``dy`` is dz, the masked gradient
     of this conv's BatchNorm OUTPUT; the BN backward (dc from dz, c and the partial rows;
-    dgamma / dbeta written or, acc, added) runs inside both GEMMs' operand staging (bnb_ok)."""
+    dgamma / dbeta written or, acc, added) runs inside both GEMMs' operand staging (bnb_ok).
+    rider: an :class:`SgdRider` applied by extra blocks of the grouped launch (or by its own
+    launch after the two GEMMs when this conv does not run grouped)."""
     _chk(dy, BF16, "dy", 4)
     _chk(w, BF16, "w", 4)
     _chk(x, BF16, "x", 4)
@@ -985,6 +987,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
                    dbias=dbias, bias_accumulate=bias_accumulate)
         r = conv_dgrad(dy, w, (B, H, W, C), KH, KW, stride, pad, addend=addend, cfg=dplan, bnf=bnf, wt=wt, _fold=fold,
                        bnf_mask=bnf_mask, _g22=g22)
+        if rider is not None:
+            rider.run_alone()
         if not fold:
             return r
         if bnf is not None:
@@ -1015,23 +1019,37 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         ibc, bpart, bG, bmean_, brstd_, bgamma, bdg, bdb, bacc = bnb
         if variant != 0:
             raise ValueError("conv_bwd bnb: register-staged igemm dgrad only")
-        HIP.call("kml_conv_bwd_pair_bnb", "p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i i p p i p p p p p i s",  # noqa: E501
-                 _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
-                 _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
-                 _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
-                 int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), int(g22),
-                 _p(ibc), _p(bpart), int(bG), _p(bgamma), _p(bmean_), _p(brstd_), _p(bdg), _p(bdb), int(bool(bacc)),
-                 _s())
+        if rider is not None:
+            rider.arm()
+        try:
+            HIP.call("kml_conv_bwd_pair_bnb", "p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i i p p i p p p p p i s",  # noqa: E501
+                     _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
+                     _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits,
+                     variant, _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
+                     int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), int(g22),
+                     _p(ibc), _p(bpart), int(bG), _p(bgamma), _p(bmean_), _p(brstd_), _p(bdg), _p(bdb),
+                     int(bool(bacc)), _s())
+        except Exception:
+            if rider is not None:
+                SgdRider.disarm()
+            raise
         if fold:
             out = out.view(B, 2, 2, C // 4)
         return (out, (part, G)) if bnf is not None else out
-    HIP.call("kml_conv_bwd_pair",
-             "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i i s",
-             _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
-             _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits, variant,
-             _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
-             int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _p(dbias),
-             int(bool(bias_accumulate)), int(g22), _s())
+    if rider is not None:
+        rider.arm()
+    try:
+        HIP.call("kml_conv_bwd_pair",
+                 "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i i s",
+                 _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
+                 _p(grp), _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits,
+                 variant, _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
+                 int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _p(dbias),
+                 int(bool(bias_accumulate)), int(g22), _s())
+    except Exception:
+        if rider is not None:
+            SgdRider.disarm()
+        raise
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out
@@ -1463,6 +1481,44 @@ def sgd_(w, g, mom, shadow, lr, wd=0.0, momentum=0.0, dampening=0.0, nesterov=Fa
     HIP.call("kml_sgd", "p p p p p f f f f i p i f l i p f f s", _p(w), _p(g), _p(mom), _p(shadow), _p(lr_dev),
              float(lr), float(wd), float(momentum), float(dampening), int(nesterov), _p(first_dev), int(first),
              float(grad_scale), n, int(max_blocks), _p(ctr), ab, an, _s())
+
+
+class SgdRider:
+    """One fused-SGD range carried by a grouped conv-backward launch (``conv_bwd(rider=...)``,
+    ``k_conv_pair``'s third role, csrc/include/kml_sgd.h): the same element update as
+    :func:`sgd_` with the learning rate and the first-step flag read on the device, so a
+    graph-captured step follows ``set_lr`` / ``reset_state``.  w / g / mom / shadow are the
+    range's views of the flat buffers."""
+    __slots__ = ("w", "g", "mom", "shadow", "lr_dev", "first_dev", "wd", "momentum", "dampening", "nesterov",
+                 "grad_scale", "blocks")
+
+    def __init__(self, w, g, mom, shadow, lr_dev, first_dev, wd, momentum, dampening, nesterov, grad_scale,
+                 blocks=128):
+        _chk(w, F32, "rider w")
+        _chk(g, F32, "rider g")
+        if lr_dev is None or w.numel() != g.numel() or (mom is not None and mom.numel() != w.numel()):
+            raise ValueError("SgdRider: device lr and matching w / g / mom ranges required")
+        self.w, self.g, self.mom, self.shadow = w, g, mom, shadow
+        self.lr_dev, self.first_dev = lr_dev, first_dev
+        self.wd, self.momentum, self.dampening = float(wd), float(momentum), float(dampening)
+        self.nesterov, self.grad_scale, self.blocks = bool(nesterov), float(grad_scale), int(blocks)
+
+    def arm(self):
+        """The next grouped launch (kml_conv_bwd_pair*) carries this update."""
+        HIP.call("kml_pair_rider_set", "p p p p p p f f f i f l i", _p(self.w), _p(self.g), _p(self.mom),
+                 _p(self.shadow), _p(self.lr_dev), _p(self.first_dev), self.wd, self.momentum, self.dampening,
+                 int(self.nesterov), self.grad_scale, self.w.numel(), self.blocks)
+
+    @staticmethod
+    def disarm():
+        """Drop an armed rider (its pair launch was not issued)."""
+        HIP.call("kml_pair_rider_set", "p p p p p p f f f i f l i", 0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 1.0, 0, 0)
+
+    def run_alone(self):
+        """The same update as its own launch (the conv it rode with ran as two launches)."""
+        sgd_(self.w, self.g, self.mom, self.shadow, 0.0, wd=self.wd, momentum=self.momentum,
+             dampening=self.dampening, nesterov=self.nesterov, grad_scale=self.grad_scale, lr_dev=self.lr_dev,
+             first_dev=self.first_dev, max_blocks=self.blocks)
 
 
 def adam_(w, g, m, v, shadow, lr, step, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, decoupled=False,

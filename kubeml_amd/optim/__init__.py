@@ -208,12 +208,13 @@ class SGD(FusedOptimizer):
         return self.supports_ranges()
 
     @torch.no_grad()
-    def step_range(self, start: int, end: int, max_blocks: int = 0, advance_step: bool = True):
+    def step_range(self, start: int, end: int, max_blocks: int = 0, advance_step: bool = True, advance=None):
         """The fused step restricted to flat elements [start, end): the gradients of a
         finished backward stage are applied while earlier stages still run backward.  The
         first-step flag stays set until :meth:`finish_ranges` (every range of the step
         reads the same value); the union of one step's ranges must cover the space once.
-        advance_step: accepted for the ranged-step protocol (SGD keeps no step counter)."""
+        advance_step: accepted for the ranged-step protocol (SGD keeps no step counter).
+        advance: (ctr, batch, n) data-counter advance folded into this launch (as :meth:`step`)."""
         g = self.param_groups[0]
         spaces, loose = self._flat_groups()
         if len(spaces) != 1 or loose:
@@ -230,7 +231,7 @@ class SGD(FusedOptimizer):
                None if sp.shadow is None else sp.shadow[start:end], g["lr"], wd=g["weight_decay"],
                momentum=g["momentum"], dampening=g["dampening"], nesterov=g["nesterov"], first=self._first,
                grad_scale=self._grad_scale, lr_dev=self.lr_tensor(sp.device), first_dev=first,
-               max_blocks=max_blocks or _RANGE_BLOCKS)
+               max_blocks=max_blocks or _RANGE_BLOCKS, advance=advance)
 
     @torch.no_grad()
     def finish_ranges(self):

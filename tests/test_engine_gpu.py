@@ -204,13 +204,13 @@ def test_bench_trace_has_compute_and_comm_tracks(tmp_path):
         assert e["dur"] >= 0
 
 
-def _graphed_run(opt_overlap, steps=3):
+def _graphed_run(opt_overlap, steps=3, ride=False, arch="resnet18"):
     from kubeml_amd.engine.dp import make_train_step
-    from kubeml_amd.models.resnet import resnet18
+    from kubeml_amd.models import resnet as R
     from kubeml_amd.nn import cross_entropy, flatten_module
     from kubeml_amd.optim import SGD
     torch.manual_seed(0)
-    m = resnet18(10).to(dev)
+    m = getattr(R, arch)(10).to(dev)
     m.train()
     sp = flatten_module(m)
     opt = SGD(m.parameters(), lr=1e-3, momentum=0.9, dampening=0.1, weight_decay=1e-4)
@@ -230,12 +230,28 @@ def _graphed_run(opt_overlap, steps=3):
         i.add_(1)
     w0 = sp.master.clone()
     step = make_train_step(m, sp, opt, cross_entropy, x, y, pre=pre, post=post, opt_overlap=opt_overlap,
-                           extra_state=[i])
+                           extra_state=[i], ride=ride)
     assert (step.segment_opt is not None) == opt_overlap
     step.capture()
     losses = [float(step()) for _ in range(steps)]
     torch.cuda.synchronize()
     return sp.master - w0, sp, losses
+
+
+@pytest.mark.parametrize("arch,plan", [("resnet18", "4f:321"), ("resnet34", "4f:321"), ("resnet34", "4f:3;3:21")])
+def test_ride_sgd_in_backward_launches_is_bit_exact(arch, plan, monkeypatch):
+    """make_train_step(ride=True): the SGD (momentum, dampening, weight decay, first step after
+    the reset) of layer4 + fc — and, with the two-group plan, of layer3 after its early gradient
+    fold — runs in extra blocks of later layers' grouped conv-backward launches (k_conv_pair's
+    rider role, the same element update as k_sgd: csrc/include/kml_sgd.h); the end-of-step
+    launch covers the rest.  Bit-identical masters, momenta and shadows."""
+    monkeypatch.setenv("KUBEML_RIDE_PLAN", plan)
+    ua, spa, la = _graphed_run(False, ride=True, arch=arch)
+    ub, spb, lb = _graphed_run(False, ride=False, arch=arch)
+    assert float(ub.abs().max()) > 1e-5
+    assert torch.equal(ua, ub)
+    assert la == lb
+    assert torch.equal(spa.shadow, spb.shadow)
 
 
 def test_graphed_optimizer_overlap_matches_end_of_step_update():
