@@ -264,6 +264,22 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     return step
 
 
+def ride_rest(covered, numel):
+    """The flat ranges of [0, numel) no ride group covers (the end-of-step update's ranges), in
+    order; ``covered``: the groups' [lo, hi) ranges, which must not overlap."""
+    covered = sorted(covered)
+    if any(a[1] > b[0] for a, b in zip(covered, covered[1:])):
+        raise ValueError("ride plan: groups overlap in the flat layout")
+    rest, pos = [], 0
+    for a, b in covered:
+        if a > pos:
+            rest.append((pos, a))
+        pos = max(pos, b)
+    if pos < numel:
+        rest.append((pos, numel))
+    return rest
+
+
 def _ride(model, space, optimizer, fwd_bwd, post, get_fold, scale):
     """make_train_step's ``ride``: SgdRider slices of each ride group armed on its host convs for
     the duration of the step's backward; the end-of-step SGD covers the remaining ranges."""
@@ -295,16 +311,7 @@ def _ride(model, space, optimizer, fwd_bwd, post, get_fold, scale):
                 g["dampening"], g["nesterov"], scale, blocks)
             riders.append((gi, r))
             object.__setattr__(conv, "_kml_rider", take_for(len(riders) - 1))
-    covered.sort()
-    if any(a[1] > b[0] for a, b in zip(covered, covered[1:])):
-        raise ValueError("ride plan: groups overlap in the flat layout")
-    rest, pos = [], 0
-    for a, b in covered:
-        if a > pos:
-            rest.append((pos, a))
-        pos = b
-    if pos < space.numel:
-        rest.append((pos, space.numel))
+    rest = ride_rest(covered, space.numel)
     state = {"active": False, "fired": set(), "taken": set()}
 
     def _rider_take_impl(j):

@@ -260,3 +260,31 @@ def test_grad_peer_reused_only_if_it_fits():
     c.grad_peer = small = _FakePeer(fits=False)
     assert km._reusable_peer(c, plan) is None and small.closed and c.grad_peer is None
     assert km._reusable_peer(c, parse_plan("rccl:end:fp32")) is None
+
+
+def test_ride_plan_groups_and_rest_ranges(monkeypatch):
+    """The SGD rider's plan (engine/dp.py ``ride``): ResNet groups from KUBEML_RIDE_PLAN, host convs
+    disjoint per group, and the end-of-step ranges = the complement of the groups' flat ranges."""
+    import pytest
+    from kubeml_amd.engine.dp import ride_rest
+    from kubeml_amd.models.resnet import resnet18, resnet50
+    from kubeml_amd.nn import flatten_module
+    m = resnet18(10)
+    sp = flatten_module(m)
+    monkeypatch.delenv("KUBEML_RIDE_PLAN", raising=False)
+    (ps, hosts), = m.ride_plan()
+    assert {id(p) for p in ps} == {id(p) for p in list(m.layer4.parameters()) + list(m.fc.parameters())}
+    assert len(hosts) == 5 + 5 + 4          # layer3 (with its downsample), layer2 (same), layer1
+    lo, hi = sp.range_of(ps)
+    assert lo == 0 and 0 < hi < sp.numel     # later layers sit first in the flat layout
+    assert ride_rest([(lo, hi)], sp.numel) == [(hi, sp.numel)]
+    monkeypatch.setenv("KUBEML_RIDE_PLAN", "4f:3;3:21")
+    g = m.ride_plan()
+    assert len(g) == 2 and not {id(h) for h in g[0][1]} & {id(h) for h in g[1][1]}
+    r = [sp.range_of(p) for p, _ in g]
+    assert ride_rest(r, sp.numel) == [(r[1][1], sp.numel)]
+    assert ride_rest([(10, 20)], 30) == [(0, 10), (20, 30)]
+    with pytest.raises(ValueError):
+        ride_rest([(0, 20), (10, 30)], 40)
+    monkeypatch.delenv("KUBEML_RIDE_PLAN", raising=False)
+    assert resnet50(10).ride_plan() == []    # measured on BasicBlock nets only
