@@ -65,6 +65,19 @@ struct KmlSgdRider {
   long long n;
 };
 
+// The rider armed for the next rider-capable launch of this process (kml_rider_set; defined in
+// util.hip, consumed — and cleared — by k_conv_pair's and k_bn_bwd_apply_v's launchers)
+extern KmlSgdRider g_kml_rider;
+
+extern "C" int kml_rider_flush(hipStream_t s);   // util.hip: an armed rider as its own launch
+
+// take the armed rider (blocks = 0: none) and disarm it
+static inline KmlSgdRider kml_rider_take() {
+  const KmlSgdRider r = g_kml_rider;
+  g_kml_rider.blocks = 0;
+  return r;
+}
+
 // block `b` of the rider's `blocks` (256 threads each)
 __device__ __forceinline__ void kml_sgd_rider_run(const KmlSgdRider& r, int b) {
   const float lr = *r.lr_ptr;

@@ -18,6 +18,7 @@
 // batch variance for normalisation, unbiased for the running estimate), which the
 // reference gets from cuDNN through torchvision resnet34 (function_resnet34.py:101).
 #include "kml_common.h"
+#include "kml_sgd.h"
 
 #include <cstdlib>
 
@@ -690,7 +691,12 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
     const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C, int acc) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C, int acc, KmlSgdRider rider) {
+  // optimizer-update rider (kml_sgd.h): the last rider.blocks blocks of the grid
+  if ((int)blockIdx.x >= (int)gridDim.x - rider.blocks) {
+    kml_sgd_rider_run(rider, (int)blockIdx.x - ((int)gridDim.x - rider.blocks));
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
   float4* red4 = reinterpret_cast<float4*>(sh);
   float* ka = sh + 4 * NT;
@@ -700,7 +706,7 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   float* rs = ka + 4 * C;
   const float invM = 1.f / (float)M;
   const int n8 = (int)(M * C / 8);
-  const int T = (int)gridDim.x * NT;
+  const int T = ((int)gridDim.x - rider.blocks) * NT;
   const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
   const bool early = C / 2 <= NT;
   EarlyRows er;
@@ -1138,15 +1144,17 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const int V = max(pick_v(n8, 4), vmin_bwd());
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
+    const KmlSgdRider rider = kml_rider_take();
 #define KML_BWD_V(VV)                                                                                          \
-  hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, dy, y, x, mean, rstd, gamma, part, \
-                     G, dgamma, dbeta, dx, dres, M, C, acc)
+  hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, mean, \
+                     rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider)
     if (V == 1) KML_BWD_V(1);
     else if (V == 2) KML_BWD_V(2);
     else KML_BWD_V(4);
 #undef KML_BWD_V
     KML_LAUNCH_CHECK();
   }
+  if (g_kml_rider.blocks > 0) (void)kml_rider_flush(s);   // an armed rider rides alone on these paths
   if (wide_sum(G, C)) {
     constexpr int NT = 1024;
     long long ab = (M * C / 8 + NT - 1) / NT;

@@ -2689,16 +2689,12 @@ using WgIg6432B = IgemmBody<WGRAD, 64, 32, 64, true, true>;
   X(0, 32, 32, 64, DgIg3232B, 32, 32, WgIg3232B, 32, 32)     \
   X(0, 32, 32, 64, DgIg3232B, 32, 32, WgIg6432B, 64, 32)
 
-// the rider the next grouped launch of this process carries (kml_pair_rider_set; consumed once)
-KmlSgdRider g_pair_rider = {};
-
 template <class DB, class WB>
 int launch_pair(const ConvArgs& ad, int dbm, int dbn, const ConvArgs& aw, int wbm, int wbn, hipStream_t s) {
   const int dgx = (ad.N + dbn - 1) / dbn, dgy = (ad.M + dbm - 1) / dbm;
   const int wgx = (aw.N + wbn - 1) / wbn, wgy = (aw.M + wbm - 1) / wbm;
   const long long nd = (long long)dgx * dgy * ad.splits, nw = (long long)wgx * wgy * aw.splits;
-  const KmlSgdRider rider = g_pair_rider;
-  g_pair_rider.blocks = 0;
+  const KmlSgdRider rider = kml_rider_take();
   if (nd + nw + rider.blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL((k_conv_pair<DB, WB>), dim3((unsigned)(nd + nw + rider.blocks)), dim3(256), 0, s, ad, aw, dgx,
                      dgy, wgx, wgy, (int)nd, (int)nw, rider);
@@ -3093,21 +3089,6 @@ KML_API int kml_conv_pair_supported(int dvariant, int dbm, int dbn, int dbk, int
 KML_API int kml_conv_pair_bnb_supported(int dvariant, int dbm, int dbn, int dbk, int wvariant, int wbm, int wbn,
                                         int wbk) {
   return pair_bnb_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk) > 0 ? 1 : 0;
-}
-
-// Arm an SGD range rider for the NEXT grouped conv-backward launch (kml_conv_bwd_pair /
-// kml_conv_bwd_pair_bnb) of this process: `blocks` extra 256-thread blocks apply the fused SGD to
-// n flat elements (w / g / mom / shadow already offset to the range; lr and the first-step flag
-// read on the device).  blocks = 0 disarms.  The caller launches the pair right after.
-KML_API int kml_pair_rider_set(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr,
-                               const float* first_ptr, float wd, float momentum, float dampening, int nesterov,
-                               float grad_scale, long long n, int blocks) {
-  if (blocks < 0 || (blocks > 0 && (!w || !g || !lr_ptr || n <= 0 || (((uintptr_t)w | (uintptr_t)g) & 15) ||
-                                    (mom && ((uintptr_t)mom & 15)) || (shadow && ((uintptr_t)shadow & 7)))))
-    return (int)hipErrorInvalidValue;
-  g_pair_rider = KmlSgdRider{w, g, mom, shadow, lr_ptr, first_ptr, wd, momentum, dampening, grad_scale, nesterov,
-                             blocks, n};
-  return (int)hipSuccess;
 }
 
 // dX (dgrad, + addend, + consumer-BN partials) and dW (wgrad, fp32 +=) of one conv in one

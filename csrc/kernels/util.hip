@@ -1,5 +1,6 @@
 // util.hip — small utility kernels: version probe, fill, scale, cast, axpby.
 #include "kml_common.h"
+#include "kml_sgd.h"
 
 KML_API int kml_abi_version() { return 1; }
 
@@ -298,5 +299,36 @@ KML_API int kml_zero_ranges(float* base, const long long* offs, const int* ns, i
   if (gx > 64) gx = 64;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(k_zero_ranges, dim3(gx, count), dim3(256), 0, s, base, zr);
+  KML_LAUNCH_CHECK();
+}
+
+
+// ---- optimizer-update riders (kml_sgd.h) ------------------------------------------------------
+KmlSgdRider g_kml_rider = {};
+
+namespace {
+__global__ __launch_bounds__(256) void k_sgd_rider_alone(KmlSgdRider r) { kml_sgd_rider_run(r, blockIdx.x); }
+}  // namespace
+
+// Arm an SGD range rider for the NEXT rider-capable launch of this process (kml_conv_bwd_pair,
+// kml_conv_bwd_pair_bnb, kml_bn_bwd / kml_bn_bwd_apply_partial): `blocks` extra 256-thread blocks
+// apply the fused SGD to n flat elements (w / g / mom / shadow offset to the range; lr and the
+// first-step flag read on the device).  blocks = 0 disarms.
+KML_API int kml_rider_set(float* w, const float* g, float* mom, bf16_t* shadow, const float* lr_ptr,
+                          const float* first_ptr, float wd, float momentum, float dampening, int nesterov,
+                          float grad_scale, long long n, int blocks) {
+  if (blocks < 0 || (blocks > 0 && (!w || !g || !lr_ptr || n <= 0 || (((uintptr_t)w | (uintptr_t)g) & 15) ||
+                                    (mom && ((uintptr_t)mom & 15)) || (shadow && ((uintptr_t)shadow & 7)))))
+    return (int)hipErrorInvalidValue;
+  g_kml_rider = KmlSgdRider{w, g, mom, shadow, lr_ptr, first_ptr, wd, momentum, dampening, grad_scale, nesterov,
+                            blocks, n};
+  return (int)hipSuccess;
+}
+
+// run an armed rider as its own launch (a rider-capable call that took another path)
+KML_API int kml_rider_flush(hipStream_t s) {
+  const KmlSgdRider r = kml_rider_take();
+  if (r.blocks <= 0) return (int)hipSuccess;
+  hipLaunchKernelGGL(k_sgd_rider_alone, dim3(r.blocks), dim3(256), 0, s, r);
   KML_LAUNCH_CHECK();
 }

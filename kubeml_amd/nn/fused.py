@@ -311,7 +311,7 @@ class ConvBNUnit:
             return dx, (dy if want_dres else None), part_out
         dres = torch.empty_like(dy) if want_dres else None
         dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
-                      dg, db, dres=dres, partial=partial, accumulate=acc)
+                      dg, db, dres=dres, partial=partial, accumulate=acc, rider=_take_rider(bn))
         object.__setattr__(conv, "_kml_wu", None)
         if need_dx:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)

@@ -1019,9 +1019,7 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         ibc, bpart, bG, bmean_, brstd_, bgamma, bdg, bdb, bacc = bnb
         if variant != 0:
             raise ValueError("conv_bwd bnb: register-staged igemm dgrad only")
-        if rider is not None:
-            rider.arm()
-        try:
+        with _Riding(rider):
             HIP.call("kml_conv_bwd_pair_bnb", "p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i i p p i p p p p p i s",  # noqa: E501
                      _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
                      _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits,
@@ -1029,16 +1027,10 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
                      int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), int(g22),
                      _p(ibc), _p(bpart), int(bG), _p(bgamma), _p(bmean_), _p(brstd_), _p(bdg), _p(bdb),
                      int(bool(bacc)), _s())
-        except Exception:
-            if rider is not None:
-                SgdRider.disarm()
-            raise
         if fold:
             out = out.view(B, 2, 2, C // 4)
         return (out, (part, G)) if bnf is not None else out
-    if rider is not None:
-        rider.arm()
-    try:
+    with _Riding(rider):
         HIP.call("kml_conv_bwd_pair",
                  "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i i s",
                  _p(dy), _p(w), _p(wt), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
@@ -1046,10 +1038,6 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
                  variant, _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
                  int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), _p(dbias),
                  int(bool(bias_accumulate)), int(g22), _s())
-    except Exception:
-        if rider is not None:
-            SgdRider.disarm()
-        raise
     if fold:
         out = out.view(B, 2, 2, C // 4)
     return (out, (part, G)) if bnf is not None else out
@@ -1215,10 +1203,11 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
 _BN_REDUCE = "fused"
 
 
-def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None, accumulate=True):
+def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, partial=None, accumulate=True,
+           rider=None):
     """dgamma/dbeta (``+=``, or ``=`` with accumulate=False) and dx; y given => ReLU mask
     applied; dres (optional) receives dz.  partial = (part, G) from conv_dgrad(bnf=...) skips
-    the reduction pass."""
+    the reduction pass.  rider: an :class:`SgdRider` run by extra blocks of the apply launch."""
     _chk(dy, BF16, "dy")
     _chk(x, BF16, "x")
     C = x.shape[-1]
@@ -1227,9 +1216,10 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         dx = torch.empty_like(x)
     if partial is not None:
         part, G = partial
-        HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s",
-                 _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
-                 _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), int(bool(accumulate)), _s())
+        with _Riding(rider):
+            HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s",
+                     _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
+                     _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), int(bool(accumulate)), _s())
         return dx
     ws = cnt = None
     if _BN_REDUCE in ("fused", "ticket"):
@@ -1237,9 +1227,10 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         ws = torch.empty(nws, dtype=F32, device=x.device)
         if _BN_REDUCE == "ticket":
             cnt = _COUNTERS.take(x.device, 1)
-    HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s",
-             _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
-             _p(dres), _p(ws), _p(cnt), M, C, int(bool(accumulate)), _s())
+    with _Riding(rider):
+        HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s",
+                 _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
+                 _p(dres), _p(ws), _p(cnt), M, C, int(bool(accumulate)), _s())
     return dx
 
 
@@ -1504,21 +1495,43 @@ class SgdRider:
         self.nesterov, self.grad_scale, self.blocks = bool(nesterov), float(grad_scale), int(blocks)
 
     def arm(self):
-        """The next grouped launch (kml_conv_bwd_pair*) carries this update."""
-        HIP.call("kml_pair_rider_set", "p p p p p p f f f i f l i", _p(self.w), _p(self.g), _p(self.mom),
+        """The next rider-capable launch (grouped conv backward, BN backward apply) carries this update."""
+        HIP.call("kml_rider_set", "p p p p p p f f f i f l i", _p(self.w), _p(self.g), _p(self.mom),
                  _p(self.shadow), _p(self.lr_dev), _p(self.first_dev), self.wd, self.momentum, self.dampening,
                  int(self.nesterov), self.grad_scale, self.w.numel(), self.blocks)
 
-    @staticmethod
-    def disarm():
-        """Drop an armed rider (its pair launch was not issued)."""
-        HIP.call("kml_pair_rider_set", "p p p p p p f f f i f l i", 0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 1.0, 0, 0)
-
     def run_alone(self):
-        """The same update as its own launch (the conv it rode with ran as two launches)."""
+        """The same update as its own launch (its host took a path without a rider role)."""
         sgd_(self.w, self.g, self.mom, self.shadow, 0.0, wd=self.wd, momentum=self.momentum,
              dampening=self.dampening, nesterov=self.nesterov, grad_scale=self.grad_scale, lr_dev=self.lr_dev,
              first_dev=self.first_dev, max_blocks=self.blocks)
+
+    @staticmethod
+    def disarm():
+        """Drop an armed rider (its host launch was not issued)."""
+        HIP.call("kml_rider_set", "p p p p p p f f f i f l i", 0, 0, 0, 0, 0, 0, 0.0, 0.0, 0.0, 0, 1.0, 0, 0)
+
+
+class _Riding:
+    """``with _Riding(rider): <one rider-capable launch>``: arm before the launch; afterwards an
+    unconsumed rider (the call took a path without a rider role) runs as its own launch; on an
+    exception it is dropped."""
+
+    def __init__(self, rider):
+        self.rider = rider
+
+    def __enter__(self):
+        if self.rider is not None:
+            self.rider.arm()
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if self.rider is not None:
+            if exc_type is None:
+                HIP.call("kml_rider_flush", "s", _s())
+            else:
+                SgdRider.disarm()
+        return False
 
 
 def adam_(w, g, m, v, shadow, lr, step, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, decoupled=False,
