@@ -448,6 +448,56 @@ __global__ __launch_bounds__(256) void k_embed_bwd_type(const long long* __restr
   }
 }
 
+// All three tables in ONE pass over dsum: one block per position p walks its B tokens
+// (t = b L + p) in batch order.  Word rows: one fp32 atomic per (token, column), consecutive lanes
+// on consecutive columns (256 contiguous bytes per wave instruction: the full atomic rate; the
+// per-token kernel above strided its lanes 16 bytes apart).  Position row: summed in registers in
+// the same order as k_embed_bwd_pos and added once (no atomics).  Token-type rows (<= 2 types):
+// per-block register sums, one atomic per block and column.
+__global__ __launch_bounds__(256) void k_embed_bwd_fused(const long long* __restrict__ ids,
+                                                         const long long* __restrict__ tt,
+                                                         const bf16_t* __restrict__ dsum, float* __restrict__ dword,
+                                                         float* __restrict__ dpos, float* __restrict__ dtype,
+                                                         long long T, int L, int N) {
+  const int p = blockIdx.x;
+  const long long B = T / L;
+  for (int c = threadIdx.x; c < N; c += 256) {
+    float ps = 0.f, ty0 = 0.f, ty1 = 0.f;
+    long long b = 0;
+    for (; b + 4 <= B; b += 4) {     // four tokens' loads in flight before their atomics
+      float v[4];
+      long long w[4];
+      int ty[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long t = (b + u) * L + p;
+        v[u] = bf2f(dsum[t * N + c]);
+        w[u] = ids[t];
+        ty[u] = tt ? (int)tt[t] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        atomicAdd(dword + w[u] * N + c, v[u]);
+        ps += v[u];
+        ty0 += ty[u] == 0 ? v[u] : 0.f;
+        ty1 += ty[u] == 1 ? v[u] : 0.f;
+      }
+    }
+    for (; b < B; ++b) {
+      const long long t = b * L + p;
+      const float v = bf2f(dsum[t * N + c]);
+      atomicAdd(dword + ids[t] * N + c, v);
+      ps += v;
+      const int ty = tt ? (int)tt[t] : 0;
+      ty0 += ty == 0 ? v : 0.f;
+      ty1 += ty == 1 ? v : 0.f;
+    }
+    dpos[(long long)p * N + c] += ps;
+    if (ty0 != 0.f) atomicAdd(dtype + c, ty0);
+    if (ty1 != 0.f) atomicAdd(dtype + N + c, ty1);
+  }
+}
+
 // ------------------------------------------------------------------------------ row gather / scatter
 __global__ void k_gather_rows(const bf16_t* __restrict__ src, const long long* __restrict__ idx,
                               bf16_t* __restrict__ dst, long long R, int N) {
@@ -607,6 +657,11 @@ KML_API int kml_embed_fwd(const long long* ids, const long long* tt, const bf16_
 KML_API int kml_embed_bwd(const long long* ids, const long long* tt, const bf16_t* dsum, float* dword, float* dpos,
                           float* dtype, long long T, int L, int N, hipStream_t s) {
   if (N % 4 || T % L) return (int)hipErrorInvalidValue;
+  if (dword && dpos && dtype) {   // the training step's case: one pass (k_embed_bwd_fused)
+    hipLaunchKernelGGL(k_embed_bwd_fused, dim3((unsigned)L), dim3(256), 0, s, ids, tt, dsum, dword, dpos, dtype, T,
+                       L, N);
+    KML_LAUNCH_CHECK();
+  }
   if (dword)
     hipLaunchKernelGGL(k_embed_bwd_word, dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, ids, dsum, dword, T, N);
   if (dpos) hipLaunchKernelGGL(k_embed_bwd_pos, dim3(L), dim3(256), 0, s, dsum, dpos, T, L, N);

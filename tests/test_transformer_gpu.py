@@ -111,11 +111,27 @@ def test_embedding_and_rows():
     assert _rel(out, ref) < 1e-2
     d = torch.randn(B * L, N, device=dev).to(torch.bfloat16)
     dw, dp, dt = torch.zeros(V, N, device=dev), torch.zeros(L, N, device=dev), torch.zeros(2, N, device=dev)
-    T.embed_bwd(ids, tt, d, dw, dp, dt, L)
+    T.embed_bwd(ids, tt, d, dw, dp, dt, L)          # all three tables: the fused one-pass kernel
     rw = torch.zeros(V, N, device=dev).index_add_(0, ids, d.float())
     assert _rel(dw, rw) < 1e-5
     assert _rel(dp, d.float().view(B, L, N).sum(0)) < 1e-5
     assert _rel(dt, torch.zeros(2, N, device=dev).index_add_(0, tt, d.float())) < 1e-5
+    # BERT's shape class (B = 5 tokens per position: the 4-token unroll plus a tail; accumulate into
+    # non-zero tables) and the per-table kernels (a table left out)
+    V2, N2, L2, B2 = 30522, 768, 64, 5
+    ids2 = torch.randint(0, V2, (B2 * L2,), device=dev)
+    ids2[:7] = 42                                   # repeated ids: concurrent atomics on one row
+    tt2 = torch.randint(0, 2, (B2 * L2,), device=dev)
+    d2 = torch.randn(B2 * L2, N2, device=dev).to(torch.bfloat16)
+    w0, p0, t0 = torch.randn(V2, N2, device=dev), torch.randn(L2, N2, device=dev), torch.randn(2, N2, device=dev)
+    dw, dp, dt = w0.clone(), p0.clone(), t0.clone()
+    T.embed_bwd(ids2, tt2, d2, dw, dp, dt, L2)
+    assert _rel(dw, w0.clone().index_add_(0, ids2, d2.float())) < 1e-6
+    assert _rel(dp, p0 + d2.float().view(B2, L2, N2).sum(0)) < 1e-6
+    assert _rel(dt, t0.clone().index_add_(0, tt2, d2.float())) < 1e-6
+    dw2 = w0.clone()
+    T.embed_bwd(ids2, None, d2, dw2, None, None, L2)   # word table alone: k_embed_bwd_word
+    assert _rel(dw2, dw) < 1e-6
     idx = torch.randperm(B * L, device=dev)[:10]
     g = T.gather_rows(out, idx)
     assert torch.equal(g, out[idx])
