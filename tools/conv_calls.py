@@ -6,7 +6,7 @@ table of the slowest calls.  Eager timing includes per-call sync overhead (a few
 it to find WHICH call is slow and with which operand shapes, then look the kernel up in a
 rocprofv3 trace of the graphed step.
 
-    python tools/conv_calls.py [--model resnet50] [--batch 128] [--size 224] [--top 30]
+    python tools/conv_calls.py [--model resnet50|vgg16] [--batch 128] [--size 224] [--top 30]
 """
 import argparse
 import json
@@ -26,17 +26,21 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
     from kubeml_amd.models import resnet as R
+    from kubeml_amd.models import vgg as VG
     from kubeml_amd.nn import backward_loss, cross_entropy, flatten_module
     from kubeml_amd.ops import kernels as K
 
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    model = getattr(R, a.model)(1000 if a.size > 64 else 10).to(dev)
+    if a.model.startswith("vgg"):
+        model = getattr(VG, a.model)(100).to(dev)     # VGG-16-BN / CIFAR-100 (config 4)
+    else:
+        model = getattr(R, a.model)(1000 if a.size > 64 else 10).to(dev)
     flatten_module(model)
     model.train()
     x = (torch.randn(a.batch, a.size, a.size, 8, device=dev) * 0.5).to(torch.bfloat16)
     x[..., 3:] = 0
-    y = torch.randint(0, 1000 if a.size > 64 else 10, (a.batch,), device=dev)
+    y = torch.randint(0, 100 if a.model.startswith("vgg") else (1000 if a.size > 64 else 10), (a.batch,), device=dev)
 
     calls = []
     active = [False]
