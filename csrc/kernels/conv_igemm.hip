@@ -1164,19 +1164,19 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU, BNB>::run(cons
   if (nk > 0) {
     const int last = nk - 1;
     issue0(0);
-    issue1(min(1, last));
+    issue1(1);  // past-the-end K-tiles load the zero page (ptr() redirects k >= kend)
     bnb_prologue();
     stash0(0);
     __syncthreads();
     for (int kt = 0;; kt += 2) {
       // even half: LDS[0] holds tile kt, stage 1 holds kt+1 (in flight), stage 0 is free
-      issue0(min(kt + 2, last));
+      issue0(kt + 2);
       compute(0);
       stash1(1);
       __syncthreads();
       if (kt + 1 > last) break;
       // odd half: LDS[1] holds kt+1, stage 0 holds kt+2 (in flight), stage 1 is free
-      issue1(min(kt + 3, last));
+      issue1(kt + 3);
       compute(1);
       stash0(0);
       __syncthreads();
@@ -1327,9 +1327,8 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    const int last = nk - 1;
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s) issue(min(s, last), s);
+    for (int s = 0; s < S - 1; ++s) issue(s, s);  // tiles past the end DMA the zero page
     int cur = 0;
     for (int t = 0; t < nk; ++t) {
       // tile t landed for this wave; S-2 younger stages may stay in flight
@@ -1340,7 +1339,7 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
       __builtin_amdgcn_sched_barrier(0);
       int nb = cur + S - 1;
       if (nb >= S) nb -= S;
-      issue(min(t + S - 1, last), nb);
+      issue(t + S - 1, nb);
       const char* sA = smem + cur * STAGE;
       const char* sB = sA + A_BYTES;
 #pragma unroll
@@ -1363,7 +1362,7 @@ __device__ __forceinline__ void GldsBody<MODE, BM, BN, S, TAPU>::run(const ConvA
       cur = (cur + 1 == S) ? 0 : cur + 1;
     }
   }
-  // drain the (clamped, redundant) tail DMAs before LDS is reused by the epilogue
+  // drain the (zero-page) tail DMAs before LDS is reused by the epilogue
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();

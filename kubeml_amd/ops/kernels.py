@@ -471,15 +471,18 @@ def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
     return (r1 - r0) == 1 and (s1 - s0) == 1 and rows
 
 
-# Large maps with K >= 512 take the tuned implicit GEMM instead: the one-shot panels (one
-# block per CU at K = 1024, 32x32 tiles) run ResNet-50's 14x14 / 28x28 1x1 convs at ~95-135
-# TF/s against 290-380 for the tuned tiles; at K = 256 the panels still win (56x56 maps).
-_ONESHOT_MAX_ROWS_LONG_K = 4096
+# Large maps take the tuned implicit GEMM instead: the one-shot panels (one block per CU at
+# K = 1024, 32x32 tiles) run ResNet-50's 14x14 / 28x28 1x1 convs at ~95-135 TF/s against
+# 290-380 for the tuned tiles, and at K = 256 the 128x64 tile now wins too (56x56 256->64:
+# 55.9 vs 79.0 us, 14x14 256->1024: 51.9 vs 71.9 us; profiles/r5/r50_1x1_fwd.md).  The panels
+# keep the small-M layers (1x1 maps, B rows).
+_ONESHOT_MAX_ROWS = 4096
+_ONESHOT_LEGACY = os.environ.get("KUBEML_ONESHOT_LEGACY", "0") == "1"  # A/B: panels for K = 256 at any M
 
 
 def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad, B=0):
     """Default one-shot panel plan for an eligible forward conv, or None."""
-    if Kd >= 512 and B * H * W > _ONESHOT_MAX_ROWS_LONG_K:
+    if B * H * W > _ONESHOT_MAX_ROWS and (Kd >= 512 or not _ONESHOT_LEGACY):
         return None
     for bm, bn in _ONESHOT_TILES.get(Kd, ()):
         if oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn):

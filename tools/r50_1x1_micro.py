@@ -1,0 +1,88 @@
+"""Graph-timed ResNet-50 1x1 forward convs (batch 128, 224^2 shapes) against the bytes they move.
+
+For each 1x1 conv: our conv_fwd with the BN partial-statistics epilogue (as the model runs it),
+without statistics, every tuned tile of the implicit GEMM, hipBLASLt (torch.mm of the same GEMM)
+and a write-only fill of the output (the HBM floor of the store side).
+
+Usage (GPU box):  python tools/r50_1x1_micro.py [--tiles]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from kubeml_amd.ops import kernels as K
+from tools.conv_micro import gtime
+
+SHAPES = [  # B, H, Cin, Cout, stride (every 1x1 forward conv of ResNet-50 at 224^2)
+    (128, 56, 64, 256, 1),
+    (128, 56, 64, 64, 1),
+    (128, 56, 256, 64, 1),
+    (128, 56, 256, 128, 1),
+    (128, 56, 256, 512, 2),
+    (128, 28, 128, 512, 1),
+    (128, 28, 512, 128, 1),
+    (128, 28, 512, 256, 1),
+    (128, 28, 512, 1024, 2),
+    (128, 14, 256, 1024, 1),
+    (128, 14, 1024, 256, 1),
+    (128, 14, 1024, 512, 1),
+    (128, 14, 1024, 2048, 2),
+    (128, 7, 512, 2048, 1),
+    (128, 7, 2048, 512, 1),
+]
+TILES = [(32, 64), (64, 32), (64, 64), (128, 32), (128, 64), (64, 128), (128, 128), (256, 128), (128, 256)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", action="store_true", help="also time every implicit-GEMM tile")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    for (B, H, C, Co, st) in SHAPES:
+        x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
+        OH = (H - 1) // st + 1
+        y = torch.empty(B, OH, OH, Co, dtype=torch.bfloat16, device=dev)
+        M = B * OH * OH
+        S = (st, st)
+        plan = K.conv_fwd_plan(C, M, Co, C, geom=(H, H, 1, 1, S, (0, 0)))
+        G = K.conv_fwd_stats_rows(x.shape, Co, 1, 1, S, (0, 0))
+        rows = torch.empty(G * 2 * Co, device=dev)
+        t_st = gtime(lambda: K.conv_fwd(x, w, 1, 1, S, (0, 0), out=y, stats=rows, stats_part=True))
+        t_ns = gtime(lambda: K.conv_fwd(x, w, 1, 1, S, (0, 0), out=y))
+        A = x[:, ::st, ::st, :].contiguous().view(M, C)
+        Bm = w.view(Co, C).t()
+        C_ = y.view(M, Co)
+        t_mm = gtime(lambda: torch.mm(A, Bm, out=C_))
+        t_fill = gtime(lambda: y.fill_(1.0))
+        byts = (x.numel() + y.numel()) * 2
+        fl = 2 * M * Co * C
+        best = (t_st, plan)
+        print(f"1x1 {H}x{H}/s{st} {C}->{Co} M={M} plan={plan} G={G}: ours+stats {t_st:.1f}us "
+              f"({byts / t_st / 1e6:.2f} TB/s, {fl / t_st / 1e6:.0f} TF/s)  ours {t_ns:.1f}us  "
+              f"hipblaslt {t_mm:.1f}us  fill(out) {t_fill:.1f}us  [bytes {byts / 1e6:.0f} MB]", flush=True)
+        if args.tiles:
+            for (bm, bn) in TILES:
+                for bk, var in [(32, 0), (64, 0), (64, 1)]:
+                    if bk > C or bn > Co or ((bm == 256 or bn == 256) and var != 1):
+                        continue
+                    cfg = (bm, bn, bk, 1, var)
+                    try:
+                        G2 = K.conv_fwd_stats_rows(x.shape, Co, 1, 1, S, (0, 0), cfg=cfg)
+                        r2 = torch.empty(G2 * 2 * Co, device=dev)
+                        t = gtime(lambda: K.conv_fwd(x, w, 1, 1, S, (0, 0), out=y, stats=r2,
+                                                     stats_part=True, cfg=cfg), reps=20)
+                    except Exception as e:  # tile not instantiated for this variant
+                        print(f"   cfg {cfg}: n/a ({str(e)[:60]})", flush=True)
+                        continue
+                    print(f"   cfg {cfg}: {t:.1f}us ({byts / t / 1e6:.2f} TB/s)", flush=True)
+                    if t < best[0]:
+                        best = (t, cfg)
+            print(f"BEST fwd M={M} N={Co} Kd={C}: {best[1]} {best[0]:.1f}us (plan {t_st:.1f}us)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
