@@ -42,6 +42,12 @@ constexpr int GEMM_ADD_C2 = 3;  // act code: C = bf16(bf16(A B) + c2)
 // the epilogue of the dgrad that produced d(activation), c2 = the saved pre-activation; the
 // column sums of C (the FFN1 bias gradient) go to colpart[M / 256][N] (one row per M-tile)
 constexpr int GEMM_GELU_BWD = 4;
+// act code (layout 0, bf16 out): BatchNorm statistics of the output in the epilogue — a 1x1
+// stride-1 convolution run as this GEMM (ops.kernels.conv_fwd's GEMM route) writes one partial
+// row [sum(N) | sumsq(N)] per M-tile to colpart[M / BM][2 N], the layout of the implicit-GEMM
+// conv's stats_part rows that the BN apply kernel folds.  Sums are over the bf16-rounded outputs
+// (the values BN normalises) in a fixed order, so the rows are deterministic.
+constexpr int GEMM_STATS = 5;
 
 struct GemmArgs {
   const bf16_t* a;
@@ -56,7 +62,7 @@ struct GemmArgs {
   int act;             // 0 none, 1 erf-GELU
   float beta;
   int kchunk;          // split-K slice length (multiple of 64)
-  float* colpart;      // GEMM_GELU_BWD: per-M-tile column sums of the output
+  float* colpart;      // GEMM_GELU_BWD: per-M-tile column sums of the output; GEMM_STATS: [M/BM][2N]
 };
 
 constexpr int BK = 64;
@@ -219,6 +225,68 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[
   }
 }
 
+// GEMM_STATS rows of a k_gemm tile (bf16 out): per-lane sums of the bf16-rounded outputs over the
+// lane's rows, a butterfly over the 16 lanes of a column group, then the two wave rows summed
+// through LDS (wave row 0 + wave row 1, fixed order).  Entered by every thread of the block.
+template <int BM, int BN, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_stats_rows(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                                int wn, int lane, char* smem) {
+  float s1[NR][4], s2[NR][4];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+    const float4 bb = (g.bias && n < g.N) ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m < g.M) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = lo_bf(pack_bf2(acc[i][j][r] + bv[r], 0.f));
+          s1[j][r] += x;
+          s2[j][r] += x * x;
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s1[j][r] += __shfl_xor(s1[j][r], off, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], off, 64);
+      }
+  }
+  __syncthreads();  // every wave is done with the operand stages
+  float* red = reinterpret_cast<float*>(smem);  // [sum | sumsq][BN] of wave row 1
+  if (wm == 1 && (lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WN + j * 16 + 4 * (lane >> 4) + r;
+        red[col] = s1[j][r];
+        red[BN + col] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  if (wm == 0 && (lane & 15) == 0) {
+    float* row = g.colpart + (long long)(m0 / BM) * 2 * g.N;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WN + j * 16 + 4 * (lane >> 4) + r, n = n0 + col;
+        if (n < g.N) {
+          row[n] = s1[j][r] + red[col];
+          row[g.N + n] = s2[j][r] + red[BN + col];
+        }
+      }
+  }
+}
+
 // OUT: 0 bf16 (bias, act, optional pre-act copy), 1 fp32 beta, 2 fp32 atomic add (split-K)
 // S: LDS stages.  S = 2: the DMA of tile t+1 overlaps tile t's MFMAs, vmcnt(0) per step.
 // S = 3: tiles t+1 and t+2 in flight; each step waits with a COUNTED vmcnt for tile t only,
@@ -311,6 +379,9 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   }
 
   gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tz);
+  if constexpr (OUT == 0) {
+    if (g.act == GEMM_STATS) gemm_stats_rows<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -681,8 +752,9 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
       __syncthreads();
     };
     // LDS tile -> 16-byte row-contiguous global stores (512 B per half-wave)
-    const bool gbwd = g.act == GEMM_GELU_BWD;
-    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // GELU_BWD: this thread's 8 columns
+    const bool gbwd = g.act == GEMM_GELU_BWD, gst = BN == 256 && g.act == GEMM_STATS;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // GELU_BWD / STATS: this thread's 8 columns
+    float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // STATS: sums of squares
     auto store = [&](bf16_t* dst) {
 #pragma unroll 2
       for (int it = 0; it < 256 * CPR / NT; ++it) {
@@ -702,6 +774,15 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
               csum[2 * k + 1] += hi_bf(ow[k]);
             }
             v = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          }
+          if (gst) {  // BN statistics of the bf16 output (BN = 256: a thread's 8 columns are fixed)
+            const unsigned ow[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float x0 = lo_bf(ow[k]), x1 = hi_bf(ow[k]);
+              csum[2 * k] += x0; csq[2 * k] += x0 * x0;
+              csum[2 * k + 1] += x1; csq[2 * k + 1] += x1 * x1;
+            }
           }
           if (g.act == GEMM_ADD_C2) {  // + bf16 addend (the staged tile is already bf16-rounded)
             const uint4 ad = *reinterpret_cast<const uint4*>(g.c2 + (long long)m * g.ldc + n);
@@ -732,6 +813,26 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) sum += red[((r << 5) + ch) * 8 + k];
         if (n < g.N) g.colpart[(long long)(m0 / 256) * g.N + n] = sum;
+      }
+    }
+    if (gst) {  // [sum | sumsq] row of this M-tile: 16 threads share each 8-column chunk, fixed order
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = csum[k]; red[tid * 16 + 8 + k] = csq[k]; }
+      __syncthreads();
+      if (tid < 256) {
+        const int ch = tid >> 3, k = tid & 7, n = n0 + tid;
+        float sum = 0.f, sq = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sum += red[((r << 5) + ch) * 16 + k];
+          sq += red[((r << 5) + ch) * 16 + 8 + k];
+        }
+        if (n < g.N) {
+          float* row = g.colpart + (long long)(m0 / 256) * 2 * g.N;
+          row[n] = sum;
+          row[g.N + n] = sq;
+        }
       }
     }
   }
@@ -840,6 +941,22 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   if (layout == 2 && out == 1) return by_tile<false, false, 1>(g, tile, 1, s);
   if (layout == 2 && out == 2) return by_tile<false, false, 2>(g, tile, splits, s);
   return (int)hipErrorInvalidValue;
+}
+
+// Forward GEMM (layout 0, bf16 out, optional fp32 bias) with BatchNorm partial statistics in the
+// epilogue (GEMM_STATS): rows[M / BM][2 N] = per-M-tile [sum | sumsq] of the bf16 outputs, BM = 256
+// (tiles 0, 1, 6) or 128 (tiles 2, 3, 4).  The GEMM route of a 1x1 / stride-1 convolution.
+KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, bf16_t* c, long long ldc,
+                           const float* bias, float* rows, const bf16_t* zp, int M, int N, int K, int tile,
+                           hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!rows || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || K % 8) return (int)hipErrorInvalidValue;
+  if (tile == 5 || tile == 7 || tile < 0 || tile > 7) return (int)hipErrorInvalidValue;
+  GemmArgs g;
+  g.a = a; g.b = b; g.c = c; g.c2 = nullptr; g.bias = bias; g.zp = zp;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.act = GEMM_STATS; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
+  return by_tile<true, true, 0>(g, tile, 1, s);
 }
 
 // dgrad (layout 1, 256x256 phase tile) with the GELU backward of the layer that produced its

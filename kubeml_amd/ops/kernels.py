@@ -372,6 +372,22 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, 0, 1, ONESHOT, 0, 0, _p(grp), _p(gcnt), tpg,
                  int(_fold), int(_g22), _s())
         return out
+    if variant == GEMM1X1:
+        if relu or _fold or _g22 or grp is not None or (stats is not None and not stats_part) or \
+                not x.is_contiguous() or not out.is_contiguous():
+            # same bm, so the statistics rows the caller sized stay valid
+            return conv_fwd(x, w, KH, KW, stride, pad, bias=bias, stats=stats, relu=relu, out=out,
+                            cfg=_GEMM1X1_FALLBACK[bm], stats_part=stats_part, _fold=_fold, _g22=_g22,
+                            stats_group=stats_group)
+        from . import gemm as G
+        zp = G._zp(x.device)
+        if stats is None:
+            HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", _p(x), C, _p(w), C, _p(out), K, 0,
+                     _p(bias), _p(zp), M, K, C, 0, 0, 0, 0.0, bk, 1, _s())
+        else:
+            HIP.call("kml_gemm_stats", "p l p l p l p p p i i i i s", _p(x), C, _p(w), C, _p(out), K, _p(bias),
+                     _p(rows), _p(zp), M, K, C, bk, _s())
+        return out
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                  KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, int(_fold),
@@ -403,6 +419,9 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
     if plan[4] == STEM and (geom is None or stem_plan(C, K, *geom, force=True) is None):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == DIRECT and C % 32:
+        plan = _norm_cfg(default_plan("fwd", M, K, Kd))
+    if plan[4] == GEMM1X1 and (geom is None or not gemm1x1_ok(C, K, *geom) or
+                               (plan[0], plan[1], plan[2]) not in _GEMM1X1_TILES):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     return plan
 
@@ -459,6 +478,19 @@ def stem_plan(C, K, H, W, KH, KW, stride, pad, force=False):
 
 ONESHOT = 5  # cfg variant id of the one-shot panel forward (single-tap convs, K in _ONESHOT_TILES)
 _ONESHOT_TILES = {512: [(32, 32), (32, 64), (64, 32)], 1024: [(32, 32)], 256: [(32, 32), (32, 64), (64, 64)]}
+
+
+GEMM1X1 = 7  # cfg variant id of the GEMM route: a 1x1 / stride-1 conv on the MFMA GEMM (gemm.hip)
+# (bm, bn) -> gemm.hip tile code of the GEMM route (cfg = (bm, bn, tile, 1, GEMM1X1)); BN statistics
+# come out of the GEMM's epilogue as one [sum | sumsq] row per bm rows (kml_gemm_stats)
+_GEMM1X1_TILES = {(256, 256, 6), (256, 256, 0), (256, 128, 1), (128, 256, 2), (128, 128, 3), (128, 128, 4)}
+# same-G implicit-GEMM stand-ins when a call cannot take the GEMM route (ReLU epilogue, grouped rows)
+_GEMM1X1_FALLBACK = {128: (128, 64, 32, 1, 0), 256: (256, 128, 64, 1, 1)}
+
+
+def gemm1x1_ok(C, K, H, W, KH, KW, stride, pad) -> bool:
+    """Can this forward conv run as a plain GEMM x[M, C] @ w[K, C]^T (1x1, stride 1, no padding)?"""
+    return (KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and C % 8 == 0 and K % 8 == 0
 
 
 def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:

@@ -111,6 +111,35 @@ def test_conv_fwd_bias_relu():
     assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [(256, 256, 6, 1, 7), (256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7),
+                                 (128, 128, 3, 1, 7), (128, 128, 4, 1, 7)])
+@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 512, 136)])
+def test_conv1x1_gemm_route_output_and_stats_rows(cfg, shape):
+    """1x1 / stride-1 conv on the MFMA GEMM (kml_gemm_stats): output vs fp32 torch, the per-M-tile
+    [sum | sumsq] rows vs the sums of the bf16 output, ragged M (M % BM != 0), with and without bias;
+    a ReLU call takes the same-G implicit-GEMM fallback."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co = shape
+    torch.manual_seed(5)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, 1, 1, Ci, device=dev) * Ci ** -0.5)
+    for bias in (None, torch.randn(Co, device=dev)):
+        yr = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias)
+        G = K.conv_fwd_stats_rows(x.shape, Co, 1, 1, (1, 1), (0, 0), cfg=cfg)
+        assert G == -(-(B * H * H) // cfg[0])
+        rows = torch.full((G * 2 * Co,), float("nan"), device=dev)
+        y = K.conv_fwd(x, w, 1, 1, (1, 1), (0, 0), bias=bias, stats=rows, stats_part=True, cfg=cfg)
+        assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+        yf = y.float().reshape(-1, Co)
+        r = rows.view(G, 2, Co).sum(0)
+        assert torch.allclose(r[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+        assert torch.allclose(r[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+        y2 = K.conv_fwd(x, w, 1, 1, (1, 1), (0, 0), bias=bias, cfg=cfg)   # no statistics: kml_gemm
+        assert torch.equal(y2, y)
+    y3 = K.conv_fwd(x, w, 1, 1, (1, 1), (0, 0), relu=True, cfg=cfg)
+    assert _rel(y3.permute(0, 3, 1, 2), F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)))) < 1e-2
+
+
 @pytest.mark.parametrize("C,M,relu,res", [(64, 4096, True, False), (128, 1000, True, True), (512, 64, False, True),
                                           (2048, 96, True, False), (64, 300000, True, True), (8, 50, False, False),
                                           (1024, 1031, True, False)])

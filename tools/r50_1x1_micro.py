@@ -39,6 +39,8 @@ TILES = [(32, 64), (64, 32), (64, 64), (128, 32), (128, 64), (64, 128), (128, 12
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", action="store_true", help="also time every implicit-GEMM tile")
+    ap.add_argument("--gemm", action="store_true", help="also time the plain MFMA GEMM (ops.gemm) tiles, no stats")
+    ap.add_argument("--route", action="store_true", help="time the conv GEMM route (BN stats epilogue) per tile")
     args = ap.parse_args()
     dev = torch.device("cuda")
     for (B, H, C, Co, st) in SHAPES:
@@ -64,6 +66,31 @@ def main():
         print(f"1x1 {H}x{H}/s{st} {C}->{Co} M={M} plan={plan} G={G}: ours+stats {t_st:.1f}us "
               f"({byts / t_st / 1e6:.2f} TB/s, {fl / t_st / 1e6:.0f} TF/s)  ours {t_ns:.1f}us  "
               f"hipblaslt {t_mm:.1f}us  fill(out) {t_fill:.1f}us  [bytes {byts / 1e6:.0f} MB]", flush=True)
+        if args.gemm and st == 1:
+            from kubeml_amd.ops import gemm as G
+            for tile in G.TILES:
+                if tile[0] > M or tile[1] > Co:
+                    continue
+                try:
+                    t = gtime(lambda: G.gemm(A, C, w.view(Co, C), C, C_, Co, M, Co, C, 0, 0, tile=tile, splits=1),
+                              reps=20)
+                except Exception as e:
+                    print(f"   gemm {tile}: n/a ({str(e)[:60]})", flush=True)
+                    continue
+                print(f"   gemm {tile}: {t:.1f}us ({byts / t / 1e6:.2f} TB/s, {fl / t / 1e6:.0f} TF/s)", flush=True)
+        if args.route and st == 1:
+            rbest = None
+            for (bm, bn, tc) in sorted(K._GEMM1X1_TILES):
+                cfg = (bm, bn, tc, 1, K.GEMM1X1)
+                G2 = K.conv_fwd_stats_rows(x.shape, Co, 1, 1, S, (0, 0), cfg=cfg)
+                r2 = torch.empty(G2 * 2 * Co, device=dev)
+                t = gtime(lambda: K.conv_fwd(x, w, 1, 1, S, (0, 0), out=y, stats=r2, stats_part=True, cfg=cfg),
+                          reps=20)
+                print(f"   route {cfg}: {t:.1f}us ({byts / t / 1e6:.2f} TB/s, {fl / t / 1e6:.0f} TF/s)", flush=True)
+                if rbest is None or t < rbest[0]:
+                    rbest = (t, cfg)
+            print(f"ROUTE fwd M={M} N={Co} Kd={C}: {rbest[1]} {rbest[0]:.1f}us (plan {plan} {t_st:.1f}us)",
+                  flush=True)
         if args.tiles:
             for (bm, bn) in TILES:
                 for bk, var in [(32, 0), (64, 0), (64, 1)]:
