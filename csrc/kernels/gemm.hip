@@ -48,6 +48,12 @@ constexpr int GEMM_GELU_BWD = 4;
 // conv's stats_part rows that the BN apply kernel folds.  Sums are over the bf16-rounded outputs
 // (the values BN normalises) in a fixed order, so the rows are deterministic.
 constexpr int GEMM_STATS = 5;
+// act code (layout 1, bf16 out, tiles 0-4): the epilogue of a 1x1 stride-1 conv's input gradient
+// (ops.kernels.conv_dgrad's GEMM route), as the implicit-GEMM dgrad's: v = A B (+ the bf16 addend
+// c2, the residual branch's gradient) rounded once; with bc (the consumer BN's input) the masked
+// dz = v * [by > 0] (by optional) gives colpart[M / BM][2 N] = per-M-tile [sum dz | sum dz * xhat],
+// xhat = (bc - bmean[n]) * brstd[n]; mask_out stores dz instead of v.
+constexpr int GEMM_BNF = 6;
 
 struct GemmArgs {
   const bf16_t* a;
@@ -62,7 +68,12 @@ struct GemmArgs {
   int act;             // 0 none, 1 erf-GELU
   float beta;
   int kchunk;          // split-K slice length (multiple of 64)
-  float* colpart;      // GEMM_GELU_BWD: per-M-tile column sums of the output; GEMM_STATS: [M/BM][2N]
+  float* colpart;      // GEMM_GELU_BWD: per-M-tile column sums of the output; GEMM_STATS / BNF: [M/BM][2N]
+  const bf16_t* by;    // GEMM_BNF: consumer BN's ReLU output (mask) or null
+  const bf16_t* bc;    // GEMM_BNF: consumer BN's input or null (no partial rows)
+  const float* bmean;  // GEMM_BNF: [N]
+  const float* brstd;  // GEMM_BNF: [N]
+  int mask_out;        // GEMM_BNF: store dz = v * [by > 0]
 };
 
 constexpr int BK = 64;
@@ -287,6 +298,101 @@ __device__ __forceinline__ void gemm_stats_rows(const GemmArgs& g, f32x4_t (&acc
   }
 }
 
+// GEMM_BNF epilogue of a k_gemm tile (layout 1, bf16 out): lane holds C[m][n .. n+3]; the addend,
+// mask and BN input are read as 8-byte chunks beside the 8-byte output store; the per-lane partial
+// sums are reduced as in gemm_stats_rows (16-lane butterfly, wave rows 0 + 1 through LDS).
+template <int BM, int BN, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                                  int wn, int lane, char* smem) {
+  const bool bnf = g.bc != nullptr;
+  float s1[NR][4], s2[NR][4];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+    const bool nok = n < g.N;
+    float mu[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bnf && nok) {
+      const float4 a4 = *reinterpret_cast<const float4*>(g.bmean + n);
+      const float4 b4 = *reinterpret_cast<const float4*>(g.brstd + n);
+      mu[0] = a4.x; mu[1] = a4.y; mu[2] = a4.z; mu[3] = a4.w;
+      rs[0] = b4.x; rs[1] = b4.y; rs[2] = b4.z; rs[3] = b4.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m >= g.M || !nok) continue;
+      const long long off = (long long)m * g.ldc + n;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.c2) {
+        const uint2 ad = *reinterpret_cast<const uint2*>(g.c2 + off);
+        v[0] += lo_bf(ad.x); v[1] += hi_bf(ad.x); v[2] += lo_bf(ad.y); v[3] += hi_bf(ad.y);
+      }
+      unsigned w0 = pack_bf2(v[0], v[1]), w1 = pack_bf2(v[2], v[3]);
+      if (bnf) {
+        const uint2 cv = *reinterpret_cast<const uint2*>(g.bc + off);
+        float dz[4] = {lo_bf(w0), hi_bf(w0), lo_bf(w1), hi_bf(w1)};
+        if (g.by) {
+          const uint2 yv = *reinterpret_cast<const uint2*>(g.by + off);
+          const bool k0 = lo_bf(yv.x) > 0.f, k1 = hi_bf(yv.x) > 0.f, k2 = lo_bf(yv.y) > 0.f, k3 = hi_bf(yv.y) > 0.f;
+          if (!k0) dz[0] = 0.f;
+          if (!k1) dz[1] = 0.f;
+          if (!k2) dz[2] = 0.f;
+          if (!k3) dz[3] = 0.f;
+          if (g.mask_out) {
+            w0 &= (k0 ? 0x0000ffffu : 0u) | (k1 ? 0xffff0000u : 0u);
+            w1 &= (k2 ? 0x0000ffffu : 0u) | (k3 ? 0xffff0000u : 0u);
+          }
+        }
+        const float c[4] = {lo_bf(cv.x), hi_bf(cv.x), lo_bf(cv.y), hi_bf(cv.y)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[j][r] += dz[r];
+          s2[j][r] += dz[r] * ((c[r] - mu[r]) * rs[r]);
+        }
+      }
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.c) + off) = make_uint2(w0, w1);
+    }
+    if (bnf) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s1[j][r] += __shfl_xor(s1[j][r], off, 64);
+          s2[j][r] += __shfl_xor(s2[j][r], off, 64);
+        }
+    }
+  }
+  if (!bnf) return;
+  __syncthreads();  // every wave is done with the operand stages
+  float* red = reinterpret_cast<float*>(smem);
+  if (wm == 1 && (lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WN + j * 16 + 4 * (lane >> 4) + r;
+        red[col] = s1[j][r];
+        red[BN + col] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  if (wm == 0 && (lane & 15) == 0) {
+    float* row = g.colpart + (long long)(m0 / BM) * 2 * g.N;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WN + j * 16 + 4 * (lane >> 4) + r, n = n0 + col;
+        if (n < g.N) {
+          row[n] = s1[j][r] + red[col];
+          row[g.N + n] = s2[j][r] + red[BN + col];
+        }
+      }
+  }
+}
+
 // OUT: 0 bf16 (bias, act, optional pre-act copy), 1 fp32 beta, 2 fp32 atomic add (split-K)
 // S: LDS stages.  S = 2: the DMA of tile t+1 overlaps tile t's MFMAs, vmcnt(0) per step.
 // S = 3: tiles t+1 and t+2 in flight; each step waits with a COUNTED vmcnt for tile t only,
@@ -378,6 +484,12 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
     }
   }
 
+  if constexpr (OUT == 0) {
+    if (g.act == GEMM_BNF) {
+      gemm_bnf_epilogue<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
+      return;
+    }
+  }
   gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tz);
   if constexpr (OUT == 0) {
     if (g.act == GEMM_STATS) gemm_stats_rows<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
@@ -931,6 +1043,7 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K; g.colpart = nullptr;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   if (M <= 0 || N <= 0) return 0;
   if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
@@ -956,7 +1069,26 @@ KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long
   g.a = a; g.b = b; g.c = c; g.c2 = nullptr; g.bias = bias; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_STATS; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   return by_tile<true, true, 0>(g, tile, 1, s);
+}
+
+// Input gradient of a 1x1 / stride-1 conv as a GEMM (layout 1: dx[M][N] = dy[M][K] W[K][N]) with the
+// implicit-GEMM dgrad's epilogue (GEMM_BNF): optional residual addend, consumer-BN partial rows
+// rows[M / BM][2 N] and ReLU-masked output.  Tiles 0-4 (register epilogue; BM = 256 for 0 / 1).
+KML_API int kml_gemm_dgrad_bnf(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, bf16_t* c,
+                               long long ldc, const bf16_t* addend, const bf16_t* y, const bf16_t* cin,
+                               const float* mean, const float* rstd, float* rows, int mask_out, const bf16_t* zp,
+                               int M, int N, int K, int tile, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (N % 8 || ldc % 8 || lda % 8 || ldb % 8 || K % 8 || tile < 0 || tile > 4) return (int)hipErrorInvalidValue;
+  if (cin && (!mean || !rstd || !rows)) return (int)hipErrorInvalidValue;
+  GemmArgs g;
+  g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(addend); g.bias = nullptr; g.zp = zp;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out;
+  return by_tile<true, false, 0>(g, tile, 1, s);
 }
 
 // dgrad (layout 1, 256x256 phase tile) with the GELU backward of the layer that produced its
@@ -971,6 +1103,7 @@ KML_API int kml_gemm_dgrad_gelu(const bf16_t* a, long long lda, const bf16_t* b,
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(pre); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_GELU_BWD; g.beta = 0.f; g.kchunk = K; g.colpart = colpart;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   return launch8<true, false, 0>(g, 1, s);
 }
 
@@ -986,6 +1119,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K; g.colpart = nullptr;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   splits = splits < 1 ? 1 : splits;
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;

@@ -746,7 +746,19 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     bm, bn, bk, splits, variant = _norm_cfg(cfg or hp or plan_conv("dgrad", M, C, ntap * K))
     if variant == HALO and (_g22 or not halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn)):
         bm, bn, bk, splits, variant = _norm_cfg(plan_conv("dgrad", M, C, ntap * K))
+    if variant == GEMM1X1 and ((bm, bn, bk) not in _GEMM1X1_TILES or bk > 4 or _fold or _g22 or wt is not None or
+                               not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad) or not dy.is_contiguous() or
+                               not out.is_contiguous()):
+        bm, bn, bk, splits, variant = _GEMM1X1_FALLBACK[bm] if bm in _GEMM1X1_FALLBACK else \
+            _norm_cfg(default_plan("dgrad", M, C, ntap * K))
     plan = (bm, bn, bk, splits, variant)
+    if variant == GEMM1X1:  # dx[M, C] = dy[M, K] @ w[K, C] on the MFMA GEMM, the dgrad epilogue fused
+        by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan)
+        from . import gemm as GM
+        HIP.call("kml_gemm_dgrad_bnf", "p l p l p l p p p p p p i p i i i i s", _p(dy), K, _p(w), C, _p(out), C,
+                 _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
+                 int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), M, C, K, bk, _s())
+        return (out, (part, G)) if bnf is not None else out
     if s2_parity_ok(B, H, W, stride, plan, _g22, _fold, operands=addend is not None or bnf is not None):
         part, G = None, 0
         by = bc = bmean = brstd = None

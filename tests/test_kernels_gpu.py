@@ -140,6 +140,41 @@ def test_conv1x1_gemm_route_output_and_stats_rows(cfg, shape):
     assert _rel(y3.permute(0, 3, 1, 2), F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)))) < 1e-2
 
 
+@pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
+                                 (128, 128, 4, 1, 7)])
+@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 136, 512)])
+def test_conv1x1_dgrad_gemm_route_matches_implicit_gemm(cfg, shape):
+    """1x1 / stride-1 dgrad on the MFMA GEMM (kml_gemm_dgrad_bnf) against the implicit-GEMM dgrad:
+    dx (+ residual addend) vs fp32 torch, the consumer-BN partial rows and the ReLU-masked output."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co = shape
+    torch.manual_seed(6)
+    dy = _bf(torch.randn(B, H, H, Co, device=dev))
+    w = _bf(torch.randn(Co, 1, 1, Ci, device=dev) * Co ** -0.5)
+    xs = (B, H, H, Ci)
+    y = _bf(torch.randn(xs, device=dev))
+    c = _bf(torch.randn(xs, device=dev) * 2 + 0.3)
+    mean, rstd = torch.randn(Ci, device=dev) * 0.1, torch.rand(Ci, device=dev) + 0.5
+    add = _bf(torch.randn(xs, device=dev))
+    ref = torch.einsum("bhwk,kc->bhwc", dy.float(), w.float().view(Co, Ci))
+    for addend in (None, add):
+        exp = ref + (addend.float() if addend is not None else 0)
+        dx = K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), addend=addend, cfg=cfg)
+        assert _rel(dx, exp) < 1e-2
+        for mask in (False, True):
+            dz, (part, G) = K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), addend=addend, cfg=cfg,
+                                         bnf=(y, c, mean, rstd), bnf_mask=mask)
+            assert G == -(-(B * H * H) // cfg[0])
+            keep = (y.float() > 0)
+            vb = dx.float()
+            assert torch.equal(dz, (dx * keep) if mask else dx)
+            dzf = (vb * keep).reshape(-1, Ci)
+            xh = ((c.float() - mean) * rstd).reshape(-1, Ci)
+            r = part.view(G, 2, Ci).sum(0)
+            assert torch.allclose(r[0], dzf.sum(0), rtol=1e-4, atol=1e-3)
+            assert torch.allclose(r[1], (dzf * xh).sum(0), rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("C,M,relu,res", [(64, 4096, True, False), (128, 1000, True, True), (512, 64, False, True),
                                           (2048, 96, True, False), (64, 300000, True, True), (8, 50, False, False),
                                           (1024, 1031, True, False)])

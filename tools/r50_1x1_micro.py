@@ -41,8 +41,12 @@ def main():
     ap.add_argument("--tiles", action="store_true", help="also time every implicit-GEMM tile")
     ap.add_argument("--gemm", action="store_true", help="also time the plain MFMA GEMM (ops.gemm) tiles, no stats")
     ap.add_argument("--route", action="store_true", help="time the conv GEMM route (BN stats epilogue) per tile")
+    ap.add_argument("--dgrad", action="store_true", help="time the 1x1 dgrads (consumer-BN epilogue, residual addend "
+                                                          "where the model has one) against the plain GEMM")
     args = ap.parse_args()
     dev = torch.device("cuda")
+    if args.dgrad:
+        return dgrad_main(dev)
     for (B, H, C, Co, st) in SHAPES:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
@@ -109,6 +113,44 @@ def main():
                     if t < best[0]:
                         best = (t, cfg)
             print(f"BEST fwd M={M} N={Co} Kd={C}: {best[1]} {best[0]:.1f}us (plan {t_st:.1f}us)", flush=True)
+
+
+def dgrad_main(dev):
+    from kubeml_amd.ops import gemm as G
+    for (B, H, C, Co, st) in SHAPES:
+        if st != 1:
+            continue
+        for addend in (False, True):
+            dy = torch.randn(B, H, H, Co, device=dev).to(torch.bfloat16)
+            w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
+            xs = (B, H, H, C)
+            yb = torch.randn(xs, device=dev).to(torch.bfloat16)
+            cb = torch.randn(xs, device=dev).to(torch.bfloat16)
+            mean = torch.zeros(C, device=dev)
+            rstd = torch.ones(C, device=dev)
+            add = torch.randn(xs, device=dev).to(torch.bfloat16) if addend else None
+            out = torch.empty(xs, dtype=torch.bfloat16, device=dev)
+            M = B * H * H
+            plan = K.plan_conv("dgrad", M, C, Co)
+            t = gtime(lambda: K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), out=out, addend=add,
+                                           bnf=(yb, cb, mean, rstd), bnf_mask=True), reps=20)
+            byts = (dy.numel() + 3 * out.numel() + (out.numel() if addend else 0)) * 2
+            fl = 2 * M * Co * C
+            line = (f"dgrad 1x1 {H}x{H} {Co}->{C} M={M} addend={addend} plan={plan}: {t:.1f}us "
+                    f"({byts / t / 1e6:.2f} TB/s, {fl / t / 1e6:.0f} TF/s)")
+            best = None
+            for (bm, bn, tc) in sorted(K._GEMM1X1_TILES):
+                if tc > 4:
+                    continue
+                cfg = (bm, bn, tc, 1, K.GEMM1X1)
+                tg = gtime(lambda: K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), out=out, addend=add, cfg=cfg,
+                                                bnf=(yb, cb, mean, rstd), bnf_mask=True), reps=20)
+                line += f"  route{cfg[:3]}: {tg:.1f}"
+                if best is None or tg < best[0]:
+                    best = (tg, cfg)
+            print(line, flush=True)
+            print(f"DROUTE dgrad M={M} N={C} Kd={Co} addend={addend}: {best[1]} {best[0]:.1f}us (plan {plan} {t:.1f}us)",
+                  flush=True)
 
 
 if __name__ == "__main__":
