@@ -63,45 +63,48 @@ __global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__
 // relu_out (optional): the pooled forward output of a fused BN -> ReLU -> max-pool; a window
 // whose maximum is not > 0 passes no gradient (its argmax sat at ReLU's zero), so dx is
 // already dz = d(BN output) and the BN backward needs no ReLU mask.
-__global__ void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char* __restrict__ idx,
-                              const bf16_t* __restrict__ relu_out, bf16_t* __restrict__ dx, PoolGeom g) {
+// One grid row per input image row (b, ih): the output-row window [oh_lo, oh_hi] is computed once
+// per row and every index is 32-bit (the flat 64-bit div / mod chain per element cost more than the
+// memory traffic on ResNet-50's 112x112 stem pool: 164 us for 256 MB).
+__global__ __launch_bounds__(256) void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char* __restrict__ idx,
+                                                     const bf16_t* __restrict__ relu_out, bf16_t* __restrict__ dx,
+                                                     PoolGeom g) {
   const int CH = g.C / 8;
-  const long long total = (long long)g.B * g.H * g.W * CH;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
-       t += (long long)gridDim.x * blockDim.x) {
-    const int ch = (int)(t % CH);
-    long long pix = t / CH;
-    const int iw = (int)(pix % g.W); pix /= g.W;
-    const int ih = (int)(pix % g.H); const int b = (int)(pix / g.H);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int per_row = g.W * CH;
+  for (int row = blockIdx.y; row < g.B * g.H; row += gridDim.y) {
+    const int b = row / g.H, ih = row - b * g.H;
     // outputs whose window contains ih: oh*s - p <= ih <= oh*s - p + k - 1
     const int oh_lo = max(0, (ih + g.p - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (ih + g.p) / g.s);
-    const int ow_lo = max(0, (iw + g.p - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (iw + g.p) / g.s);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int r = ih - (oh * g.s - g.p);
-      if (r < 0 || r >= g.k) continue;
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int q = iw - (ow * g.s - g.p);
-        if (q < 0 || q >= g.k) continue;
-        const long long o = ((long long)(b * g.OH + oh) * g.OW + ow) * CH + ch;
-        const uint2 pk = reinterpret_cast<const uint2*>(idx)[o];
-        float d[8];
-        unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
-        if (relu_out) {
-          float m[8];
-          unpack8(reinterpret_cast<const uint4*>(relu_out)[o], m);
+    for (int u = blockIdx.x * 256 + threadIdx.x; u < per_row; u += gridDim.x * 256) {
+      const int iw = u / CH, ch = u - iw * CH;
+      const int ow_lo = max(0, (iw + g.p - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (iw + g.p) / g.s);
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        const int r = ih - (oh * g.s - g.p);
+        if (r < 0 || r >= g.k) continue;
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const int q = iw - (ow * g.s - g.p);
+          if (q < 0 || q >= g.k) continue;
+          const long long o = ((long long)(b * g.OH + oh) * g.OW + ow) * CH + ch;
+          const uint2 pk = reinterpret_cast<const uint2*>(idx)[o];
+          float d[8];
+          unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+          if (relu_out) {
+            float m[8];
+            unpack8(reinterpret_cast<const uint4*>(relu_out)[o], m);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) d[i] = m[i] > 0.f ? d[i] : 0.f;
-        }
-        const int tap = r * g.k + q;
+            for (int i = 0; i < 8; ++i) d[i] = m[i] > 0.f ? d[i] : 0.f;
+          }
+          const int tap = r * g.k + q;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const unsigned w = i < 4 ? pk.x : pk.y;
-          if ((int)((w >> (8 * (i & 3))) & 0xff) == tap) acc[i] += d[i];
+          for (int i = 0; i < 8; ++i) {
+            const unsigned w = i < 4 ? pk.x : pk.y;
+            if ((int)((w >> (8 * (i & 3))) & 0xff) == tap) acc[i] += d[i];
+          }
         }
       }
+      reinterpret_cast<uint4*>(dx)[(long long)row * per_row + u] = pack8(acc);
     }
-    reinterpret_cast<uint4*>(dx)[t] = pack8(acc);
   }
 }
 
@@ -189,9 +192,9 @@ KML_API int kml_maxpool_bwd(const bf16_t* dy, const unsigned char* idx, const bf
                             int H, int W, int C, int k, int s, int p, hipStream_t st) {
   if (C % 8) return (int)hipErrorInvalidValue;
   PoolGeom g{B, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
-  long long total = (long long)B * H * W * (C / 8);
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(kml_stream_grid(total, 256)), dim3(256), 0, st, dy, idx, relu_out, dx,
-                     g);
+  const int per_row = W * (C / 8), rows = B * H;
+  const dim3 grid((per_row + 255) / 256, rows < 65535 ? rows : 65535);
+  hipLaunchKernelGGL(k_maxpool_bwd, grid, dim3(256), 0, st, dy, idx, relu_out, dx, g);
   KML_LAUNCH_CHECK();
 }
 
