@@ -492,7 +492,8 @@ class BlockFn(Function):
             is_last = role == "last"
             is_first = k == 0
             addend = None
-            if is_first:
+            swap = is_first and short and not is_last and _short_last(saved[short[0][0]], short[0][1][0])
+            if is_first and not swap:
                 # shortcut gradient joins here: identity -> dres, projection -> its dgrad
                 if short:
                     j, (sc, sb, sr, _) = short[0]
@@ -502,6 +503,17 @@ class BlockFn(Function):
             consumer = saved[main[k - 1][0]] if k > 0 else (prev_saved if need_x else None)
             if not _BN_FUSE:
                 consumer = None
+            if swap:
+                # strided projection shortcut on a large map: the main conv's dgrad runs plain and the
+                # shortcut's dgrad takes it as its residual addend plus the consumer-BN epilogue —
+                # with operands, the stride-2 dgrad runs by parity class (3/4 of its output rows are
+                # epilogue only) instead of multiplying the zero taps of the whole input map
+                j, (sc, sb, _, _) = short[0]
+                dx1, _, _ = ConvBNUnit.backward(g, saved[i], conv, bn, want_dres=False, need_dx=need_x,
+                                                partial=partial)
+                g, _, partial = ConvBNUnit.backward(dres, saved[j], sc, sb, False, need_x, addend=dx1,
+                                                    consumer=consumer)
+                continue
             dx, dz, part_out = ConvBNUnit.backward(g, saved[i], conv, bn, want_dres=is_last,
                                                    need_dx=(not is_first) or need_x,
                                                    addend=addend if is_first else None, partial=partial,
@@ -515,6 +527,22 @@ class BlockFn(Function):
         ctx.saved = None
         object.__setattr__(block, "_kml_last_saved", None)
         return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+
+
+_SHORT_LAST = os.environ.get("KUBEML_SHORT_LAST", "1") != "0"
+
+
+def _short_last(short_saved, sc) -> bool:
+    """Run a block's projection-shortcut dgrad after the main branch's (see the block backward):
+    a stride-2 shortcut whose input map is large enough for the parity-class dgrad."""
+    from ..ops import kernels as K
+    if not _SHORT_LAST:
+        return False
+    x = short_saved[0]
+    if not x.is_cuda or tuple(sc.stride) != (2, 2):
+        return False
+    B, H, W, _ = x.shape
+    return B * H * W >= K._S2_PARITY_MIN_ROWS
 
 
 def _out_hw_c(c_in_shape, conv):
