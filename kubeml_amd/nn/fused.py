@@ -492,7 +492,7 @@ class BlockFn(Function):
             is_last = role == "last"
             is_first = k == 0
             addend = None
-            swap = is_first and short and not is_last and _short_last(saved[short[0][0]], short[0][1][0])
+            swap = is_first and short and not is_last and _short_last(saved[short[0][0]], short[0][1][0], conv)
             if is_first and not swap:
                 # shortcut gradient joins here: identity -> dres, projection -> its dgrad
                 if short:
@@ -532,14 +532,16 @@ class BlockFn(Function):
 _SHORT_LAST = os.environ.get("KUBEML_SHORT_LAST", "1") != "0"
 
 
-def _short_last(short_saved, sc) -> bool:
+def _short_last(short_saved, sc, conv1) -> bool:
     """Run a block's projection-shortcut dgrad after the main branch's (see the block backward):
-    a stride-2 shortcut whose input map is large enough for the parity-class dgrad."""
+    a stride-2 shortcut whose input map is large enough for the parity-class dgrad, next to an
+    unstrided first main conv (a Bottleneck's 1x1: its plain dgrad loses nothing, while a
+    BasicBlock's strided 3x3 needs the operands for its own parity-class dgrad)."""
     from ..ops import kernels as K
     if not _SHORT_LAST:
         return False
     x = short_saved[0]
-    if not x.is_cuda or tuple(sc.stride) != (2, 2):
+    if not x.is_cuda or tuple(sc.stride) != (2, 2) or tuple(conv1.stride) != (1, 1):
         return False
     B, H, W, _ = x.shape
     return B * H * W >= K._S2_PARITY_MIN_ROWS
