@@ -74,6 +74,9 @@ struct GemmArgs {
   const float* bmean;  // GEMM_BNF: [N]
   const float* brstd;  // GEMM_BNF: [N]
   int mask_out;        // GEMM_BNF: store dz = v * [by > 0]
+  // implicit-GEMM forward (k_gemm AG = 1): A = im2col(x) gathered by ConvStagerA; x NHWC [B][H][W][C],
+  // output pixel m = (b, oh, ow), K index k = tap * C + c (C % 64 == 0: a K-tile sits in one tap)
+  int cH, cW, cC, cOH, cOW, cKW, csh, csw, cph, cpw;
 };
 
 constexpr int BK = 64;
@@ -143,6 +146,48 @@ struct Stager {
     for (int j = 0; j < NI; ++j) {
       const bool in = ok[j] && kb + lim[j] < kend;
       const bf16_t* src = in ? base[j] + (long long)kb * kstep : zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
+                                       0);
+    }
+  }
+};
+
+// A operand of the implicit-GEMM forward: the KC [R][64] tile of im2col(x) for R output pixels.
+// Same lane -> (row, chunk) mapping and LDS image as Stager<R, true>; per K-tile the tap is uniform
+// (k = tap * C + c, C % 64 == 0), so a lane's source is its pixel's input row shifted by the tap,
+// or the zero page where the tap falls in the padding.
+template <int R>
+struct ConvStagerA {
+  static constexpr int NI = R / 64;
+  const bf16_t* base[NI];   // x + ((b H + ih0) W + iw0) C + chunk * 8 (ih0 = oh sh - ph; may point before x)
+  int ih0[NI], iw0[NI];
+  bool ok[NI];
+  __device__ void init(const GemmArgs& g, int r0, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int u = wave * NI + j;
+      const int row = 8 * u + (lane >> 3);
+      const int chunk = (lane & 7) ^ (row & 7);
+      const int m = r0 + row;
+      ok[j] = m < g.M;
+      const int mm = ok[j] ? m : 0;
+      const int t = mm / g.cOW, ow = mm - t * g.cOW;
+      const int b = t / g.cOH, oh = t - b * g.cOH;
+      ih0[j] = oh * g.csh - g.cph;
+      iw0[j] = ow * g.csw - g.cpw;
+      base[j] = g.a + ((long long)(b * g.cH + ih0[j]) * g.cW + iw0[j]) * g.cC + chunk * 8;
+    }
+  }
+  __device__ __forceinline__ void issue(char* lds, const GemmArgs& g, int kb, int kend, int wave) const {
+    const int tap = kb / g.cC, c0 = kb - tap * g.cC;
+    const int r = tap / g.cKW, sx = tap - r * g.cKW;
+    const long long shift = ((long long)r * g.cW + sx) * g.cC + c0;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int ih = ih0[j] + r, iw = iw0[j] + sx;
+      const bool in = ok[j] && kb < kend && (unsigned)ih < (unsigned)g.cH && (unsigned)iw < (unsigned)g.cW;
+      const bf16_t* src = in ? base[j] + shift : g.zp;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
                                        0);
@@ -399,8 +444,9 @@ __device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&a
 // so one tile's DMA stays in flight across the raw s_barrier (CDNA guide §5 "Pipelining
 // across barriers"; trailing steps re-issue the last tile into a stage nobody reads, so
 // the count never changes).
-template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S>
+template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S, int AG = 0>
 __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
+  static_assert(AG == 0 || (A_KC && B_KC && OUT == 0), "implicit-GEMM gather: forward layout, bf16 out");
   constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NI = BM / 64 + BN / 64;   // DMA instructions per wave per stage
@@ -416,9 +462,10 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  Stager<BM, A_KC> sa;
+  typename std::conditional<AG == 1, ConvStagerA<BM>, Stager<BM, A_KC>>::type sa;
   Stager<BN, B_KC> sb;
-  sa.init(g.a, g.lda, m0, g.M, wave, lane);
+  if constexpr (AG == 1) sa.init(g, m0, wave, lane);
+  else sa.init(g.a, g.lda, m0, g.M, wave, lane);
   sb.init(g.b, g.ldb, n0, g.N, wave, lane);
 
   f32x4_t acc[MR][NR];
@@ -429,7 +476,8 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
 
   auto issue = [&](int kt, int st) {
     char* dst = smem + st * STAGE;
-    sa.issue(dst, kbeg + kt * BK, kend, g.zp, wave);
+    if constexpr (AG == 1) sa.issue(dst, g, kbeg + kt * BK, kend, wave);
+    else sa.issue(dst, kbeg + kt * BK, kend, g.zp, wave);
     sb.issue(dst + A_BYTES, kbeg + kt * BK, kend, g.zp, wave);
   };
   auto compute = [&](int st) {
@@ -963,7 +1011,8 @@ int launch8(GemmArgs g, int splits, hipStream_t s) {
   KML_LAUNCH_CHECK();
 }
 
-template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S = (3 * (BM + BN) * BK * 2 <= 160 * 1024) ? 3 : 2>
+template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S = (3 * (BM + BN) * BK * 2 <= 160 * 1024) ? 3 : 2,
+          int AG = 0>
 int launch(GemmArgs g, int splits, hipStream_t s) {
   splits = splits < 1 ? 1 : splits;
   int chunk = (g.K + splits - 1) / splits;
@@ -971,7 +1020,7 @@ int launch(GemmArgs g, int splits, hipStream_t s) {
   g.kchunk = chunk > 0 ? chunk : BK;
   const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, z);
-  hipLaunchKernelGGL((k_gemm<BM, BN, A_KC, B_KC, OUT, S>), grid, dim3(NT), 0, s, g);
+  hipLaunchKernelGGL((k_gemm<BM, BN, A_KC, B_KC, OUT, S, AG>), grid, dim3(NT), 0, s, g);
   KML_LAUNCH_CHECK();
 }
 
@@ -1053,6 +1102,32 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   if (layout == 1 && out == 0) return by_tile<true, false, 0>(g, tile, 1, s);
   if (layout == 2 && out == 1) return by_tile<false, false, 1>(g, tile, 1, s);
   if (layout == 2 && out == 2) return by_tile<false, false, 2>(g, tile, splits, s);
+  return (int)hipErrorInvalidValue;
+}
+
+// Implicit-GEMM convolution forward on the k_gemm tiles (0-4): y[M = B OH OW][N = K] = im2col(x) W^T
+// with W [K][KH][KW][C] as the KC B operand (ldb = KH KW C) and A gathered per K-tile by ConvStagerA
+// (C % 64 == 0).  rows: the GEMM_STATS partial rows [M / BM][2 N] or null (plain bf16 output + bias).
+KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* rows,
+                              const bf16_t* zp, int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw,
+                              int ph, int pw, int tile, hipStream_t s) {
+  if (C % 64 || K % 8 || tile < 0 || tile > 4 || KH < 1 || KW < 1 || sh < 1 || sw < 1) return (int)hipErrorInvalidValue;
+  const int OH = (H + 2 * ph - KH) / sh + 1, OW = (W + 2 * pw - KW) / sw + 1;
+  if (OH <= 0 || OW <= 0) return 0;
+  GemmArgs g;
+  g.a = x; g.b = w; g.c = y; g.c2 = nullptr; g.bias = bias; g.zp = zp;
+  g.lda = C; g.ldb = (long long)KH * KW * C; g.ldc = K;
+  g.M = B * OH * OW; g.N = K; g.K = KH * KW * C; g.act = rows ? GEMM_STATS : 0; g.beta = 0.f; g.kchunk = g.K;
+  g.colpart = rows;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
+  switch (tile) {
+    case 0: return launch<256, 256, true, true, 0, 2, 1>(g, 1, s);
+    case 1: return launch<256, 128, true, true, 0, 3, 1>(g, 1, s);
+    case 2: return launch<128, 256, true, true, 0, 3, 1>(g, 1, s);
+    case 3: return launch<128, 128, true, true, 0, 3, 1>(g, 1, s);
+    case 4: return launch<128, 128, true, true, 0, 2, 1>(g, 1, s);
+  }
   return (int)hipErrorInvalidValue;
 }
 

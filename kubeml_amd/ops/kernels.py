@@ -381,6 +381,10 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
                             stats_group=stats_group)
         from . import gemm as G
         zp = G._zp(x.device)
+        if not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad):   # implicit GEMM: A gathered per K-tile
+            HIP.call("kml_gemm_conv_fwd", "p p p p p p i i i i i i i i i i i i s", _p(x), _p(w), _p(out), _p(bias),
+                     _p(rows), _p(zp), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, _s())
+            return out
         if stats is None:
             HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", _p(x), C, _p(w), C, _p(out), K, 0,
                      _p(bias), _p(zp), M, K, C, 0, 0, 0, 0.0, bk, 1, _s())
@@ -420,8 +424,8 @@ def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     if plan[4] == DIRECT and C % 32:
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
-    if plan[4] == GEMM1X1 and (geom is None or not gemm1x1_ok(C, K, *geom) or
-                               (plan[0], plan[1], plan[2]) not in _GEMM1X1_TILES):
+    if plan[4] == GEMM1X1 and (geom is None or (plan[0], plan[1], plan[2]) not in _GEMM1X1_TILES or
+                               not (gemm1x1_ok(C, K, *geom) or (plan[2] <= 4 and gemm_conv_ok(C, K, *geom)))):
         plan = _norm_cfg(default_plan("fwd", M, K, Kd))
     return plan
 
@@ -491,6 +495,12 @@ _GEMM1X1_FALLBACK = {128: (128, 64, 32, 1, 0), 256: (256, 128, 64, 1, 1)}
 def gemm1x1_ok(C, K, H, W, KH, KW, stride, pad) -> bool:
     """Can this forward conv run as a plain GEMM x[M, C] @ w[K, C]^T (1x1, stride 1, no padding)?"""
     return (KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and C % 8 == 0 and K % 8 == 0
+
+
+def gemm_conv_ok(C, K, H, W, KH, KW, stride, pad) -> bool:
+    """Can this forward conv run on the GEMM tiles as an implicit GEMM (kml_gemm_conv_fwd: the A
+    operand gathered from x per K-tile, one filter tap per tile)?"""
+    return C % 64 == 0 and K % 8 == 0
 
 
 def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:

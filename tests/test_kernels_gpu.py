@@ -142,6 +142,33 @@ def test_conv1x1_gemm_route_output_and_stats_rows(cfg, shape):
 
 @pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
                                  (128, 128, 4, 1, 7)])
+@pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1, 1), (2, 15, 128, 64, 3, 2, 1), (2, 9, 64, 72, 1, 2, 0),
+                                  (3, 8, 192, 256, 3, 1, 1)])
+def test_conv_gemm_gather_route_matches_torch(cfg, geom):
+    """Implicit-GEMM forward on the GEMM tiles (kml_gemm_conv_fwd: im2col A gathered per K-tile by the
+    DMA stager, padding taps from the zero page): output and BN statistics rows vs fp32 torch, incl.
+    stride 2, ragged M, bias."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co, k, s, p = geom
+    torch.manual_seed(7)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * (k * k * Ci) ** -0.5)
+    bias = torch.randn(Co, device=dev)
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, stride=s, padding=p)
+    assert K.conv_fwd_plan(Ci, yr.shape[0] * yr.shape[2] * yr.shape[3], Co, k * k * Ci, cfg=cfg,
+                           geom=(H, H, k, k, (s, s), (p, p))) == cfg
+    G = K.conv_fwd_stats_rows(x.shape, Co, k, k, (s, s), (p, p), cfg=cfg)
+    rows = torch.full((G * 2 * Co,), float("nan"), device=dev)
+    y = K.conv_fwd(x, w, k, k, (s, s), (p, p), bias=bias, stats=rows, stats_part=True, cfg=cfg)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 1e-2
+    yf = y.float().reshape(-1, Co)
+    r = rows.view(G, 2, Co).sum(0)
+    assert torch.allclose(r[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(r[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
+                                 (128, 128, 4, 1, 7)])
 @pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 136, 512)])
 def test_conv1x1_dgrad_gemm_route_matches_implicit_gemm(cfg, shape):
     """1x1 / stride-1 dgrad on the MFMA GEMM (kml_gemm_dgrad_bnf) against the implicit-GEMM dgrad:

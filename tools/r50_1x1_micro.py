@@ -41,12 +41,15 @@ def main():
     ap.add_argument("--tiles", action="store_true", help="also time every implicit-GEMM tile")
     ap.add_argument("--gemm", action="store_true", help="also time the plain MFMA GEMM (ops.gemm) tiles, no stats")
     ap.add_argument("--route", action="store_true", help="time the conv GEMM route (BN stats epilogue) per tile")
+    ap.add_argument("--conv3", action="store_true", help="3x3 forward convs: implicit GEMM vs the GEMM gather route")
     ap.add_argument("--dgrad", action="store_true", help="time the 1x1 dgrads (consumer-BN epilogue, residual addend "
                                                           "where the model has one) against the plain GEMM")
     args = ap.parse_args()
     dev = torch.device("cuda")
     if args.dgrad:
         return dgrad_main(dev)
+    if args.conv3:
+        return conv3_main(dev)
     for (B, H, C, Co, st) in SHAPES:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
@@ -113,6 +116,41 @@ def main():
                     if t < best[0]:
                         best = (t, cfg)
             print(f"BEST fwd M={M} N={Co} Kd={C}: {best[1]} {best[0]:.1f}us (plan {t_st:.1f}us)", flush=True)
+
+
+CONV3 = [  # B, H, C, K, stride: the 3x3 convs of ResNet-50 at 224^2
+    (128, 56, 64, 64, 1), (128, 56, 128, 128, 2), (128, 28, 128, 128, 1), (128, 28, 256, 256, 2),
+    (128, 14, 256, 256, 1), (128, 14, 512, 512, 2), (128, 7, 512, 512, 1)]
+
+
+def conv3_main(dev):
+    for (B, H, C, Co, st) in CONV3:
+        x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, 3, 3, C, device=dev) * 0.02).to(torch.bfloat16)
+        S, P = (st, st), (1, 1)
+        OH = (H - 1) // st + 1
+        M = B * OH * OH
+        y = torch.empty(B, OH, OH, Co, dtype=torch.bfloat16, device=dev)
+        plan = K.conv_fwd_plan(C, M, Co, 9 * C, geom=(H, H, 3, 3, S, P))
+        G = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, S, P)
+        rows = torch.empty(G * 2 * Co, device=dev)
+        t = gtime(lambda: K.conv_fwd(x, w, 3, 3, S, P, out=y, stats=rows, stats_part=True), reps=20)
+        fl = 2 * M * Co * 9 * C
+        line = f"conv3 {H}x{H}/s{st} {C}->{Co} M={M} plan={plan}: {t:.1f}us ({fl / t / 1e6:.0f} TF/s)"
+        best = None
+        for (bm, bn, tc) in sorted(K._GEMM1X1_TILES):
+            if tc > 4:
+                continue
+            cfg = (bm, bn, tc, 1, K.GEMM1X1)
+            G2 = K.conv_fwd_stats_rows(x.shape, Co, 3, 3, S, P, cfg=cfg)
+            r2 = torch.empty(G2 * 2 * Co, device=dev)
+            tg = gtime(lambda: K.conv_fwd(x, w, 3, 3, S, P, out=y, stats=r2, stats_part=True, cfg=cfg), reps=20)
+            line += f"  g{cfg[:3]}: {tg:.1f}"
+            if best is None or tg < best[0]:
+                best = (tg, cfg)
+        print(line, flush=True)
+        print(f"C3ROUTE fwd M={M} N={Co} Kd={9 * C}: {best[1]} {best[0]:.1f}us (plan {plan} {t:.1f}us) "
+              f"[{fl / best[0] / 1e6:.0f} TF/s]", flush=True)
 
 
 def dgrad_main(dev):
