@@ -77,6 +77,7 @@ struct GemmArgs {
   // implicit-GEMM forward (k_gemm AG = 1): A = im2col(x) gathered by ConvStagerA; x NHWC [B][H][W][C],
   // output pixel m = (b, oh, ow), K index k = tap * C + c (C % 64 == 0: a K-tile sits in one tap)
   int cH, cW, cC, cOH, cOW, cKW, csh, csw, cph, cpw;
+  int cK;              // implicit-GEMM dgrad (AG = 2): output channels of dy (K % 64 == 0)
 };
 
 constexpr int BK = 64;
@@ -157,13 +158,19 @@ struct Stager {
 // Same lane -> (row, chunk) mapping and LDS image as Stager<R, true>; per K-tile the tap is uniform
 // (k = tap * C + c, C % 64 == 0), so a lane's source is its pixel's input row shifted by the tap,
 // or the zero page where the tap falls in the padding.
-template <int R>
+template <int R, bool DG = false>
 struct ConvStagerA {
+  // DG = false (forward): row = output pixel (b, oh, ow), source x [B][H][W][C], tap (r, s) reads
+  //   (oh sh - ph + r, ow sw - pw + s).
+  // DG = true (stride-1 input gradient): row = input pixel (b, ih, iw), source dy [B][OH][OW][K],
+  //   tap (r, s) reads (ih + ph - r, iw + pw - s); k = tap * K + cout.
   static constexpr int NI = R / 64;
-  const bf16_t* base[NI];   // x + ((b H + ih0) W + iw0) C + chunk * 8 (ih0 = oh sh - ph; may point before x)
-  int ih0[NI], iw0[NI];
+  const bf16_t* base[NI];   // source + ((b SH + p0) SW + q0) SC + chunk * 8 (may point outside the source)
+  int p0[NI], q0[NI];
   bool ok[NI];
   __device__ void init(const GemmArgs& g, int r0, int wave, int lane) {
+    const int GW = DG ? g.cW : g.cOW, GH = DG ? g.cH : g.cOH;
+    const int SH = DG ? g.cOH : g.cH, SW = DG ? g.cOW : g.cW, SC = DG ? g.cK : g.cC;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int u = wave * NI + j;
@@ -172,21 +179,57 @@ struct ConvStagerA {
       const int m = r0 + row;
       ok[j] = m < g.M;
       const int mm = ok[j] ? m : 0;
-      const int t = mm / g.cOW, ow = mm - t * g.cOW;
-      const int b = t / g.cOH, oh = t - b * g.cOH;
-      ih0[j] = oh * g.csh - g.cph;
-      iw0[j] = ow * g.csw - g.cpw;
-      base[j] = g.a + ((long long)(b * g.cH + ih0[j]) * g.cW + iw0[j]) * g.cC + chunk * 8;
+      const int t = mm / GW, x = mm - t * GW;
+      const int b = t / GH, y = t - b * GH;
+      p0[j] = DG ? y + g.cph : y * g.csh - g.cph;
+      q0[j] = DG ? x + g.cpw : x * g.csw - g.cpw;
+      base[j] = g.a + ((long long)(b * SH + p0[j]) * SW + q0[j]) * SC + chunk * 8;
     }
   }
   __device__ __forceinline__ void issue(char* lds, const GemmArgs& g, int kb, int kend, int wave) const {
-    const int tap = kb / g.cC, c0 = kb - tap * g.cC;
+    const int SH = DG ? g.cOH : g.cH, SW = DG ? g.cOW : g.cW, SC = DG ? g.cK : g.cC;
+    const int tap = kb / SC, c0 = kb - tap * SC;
     const int r = tap / g.cKW, sx = tap - r * g.cKW;
-    const long long shift = ((long long)r * g.cW + sx) * g.cC + c0;
+    const long long shift = (DG ? -((long long)r * SW + sx) : ((long long)r * SW + sx)) * SC + c0;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int ih = ih0[j] + r, iw = iw0[j] + sx;
-      const bool in = ok[j] && kb < kend && (unsigned)ih < (unsigned)g.cH && (unsigned)iw < (unsigned)g.cW;
+      const int ih = DG ? p0[j] - r : p0[j] + r, iw = DG ? q0[j] - sx : q0[j] + sx;
+      const bool in = ok[j] && kb < kend && (unsigned)ih < (unsigned)SH && (unsigned)iw < (unsigned)SW;
+      const bf16_t* src = in ? base[j] + shift : g.zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
+                                       0);
+    }
+  }
+};
+
+// B operand of the implicit-GEMM input gradient: the KS [64][R] tile of W^T with k = tap * K + cout
+// and n = cin — W [K][KH][KW][C] read as rows cout (stride KH KW C) shifted by the K-tile's tap.
+// Same lane mapping / LDS image as Stager<R, false>.
+template <int R>
+struct ConvStagerB {
+  static constexpr int NI = R / 64;
+  const bf16_t* base[NI];
+  int lim[NI];
+  bool ok[NI];
+  __device__ void init(const GemmArgs& g, int r0, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int u = wave * NI + j;
+      constexpr int CPR = R / 8, RPI = 64 / CPR;
+      const int krow = RPI * u + lane / CPR;
+      const int chunk = (lane % CPR) ^ swz_ks<R>(krow);
+      ok[j] = r0 + chunk * 8 < g.N;
+      base[j] = g.b + (long long)krow * g.ldb + (ok[j] ? r0 + chunk * 8 : 0);
+      lim[j] = krow;
+    }
+  }
+  __device__ __forceinline__ void issue(char* lds, const GemmArgs& g, int kb, int kend, int wave) const {
+    const int tap = kb / g.cK, k0 = kb - tap * g.cK;
+    const long long shift = (long long)k0 * g.ldb + (long long)tap * g.cC;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const bool in = ok[j] && kb + lim[j] < kend;
       const bf16_t* src = in ? base[j] + shift : g.zp;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
@@ -446,7 +489,8 @@ __device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&a
 // the count never changes).
 template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S, int AG = 0>
 __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
-  static_assert(AG == 0 || (A_KC && B_KC && OUT == 0), "implicit-GEMM gather: forward layout, bf16 out");
+  static_assert(AG == 0 || (AG == 1 && A_KC && B_KC && OUT == 0) || (AG == 2 && A_KC && !B_KC && OUT == 0),
+                "implicit-GEMM gather: forward (AG 1) or input-gradient (AG 2) layout, bf16 out");
   constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NI = BM / 64 + BN / 64;   // DMA instructions per wave per stage
@@ -462,11 +506,12 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  typename std::conditional<AG == 1, ConvStagerA<BM>, Stager<BM, A_KC>>::type sa;
-  Stager<BN, B_KC> sb;
-  if constexpr (AG == 1) sa.init(g, m0, wave, lane);
+  typename std::conditional<AG != 0, ConvStagerA<BM, AG == 2>, Stager<BM, A_KC>>::type sa;
+  typename std::conditional<AG == 2, ConvStagerB<BN>, Stager<BN, B_KC>>::type sb;
+  if constexpr (AG != 0) sa.init(g, m0, wave, lane);
   else sa.init(g.a, g.lda, m0, g.M, wave, lane);
-  sb.init(g.b, g.ldb, n0, g.N, wave, lane);
+  if constexpr (AG == 2) sb.init(g, n0, wave, lane);
+  else sb.init(g.b, g.ldb, n0, g.N, wave, lane);
 
   f32x4_t acc[MR][NR];
 #pragma unroll
@@ -476,9 +521,10 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
 
   auto issue = [&](int kt, int st) {
     char* dst = smem + st * STAGE;
-    if constexpr (AG == 1) sa.issue(dst, g, kbeg + kt * BK, kend, wave);
+    if constexpr (AG != 0) sa.issue(dst, g, kbeg + kt * BK, kend, wave);
     else sa.issue(dst, kbeg + kt * BK, kend, g.zp, wave);
-    sb.issue(dst + A_BYTES, kbeg + kt * BK, kend, g.zp, wave);
+    if constexpr (AG == 2) sb.issue(dst + A_BYTES, g, kbeg + kt * BK, kend, wave);
+    else sb.issue(dst + A_BYTES, kbeg + kt * BK, kend, g.zp, wave);
   };
   auto compute = [&](int st) {
     const char* sA = smem + st * STAGE;
@@ -1127,6 +1173,36 @@ KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const
     case 2: return launch<128, 256, true, true, 0, 3, 1>(g, 1, s);
     case 3: return launch<128, 128, true, true, 0, 3, 1>(g, 1, s);
     case 4: return launch<128, 128, true, true, 0, 2, 1>(g, 1, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Implicit-GEMM input gradient of a stride-1 conv on the k_gemm tiles (0-4): dx[M = B H W][N = C] =
+// sum over (tap, cout) of dy[pixel shifted by the tap][cout] W[cout][tap][cin]; A gathered from dy by
+// ConvStagerA<DG>, B = W read per tap by ConvStagerB (K % 64 == 0), the dgrad epilogue of
+// kml_gemm_dgrad_bnf (addend, consumer-BN rows, ReLU mask).
+KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, const bf16_t* y,
+                                const bf16_t* cin, const float* mean, const float* rstd, float* rows, int mask_out,
+                                const bf16_t* zp, int B, int H, int W, int C, int K, int KH, int KW, int ph, int pw,
+                                int tile, hipStream_t s) {
+  if (K % 64 || C % 8 || tile < 0 || tile > 4 || KH < 1 || KW < 1) return (int)hipErrorInvalidValue;
+  if (cin && (!mean || !rstd || !rows)) return (int)hipErrorInvalidValue;
+  const int OH = H + 2 * ph - KH + 1, OW = W + 2 * pw - KW + 1;
+  if (OH <= 0 || OW <= 0 || B * H * W <= 0) return 0;
+  GemmArgs g;
+  g.a = dy; g.b = w; g.c = dx; g.c2 = const_cast<bf16_t*>(addend); g.bias = nullptr; g.zp = zp;
+  g.lda = K; g.ldb = (long long)KH * KW * C; g.ldc = C;
+  g.M = B * H * W; g.N = C; g.K = KH * KW * K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = g.K;
+  g.colpart = rows;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out;
+  g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = 1; g.csw = 1; g.cph = ph; g.cpw = pw;
+  g.cK = K;
+  switch (tile) {
+    case 0: return launch<256, 256, true, false, 0, 2, 2>(g, 1, s);
+    case 1: return launch<256, 128, true, false, 0, 3, 2>(g, 1, s);
+    case 2: return launch<128, 256, true, false, 0, 3, 2>(g, 1, s);
+    case 3: return launch<128, 128, true, false, 0, 3, 2>(g, 1, s);
+    case 4: return launch<128, 128, true, false, 0, 2, 2>(g, 1, s);
   }
   return (int)hipErrorInvalidValue;
 }

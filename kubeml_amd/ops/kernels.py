@@ -497,6 +497,12 @@ def gemm1x1_ok(C, K, H, W, KH, KW, stride, pad) -> bool:
     return (KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0) and C % 8 == 0 and K % 8 == 0
 
 
+def gemm_dgrad_gather_ok(C, K, stride) -> bool:
+    """Can this conv's input gradient run on the GEMM tiles as an implicit GEMM (kml_gemm_conv_dgrad:
+    stride 1, one filter tap per K-tile of dy's channels)?"""
+    return tuple(stride) == (1, 1) and K % 64 == 0 and C % 8 == 0
+
+
 def gemm_conv_ok(C, K, H, W, KH, KW, stride, pad) -> bool:
     """Can this forward conv run on the GEMM tiles as an implicit GEMM (kml_gemm_conv_fwd: the A
     operand gathered from x per K-tile, one filter tap per tile)?"""
@@ -756,8 +762,9 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     bm, bn, bk, splits, variant = _norm_cfg(cfg or hp or plan_conv("dgrad", M, C, ntap * K))
     if variant == HALO and (_g22 or not halo_dgrad_ok(C, K, H, W, KH, KW, stride, pad, bm, bn)):
         bm, bn, bk, splits, variant = _norm_cfg(plan_conv("dgrad", M, C, ntap * K))
+    gather = not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad)   # implicit GEMM: A gathered from dy per K-tile
     if variant == GEMM1X1 and ((bm, bn, bk) not in _GEMM1X1_TILES or bk > 4 or _fold or _g22 or wt is not None or
-                               not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad) or not dy.is_contiguous() or
+                               (gather and not gemm_dgrad_gather_ok(C, K, stride)) or not dy.is_contiguous() or
                                not out.is_contiguous()):
         bm, bn, bk, splits, variant = _GEMM1X1_FALLBACK[bm] if bm in _GEMM1X1_FALLBACK else \
             _norm_cfg(default_plan("dgrad", M, C, ntap * K))
@@ -765,6 +772,12 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
     if variant == GEMM1X1:  # dx[M, C] = dy[M, K] @ w[K, C] on the MFMA GEMM, the dgrad epilogue fused
         by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan)
         from . import gemm as GM
+        if gather:
+            HIP.call("kml_gemm_conv_dgrad", "p p p p p p p p p i p i i i i i i i i i i s", _p(dy), _p(w), _p(out),
+                     _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
+                     int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), B, H, W, C, K, KH, KW, ph, pw,
+                     bk, _s())
+            return (out, (part, G)) if bnf is not None else out
         HIP.call("kml_gemm_dgrad_bnf", "p l p l p l p p p p p p i p i i i i s", _p(dy), K, _p(w), C, _p(out), C,
                  _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
                  int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), M, C, K, bk, _s())

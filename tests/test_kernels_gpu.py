@@ -169,6 +169,38 @@ def test_conv_gemm_gather_route_matches_torch(cfg, geom):
 
 @pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
                                  (128, 128, 4, 1, 7)])
+@pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1), (3, 7, 136, 64, 3, 1), (2, 9, 72, 192, 3, 1)])
+def test_conv_dgrad_gemm_gather_route_matches_torch(cfg, geom):
+    """Implicit-GEMM input gradient on the GEMM tiles (kml_gemm_conv_dgrad, stride 1): dx vs fp32
+    torch autograd with a residual addend, and the consumer-BN rows / ReLU mask vs that dx."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co, k, p = geom
+    torch.manual_seed(8)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * (k * k * Co) ** -0.5)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, w.float().permute(0, 3, 1, 2), padding=p)
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    add = _bf(torch.randn(B, H, H, Ci, device=dev))
+    dx = K.conv_dgrad(dyn, w, x.shape, k, k, (1, 1), (p, p), addend=add, cfg=cfg)
+    assert _rel(dx.permute(0, 3, 1, 2), xr.grad + add.float().permute(0, 3, 1, 2)) < 1e-2
+    yb = _bf(torch.randn(B, H, H, Ci, device=dev))
+    cb = _bf(torch.randn(B, H, H, Ci, device=dev))
+    mean, rstd = torch.randn(Ci, device=dev) * 0.1, torch.rand(Ci, device=dev) + 0.5
+    dz, (part, G) = K.conv_dgrad(dyn, w, x.shape, k, k, (1, 1), (p, p), addend=add, cfg=cfg,
+                                 bnf=(yb, cb, mean, rstd), bnf_mask=True)
+    keep = yb.float() > 0
+    assert torch.equal(dz, dx * keep)
+    dzf = (dx.float() * keep).reshape(-1, Ci)
+    r = part.view(G, 2, Ci).sum(0)
+    assert torch.allclose(r[0], dzf.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(r[1], (dzf * ((cb.float() - mean) * rstd).reshape(-1, Ci)).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
+                                 (128, 128, 4, 1, 7)])
 @pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 136, 512)])
 def test_conv1x1_dgrad_gemm_route_matches_implicit_gemm(cfg, shape):
     """1x1 / stride-1 dgrad on the MFMA GEMM (kml_gemm_dgrad_bnf) against the implicit-GEMM dgrad:

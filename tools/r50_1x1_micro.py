@@ -151,6 +151,32 @@ def conv3_main(dev):
         print(line, flush=True)
         print(f"C3ROUTE fwd M={M} N={Co} Kd={9 * C}: {best[1]} {best[0]:.1f}us (plan {plan} {t:.1f}us) "
               f"[{fl / best[0] / 1e6:.0f} TF/s]", flush=True)
+        if st != 1:
+            continue
+        # input gradient with the consumer-BN epilogue (as the model runs it)
+        dy = torch.randn(B, H, H, Co, device=dev).to(torch.bfloat16)
+        xs = (B, H, H, C)
+        yb = torch.randn(xs, device=dev).to(torch.bfloat16)
+        cb = torch.randn(xs, device=dev).to(torch.bfloat16)
+        mean, rstd = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        out = torch.empty(xs, dtype=torch.bfloat16, device=dev)
+        dplan = K.plan_conv("dgrad", B * H * H, C, 9 * Co)
+        td = gtime(lambda: K.conv_dgrad(dy, w, xs, 3, 3, S, P, out=out, bnf=(yb, cb, mean, rstd), bnf_mask=True),
+                   reps=20)
+        dbest = None
+        line = f"dgrad3 {H}x{H} {Co}->{C} plan={dplan}: {td:.1f}us"
+        for (bm, bn, tc) in sorted(K._GEMM1X1_TILES):
+            if tc > 4:
+                continue
+            cfg = (bm, bn, tc, 1, K.GEMM1X1)
+            tg = gtime(lambda: K.conv_dgrad(dy, w, xs, 3, 3, S, P, out=out, cfg=cfg, bnf=(yb, cb, mean, rstd),
+                                            bnf_mask=True), reps=20)
+            line += f"  g{cfg[:3]}: {tg:.1f}"
+            if dbest is None or tg < dbest[0]:
+                dbest = (tg, cfg)
+        print(line, flush=True)
+        print(f"D3ROUTE dgrad M={B * H * H} N={C} Kd={9 * Co}: {dbest[1]} {dbest[0]:.1f}us (plan {dplan} {td:.1f}us) "
+              f"[{fl / dbest[0] / 1e6:.0f} TF/s]", flush=True)
 
 
 def dgrad_main(dev):
