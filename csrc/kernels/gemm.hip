@@ -206,6 +206,48 @@ struct ConvStagerA {
 // B operand of the implicit-GEMM input gradient: the KS [64][R] tile of W^T with k = tap * K + cout
 // and n = cin — W [K][KH][KW][C] read as rows cout (stride KH KW C) shifted by the K-tile's tap.
 // Same lane mapping / LDS image as Stager<R, false>.
+// B operand of the implicit-GEMM weight gradient: the KS [64][R] tile of im2col(x), k = output pixel,
+// n = tap * C + cin.  A lane's 8-channel column chunk stays in one tap (C % 8 == 0), so (r, s, c) are
+// fixed at init; its k-row's pixel (b, oh, ow) is decoded per K-tile.
+template <int R>
+struct ConvStagerBW {
+  static constexpr int NI = R / 64;
+  int krow[NI], r[NI], sx[NI], c[NI];
+  bool ok[NI];
+  __device__ void init(const GemmArgs& g, int n0, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int u = wave * NI + j;
+      constexpr int CPR = R / 8, RPI = 64 / CPR;
+      krow[j] = RPI * u + lane / CPR;
+      const int chunk = (lane % CPR) ^ swz_ks<R>(krow[j]);
+      const int col = n0 + chunk * 8;
+      ok[j] = col < g.N;
+      const int cc = ok[j] ? col : 0;
+      const int tap = cc / g.cC;
+      c[j] = cc - tap * g.cC;
+      r[j] = tap / g.cKW;
+      sx[j] = tap - r[j] * g.cKW;
+    }
+  }
+  __device__ __forceinline__ void issue(char* lds, const GemmArgs& g, int kb, int kend, int wave) const {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int p = kb + krow[j];
+      bool in = ok[j] && p < kend;
+      const int pp = in ? p : 0;
+      const int t = pp / g.cOW, ow = pp - t * g.cOW;
+      const int b = t / g.cOH, oh = t - b * g.cOH;
+      const int ih = oh * g.csh - g.cph + r[j], iw = ow * g.csw - g.cpw + sx[j];
+      in = in && (unsigned)ih < (unsigned)g.cH && (unsigned)iw < (unsigned)g.cW;
+      const bf16_t* src = in ? g.b + ((long long)(b * g.cH + ih) * g.cW + iw) * g.cC + c[j] : g.zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(lds + (wave * NI + j) * 1024), 16, 0,
+                                       0);
+    }
+  }
+};
+
 template <int R>
 struct ConvStagerB {
   static constexpr int NI = R / 64;
@@ -489,8 +531,9 @@ __device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&a
 // the count never changes).
 template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S, int AG = 0>
 __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
-  static_assert(AG == 0 || (AG == 1 && A_KC && B_KC && OUT == 0) || (AG == 2 && A_KC && !B_KC && OUT == 0),
-                "implicit-GEMM gather: forward (AG 1) or input-gradient (AG 2) layout, bf16 out");
+  static_assert(AG == 0 || (AG == 1 && A_KC && B_KC && OUT == 0) || (AG == 2 && A_KC && !B_KC && OUT == 0) ||
+                    (AG == 3 && !A_KC && !B_KC && OUT == 3),
+                "implicit-GEMM gather: forward (AG 1) / input-gradient (AG 2) bf16 out, weight gradient (AG 3) slabs");
   constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NI = BM / 64 + BN / 64;   // DMA instructions per wave per stage
@@ -506,11 +549,13 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  typename std::conditional<AG != 0, ConvStagerA<BM, AG == 2>, Stager<BM, A_KC>>::type sa;
-  typename std::conditional<AG == 2, ConvStagerB<BN>, Stager<BN, B_KC>>::type sb;
-  if constexpr (AG != 0) sa.init(g, m0, wave, lane);
+  constexpr bool AGA = AG == 1 || AG == 2;   // gathered A (forward / input gradient)
+  typename std::conditional<AGA, ConvStagerA<BM, AG == 2>, Stager<BM, A_KC>>::type sa;
+  typename std::conditional<AG == 2, ConvStagerB<BN>,
+                            typename std::conditional<AG == 3, ConvStagerBW<BN>, Stager<BN, B_KC>>::type>::type sb;
+  if constexpr (AGA) sa.init(g, m0, wave, lane);
   else sa.init(g.a, g.lda, m0, g.M, wave, lane);
-  if constexpr (AG == 2) sb.init(g, n0, wave, lane);
+  if constexpr (AG >= 2) sb.init(g, n0, wave, lane);
   else sb.init(g.b, g.ldb, n0, g.N, wave, lane);
 
   f32x4_t acc[MR][NR];
@@ -521,9 +566,9 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
 
   auto issue = [&](int kt, int st) {
     char* dst = smem + st * STAGE;
-    if constexpr (AG != 0) sa.issue(dst, g, kbeg + kt * BK, kend, wave);
+    if constexpr (AGA) sa.issue(dst, g, kbeg + kt * BK, kend, wave);
     else sa.issue(dst, kbeg + kt * BK, kend, g.zp, wave);
-    if constexpr (AG == 2) sb.issue(dst + A_BYTES, g, kbeg + kt * BK, kend, wave);
+    if constexpr (AG >= 2) sb.issue(dst + A_BYTES, g, kbeg + kt * BK, kend, wave);
     else sb.issue(dst + A_BYTES, kbeg + kt * BK, kend, g.zp, wave);
   };
   auto compute = [&](int st) {
@@ -1205,6 +1250,40 @@ KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, c
     case 4: return launch<128, 128, true, false, 0, 2, 2>(g, 1, s);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Implicit-GEMM weight gradient on the k_gemm tiles (0-4): dw[M = K][N = KH KW C] = beta dw + sum over the
+// output pixels of dy[p][k] im2col(x)[p][(tap, c)] (dy the KS A operand, ld K; im2col(x) gathered by
+// ConvStagerBW), each K-slice's fp32 tile to slab[z] and one ordered pass summing the slabs into dw
+// (deterministic, as kml_gemm_wgrad_splitk).  slab holds ceil(P / chunk) * M * N floats.
+KML_API int kml_gemm_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, float* slab, const bf16_t* zp, int B,
+                                int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph, int pw, float beta,
+                                int tile, int splits, hipStream_t s) {
+  if (C % 8 || K % 4 || tile < 0 || tile > 4 || KH < 1 || KW < 1 || sh < 1 || sw < 1) return (int)hipErrorInvalidValue;
+  const int OH = (H + 2 * ph - KH) / sh + 1, OW = (W + 2 * pw - KW) / sw + 1;
+  if (OH <= 0 || OW <= 0) return 0;
+  GemmArgs g;
+  g.a = dy; g.b = x; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
+  g.lda = K; g.ldb = 0; g.ldc = (long long)KH * KW * C;
+  g.M = K; g.N = KH * KW * C; g.K = B * OH * OW; g.act = 0; g.beta = 0.f; g.kchunk = g.K; g.colpart = nullptr;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
+  g.cK = K;
+  splits = splits < 1 ? 1 : splits;
+  int rc = (int)hipErrorInvalidValue;
+  switch (tile) {
+    case 0: rc = launch<256, 256, false, false, 3, 2, 3>(g, splits, s); break;
+    case 1: rc = launch<256, 128, false, false, 3, 3, 3>(g, splits, s); break;
+    case 2: rc = launch<128, 256, false, false, 3, 3, 3>(g, splits, s); break;
+    case 3: rc = launch<128, 128, false, false, 3, 3, 3>(g, splits, s); break;
+    case 4: rc = launch<128, 128, false, false, 3, 2, 3>(g, splits, s); break;
+  }
+  if (rc) return rc;
+  const int chunk = ((g.K + splits - 1) / splits + BK - 1) / BK * BK;
+  const int z = (g.K + chunk - 1) / chunk;
+  const long long n4 = (long long)g.M * g.N / 4;
+  hipLaunchKernelGGL(k_splitk_reduce, dim3(kml_stream_grid(n4, 256)), dim3(256), 0, s, slab, dw, n4, z, beta);
+  KML_LAUNCH_CHECK();
 }
 
 // Forward GEMM (layout 0, bf16 out, optional fp32 bias) with BatchNorm partial statistics in the

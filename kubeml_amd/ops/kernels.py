@@ -835,20 +835,48 @@ _WGRAD_GEMM: dict = {}
 if os.path.exists(_WGRAD_GEMM_FILE):
     with open(_WGRAD_GEMM_FILE) as _f:
         for _e in json.load(_f).get("entries", []):
-            _WGRAD_GEMM[(int(_e["P"]), int(_e["K"]), int(_e["C"]))] = tuple(_e["route"])
+            # key: (input pixels, K, C, KH, stride); 1x1/s1 entries omit KH / S
+            _WGRAD_GEMM[(int(_e["P"]), int(_e["K"]), int(_e["C"]), int(_e.get("KH", 1)), int(_e.get("S", 1)))] = \
+                tuple(_e["route"])
 
 
 def wgrad_gemm_route(x_shape, K, KH, KW, stride, pad, dbias=None):
-    """The table's GEMM route for this conv's weight gradient, or None (implicit-GEMM wgrad)."""
-    if not _WGRAD_GEMM or dbias is not None or (KH, KW) != (1, 1) or tuple(stride) != (1, 1) or tuple(pad) != (0, 0):
+    """The table's GEMM route for this conv's weight gradient, or None (implicit-GEMM wgrad):
+    ["blas"] / ["slab", ...] for 1x1/s1 convs (a plain GEMM), ["gather", BM, BN, stages, splits] for
+    the implicit GEMM on the GEMM tiles (kml_gemm_conv_wgrad: square kernel, pad (KH - 1) / 2)."""
+    if not _WGRAD_GEMM or dbias is not None or KH != KW or stride[0] != stride[1]:
         return None
     B, H, W, C = x_shape
-    return _WGRAD_GEMM.get((B * H * W, K, C))
+    r = _WGRAD_GEMM.get((B * H * W, K, C, KH, stride[0]))
+    if r is None:
+        return None
+    if r[0] == "gather":
+        ok = tuple(pad) == ((KH - 1) // 2,) * 2 and C % 8 == 0 and K % 4 == 0
+    else:
+        ok = (KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
+    return r if ok else None
 
 
-def _wgrad_gemm(route, x, dy, dw, accumulate):
+def _wgrad_gemm(route, x, dy, dw, accumulate, stride=(1, 1)):
     B, H, W, C = x.shape
     K, P = dy.shape[3], B * H * W
+    if route[0] == "gather":
+        from . import gemm as G
+        _, bm, bn, st, splits = route
+        KH = dw.shape[1]
+        pad = (KH - 1) // 2
+        OH, OW = dy.shape[1], dy.shape[2]
+        sh = int(stride[0])
+        Pout = B * OH * OW
+        chunk = _cdiv(_cdiv(Pout, max(1, splits)), 64) * 64
+        nz = _cdiv(Pout, chunk)
+        N = dw.numel() // K
+        slab = torch.empty(nz * K * N, dtype=F32, device=dw.device)
+        tile = G.TILES[(bm, bn, st) if st else (bm, bn)]
+        HIP.call("kml_gemm_conv_wgrad", "p p p p p i i i i i i i i i i i f i i s", _p(x), _p(dy), _p(dw), _p(slab),
+                 _p(G._zp(x.device)), B, H, W, C, K, KH, KH, sh, sh, pad, pad, 1.0 if accumulate else 0.0, tile,
+                 int(splits), _s())
+        return dw
     x2, dy2, dw2 = x.reshape(P, C), dy.reshape(P, K), dw.view(K, C)
     if route[0] == "blas":
         if accumulate:
@@ -1187,7 +1215,7 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulat
         raise ValueError("wgrad shape mismatch")
     route = None if cfg is not None else wgrad_gemm_route(x.shape, K, KH, KW, stride, pad, dbias)
     if route is not None:
-        return _wgrad_gemm(route, x, dy, dw, accumulate)
+        return _wgrad_gemm(route, x, dy, dw, accumulate, stride)
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
     bm, bn, bk, splits, variant = cfg

@@ -167,6 +167,32 @@ def test_conv_gemm_gather_route_matches_torch(cfg, geom):
     assert torch.allclose(r[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("route", [("gather", 128, 128, 2, 1), ("gather", 128, 128, 2, 5), ("gather", 256, 128, 0, 3),
+                                   ("gather", 128, 256, 0, 2), ("gather", 256, 256, 0, 8)])
+@pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1), (2, 15, 64, 72, 3, 2), (3, 7, 136, 64, 3, 1)])
+def test_conv_wgrad_gemm_gather_route_matches_torch(route, geom, monkeypatch):
+    """Implicit-GEMM weight gradient on the GEMM tiles (kml_gemm_conv_wgrad: im2col(x) gathered per
+    K-tile of output pixels, slab split-K, ordered reduce) vs fp32 torch autograd, store and add."""
+    from kubeml_amd.ops import kernels as K
+    B, H, Ci, Co, k, s = geom
+    p = (k - 1) // 2
+    torch.manual_seed(9)
+    x = _bf(torch.randn(B, H, H, Ci, device=dev))
+    w = _bf(torch.randn(Co, k, k, Ci, device=dev) * 0.05)
+    wr = w.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(x.float().permute(0, 3, 1, 2), wr, stride=s, padding=p)
+    dy = _bf(torch.randn_like(yr))
+    yr.backward(dy.float())
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    monkeypatch.setitem(K._WGRAD_GEMM, (B * H * H, Co, Ci, k, s), route)
+    assert K.wgrad_gemm_route(x.shape, Co, k, k, (s, s), (p, p)) == route
+    dw = torch.full((Co, k, k, Ci), float("nan"), device=dev)
+    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p), accumulate=False)
+    assert _rel(dw.permute(0, 3, 1, 2), wr.grad) < 1e-2
+    K.conv_wgrad(x, dyn, dw, k, k, (s, s), (p, p), accumulate=True)
+    assert _rel(dw.permute(0, 3, 1, 2), 2 * wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
                                  (128, 128, 4, 1, 7)])
 @pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1), (3, 7, 136, 64, 3, 1), (2, 9, 72, 192, 3, 1)])

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--gemm", action="store_true", help="also time the plain MFMA GEMM (ops.gemm) tiles, no stats")
     ap.add_argument("--route", action="store_true", help="time the conv GEMM route (BN stats epilogue) per tile")
     ap.add_argument("--conv3", action="store_true", help="3x3 forward convs: implicit GEMM vs the GEMM gather route")
+    ap.add_argument("--wgrad3", action="store_true", help="3x3 weight gradients: implicit GEMM vs the gather route")
     ap.add_argument("--dgrad", action="store_true", help="time the 1x1 dgrads (consumer-BN epilogue, residual addend "
                                                           "where the model has one) against the plain GEMM")
     args = ap.parse_args()
@@ -50,6 +51,8 @@ def main():
         return dgrad_main(dev)
     if args.conv3:
         return conv3_main(dev)
+    if args.wgrad3:
+        return wgrad3_main(dev)
     for (B, H, C, Co, st) in SHAPES:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
@@ -177,6 +180,32 @@ def conv3_main(dev):
         print(line, flush=True)
         print(f"D3ROUTE dgrad M={B * H * H} N={C} Kd={9 * Co}: {dbest[1]} {dbest[0]:.1f}us (plan {dplan} {td:.1f}us) "
               f"[{fl / dbest[0] / 1e6:.0f} TF/s]", flush=True)
+
+
+def wgrad3_main(dev):
+    for (B, H, C, Co, st) in CONV3:
+        x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+        OH = (H - 1) // st + 1
+        dy = torch.randn(B, OH, OH, Co, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(Co, 3, 3, C, device=dev)
+        S, P = (st, st), (1, 1)
+        t = gtime(lambda: K.conv_wgrad(x, dy, dw, 3, 3, S, P, accumulate=True), reps=20)
+        fl = 2 * B * OH * OH * Co * 9 * C
+        line = f"wgrad3 {H}x{H}/s{st} {C}->{Co}: {t:.1f}us ({fl / t / 1e6:.0f} TF/s)"
+        best = None
+        key = (B * H * H, Co, C, 3, st)
+        for (bm, bn, stg) in [(128, 128, 2), (128, 128, 0), (256, 128, 0), (128, 256, 0)]:
+            for sp in (2, 4, 8, 16, 32):
+                route = ("gather", bm, bn, stg, sp)
+                K._WGRAD_GEMM[key] = route
+                tg = gtime(lambda: K.conv_wgrad(x, dy, dw, 3, 3, S, P, accumulate=True), reps=20)
+                del K._WGRAD_GEMM[key]
+                line += f" {bm}x{bn}s{stg}/{sp}:{tg:.1f}"
+                if best is None or tg < best[0]:
+                    best = (tg, route)
+        print(line, flush=True)
+        print(f"W3ROUTE P={B * H * H} K={Co} C={C} KH=3 S={st}: {list(best[1])} {best[0]:.1f}us (implicit {t:.1f}us) "
+              f"[{fl / best[0] / 1e6:.0f} TF/s]", flush=True)
 
 
 def dgrad_main(dev):
