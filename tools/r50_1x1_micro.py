@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--route", action="store_true", help="time the conv GEMM route (BN stats epilogue) per tile")
     ap.add_argument("--conv3", action="store_true", help="3x3 forward convs: implicit GEMM vs the GEMM gather route")
     ap.add_argument("--wgrad3", action="store_true", help="3x3 weight gradients: implicit GEMM vs the gather route")
+    ap.add_argument("--stem", action="store_true", help="with --wgrad3: the 7x7/s2 stem's weight gradient instead")
     ap.add_argument("--dgrad", action="store_true", help="time the 1x1 dgrads (consumer-BN epilogue, residual addend "
                                                           "where the model has one) against the plain GEMM")
     args = ap.parse_args()
@@ -52,7 +53,7 @@ def main():
     if args.conv3:
         return conv3_main(dev)
     if args.wgrad3:
-        return wgrad3_main(dev)
+        return wgrad3_main(dev, args.stem)
     for (B, H, C, Co, st) in SHAPES:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
@@ -182,29 +183,31 @@ def conv3_main(dev):
               f"[{fl / dbest[0] / 1e6:.0f} TF/s]", flush=True)
 
 
-def wgrad3_main(dev):
-    for (B, H, C, Co, st) in CONV3:
+def wgrad3_main(dev, stem=False):
+    shapes = [(128, 224, 8, 64, 2, 7)] if stem else [c + (3,) for c in CONV3]
+    for (B, H, C, Co, st, kk) in shapes:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
-        OH = (H - 1) // st + 1
+        pd = (kk - 1) // 2
+        OH = (H + 2 * pd - kk) // st + 1
         dy = torch.randn(B, OH, OH, Co, device=dev).to(torch.bfloat16)
-        dw = torch.zeros(Co, 3, 3, C, device=dev)
-        S, P = (st, st), (1, 1)
-        t = gtime(lambda: K.conv_wgrad(x, dy, dw, 3, 3, S, P, accumulate=True), reps=20)
-        fl = 2 * B * OH * OH * Co * 9 * C
+        dw = torch.zeros(Co, kk, kk, C, device=dev)
+        S, P = (st, st), (pd, pd)
+        t = gtime(lambda: K.conv_wgrad(x, dy, dw, kk, kk, S, P, accumulate=True), reps=10)
+        fl = 2 * B * OH * OH * Co * kk * kk * C
         line = f"wgrad3 {H}x{H}/s{st} {C}->{Co}: {t:.1f}us ({fl / t / 1e6:.0f} TF/s)"
         best = None
-        key = (B * H * H, Co, C, 3, st)
+        key = (B * H * H, Co, C, kk, st)
         for (bm, bn, stg) in [(128, 128, 2), (128, 128, 0), (256, 128, 0), (128, 256, 0)]:
-            for sp in (2, 4, 8, 16, 32):
+            for sp in ((16, 32, 64, 128) if stem else (2, 4, 8, 16, 32)):
                 route = ("gather", bm, bn, stg, sp)
                 K._WGRAD_GEMM[key] = route
-                tg = gtime(lambda: K.conv_wgrad(x, dy, dw, 3, 3, S, P, accumulate=True), reps=20)
+                tg = gtime(lambda: K.conv_wgrad(x, dy, dw, kk, kk, S, P, accumulate=True), reps=10)
                 del K._WGRAD_GEMM[key]
                 line += f" {bm}x{bn}s{stg}/{sp}:{tg:.1f}"
                 if best is None or tg < best[0]:
                     best = (tg, route)
         print(line, flush=True)
-        print(f"W3ROUTE P={B * H * H} K={Co} C={C} KH=3 S={st}: {list(best[1])} {best[0]:.1f}us (implicit {t:.1f}us) "
+        print(f"W3ROUTE P={B * H * H} K={Co} C={C} KH={kk} S={st}: {list(best[1])} {best[0]:.1f}us (implicit {t:.1f}us) "
               f"[{fl / best[0] / 1e6:.0f} TF/s]", flush=True)
 
 
@@ -213,7 +216,7 @@ def dgrad_main(dev):
     for (B, H, C, Co, st) in SHAPES:
         if st != 1:
             continue
-        for addend in (False, True):
+        for addend in (False, True, None):   # None: plain dgrad (no consumer BN, no addend)
             dy = torch.randn(B, H, H, Co, device=dev).to(torch.bfloat16)
             w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
             xs = (B, H, H, C)
@@ -222,11 +225,12 @@ def dgrad_main(dev):
             mean = torch.zeros(C, device=dev)
             rstd = torch.ones(C, device=dev)
             add = torch.randn(xs, device=dev).to(torch.bfloat16) if addend else None
+            bnfa = None if addend is None else (yb, cb, mean, rstd)
             out = torch.empty(xs, dtype=torch.bfloat16, device=dev)
             M = B * H * H
             plan = K.plan_conv("dgrad", M, C, Co)
             t = gtime(lambda: K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), out=out, addend=add,
-                                           bnf=(yb, cb, mean, rstd), bnf_mask=True), reps=20)
+                                           bnf=bnfa, bnf_mask=True), reps=20)
             byts = (dy.numel() + 3 * out.numel() + (out.numel() if addend else 0)) * 2
             fl = 2 * M * Co * C
             line = (f"dgrad 1x1 {H}x{H} {Co}->{C} M={M} addend={addend} plan={plan}: {t:.1f}us "
@@ -237,7 +241,7 @@ def dgrad_main(dev):
                     continue
                 cfg = (bm, bn, tc, 1, K.GEMM1X1)
                 tg = gtime(lambda: K.conv_dgrad(dy, w, xs, 1, 1, (1, 1), (0, 0), out=out, addend=add, cfg=cfg,
-                                                bnf=(yb, cb, mean, rstd), bnf_mask=True), reps=20)
+                                                bnf=bnfa, bnf_mask=True), reps=20)
                 line += f"  route{cfg[:3]}: {tg:.1f}"
                 if best is None or tg < best[0]:
                     best = (tg, cfg)
