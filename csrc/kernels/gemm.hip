@@ -523,6 +523,88 @@ __device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&a
   }
 }
 
+// GEMM_BNF epilogue through LDS rows (128 x 128 tiles): the fp32 tile is staged in LDS (16-byte
+// chunks XOR-swizzled by row), then every thread owns one 8-column chunk and walks rows with 16-byte
+// loads of the addend / mask / BN input and 16-byte stores — full cache lines instead of the register
+// epilogue's 16 rows x 32 B per wave instruction.  v = acc + addend is rounded once, as in the
+// register path; the partial rows are summed in a fixed order (deterministic).
+template <int BM, int BN, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_bnf_rowpass(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                                 int wn, int lane, int tid, char* smem) {
+  constexpr int CPR = BN / 8, RSTEP = NT / CPR;
+  float* sF = reinterpret_cast<float*>(smem);
+  __syncthreads();  // every wave is done with the operand stages
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int row = wm * WM + i * 16 + (lane & 15), ch = (wn * WN + j * 16) / 4 + (lane >> 4);
+      const f32x4_t a = acc[i][j];
+      *reinterpret_cast<float4*>(sF + row * BN + ((ch ^ (row & 15)) << 2)) = make_float4(a[0], a[1], a[2], a[3]);
+    }
+  __syncthreads();
+  const int q = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + q * 8;
+  const bool nok = n < g.N, bnf = g.bc != nullptr;
+  float mu[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { mu[k] = 0.f; rs[k] = 0.f; s1[k] = 0.f; s2[k] = 0.f; }
+  if (bnf && nok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { mu[k] = g.bmean[n + k]; rs[k] = g.brstd[n + k]; }
+  }
+  for (int r = r0; r < BM; r += RSTEP) {
+    const int m = m0 + r;
+    if (m >= g.M || !nok) continue;
+    const int c0 = 2 * q, c1 = 2 * q + 1;
+    const float4 p0 = *reinterpret_cast<const float4*>(sF + r * BN + ((c0 ^ (r & 15)) << 2));
+    const float4 p1 = *reinterpret_cast<const float4*>(sF + r * BN + ((c1 ^ (r & 15)) << 2));
+    float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    const long long off = (long long)m * g.ldc + n;
+    if (g.c2) {
+      const uint4 ad = *reinterpret_cast<const uint4*>(g.c2 + off);
+      const unsigned aw[4] = {ad.x, ad.y, ad.z, ad.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[2 * k] += lo_bf(aw[k]); v[2 * k + 1] += hi_bf(aw[k]); }
+    }
+    unsigned ow[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ow[k] = pack_bf2(v[2 * k], v[2 * k + 1]);
+    if (bnf) {
+      const uint4 cv = *reinterpret_cast<const uint4*>(g.bc + off);
+      const uint4 yv = g.by ? *reinterpret_cast<const uint4*>(g.by + off) : make_uint4(0, 0, 0, 0);
+      const unsigned cw[4] = {cv.x, cv.y, cv.z, cv.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float dz0 = lo_bf(ow[k]), dz1 = hi_bf(ow[k]);
+        if (g.by) {
+          const bool k0 = lo_bf(yw[k]) > 0.f, k1 = hi_bf(yw[k]) > 0.f;
+          if (!k0) dz0 = 0.f;
+          if (!k1) dz1 = 0.f;
+          if (g.mask_out) ow[k] &= (k0 ? 0x0000ffffu : 0u) | (k1 ? 0xffff0000u : 0u);
+        }
+        s1[2 * k] += dz0; s2[2 * k] += dz0 * ((lo_bf(cw[k]) - mu[2 * k]) * rs[2 * k]);
+        s1[2 * k + 1] += dz1; s2[2 * k + 1] += dz1 * ((hi_bf(cw[k]) - mu[2 * k + 1]) * rs[2 * k + 1]);
+      }
+    }
+    *reinterpret_cast<uint4*>(static_cast<bf16_t*>(g.c) + off) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+  if (!bnf) return;
+  __syncthreads();  // staging reads done: the area is reused as [NT][16] partial sums
+  float* red = sF;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = s1[k]; red[tid * 16 + 8 + k] = s2[k]; }
+  __syncthreads();
+  for (int t = tid; t < 2 * BN; t += NT) {
+    const int half = t / BN, cl = t - half * BN, nn = n0 + cl;
+    if (nn >= g.N) continue;
+    const int qq = cl >> 3, k = (cl & 7) + 8 * half;
+    float sum = 0.f;
+    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
+    g.colpart[(long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn] = sum;
+  }
+}
+
 // OUT: 0 bf16 (bias, act, optional pre-act copy), 1 fp32 beta, 2 fp32 atomic add (split-K)
 // S: LDS stages.  S = 2: the DMA of tile t+1 overlaps tile t's MFMAs, vmcnt(0) per step.
 // S = 3: tiles t+1 and t+2 in flight; each step waits with a COUNTED vmcnt for tile t only,
@@ -625,7 +707,11 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
 
   if constexpr (OUT == 0) {
     if (g.act == GEMM_BNF) {
-      gemm_bnf_epilogue<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
+      if constexpr (BM == 128 && BN == 128 && S * STAGE >= BM * BN * 4) {
+        gemm_bnf_rowpass<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tid, smem);
+      } else {
+        gemm_bnf_epilogue<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
+      }
       return;
     }
   }
