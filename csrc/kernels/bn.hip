@@ -838,9 +838,14 @@ static int env_vmin(const char* name) {
 }
 static int vmin_fwd() { static const int v = env_vmin("KUBEML_BN_VMIN_FWD"); return v; }
 static int vmin_bwd() { static const int v = env_vmin("KUBEML_BN_VMIN_BWD"); return v < 4 ? v : 4; }
+static int grid_cap() {  // blocks of the vectorised BN kernels (KUBEML_BN_GRID_CAP: tuning experiments)
+  static const int v = [] { const char* e = getenv("KUBEML_BN_GRID_CAP"); const int r = e ? atoi(e) : 0;
+                            return r >= 256 ? r : 1024; }();
+  return v;
+}
 static unsigned v_grid(long long n8, int V) {
   long long g = (n8 + (long long)TPB * V - 1) / ((long long)TPB * V);
-  if (g > 1024) g = 1024;
+  if (g > grid_cap()) g = grid_cap();
   return (unsigned)(g < 1 ? 1 : g);
 }
 

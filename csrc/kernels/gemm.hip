@@ -78,7 +78,14 @@ struct GemmArgs {
   // output pixel m = (b, oh, ow), K index k = tap * C + c (C % 64 == 0: a K-tile sits in one tap)
   int cH, cW, cC, cOH, cOW, cKW, csh, csw, cph, cpw;
   int cK;              // implicit-GEMM dgrad (AG = 2): output channels of dy (K % 64 == 0)
+  int rowpass;         // bf16 output of a 128 x 128 tile through LDS rows (gemm_out_rowpass)
 };
+
+// the conv routes' forward GEMMs store through LDS rows with KUBEML_GEMM_OUT_ROWPASS=1
+static int out_rowpass_default() {
+  static const int v = [] { const char* e = getenv("KUBEML_GEMM_OUT_ROWPASS"); return (e && e[0] == '1') ? 1 : 0; }();
+  return v;
+}
 
 constexpr int BK = 64;
 constexpr int NT = 512;
@@ -605,6 +612,67 @@ __device__ __forceinline__ void gemm_bnf_rowpass(const GemmArgs& g, f32x4_t (&ac
   }
 }
 
+// bf16 output of a 128 x 128 k_gemm tile through LDS rows (act 0 or GEMM_STATS, no c2): fp32 tile
+// (+ bias) staged as in gemm_bnf_rowpass, then 16-byte row-contiguous stores; with GEMM_STATS every
+// thread sums its 8 columns' bf16 outputs over its rows and the 32 partials per chunk are added in a
+// fixed order into the tile's [sum | sumsq] row.
+template <int BM, int BN, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_out_rowpass(const GemmArgs& g, f32x4_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                                 int wn, int lane, int tid, char* smem) {
+  constexpr int CPR = BN / 8, RSTEP = NT / CPR;
+  float* sF = reinterpret_cast<float*>(smem);
+  __syncthreads();  // every wave is done with the operand stages
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int col = wn * WN + j * 16 + 4 * (lane >> 4), n = n0 + col;
+    const float4 bb = (g.bias && n < g.N) ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int row = wm * WM + i * 16 + (lane & 15), ch = col / 4;
+      const f32x4_t a = acc[i][j];
+      *reinterpret_cast<float4*>(sF + row * BN + ((ch ^ (row & 15)) << 2)) =
+          make_float4(a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w);
+    }
+  }
+  __syncthreads();
+  const int q = tid % CPR, r0 = tid / CPR;
+  const int n = n0 + q * 8;
+  const bool nok = n < g.N, st = g.act == GEMM_STATS;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  for (int r = r0; r < BM; r += RSTEP) {
+    const int m = m0 + r;
+    if (m >= g.M || !nok) continue;
+    const float4 p0 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q) ^ (r & 15)) << 2));
+    const float4 p1 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + 1) ^ (r & 15)) << 2));
+    const unsigned ow[4] = {pack_bf2(p0.x, p0.y), pack_bf2(p0.z, p0.w), pack_bf2(p1.x, p1.y), pack_bf2(p1.z, p1.w)};
+    if (st) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x0 = lo_bf(ow[k]), x1 = hi_bf(ow[k]);
+        s1[2 * k] += x0; s2[2 * k] += x0 * x0;
+        s1[2 * k + 1] += x1; s2[2 * k + 1] += x1 * x1;
+      }
+    }
+    *reinterpret_cast<uint4*>(static_cast<bf16_t*>(g.c) + (long long)m * g.ldc + n) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+  }
+  if (!st) return;
+  __syncthreads();
+  float* red = sF;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = s1[k]; red[tid * 16 + 8 + k] = s2[k]; }
+  __syncthreads();
+  for (int t = tid; t < 2 * BN; t += NT) {
+    const int half = t / BN, cl = t - half * BN, nn = n0 + cl;
+    if (nn >= g.N) continue;
+    const int qq = cl >> 3, k = (cl & 7) + 8 * half;
+    float sum = 0.f;
+    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
+    g.colpart[(long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn] = sum;
+  }
+}
+
 // OUT: 0 bf16 (bias, act, optional pre-act copy), 1 fp32 beta, 2 fp32 atomic add (split-K)
 // S: LDS stages.  S = 2: the DMA of tile t+1 overlaps tile t's MFMAs, vmcnt(0) per step.
 // S = 3: tiles t+1 and t+2 in flight; each step waits with a COUNTED vmcnt for tile t only,
@@ -712,6 +780,12 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
       } else {
         gemm_bnf_epilogue<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
       }
+      return;
+    }
+  }
+  if constexpr (OUT == 0 && BM == 128 && BN == 128 && S * STAGE >= BM * BN * 4) {
+    if (g.rowpass && (g.act == 0 || g.act == GEMM_STATS) && !g.c2 && g.N % 8 == 0 && g.ldc % 8 == 0) {
+      gemm_out_rowpass<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tid, smem);
       return;
     }
   }
@@ -1269,7 +1343,7 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
   if (M <= 0 || N <= 0) return 0;
   if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
@@ -1296,8 +1370,9 @@ KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const
   g.lda = C; g.ldb = (long long)KH * KW * C; g.ldc = K;
   g.M = B * OH * OW; g.N = K; g.K = KH * KW * C; g.act = rows ? GEMM_STATS : 0; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
+  g.rowpass = out_rowpass_default();
   switch (tile) {
     case 0: return launch<256, 256, true, true, 0, 2, 1>(g, 1, s);
     case 1: return launch<256, 128, true, true, 0, 3, 1>(g, 1, s);
@@ -1325,7 +1400,7 @@ KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, c
   g.lda = K; g.ldb = (long long)KH * KW * C; g.ldc = C;
   g.M = B * H * W; g.N = C; g.K = KH * KW * K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = 1; g.csw = 1; g.cph = ph; g.cpw = pw;
   g.cK = K;
   switch (tile) {
@@ -1352,7 +1427,7 @@ KML_API int kml_gemm_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, fl
   g.a = dy; g.b = x; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = K; g.ldb = 0; g.ldc = (long long)KH * KW * C;
   g.M = K; g.N = KH * KW * C; g.K = B * OH * OW; g.act = 0; g.beta = 0.f; g.kchunk = g.K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
   g.cK = K;
   splits = splits < 1 ? 1 : splits;
@@ -1386,6 +1461,7 @@ KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_STATS; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
   g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.rowpass = out_rowpass_default();
   return by_tile<true, true, 0>(g, tile, 1, s);
 }
 
@@ -1403,7 +1479,7 @@ KML_API int kml_gemm_dgrad_bnf(const bf16_t* a, long long lda, const bf16_t* b, 
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(addend); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0;
   return by_tile<true, false, 0>(g, tile, 1, s);
 }
 
@@ -1419,7 +1495,7 @@ KML_API int kml_gemm_dgrad_gelu(const bf16_t* a, long long lda, const bf16_t* b,
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(pre); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_GELU_BWD; g.beta = 0.f; g.kchunk = K; g.colpart = colpart;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
   return launch8<true, false, 0>(g, 1, s);
 }
 
@@ -1435,7 +1511,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
   splits = splits < 1 ? 1 : splits;
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;
