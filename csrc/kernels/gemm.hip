@@ -81,9 +81,10 @@ struct GemmArgs {
   int rowpass;         // bf16 output of a 128 x 128 tile through LDS rows (gemm_out_rowpass)
 };
 
-// the conv routes' forward GEMMs store through LDS rows with KUBEML_GEMM_OUT_ROWPASS=1
+// the conv routes' forward GEMMs store through LDS rows unless KUBEML_GEMM_OUT_ROWPASS=0 (A/B:
+// ResNet-50 15.82 -> 15.63 ms/step, profiles/r5/r50/r50_ab_out_rowpass.txt)
 static int out_rowpass_default() {
-  static const int v = [] { const char* e = getenv("KUBEML_GEMM_OUT_ROWPASS"); return (e && e[0] == '1') ? 1 : 0; }();
+  static const int v = [] { const char* e = getenv("KUBEML_GEMM_OUT_ROWPASS"); return (e && e[0] == '0') ? 0 : 1; }();
   return v;
 }
 
