@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--conv3", action="store_true", help="3x3 forward convs: implicit GEMM vs the GEMM gather route")
     ap.add_argument("--wgrad3", action="store_true", help="3x3 weight gradients: implicit GEMM vs the gather route")
     ap.add_argument("--stem", action="store_true", help="with --wgrad3: the 7x7/s2 stem's weight gradient instead")
+    ap.add_argument("--vgg", action="store_true", help="with --conv3 / --wgrad3: VGG-16 (CIFAR) 3x3 shapes")
     ap.add_argument("--dgrad", action="store_true", help="time the 1x1 dgrads (consumer-BN epilogue, residual addend "
                                                           "where the model has one) against the plain GEMM")
     args = ap.parse_args()
@@ -51,9 +52,9 @@ def main():
     if args.dgrad:
         return dgrad_main(dev)
     if args.conv3:
-        return conv3_main(dev)
+        return conv3_main(dev, args.vgg)
     if args.wgrad3:
-        return wgrad3_main(dev, args.stem)
+        return wgrad3_main(dev, args.stem, args.vgg)
     for (B, H, C, Co, st) in SHAPES:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 1, 1, C, device=dev) * 0.05).to(torch.bfloat16)
@@ -127,8 +128,13 @@ CONV3 = [  # B, H, C, K, stride: the 3x3 convs of ResNet-50 at 224^2
     (128, 14, 256, 256, 1), (128, 14, 512, 512, 2), (128, 7, 512, 512, 1)]
 
 
-def conv3_main(dev):
-    for (B, H, C, Co, st) in CONV3:
+VGG3 = [  # B, H, C, K, stride: VGG-16 (CIFAR, batch 128) 3x3 convs with C % 64 == 0
+    (128, 32, 64, 64, 1), (128, 16, 64, 128, 1), (128, 16, 128, 128, 1), (128, 8, 128, 256, 1),
+    (128, 8, 256, 256, 1), (128, 4, 256, 512, 1), (128, 4, 512, 512, 1)]
+
+
+def conv3_main(dev, vgg=False):
+    for (B, H, C, Co, st) in (VGG3 if vgg else CONV3):
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 3, 3, C, device=dev) * 0.02).to(torch.bfloat16)
         S, P = (st, st), (1, 1)
@@ -183,8 +189,8 @@ def conv3_main(dev):
               f"[{fl / dbest[0] / 1e6:.0f} TF/s]", flush=True)
 
 
-def wgrad3_main(dev, stem=False):
-    shapes = [(128, 224, 8, 64, 2, 7)] if stem else [c + (3,) for c in CONV3]
+def wgrad3_main(dev, stem=False, vgg=False):
+    shapes = [(128, 224, 8, 64, 2, 7)] if stem else [c + (3,) for c in (VGG3 if vgg else CONV3)]
     for (B, H, C, Co, st, kk) in shapes:
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         pd = (kk - 1) // 2
@@ -198,7 +204,7 @@ def wgrad3_main(dev, stem=False):
         best = None
         key = (B * H * H, Co, C, kk, st)
         for (bm, bn, stg) in [(128, 128, 2), (128, 128, 0), (256, 128, 0), (128, 256, 0)]:
-            for sp in ((16, 32, 64, 128) if stem else (2, 4, 8, 16, 32)):
+            for sp in ((128, 256, 512) if stem else (2, 4, 8, 16, 32)):
                 route = ("gather", bm, bn, stg, sp)
                 K._WGRAD_GEMM[key] = route
                 tg = gtime(lambda: K.conv_wgrad(x, dy, dw, kk, kk, S, P, accumulate=True), reps=10)
