@@ -39,4 +39,34 @@ def test_wgrad_gemm_route_only_for_plain_1x1():
     assert K.wgrad_gemm_route(shape, e["K"], 1, 1, (1, 1), (0, 0), dbias=object()) is None
     assert K.wgrad_gemm_route((B, hw, hw, e["C"] + 8), e["K"], 1, 1, (1, 1), (0, 0)) is None
     for r in d["entries"]:
-        assert r["route"][0] in ("blas", "slab")
+        if r.get("KH", 1) == 1:
+            assert r["route"][0] in ("blas", "slab")
+        else:   # implicit-GEMM weight gradients on the GEMM tiles: only their exact geometry
+            assert r["route"][0] == "gather"
+            kh, st = r["KH"], r["S"]
+            hw2 = int(round((r["P"] // B) ** 0.5))
+            xs = (B, hw2, hw2, r["C"])
+            p = (kh - 1) // 2
+            assert K.wgrad_gemm_route(xs, r["K"], kh, kh, (st, st), (p, p)) == tuple(r["route"])
+            assert K.wgrad_gemm_route(xs, r["K"], kh, kh, (st, st), (0, 0)) is None          # other padding
+            assert K.wgrad_gemm_route(xs, r["K"], kh, kh, (3 - st, 3 - st), (p, p)) is None  # other stride
+            assert K.wgrad_gemm_route(xs, r["K"], 1, 1, (1, 1), (0, 0)) is None              # other kernel
+
+
+def test_conv_gemm_route_plans_only_for_eligible_geometry():
+    """conv_tuning.json entries with variant GEMM1X1 (the conv GEMM routes) are planned only for
+    geometries the route runs: a plain GEMM for 1x1 / stride 1, an implicit GEMM (C % 64) otherwise;
+    any other conv with the same GEMM dimensions falls back to an implicit-GEMM tile."""
+    d = json.load(open(os.path.join(OPS, "conv_tuning.json")))
+    routed = [e for e in d["entries"] if e["mode"] == "fwd" and len(e["cfg"]) == 5 and e["cfg"][4] == K.GEMM1X1]
+    assert routed
+    for e in routed:
+        M, N, Kd = e["M"], e["N"], e["Kd"]
+        if Kd % 64 == 0 and Kd // 9 % 64 == 0 and Kd % 9 == 0:     # a 3x3 conv over C = Kd / 9
+            C, geom = Kd // 9, (14, 14, 3, 3, (1, 1), (1, 1))
+        else:
+            C, geom = Kd, (7, 7, 1, 1, (1, 1), (0, 0))
+        assert K.conv_fwd_plan(C, M, N, Kd, geom=geom)[4] == K.GEMM1X1
+        # C not a multiple of 64 and not a 1x1 conv: never the GEMM route
+        assert K.conv_fwd_plan(C + 8, M, N, Kd, cfg=tuple(e["cfg"]),
+                               geom=(14, 14, 3, 3, (1, 1), (1, 1)))[4] != K.GEMM1X1
