@@ -1344,7 +1344,10 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   g.a = a; g.b = b; g.c = c; g.c2 = c2; g.bias = bias; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = act; g.beta = beta; g.kchunk = K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
+  // the linear-layer GEMMs keep the register epilogue: BERT's QKV forward on the 128 x 128 row-pass
+  // tile beat hipBLASLt alone (71 vs 88 us) but not inside the step (profiles/r5/bert_qkv_rowpass.md)
+  g.rowpass = 0;
   if (M <= 0 || N <= 0) return 0;
   if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
