@@ -79,6 +79,12 @@ struct GemmArgs {
   int cH, cW, cC, cOH, cOW, cKW, csh, csw, cph, cpw;
   int cK;              // implicit-GEMM dgrad (AG = 2): output channels of dy (K % 64 == 0)
   int rowpass;         // bf16 output of a 128 x 128 tile through LDS rows (gemm_out_rowpass)
+  // group reduction of the row-pass partial rows (GEMM_STATS / GEMM_BNF): every grp_tiles consecutive
+  // M-tiles form a group whose last-arriving block (agent-scope ticket per (group, n-tile)) sums the
+  // group's rows in order into grp_out[g][2N] — the BN kernel then reads <= 16 rows, no fold launch
+  float* grp_out;
+  unsigned* grp_cnt;
+  int grp_tiles;
 };
 
 // the conv routes' forward GEMMs store through LDS rows unless KUBEML_GEMM_OUT_ROWPASS=0 (A/B:
@@ -531,6 +537,49 @@ __device__ __forceinline__ void gemm_bnf_epilogue(const GemmArgs& g, f32x4_t (&a
   }
 }
 
+// Partial-row store of a row-pass epilogue: write-through at agent scope when a group reduction in
+// this launch reads it (the conv kernels' store_row / group_reduce_rows protocol: no fences; every
+// storing wave drains before the ticket; the last arriver reads past its L1 with agent-scope loads).
+__device__ __forceinline__ void gemm_store_row(float* p, float v, bool grp) {
+  if (grp) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void gemm_group_rows(const GemmArgs& g, int m0, int n0, int tid, unsigned* flag) {
+  const int tile_m = m0 / BM, tile_n = n0 / BN;
+  const int ntn = (g.N + BN - 1) / BN, ntm = (g.M + BM - 1) / BM;
+  const int grp = tile_m / g.grp_tiles;
+  const int t0 = grp * g.grp_tiles, t1 = min(ntm, t0 + g.grp_tiles);
+  unsigned* cnt = g.grp_cnt + grp * ntn + tile_n;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its rows
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = (t == (unsigned)(t1 - t0 - 1)) ? 1u : 0u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  for (int q = tid; q < 2 * BN; q += NT) {
+    const int half = q / BN, col = n0 + (q - half * BN);
+    if (col >= g.N) continue;
+    const float* src = g.colpart + (long long)half * g.N + col;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = t0;
+    for (; r + 4 <= t1; r += 4) {  // 4 loads in flight, fixed summation order
+      a0 += __hip_atomic_load(const_cast<float*>(src + (long long)r * 2 * g.N), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a1 += __hip_atomic_load(const_cast<float*>(src + (long long)(r + 1) * 2 * g.N), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a2 += __hip_atomic_load(const_cast<float*>(src + (long long)(r + 2) * 2 * g.N), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a3 += __hip_atomic_load(const_cast<float*>(src + (long long)(r + 3) * 2 * g.N), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (; r < t1; ++r)
+      a0 += __hip_atomic_load(const_cast<float*>(src + (long long)r * 2 * g.N), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g.grp_out[(long long)grp * 2 * g.N + (long long)half * g.N + col] = (a0 + a1) + (a2 + a3);
+  }
+}
+
 // GEMM_BNF epilogue through LDS rows (128 x 128 tiles): the fp32 tile is staged in LDS (16-byte
 // chunks XOR-swizzled by row), then every thread owns one 8-column chunk and walks rows with 16-byte
 // loads of the addend / mask / BN input and 16-byte stores — full cache lines instead of the register
@@ -609,7 +658,11 @@ __device__ __forceinline__ void gemm_bnf_rowpass(const GemmArgs& g, f32x4_t (&ac
     const int qq = cl >> 3, k = (cl & 7) + 8 * half;
     float sum = 0.f;
     for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
-    g.colpart[(long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn] = sum;
+    gemm_store_row(g.colpart + (long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn, sum, g.grp_out != nullptr);
+  }
+  if (g.grp_out) {
+    __syncthreads();  // red reads done: smem word 0 becomes the ticket flag
+    gemm_group_rows<BM, BN>(g, m0, n0, tid, reinterpret_cast<unsigned*>(smem));
   }
 }
 
@@ -670,7 +723,11 @@ __device__ __forceinline__ void gemm_out_rowpass(const GemmArgs& g, f32x4_t (&ac
     const int qq = cl >> 3, k = (cl & 7) + 8 * half;
     float sum = 0.f;
     for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
-    g.colpart[(long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn] = sum;
+    gemm_store_row(g.colpart + (long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn, sum, g.grp_out != nullptr);
+  }
+  if (g.grp_out) {
+    __syncthreads();  // red reads done: smem word 0 becomes the ticket flag
+    gemm_group_rows<BM, BN>(g, m0, n0, tid, reinterpret_cast<unsigned*>(smem));
   }
 }
 
@@ -1347,7 +1404,7 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   // the linear-layer GEMMs keep the register epilogue: BERT's QKV forward on the 128 x 128 row-pass
   // tile beat hipBLASLt alone (71 vs 88 us) but not inside the step (profiles/r5/bert_qkv_rowpass.md)
-  g.rowpass = 0;
+  g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   if (M <= 0 || N <= 0) return 0;
   if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
@@ -1365,7 +1422,8 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
 // (C % 64 == 0).  rows: the GEMM_STATS partial rows [M / BM][2 N] or null (plain bf16 output + bias).
 KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const float* bias, float* rows,
                               const bf16_t* zp, int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw,
-                              int ph, int pw, int tile, hipStream_t s) {
+                              int ph, int pw, int tile, float* grp_out, unsigned* grp_cnt, int grp_tiles,
+                              hipStream_t s) {
   if (C % 64 || K % 8 || tile < 0 || tile > 4 || KH < 1 || KW < 1 || sh < 1 || sw < 1) return (int)hipErrorInvalidValue;
   const int OH = (H + 2 * ph - KH) / sh + 1, OW = (W + 2 * pw - KW) / sw + 1;
   if (OH <= 0 || OW <= 0) return 0;
@@ -1374,9 +1432,13 @@ KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const
   g.lda = C; g.ldb = (long long)KH * KW * C; g.ldc = K;
   g.M = B * OH * OW; g.N = K; g.K = KH * KW * C; g.act = rows ? GEMM_STATS : 0; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
-  g.rowpass = out_rowpass_default();
+  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
+  if (grp_out) {
+    if (!rows || !grp_cnt || grp_tiles < 1 || !g.rowpass || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
+    g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
+  }
   switch (tile) {
     case 0: return launch<256, 256, true, true, 0, 2, 1>(g, 1, s);
     case 1: return launch<256, 128, true, true, 0, 3, 1>(g, 1, s);
@@ -1394,7 +1456,7 @@ KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const
 KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const bf16_t* addend, const bf16_t* y,
                                 const bf16_t* cin, const float* mean, const float* rstd, float* rows, int mask_out,
                                 const bf16_t* zp, int B, int H, int W, int C, int K, int KH, int KW, int ph, int pw,
-                                int tile, hipStream_t s) {
+                                int tile, float* grp_out, unsigned* grp_cnt, int grp_tiles, hipStream_t s) {
   if (K % 64 || C % 8 || tile < 0 || tile > 4 || KH < 1 || KW < 1) return (int)hipErrorInvalidValue;
   if (cin && (!mean || !rstd || !rows)) return (int)hipErrorInvalidValue;
   const int OH = H + 2 * ph - KH + 1, OW = W + 2 * pw - KW + 1;
@@ -1404,9 +1466,13 @@ KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, c
   g.lda = K; g.ldb = (long long)KH * KW * C; g.ldc = C;
   g.M = B * H * W; g.N = C; g.K = KH * KW * K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = 1; g.csw = 1; g.cph = ph; g.cpw = pw;
   g.cK = K;
+  if (grp_out) {
+    if (!cin || !grp_cnt || grp_tiles < 1 || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
+    g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
+  }
   switch (tile) {
     case 0: return launch<256, 256, true, false, 0, 2, 2>(g, 1, s);
     case 1: return launch<256, 128, true, false, 0, 3, 2>(g, 1, s);
@@ -1431,7 +1497,7 @@ KML_API int kml_gemm_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, fl
   g.a = dy; g.b = x; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = K; g.ldb = 0; g.ldc = (long long)KH * KW * C;
   g.M = K; g.N = KH * KW * C; g.K = B * OH * OW; g.act = 0; g.beta = 0.f; g.kchunk = g.K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
   g.cK = K;
   splits = splits < 1 ? 1 : splits;
@@ -1456,7 +1522,7 @@ KML_API int kml_gemm_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, fl
 // (tiles 0, 1, 6) or 128 (tiles 2, 3, 4).  The GEMM route of a 1x1 / stride-1 convolution.
 KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, bf16_t* c, long long ldc,
                            const float* bias, float* rows, const bf16_t* zp, int M, int N, int K, int tile,
-                           hipStream_t s) {
+                           float* grp_out, unsigned* grp_cnt, int grp_tiles, hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (!rows || N % 8 || ldc % 8 || lda % 8 || ldb % 8 || K % 8) return (int)hipErrorInvalidValue;
   if (tile == 5 || tile == 7 || tile < 0 || tile > 7) return (int)hipErrorInvalidValue;
@@ -1465,7 +1531,11 @@ KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_STATS; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
   g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
-  g.rowpass = out_rowpass_default();
+  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
+  if (grp_out) {  // group reduction: row-pass tiles only
+    if (!grp_cnt || grp_tiles < 1 || !g.rowpass || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
+    g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
+  }
   return by_tile<true, true, 0>(g, tile, 1, s);
 }
 
@@ -1475,7 +1545,8 @@ KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long
 KML_API int kml_gemm_dgrad_bnf(const bf16_t* a, long long lda, const bf16_t* b, long long ldb, bf16_t* c,
                                long long ldc, const bf16_t* addend, const bf16_t* y, const bf16_t* cin,
                                const float* mean, const float* rstd, float* rows, int mask_out, const bf16_t* zp,
-                               int M, int N, int K, int tile, hipStream_t s) {
+                               int M, int N, int K, int tile, float* grp_out, unsigned* grp_cnt, int grp_tiles,
+                               hipStream_t s) {
   if (M <= 0 || N <= 0) return 0;
   if (N % 8 || ldc % 8 || lda % 8 || ldb % 8 || K % 8 || tile < 0 || tile > 4) return (int)hipErrorInvalidValue;
   if (cin && (!mean || !rstd || !rows)) return (int)hipErrorInvalidValue;
@@ -1483,7 +1554,11 @@ KML_API int kml_gemm_dgrad_bnf(const bf16_t* a, long long lda, const bf16_t* b, 
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(addend); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0;
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
+  if (grp_out) {  // the BNF row pass runs on the 128 x 128 tiles
+    if (!cin || !grp_cnt || grp_tiles < 1 || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
+    g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
+  }
   return by_tile<true, false, 0>(g, tile, 1, s);
 }
 
@@ -1499,7 +1574,7 @@ KML_API int kml_gemm_dgrad_gelu(const bf16_t* a, long long lda, const bf16_t* b,
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(pre); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_GELU_BWD; g.beta = 0.f; g.kchunk = K; g.colpart = colpart;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   return launch8<true, false, 0>(g, 1, s);
 }
 
@@ -1515,7 +1590,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0;
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   splits = splits < 1 ? 1 : splits;
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;

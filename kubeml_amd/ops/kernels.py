@@ -182,10 +182,25 @@ _GRP_MIN = 0
 _GRP_ROWS = 16
 
 
+def _gemm_grouped(cfg) -> bool:
+    """Does this plan's producer group-reduce its partial rows (the conv GEMM route on the 128x128
+    row-pass tiles: the last block of every group of M-tiles sums the group's rows, so the BN kernel
+    reads <= _GRP_ROWS rows and no k_rows_fold launch runs)?"""
+    c = tuple(cfg) + (0,) * (5 - len(cfg))
+    return _GEMM_GROUP and c[4] == GEMM1X1 and c[2] in (3, 4)
+
+
+# KUBEML_GEMM_GROUP_ROWS=1: group-reduce the GEMM route's rows in the producer; off: one row per M-tile
+# (folded by k_rows_fold).  The forward statistics rows need the row-pass epilogue
+# (KUBEML_GEMM_OUT_ROWPASS, on by default)
+_GEMM_GROUP = os.environ.get("KUBEML_GEMM_GROUP_ROWS", "0") == "1" and os.environ.get("KUBEML_GEMM_OUT_ROWPASS", "1") != "0"
+
+
 def _stats_layout(M, cfg, group=False):
     """(per-wave rows G, M-tiles per group or 0, rows the consumer reads).  group: reduce
     to at most _GRP_ROWS rows regardless of _GRP_MIN (a consumer whose every block reads all
     rows, e.g. the BN-folding halo conv)."""
+    group = group or _gemm_grouped(cfg)
     bm = _norm_cfg(cfg)[0]
     tiles = _cdiv(M, bm)
     # one row per M tile (the epilogue sums the tile's wave row-bands; tail tiles included)
@@ -373,24 +388,26 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
                  int(_fold), int(_g22), _s())
         return out
     if variant == GEMM1X1:
-        if relu or _fold or _g22 or grp is not None or (stats is not None and not stats_part) or \
+        gemm_grp = _gemm_grouped((bm, bn, bk, splits, variant))
+        if relu or _fold or _g22 or (grp is not None and not gemm_grp) or (stats is not None and not stats_part) or \
                 not x.is_contiguous() or not out.is_contiguous():
-            # same bm, so the statistics rows the caller sized stay valid
+            # same bm (and the same row grouping), so the statistics rows the caller sized stay valid
             return conv_fwd(x, w, KH, KW, stride, pad, bias=bias, stats=stats, relu=relu, out=out,
                             cfg=_GEMM1X1_FALLBACK[bm], stats_part=stats_part, _fold=_fold, _g22=_g22,
-                            stats_group=stats_group)
+                            stats_group=stats_group or gemm_grp)
         from . import gemm as G
         zp = G._zp(x.device)
         if not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad):   # implicit GEMM: A gathered per K-tile
-            HIP.call("kml_gemm_conv_fwd", "p p p p p p i i i i i i i i i i i i s", _p(x), _p(w), _p(out), _p(bias),
-                     _p(rows), _p(zp), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, _s())
+            HIP.call("kml_gemm_conv_fwd", "p p p p p p i i i i i i i i i i i i p p i s", _p(x), _p(w), _p(out),
+                     _p(bias), _p(rows), _p(zp), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bk, _p(grp), _p(gcnt), tpg,
+                     _s())
             return out
         if stats is None:
             HIP.call("kml_gemm", "p l p l p l p p p i i i i i i f i i s", _p(x), C, _p(w), C, _p(out), K, 0,
                      _p(bias), _p(zp), M, K, C, 0, 0, 0, 0.0, bk, 1, _s())
         else:
-            HIP.call("kml_gemm_stats", "p l p l p l p p p i i i i s", _p(x), C, _p(w), C, _p(out), K, _p(bias),
-                     _p(rows), _p(zp), M, K, C, bk, _s())
+            HIP.call("kml_gemm_stats", "p l p l p l p p p i i i i p p i s", _p(x), C, _p(w), C, _p(out), K, _p(bias),
+                     _p(rows), _p(zp), M, K, C, bk, _p(grp), _p(gcnt), tpg, _s())
         return out
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
@@ -773,14 +790,15 @@ def conv_dgrad(dy, w, in_shape, KH, KW, stride, pad, out=None, addend=None, cfg=
         by, bc, bmean, brstd, part, rows, grp, gcnt, tpg, G = _bnf_ws(bnf, out, M, C, plan)
         from . import gemm as GM
         if gather:
-            HIP.call("kml_gemm_conv_dgrad", "p p p p p p p p p i p i i i i i i i i i i s", _p(dy), _p(w), _p(out),
-                     _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
+            HIP.call("kml_gemm_conv_dgrad", "p p p p p p p p p i p i i i i i i i i i i p p i s", _p(dy), _p(w),
+                     _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
                      int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), B, H, W, C, K, KH, KW, ph, pw,
-                     bk, _s())
+                     bk, _p(grp), _p(gcnt), tpg, _s())
             return (out, (part, G)) if bnf is not None else out
-        HIP.call("kml_gemm_dgrad_bnf", "p l p l p l p p p p p p i p i i i i s", _p(dy), K, _p(w), C, _p(out), C,
+        HIP.call("kml_gemm_dgrad_bnf", "p l p l p l p p p p p p i p i i i i p p i s", _p(dy), K, _p(w), C, _p(out), C,
                  _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows),
-                 int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), M, C, K, bk, _s())
+                 int(bool(bnf_mask) and bnf is not None), _p(GM._zp(dy.device)), M, C, K, bk, _p(grp), _p(gcnt), tpg,
+                 _s())
         return (out, (part, G)) if bnf is not None else out
     if s2_parity_ok(B, H, W, stride, plan, _g22, _fold, operands=addend is not None or bnf is not None):
         part, G = None, 0

@@ -113,7 +113,7 @@ def test_conv_fwd_bias_relu():
 
 @pytest.mark.parametrize("cfg", [(256, 256, 6, 1, 7), (256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7),
                                  (128, 128, 3, 1, 7), (128, 128, 4, 1, 7)])
-@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 512, 136)])
+@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 512, 136), (9, 31, 64, 128)])
 def test_conv1x1_gemm_route_output_and_stats_rows(cfg, shape):
     """1x1 / stride-1 conv on the MFMA GEMM (kml_gemm_stats): output vs fp32 torch, the per-M-tile
     [sum | sumsq] rows vs the sums of the bf16 output, ragged M (M % BM != 0), with and without bias;
@@ -195,7 +195,8 @@ def test_conv_wgrad_gemm_gather_route_matches_torch(route, geom, monkeypatch):
 
 @pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
                                  (128, 128, 4, 1, 7)])
-@pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1), (3, 7, 136, 64, 3, 1), (2, 9, 72, 192, 3, 1)])
+@pytest.mark.parametrize("geom", [(4, 14, 64, 128, 3, 1), (3, 7, 136, 64, 3, 1), (2, 9, 72, 192, 3, 1),
+                                  (9, 31, 64, 64, 3, 1)])
 def test_conv_dgrad_gemm_gather_route_matches_torch(cfg, geom):
     """Implicit-GEMM input gradient on the GEMM tiles (kml_gemm_conv_dgrad, stride 1): dx vs fp32
     torch autograd with a residual addend, and the consumer-BN rows / ReLU mask vs that dx."""
@@ -227,7 +228,7 @@ def test_conv_dgrad_gemm_gather_route_matches_torch(cfg, geom):
 
 @pytest.mark.parametrize("cfg", [(256, 256, 0, 1, 7), (256, 128, 1, 1, 7), (128, 256, 2, 1, 7), (128, 128, 3, 1, 7),
                                  (128, 128, 4, 1, 7)])
-@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 136, 512)])
+@pytest.mark.parametrize("shape", [(4, 14, 64, 256), (3, 7, 256, 64), (2, 9, 136, 512), (9, 31, 128, 64)])
 def test_conv1x1_dgrad_gemm_route_matches_implicit_gemm(cfg, shape):
     """1x1 / stride-1 dgrad on the MFMA GEMM (kml_gemm_dgrad_bnf) against the implicit-GEMM dgrad:
     dx (+ residual addend) vs fp32 torch, the consumer-BN partial rows and the ReLU-masked output."""
