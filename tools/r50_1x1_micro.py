@@ -204,7 +204,7 @@ def wgrad3_main(dev, stem=False, vgg=False):
         best = None
         key = (B * H * H, Co, C, kk, st)
         for (bm, bn, stg) in [(128, 128, 2), (128, 128, 0), (256, 128, 0), (128, 256, 0)]:
-            for sp in ((128, 256, 512) if stem else (2, 4, 8, 16, 32)):
+            for sp in ((128, 256, 512) if stem else (8, 16, 32, 64, 128)):
                 route = ("gather", bm, bn, stg, sp)
                 K._WGRAD_GEMM[key] = route
                 tg = gtime(lambda: K.conv_wgrad(x, dy, dw, kk, kk, S, P, accumulate=True), reps=10)
