@@ -1,8 +1,10 @@
-// Host-only tests of the native runtime (policy, merger, npy loader), built with
-// AddressSanitizer + UndefinedBehaviorSanitizer and run without a GPU
-// (sanitizers on the C++ runtime's host code; GPU ASan is not available).
-// Also hammers the policy from several threads (the reference's policy had unlocked
-// map writes, policy.go:70-84).
+// Host-only tests of the native runtime (policy, merger, npy loader), built twice by
+// tests/test_sanitize_cpu.py — AddressSanitizer + UndefinedBehaviorSanitizer, and
+// ThreadSanitizer — and run without a GPU (sanitizers on the C++ runtime's host
+// code; GPU ASan is not available).  Hammers the policy from several threads (the reference's
+// policy had unlocked map writes, policy.go:70-84) and drives the loader's fill thread with
+// concurrent push / take / pending calls from three threads.
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -161,11 +163,67 @@ static void test_prefetch(const char* dir) {
   kml_npy_close(h);
 }
 
+// the fill thread against a producer thread pushing ranges, a consumer thread taking them in
+// order (byte-exact), and a thread polling pending() — the interleavings ThreadSanitizer watches —
+// then free() racing the fill thread with ranges still queued, several times over
+static void test_prefetch_concurrent(const char* dir) {
+  std::string path = std::string(dir) + "/rt_prefetch_mt.npy";
+  const int rows = 4000, cols = 3;
+  write_npy(path.c_str(), rows, cols);
+  void* h = kml_npy_open(path.c_str());
+  CHECK(h != nullptr);
+  if (!h) return;
+  for (int round = 0; round < 4; ++round) {
+    void* pf = kml_prefetch_new(h, 2 + round, 32);
+    CHECK(pf != nullptr);
+    const int nranges = 120;
+    std::atomic<int> pushed{0};
+    std::atomic<bool> done{false};
+    std::atomic<int> bad{0};
+    std::thread producer([&] {
+      for (int i = 0; i < nranges; ++i) {
+        const long long r0 = (i * 37LL) % (rows - 32);
+        if (kml_prefetch_push(pf, r0, 1 + i % 32) < 0) bad.fetch_add(1);
+        pushed.fetch_add(1);
+        if (i % 7 == 0) std::this_thread::yield();
+      }
+    });
+    std::thread consumer([&] {
+      std::vector<float> dst(32 * cols);
+      for (int i = 0; i < nranges; ++i) {
+        while (pushed.load() <= i) std::this_thread::yield();
+        const long long n = kml_prefetch_take_host(pf, dst.data());
+        const long long r0 = (i * 37LL) % (rows - 32);
+        if (n != 1 + i % 32) { bad.fetch_add(1); continue; }
+        for (long long k = 0; k < n; ++k)
+          for (int c = 0; c < cols; ++c)
+            if (dst[k * cols + c] != (float)((r0 + k) * 1000 + c)) bad.fetch_add(1);
+      }
+      done.store(true);
+    });
+    std::thread monitor([&] {
+      while (!done.load()) {
+        const long long p = kml_prefetch_pending(pf);
+        if (p < 0 || p > nranges) bad.fetch_add(1);
+        std::this_thread::yield();
+      }
+    });
+    producer.join();
+    consumer.join();
+    monitor.join();
+    CHECK(bad.load() == 0);
+    for (int i = 0; i < 5; ++i) kml_prefetch_push(pf, 32 * i, 32);   // queued when freed
+    kml_prefetch_free(pf);
+  }
+  kml_npy_close(h);
+}
+
 int main(int argc, char** argv) {
   test_policy();
   test_merger();
   test_npy(argc > 1 ? argv[1] : "/tmp");
   test_prefetch(argc > 1 ? argv[1] : "/tmp");
+  test_prefetch_concurrent(argc > 1 ? argv[1] : "/tmp");
   if (failures) {
     std::fprintf(stderr, "%d failures\n", failures);
     return 1;
