@@ -829,23 +829,12 @@ static int pick_v(long long n8, int vmax) {
   while (r < v && r < vmax) r *= 2;
   return r;
 }
-// lower bound on V from the environment (tuning experiments: fewer, fuller blocks re-read the
-// partial rows fewer times); 1 = the default pick
-static int env_vmin(const char* name) {
-  const char* v = getenv(name);
-  const int r = v ? atoi(v) : 1;
-  return r == 2 || r == 4 || r == 8 ? r : 1;
-}
-static int vmin_fwd() { static const int v = env_vmin("KUBEML_BN_VMIN_FWD"); return v; }
-static int vmin_bwd() { static const int v = env_vmin("KUBEML_BN_VMIN_BWD"); return v < 4 ? v : 4; }
-static int grid_cap() {  // blocks of the vectorised BN kernels (KUBEML_BN_GRID_CAP: tuning experiments)
-  static const int v = [] { const char* e = getenv("KUBEML_BN_GRID_CAP"); const int r = e ? atoi(e) : 0;
-                            return r >= 256 ? r : 1024; }();
-  return v;
-}
+// (fewer, fuller blocks — V >= 2/4/8 chunks per thread, or a grid cap below 1024 — measured
+// slower on ResNet-34: profiles/r5/bn_fold_ab.md, profiles/r5/r50/bn_grid_cap_probe.txt)
 static unsigned v_grid(long long n8, int V) {
+  constexpr long long GRID_CAP = 1024;
   long long g = (n8 + (long long)TPB * V - 1) / ((long long)TPB * V);
-  if (g > grid_cap()) g = grid_cap();
+  if (g > GRID_CAP) g = GRID_CAP;
   return (unsigned)(g < 1 ? 1 : g);
 }
 
@@ -1146,7 +1135,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
                                 hipStream_t s) {
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = max(pick_v(n8, 4), vmin_bwd());
+    const int V = pick_v(n8, 4);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
     const KmlSgdRider rider = kml_rider_take();
@@ -1199,7 +1188,7 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
   if (mode == 0 && stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
-    const int V = max(pick_v(n8, 8), stats_rows > 0 ? vmin_fwd() : 1);
+    const int V = pick_v(n8, 8);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
 #define KML_AP_V(VV)                                                                                           \

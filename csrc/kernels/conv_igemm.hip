@@ -864,84 +864,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4_t (&acc)[
   }
 }
 
-// -------------------------------------------------------------------------------------
-// BN backward folded into the operand staging of the conv that produced the BN's input
-// (DGRAD / WGRAD bodies with BNB = true).  The upstream dgrad already wrote dz (the masked
-// gradient of this BN's output) and this BN's [dbeta | dgamma] partial rows (bnf_*), so the
-// separate BN-backward launch only computed dc = a (dz - b - xhat g) per element; here each
-// A chunk of dz is transformed on its way into LDS, with c (the BN input, same NHWC offset)
-// loaded beside it:
-//   ibn_y  = c (bf16, the layout of dy)      ibn_rows / ibn_G = [G][2 Cbn] partial rows
-//   ibn_M  = pixels of the BN                ibn_gamma / ibn_mean / ibn_rstd = gamma, saved stats
-//   ibn_rmean / ibn_rvar = dgamma / dbeta outputs (DGRAD block 0; accumulate = add)
-// Cbn (BN channels, a power of two) = K, or K / 4 for an unrolled conv (fold_c set); the
-// channel of a chunk is its element offset & (Cbn - 1).  Row sums follow bn.hip's EarlyRows
-// order (256 threads), and dc the apply kernel's expression, so the fold matches it bit for bit.
-// -------------------------------------------------------------------------------------
-constexpr int BNB_MAXC = 512;
-
-__device__ __forceinline__ int bnb_channels(const ConvArgs& a, int width) {
-  return a.fold_c ? width >> 2 : width;
-}
-
-// sum of G rows of W floats into out[W] (W / 4 <= 256): slices of rows, fixed order
-__device__ __forceinline__ void bnb_row_sums(const float* __restrict__ part, int G, int W, float* out,
-                                             float4* scratch, const float4 (&early)[16]) {
-  const int Q = W / 4, S = 256 / Q, tid = threadIdx.x, q = tid % Q, sl = tid / Q;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (sl < S) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const bool in = sl + u * S < G;
-      acc.x += in ? early[u].x : 0.f; acc.y += in ? early[u].y : 0.f;
-      acc.z += in ? early[u].z : 0.f; acc.w += in ? early[u].w : 0.f;
-    }
-    const float4* p4 = reinterpret_cast<const float4*>(part) + q;
-    for (int r = sl + 16 * S; r < G; r += S) {
-      const float4 v = p4[(long long)r * Q];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-  }
-  scratch[tid] = acc;
-  __syncthreads();
-  if (tid < Q) {
-    float4 t4 = scratch[tid];
-    for (int k = 1; k < S; ++k) {
-      const float4 v = scratch[k * Q + tid];
-      t4.x += v.x; t4.y += v.y; t4.z += v.z; t4.w += v.w;
-    }
-    reinterpret_cast<float4*>(out)[tid] = t4;
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void bnb_early(const ConvArgs& a, int W, float4 (&early)[16]) {
-  const int Q = W / 4, S = 256 / Q, tid = threadIdx.x, q = tid % Q, sl = tid / Q;
-  if (sl < S) {
-    const float4* p4 = reinterpret_cast<const float4*>(a.ibn_rows) + q;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) early[u] = p4[(long long)min(sl + u * S, a.ibn_G - 1) * Q];
-  }
-}
-
-// dc of one 16-byte chunk: 8 channels' coefficients ka (gamma rstd), kb (dbeta / M),
-// kc (dgamma / M), mu (mean), rs (rstd)
-__device__ __forceinline__ uint4 bnb_apply8(uint4 dz, uint4 cv, const float (&ka)[8], const float (&kb)[8],
-                                            const float (&kc)[8], const float (&mu)[8], const float (&rs)[8]) {
-  const unsigned dw[4] = {dz.x, dz.y, dz.z, dz.w}, cw[4] = {cv.x, cv.y, cv.z, cv.w};
-  unsigned o[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float x0 = (lo_bf(cw[k]) - mu[2 * k]) * rs[2 * k];
-    const float x1 = (hi_bf(cw[k]) - mu[2 * k + 1]) * rs[2 * k + 1];
-    const float o0 = ka[2 * k] * (lo_bf(dw[k]) - kb[2 * k] - x0 * kc[2 * k]);
-    const float o1 = ka[2 * k + 1] * (hi_bf(dw[k]) - kb[2 * k + 1] - x1 * kc[2 * k + 1]);
-    o[k] = pack_bf2(o0, o1);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-template <int MODE, int BM, int BN, int BK, bool TAPU, bool BNB = false>
+template <int MODE, int BM, int BN, int BK, bool TAPU>
 struct IgemmBody {
   static constexpr bool A_KC = (MODE != WGRAD);
   static constexpr bool B_KC = (MODE == FWD);
@@ -950,20 +873,15 @@ struct IgemmBody {
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;
   static constexpr int THREADS = 256;
   static constexpr int SMEM_PIPE = 2 * STAGE * (int)sizeof(bf16_t);
-  // BNB: the DGRAD body keeps [5][Cbn] coefficients past the pipeline (the WGRAD body holds its
-  // 8 channels' in registers); the prologue's row scratch (4 KiB + 2 Cbn floats) reuses the stages
-  static constexpr int SMEM_BNB = (BNB && MODE == DGRAD) ? 5 * BNB_MAXC * 4 : 0;
-  static constexpr int SMEM = SMEM_PIPE + SMEM_BNB;
-  static_assert(!BNB || MODE != FWD, "BN-backward staging is for the backward bodies");
-  static_assert(!BNB || SMEM_PIPE >= 4096 + 2 * BNB_MAXC * 4, "BN-backward prologue scratch must fit the stages");
+  static constexpr int SMEM = SMEM_PIPE;
   static_assert(MODE == WGRAD || SMEM >= 16 + 8 * BN, "epilogue BN-row scratch must fit the LDS");
   static_assert(MODE == WGRAD || BM * BN < 8192 || SMEM >= 16 + BM * (BN + 8) * 2 + 8 * BN,
                 "epilogue output staging must fit the LDS");
   __device__ __forceinline__ static void run(const ConvArgs& a, const Blk& bk, char* smem_raw);
 };
 
-template <int MODE, int BM, int BN, int BK, bool TAPU, bool BNB>
-__device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU, BNB>::run(const ConvArgs& a, const Blk& bk,
+template <int MODE, int BM, int BN, int BK, bool TAPU>
+__device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const ConvArgs& a, const Blk& bk,
                                                                            char* smem_raw) {
   constexpr int WM = BM / 2, WN = BN / 2, MR = WM / 16, NR = WN / 16;
   constexpr int KC = BK / 8;  // 16-byte chunks per K-contiguous row
@@ -1014,124 +932,27 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU, BNB>::run(cons
     }
   }
 
-  // BNB: the consumer BN's partial rows are requested before any operand (vmcnt retires in
-  // issue order), then gamma / mean / rstd of this thread's channels
-  const int cbn = BNB ? bnb_channels(a, MODE == DGRAD ? a.K : a.M) : 1;
-  float4 brow[BNB ? 16 : 1];
-  float bpre[BNB ? (MODE == DGRAD ? 6 : 24) : 1];
-  if constexpr (BNB) {
-    bnb_early(a, 2 * cbn, brow);
-    if constexpr (MODE == DGRAD) {  // channels tid, tid + 256 of the [5][Cbn] table
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int c = min(tid + u * 256, cbn - 1);
-        bpre[3 * u] = a.ibn_gamma ? a.ibn_gamma[c] : 1.f;
-        bpre[3 * u + 1] = a.ibn_mean[c];
-        bpre[3 * u + 2] = a.ibn_rstd[c];
-      }
-    } else {  // WGRAD: the 8 output channels of this thread's A chunks (fixed over K)
-      const int c0 = (m0 + (tid % (BM / 8)) * 8) & (cbn - 1);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        bpre[k] = a.ibn_gamma ? a.ibn_gamma[c0 + k] : 1.f;
-        bpre[8 + k] = a.ibn_mean[c0 + k];
-        bpre[16 + k] = a.ibn_rstd[c0 + k];
-      }
-    }
-  }
-  // per stage: the BN input chunk beside each dz chunk and its channel (-1: zero page)
-  uint4 rc0[BNB ? PA : 1], rc1[BNB ? PA : 1];
-  int cc0[BNB ? PA : 1], cc1[BNB ? PA : 1];
-  float* const bcoef = reinterpret_cast<float*>(smem_raw + SMEM_PIPE);  // DGRAD [5][Cbn]
-  float wka[8], wkb[8], wkc[8], wmu[8], wrs[8];                          // WGRAD registers
-
   uint4 ra0[PA], rb0[PB], ra1[PA], rb1[PB];
-  auto issue_bnb = [&](uint4* ra, uint4* rb, uint4* rc, int* cc, int kt) {
+  auto issue = [&](uint4* ra, uint4* rb, int kt) {
     const int kb = kbeg + kt * BK;
 #pragma unroll
-    for (int i = 0; i < PA; ++i) {
-      const bf16_t* p = ga[i].ptr(a, kb, kend);
-      ra[i] = ld16(p);
-      if constexpr (BNB) {
-        const bool ok = p != a.zp;
-        const long long off = p - a.dy;
-        rc[i] = ld16(ok ? a.ibn_y + off : a.zp);
-        cc[i] = ok ? (int)(off & (long long)(cbn - 1)) : -1;
-      }
-    }
+    for (int i = 0; i < PA; ++i) ra[i] = ld16(ga[i].ptr(a, kb, kend));
 #pragma unroll
     for (int i = 0; i < PB; ++i) rb[i] = ld16(gb[i].ptr(a, kb, kend));
   };
-  auto stash_bnb = [&](const uint4* ra, const uint4* rb, const uint4* rc, const int* cc, int buf) {
+  auto stash = [&](const uint4* ra, const uint4* rb, int buf) {
     bf16_t* sA = smem + buf * STAGE;
     bf16_t* sB = sA + TA::ELEMS;
 #pragma unroll
-    for (int i = 0; i < PA; ++i) {
-      uint4 v = ra[i];
-      if constexpr (BNB) {
-        if (cc[i] < 0) {
-          v = make_uint4(0, 0, 0, 0);
-        } else if constexpr (MODE == DGRAD) {
-          float ka[8], kb[8], kc[8], mu[8], rs[8];
-          const float* t = bcoef + cc[i];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            ka[k] = t[k]; kb[k] = t[cbn + k]; kc[k] = t[2 * cbn + k]; mu[k] = t[3 * cbn + k]; rs[k] = t[4 * cbn + k];
-          }
-          v = bnb_apply8(v, rc[i], ka, kb, kc, mu, rs);
-        } else {
-          v = bnb_apply8(v, rc[i], wka, wkb, wkc, wmu, wrs);
-        }
-      }
-      *reinterpret_cast<uint4*>(sA + offA[i]) = v;
-    }
+    for (int i = 0; i < PA; ++i) *reinterpret_cast<uint4*>(sA + offA[i]) = ra[i];
 #pragma unroll
     for (int i = 0; i < PB; ++i) *reinterpret_cast<uint4*>(sB + offB[i]) = rb[i];
   };
-  static_assert(!BNB || MODE != WGRAD || TA::CHUNKS % 256 == 0, "BNB wgrad: every thread's chunks share one channel");
   // register stage 0 / 1 (no runtime choice between register arrays: they must stay in VGPRs)
-  auto issue0 = [&](int kt) { issue_bnb(ra0, rb0, rc0, cc0, kt); };
-  auto issue1 = [&](int kt) { issue_bnb(ra1, rb1, rc1, cc1, kt); };
-  auto stash0 = [&](int buf) { stash_bnb(ra0, rb0, rc0, cc0, buf); };
-  auto stash1 = [&](int buf) { stash_bnb(ra1, rb1, rc1, cc1, buf); };
-  // BNB prologue, after the first two stages' loads are in flight: row sums -> coefficients
-  auto bnb_prologue = [&]() {
-    if constexpr (BNB) {
-      float* sums = reinterpret_cast<float*>(smem_raw + 4096);
-      bnb_row_sums(a.ibn_rows, a.ibn_G, 2 * cbn, sums, reinterpret_cast<float4*>(smem_raw), brow);
-      const float invM = 1.f / (float)a.ibn_M;
-      if constexpr (MODE == DGRAD) {
-        const bool writer = bk.x == 0 && bk.y == 0 && bk.z == 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int c = tid + u * 256;
-          if (c < cbn) {
-            const float sb = sums[c], sg = sums[cbn + c];
-            if (writer) {  // one writer: store (overwrite) or add (accumulate)
-              a.ibn_rvar[c] = a.accumulate ? a.ibn_rvar[c] + sb : sb;    // dbeta
-              a.ibn_rmean[c] = a.accumulate ? a.ibn_rmean[c] + sg : sg;  // dgamma
-            }
-            bcoef[c] = bpre[3 * u] * bpre[3 * u + 2];
-            bcoef[cbn + c] = sb * invM;
-            bcoef[2 * cbn + c] = sg * invM;
-            bcoef[3 * cbn + c] = bpre[3 * u + 1];
-            bcoef[4 * cbn + c] = bpre[3 * u + 2];
-          }
-        }
-      } else {
-        const int c0 = (m0 + (tid % (BM / 8)) * 8) & (cbn - 1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          wka[k] = bpre[k] * bpre[16 + k];
-          wkb[k] = sums[c0 + k] * invM;
-          wkc[k] = sums[cbn + c0 + k] * invM;
-          wmu[k] = bpre[8 + k];
-          wrs[k] = bpre[16 + k];
-        }
-      }
-      __syncthreads();  // coefficients visible / row scratch free for the first stash
-    }
-  };
+  auto issue0 = [&](int kt) { issue(ra0, rb0, kt); };
+  auto issue1 = [&](int kt) { issue(ra1, rb1, kt); };
+  auto stash0 = [&](int buf) { stash(ra0, rb0, buf); };
+  auto stash1 = [&](int buf) { stash(ra1, rb1, buf); };
 
   f32x4_t acc[MR][NR];
 #pragma unroll
@@ -1165,7 +986,6 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU, BNB>::run(cons
     const int last = nk - 1;
     issue0(0);
     issue1(1);  // past-the-end K-tiles load the zero page (ptr() redirects k >= kend)
-    bnb_prologue();
     stash0(0);
     __syncthreads();
     for (int kt = 0;; kt += 2) {
@@ -1182,8 +1002,6 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU, BNB>::run(cons
       __syncthreads();
       if (kt + 2 > last) break;
     }
-  } else {
-    bnb_prologue();   // the DGRAD writer still owes dgamma / dbeta
   }
 
   conv_epilogue<MODE, MR, NR, WM, WN, false, false, SMEM_PIPE>(a, acc, m0, n0, wm, wn, lane, tid,
@@ -1965,13 +1783,7 @@ int dispatch_halo(const ConvArgs& a, int bm, int bn, hipStream_t s) {
 // fragment's 16 rows x 4 chunks).  The unrolled convs' B rows are gathered from the 3x3
 // weight (g22) per 16-byte chunk.
 // =====================================================================================
-// BNIN (FWD): the A rows are the raw output c of the producing conv; its BatchNorm (training
-// statistics from the producer's partial rows ibn_rows / ibn_G, the BN apply kernel's summation
-// order and arithmetic) + ReLU is applied while the A panel is staged — through registers instead
-// of the DMA — and the N-tile-0 blocks write the normalised rows to ibn_y (the activation the
-// backward keeps).  BN channel of column k: k & (Cbn - 1), Cbn = Cin (1x1 maps) or Cin / 4 for
-// a gathered unrolled conv (g22: 4 map positions per row).
-template <int BM, int BN, int KD, bool BNIN = false>
+template <int BM, int BN, int KD>
 struct OneShotBody {
   static constexpr int CPR = KD / 8;                    // 16-byte chunks per panel row
   static constexpr int A_BYTES = BM * KD * 2, B_BYTES = BN * KD * 2;
@@ -1979,8 +1791,7 @@ struct OneShotBody {
   static constexpr int NIA = BM * CPR / 64, NIB = BN * CPR / 64;  // 1 KiB DMA instructions per panel
   static constexpr int SMEM_EPI = 16 + BM * (BN + 8) * 2 + 2 * BN * 4;
   static constexpr int SMEM_PANELS = A_BYTES + B_BYTES > SMEM_EPI ? A_BYTES + B_BYTES : SMEM_EPI;
-  static constexpr int SMEM_BN = BNIN ? (2 * BNB_MAXC + 2 * BNB_MAXC) * 4 + 256 * 16 : 0;  // scale, shift, sums, scratch
-  static constexpr int SMEM = SMEM_PANELS + SMEM_BN;
+  static constexpr int SMEM = SMEM_PANELS;
   static constexpr int THREADS = 256;
   static_assert(CPR % 16 == 0 && NIA % 4 == 0 && NIB % 4 == 0, "one-shot panel shape");
   static_assert(SMEM <= 160 * 1024, "one-shot panels exceed LDS");
@@ -1988,38 +1799,14 @@ struct OneShotBody {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
     const int m0 = bk.y * BM, n0 = bk.x * BN;
     const int tapoff = (a.r0 * a.KW + a.s0) * a.C;
-    constexpr int NA = BNIN ? NIA / 4 : 1;
-    uint4 av[NA], rv[NA];
-    float4 brow[BNIN ? 16 : 1];
-    const int cbn = BNIN ? (a.g22 ? a.fd_gC.d : a.C) : 1;
-    if constexpr (BNIN) {
-      bnb_early(a, 2 * cbn, brow);  // the statistics rows first: they retire before the panels
 #pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int u = j * 4 + wave;
-        const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
-        const int m = m0 + row;
-        av[j] = ld16(m < a.M ? a.x + (long long)m * a.C + lc * 8 : a.zp);
-      }
-      if (a.addend) {  // residual of the folded BN: y = relu(bn(c) + res)
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-          const int u = j * 4 + wave;
-          const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
-          const int m = m0 + row;
-          rv[j] = ld16(m < a.M ? a.addend + (long long)m * a.C + lc * 8 : a.zp);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NIA / 4; ++j) {
-        const int u = j * 4 + wave;
-        const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
-        const int m = m0 + row;
-        const bf16_t* src = m < a.M ? a.x + (long long)m * a.C + lc * 8 : a.zp;
-        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(smem + u * 1024),
-                                         16, 0, 0);
-      }
+    for (int j = 0; j < NIA / 4; ++j) {
+      const int u = j * 4 + wave;
+      const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
+      const int m = m0 + row;
+      const bf16_t* src = m < a.M ? a.x + (long long)m * a.C + lc * 8 : a.zp;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(smem + u * 1024),
+                                       16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < NIB / 4; ++j) {
@@ -2037,52 +1824,6 @@ struct OneShotBody {
       }
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(smem + A_BYTES + u * 1024), 16, 0, 0);
-    }
-    if constexpr (BNIN) {
-      float* scale = reinterpret_cast<float*>(smem + SMEM_PANELS);
-      float* shift = scale + BNB_MAXC;
-      float* sums = shift + BNB_MAXC;
-      float4* scratch = reinterpret_cast<float4*>(sums + 2 * BNB_MAXC);
-      bnb_row_sums(a.ibn_rows, a.ibn_G, 2 * cbn, sums, scratch, brow);
-      const float M = (float)a.ibn_M;
-      for (int c = tid; c < cbn; c += 256) {
-        const float mean = sums[c] / M;
-        const float var = fmaxf(sums[cbn + c] / M - mean * mean, 0.f);
-        const float rstd = rsqrtf(var + a.ibn_eps);
-        const float g = a.ibn_gamma ? a.ibn_gamma[c] : 1.f, bb = a.ibn_beta ? a.ibn_beta[c] : 0.f;
-        scale[c] = g * rstd;
-        shift[c] = bb - mean * g * rstd;
-        if (bk.x == 0 && bk.y == 0) {
-          if (a.ibn_mean) { a.ibn_mean[c] = mean; a.ibn_rstd[c] = rstd; }
-          if (a.ibn_rmean) {
-            const float unb = a.ibn_M > 1 ? var * (float)a.ibn_M / (float)(a.ibn_M - 1) : var;
-            a.ibn_rmean[c] = (1.f - a.ibn_mom) * a.ibn_rmean[c] + a.ibn_mom * mean;
-            a.ibn_rvar[c] = (1.f - a.ibn_mom) * a.ibn_rvar[c] + a.ibn_mom * unb;
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int u = j * 4 + wave;
-        const int L = u * 64 + lane, row = L / CPR, lc = (L % CPR) ^ (row & 15);
-        const int m = m0 + row;
-        const int c0 = (lc * 8) & (cbn - 1);
-        const unsigned w32[4] = {av[j].x, av[j].y, av[j].z, av[j].w};
-        const unsigned r32[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};
-        unsigned o32[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int cc = c0 + 2 * k;
-          float lo = lo_bf(w32[k]) * scale[cc] + shift[cc];
-          float hi = hi_bf(w32[k]) * scale[cc + 1] + shift[cc + 1];
-          if (a.addend) { lo += lo_bf(r32[k]); hi += hi_bf(r32[k]); }
-          o32[k] = pack_bf2(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
-        }
-        const uint4 v = m < a.M ? make_uint4(o32[0], o32[1], o32[2], o32[3]) : make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(smem + u * 1024 + lane * 16) = v;
-        if (bk.x == 0 && m < a.M) *reinterpret_cast<uint4*>(a.ibn_y + (long long)m * a.C + lc * 8) = v;
-      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2262,9 +2003,9 @@ int dispatch_oneshot_bwd(const ConvArgs& a, int bm, int bn, hipStream_t s) {
   return (int)hipErrorInvalidValue;
 }
 
-template <int BM, int BN, int KD, bool BNIN = false>
+template <int BM, int BN, int KD>
 __global__ __launch_bounds__(256) void k_conv_oneshot(ConvArgs a) {
-  using Body = OneShotBody<BM, BN, KD, BNIN>;
+  using Body = OneShotBody<BM, BN, KD>;
   __shared__ __attribute__((aligned(1024))) char smem[Body::SMEM];
   Body::run(a, xcd_blk(), smem);
 }
@@ -2282,10 +2023,7 @@ int dispatch_oneshot(const ConvArgs& a, int bm, int bn, hipStream_t s) {
   dim3 grid((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, 1);
 #define KML_O(BMv, BNv, KDv)                                                          \
   if (bm == BMv && bn == BNv && a.Kd == KDv) {                                        \
-    if (a.ibn_rows)                                                                   \
-      hipLaunchKernelGGL((k_conv_oneshot<BMv, BNv, KDv, true>), grid, dim3(256), 0, s, a); \
-    else                                                                              \
-      hipLaunchKernelGGL((k_conv_oneshot<BMv, BNv, KDv>), grid, dim3(256), 0, s, a);   \
+    hipLaunchKernelGGL((k_conv_oneshot<BMv, BNv, KDv>), grid, dim3(256), 0, s, a);     \
     KML_LAUNCH_CHECK();                                                               \
   }
   KML_O(32, 32, 512) KML_O(32, 32, 1024) KML_O(32, 64, 512) KML_O(64, 32, 512) KML_O(32, 32, 256)
@@ -2677,17 +2415,6 @@ using DgHa128x4 = HaloBody<DGRAD, 128, 4, 4, 32, 1>;
   X(3, 64, 32, 4, DgDi6432, 64, 32, WgIg3232, 32, 32)      \
   X(3, 64, 32, 4, DgDi6432, 64, 32, WgIg6432, 64, 32)
 
-// BN-backward-folded pairs (BNB bodies): the register-staged igemm pairs only
-using DgIg3264B = IgemmBody<DGRAD, 32, 64, 64, true, true>;
-using DgIg3232B = IgemmBody<DGRAD, 32, 32, 64, true, true>;
-using WgIg3232B = IgemmBody<WGRAD, 32, 32, 64, true, true>;
-using WgIg6432B = IgemmBody<WGRAD, 64, 32, 64, true, true>;
-#define KML_PAIR_BNB_LIST(X)                                 \
-  X(0, 32, 64, 64, DgIg3264B, 32, 64, WgIg3232B, 32, 32)     \
-  X(0, 32, 64, 64, DgIg3264B, 32, 64, WgIg6432B, 64, 32)     \
-  X(0, 32, 32, 64, DgIg3232B, 32, 32, WgIg3232B, 32, 32)     \
-  X(0, 32, 32, 64, DgIg3232B, 32, 32, WgIg6432B, 64, 32)
-
 template <class DB, class WB>
 int launch_pair(const ConvArgs& ad, int dbm, int dbn, const ConvArgs& aw, int wbm, int wbn, hipStream_t s) {
   const int dgx = (ad.N + dbn - 1) / dbn, dgy = (ad.M + dbm - 1) / dbm;
@@ -2717,27 +2444,6 @@ int dispatch_pair(int which, const ConvArgs& ad, const ConvArgs& aw, hipStream_t
 #define KML_PAIR_RUN(DV, DBM, DBN, DBK, DB, DTM, DTN, WB, WBM, WBN) \
   if (++idx == which) return launch_pair<DB, WB>(ad, DTM, DTN, aw, WBM, WBN, s);
   KML_PAIR_LIST(KML_PAIR_RUN)
-#undef KML_PAIR_RUN
-  return (int)hipErrorInvalidValue;
-}
-
-// 1 + index of the instantiated BN-backward-folded pair, 0 if none
-int pair_bnb_index(int dv, int dbm, int dbn, int dbk, int wv, int wbm, int wbn, int wbk) {
-  int idx = 0;
-#define KML_PAIR_FIND(DV, DBM, DBN, DBK, DB, DTM, DTN, WB, WBM, WBN)                                   \
-  ++idx;                                                                                             \
-  if (dv == DV && dbm == DBM && dbn == DBN && dbk == DBK && wv == 0 && wbm == WBM && wbn == WBN && wbk == 64) \
-    return idx;
-  KML_PAIR_BNB_LIST(KML_PAIR_FIND)
-#undef KML_PAIR_FIND
-  return 0;
-}
-
-int dispatch_pair_bnb(int which, const ConvArgs& ad, const ConvArgs& aw, hipStream_t s) {
-  int idx = 0;
-#define KML_PAIR_RUN(DV, DBM, DBN, DBK, DB, DTM, DTN, WB, WBM, WBN) \
-  if (++idx == which) return launch_pair<DB, WB>(ad, DTM, DTN, aw, WBM, WBN, s);
-  KML_PAIR_BNB_LIST(KML_PAIR_RUN)
 #undef KML_PAIR_RUN
   return (int)hipErrorInvalidValue;
 }
@@ -2989,37 +2695,6 @@ KML_API int kml_conv_fwd_bnin(const bf16_t* x, const bf16_t* w, bf16_t* y, float
   return dispatch_halo<FWD>(a, bm, bn, s);
 }
 
-// One-shot forward (single-tap, contiguous rows: 1x1 maps, or an unrolled 2x2 conv in its
-// gathered 1x1 form, g22) with the INPUT's BatchNorm + ReLU applied while the A panel is staged
-// (OneShotBody BNIN): x is the producer's raw output c, ibn_rows / ibn_G its partial statistics
-// rows [G][2 Cbn], ibn_M the BN's pixel count; the normalised input is written to ibn_y.
-// fold_c / g22 as in kml_conv_fwd.  Cbn (Cin, or Cin / 4 with g22) a power of two <= 512.
-KML_API int kml_conv_fwd_oneshot_bnin(const bf16_t* x, const bf16_t* w, bf16_t* y, float* stats, int stats_part,
-                                      int B, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                                      int pw, int bm, int bn, int fold_c, int g22, const float* ibn_rows, int ibn_G,
-                                      long long ibn_M, const float* gamma, const float* beta, float* mean, float* rstd,
-                                      float* rmean, float* rvar, float eps, float momentum, bf16_t* ibn_y,
-                                      const bf16_t* res, hipStream_t s) {
-  if (g22 && !g22_ok(C, K, KH, KW)) return (int)hipErrorInvalidValue;
-  if (fold_c && (K % fold_c || (stats && !stats_part))) return (int)hipErrorInvalidValue;
-  const int cbn = g22 ? C / 4 : C;
-  if (C % 8 || !ibn_rows || ibn_G < 1 || ibn_M < 1 || !ibn_y || cbn > BNB_MAXC || cbn < 8 || (cbn & (cbn - 1)))
-    return (int)hipErrorInvalidValue;
-  ConvArgs a = make_args(B, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  a.x = x; a.w = w; a.out = y; a.stats = stats; a.stats_part = stats_part; a.fold_c = fold_c;
-  set_g22(a, g22, C, K);
-  a.zp = zero_page();
-  a.M = B * a.OH * a.OW; a.N = K; a.Kd = (a.r1 - a.r0) * (a.s1 - a.s0) * C;
-  a.splits = 1; a.kchunk = a.Kd;
-  a.ibn_rows = ibn_rows; a.ibn_G = ibn_G; a.ibn_M = ibn_M;
-  a.ibn_gamma = gamma; a.ibn_beta = beta; a.ibn_mean = mean; a.ibn_rstd = rstd; a.ibn_rmean = rmean;
-  a.ibn_rvar = rvar; a.ibn_eps = eps; a.ibn_mom = momentum; a.ibn_y = ibn_y;
-  a.addend = res;   // FWD: the folded BN's residual (y = relu(bn(x) + res))
-  if (!a.zp) return (int)hipErrorInvalidSymbol;
-  if (!oneshot_shape_ok(a) || (g22 ? a.fd_gC.d : a.C) != cbn) return (int)hipErrorInvalidValue;
-  return dispatch_oneshot(a, bm, bn, s);
-}
-
 namespace {
 int prep_dgrad(ConvArgs& a, const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
                const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean, const float* bnf_rstd,
@@ -3084,12 +2759,6 @@ KML_API int kml_conv_pair_supported(int dvariant, int dbm, int dbn, int dbk, int
   return pair_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk) > 0 ? 1 : 0;
 }
 
-// is there a BN-backward-folded instantiation of this pair (kml_conv_bwd_pair_bnb)?
-KML_API int kml_conv_pair_bnb_supported(int dvariant, int dbm, int dbn, int dbk, int wvariant, int wbm, int wbn,
-                                        int wbk) {
-  return pair_bnb_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk) > 0 ? 1 : 0;
-}
-
 // dX (dgrad, + addend, + consumer-BN partials) and dW (wgrad, fp32 +=) of one conv in one
 // launch.  wt: transposed weights for the direct dgrad variant (else null).
 KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, const bf16_t* addend,
@@ -3114,47 +2783,6 @@ KML_API int kml_conv_bwd_pair(const bf16_t* dy, const bf16_t* w, const bf16_t* w
                  wcounters, wbias, wbias_acc);
   if (e) return e;
   return dispatch_pair(which, ad, aw, s);
-}
-
-// kml_conv_bwd_pair with this conv's OWN BatchNorm backward folded into both GEMMs' dz staging
-// (see IgemmBody BNB): dz (the masked gradient of the BN output, as `dy`), bc = the BN input c,
-// rows / G = its [dbeta | dgamma] partial rows from the upstream dgrad, gamma / mean / rstd;
-// dgamma / dbeta are written (bn_acc: added) by dgrad block 0.  The separate BN-backward launch
-// disappears.  BN channels (K, or K / 4 unrolled) must be a power of two <= 512 and 2 Cbn / 4
-// must divide 256 (row-sum slices).
-KML_API int kml_conv_bwd_pair_bnb(const bf16_t* dz, const bf16_t* w, bf16_t* dx, const bf16_t* addend,
-                                  const bf16_t* bnf_y, const bf16_t* bnf_c, const float* bnf_mean,
-                                  const float* bnf_rstd, float* bnf_part, float* grp_out, unsigned* grp_cnt,
-                                  int grp_tiles, const bf16_t* x, float* dw, int B, int H, int W, int C, int K, int KH,
-                                  int KW, int sh, int sw, int ph, int pw, int dbm, int dbn, int dbk, int dsplits,
-                                  int dvariant, float* slab, unsigned* counters, int wbm, int wbn, int wbk,
-                                  int wsplits, int wvariant, int fold_c, int bnf_mask_out, float* wslab,
-                                  unsigned* wcounters, int waccumulate, int g22, const bf16_t* bc, const float* rows,
-                                  int G, const float* gamma, const float* mean, const float* rstd, float* dgamma,
-                                  float* dbeta, int bn_acc, hipStream_t s) {
-  const int which = pair_bnb_index(dvariant, dbm, dbn, dbk, wvariant, wbm, wbn, wbk);
-  const int cbn = fold_c ? K / 4 : K;
-  if (!which || !bc || !rows || G < 1 || !mean || !rstd || !dgamma || !dbeta || cbn > BNB_MAXC || cbn < 8 ||
-      (cbn & (cbn - 1)) || (256 % (2 * cbn / 4)) != 0 || (fold_c && K % 4))
-    return (int)hipErrorInvalidValue;
-  ConvArgs ad, aw;
-  int e = prep_dgrad(ad, dz, w, nullptr, dx, addend, bnf_y, bnf_c, bnf_mean, bnf_rstd, bnf_part, grp_out, grp_cnt,
-                     grp_tiles, B, H, W, C, K, KH, KW, sh, sw, ph, pw, dbk, dsplits, dvariant, slab, counters,
-                     fold_c, bnf_mask_out, g22);
-  if (e) return e;
-  e = prep_wgrad(aw, x, dz, dw, B, H, W, C, K, KH, KW, sh, sw, ph, pw, wbk, wsplits, wvariant, waccumulate, wslab,
-                 wcounters, nullptr, 0);
-  if (e) return e;
-  for (ConvArgs* p : {&ad, &aw}) {
-    p->ibn_y = const_cast<bf16_t*>(bc);
-    p->ibn_rows = rows; p->ibn_G = G;
-    p->ibn_gamma = gamma; p->ibn_mean = const_cast<float*>(mean); p->ibn_rstd = const_cast<float*>(rstd);
-  }
-  const long long pix = (long long)B * ad.OH * ad.OW * (fold_c ? 4 : 1);
-  ad.ibn_M = aw.ibn_M = pix;
-  ad.ibn_rmean = dgamma; ad.ibn_rvar = dbeta; ad.accumulate = bn_acc ? 1 : 0;
-  aw.fold_c = fold_c;   // the WGRAD epilogue ignores fold_c; BNB reads it for the channel count
-  return dispatch_pair_bnb(which, ad, aw, s);
 }
 
 // Up to 16 transposes wT = [C][KH*KW][Kp] (Kp = roundup(K, 32)) in one launch.

@@ -85,20 +85,11 @@ struct GemmArgs {
   float* grp_out;
   unsigned* grp_cnt;
   int grp_tiles;
-  int swz;             // row-pass reads in conflict-free 16-lane phases (KUBEML_GEMM_ROWPASS_SWZ=1; A/B)
 };
 
-static int rowpass_swz_default() {
-  static const int v = [] { const char* e = getenv("KUBEML_GEMM_ROWPASS_SWZ"); return (e && e[0] == '1') ? 1 : 0; }();
-  return v;
-}
-
-// the conv routes' forward GEMMs store through LDS rows unless KUBEML_GEMM_OUT_ROWPASS=0 (A/B:
-// ResNet-50 15.82 -> 15.63 ms/step, profiles/r5/r50/r50_ab_out_rowpass.txt)
-static int out_rowpass_default() {
-  static const int v = [] { const char* e = getenv("KUBEML_GEMM_OUT_ROWPASS"); return (e && e[0] == '0') ? 0 : 1; }();
-  return v;
-}
+// the conv routes' forward GEMMs store through LDS rows (ResNet-50 15.82 -> 15.63 ms/step,
+// profiles/r5/r50/r50_ab_out_rowpass.txt)
+static int out_rowpass_default() { return 1; }
 
 constexpr int BK = 64;
 constexpr int NT = 512;
@@ -619,11 +610,10 @@ __device__ __forceinline__ void gemm_bnf_rowpass(const GemmArgs& g, f32x4_t (&ac
   for (int r = r0; r < BM; r += RSTEP) {
     const int m = m0 + r;
     if (m >= g.M || !nok) continue;
-    // lanes q >= 8 read their odd chunk first: a 16-lane phase then covers all 64 banks
-    const int h = g.swz ? (q >> 3) & 1 : 0;
-    const float4 pa = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + h) ^ (r & 15)) << 2));
-    const float4 pb = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + 1 - h) ^ (r & 15)) << 2));
-    const float4 p0 = h ? pb : pa, p1 = h ? pa : pb;
+    // (reading the odd chunk first on lanes q >= 8, conflict-free 16-lane phases, measured neutral:
+    // profiles/r5/r50/ab12_rowpass_swz_run{1,2}.txt)
+    const float4 p0 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q) ^ (r & 15)) << 2));
+    const float4 p1 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + 1) ^ (r & 15)) << 2));
     float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
     const long long off = (long long)m * g.ldc + n;
     if (g.c2) {
@@ -706,10 +696,8 @@ __device__ __forceinline__ void gemm_out_rowpass(const GemmArgs& g, f32x4_t (&ac
   for (int r = r0; r < BM; r += RSTEP) {
     const int m = m0 + r;
     if (m >= g.M || !nok) continue;
-    const int h = g.swz ? (q >> 3) & 1 : 0;   // as in gemm_bnf_rowpass: conflict-free 16-lane phases
-    const float4 pa = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + h) ^ (r & 15)) << 2));
-    const float4 pb = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + 1 - h) ^ (r & 15)) << 2));
-    const float4 p0 = h ? pb : pa, p1 = h ? pa : pb;
+    const float4 p0 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q) ^ (r & 15)) << 2));
+    const float4 p1 = *reinterpret_cast<const float4*>(sF + r * BN + (((2 * q + 1) ^ (r & 15)) << 2));
     const unsigned ow[4] = {pack_bf2(p0.x, p0.y), pack_bf2(p0.z, p0.w), pack_bf2(p1.x, p1.y), pack_bf2(p1.z, p1.w)};
     if (st) {
 #pragma unroll
@@ -1414,7 +1402,7 @@ KML_API int kml_gemm(const bf16_t* a, long long lda, const bf16_t* b, long long 
   g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
   // the linear-layer GEMMs keep the register epilogue: BERT's QKV forward on the 128 x 128 row-pass
   // tile beat hipBLASLt alone (71 vs 88 us) but not inside the step (profiles/r5/bert_qkv_rowpass.md)
-  g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   if (M <= 0 || N <= 0) return 0;
   if (act == GEMM_GELU_BWD) return (int)hipErrorInvalidValue;  // kml_gemm_dgrad_gelu
   if (layout == 0 && out == 0) return by_tile<true, true, 0>(g, tile, 1, s);
@@ -1442,9 +1430,9 @@ KML_API int kml_gemm_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const
   g.lda = C; g.ldb = (long long)KH * KW * C; g.ldc = K;
   g.M = B * OH * OW; g.N = K; g.K = KH * KW * C; g.act = rows ? GEMM_STATS : 0; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
-  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   if (grp_out) {
     if (!rows || !grp_cnt || grp_tiles < 1 || !g.rowpass || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
     g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
@@ -1476,7 +1464,7 @@ KML_API int kml_gemm_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, c
   g.lda = K; g.ldb = (long long)KH * KW * C; g.ldc = C;
   g.M = B * H * W; g.N = C; g.K = KH * KW * K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = g.K;
   g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = 1; g.csw = 1; g.cph = ph; g.cpw = pw;
   g.cK = K;
   if (grp_out) {
@@ -1507,7 +1495,7 @@ KML_API int kml_gemm_conv_wgrad(const bf16_t* x, const bf16_t* dy, float* dw, fl
   g.a = dy; g.b = x; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = K; g.ldb = 0; g.ldc = (long long)KH * KW * C;
   g.M = K; g.N = KH * KW * C; g.K = B * OH * OW; g.act = 0; g.beta = 0.f; g.kchunk = g.K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cOH = OH; g.cOW = OW; g.cKW = KW; g.csh = sh; g.csw = sw; g.cph = ph; g.cpw = pw;
   g.cK = K;
   splits = splits < 1 ? 1 : splits;
@@ -1541,7 +1529,7 @@ KML_API int kml_gemm_stats(const bf16_t* a, long long lda, const bf16_t* b, long
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_STATS; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
   g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0;
-  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.rowpass = out_rowpass_default(); g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   if (grp_out) {  // group reduction: row-pass tiles only
     if (!grp_cnt || grp_tiles < 1 || !g.rowpass || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
     g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
@@ -1564,7 +1552,7 @@ KML_API int kml_gemm_dgrad_bnf(const bf16_t* a, long long lda, const bf16_t* b, 
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(addend); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_BNF; g.beta = 0.f; g.kchunk = K; g.colpart = rows;
-  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = y; g.bc = cin; g.bmean = mean; g.brstd = rstd; g.mask_out = mask_out; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   if (grp_out) {  // the BNF row pass runs on the 128 x 128 tiles
     if (!cin || !grp_cnt || grp_tiles < 1 || (tile != 3 && tile != 4)) return (int)hipErrorInvalidValue;
     g.grp_out = grp_out; g.grp_cnt = grp_cnt; g.grp_tiles = grp_tiles;
@@ -1584,7 +1572,7 @@ KML_API int kml_gemm_dgrad_gelu(const bf16_t* a, long long lda, const bf16_t* b,
   g.a = a; g.b = b; g.c = c; g.c2 = const_cast<bf16_t*>(pre); g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.act = GEMM_GELU_BWD; g.beta = 0.f; g.kchunk = K; g.colpart = colpart;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   return launch8<true, false, 0>(g, 1, s);
 }
 
@@ -1600,7 +1588,7 @@ KML_API int kml_gemm_wgrad_splitk(const bf16_t* a, long long lda, const bf16_t* 
   g.a = a; g.b = b; g.c = slab; g.c2 = nullptr; g.bias = nullptr; g.zp = zp;
   g.lda = lda; g.ldb = ldb; g.ldc = N;
   g.M = M; g.N = N; g.K = K; g.act = 0; g.beta = 0.f; g.kchunk = K; g.colpart = nullptr;
-  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0; g.swz = rowpass_swz_default();
+  g.by = nullptr; g.bc = nullptr; g.bmean = nullptr; g.brstd = nullptr; g.mask_out = 0; g.rowpass = 0; g.grp_out = nullptr; g.grp_cnt = nullptr; g.grp_tiles = 0;
   splits = splits < 1 ? 1 : splits;
   int rc = by_tile<false, false, 3>(g, tile, splits, s);
   if (rc) return rc;

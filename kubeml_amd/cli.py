@@ -78,6 +78,10 @@ def cmd_train(a):
         raise KubeMLException("learning rate must be positive", 400)
     if req.options.sync == "grad" and req.options.k != 1:
         raise KubeMLException("--grad-sync runs K = 1 rounds: pass --K 1", 400)
+    if req.options.sync == "grad" and not req.options.static_parallelism:
+        # the optimizer state persists across rounds and lives sharded per rank: a resize would
+        # leave new workers with zero moments and hand chunks to stale owners
+        raise KubeMLException("--grad-sync keeps optimizer state on the workers: pass --static", 400)
     c.datasets.get(req.dataset)
     if not any(f["name"] == req.function_name for f in c.functions.list()):
         raise KubeMLException(f"function {req.function_name} does not exist", 404)

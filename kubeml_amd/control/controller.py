@@ -42,6 +42,12 @@ class Controller:
 
     # --- network (networkApi.go) ---------------------------------------------------
     def train(self, req: TrainRequest) -> str:
+        opts = req.options
+        if getattr(opts, "sync", "") == "grad" and (int(opts.k) != 1 or not opts.static_parallelism):
+            # persistent (sharded) optimizer state across K = 1 rounds: an elastic resize would start
+            # new workers from zero moments and move shard ownership; the CLI checks too
+            from ..api.errors import KubeMLException
+            raise KubeMLException("sync='grad' needs k = 1 and static_parallelism", 400)
         if not self.shards.exists(req.dataset):
             raise NotFoundError(f"dataset {req.dataset}")
         if not self.functions.exists(req.function_name):

@@ -289,7 +289,7 @@ def _ride(model, space, optimizer, fwd_bwd, post, get_fold, scale):
     mom = optimizer._bufs(space, ["momentum"])["momentum"] if g["momentum"] != 0 else None
     first = optimizer.first_tensor(dev) if mom is not None else None
     lr = optimizer.lr_tensor(dev)
-    blocks = int(os.environ.get("KUBEML_RIDE_BLOCKS", "512"))   # measured: 32 / 64 lose, 512-1024 best
+    blocks = 512   # rider blocks per launch: measured, 32 / 64 lose, 512-1024 best
     riders, covered, seen = [], [], set()       # riders: (group, SgdRider)
     groups = model.ride_plan()
     holder = {}                                 # this step's take(): set below

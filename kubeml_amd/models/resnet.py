@@ -220,9 +220,8 @@ class ResNet(tnn.Module):
         for part in filter(None, spec.split(";")):
             own, host = part.split(":")
             ps = [p for d in own for p in (self.fc if d == "f" else getattr(self, f"layer{d}")).parameters()]
-            kinds = os.environ.get("KUBEML_RIDE_HOSTKIND", "conv")   # conv | bn | both
-            want = {"conv": (M.Conv2d,), "bn": (M.BatchNorm2d,), "both": (M.Conv2d, M.BatchNorm2d)}[kinds]
-            hosts = [m for d in host for m in getattr(self, f"layer{d}").modules() if isinstance(m, want)]
+            # the riders sit on the hosts' conv-backward pairs (BN-backward hosts measured no better)
+            hosts = [m for d in host for m in getattr(self, f"layer{d}").modules() if isinstance(m, M.Conv2d)]
             groups.append((ps, hosts))
         return groups
 

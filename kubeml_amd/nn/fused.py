@@ -30,13 +30,10 @@ import os
 from .flat import grad_out, grad_out_pair, master_of, shadow_of
 
 # every BN backward takes its dgamma/dbeta partial rows from the dgrad epilogue that produced
-# its input gradient (False: its own reduction pass; tests compare the two)
+# its input gradient (False: its own reduction pass; tests compare the two).  Folding the BN
+# backward into the next conv pair's dz staging measured 1.3-2.6x slower pairs even with the rows
+# pre-reduced to one (profiles/r5/bn_fold_ab.md, profiles/r6/bn_final_rows.md): removed.
 _BN_FUSE = True
-# ... and, where the conv's backward pair has a BN-folded instantiation (ops.kernels.bnb_ok), may
-# run inside that pair's dz staging instead of its own launch.  Opt-in (KUBEML_BNB_FOLD=1): exact,
-# but every block of the pair re-reads the partial rows from the other XCDs' writes, and the
-# ResNet-34 step measured 1.423 vs 1.331 ms/step without it (profiles/r5/bn_fold_ab.md)
-_BNB_FOLD = os.environ.get("KUBEML_BNB_FOLD", "0") == "1"
 
 
 def _wg_buf(conv, x):
@@ -295,20 +292,6 @@ class ConvBNUnit:
         wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
         dx, part_out = None, None
         bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
-        if (_BNB_FOLD and partial is not None and need_dx and x.is_cuda and
-                K.bnb_ok(x.shape, c.shape[-1], kh, kw, conv.stride, conv.padding, partial[1], unroll=wu is not None)):
-            # the BN backward runs inside the conv pair's dz staging: no BN launch, and the
-            # residual gradient IS dy (the upstream dgrad already applied this BN's ReLU mask)
-            object.__setattr__(conv, "_kml_wu", None)
-            w = shadow_of(conv.weight)
-            dw, wacc = _wgrad_target(conv, x, wu is not None)
-            bnb = (c, partial[0], partial[1], mean, rstd, master_of(bn.weight), dg, db, acc)
-            r = K.conv_bwd(dy, w, x, dw, kh, kw, conv.stride, conv.padding, addend=addend, bnf=bnf, wu=wu,
-                           bnf_mask=True, accumulate=wacc, bnb=bnb, rider=_take_rider(conv))
-            if wu is not None:
-                conv.weight._kml_flat.defer_fold22(conv.weight, dw)
-            dx, part_out = r if bnf is not None else (r, None)
-            return dx, (dy if want_dres else None), part_out
         dres = torch.empty_like(dy) if want_dres else None
         dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
                       dg, db, dres=dres, partial=partial, accumulate=acc, rider=_take_rider(bn))
@@ -369,7 +352,7 @@ class PendingBN:
 # cross-block fold: a BasicBlock's output BN + residual + ReLU is applied by the next block's first
 # conv (halo / one-shot BN-in staging) instead of its own launch.  Only inside a model forward that
 # drives the chain (``chain()``: ResNet.forward), so a block called on its own never defers.
-_CROSS_FOLD = os.environ.get("KUBEML_CROSS_FOLD", "1") != "0"
+_CROSS_FOLD = True
 _CHAIN = [0]
 
 
@@ -529,7 +512,7 @@ class BlockFn(Function):
         return (g, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
-_SHORT_LAST = os.environ.get("KUBEML_SHORT_LAST", "1") != "0"
+_SHORT_LAST = True
 
 
 def _short_last(short_saved, sc, conv1) -> bool:

@@ -23,7 +23,7 @@ TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 
 _TUNE_FILE = os.environ.get("KUBEML_GEMM_TUNING_FILE") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _TUNED: dict = {}
-if os.path.exists(_TUNE_FILE) and os.environ.get("KUBEML_GEMM_TUNING", "1") != "0":
+if os.path.exists(_TUNE_FILE):   # KUBEML_GEMM_TUNING_FILE=none: every GEMM on its default tile
     with open(_TUNE_FILE) as f:
         for e in json.load(f).get("entries", []):
             _TUNED[(e["layout"], e["M"], e["N"], e["K"])] = (tuple(e["tile"]), int(e.get("splits", 1)))

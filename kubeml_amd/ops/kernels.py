@@ -58,8 +58,7 @@ _TUNE_FILE = os.environ.get("KUBEML_CONV_TUNING_FILE") or \
 
 
 def _load_tuning():
-    if os.environ.get("KUBEML_CONV_TUNING", "1") == "0":
-        return
+    # KUBEML_CONV_TUNING_FILE=none: every conv on its default plan
     if os.path.exists(_TUNE_FILE):
         with open(_TUNE_FILE) as f:
             for e in json.load(f).get("entries", []):
@@ -182,25 +181,12 @@ _GRP_MIN = 0
 _GRP_ROWS = 16
 
 
-def _gemm_grouped(cfg) -> bool:
-    """Does this plan's producer group-reduce its partial rows (the conv GEMM route on the 128x128
-    row-pass tiles: the last block of every group of M-tiles sums the group's rows, so the BN kernel
-    reads <= _GRP_ROWS rows and no k_rows_fold launch runs)?"""
-    c = tuple(cfg) + (0,) * (5 - len(cfg))
-    return _GEMM_GROUP and c[4] == GEMM1X1 and c[2] in (3, 4)
-
-
-# KUBEML_GEMM_GROUP_ROWS=1: group-reduce the GEMM route's rows in the producer; off: one row per M-tile
-# (folded by k_rows_fold).  The forward statistics rows need the row-pass epilogue
-# (KUBEML_GEMM_OUT_ROWPASS, on by default)
-_GEMM_GROUP = os.environ.get("KUBEML_GEMM_GROUP_ROWS", "0") == "1" and os.environ.get("KUBEML_GEMM_OUT_ROWPASS", "1") != "0"
 
 
 def _stats_layout(M, cfg, group=False):
     """(per-wave rows G, M-tiles per group or 0, rows the consumer reads).  group: reduce
     to at most _GRP_ROWS rows regardless of _GRP_MIN (a consumer whose every block reads all
     rows, e.g. the BN-folding halo conv)."""
-    group = group or _gemm_grouped(cfg)
     bm = _norm_cfg(cfg)[0]
     tiles = _cdiv(M, bm)
     # one row per M tile (the epilogue sums the tile's wave row-bands; tail tiles included)
@@ -388,13 +374,12 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
                  int(_fold), int(_g22), _s())
         return out
     if variant == GEMM1X1:
-        gemm_grp = _gemm_grouped((bm, bn, bk, splits, variant))
-        if relu or _fold or _g22 or (grp is not None and not gemm_grp) or (stats is not None and not stats_part) or \
+        if relu or _fold or _g22 or grp is not None or (stats is not None and not stats_part) or \
                 not x.is_contiguous() or not out.is_contiguous():
             # same bm (and the same row grouping), so the statistics rows the caller sized stay valid
             return conv_fwd(x, w, KH, KW, stride, pad, bias=bias, stats=stats, relu=relu, out=out,
                             cfg=_GEMM1X1_FALLBACK[bm], stats_part=stats_part, _fold=_fold, _g22=_g22,
-                            stats_group=stats_group or gemm_grp)
+                            stats_group=stats_group)
         from . import gemm as G
         zp = G._zp(x.device)
         if not gemm1x1_ok(C, K, H, W, KH, KW, stride, pad):   # implicit GEMM: A gathered per K-tile
@@ -542,12 +527,11 @@ def oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn) -> bool:
 # 55.9 vs 79.0 us, 14x14 256->1024: 51.9 vs 71.9 us; profiles/r5/r50_1x1_fwd.md).  The panels
 # keep the small-M layers (1x1 maps, B rows).
 _ONESHOT_MAX_ROWS = 4096
-_ONESHOT_LEGACY = os.environ.get("KUBEML_ONESHOT_LEGACY", "0") == "1"  # A/B: panels for K = 256 at any M
 
 
 def oneshot_plan(C, K, Kd, H, W, KH, KW, stride, pad, B=0):
     """Default one-shot panel plan for an eligible forward conv, or None."""
-    if B * H * W > _ONESHOT_MAX_ROWS and (Kd >= 512 or not _ONESHOT_LEGACY):
+    if B * H * W > _ONESHOT_MAX_ROWS:
         return None
     for bm, bn in _ONESHOT_TILES.get(Kd, ()):
         if oneshot_ok(C, K, Kd, H, W, KH, KW, stride, pad, bm, bn):
@@ -601,42 +585,20 @@ def conv_fwd_stats_rows(x_shape, K, KH, KW, stride, pad, cfg=None, unroll=False,
 
 def bnin_ok(x_shape, K, KH, KW, stride, pad) -> bool:
     """Can this forward conv apply its input's BatchNorm + ReLU while staging (conv_fwd_bnin)?
-    The halo kernel (3x3/s1/p1 on 8x8 / 4x4 maps) or the one-shot panels (1x1 maps, or a 2x2
-    map in its gathered unrolled form)."""
+    The halo kernel (3x3/s1/p1 on 8x8 / 4x4 maps).  The one-shot panels' BN-in form (layers 3-4)
+    measured slower than the separate BN apply and was removed (profiles/r5/bn_fold_ab.md,
+    profiles/r6/bn_final_rows.md)."""
     B, H, W, C = x_shape
     if not _BNIN_ON:
         return False
     if halo_plan(C, K, H, W, KH, KW, stride, pad) is not None:
         return 2 * C <= 1024 and 256 % (C // 2) == 0
-    return _BNIN_ONESHOT and _oneshot_bnin_plan(x_shape, K, KH, KW, stride, pad) is not None
-
-
-# one-shot panels with the input BN applied in staging: opt-in (KUBEML_BNIN_ONESHOT=1); exact, and
-# 10 us/step slower than the separate BN apply (profiles/r5/bn_fold_ab.md; round 3 found the same)
-_BNIN_ONESHOT = os.environ.get("KUBEML_BNIN_ONESHOT", "0") == "1"
-
-
-def _oneshot_bnin_plan(x_shape, K, KH, KW, stride, pad):
-    """(plan, unrolled) of a BN-in one-shot forward for this conv, or None."""
-    B, H, W, C = x_shape
-    if C < 8 or C > 512 or C & (C - 1) or (KH, KW) != (3, 3) or tuple(stride) != (1, 1) or tuple(pad) != (1, 1):
-        return None
-    if unrolled22(H, W, KH, KW, stride, pad):
-        if (4 * C) % 32 or K % 8:
-            return None
-        p = oneshot_plan(4 * C, 4 * K, 4 * C, 1, 1, 1, 1, (1, 1), (0, 0), B=B)
-        return (p, True) if p is not None else None
-    if H * W != 1:
-        return None
-    p = oneshot_plan(C, K, C, H, W, KH, KW, stride, pad, B=B)
-    return (p, False) if p is not None else None
+    return False
 
 
 def bnin_stats_rows(x_shape, K):
     """G of the output statistics rows of conv_fwd_bnin on an input of x_shape (3x3/s1/p1)."""
-    op = None if halo_plan(x_shape[3], K, x_shape[1], x_shape[2], 3, 3, (1, 1), (1, 1)) is not None else \
-        _oneshot_bnin_plan(x_shape, K, 3, 3, (1, 1), (1, 1))
-    return conv_fwd_stats_rows(x_shape, K, 3, 3, (1, 1), (1, 1), unroll=bool(op and op[1]))
+    return conv_fwd_stats_rows(x_shape, K, 3, 3, (1, 1), (1, 1))
 
 
 _BNIN_ON = True
@@ -662,13 +624,7 @@ def conv_fwd_bnin(c_in, w, rows, G, gamma, beta, save_mean, save_rstd, run_mean,
     if tuple(w.shape) != (K, 3, 3, C) or tuple(y_in.shape) != tuple(c_in.shape):
         raise ValueError("conv_fwd_bnin: 3x3 weight over c_in's channels and a y_in like c_in")
     plan = halo_plan(C, K, H, W, 3, 3, (1, 1), (1, 1))
-    if plan is None:
-        op = _oneshot_bnin_plan(c_in.shape, K, 3, 3, (1, 1), (1, 1))
-        if op is None or not _BNIN_ON:
-            raise ValueError("conv_fwd_bnin: conv is neither halo- nor one-shot-eligible")
-        return _conv_fwd_oneshot_bnin(c_in, w, op, rows, G, gamma, beta, save_mean, save_rstd, run_mean, run_var,
-                                      eps, momentum, y_in, stats, stats_part, out, res)
-    if not bnin_ok(c_in.shape, K, 3, 3, (1, 1), (1, 1)):
+    if plan is None or not bnin_ok(c_in.shape, K, 3, 3, (1, 1), (1, 1)):
         raise ValueError("conv_fwd_bnin: conv is not halo-eligible")
     bm, bn = plan[0], plan[1]
     if out is None:
@@ -688,40 +644,6 @@ def conv_fwd_bnin(c_in, w, rows, G, gamma, beta, save_mean, save_rstd, run_mean,
              _p(c_in), _p(w), _p(out), _p(srows), int(stats_part), B, H, W, C, K, bm, bn, _p(grp), _p(gcnt), tpg,
              _p(rows), int(G), _p(gamma), _p(beta), _p(save_mean), _p(save_rstd), _p(run_mean), _p(run_var),
              float(eps), float(momentum), _p(y_in), _p(res), _s())
-    return out
-
-
-def _conv_fwd_oneshot_bnin(c_in, w, op, rows, G, gamma, beta, save_mean, save_rstd, run_mean, run_var, eps,
-                           momentum, y_in, stats, stats_part, out, res=None):
-    """conv_fwd_bnin on the one-shot panels (kml_conv_fwd_oneshot_bnin)."""
-    (bm, bn, _, _, _), unroll = op
-    B, H, W, C = c_in.shape
-    K = w.shape[0]
-    if out is None:
-        out = torch.empty((B, H, W, K), dtype=BF16, device=c_in.device)
-    r1 = res
-    if unroll:   # 1x1 form of the 2x2 map: rows [B][4C], 3x3 weight gathered (g22), stats folded
-        x1, y1, o1 = c_in.view(B, 1, 1, 4 * C), y_in.view(B, 1, 1, 4 * C), out.view(B, 1, 1, 4 * K)
-        r1 = None if res is None else res.reshape(B, 1, 1, 4 * C)
-        geom = (B, 1, 1, 4 * C, 4 * K, 1, 1, 1, 1, 0, 0)
-        fold, g22 = K, 1
-        G_out = conv_fwd_stats_rows(c_in.shape, K, 3, 3, (1, 1), (1, 1), unroll=True)
-    else:
-        x1, y1, o1 = c_in, y_in, out
-        geom = (B, H, W, C, K, 3, 3, 1, 1, 1, 1)
-        fold, g22 = 0, 0
-        G_out = conv_fwd_stats_rows(c_in.shape, K, 3, 3, (1, 1), (1, 1))
-    if stats is not None:
-        _chk(stats, F32, "stats")
-        if not stats_part or stats.numel() < G_out * 2 * K:
-            raise ValueError(f"conv_fwd_bnin: stats needs stats_part and {G_out} x 2K floats")
-    _chk(rows, F32, "rows")
-    if rows.numel() < G * 2 * C:
-        raise ValueError("conv_fwd_bnin: partial rows smaller than G x 2C")
-    HIP.call("kml_conv_fwd_oneshot_bnin", "p p p p i i i i i i i i i i i i i i i i p i l p p p p p p f f p p s",
-             _p(x1), _p(w), _p(o1), _p(stats), int(stats is not None), *geom, bm, bn, fold, g22, _p(rows), int(G),
-             B * H * W, _p(gamma), _p(beta), _p(save_mean), _p(save_rstd), _p(run_mean), _p(run_var), float(eps),
-             float(momentum), _p(y1), _p(r1), _s())
     return out
 
 
@@ -1000,45 +922,8 @@ def conv_pair_supported(dcfg, wcfg) -> bool:
     return ok
 
 
-_PAIR_BNB_OK: dict = {}
-
-# BN backward folded into the conv pair's dz staging (kml_conv_bwd_pair_bnb): on for partial-row
-# buffers up to this many floats (every block of the pair sums them in its prologue)
-_BNB_ON = True
-_BNB_MAX_ROW_FLOATS = 16384
-
-
-def conv_pair_bnb_supported(dcfg, wcfg) -> bool:
-    """True if the (dgrad plan, wgrad plan) pair has a BN-backward-folded instantiation."""
-    key = (tuple(dcfg), tuple(wcfg))
-    ok = _PAIR_BNB_OK.get(key)
-    if ok is None:
-        dbm, dbn, dbk, _, dv = dcfg
-        wbm, wbn, wbk, _, wv = wcfg
-        ok = _PAIR_BNB_OK[key] = bool(HIP.fn("kml_conv_pair_bnb_supported", "i i i i i i i i")(
-            dv, dbm, dbn, dbk, wv, wbm, wbn, wbk))
-    return ok
-
-
-def bnb_ok(x_shape, K, KH, KW, stride, pad, G, unroll=False) -> bool:
-    """Can conv_bwd fold this conv's own BatchNorm backward (``bnb``) for partial rows of G x 2K?
-    Needs the grouped register-staged igemm pair (no wgrad-GEMM route, no parity dgrad), a
-    power-of-two channel count <= 512 and a row buffer within _BNB_MAX_ROW_FLOATS."""
-    if not _BNB_ON or K > 512 or K < 8 or K & (K - 1) or G * 2 * K > _BNB_MAX_ROW_FLOATS:
-        return False
-    B, H, W, C = x_shape
-    if C % 8:
-        return False
-    dplan, wplan, grouped = bwd_plans(x_shape, K, KH, KW, stride, pad, unroll=unroll)
-    if not grouped or not conv_pair_bnb_supported(dplan, wplan):
-        return False
-    if not unroll and wgrad_gemm_route(x_shape, K, KH, KW, stride, pad) is not None:
-        return False
-    return not s2_parity_ok(B, H, W, stride, dplan, False, C if unroll else 0, operands=True)
-
-
 def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, dcfg=None, wcfg=None, wu=None,
-             bnf_mask=False, accumulate=True, dbias=None, bias_accumulate=True, bnb=None, rider=None):
+             bnf_mask=False, accumulate=True, dbias=None, bias_accumulate=True, rider=None):
     """Both backward GEMMs of a conv: dx (+addend, + consumer-BN partials as in
     :func:`conv_dgrad`) and ``dw += wgrad`` (``accumulate=False``: ``dw = wgrad``).  Runs as ONE grouped launch
     (``k_conv_pair``: dgrad tiles and wgrad tiles share a grid) when the two plans have an
@@ -1049,9 +934,6 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     ``[4K,1,1,4C]`` fp32 scratch of the 1x1-form weight gradient (stored), which
     :func:`fold22_multi` folds onto the 3x3 taps.  bnf_mask: as in :func:`conv_dgrad`.
     dbias: as in :func:`conv_wgrad` (1x1/s1/p0 convs).
-    bnb = (c, part, G, mean, rstd, gamma, dgamma, dbeta, acc): ``dy`` is dz, the masked gradient
-    of this conv's BatchNorm OUTPUT; the BN backward (dc from dz, c and the partial rows;
-    dgamma / dbeta written or, acc, added) runs inside both GEMMs' operand staging (bnb_ok).
     rider: an :class:`SgdRider` applied by extra blocks of the grouped launch (or by its own
     launch after the two GEMMs when this conv does not run grouped)."""
     _chk(dy, BF16, "dy", 4)
@@ -1069,14 +951,8 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     if K % 8 or C % 8:
         raise ValueError("channels must be multiples of 8")
     fold, g22 = 0, False
-    if bnb is not None:
-        _chk(bnb[0], BF16, "bnb c", 4)
-        if tuple(bnb[0].shape) != tuple(dy.shape) or dbias is not None:
-            raise ValueError("conv_bwd bnb: c must match dy (and no dbias / direct dgrad)")
     if wu is not None:
         _check_wu(x.shape, w, wu, KH, KW, stride, pad)
-        if bnb is not None:
-            bnb = (bnb[0].reshape(B, 1, 1, 4 * K),) + tuple(bnb[1:])
         dy, x, addend, bnf = _u22_views(B, C, K, dy=dy, x=x, addend=addend, bnf=bnf)
         g22 = wu is GATHER22
         w, fold, accumulate = (w if g22 else wu), C, False
@@ -1096,8 +972,6 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
         grouped = False
     if dbias is not None and wu is not None:
         raise ValueError("conv_bwd: dbias needs a 1x1 conv")
-    if bnb is not None and not (grouped and conv_pair_bnb_supported(dplan, wplan)):
-        raise ValueError("conv_bwd bnb: no BN-folded pair for this conv's plans (check bnb_ok first)")
     if not grouped:
         conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None if wroute is not None else wplan, accumulate=accumulate,
                    dbias=dbias, bias_accumulate=bias_accumulate)
@@ -1131,21 +1005,6 @@ def conv_bwd(dy, w, x, dw, KH, KW, stride, pad, addend=None, bnf=None, wt=None, 
     wbm, wbn, wbk, wsplits, wvariant = wplan
     _chk_dbias(dbias, K, KH, KW, stride, pad)
     wslab, wcnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, wplan, dbias is not None)
-    if bnb is not None:
-        ibc, bpart, bG, bmean_, brstd_, bgamma, bdg, bdb, bacc = bnb
-        if variant != 0:
-            raise ValueError("conv_bwd bnb: register-staged igemm dgrad only")
-        with _Riding(rider):
-            HIP.call("kml_conv_bwd_pair_bnb", "p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i i p p i p p p p p i s",  # noqa: E501
-                     _p(dy), _p(w), _p(out), _p(addend), _p(by), _p(bc), _p(bmean), _p(brstd), _p(rows), _p(grp),
-                     _p(gcnt), tpg, _p(x), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, dsplits,
-                     variant, _p(slab), _p(cnt), wbm, wbn, wbk, wsplits, wvariant, int(fold),
-                     int(bool(bnf_mask) and bnf is not None), _p(wslab), _p(wcnt), int(bool(accumulate)), int(g22),
-                     _p(ibc), _p(bpart), int(bG), _p(bgamma), _p(bmean_), _p(brstd_), _p(bdg), _p(bdb),
-                     int(bool(bacc)), _s())
-        if fold:
-            out = out.view(B, 2, 2, C // 4)
-        return (out, (part, G)) if bnf is not None else out
     with _Riding(rider):
         HIP.call("kml_conv_bwd_pair",
                  "p p p p p p p p p p p p i p p i i i i i i i i i i i i i i i i p p i i i i i i i p p i p i i s",

@@ -188,19 +188,11 @@ def embed_fwd(ids, tt, word, pos, type_, L):
     return out
 
 
-_EMBED_FUSED = os.environ.get("KUBEML_EMBED_FUSED", "1") != "0"   # A/B knob: per-table kernels
-
-
 def embed_bwd(ids, tt, dsum, dword, dpos, dtype, L):
     """Word / position / token-type table gradients (+=).  With all three tables: one pass over
-    dsum (k_embed_bwd_fused); KUBEML_EMBED_FUSED=0 runs the per-table kernels (A/B)."""
+    dsum (k_embed_bwd_fused)."""
     T = ids.numel()
     N = dsum.shape[-1]
-    if not _EMBED_FUSED and dtype is not None:
-        HIP.call("kml_embed_bwd", "p p p p p p l i i s", _p(ids), _p(tt), _p(dsum), _p(dword), _p(dpos), 0, T, L, N,
-                 _s())
-        HIP.call("kml_embed_bwd", "p p p p p p l i i s", _p(ids), _p(tt), _p(dsum), 0, 0, _p(dtype), T, L, N, _s())
-        return
     HIP.call("kml_embed_bwd", "p p p p p p l i i s", _p(ids), _p(tt), _p(dsum), _p(dword), _p(dpos), _p(dtype), T, L,
              N, _s())
 

@@ -214,7 +214,7 @@ class TorchComm(Comm):
             self.kavg_p.close()
             self.kavg_p = None
         self.kavg_p = verified_peer(self.group, cap_bytes=slot_bytes(t.numel(), self.world, "twoshot"),
-                                    device=t.device)
+                                    device=t.device, kavg=True)
         self._kavg_off = self.kavg_p is None
         return self.kavg_p
 

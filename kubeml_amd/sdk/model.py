@@ -92,6 +92,7 @@ class KubeModel(ABC):
         self._synced_steps = 0
         self.sync_seconds = 0.0
         self._dry = False              # job warm-up (_warm): step / evaluate capture only
+        self._dry_calls = 0            # step / evaluate calls seen in dry mode
         ctx = current_task()
         if ctx is not None:
             ctx.extra["kubemodel"] = self
@@ -482,6 +483,14 @@ class KubeModel(ABC):
         (capture never mutates training state: engine/step.py) but replay nothing, so the
         model, the optimizer and the BN statistics are untouched.  The reference has no graphs
         to build; its clock (ml/pkg/train/job.go:183) also starts after initialisation.
+
+        A ``train`` written as the reference's manual loop (``loss.backward();
+        self.optimizer.step()``, e.g. examples/function_lenet.py) does not go through ``step``,
+        so its dry call WOULD update the model: every tensor a training step mutates (flat
+        master / shadow / gradients / buffers and counters, or the loose parameters and buffers,
+        and the optimizer's state) is snapshotted before the warm-up and restored after it, and
+        a dry ``train`` that never called ``step`` ends the train-shape scan (it has no graph to
+        capture).  Epoch 1 therefore starts from exactly the recovery-base model.
         Returns the number of graphs captured."""
         self._on_train_start()
         if self.device is None or self.device.type != "cuda" or os.environ.get("KUBEML_NO_GRAPH") == "1":
@@ -489,30 +498,43 @@ class KubeModel(ABC):
         comm = self._comm()
         N, fid, K = self.args._N, self.args._func_id, self.args._K
         bs = self.batch_size
-        assigned = split_minibatches(range(self._dataset.num_docs), N)[fid]
+        splits = split_minibatches(range(self._dataset.num_docs), N)
+        assigned = splits[fid]
         per = max(get_subset_period(K, bs, assigned), 1)
         intervals = [(i, min(assigned.stop, i + per)) for i in range(assigned.start, assigned.stop, per)]
+        # as in _train: rounds below full_rounds sync gradients, a ragged tail runs local
+        full_rounds = min(-(-len(sp) // max(get_subset_period(K, bs, sp), 1)) for sp in splits)
         grad_ok = self._grad_sync_ok(comm, K)
         if grad_ok:
             self._grad_comm = comm
             self._prime_grad_sync()
         done = 0
+        snap = self._training_snapshot()
         self._dry = True
         try:
             self._sync_mode = "grad" if grad_ok else "local"
             seen = set()
+            manual = False
             streamed = self._dataset._plan_stream("train", intervals, bs, self.device)
             # a resident / streamed split yields batches as device views (cheap to walk); a host
             # loader only walks the first and the last interval (the shapes a ragged end adds)
-            scan = intervals if streamed else list(dict.fromkeys([intervals[0], intervals[-1]])) if intervals else []
-            for i, e in scan:
+            rs = range(len(intervals)) if streamed else sorted({0, len(intervals) - 1}) if intervals else []
+            for r in rs:
+                if manual:
+                    break
+                i, e = intervals[r]
+                self._sync_mode = "grad" if (grad_ok and r < full_rounds) else "local"
                 self._dataset._load_train_data(start=i, end=e)
                 for batch in self._batches():
                     shape = tuple(getattr(batch[0], "shape", ())) if isinstance(batch, (tuple, list)) else None
-                    if shape in seen:
+                    if (shape, self._sync_mode) in seen:
                         continue
-                    seen.add(shape)
+                    seen.add((shape, self._sync_mode))
+                    before = self._dry_calls
                     self.train(self._batch_to_device(batch), 0)
+                    if self._dry_calls == before:   # a manual loop: it stepped for real (restored below)
+                        manual = True
+                        break
                     done += 1
             self._dataset._stream_end()
             self._sync_mode = "local"
@@ -528,7 +550,10 @@ class KubeModel(ABC):
                         if shape in seen:
                             continue
                         seen.add(shape)
+                        before = self._dry_calls
                         self.validate(self._batch_to_device(batch), 0)
+                        if self._dry_calls == before:   # no evaluate(): nothing to capture
+                            break
                         done += 1
                     self._dataset._stream_end()
                 self._network.train()
@@ -536,8 +561,60 @@ class KubeModel(ABC):
             self._dry = False
             self._sync_mode = "local"
             self._grad_comm = None
+            self._training_restore(snap)
         torch.cuda.synchronize(self.device)
         return done
+
+    def _training_snapshot(self):
+        """(tensors, copies, optimizer host state) of everything a real training step mutates:
+        the flat space's state (fp32 master, parameter buffers, i64 counters), gradient and bf16
+        shadow — or the loose parameters, gradients and buffers — and the optimizer's device
+        state (momenta / moments, step and first-step flags) with its host-side counters."""
+        import copy
+        ts = []
+        sp = self._flat
+        if sp is not None and getattr(sp, "state", None) is not None:
+            ts += [t for t in (sp.state, sp.grad, getattr(sp, "shadow", None)) if t is not None]
+        else:
+            ts += [p for p in self._network.parameters()]
+            ts += [p.grad for p in self._network.parameters() if p.grad is not None]
+            ts += [b for b in self._network.buffers()]
+        opt = self.optimizer
+        host = None
+        if opt is not None:
+            if hasattr(opt, "state_tensors"):
+                ts += opt.state_tensors()
+                # keys are the parameters themselves: copy the values, never the keys
+                st = {k: ({n: (v.detach().clone() if torch.is_tensor(v) else copy.copy(v)) for n, v in d.items()}
+                          if isinstance(d, dict) else d) for k, d in opt.state.items()}
+                host = (st, getattr(opt, "_first", None), getattr(opt, "_step_host", None))
+            else:
+                host = copy.deepcopy(opt.state_dict())
+        seen, uniq = set(), []
+        for t in ts:
+            if id(t) not in seen:
+                seen.add(id(t))
+                uniq.append(t)
+        with torch.no_grad():
+            return uniq, [t.detach().clone() for t in uniq], host
+
+    def _training_restore(self, snap):
+        ts, copies, host = snap
+        with torch.no_grad():
+            for t, c in zip(ts, copies):
+                t.copy_(c)
+        opt = self.optimizer
+        if opt is None or host is None:
+            return
+        if hasattr(opt, "state_tensors"):
+            opt.state.clear()
+            opt.state.update(host[0])
+            if host[1] is not None:
+                opt._first = host[1]
+            if host[2] is not None:
+                opt._step_host = host[2]
+        else:
+            opt.load_state_dict(host)
 
     # ---- validation (network.py:320-360) --------------------------------------------------
     def _on_validation_start(self):
@@ -615,8 +692,8 @@ class KubeModel(ABC):
 
     # ---- MI355X helper: graph-captured step --------------------------------------------------
     MAX_GRAPHS = 8
-    PEER_CHECK_EVERY = int(os.environ.get("KUBEML_PEER_CHECK_EVERY", "16"))
-    COMM_TIMING = int(os.environ.get("KUBEML_COMM_TIMING", "50"))   # sample the in-graph all-reduce every N steps
+    PEER_CHECK_EVERY = 16   # verify the peer data plane's checksums every N grad-sync steps
+    COMM_TIMING = 50        # sample the in-graph all-reduce every N steps
 
     def step(self, x, y, loss_fn=None, forward=None):
         """forward + loss + backward + optimizer step for one batch; on the GPU the first
@@ -645,6 +722,7 @@ class KubeModel(ABC):
         if g is None:
             g = self._build_step(key, x, y, loss_fn, comm, forward)
         if self._dry:                 # job warm-up: graph built and captured, nothing replayed
+            self._dry_calls += 1
             return torch.zeros((), dtype=torch.float32, device=x.device)
         g["x"].copy_(x, non_blocking=True)
         g["y"].copy_(y, non_blocking=True)
@@ -674,7 +752,10 @@ class KubeModel(ABC):
                              comm.world if comm is not None else 1, plan.tag() if plan is not None else None,
                              type(st.peer).__name__ if st.peer is not None else None)
             if st.peer is not None and comm is not None:
-                if st.schedule == "shard":
+                if st.schedule in ("shard", "shardov"):
+                    old = self._shards.get(id(comm))
+                    if old is not None and old is not st.peer:
+                        old.close()                        # collective: every rank builds the same plans
                     self._shards[id(comm)] = st.peer       # bound to this model's flat buffers
                 else:
                     comm.grad_peer = st.peer          # one gradient transport per group, reused
@@ -690,7 +771,7 @@ class KubeModel(ABC):
         (one that does not is closed — collectively: every rank sees the same sizes)."""
         if plan.backend != "peer":
             return None
-        if plan.schedule == "shard":
+        if plan.schedule in ("shard", "shardov"):    # both run on the PeerShard of this model's space
             sh = self._shards.get(id(comm))
             return sh if sh is not None and sh.region is not None else None
         gp = getattr(comm, "grad_peer", None)
@@ -744,6 +825,7 @@ class KubeModel(ABC):
             g = self._eval_graphs[key] = {"x": xs, "y": ys, "graph": graph, "out": outs}
             _sp.__exit__(None, None, None)
         if self._dry:                 # job warm-up: captured, not replayed
+            self._dry_calls += 1
             z = torch.zeros((), dtype=torch.float32, device=x.device)
             return z, z.clone()
         g["x"].copy_(x, non_blocking=True)

@@ -174,6 +174,12 @@ def test_request_validation_errors(env):
     with pytest.raises(HttpError) as e:
         c.networks.train(TrainRequest(batch_size=64, epochs=1, dataset="mnist", lr=0.1, function_name="nofn"))
     assert e.value.status_code == 404
+    # persistent (sharded) optimizer state needs a fixed worker group and K = 1
+    for opts in (TrainOptions(k=1, sync="grad"), TrainOptions(k=4, static_parallelism=True, sync="grad")):
+        with pytest.raises(HttpError) as e:
+            c.networks.train(TrainRequest(batch_size=64, epochs=1, dataset="mnist", lr=0.1, function_name="lenet",
+                                          options=opts))
+        assert e.value.status_code == 400
 
 
 def test_stop_task(env):

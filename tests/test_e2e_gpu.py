@@ -291,3 +291,57 @@ def test_gpu_worker_killed_mid_round_pool_rebuilds_and_job_finishes(tmp_path):
         assert len(h.accuracy) == 2
     finally:
         srv.stop()
+
+
+def test_warm_leaves_a_manual_loop_function_untouched():
+    """Job warm-up (KubeModel._warm) on a function written as the reference's manual loop
+    (loss.backward(); self.optimizer.step(), like examples/function_lenet.py): its dry train()
+    call bypasses self.step and really updates the model, so the warm-up must restore the
+    parameters, BN buffers and optimizer state it snapshotted — epoch 1 starts from the
+    recovery-base model — and stop scanning train shapes (nothing to capture)."""
+    import torch
+    import torch.nn as nn
+    from kubeml_amd.models.lenet import LeNet
+    from kubeml_amd.sdk.dataset import _KubeArgs
+    from kubeml_amd.sdk.model import KubeModel
+
+    class _DS:   # the parts of a KubeDataset the warm-up touches
+        num_docs, num_val_docs = 4, 0
+
+        def _plan_stream(self, *a, **k):
+            return False
+
+        def _load_train_data(self, start, end):
+            pass
+
+        def _stream_end(self):
+            pass
+
+    class Manual(KubeModel):
+        def configure_optimizers(self):
+            return torch.optim.SGD(self.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+
+        def train(self, batch, batch_index):
+            x, y = batch
+            self.optimizer.zero_grad()
+            loss = nn.functional.cross_entropy(self(x), y)
+            loss.backward()
+            self.optimizer.step()
+            self.calls += 1
+            return loss.item()
+
+    torch.manual_seed(0)
+    m = Manual(LeNet(), _DS(), gpu=True)
+    m.calls = 0
+    m.args = _KubeArgs("warmjob", 1, 1, "train", 0, 1, lr=0.1, batch_size=64)
+    m.lr, m.batch_size, m.epoch = 0.1, 64, 1
+    xs, ys = torch.randn(64, 1, 28, 28), torch.randint(0, 10, (64,))
+    m._batches = lambda: iter([(xs, ys), (xs[:32], ys[:32])])
+    m._on_train_start()
+    c0 = m.model_checksum()
+    w0 = [p.detach().clone() for p in m.parameters()]
+    assert m._warm() == 0
+    assert m.calls == 1                       # the manual loop ran once, then the scan stopped
+    assert m.model_checksum() == c0
+    assert all(torch.equal(p, q) for p, q in zip(m.parameters(), w0))
+    assert len(m.optimizer.state) == 0        # no momentum buffers survive the dry call

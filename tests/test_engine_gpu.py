@@ -238,17 +238,14 @@ def _graphed_run(opt_overlap, steps=3, ride=False, arch="resnet18"):
     return sp.master - w0, sp, losses
 
 
-@pytest.mark.parametrize("arch,plan,kind", [("resnet18", "4f:321", "conv"), ("resnet34", "4f:321", "conv"),
-                                            ("resnet34", "4f:3;3:21", "conv"), ("resnet34", "4f:321", "bn"),
-                                            ("resnet34", "4f:321", "both")])
-def test_ride_sgd_in_backward_launches_is_bit_exact(arch, plan, kind, monkeypatch):
+@pytest.mark.parametrize("arch,plan", [("resnet18", "4f:321"), ("resnet34", "4f:321"), ("resnet34", "4f:3;3:21")])
+def test_ride_sgd_in_backward_launches_is_bit_exact(arch, plan, monkeypatch):
     """make_train_step(ride=True): the SGD (momentum, dampening, weight decay, first step after
     the reset) of layer4 + fc — and, with the two-group plan, of layer3 after its early gradient
     fold — runs in extra blocks of later layers' grouped conv-backward launches (k_conv_pair's
     rider role, the same element update as k_sgd: csrc/include/kml_sgd.h); the end-of-step
     launch covers the rest.  Bit-identical masters, momenta and shadows."""
     monkeypatch.setenv("KUBEML_RIDE_PLAN", plan)
-    monkeypatch.setenv("KUBEML_RIDE_HOSTKIND", kind)       # grouped conv backward / BN backward apply
     ua, spa, la = _graphed_run(False, ride=True, arch=arch)
     ub, spb, lb = _graphed_run(False, ride=False, arch=arch)
     assert float(ub.abs().max()) > 1e-5

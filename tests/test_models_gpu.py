@@ -351,7 +351,7 @@ def test_resnet34_bn_fold_matches_unfolded():
     y = torch.randint(0, 1000, (64,), device=dev)
     from kubeml_amd.ops import kernels as K
     res, applies = [], []
-    old = fused._BN_FOLD, fused._FOLD_GROUP, K._BNIN_ONESHOT
+    old = fused._BN_FOLD, fused._FOLD_GROUP
     real = K.bn_apply
     n = [0]
 
@@ -361,8 +361,7 @@ def test_resnet34_bn_fold_matches_unfolded():
     K.bn_apply = counting
     try:
         for fold, group in ((False, False), (True, False)):
-            # the one-shot BN-in path is opt-in (slower in the step); its numerics are checked here
-            fused._BN_FOLD, fused._FOLD_GROUP, K._BNIN_ONESHOT = fold, group, fold
+            fused._BN_FOLD, fused._FOLD_GROUP = fold, group
             n[0] = 0
             torch.manual_seed(3)
             m = resnet34(1000).to(dev)
@@ -378,57 +377,14 @@ def test_resnet34_bn_fold_matches_unfolded():
                         m.layer4[1].bn1.running_mean.clone()))
             applies.append(n[0])
     finally:
-        fused._BN_FOLD, fused._FOLD_GROUP, K._BNIN_ONESHOT = old
+        fused._BN_FOLD, fused._FOLD_GROUP = old
         K.bn_apply = real
     (o0, l0, g0, rv0, rm0, r30, r40), (o1, l1, g1, rv1, rm1, r31, r41) = res
-    # every BasicBlock's bn1 folds (halo: layers 1-2, one-shot panels: layers 3-4), and every
-    # block output that feeds a non-downsampling block is applied by that block's first conv
-    assert applies[0] - applies[1] == 16 + 12, applies
+    # the bn1 of every BasicBlock whose second conv runs on the halo kernel (layers 1-2: 3 + 4)
+    # folds, and so does every block output that feeds a non-downsampling halo block (5)
+    assert applies[0] - applies[1] == 7 + 5, applies
     assert torch.equal(r31, r30) and torch.equal(r41, r40)
     # the rows are summed in the BN apply kernel's own order and arithmetic: bit-identical
     assert torch.equal(o1, o0), _rel(o1, o0)
     assert l1 == l0 and torch.equal(rv1, rv0) and torch.equal(rm1, rm0)
     assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
-
-
-def test_resnet34_bnb_fold_matches_unfolded():
-    """The conv pair with its own BatchNorm backward folded into the dz staging
-    (fused._BNB_FOLD, kernels.conv_bwd(bnb=...)) vs a separate BN-backward launch: same loss,
-    every gradient within 1e-5 (same row order, same arithmetic), and the folded path really
-    replaces BN-backward launches."""
-    from kubeml_amd.models.resnet import resnet34
-    from kubeml_amd.nn import cross_entropy, flatten_module
-    from kubeml_amd.nn import fused
-    from kubeml_amd.ops import kernels as K
-    torch.manual_seed(0)
-    x = torch.randn(64, 32, 32, 8, device=dev).to(torch.bfloat16)
-    y = torch.randint(0, 1000, (64,), device=dev)
-    res, calls = [], []
-    old, real = fused._BNB_FOLD, K.bn_bwd
-    n = [0]
-
-    def counting(*a, **k):
-        n[0] += 1
-        return real(*a, **k)
-    try:
-        K.bn_bwd = counting
-        for fold in (False, True):
-            fused._BNB_FOLD = fold
-            n[0] = 0
-            torch.manual_seed(3)
-            m = resnet34(1000).to(dev)
-            sp = flatten_module(m)
-            m.train()
-            sp.zero_grad()
-            loss = cross_entropy(m(x), y)
-            loss.backward()
-            sp.finish_grads()
-            torch.cuda.synchronize()
-            res.append((float(loss), sp.grad.clone()))
-            calls.append(n[0])
-    finally:
-        fused._BNB_FOLD, K.bn_bwd = old, real
-    (l0, g0), (l1, g1) = res
-    assert l1 == l0
-    assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
-    assert calls[1] < calls[0] - 10, calls   # layer3 / layer4 BN backwards run inside the pairs

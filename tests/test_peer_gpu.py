@@ -162,7 +162,7 @@ def _run(rank, world, port, q, late):
         if not torch.allclose(t, _expect(world, 777, 900, dev, torch.float32, 1.0 / world), rtol=0, atol=1e-6):
             bad.append(("comm", 777))
         comm.check()
-        if not ar.self_test():
+        if not ar.self_test(kavg=True):       # gradient transport + the fused K-AVG round
             bad.append(("self_test",))
         errs = ar.errors()
         ar.close()
