@@ -1009,8 +1009,16 @@ __device__ __forceinline__ void IgemmBody<MODE, BM, BN, BK, TAPU>::run(const Con
                                                           reinterpret_cast<unsigned*>(smem));
 }
 
+// rider: an SGD range (kml_sgd.h) carried by the z-slices past the split-K slices of a WGRAD
+// launch (ResNet's stem weight gradient: 416 latency-bound tiles on 256 CUs, the last kernel of
+// the backward, carries the update of layers 2-3 — engine/dp.py ``ride``)
 template <int MODE, int BM, int BN, int BK, bool TAPU>
-__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a) {
+__global__ __launch_bounds__(256) void k_conv_igemm(ConvArgs a, KmlSgdRider rider) {
+  if (MODE == WGRAD && rider.blocks > 0 && (int)blockIdx.z >= a.splits) {
+    kml_sgd_rider_run(rider, (((int)blockIdx.z - a.splits) * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x +
+                                 (int)blockIdx.x);
+    return;
+  }
   using Body = IgemmBody<MODE, BM, BN, BK, TAPU>;
   __shared__ __attribute__((aligned(16))) char smem[Body::SMEM];
   Body::run(a, hw_blk(), smem);
@@ -1227,10 +1235,21 @@ int launch_glds(const ConvArgs& a, hipStream_t s) {
 template <int MODE, int BM, int BN, int BK>
 int launch(const ConvArgs& a, hipStream_t s) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.splits);
+  // a WGRAD launch takes the armed SGD rider (whole extra z-slices of gx * gy blocks)
+  KmlSgdRider rider{};
+  if constexpr (MODE == WGRAD) {
+    rider = kml_rider_take();
+    if (rider.blocks > 0) {
+      const int per = (int)(grid.x * grid.y);
+      const int ez = (rider.blocks + per - 1) / per;
+      rider.blocks = ez * per;
+      grid.z += ez;
+    }
+  }
   // K-tile inside one tap: FWD needs Cin % BK == 0; DGRAD/WGRAD tap math is already per-tile/per-column
   const bool tapu = (MODE != FWD) || (a.C % BK == 0);
-  if (tapu) hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, false>), grid, dim3(256), 0, s, a);
+  if (tapu) hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, true>), grid, dim3(256), 0, s, a, rider);
+  else hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, false>), grid, dim3(256), 0, s, a, rider);
   return (int)hipGetLastError();
 }
 
@@ -2271,7 +2290,7 @@ int dispatch_par(const ConvArgs& a, int bm, int bn, int bk, int variant, hipStre
   dim3 grid((a.N + bn - 1) / bn, (a.M + bm - 1) / bm, 1);
 #define KML_P(BMv, BNv, BKv)                                                                             \
   if (variant == 0 && bm == BMv && bn == BNv && bk == BKv) {                                             \
-    hipLaunchKernelGGL((k_conv_igemm<DGRAD, BMv, BNv, BKv, false>), grid, dim3(256), 0, s, a);           \
+    hipLaunchKernelGGL((k_conv_igemm<DGRAD, BMv, BNv, BKv, false>), grid, dim3(256), 0, s, a, KmlSgdRider{}); \
     return (int)hipGetLastError();                                                                       \
   }
 #define KML_PG(BMv, BNv, Sv, Vv)                                                                         \

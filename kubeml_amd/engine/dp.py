@@ -260,7 +260,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             peer_blocks=plan.max_blocks if plan is not None else 256, comm_timing=comm_timing,
                             shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1),
                             segment_shard=seg_shard)
-    step.ride_plan = (os.environ.get("KUBEML_RIDE_PLAN") or "4f:321") if riding else None
+    step.ride_plan = (os.environ.get("KUBEML_RIDE_PLAN") or "4f:321;123:s") if riding else None
     return step
 
 

@@ -8,8 +8,8 @@ embeddings) on the MI355X layers:
 * token-major bf16 activations ``[B*L, 768]``; fused QKV projection (one ``[T, 2304]`` GEMM
   per layer); the weight gradients (deterministic fp32 slab split-K) and FFN2's dgrad (FFN1's
   GELU backward in its epilogue) on the hand-written LDS-DMA MFMA kernel (csrc/kernels/gemm.hip);
-  the plain forward / dgrad GEMMs there too, or on hipBLASLt where ops/gemm_tuning.json
-  measured the library faster inside the step (BERT-base's shapes);
+  the plain forward / dgrad GEMMs there too, on the tile ops/gemm_tuning.json measured best per
+  shape (no library GEMM in the step);
 * attention is the fused flash-attention kernel (scores stay in LDS/registers);
 * LayerNorm with fused residual add, erf GELU, counter-based dropout (hidden dropout
   0.1, and attention-probability dropout 0.1 applied inside the fused attention kernels

@@ -152,6 +152,12 @@ class ResNet(tnn.Module):
         with self._chain(x):
             x = self._head(x)
             x = self.layer4(self.layer3(x))
+        # 1x1 maps: the classifier reads the last block's output as is, so its dgrad can hand that
+        # block's output-BN partial rows over (nn/modules.py _LinearFn)
+        last = self.layer4[-1]
+        object.__setattr__(self.fc, "_kml_bnf_block",
+                           last if (self.training and x.is_cuda and x.dim() == 4 and x.shape[1] * x.shape[2] == 1
+                                    and getattr(last, "_kml_plan", None) is not None) else None)
         x = self.avgpool(x)
         return self.fc(x)
 
@@ -206,22 +212,25 @@ class ResNet(tnn.Module):
         in extra blocks of its host convs' grouped backward launches, which all run after the
         group's gradients are final (backward order: fc, layer4, layer3, layer2, layer1).
         ``KUBEML_RIDE_PLAN`` = groups separated by ``;``, each ``<layers>:<host layers>`` with
-        ``f`` for fc: "4f:3;3:21" rides layer4 + fc on layer3's convs and layer3 on layer2's and
-        layer1's.  Layer3's 3x3 convs run unrolled; their deferred gradient fold runs when the
-        first layer-2 host takes its slice (the same single fold launch, earlier)."""
+        ``f`` for fc and host ``s`` for the stem conv: "4f:3;3:21" rides layer4 + fc on layer3's convs
+        and layer3 on layer2's and layer1's; "123:s" rides layers 1-3 on the stem's weight-gradient
+        launch (the last of the backward: 416 latency-bound tiles, kernels.conv_wgrad's rider
+        z-slices).  Layer3's 3x3 convs run unrolled; their deferred gradient fold runs when the
+        first host of a group holding layer3 takes its slice (the same single fold launch, earlier)."""
         import os
         spec = os.environ.get("KUBEML_RIDE_PLAN")
         if spec is None:
             # measured on ResNet-34 / CIFAR (BasicBlock); other depths ride only when asked
             if not isinstance(self.layer1[0], BasicBlock):
                 return []
-            spec = "4f:321"
+            spec = "4f:321;123:s"
         groups = []
         for part in filter(None, spec.split(";")):
             own, host = part.split(":")
             ps = [p for d in own for p in (self.fc if d == "f" else getattr(self, f"layer{d}")).parameters()]
             # the riders sit on the hosts' conv-backward pairs (BN-backward hosts measured no better)
-            hosts = [m for d in host for m in getattr(self, f"layer{d}").modules() if isinstance(m, M.Conv2d)]
+            hosts = [m for d in host for m in
+                     ([self.conv1] if d == "s" else getattr(self, f"layer{d}").modules()) if isinstance(m, M.Conv2d)]
             groups.append((ps, hosts))
         return groups
 

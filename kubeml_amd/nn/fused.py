@@ -55,11 +55,11 @@ def _wgrad_target(conv, x, unroll):
     return grad_out(conv.weight)
 
 
-def _wgrad(x, dc, conv, unroll=False):
+def _wgrad(x, dc, conv, unroll=False, rider=None):
     from ..ops import kernels as K
     kh, kw = conv.kernel_size
     dw, acc = _wgrad_target(conv, x, unroll)
-    K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc)
+    K.conv_wgrad(x, dc, dw, kh, kw, conv.stride, conv.padding, unroll=unroll, accumulate=acc, rider=rider)
     if unroll:
         conv.weight._kml_flat.defer_fold22(conv.weight, dw)
 
@@ -312,10 +312,7 @@ class ConvBNUnit:
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
             return dx, dres, part_out
-        _wgrad(x, dc, conv, unroll=wu is not None)
-        rider = _take_rider(conv)
-        if rider is not None:
-            rider.run_alone()
+        _wgrad(x, dc, conv, unroll=wu is not None, rider=_take_rider(conv))
         if need_dx:
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
                              addend=addend, bnf=bnf, wu=wu, bnf_mask=True)

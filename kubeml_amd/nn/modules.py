@@ -264,10 +264,23 @@ class _LinearFn(Function):
                 addend = None
             G.linear_wgrad_(dw4.view(op, ip), dy, ctx.x, accumulate=wacc)
         elif ctx.needs_input_grad[0]:
-            # dgrad + wgrad as one grouped launch
+            # dgrad + wgrad as one grouped launch; when this Linear reads a residual block's output
+            # directly (a classifier on 1x1 maps: ResNet on 32x32 input), the dgrad epilogue also
+            # emits that block's output-BN partial rows and applies its ReLU mask, so the block's
+            # BN backward skips its reduction pass (the nn/fused.py block-to-block hand-off)
             w = shadow_of(mod.weight).view(op, 1, 1, ip)
-            dx = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc, dbias=dbias,
-                            bias_accumulate=bacc).view(B, ip)
+            blk = getattr(mod, "_kml_bnf_block", None)
+            saved = getattr(blk, "_kml_last_saved", None) if blk is not None else None
+            bnf = None
+            if (saved is not None and saved[2] is not None and addend is None and ctx.x.is_cuda and
+                    tuple(saved[1].shape) == (B, 1, 1, ip) and saved[2].data_ptr() == ctx.x.data_ptr()):
+                bnf = (saved[2], saved[1], saved[3], saved[4])
+            r = K.conv_bwd(dy4, w, x4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc, dbias=dbias,
+                           bias_accumulate=bacc, bnf=bnf, bnf_mask=bnf is not None)
+            if bnf is not None:
+                r, part = r
+                object.__setattr__(blk, "_kml_in_partial", (r.data_ptr(), part))
+            dx = r.view(B, ip)
         else:
             K.conv_wgrad(x4, dy4, dw4, 1, 1, (1, 1), (0, 0), accumulate=wacc, dbias=dbias, bias_accumulate=bacc)
         if ctx.has_bias and not bias_done:

@@ -28,15 +28,10 @@ if os.path.exists(_TUNE_FILE):   # KUBEML_GEMM_TUNING_FILE=none: every GEMM on i
         for e in json.load(f).get("entries", []):
             _TUNED[(e["layout"], e["M"], e["N"], e["K"])] = (tuple(e["tile"]), int(e.get("splits", 1)))
 
-# A table entry with tile ["blas"] runs that forward / dgrad GEMM on hipBLASLt (torch.mm /
-# addmm) — only where the GEMM is plain (bias or a C addend, no fused activation) and the
-# library kernel measured faster inside the step.
-BLAS = ("blas",)
-
-
-def _blas(layout, M, N, K) -> bool:
-    t = _TUNED.get((layout, M, N, K))
-    return t is not None and t[0] == BLAS
+# Every GEMM runs on the hand-written MFMA kernels of gemm.hip: the round-5 table still sent 11
+# plain forward / dgrad BERT shapes to hipBLASLt; round 6 routes them to their best measured
+# hand tile (profiles/r6/gemm/blas_shapes.jsonl: 0.83-0.96x the library on the 16384-token
+# shapes, 1.4-1.7x on the MLM head's 2432-token ones).
 
 _ZP = {}
 
@@ -70,7 +65,7 @@ def plan(layout: int, M: int, N: int, K: int):
     general choice — 128x128 two-stage tiles (two blocks per CU hide each other's
     prologue / epilogue), split-K when the output tiles cannot fill 256 CUs."""
     t = _TUNED.get((layout, M, N, K))
-    if t is not None and t[0] != BLAS:
+    if t is not None:
         return t
     tile = (128, 128, 2)
     tiles = _cdiv(M, 128) * _cdiv(N, 128)
@@ -149,24 +144,12 @@ def wgrad_splitk_(dw, a, lda, b, ldb, M, N, K, beta=1.0, tile=(256, 256, 8), spl
 
 def linear_fwd(x, w, bias=None, act=0, pre=None, bias16=None):
     """y[T, op] = act(x[T, ip] @ w[op, ip]^T + bias); ``pre`` receives the pre-activation.
-    bias16: the bias's bf16 shadow, used by the library route (whose epilogue takes a bias of
-    the output type) instead of a conversion per call."""
+    bias16: accepted for API compatibility (the MFMA epilogue adds the fp32 bias)."""
     T, ip = x.shape
     op = w.shape[0]
     if w.shape[1] != ip:
         raise ValueError(f"linear_fwd: x {tuple(x.shape)} vs w {tuple(w.shape)}")
     y = torch.empty((T, op), dtype=BF16, device=x.device)
-    if _blas(0, T, op, ip) and (act == 0 and pre is None or act == 1 and pre is not None):
-        # act 1 (erf-GELU, pre-activation kept): the library GEMM writes pre, one pass applies GELU
-        z = y if act == 0 else pre
-        if bias is None:
-            torch.mm(x, w.t(), out=z)
-        else:
-            b16 = bias16[:op] if bias16 is not None else bias[:op].to(BF16)
-            torch.addmm(b16, x, w.t(), out=z)
-        if act == 1:
-            HIP.call("kml_gelu_fwd", "p p l s", pre.data_ptr(), y.data_ptr(), pre.numel(), stream_ptr())
-        return y
     gemm(x, ip, w, ip, y, op, T, op, ip, 0, 0, bias=bias, act=act, c2=pre)
     return y
 
@@ -183,9 +166,6 @@ def linear_dgrad(dy, w, addend=None):
         raise ValueError(f"linear_dgrad: dy {tuple(dy.shape)} vs w {tuple(w.shape)}")
     if addend is not None and (tuple(addend.shape) != (T, ip) or not addend.is_contiguous()):
         raise ValueError("linear_dgrad: addend must be a contiguous [T, ip] tensor")
-    if _blas(1, T, ip, op):
-        # the addend is a fresh residual gradient owned by this call: accumulate into it
-        return torch.mm(dy, w) if addend is None else addend.addmm_(dy, w)
     dx = torch.empty((T, ip), dtype=BF16, device=dy.device)
     tile, splits = plan(1, T, ip, op)
     if splits > 1:

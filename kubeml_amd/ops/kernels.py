@@ -767,8 +767,8 @@ _S2_OK: dict = {}
 
 # 1x1 / stride-1 / pad-0 conv weight gradients are plain GEMMs (dw[K][C] = dy^T x over the
 # pixels).  ``wgrad_gemm.json`` maps (pixels, K, C) to the GEMM that measured faster than the
-# implicit-GEMM wgrad inside the step (tools/wgrad_1x1.py): ["blas"] (hipBLASLt, fp32 out,
-# beta 1) or ["slab", BM, BN, stages, splits] (gemm.hip's deterministic slab split-K).
+# implicit-GEMM wgrad inside the step (tools/wgrad_1x1.py): ["slab", BM, BN, stages, splits]
+# (gemm.hip's deterministic slab split-K) or ["gather", ...] (the implicit GEMM on the GEMM tiles).
 _WGRAD_GEMM_FILE = os.environ.get("KUBEML_WGRAD_GEMM_FILE") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "wgrad_gemm.json")
 _WGRAD_GEMM: dict = {}
@@ -782,7 +782,7 @@ if os.path.exists(_WGRAD_GEMM_FILE):
 
 def wgrad_gemm_route(x_shape, K, KH, KW, stride, pad, dbias=None):
     """The table's GEMM route for this conv's weight gradient, or None (implicit-GEMM wgrad):
-    ["blas"] / ["slab", ...] for 1x1/s1 convs (a plain GEMM), ["gather", BM, BN, stages, splits] for
+    ["slab", ...] for 1x1/s1 convs (a plain GEMM), ["gather", BM, BN, stages, splits] for
     the implicit GEMM on the GEMM tiles (kml_gemm_conv_wgrad: square kernel, pad (KH - 1) / 2)."""
     if not _WGRAD_GEMM or dbias is not None or KH != KW or stride[0] != stride[1]:
         return None
@@ -792,6 +792,8 @@ def wgrad_gemm_route(x_shape, K, KH, KW, stride, pad, dbias=None):
         return None
     if r[0] == "gather":
         ok = tuple(pad) == ((KH - 1) // 2,) * 2 and C % 8 == 0 and K % 4 == 0
+    elif r[0] != "slab":
+        raise ValueError(f"wgrad_gemm.json: unknown route {r!r} (slab / gather: hand-written GEMMs only)")
     else:
         ok = (KH, KW) == (1, 1) and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
     return r if ok else None
@@ -818,12 +820,6 @@ def _wgrad_gemm(route, x, dy, dw, accumulate, stride=(1, 1)):
                  int(splits), _s())
         return dw
     x2, dy2, dw2 = x.reshape(P, C), dy.reshape(P, K), dw.view(K, C)
-    if route[0] == "blas":
-        if accumulate:
-            torch.addmm(dw2, dy2.t(), x2, out_dtype=F32, out=dw2)
-        else:
-            torch.mm(dy2.t(), x2, out_dtype=F32, out=dw2)
-        return dw
     from . import gemm as G
     _, bm, bn, st, splits = route
     G.wgrad_splitk_(dw2, dy2, K, x2, C, K, C, P, beta=1.0 if accumulate else 0.0,
@@ -1063,7 +1059,7 @@ def _chk_dbias(dbias, K, KH, KW, stride, pad):
 
 
 def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulate=True, dbias=None,
-               bias_accumulate=True):
+               bias_accumulate=True, rider=None):
     """Conv weight gradient into dw[Cout,KH,KW,Cin] (fp32): ``dw += wgrad`` (accumulate) or
     ``dw = wgrad`` (overwrite: the buffer need not be zeroed).  Deterministic: one writer per
     element, split-K partials summed in split order.  unroll: an unrolled conv
@@ -1082,7 +1078,8 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulat
         if not unrolled22(H, W, KH, KW, stride, pad) or tuple(dw.shape) != (4 * K, 1, 1, 4 * C):
             raise ValueError("unrolled wgrad: needs the [4K,1,1,4C] fp32 scratch")
         _, x1, _, _ = _u22_views(B, C, K, x=x)
-        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, accumulate=False)
+        return conv_wgrad(x1, dy.reshape(B, 1, 1, 4 * K), dw, 1, 1, (1, 1), (0, 0), cfg=cfg, accumulate=False,
+                          rider=rider)
     B, H, W, C = x.shape
     K = dy.shape[3]
     sh, sw = stride
@@ -1092,15 +1089,19 @@ def conv_wgrad(x, dy, dw, KH, KW, stride, pad, cfg=None, unroll=False, accumulat
         raise ValueError("wgrad shape mismatch")
     route = None if cfg is not None else wgrad_gemm_route(x.shape, K, KH, KW, stride, pad, dbias)
     if route is not None:
-        return _wgrad_gemm(route, x, dy, dw, accumulate, stride)
+        r = _wgrad_gemm(route, x, dy, dw, accumulate, stride)
+        if rider is not None:
+            rider.run_alone()
+        return r
     r0, r1, s0, s1 = tap_window(H, W, KH, KW, sh, sw, ph, pw)
     cfg = _norm_cfg(cfg or plan_conv("wgrad", K, (r1 - r0) * (s1 - s0) * C, B * OH * OW))
     bm, bn, bk, splits, variant = cfg
     _chk_dbias(dbias, K, KH, KW, stride, pad)
     slab, cnt = _wgrad_ws(dw.device, B, H, W, C, K, KH, KW, stride, pad, cfg, dbias is not None)
-    HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i p p p i s",
-             _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant,
-             int(bool(accumulate)), _p(slab), _p(cnt), _p(dbias), int(bool(bias_accumulate)), _s())
+    with _Riding(rider):   # the register-staged wgrad carries it in extra z-slices (else its own launch)
+        HIP.call("kml_conv_wgrad", "p p p i i i i i i i i i i i i i i i i i p p p i s",
+                 _p(x), _p(dy), _p(dw), B, H, W, C, K, KH, KW, sh, sw, ph, pw, bm, bn, bk, splits, variant,
+                 int(bool(accumulate)), _p(slab), _p(cnt), _p(dbias), int(bool(bias_accumulate)), _s())
     return dw
 
 

@@ -272,12 +272,15 @@ def test_ride_plan_groups_and_rest_ranges(monkeypatch):
     m = resnet18(10)
     sp = flatten_module(m)
     monkeypatch.delenv("KUBEML_RIDE_PLAN", raising=False)
-    (ps, hosts), = m.ride_plan()
+    (ps, hosts), (ps2, hosts2) = m.ride_plan()   # default "4f:321;123:s"
     assert {id(p) for p in ps} == {id(p) for p in list(m.layer4.parameters()) + list(m.fc.parameters())}
     assert len(hosts) == 5 + 5 + 4          # layer3 (with its downsample), layer2 (same), layer1
+    assert {id(p) for p in ps2} == {id(p) for d in (1, 2, 3) for p in getattr(m, f"layer{d}").parameters()}
+    assert [id(h) for h in hosts2] == [id(m.conv1)]   # the stem's weight-gradient launch
     lo, hi = sp.range_of(ps)
-    assert lo == 0 and 0 < hi < sp.numel     # later layers sit first in the flat layout
-    assert ride_rest([(lo, hi)], sp.numel) == [(hi, sp.numel)]
+    lo2, hi2 = sp.range_of(ps2)
+    assert lo == 0 and 0 < hi == lo2 < hi2 < sp.numel   # later layers sit first in the flat layout
+    assert ride_rest([(lo, hi), (lo2, hi2)], sp.numel) == [(hi2, sp.numel)]   # the stem's own update
     monkeypatch.setenv("KUBEML_RIDE_PLAN", "4f:3;3:21")
     g = m.ride_plan()
     assert len(g) == 2 and not {id(h) for h in g[0][1]} & {id(h) for h in g[1][1]}

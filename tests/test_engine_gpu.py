@@ -238,7 +238,8 @@ def _graphed_run(opt_overlap, steps=3, ride=False, arch="resnet18"):
     return sp.master - w0, sp, losses
 
 
-@pytest.mark.parametrize("arch,plan", [("resnet18", "4f:321"), ("resnet34", "4f:321"), ("resnet34", "4f:3;3:21")])
+@pytest.mark.parametrize("arch,plan", [("resnet18", "4f:321"), ("resnet34", "4f:321"), ("resnet34", "4f:3;3:21"),
+                                       ("resnet34", "4f:321;23:s"), ("resnet34", "4f:321;123:s")])
 def test_ride_sgd_in_backward_launches_is_bit_exact(arch, plan, monkeypatch):
     """make_train_step(ride=True): the SGD (momentum, dampening, weight decay, first step after
     the reset) of layer4 + fc — and, with the two-group plan, of layer3 after its early gradient

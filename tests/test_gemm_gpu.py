@@ -161,36 +161,9 @@ def test_linear_dgrad_addend_paths():
         add = _rand(T, ip)
         ref = G.linear_dgrad(dy, w)
         want = (ref.float() + add.float()).to(torch.bfloat16)
-        out = G.linear_dgrad(dy, w, addend=add)        # may accumulate into the addend (library route)
-        if G._blas(1, T, ip, op):                      # hipBLASLt: C added in fp32 before the rounding
-            assert _rel(out, want) < 1e-2
-        elif G.plan(1, T, ip, op)[1] == 1:
+        out = G.linear_dgrad(dy, w, addend=add)
+        if G.plan(1, T, ip, op)[1] == 1:
             torch.testing.assert_close(out, want, rtol=0, atol=0)
         else:   # fp32 split-K atomics: summation order differs run to run
             assert _rel(out, want) < 1e-2
 
-
-def test_library_gemm_routes_match_torch(monkeypatch):
-    """Table entries with tile ["blas"] (plain GEMMs measured faster on hipBLASLt inside the
-    BERT step): forward + bias, forward + erf-GELU with the pre-activation kept (library GEMM
-    then the GELU pass), dgrad with and without the residual addend — against fp32 torch."""
-    from kubeml_amd.ops import gemm as G
-    torch.manual_seed(5)
-    T, ip, op = 1024, 768, 1536
-    for key in [(0, T, op, ip), (1, T, ip, op)]:
-        monkeypatch.setitem(G._TUNED, key, (G.BLAS, 1))
-    x, w = _rand(T, ip), _rand(op, ip, scale=0.05)
-    b = torch.randn(op, device=dev)
-    h = x.float() @ w.float().t() + b
-    assert _rel(G.linear_fwd(x, w, b), h) < 1e-2
-    pre = torch.empty(T, op, dtype=torch.bfloat16, device=dev)
-    y = G.linear_fwd(x, w, b, act=1, pre=pre)
-    assert _rel(pre, h) < 1e-2
-    # the GELU pass applied to the stored pre-activation (at most a bf16 rounding step apart)
-    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(pre.float()), rtol=8e-3, atol=1e-3)
-    dy = _rand(T, op)
-    dx_ref = dy.float() @ w.float()
-    assert _rel(G.linear_dgrad(dy, w), dx_ref) < 1e-2
-    add = _rand(T, ip)
-    want = dx_ref + add.float()
-    assert _rel(G.linear_dgrad(dy, w, addend=add), want) < 1e-2

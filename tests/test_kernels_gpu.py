@@ -1325,10 +1325,10 @@ def test_kavg_async_snap_and_apply_match_torch(n, n_params):
     assert torch.equal(shadow, ref[:n_params].to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("route", [("blas",), ("slab", 128, 128, 2, 16)])
+@pytest.mark.parametrize("route", [("slab", 128, 128, 2, 16), ("slab", 128, 128, 2, 4)])
 def test_conv1x1_wgrad_gemm_routes(monkeypatch, route):
-    """1x1/s1 conv weight gradient on a GEMM route (wgrad_gemm.json): hipBLASLt or the slab
-    split-K kernel, stored and accumulated, alone and through conv_bwd (which then runs the
+    """1x1/s1 conv weight gradient on a GEMM route (wgrad_gemm.json): the slab split-K kernel
+    (hand-written; no library route is left), stored and accumulated, alone and through conv_bwd (which then runs the
     dgrad on its own) — against fp32 torch."""
     from kubeml_amd.ops import kernels as K
     torch.manual_seed(23)

@@ -1,8 +1,8 @@
 """Measured-table routing (no GPU needed): which GEMM runs a linear / 1x1-conv product.
 
-ops/gemm_tuning.json entries with tile ["blas"] send a plain forward / dgrad to hipBLASLt;
+ops/gemm_tuning.json picks a hand-written MFMA tile per shape (no library route is left);
 ops/wgrad_gemm.json sends a 1x1 / stride-1 conv weight gradient to gemm.hip's slab split-K.
-Everything not in a table stays on the hand-written kernels."""
+Everything not in a table stays on the hand-written kernels' default plans."""
 import json
 import os
 
@@ -12,18 +12,20 @@ from kubeml_amd.ops import kernels as K
 OPS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kubeml_amd", "ops")
 
 
-def test_library_entries_are_plain_bert_shapes_only():
+def test_every_gemm_route_is_a_hand_written_tile():
     d = json.load(open(os.path.join(OPS, "gemm_tuning.json")))
-    blas = [(e["layout"], e["M"], e["N"], e["K"]) for e in d["entries"] if e["tile"] == ["blas"]]
-    assert blas, "the shipped table routes BERT-base's plain GEMMs to the library"
-    assert all(layout in (0, 1) for layout, *_ in blas)          # never a weight gradient
-    # FFN2's dgrad keeps the hand-written kernel: its epilogue applies FFN1's GELU backward
-    assert (1, 16384, 3072, 768) not in blas
-    for key in blas:
-        assert G._blas(*key)
-        tile, _ = G.plan(*key)                 # kernel callers never see the library tile
-        assert tile != G.BLAS
-    assert not G._blas(0, 4096, 3072, 768)     # shapes outside the table: hand-written
+    assert d["entries"]
+    for e in d["entries"]:
+        key = (e["layout"], e["M"], e["N"], e["K"])
+        tile, splits = G.plan(*key)
+        base = tuple(t for t in tile if t != "slab")
+        assert base in G.TILES, (key, tile)    # a gemm.hip tile, never a library route
+        assert splits >= 1
+    for e in json.load(open(os.path.join(OPS, "wgrad_gemm.json")))["entries"]:
+        assert e["route"][0] in ("slab", "gather")
+    assert G.plan(0, 4096, 3072, 768)[0] in G.TILES    # shapes outside the table: default tile
+    import inspect
+    assert "torch.mm" not in inspect.getsource(G) and "addmm" not in inspect.getsource(G)
 
 
 def test_wgrad_gemm_route_only_for_plain_1x1():
@@ -40,7 +42,7 @@ def test_wgrad_gemm_route_only_for_plain_1x1():
     assert K.wgrad_gemm_route((B, hw, hw, e["C"] + 8), e["K"], 1, 1, (1, 1), (0, 0)) is None
     for r in d["entries"]:
         if r.get("KH", 1) == 1:
-            assert r["route"][0] in ("blas", "slab")
+            assert r["route"][0] == "slab"
         else:   # implicit-GEMM weight gradients on the GEMM tiles: only their exact geometry
             assert r["route"][0] == "gather"
             kh, st = r["KH"], r["S"]
