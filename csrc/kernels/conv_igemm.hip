@@ -1235,10 +1235,11 @@ int launch_glds(const ConvArgs& a, hipStream_t s) {
 template <int MODE, int BM, int BN, int BK>
 int launch(const ConvArgs& a, hipStream_t s) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.splits);
-  // a WGRAD launch takes the armed SGD rider (whole extra z-slices of gx * gy blocks)
+  // a WGRAD launch takes an armed SGD-range rider (whole extra z-slices of gx * gy blocks; a
+  // peer-shard slice, whose phase counts its blocks exactly, stays armed and runs alone)
   KmlSgdRider rider{};
   if constexpr (MODE == WGRAD) {
-    rider = kml_rider_take();
+    if (g_kml_rider.blocks > 0 && g_kml_rider.kind == KML_RIDER_SGD) rider = kml_rider_take();
     if (rider.blocks > 0) {
       const int per = (int)(grid.x * grid.y);
       const int ez = (rider.blocks + per - 1) / per;

@@ -325,6 +325,57 @@ KML_API int kml_rider_set(float* w, const float* g, float* mom, bf16_t* shadow, 
   return (int)hipSuccess;
 }
 
+// Arm a peer-shard slice (kml_sgd.h KmlZsRider; parallel/peer.py ShardRider) for the next
+// rider-capable launch: kind 1 = reduce-scatter + fused SGD of this rank's chunk vectors [v0, v1)
+// (w / mom / shadow at the segment, flags / data = every rank's flags area and fp32 gradient at the
+// segment), kind 2 = all-gather of the peers' bf16 shadow chunks (data = every rank's shadow at the
+// segment, shadow = the own).  Offsets / counts as in KmlZsRider; timeout_s bounds every wait.
+KML_API int kml_zs_rider_set(int kind, const void* const* flags, const void* const* data, void* own_flags, void* ctrl,
+                             int rank, int world, long long a, long long b, long long v0, long long v1, int ready,
+                             int wait, int done, int done_blocks, int done_word, int advance, double timeout_s,
+                             float* w, float* mom, bf16_t* shadow, const float* lr_ptr, const float* first_ptr,
+                             float wd, float momentum, float dampening, int nesterov, float grad_scale, int blocks) {
+  if ((kind != KML_RIDER_ZS_RS && kind != KML_RIDER_ZS_AG) || world < 1 || world > KML_ZS_MAX || rank < 0 ||
+      rank >= world || blocks <= 0 || !flags || !data || !own_flags || !ctrl || !shadow || v1 < v0 ||
+      done_word < 5 || done_word > 15 || (kind == KML_RIDER_ZS_RS && (!w || !lr_ptr)))
+    return (int)hipErrorInvalidValue;
+  KmlSgdRider r = {};
+  r.w = w;
+  r.mom = mom;
+  r.shadow = shadow;
+  r.lr_ptr = lr_ptr;
+  r.first_ptr = first_ptr;
+  r.wd = wd;
+  r.momentum = momentum;
+  r.dampening = dampening;
+  r.grad_scale = grad_scale;
+  r.nesterov = nesterov;
+  r.blocks = blocks;
+  r.n = 0;
+  r.kind = kind;
+  for (int p = 0; p < world; ++p) {
+    r.zs.flags[p] = static_cast<const char*>(flags[p]);
+    r.zs.data[p] = static_cast<const char*>(data[p]);
+  }
+  r.zs.own_flags = static_cast<unsigned*>(own_flags);
+  r.zs.ctrl = static_cast<unsigned*>(ctrl);
+  r.zs.rank = rank;
+  r.zs.world = world;
+  r.zs.a = a;
+  r.zs.b = b;
+  r.zs.v0 = v0;
+  r.zs.v1 = v1;
+  r.zs.ready = ready;
+  r.zs.wait = wait;
+  r.zs.done = done;
+  r.zs.done_blocks = done_blocks;
+  r.zs.done_word = done_word;
+  r.zs.advance = advance;
+  r.zs.limit = (unsigned long long)(timeout_s * 1e8);   // s_memrealtime runs at 100 MHz
+  g_kml_rider = r;
+  return (int)hipSuccess;
+}
+
 // run an armed rider as its own launch (a rider-capable call that took another path)
 KML_API int kml_rider_flush(hipStream_t s) {
   const KmlSgdRider r = kml_rider_take();

@@ -72,6 +72,16 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     comm = world > 1 or force_comm
     shard = None
     staged_shard = False
+    ride_shard = False
+    if plan is not None and plan.schedule == "shardride":
+        # the sharded update of the stages whose gradients are final early (ResNet: layer4 + fc,
+        # then layer3) rides in later backward launches of the same queue (_shard_ride)
+        ride_shard = (forward is None and hasattr(model, "comm_ride_plan") and
+                      getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges() and
+                      bool(model.comm_ride_plan()))
+        from ..parallel.plan import CommPlan
+        plan = CommPlan("peer", "shard", plan.wire, plan.max_blocks,
+                        source=plan.source + ("" if ride_shard else " (shardride -> shard: no ride plan / fused SGD)"))
     if plan is not None and plan.schedule == "shardov":
         # per-stage shard steps need stage-contiguous gradient ranges and the fused SGD
         staged_shard = (forward is None and hasattr(model, "stages") and hasattr(model, "stage_params") and
@@ -203,6 +213,8 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     if riding:
         fwd_bwd, opt_step = _ride(model, space, optimizer, fwd_bwd, post, lambda: fold, scale)
     shard_step = on_replay = seg_shard = None
+    step_ref = {}                 # the GraphedTrainStep (its _comm_on gates the shard riders)
+    shard_ride_info = None
     if shard is not None:
         blocks = plan.max_blocks
         fused_sgd = getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges()
@@ -247,11 +259,15 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                 if post is not None:
                     post()
 
+        if ride_shard and fused_sgd and fwd_bwd is not None and seg_shard is None:
+            fwd_bwd, shard_step, shard_ride_info = _shard_ride(model, space, optimizer, shard, fwd_bwd, post,
+                                                               lambda: fold, min(blocks, 512), step_ref)
+
         def on_replay():
             space._master_stale = True
 
     optimizer.set_grad_scale(scale)
-    step = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
+    step = step_ref["step"] = GraphedTrainStep(fwd_bwd, opt_step, [space.grad], group=group, use_graph=use_graph, warmup=warmup,
                             bucket_mb=bucket_mb, segments=segs, segment_grads=seg_grads, force_comm=force_comm,
                             graph_comm=graph_comm, comm_dtype=comm_dtype,
                             state_tensors=train_state_tensors(model, space, optimizer, extra_state),
@@ -261,7 +277,78 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                             shard_step=shard_step, on_replay=on_replay, world=max(int(world), 1),
                             segment_shard=seg_shard)
     step.ride_plan = (os.environ.get("KUBEML_RIDE_PLAN") or "4f:321;123:s") if riding else None
+    step.shard_ride = shard_ride_info   # {"slices": n, "taken": set of the last step's carried slices}
     return step
+
+
+def _shard_ride(model, space, optimizer, shard, fwd_bwd, post, get_fold, blocks, step_ref):
+    """make_train_step's ``shardride`` plan: ``model.comm_ride_plan()`` = [(parameters, RS hosts,
+    AG hosts)] for two early-final stages that must lead the flat layout (ResNet: layer4 + fc, then
+    layer3).  The shard is cut per stage (rank r owns chunk r of each); each stage's reduce-scatter
+    + fused SGD runs as :class:`~kubeml_amd.parallel.peer.ShardRider` slices in its RS hosts'
+    backward launches and its shadow all-gather in its AG hosts' launches (same queue, no side
+    stream; cross-rank progress counters, csrc/include/kml_sgd.h), so only the last stage (the rest
+    of the space: ResNet's layer2 + layer1 + stem, ~7 % of the bytes) remains after the backward.
+    The riders run only while the step's collectives are on (never in the local warm-up)."""
+    from ..parallel.peer import PeerShard
+    groups = model.comm_ride_plan()
+    if len(groups) != PeerShard.RIDER_STAGES:
+        raise ValueError(f"comm ride plan: {PeerShard.RIDER_STAGES} groups (parameters, RS hosts, AG hosts)")
+    ranges = [space.range_of(ps) for ps, _, _ in groups]
+    if ranges[0][0] != 0 or ranges[0][1] != ranges[1][0] or not ranges[1][1] < space.numel:
+        raise ValueError("comm ride plan: the riding stages must lead the flat layout, in backward order")
+    space.sync_master()                # collective: the master is complete before the ownership switch
+    shard.set_stages([ranges[0], ranges[1], (ranges[1][1], space.numel)])
+    riders, seen = [], set()           # (group, kind, ShardRider), in phase order
+    holder = {}
+
+    def take_for(j):
+        return lambda: holder["take"](j)
+    for gi, (ps, rs_hosts, ag_hosts) in enumerate(groups):
+        for kind, hosts in (("rs", rs_hosts), ("ag", ag_hosts)):
+            if not hosts or any(id(h) in seen for h in hosts):
+                raise ValueError("comm ride plan: every phase needs host convs of its own")
+            seen.update(id(h) for h in hosts)
+            for h, r in zip(hosts, shard.rider_slices(gi, kind, len(hosts), optimizer, blocks)):
+                riders.append((gi, kind, r))
+                object.__setattr__(h, "_kml_rider", take_for(len(riders) - 1))
+    state = {"active": False, "taken": set(), "fired": set()}
+
+    def _take(j):
+        gi, kind, r = riders[j]
+        if not state["active"] or j in state["taken"]:
+            return None
+        if kind == "rs" and gi not in state["fired"]:
+            space.finish_grads(groups[gi][0])   # e.g. layer3's deferred unrolled-weight folds, here
+            state["fired"].add(gi)
+        state["taken"].add(j)
+        return r
+    holder["take"] = _take
+
+    def ride_fwd_bwd():
+        st = step_ref.get("step")
+        state["active"] = st is not None and st.comm and st._comm_on
+        state["taken"], state["fired"] = set(), set()
+        try:
+            return fwd_bwd()
+        finally:
+            state["active"] = False
+
+    def shard_step(stamps=None):
+        """The rest of the space after the backward (stage 2), plus any slice whose host did not
+        carry it (in phase order; on ResNet every host conv runs a rider-capable launch)."""
+        left = [j for j in range(len(riders)) if j not in state["taken"]]
+        if left:
+            _log.warning("shard riders: %d slice(s) ran on their own launch", len(left))
+            for j in left:
+                riders[j][2].run_alone()
+        space.finish_grads()
+        st = None if stamps is None else (stamps.data_ptr(), stamps.data_ptr() + 8)
+        shard.stage_step(2, optimizer, advance=get_fold(), max_blocks=blocks, first_stage=True, last_stage=True,
+                         stamps=st)
+        if post is not None:
+            post()
+    return ride_fwd_bwd, shard_step, {"slices": len(riders), "state": state}
 
 
 def ride_rest(covered, numel):

@@ -234,6 +234,23 @@ class ResNet(tnn.Module):
             groups.append((ps, hosts))
         return groups
 
+    def comm_ride_plan(self):
+        """[(parameters, RS host convs, AG host convs)] of the peer-shard riders (engine/dp.py
+        ``shardride``, N > 1): layer4 + fc (62 % of ResNet-34's gradient bytes) reduce-scatter + SGD
+        in layer3's backward launches and all-gather in the first half of layer2's; layer3 (31 %)
+        reduce-scatters + SGD in the second half of layer2's and all-gathers in layer1's.  Only
+        layer2 + layer1 + stem (7 %) remain after the backward.  BasicBlock nets only (measured
+        plan), [] otherwise."""
+        if not isinstance(self.layer1[0], BasicBlock):
+            return []
+
+        def convs(layer):
+            return [m for m in layer.modules() if isinstance(m, M.Conv2d)]
+        l2 = convs(self.layer2)
+        half = len(l2) // 2
+        return [(list(self.layer4.parameters()) + list(self.fc.parameters()), convs(self.layer3), l2[:half]),
+                (list(self.layer3.parameters()), l2[half:], convs(self.layer1))]
+
     def stage_params(self):
         """Parameters owned by each stage of :meth:`stages`."""
         later = ("layer2.", "layer3.", "layer4.", "fc.")

@@ -545,6 +545,59 @@ class PeerShard:
                  stamps[1] if (stamps is not None and last_stage) else None, self._stream())
         self.space._master_stale = True
 
+    # ------------------------------------------------------------------ rider slices
+    # Progress offsets of the step's rider phases (kml_sgd.h KmlZsRider): stage s (0 or 1) of a
+    # staged layout publishes READY = 2 s + 1 and DONE = 2 s + 2; the last AG phase advances the
+    # base by 4 for the next step.  ctrl words 5..7 count the finished blocks of RS-0, RS-1, AG-1.
+    RIDER_STAGES = 2
+
+    def rider_slices(self, seg: int, kind: str, n_hosts: int, optimizer, blocks: int = 256) -> List["ShardRider"]:
+        """The ``n_hosts`` slices of stage ``seg``'s reduce-scatter (``kind`` "rs": this rank's
+        chunk, summed over every rank's gradient, fused SGD, shadow chunk published) or all-gather
+        ("ag": the peers' shadow chunks) as riders (:class:`ShardRider`) for ``n_hosts`` later
+        backward launches — every rank must build the same slices (same hosts, same blocks)."""
+        if seg >= self.RIDER_STAGES or len(self.segments) <= seg:
+            raise ValueError("rider slices need a staged layout (set_stages) and stage 0 or 1")
+        if n_hosts < 1 or blocks < 1:
+            raise ValueError("rider slices: at least one host launch and one block")
+        sp = self.space
+        s0, s1, ch = self.segments[seg]
+        arr = ctypes.c_void_p * self.world
+        if kind == "rs":
+            lo = min(s1, s0 + self.rank * ch)
+            hi = min(s1, lo + ch)
+            if (hi - lo) % 4:
+                raise ValueError("rider RS: the own chunk must hold whole fp32x4 vectors")
+            a, b, nv = lo - s0, hi - s0, (hi - lo) // 4
+            data = arr(*[int(v) + 4 * s0 for v in self._grads])
+            g = optimizer.param_groups[0]
+            lr = optimizer.lr_tensor(sp.device)
+            mom = first = None
+            if g["momentum"] != 0:
+                mom = optimizer._bufs(sp, ["momentum"])["momentum"]
+                first = optimizer.first_tensor(sp.device)
+            sgd = dict(w=sp.master.data_ptr() + 4 * s0, mom=None if mom is None else mom.data_ptr() + 4 * s0,
+                       lr=lr, first=first, wd=g["weight_decay"], momentum=g["momentum"], dampening=g["dampening"],
+                       nesterov=int(g["nesterov"]), grad_scale=1.0 / self.world)
+            ready, wait, done, word, adv = 2 * seg + 1, 2 * seg + 1, 2 * seg + 2, 5 + seg, 0
+        elif kind == "ag":
+            a, b = ch, s1 - s0
+            nv = (self.world - 1) * (ch * 2 // 16)
+            data = arr(*[int(v) + 2 * s0 for v in self._shadows])
+            sgd = dict(w=None, mom=None, lr=None, first=None, wd=0.0, momentum=0.0, dampening=0.0, nesterov=0,
+                       grad_scale=1.0)
+            last = seg == self.RIDER_STAGES - 1
+            ready, wait, done, word, adv = 0, 2 * seg + 2, 0, 7, (4 if last else 0)
+            if not last:
+                word = 0      # no completion count for the first stage's gather
+        else:
+            raise ValueError(f"rider kind {kind!r}")
+        cuts = [nv * i // n_hosts for i in range(n_hosts + 1)]
+        total = n_hosts * blocks if word else 0
+        return [ShardRider(self, 1 if kind == "rs" else 2, data, a, b, cuts[i], cuts[i + 1], ready, wait, done,
+                           total, word if word else 5, adv, sp.shadow.data_ptr() + 2 * s0, blocks, sgd)
+                for i in range(n_hosts)]
+
     def gather_master(self, max_blocks: int = 256):
         """Collective: complete the fp32 master from the owners' chunks.  Entry barrier, gather,
         then an exit barrier: callers overwrite their own master chunk right after this (tail
@@ -636,6 +689,37 @@ class PeerShard:
         self.dist.barrier(group=self.group)
         self._release()
         self.dist.barrier(group=self.group)
+
+
+class ShardRider:
+    """One peer-shard slice carried by a later backward launch (csrc/include/kml_sgd.h KmlZsRider:
+    the conv pair's rider blocks, or its own launch when the host took another path): the same
+    arm() / run_alone() protocol as :class:`~kubeml_amd.ops.kernels.SgdRider`."""
+
+    def __init__(self, shard, kind, data, a, b, v0, v1, ready, wait, done, done_blocks, done_word, advance, shadow,
+                 blocks, sgd):
+        self.shard, self.kind, self.data = shard, kind, data
+        self.a, self.b, self.v0, self.v1 = int(a), int(b), int(v0), int(v1)
+        self.ready, self.wait, self.done = int(ready), int(wait), int(done)
+        self.done_blocks, self.done_word, self.advance = int(done_blocks), int(done_word), int(advance)
+        self.shadow, self.blocks, self.sgd = int(shadow), int(blocks), sgd
+
+    def arm(self):
+        sh, g = self.shard, self.sgd
+        if sh.region is None:
+            raise PeerCommError("shard rider used after close()")
+        HIP.call("kml_zs_rider_set", "i p p p p i i l l l l i i i i i i d p p p p p f f f i f i", self.kind,
+                 ctypes.addressof(sh._flags), ctypes.addressof(self.data), sh.region, sh.ctrl, sh.rank, sh.world,
+                 self.a, self.b, self.v0, self.v1, self.ready, self.wait, self.done, self.done_blocks,
+                 self.done_word, self.advance, sh.timeout_s, g["w"], g["mom"], self.shadow,
+                 None if g["lr"] is None else g["lr"].data_ptr(),
+                 None if g["first"] is None else g["first"].data_ptr(), float(g["wd"]), float(g["momentum"]),
+                 float(g["dampening"]), int(g["nesterov"]), float(g["grad_scale"]), self.blocks)
+
+    def run_alone(self):
+        """The same slice as its own launch (its host took a path without a rider role)."""
+        self.arm()
+        HIP.call("kml_rider_flush", "s", torch.cuda.current_stream(self.shard.device).cuda_stream)
 
 
 def verified_shard(space, group=None, log=None) -> Optional[PeerShard]:

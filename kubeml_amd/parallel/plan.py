@@ -15,7 +15,10 @@ gradient all-reduce:
   bf16 weights, which is what the forward computes with anyway); ``"shardov"`` — the same
   per backward stage on a side stream: each stage's reduce-scatter + SGD + all-gather runs as
   soon as its gradients are final, beside the backward of the stages before it (fused SGD,
-  models with ``stages()``; otherwise it runs as ``"shard"``).
+  models with ``stages()``; otherwise it runs as ``"shard"``); ``"shardride"`` — the same per
+  stage for the stages whose gradients are final early (``model.comm_ride_plan()``: ResNet's
+  layer4 + fc, then layer3), but as rider blocks of later backward launches on the SAME queue
+  (peer.ShardRider), so only the rest of the space is exchanged after the backward.
 * ``wire``     fp32, or bf16 (half the link bytes; the sum accumulates in fp32).
 * ``max_blocks`` the grid cap of every peer launch (the CUs the collective may hold).
 
@@ -55,9 +58,9 @@ class CommPlan:
     def __post_init__(self):
         if self.backend not in ("peer", "rccl"):
             raise ValueError(f"backend must be peer or rccl, not {self.backend!r}")
-        if self.schedule not in ("end", "overlap", "shard", "shardov"):
-            raise ValueError(f"schedule must be end, overlap, shard or shardov, not {self.schedule!r}")
-        if self.schedule in ("shard", "shardov") and self.backend != "peer":
+        if self.schedule not in ("end", "overlap", "shard", "shardov", "shardride"):
+            raise ValueError(f"schedule must be end, overlap, shard, shardov or shardride, not {self.schedule!r}")
+        if self.schedule in ("shard", "shardov", "shardride") and self.backend != "peer":
             raise ValueError("the shard schedules run on the peer backend")
         if self.wire not in _WIRES:
             raise ValueError(f"wire must be fp32 or bf16, not {self.wire!r}")

@@ -771,7 +771,7 @@ class KubeModel(ABC):
         (one that does not is closed — collectively: every rank sees the same sizes)."""
         if plan.backend != "peer":
             return None
-        if plan.schedule in ("shard", "shardov"):    # both run on the PeerShard of this model's space
+        if plan.schedule in ("shard", "shardov", "shardride"):   # all run on the PeerShard of this model's space
             sh = self._shards.get(id(comm))
             return sh if sh is not None and sh.region is not None else None
         gp = getattr(comm, "grad_peer", None)

@@ -122,6 +122,9 @@ def _rank_main(rank, world, port, q, cases):
             shadow_ok = bool(torch.equal(sp.shadow, sp.master.to(torch.bfloat16)))
             res = {"transport": transport, "digests": digests, "shadow_is_bf16_master": shadow_ok,
                    "finite": bool(torch.isfinite(sp.master).all())}
+            ride = getattr(step, "shard_ride", None)
+            if ride is not None:   # slices carried by the backward launches of the last replay's capture
+                res["ride_slices"], res["ride_taken"] = ride["slices"], len(ride["state"]["taken"])
             if rank == 0:
                 ref = _reference_update(world, dev, opt_kind).cpu()
                 res["rel"] = float((upd1 - ref).norm() / ref.norm())
@@ -162,7 +165,8 @@ def _spawn(world, cases):
 
 CASES = [("peer:end:fp32:256", "sgd", 4), ("peer:end:bf16:256", "sgd", 4), ("peer:shard:fp32:256", "sgd", 4),
          ("peer:shard:fp32:256", "sgdm", 3), ("peer:shard:fp32:256", "adamw", 3),
-         ("peer:shardov:fp32:64", "sgd", 4), ("peer:shardov:fp32:64", "sgdm", 3)]
+         ("peer:shardov:fp32:64", "sgd", 4), ("peer:shardov:fp32:64", "sgdm", 3),
+         ("peer:shardride:fp32:256", "sgd", 4), ("peer:shardride:fp32:256", "sgdm", 3)]
 
 
 def _check(world, res):
@@ -175,6 +179,8 @@ def _check(world, res):
         # every rank holds bit-identical weights after the replays
         assert all(r["digests"] == rs[0]["digests"] for r in rs), (key, [r["digests"] for r in rs])
         assert all(r["shadow_is_bf16_master"] for r in rs), key
+        if ":shardride:" in spec:   # every slice rode a backward launch (none ran on its own)
+            assert all(r["ride_slices"] > 0 and r["ride_taken"] == r["ride_slices"] for r in rs), key
         rel = rs[0]["rel"]
         if ":bf16:" in spec:
             assert 0 < rel < 1e-2, (key, rel)
