@@ -123,19 +123,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t kml_zs_rsrc(const void* p) {
 }
 constexpr int KML_ZS_SYS = 17;  // buffer cache-policy bits sc0 | sc1: system-coherent access
 
-// thread 0: store `value` into rank r's progress word of every peer's flags area.  Relaxed at system
-// scope, no release fence (a system-scope release writes back the XCD's whole L2 — the running conv
-// tiles' dirty lines — in every block that publishes): what a flag hands over is either complete
-// before this launch (READY: the gradients, written back at the kernel boundary) or was stored
-// write-through at system scope and drained by every storing wave before the phase count reached
-// this block (DONE: the shadow chunk) — CDNA guide §6 G16, R1
+// thread 0: store `value` into rank r's progress word of every peer's flags area, relaxed at system
+// scope.  DONE needs no fence: the shadow chunk it hands over was stored write-through at system
+// scope and drained by every storing wave before the phase count reached this block.  READY (the
+// gradients, written by earlier launches) takes the release the standalone shard kernels' block 0
+// takes (comm.hip pc_barrier) — one wave per slice (a system release writes back the XCD's L2: in
+// every rider block it would sweep the running conv tiles' working set each time)
+template <bool RELEASE = false>
 __device__ __forceinline__ void kml_zs_publish(const KmlZsRider& z, unsigned value) {
   if (threadIdx.x != 0) return;
 #pragma unroll
   for (int p = 0; p < KML_ZS_MAX; ++p)
     if (p < z.world)
       __hip_atomic_store(reinterpret_cast<unsigned*>(const_cast<char*>(z.flags[p])) + KML_ZS_PROGRESS + z.rank, value,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                         RELEASE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // every thread: true once every rank's progress reached `target` in time (false at once when the
@@ -166,17 +167,23 @@ __device__ inline bool kml_zs_wait(const KmlZsRider& z, unsigned target) {
 }
 
 // end of a rider block: count it toward its phase; the block completing the phase resets the
-// counter, publishes DONE (after every block's write-through stores drained) and advances the base
+// counter, publishes DONE (after every block's write-through stores drained) and advances the base.
+// Relaxed atomics only: an agent-scope release / acquire writes back / invalidates the XCD's L2
+// (the conv tiles' working set) and, taken by every rider block, cost the host launches more than
+// the slice's own traffic (profiles/r6/shardride.md).  What DONE hands over was stored write-through
+// at system scope and drained (vmcnt(0)) by every wave before its block counted itself; the counter
+// and the base are atomics the memory side serialises, read by later launches or this phase's last
+// block only.
 __device__ inline void kml_zs_finish(const KmlZsRider& z, unsigned base) {
   if (z.done_blocks <= 0) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's system-scope stores have landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(z.ctrl + z.done_word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(z.ctrl + z.done_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (unsigned)z.done_blocks - 1u) {
       __hip_atomic_store(z.ctrl + z.done_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (z.done) kml_zs_publish(z, base + (unsigned)z.done);
-      if (z.advance) __hip_atomic_fetch_add(z.ctrl + KML_ZS_BASE, (unsigned)z.advance, __ATOMIC_RELEASE,
+      if (z.advance) __hip_atomic_fetch_add(z.ctrl + KML_ZS_BASE, (unsigned)z.advance, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -188,7 +195,7 @@ __device__ inline void kml_zs_finish(const KmlZsRider& z, unsigned base) {
 __device__ inline void kml_zs_rs_run(const KmlSgdRider& r, int b) {
   const KmlZsRider& z = r.zs;
   const unsigned base = __hip_atomic_load(z.ctrl + KML_ZS_BASE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (z.ready && b == 0) kml_zs_publish(z, base + (unsigned)z.ready);   // block 0 of each RS slice
+  if (z.ready && b == 0) kml_zs_publish<true>(z, base + (unsigned)z.ready);   // block 0 of each RS slice
   const bool ok = kml_zs_wait(z, base + (unsigned)z.wait);
   const float lr = *r.lr_ptr;
   const int first = r.first_ptr ? (*r.first_ptr != 0.f) : 0;

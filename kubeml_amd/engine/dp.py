@@ -23,6 +23,10 @@ from .step import GraphedTrainStep, train_state_tensors
 
 _log = logging.getLogger("kubeml.dp")
 
+# rider blocks per shard-rider slice (``shardride``): a slice alone runs fastest at 256 (1.05M
+# elements: 9.7 us at 256, 11.6 at 512, 16.7 at 1024 blocks; tools/diag/zs_rider_micro.py)
+SHARD_RIDE_BLOCKS = 256
+
 
 def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable, x: torch.Tensor,
                     y: torch.Tensor, *, pre: Optional[Callable[[], None]] = None,
@@ -261,7 +265,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
 
         if ride_shard and fused_sgd and fwd_bwd is not None and seg_shard is None:
             fwd_bwd, shard_step, shard_ride_info = _shard_ride(model, space, optimizer, shard, fwd_bwd, post,
-                                                               lambda: fold, min(blocks, 512), step_ref)
+                                                               lambda: fold, min(blocks, SHARD_RIDE_BLOCKS), step_ref)
 
         def on_replay():
             space._master_stale = True

@@ -152,14 +152,18 @@ class ResNet(tnn.Module):
         with self._chain(x):
             x = self._head(x)
             x = self.layer4(self.layer3(x))
-        # 1x1 maps: the classifier reads the last block's output as is, so its dgrad can hand that
-        # block's output-BN partial rows over (nn/modules.py _LinearFn)
+        return self._classify(x)
+
+    def _classify(self, x):
+        """avgpool + fc of layer4's output, on every forward path (plain and staged): at 1x1 maps
+        the classifier reads the last block's output as is, so its dgrad can hand that block's
+        output-BN partial rows over (nn/modules.py _LinearFn); the hand-off flag is decided here
+        for each forward, never left over from another path's forward."""
         last = self.layer4[-1]
         object.__setattr__(self.fc, "_kml_bnf_block",
                            last if (self.training and x.is_cuda and x.dim() == 4 and x.shape[1] * x.shape[2] == 1
                                     and getattr(last, "_kml_plan", None) is not None) else None)
-        x = self.avgpool(x)
-        return self.fc(x)
+        return self.fc(self.avgpool(x))
 
     def _chain(self, x):
         """Training forward on the GPU: blocks may hand their output BN to the next block's
@@ -205,7 +209,7 @@ class ResNet(tnn.Module):
         the stages in reverse, so the all-reduce that nothing can hide (the first stage's)
         carries only the stem + layer1 gradients (~1 % of ResNet-34's 87 MB)."""
         return [self._chained(self._stem_l1), self._chained(self.layer2), self._chained(self.layer3),
-                lambda h: self.fc(self.avgpool(self._chained(self.layer4)(h)))]
+                lambda h: self._classify(self._chained(self.layer4)(h))]
 
     def ride_plan(self):
         """[(parameters, host convs), ...] for engine/dp.py ``ride``: each group's SGD update runs

@@ -594,6 +594,8 @@ class PeerShard:
             raise ValueError(f"rider kind {kind!r}")
         cuts = [nv * i // n_hosts for i in range(n_hosts + 1)]
         total = n_hosts * blocks if word else 0
+        # READY: every slice publishes it (block 0) — the backward runs the hosts in an order these
+        # slices do not know, and a slice may only wait for what an earlier launch published
         return [ShardRider(self, 1 if kind == "rs" else 2, data, a, b, cuts[i], cuts[i + 1], ready, wait, done,
                            total, word if word else 5, adv, sp.shadow.data_ptr() + 2 * s0, blocks, sgd)
                 for i in range(n_hosts)]
