@@ -124,11 +124,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t kml_zs_rsrc(const void* p) {
 constexpr int KML_ZS_SYS = 17;  // buffer cache-policy bits sc0 | sc1: system-coherent access
 
 // thread 0: store `value` into rank r's progress word of every peer's flags area, relaxed at system
-// scope.  DONE needs no fence: the shadow chunk it hands over was stored write-through at system
-// scope and drained by every storing wave before the phase count reached this block.  READY (the
-// gradients, written by earlier launches) takes the release the standalone shard kernels' block 0
-// takes (comm.hip pc_barrier) — one wave per slice (a system release writes back the XCD's L2: in
-// every rider block it would sweep the running conv tiles' working set each time)
+// scope, no release (a system release writes back the XCD's L2 — the running conv tiles' working
+// set — and cost ~10 us per host launch).  What a flag hands over is already in memory: READY the
+// gradients of launches that completed before this one (a kernel boundary writes the L2s back: the
+// next launch's blocks on other XCDs read them), DONE the shadow chunk, stored write-through at
+// system scope and drained by every storing wave before the phase count reached this block
 template <bool RELEASE = false>
 __device__ __forceinline__ void kml_zs_publish(const KmlZsRider& z, unsigned value) {
   if (threadIdx.x != 0) return;
@@ -195,7 +195,7 @@ __device__ inline void kml_zs_finish(const KmlZsRider& z, unsigned base) {
 __device__ inline void kml_zs_rs_run(const KmlSgdRider& r, int b) {
   const KmlZsRider& z = r.zs;
   const unsigned base = __hip_atomic_load(z.ctrl + KML_ZS_BASE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (z.ready && b == 0) kml_zs_publish<true>(z, base + (unsigned)z.ready);   // block 0 of each RS slice
+  if (z.ready && b == 0) kml_zs_publish(z, base + (unsigned)z.ready);   // block 0 of each RS slice
   const bool ok = kml_zs_wait(z, base + (unsigned)z.wait);
   const float lr = *r.lr_ptr;
   const int first = r.first_ptr ? (*r.first_ptr != 0.f) : 0;

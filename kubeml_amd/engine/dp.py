@@ -24,8 +24,12 @@ from .step import GraphedTrainStep, train_state_tensors
 _log = logging.getLogger("kubeml.dp")
 
 # rider blocks per shard-rider slice (``shardride``): a slice alone runs fastest at 256 (1.05M
-# elements: 9.7 us at 256, 11.6 at 512, 16.7 at 1024 blocks; tools/diag/zs_rider_micro.py)
+# elements: 9.7 us at 256, 11.6 at 512, 16.7 at 1024 blocks; tools/diag/zs_rider_micro.py).
+# Ranks packed on one GPU (tests, packed workers) share PACKED_RIDE_BLOCKS: a rider block spins
+# until every peer published, and the spinning blocks of P - 1 ranks must never fill the CUs the
+# last rank's launch needs to publish (4 ranks x 256 did)
 SHARD_RIDE_BLOCKS = 256
+PACKED_RIDE_BLOCKS = 128
 
 
 def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable, x: torch.Tensor,
@@ -264,8 +268,10 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     post()
 
         if ride_shard and fused_sgd and fwd_bwd is not None and seg_shard is None:
-            fwd_bwd, shard_step, shard_ride_info = _shard_ride(model, space, optimizer, shard, fwd_bwd, post,
-                                                               lambda: fold, min(blocks, SHARD_RIDE_BLOCKS), step_ref)
+            got = _shard_ride(model, space, optimizer, shard, fwd_bwd, post, lambda: fold,
+                              _ride_blocks(shard, blocks), step_ref)
+            if got is not None:
+                fwd_bwd, shard_step, shard_ride_info = got
 
         def on_replay():
             space._master_stale = True
@@ -283,6 +289,12 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     step.ride_plan = (os.environ.get("KUBEML_RIDE_PLAN") or "4f:321;123:s") if riding else None
     step.shard_ride = shard_ride_info   # {"slices": n, "taken": set of the last step's carried slices}
     return step
+
+
+def _ride_blocks(shard, blocks):
+    per = max(1, int(getattr(shard, "ranks_per_device", 1)))
+    cap = SHARD_RIDE_BLOCKS if per == 1 else max(16, PACKED_RIDE_BLOCKS // per)
+    return max(1, min(int(blocks), cap))
 
 
 def _shard_ride(model, space, optimizer, shard, fwd_bwd, post, get_fold, blocks, step_ref):
@@ -316,6 +328,14 @@ def _shard_ride(model, space, optimizer, shard, fwd_bwd, post, get_fold, blocks,
             for h, r in zip(hosts, shard.rider_slices(gi, kind, len(hosts), optimizer, blocks)):
                 riders.append((gi, kind, r))
                 object.__setattr__(h, "_kml_rider", take_for(len(riders) - 1))
+    if not shard.rider_self_test([r for _, _, r in riders], optimizer):   # collective
+        # every rank alike: no riders, the whole space back to one end-of-backward shard step
+        _log.warning("shard riders failed their self-test; using the end-of-backward shard step")
+        for _, rs_hosts, ag_hosts in groups:
+            for h in list(rs_hosts) + list(ag_hosts):
+                object.__setattr__(h, "_kml_rider", None)
+        shard.set_stages([(0, space.numel)])
+        return None
     state = {"active": False, "taken": set(), "fired": set()}
 
     def _take(j):

@@ -241,10 +241,12 @@ class ResNet(tnn.Module):
     def comm_ride_plan(self):
         """[(parameters, RS host convs, AG host convs)] of the peer-shard riders (engine/dp.py
         ``shardride``, N > 1): layer4 + fc (62 % of ResNet-34's gradient bytes) reduce-scatter + SGD
-        in layer3's backward launches and all-gather in the first half of layer2's; layer3 (31 %)
-        reduce-scatters + SGD in the second half of layer2's and all-gathers in layer1's.  Only
-        layer2 + layer1 + stem (7 %) remain after the backward.  BasicBlock nets only (measured
-        plan), [] otherwise."""
+        in layer3's 13 backward launches and all-gather in the last 4 of layer2's; layer3 (31 %)
+        reduce-scatters + SGD in the first 5 of layer2's and all-gathers in layer1's 6.  Only
+        layer2 + layer1 + stem (7 %) remain after the backward.  Measured against spreading
+        layer3's reduce-scatter over all 9 layer2 launches (both gathers in layer1): 1.405 vs
+        1.448 ms per 1-rank rehearsal step — each slice costs its host launch a fixed ~10 us
+        besides its bytes (profiles/r6/shardride.md).  BasicBlock nets only, [] otherwise."""
         if not isinstance(self.layer1[0], BasicBlock):
             return []
 
@@ -252,6 +254,8 @@ class ResNet(tnn.Module):
             return [m for m in layer.modules() if isinstance(m, M.Conv2d)]
         l2 = convs(self.layer2)
         half = len(l2) // 2
+        # backward runs layer2's convs in reverse module order: l2[half:] (the second stage's
+        # reduce-scatter) first, then l2[:half] (the first stage's gather)
         return [(list(self.layer4.parameters()) + list(self.fc.parameters()), convs(self.layer3), l2[:half]),
                 (list(self.layer3.parameters()), l2[half:], convs(self.layer1))]
 

@@ -418,6 +418,7 @@ class PeerShard:
             # fence, and ranks that share one GPU (packed workers, tests) cannot fill the CUs a
             # peer still needs to reach the barrier
             self.packed = len({a[1] for a in allh}) < self.world
+            self.ranks_per_device = sum(1 for a in allh if a[1] == _device_ident(self.device))
             self.split = True
             allh = [a[0] for a in allh]
             cols: List[list] = [[0] * self.world for _ in range(4)]
@@ -665,6 +666,53 @@ class PeerShard:
             for t, s in zip((sp.grad, sp.shadow, sp.state), saved):
                 t.copy_(s)
             sp._master_stale = False
+            torch.cuda.synchronize(self.device)
+        flags: List[bool] = [False] * self.world
+        self.dist.all_gather_object(flags, ok, group=self.group)
+        return all(flags)
+
+    def rider_self_test(self, riders, optimizer) -> bool:
+        """Collective: every rider slice (:meth:`rider_slices`, in phase order) run once on its own
+        launch on rank-dependent integer gradients with the master zeroed, lr = -1 and the first
+        momentum step, so each owner's master chunk becomes the rank-ordered gradient mean (times
+        1 + momentum with Nesterov) and every shadow of the riding stages its bf16; compared with
+        the closed form, then every touched buffer restored.  True on every rank only if every rank
+        was exact and no wait timed out (engine/dp.py then keeps the riders, else the plain shard
+        step)."""
+        sp = self.space
+        g = optimizer.param_groups[0]
+        mom = optimizer._bufs(sp, ["momentum"])["momentum"] if g["momentum"] != 0 else None
+        lr = optimizer.lr_tensor(sp.device)
+        first = optimizer.first_tensor(sp.device) if mom is not None else None
+        keep = [sp.grad, sp.shadow, sp.master, lr] + ([mom, first] if mom is not None else [])
+        saved = [t.clone() for t in keep]
+        ok = True
+        try:
+            idx = torch.arange(self.n, device=self.device)
+            base = (idx % 8).float()
+            sp.grad.copy_(base * float(self.rank + 1))
+            sp.master.zero_()
+            lr.fill_(-1.0)
+            if mom is not None:
+                mom.zero_()
+                first.fill_(1.0)
+            for r in riders:
+                r.run_alone()
+            torch.cuda.synchronize(self.device)
+            d = (base * float(self.world * (self.world + 1) // 2)) * (1.0 / self.world)
+            want = d + g["momentum"] * d if (mom is not None and g["nesterov"]) else d
+            for k in range(min(self.RIDER_STAGES, len(self.segments))):
+                s0, s1, ch = self.segments[k]
+                lo = min(s1, s0 + self.rank * ch)
+                hi = min(s1, lo + ch)
+                ok = ok and bool(torch.allclose(sp.master[lo:hi], want[lo:hi], rtol=1e-6, atol=0))
+                ok = ok and bool(torch.equal(sp.shadow[s0:s1].float(), want[s0:s1].to(torch.bfloat16).float()))
+            ok = ok and self.errors() == 0
+        except Exception:
+            ok = False
+        finally:
+            for t, v in zip(keep, saved):
+                t.copy_(v)
             torch.cuda.synchronize(self.device)
         flags: List[bool] = [False] * self.world
         self.dist.all_gather_object(flags, ok, group=self.group)

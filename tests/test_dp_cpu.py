@@ -201,6 +201,20 @@ def test_shipped_plan_table_is_exact_fp32():
         assert choose_plan(n, 1 << 24).wire == "fp32"
 
 
+def test_shipped_plan_rides_the_shard_step_when_it_predicts_faster(monkeypatch):
+    """N > 1 defaults to the same-queue shard riders exactly where the probe's prediction beats
+    the end-of-backward shard step (comm_plan.json shard_plans, tools/shard_plan_probe.py)."""
+    import json as _json
+    from kubeml_amd.parallel.plan import PLAN_FILE, choose_plan
+    monkeypatch.delenv("KUBEML_COMM_PLAN", raising=False)
+    table = _json.load(open(PLAN_FILE))
+    for n in ("2", "4", "8"):
+        pred = table["shard_plans"]["predicted_ms"][n]
+        best = min(pred, key=pred.get)
+        assert choose_plan(int(n), 1 << 24).tag() == best == table["choice"][n]
+        assert pred["peer:shardride:fp32:1024"] < pred["peer:shard:fp32:1024"]
+
+
 class _FakePeer:
     def __init__(self, poisoned=False, fits=True):
         self.poisoned, self.fits, self.released, self.closed = poisoned, fits, False, False

@@ -14,10 +14,16 @@ N-rank prediction (the link is not measurable on one GPU; documented model):
                   f_first = the first stage's share of the bytes (stem + layer1: it cannot hide);
                   window  = the measured side-stream collective span at world 1 (what the backward
                   after the first stage leaves to hide in)
+  shardride(N)  = t(shardride) + f_rest * link(N) + sum over the four rider phases of
+                  max(0, bytes_phase(N) / B_link - host_window_phase)
+                  (engine/dp.py ``shardride``: each phase's link bytes are read by rider blocks of
+                  its host launches, so they hide in those launches' span; host windows from the
+                  round-6 shardride timeline, profiles/r6/shardride.md; f_rest = layer2 + layer1 +
+                  stem, the part still exchanged after the backward)
 The smaller prediction per N becomes ``choice`` (ties keep "shard": no second queue).
 
   python tools/shard_plan_probe.py [--link-gbs 750] [--from-dir gpurun_out/r5] [--write]
-``--from-dir`` reads existing ``reh_*.json`` bench lines (scripts/r5/shardov.sh) instead of running.
+``--from-dir`` reads existing ``reh_*.json`` / ``b_peer_*.json`` bench lines instead of running.
 """
 import argparse
 import glob
@@ -30,6 +36,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PLAN = os.path.join(ROOT, "kubeml_amd", "parallel", "comm_plan.json")
 N_PARAMS = 21_814_696          # ResNet-34, 1000 classes (flat fp32 space)
 FIRST_STAGE_FRAC = 0.0107      # stem + layer1 parameters / all (models/resnet.py stages())
+RIDE_A, RIDE_B = 13_627_392, 6_822_400   # layer4 + fc, layer3 (models/resnet.py comm_ride_plan())
+# host-launch spans the rider phases hide in (us; profiles/r6/shardride.md): RS-A on layer3's 13
+# conv-backward launches, AG-A on 4 of layer2's, RS-B on the other 5, AG-B on layer1's 6
+RIDE_WINDOWS_US = {"rs_a": 220.0, "ag_a": 80.0, "rs_b": 100.0, "ag_b": 120.0}
 
 
 def _bench(args):
@@ -49,7 +59,7 @@ def main():
     a = ap.parse_args()
     meas = {}
     if a.from_dir:
-        for f in glob.glob(os.path.join(a.from_dir, "reh_*.json")):
+        for f in glob.glob(os.path.join(a.from_dir, "reh_*.json")) + glob.glob(os.path.join(a.from_dir, "b_peer_*.json")):
             d = json.loads(open(f).read().strip().splitlines()[-1])
             key = d["config"].get("comm_plan") or "base"
             meas.setdefault(key, []).append((d["ms_per_step"], d.get("allreduce_ms")))
@@ -60,6 +70,8 @@ def main():
         for b in a.blocks.split(","):
             d = _bench(["--force-comm", "--comm-plan", f"peer:shardov:fp32:{b}"])
             meas[d["config"]["comm_plan"]] = [(d["ms_per_step"], d.get("allreduce_ms"))]
+        d = _bench(["--force-comm", "--comm-plan", "peer:shardride:fp32:1024"])
+        meas[d["config"]["comm_plan"]] = [(d["ms_per_step"], d.get("allreduce_ms"))]
     med = {k: (sorted(x[0] for x in v)[len(v) // 2], max((x[1] or 0.0) for x in v)) for k, v in meas.items()}
     pred = {}
     for N in (2, 4, 8):
@@ -71,6 +83,12 @@ def main():
             elif k.startswith("peer:shardov:"):
                 hide = span or 0.0
                 row[k] = round(t + FIRST_STAGE_FRAC * link + max(0.0, (1 - FIRST_STAGE_FRAC) * link - hide), 4)
+            elif k.startswith("peer:shardride:"):
+                f = (N - 1) / N / (a.link_gbs * 1e9) * 1e3                     # ms per byte-count unit
+                phases = {"rs_a": 4 * RIDE_A, "rs_b": 4 * RIDE_B, "ag_a": 2 * RIDE_A, "ag_b": 2 * RIDE_B}
+                exposed = sum(max(0.0, nb * f - RIDE_WINDOWS_US[p] / 1e3) for p, nb in phases.items())
+                rest = 6 * (N_PARAMS - RIDE_A - RIDE_B) * f
+                row[k] = round(t + rest + exposed, 4)
         pred[str(N)] = dict(sorted(row.items(), key=lambda kv: kv[1]))
     out = {"measured_world1_ms": {k: v[0] for k, v in med.items()},
            "side_span_world1_ms": {k: v[1] for k, v in med.items() if k.startswith("peer:shardov")},
