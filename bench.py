@@ -343,6 +343,9 @@ def main():
                        "comm_transport": (("peer" if getattr(step, "peer", None) is not None else "rccl")
                                           if comm else None),
                        "sgd_rider": getattr(step, "ride_plan", None),
+                       "shard_riders": ({"slices": step.shard_ride["slices"],
+                                         "carried_in_graph": len(step.shard_ride["state"]["taken"])}
+                                        if getattr(step, "shard_ride", None) else None),
                        "step": "kubeml_amd.engine.dp.make_train_step"},
             "loss_first_last": [round(first_loss, 4), round(last_loss, 4)],
         }
