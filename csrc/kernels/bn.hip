@@ -587,6 +587,15 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_fin(
   }
 }
 
+// Channel-transposed coefficient slots: channel c at (c % 8) * TSTRIDE + c / 8.  The apply loops
+// read slot k * TSTRIDE + j (j consecutive across lanes: conflict-free for any stride); the
+// per-channel writes (lane = channel; ds_write_b32 banks are (a / 4) mod 32 per 32-lane half) are
+// conflict-free when TSTRIDE = 4 (mod 32): a half's 32 (c % 8, c / 8) pairs then map onto 32
+// distinct banks.  The unpadded C / 8 stride put them on 8 and was most of these kernels' LDS
+// bank conflicts (k_bn_bwd_apply_v 44 %, k_bn_apply_v 38 %; profiles/r6/bn_lds.md).
+__host__ __device__ constexpr int bn_tstride(int ch8) { return ch8 + (((4 - ch8) % 32) + 32) % 32; }
+__host__ __device__ constexpr int bn_tslots(int C) { return 8 * bn_tstride(C >> 3); }
+
 // ---------------------------------------------------------------------------------------
 // Register-resident apply kernels (the default).  Each thread owns V 16-byte chunks
 // i0, i0 + T, ..., T = grid * NT a multiple of C/8, so all its chunks hold the SAME 8
@@ -604,9 +613,10 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
     float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode,
     int stats_rows) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[C], shift[C], (sums[2C], scratch)
+  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[TS], shift[TS], (sums[2C], scratch)
+  const int TS = bn_tslots(C), TSTR = bn_tstride(C >> 3);
   float* scale = sh;
-  float* shift = sh + C;
+  float* shift = sh + TS;
   const int n8 = (int)(M * C / 8);
   const int T = (int)gridDim.x * NT;
   const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
@@ -623,9 +633,9 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
   }
   const float* st = stats;
   if (parts) {
-    float* sums = sh + 2 * C;
-    if (early) er.finish(stats, stats_rows, sums, reinterpret_cast<float4*>(sh + 4 * C));
-    else sum_partial_rows<NT>(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 4 * C));
+    float* sums = sh + 2 * TS;
+    if (early) er.finish(stats, stats_rows, sums, reinterpret_cast<float4*>(sh + 2 * TS + 2 * C));
+    else sum_partial_rows<NT>(stats, stats_rows, 2 * C, sums, reinterpret_cast<float4*>(sh + 2 * TS + 2 * C));
     st = sums;
   }
   for (int c = threadIdx.x; c < C; c += NT) {
@@ -639,9 +649,9 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
     }
     const float rstd = rsqrtf(var + eps);
     const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
-    // channel-transposed slots (c % 8) * C/8 + c / 8: the 8-channel reads below then hit
-    // consecutive words across consecutive lanes (no LDS bank conflicts)
-    const int tslot = (c & 7) * (C >> 3) + (c >> 3);
+    // channel-transposed slots (bn_tstride): the 8-channel reads below hit consecutive words
+    // across consecutive lanes, these writes 64 distinct banks
+    const int tslot = (c & 7) * TSTR + (c >> 3);
     scale[tslot] = g * rstd;
     shift[tslot] = bb - mean * g * rstd;
     if (mode == 0 && blockIdx.x == 0) {
@@ -657,7 +667,7 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
   const int CH8 = C >> 3, j8 = i0 % CH8;
   float sc[8], sf[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { sc[k] = scale[k * CH8 + j8]; sf[k] = shift[k * CH8 + j8]; }
+  for (int k = 0; k < 8; ++k) { sc[k] = scale[k * TSTR + j8]; sf[k] = shift[k * TSTR + j8]; }
   // grid-stride batches of V chunks (large tensors); T % (C/8) == 0 keeps the channels
   for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
     if (it > 0) {
@@ -729,7 +739,8 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   // per-channel coefficients into channel-transposed slots (c % 8) * C/8 + c / 8 of a second
   // area (kb | kc stay readable by other channels' threads until the barrier): the 8-channel
   // reads below hit consecutive words across consecutive lanes (no LDS bank conflicts)
-  float* tco = ka + 5 * C;  // [5][C]: ka, kb/M, kc/M, mu, rs transposed
+  float* tco = ka + 5 * C;  // [5][TS]: ka, kb/M, kc/M, mu, rs transposed (bn_tstride)
+  const int TS = bn_tslots(C), TSTR = bn_tstride(C >> 3);
   for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
     if (blockIdx.x == 0) {  // one writer: store (overwrite) or add (accumulate)
@@ -737,21 +748,21 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
       dgamma[c] = acc ? dgamma[c] + sg : sg;
     }
     const float gm = gamma ? gamma[c] : 1.f;
-    const int tslot = (c & 7) * (C >> 3) + (c >> 3);
+    const int tslot = (c & 7) * TSTR + (c >> 3);
     tco[tslot] = gm * rstd[c];
-    tco[C + tslot] = sb * invM;
-    tco[2 * C + tslot] = sg * invM;
-    tco[3 * C + tslot] = mean[c];
-    tco[4 * C + tslot] = rstd[c];
+    tco[TS + tslot] = sb * invM;
+    tco[2 * TS + tslot] = sg * invM;
+    tco[3 * TS + tslot] = mean[c];
+    tco[4 * TS + tslot] = rstd[c];
   }
   __syncthreads();
   const int CH8 = C >> 3, j8 = i0 % CH8;
   float a8[8], b8[8], g8[8], m8[8], r8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int t = k * CH8 + j8;
-    a8[k] = tco[t]; b8[k] = tco[C + t]; g8[k] = tco[2 * C + t];
-    m8[k] = tco[3 * C + t]; r8[k] = tco[4 * C + t];
+    const int t = k * TSTR + j8;
+    a8[k] = tco[t]; b8[k] = tco[TS + t]; g8[k] = tco[2 * TS + t];
+    m8[k] = tco[3 * TS + t]; r8[k] = tco[4 * TS + t];
   }
   for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
     if (it > 0) {
@@ -1137,7 +1148,7 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 4);
     const unsigned grid = v_grid(n8, V);
-    const size_t shm = (4 * TPB + 10 * C) * sizeof(float);  // + transposed coefficients
+    const size_t shm = (4 * TPB + 5 * C + 5 * bn_tslots(C)) * sizeof(float);  // + transposed coefficients
     const KmlSgdRider rider = kml_rider_take();
 #define KML_BWD_V(VV)                                                                                          \
   hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, mean, \
@@ -1190,7 +1201,7 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
     const long long n8 = M * C / 8;
     const int V = pick_v(n8, 8);
     const unsigned grid = v_grid(n8, V);
-    const size_t shm = (stats_rows > 0 ? (4 * C + 4 * TPB) : 2 * C) * sizeof(float);
+    const size_t shm = (2 * bn_tslots(C) + (stats_rows > 0 ? (2 * C + 4 * TPB) : 0)) * sizeof(float);
 #define KML_AP_V(VV)                                                                                           \
   hipLaunchKernelGGL((k_bn_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y,        \
                      save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows)
