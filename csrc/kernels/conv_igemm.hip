@@ -612,13 +612,13 @@ __device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[
       s1[k] += __shfl_xor(s1[k], off, 64);
       s2[k] += __shfl_xor(s2[k], off, 64);
     }
-  __syncthreads();  // staging reads done: the tile area is reused as [4 waves][CPR][16]
+  __syncthreads();  // staging reads done: the tile area is reused as [4 waves][CPR][17]
   const int wave = tid >> 6;
   if (lane < CPR) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      sF[(wave * CPR + lane) * 16 + k] = s1[k];
-      sF[(wave * CPR + lane) * 16 + 8 + k] = s2[k];
+      sF[(wave * CPR + lane) * 17 + k] = s1[k];   // odd row stride: the active lanes' stores hit distinct banks
+      sF[(wave * CPR + lane) * 17 + 8 + k] = s2[k];
     }
   }
   __syncthreads();
@@ -629,8 +629,8 @@ __device__ __forceinline__ void dgrad_rowpass(const ConvArgs& a, f32x4_t (&acc)[
     const int half = q / BNT, cl = q - half * BNT, col = n0 + cl;
     if (col >= a.N) continue;
     const int c8 = cl >> 3, k = (cl & 7) + 8 * half;
-    const float sum = ((sF[(0 * CPR + c8) * 16 + k] + sF[(1 * CPR + c8) * 16 + k]) +
-                       sF[(2 * CPR + c8) * 16 + k]) + sF[(3 * CPR + c8) * 16 + k];
+    const float sum = ((sF[(0 * CPR + c8) * 17 + k] + sF[(1 * CPR + c8) * 17 + k]) +
+                       sF[(2 * CPR + c8) * 17 + k]) + sF[(3 * CPR + c8) * 17 + k];
     store_row(rows + rrow + row_off(a, col) + (half ? sq_off(a) : 0), sum, sc1_rows);
   }
   if (a.grp_out) group_reduce_rows<BMT, BNT, 1, false>(a, rows, m0, n0, tid, flag);

@@ -577,6 +577,11 @@ __device__ __forceinline__ void gemm_group_rows(const GemmArgs& g, int m0, int n
   }
 }
 
+// Per-thread rows of the epilogue column-sum partials: 16 (or 8) floats padded to an odd stride,
+// so the per-k stores of a 32-lane half hit 32 distinct banks (a 16-float stride put every other
+// lane on one bank: a 16-way ds_write_b32 conflict) and the fixed-order column reads at most 2-way.
+constexpr int RED_STR = 17, RED_STR8 = 9;
+
 // GEMM_BNF epilogue through LDS rows (128 x 128 tiles): the fp32 tile is staged in LDS (16-byte
 // chunks XOR-swizzled by row), then every thread owns one 8-column chunk and walks rows with 16-byte
 // loads of the addend / mask / BN input and 16-byte stores — full cache lines instead of the register
@@ -648,14 +653,14 @@ __device__ __forceinline__ void gemm_bnf_rowpass(const GemmArgs& g, f32x4_t (&ac
   __syncthreads();  // staging reads done: the area is reused as [NT][16] partial sums
   float* red = sF;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = s1[k]; red[tid * 16 + 8 + k] = s2[k]; }
+  for (int k = 0; k < 8; ++k) { red[tid * RED_STR + k] = s1[k]; red[tid * RED_STR + 8 + k] = s2[k]; }
   __syncthreads();
   for (int t = tid; t < 2 * BN; t += NT) {
     const int half = t / BN, cl = t - half * BN, nn = n0 + cl;
     if (nn >= g.N) continue;
     const int qq = cl >> 3, k = (cl & 7) + 8 * half;
     float sum = 0.f;
-    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
+    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * RED_STR + k];
     gemm_store_row(g.colpart + (long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn, sum, g.grp_out != nullptr);
   }
   if (g.grp_out) {
@@ -713,14 +718,14 @@ __device__ __forceinline__ void gemm_out_rowpass(const GemmArgs& g, f32x4_t (&ac
   __syncthreads();
   float* red = sF;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = s1[k]; red[tid * 16 + 8 + k] = s2[k]; }
+  for (int k = 0; k < 8; ++k) { red[tid * RED_STR + k] = s1[k]; red[tid * RED_STR + 8 + k] = s2[k]; }
   __syncthreads();
   for (int t = tid; t < 2 * BN; t += NT) {
     const int half = t / BN, cl = t - half * BN, nn = n0 + cl;
     if (nn >= g.N) continue;
     const int qq = cl >> 3, k = (cl & 7) + 8 * half;
     float sum = 0.f;
-    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * 16 + k];
+    for (int rr = 0; rr < RSTEP; ++rr) sum += red[(rr * CPR + qq) * RED_STR + k];
     gemm_store_row(g.colpart + (long long)(m0 / BM) * 2 * g.N + (half ? g.N : 0) + nn, sum, g.grp_out != nullptr);
   }
   if (g.grp_out) {
@@ -1272,28 +1277,28 @@ __global__ __launch_bounds__(NT) void k_gemm8(GemmArgs g) {
     if (BN == 256 && gbwd) {  // column sums: 16 threads (tid >> 5) share each 8-column chunk; fixed order
       float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) red[tid * 8 + k] = csum[k];
+      for (int k = 0; k < 8; ++k) red[tid * RED_STR8 + k] = csum[k];
       __syncthreads();
       if (tid < 256) {
         const int ch = tid >> 3, k = tid & 7, n = n0 + tid;
         float sum = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sum += red[((r << 5) + ch) * 8 + k];
+        for (int r = 0; r < 16; ++r) sum += red[((r << 5) + ch) * RED_STR8 + k];
         if (n < g.N) g.colpart[(long long)(m0 / 256) * g.N + n] = sum;
       }
     }
     if (gst) {  // [sum | sumsq] row of this M-tile: 16 threads share each 8-column chunk, fixed order
       float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { red[tid * 16 + k] = csum[k]; red[tid * 16 + 8 + k] = csq[k]; }
+      for (int k = 0; k < 8; ++k) { red[tid * RED_STR + k] = csum[k]; red[tid * RED_STR + 8 + k] = csq[k]; }
       __syncthreads();
       if (tid < 256) {
         const int ch = tid >> 3, k = tid & 7, n = n0 + tid;
         float sum = 0.f, sq = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          sum += red[((r << 5) + ch) * 16 + k];
-          sq += red[((r << 5) + ch) * 16 + 8 + k];
+          sum += red[((r << 5) + ch) * RED_STR + k];
+          sq += red[((r << 5) + ch) * RED_STR + 8 + k];
         }
         if (n < g.N) {
           float* row = g.colpart + (long long)(m0 / 256) * 2 * g.N;
