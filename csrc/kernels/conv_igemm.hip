@@ -52,7 +52,7 @@
 
 namespace {
 
-constexpr int PADK = 8;  // K-contiguous LDS rows: BK+8 bf16
+constexpr int PADK = 16;  // K-contiguous LDS rows: BK+16 bf16 (fragment reads conflict-free; +8 was 2-way)
 constexpr int PADR = 8;  // K-strided LDS rows: R+8 bf16
 
 enum { FWD = 0, DGRAD = 1, WGRAD = 2 };
