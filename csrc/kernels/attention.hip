@@ -33,6 +33,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -343,7 +344,10 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dQ (+D)
-template <int OCC>
+// DM: dropout mode (0 none, 1 the forward's keep bits, 2 re-hashed), BIAS: additive key bias —
+// compile-time, so the per-probability code carries no uniform branches (a branch per element
+// was a scheduling barrier between the VALU work and the MFMAs around it)
+template <int OCC, int DM, bool BIAS>
 __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char sK2[2][8192];   // K/V double-buffered (k_attn_fwd)
   __shared__ __attribute__((aligned(16))) char sV2[2][8192];
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
   const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
   const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
   const float sl2 = a.scale * LOG2E;
-  const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
+  const float* bias = BIAS ? a.bias + (long long)b * L : nullptr;
 
   Drop drop;
   drop.init(a, bh);
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
   }
   __syncthreads();
   // this lane's u16 of the stored keep bits for key tile kb (Drop), prefetched with K/V
-  const bool kbits = drop.on && a.keep != nullptr;
+  constexpr bool kbits = DM == 1;
   const unsigned short* kp16 =
       reinterpret_cast<const unsigned short*>(a.keep + ((long long)bh * nkb * (nkb * 64) + (qok ? q : 0)) * 8 + 2 * g);
   const long long kstride = (long long)nkb * 64 * 4;   // u16 units per key tile
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
     const char* sV = sV2[kb & 1];
     unsigned bits = knext;
     if (kbits && kb + 1 < nkb) knext = kp16[(kb + 1) * kstride];
-    if (drop.on && !kbits) bits = drop.bits16(q, kb * 64 + 4 * g);
+    if constexpr (DM == 2) bits = drop.bits16(q, kb * 64 + 4 * g);
     f32x4_t s[4], dp[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -419,7 +423,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
       dp[t] = MFMA16(frag_rows(sV, 16 * t, 1, lane), df1, dp[t]);
     }
     // dS = P (.) (dP (.) Z/(1-p) - D); bias / key tail only on the general path
-    const bool gen = bias != nullptr || kb * 64 + 64 > L;
+    const bool gen = BIAS || kb * 64 + 64 > L;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -428,13 +432,17 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
         float p = 0.f;
         if (gen) {
           float v = s[t][i] * sl2;
-          if (bias && key < L) v += bias[key] * LOG2E;
+          if (BIAS && key < L) v += bias[key] * LOG2E;
           if (key < L) p = fexp2(v - lse);
         } else {
           p = fexp2(fmaf(s[t][i], sl2, -lse));
         }
-        const float dpz = drop.on ? fmask(dp[t][i], bitmask(bits, 4 * t + i)) : dp[t][i];
-        s[t][i] = p * fmaf(dpz, drop.sc, -D);
+        if constexpr (DM != 0) {
+          const float dpz = fmask(dp[t][i], bitmask(bits, 4 * t + i));
+          s[t][i] = p * fmaf(dpz, drop.sc, -D);
+        } else {
+          s[t][i] = p * (dp[t][i] - D);
+        }
       }
     const bf16x8_t d0 = pack_p(s[0], s[1]), d1 = pack_p(s[2], s[3]);
 #pragma unroll
@@ -460,7 +468,9 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dq(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dK, dV
-template <int OCC>
+// DM / BIAS as k_attn_bwd_dq.  Without a bias the keys past L keep a zero bias: their dK / dV
+// rows are never stored and no other key's rows read them.
+template <int OCC, int DM, bool BIAS>
 __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
   // double-buffered like k_attn_fwd: Q, dO, LSE, D and the keep bits of a query tile
   __shared__ __attribute__((aligned(16))) char sQ2[2][8192];
@@ -484,7 +494,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
   const bf16_t* vrow = a.v + (long long)(b * L + (kok ? key : 0)) * a.ldv + h * 64;
   const bf16x8_t kf0 = load_frag_g(krow, 0, g, kok), kf1 = load_frag_g(krow, 1, g, kok);
   const bf16x8_t vf0 = load_frag_g(vrow, 0, g, kok), vf1 = load_frag_g(vrow, 1, g, kok);
-  const float kb2 = !kok ? -INFINITY : (a.bias ? a.bias[(long long)b * L + key] * LOG2E : 0.f);
+  const float kb2 = BIAS ? (!kok ? -INFINITY : a.bias[(long long)b * L + key] * LOG2E) : 0.f;
   Drop drop;
   drop.init(a, bh);
 
@@ -494,7 +504,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
   const int nqb = (L + 63) / 64;
   // stored keep bits (Drop): the 512-byte tile of words (q = qb*64.., this key tile) is
   // staged in LDS; this lane's key sits at bit kbit of each word
-  const bool kbits = drop.on && a.keep != nullptr;
+  constexpr bool kbits = DM == 1;
   const uint4* kw = reinterpret_cast<const uint4*>(a.keep + ((long long)bh * nqb + xt) * (nqb * 64) * 8);
   const int kl = 16 * w + (lane & 15), kbit = 16 * ((kl >> 2) & 3) + 4 * (kl >> 4) + (kl & 3);
   TileRegs rq, ro;
@@ -551,13 +561,16 @@ __global__ __launch_bounds__(256, OCC) void k_attn_bwd_dkv(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * t + 4 * g + i;
-        const float p = fexp2(fmaf(s[t][i], sl2, kb2 - lv[i]));
-        int m = -1;
-        if (kbits) m = bitmask(mv[i], kbit & 31);
-        else if (drop.on) m = drop.keep1(qb * 64 + r, key);
-        // dV takes P (.) Z (1/(1-p) applied at the store), dS = P (.) (dP (.) Z/(1-p) - D)
-        s[t][i] = fmask(p, m);
-        dp[t][i] = p * fmaf(fmask(dp[t][i], m), drop.sc, -dv[i]);
+        const float p = fexp2(fmaf(s[t][i], sl2, BIAS ? kb2 - lv[i] : -lv[i]));
+        if constexpr (DM != 0) {
+          const int m = DM == 1 ? bitmask(mv[i], kbit & 31) : drop.keep1(qb * 64 + r, key);
+          // dV takes P (.) Z (1/(1-p) applied at the store), dS = P (.) (dP (.) Z/(1-p) - D)
+          s[t][i] = fmask(p, m);
+          dp[t][i] = p * fmaf(fmask(dp[t][i], m), drop.sc, -dv[i]);
+        } else {
+          s[t][i] = p;
+          dp[t][i] = p * (dp[t][i] - dv[i]);
+        }
       }
     }
     const bf16x8_t p0 = pack_p(s[0], s[1]), p1 = pack_p(s[2], s[3]);
@@ -629,7 +642,22 @@ KML_API int kml_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   const dim3 grid((L + 63) / 64, B * H);
   // occupancy from the register budgets (profiles/bert_base_r3.md): dQ at 4 waves per SIMD
   // (124 VGPRs, no spills), dKV at 2 (~211 VGPRs; 3 spills and doubles its time)
-  hipLaunchKernelGGL(k_attn_bwd_dq<4>, grid, dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_attn_bwd_dkv<2>, grid, dim3(256), 0, s, a);
+  const int dm = (ctr == nullptr || pdrop <= 0.f) ? 0 : (keep != nullptr ? 1 : 2);
+  constexpr int DKV_OCC = 3;
+#define KML_ATTN_BWD(DM, BI)                                              \
+  do {                                                                    \
+    hipLaunchKernelGGL((k_attn_bwd_dq<4, DM, BI>), grid, dim3(256), 0, s, a);  \
+    hipLaunchKernelGGL((k_attn_bwd_dkv<DKV_OCC, DM, BI>), grid, dim3(256), 0, s, a); \
+  } while (0)
+  if (bias) {
+    if (dm == 0) KML_ATTN_BWD(0, true);
+    else if (dm == 1) KML_ATTN_BWD(1, true);
+    else KML_ATTN_BWD(2, true);
+  } else {
+    if (dm == 0) KML_ATTN_BWD(0, false);
+    else if (dm == 1) KML_ATTN_BWD(1, false);
+    else KML_ATTN_BWD(2, false);
+  }
+#undef KML_ATTN_BWD
   KML_LAUNCH_CHECK();
 }
