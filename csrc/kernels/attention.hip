@@ -205,7 +205,9 @@ __device__ __forceinline__ void store4(bf16_t* p, const f32x4_t& v, float s) {
 // ------------------------------------------------------------------------------ forward
 // OCC: waves per SIMD the register budget is sized for (launch bounds; the occupancy /
 // register trade of each kernel was measured, profiles/bert_base_r3.md)
-template <int OCC>
+// DM: dropout mode (0 none, 1 hashed keep decisions, stored as bits when a.keep is set), BIAS:
+// additive key bias — compile-time like the backward kernels
+template <int OCC, int DM, bool BIAS>
 __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
   // K/V double-buffered (40 KB: 4 blocks per CU, the VGPR occupancy): one barrier per key
   // tile, and the register-staged next tile is stored after this tile's MFMAs, a whole tile
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
   const bf16_t* Kb = a.k + (long long)b * L * a.ldk + h * 64;
   const bf16_t* Vb = a.v + (long long)b * L * a.ldv + h * 64;
   const float sl2 = a.scale * LOG2E;
-  const float* bias = a.bias ? a.bias + (long long)b * L : nullptr;
+  const float* bias = BIAS ? a.bias + (long long)b * L : nullptr;
   Drop drop;
   drop.init(a, bh);
 
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
     }
     // bias or key tail: scale + bias + mask every score; otherwise the max of the raw scores
     // (scale > 0) and one fma per probability below
-    const bool gen = bias != nullptr || kb * 64 + 64 > L;
+    const bool gen = BIAS || kb * 64 + 64 > L;
     float mx = -INFINITY;
     if (gen) {
 #pragma unroll
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int key = kb * 64 + 16 * t + 4 * g + i;
           float v = s[t][i] * sl2;
-          if (bias && key < L) v += bias[key] * LOG2E;
+          if (BIAS && key < L) v += bias[key] * LOG2E;
           if (key >= L) v = -INFINITY;
           s[t][i] = v;
           mx = fmaxf(mx, v);
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(256, OCC) void k_attn_fwd(AttnArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) lsum += (s[t][0] + s[t][1]) + (s[t][2] + s[t][3]);
-    if (drop.on) {   // zero the dropped probabilities (1/(1-p) is applied to O at the end)
+    if constexpr (DM != 0) {   // zero the dropped probabilities (1/(1-p) is applied to O at the end)
       const int qq = q0 + 16 * w + (lane & 15);
       const unsigned bits = drop.bits16(qq, kb * 64 + 4 * g);
 #pragma unroll
@@ -618,7 +620,14 @@ KML_API int kml_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16
   a.ctr = ctr; a.salt = (unsigned)salt; a.pdrop = pdrop; a.xcd = 1; a.keep = keep;
   if (pdrop < 0.f || pdrop >= 1.f) return (int)hipErrorInvalidValue;
   const dim3 grid((L + 63) / 64, B * H);
-  hipLaunchKernelGGL(k_attn_fwd<4>, grid, dim3(256), 0, s, a);
+  const bool dm = ctr != nullptr && pdrop > 0.f;
+  if (bias) {
+    if (dm) hipLaunchKernelGGL((k_attn_fwd<4, 1, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_fwd<4, 0, true>), grid, dim3(256), 0, s, a);
+  } else {
+    if (dm) hipLaunchKernelGGL((k_attn_fwd<4, 1, false>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attn_fwd<4, 0, false>), grid, dim3(256), 0, s, a);
+  }
   KML_LAUNCH_CHECK();
 }
 

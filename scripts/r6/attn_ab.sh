@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-out=$R/gpurun_out/r6/attnab
+out=$R/gpurun_out/r6/attnab${1:-}
 mkdir -p $out
 timeout -k 10 300 python -u -m pytest tests/test_transformer_gpu.py tests/test_bert_gpu.py -x -q --timeout 120 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
 tail -1 $out/tests.log
