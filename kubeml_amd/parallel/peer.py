@@ -708,6 +708,8 @@ class PeerShard:
                 ok = ok and bool(torch.allclose(sp.master[lo:hi], want[lo:hi], rtol=1e-6, atol=0))
                 ok = ok and bool(torch.equal(sp.shadow[s0:s1].float(), want[s0:s1].to(torch.bfloat16).float()))
             ok = ok and self.errors() == 0
+            from ..utils import fault
+            fault.point("rider_selftest", rank=self.rank)    # failure-path tests: this rank's check fails
         except Exception:
             ok = False
         finally:

@@ -296,3 +296,22 @@ def test_shard_selftest_failure_falls_back_to_allreduce():
     assert all(r["transport"] == "PeerAllReduce" for r in rs), [r["transport"] for r in rs]
     assert rs[0]["digests"] == rs[1]["digests"] and all(r["finite"] for r in rs)
     assert rs[0]["rel"] <= 1e-5, rs[0]["rel"]
+
+
+def test_shard_rider_selftest_failure_falls_back_to_the_shard_step():
+    """A failing shard-rider self-test (fault-injected on rank 1) must leave EVERY rank on the
+    end-of-backward shard step: no rider armed on any host, same update, identical ranks."""
+    old = os.environ.get("KUBEML_FAULT")
+    os.environ["KUBEML_FAULT"] = "raise:at=rider_selftest:rank=1"
+    try:
+        res = _spawn(2, [("peer:shardride:fp32:256", "sgdm", 3)])
+    finally:
+        if old is None:
+            os.environ.pop("KUBEML_FAULT", None)
+        else:
+            os.environ["KUBEML_FAULT"] = old
+    rs = [res[r]["peer:shardride:fp32:256/sgdm"] for r in range(2)]
+    assert all(r["transport"] == "PeerShard" for r in rs), [r["transport"] for r in rs]
+    assert all("ride_slices" not in r for r in rs), rs          # the fallback step carries no riders
+    assert rs[0]["digests"] == rs[1]["digests"] and all(r["finite"] for r in rs)
+    assert rs[0]["rel"] <= 1e-5, rs[0]["rel"]
