@@ -246,7 +246,8 @@ class ResNet(tnn.Module):
         layer2 + layer1 + stem (7 %) remain after the backward.  Measured against spreading
         layer3's reduce-scatter over all 9 layer2 launches (both gathers in layer1): 1.405 vs
         1.448 ms per 1-rank rehearsal step; riding every 2nd / 3rd launch only (thicker slices):
-        1.408 / 1.414 vs 1.392 ms (profiles/r6/shardride.md).  BasicBlock nets only, [] otherwise."""
+        1.408 / 1.414 vs 1.392 ms; adding the BN-backward launches as hosts (56 slices): 1.50 ms
+        (profiles/r6/shardride.md).  BasicBlock nets only, [] otherwise."""
         if not isinstance(self.layer1[0], BasicBlock):
             return []
 
