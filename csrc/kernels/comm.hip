@@ -884,6 +884,61 @@ KML_API int kml_zs_all_gather(const void* const* flags, const void* const* bufs,
   KML_LAUNCH_CHECK();
 }
 
+// Fresh fp32 master values of the parameters the forward / backward read in fp32 (BN / LN affine,
+// biases: nn master_of): under the ZeRO-1 layout a rank's master is current only on the chunks it
+// owns, so after the step's last all-gather every listed element owned elsewhere is re-read from
+// its owner's master (system-scope loads: nothing this GPU caches of a peer survives).  Element e
+// of segment k belongs to rank (e - s0[k]) / ch[k].  Runs after the step's final gather in stream
+// order: the owners' updates are complete (that gather's barrier), and no owner rewrites its
+// master before this rank publishes the next step's READY.
+struct FreshArgs {
+  const char* bufs[PC_MAX_RANKS];   // every rank's master (fp32, flat index e at byte 4 e)
+  long long s0[4], s1[4], ch[4];
+  int nseg, rank;
+};
+
+__global__ __launch_bounds__(256) void k_zs_fresh(const int* __restrict__ idx, long long n, FreshArgs f) {
+  float* own = reinterpret_cast<float*>(const_cast<char*>(f.bufs[f.rank]));
+  for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < n; j += (long long)gridDim.x * 256) {
+    const long long e = idx[j];
+    int q = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < f.nseg && e >= f.s0[k] && e < f.s1[k]) q = (int)((e - f.s0[k]) / f.ch[k]);
+    if (q < 0 || q == f.rank) continue;
+    unsigned v = 0u;
+#pragma unroll
+    for (int p = 0; p < PC_MAX_RANKS; ++p)  // uniform-index select keeps the descriptors in SGPRs
+      if (p == q) v = __builtin_amdgcn_raw_buffer_load_b32(pc_rsrc(f.bufs[p], 0x7fffffff), (int)(e * 4), 0, PC_AUX_SYS);
+    own[e] = __uint_as_float(v);
+  }
+}
+
+KML_API int kml_zs_fresh(const int* idx, long long n, const void* const* bufs, int rank, int world,
+                         const long long* segs, int nseg, hipStream_t s) {
+  if (n < 0 || world < 1 || world > PC_MAX_RANKS || rank < 0 || rank >= world || nseg < 1 || nseg > 4 || !bufs ||
+      !segs || (n > 0 && !idx))
+    return (int)hipErrorInvalidValue;
+  if (n == 0 || world == 1) return (int)hipSuccess;
+  FreshArgs f{};
+  for (int p = 0; p < world; ++p) {
+    if (!bufs[p]) return (int)hipErrorInvalidValue;
+    f.bufs[p] = static_cast<const char*>(bufs[p]);
+  }
+  for (int k = 0; k < nseg; ++k) {
+    f.s0[k] = segs[3 * k];
+    f.s1[k] = segs[3 * k + 1];
+    f.ch[k] = segs[3 * k + 2];
+    if (f.ch[k] <= 0 || f.s1[k] < f.s0[k] || f.s1[k] * 4 >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  }
+  f.nseg = nseg;
+  f.rank = rank;
+  long long g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_zs_fresh, dim3((unsigned)g), dim3(256), 0, s, idx, n, f);
+  KML_LAUNCH_CHECK();
+}
+
 // standalone barrier `bar` past the current sequence (one-block launch).  gather_master closes
 // with it (all-gather with finish = 2, then bar = 0): no rank leaves the call — and overwrites
 // its own master chunk with a local step, a broadcast or a restore — while a peer may still be

@@ -226,6 +226,9 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
     if shard is not None:
         blocks = plan.max_blocks
         fused_sgd = getattr(optimizer, "kind", None) == "sgd" and optimizer.supports_ranges()
+        # the parameters the step reads from the fp32 master (BN / LN affine, biases) are re-read
+        # from their owners after every step: the ZeRO-1 master is current only on own chunks
+        shard.set_fresh([space.range_of([p]) for p in model.parameters() if p.requires_grad and p.dim() == 1])
         if staged_shard:
             # ownership cut per backward stage (every rank the same ranges): stage k's
             # reduce-scatter + SGD + all-gather run on a side stream once its gradients are final
@@ -240,6 +243,8 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                 s0, s1 = stamps if stamps is not None else (None, None)
                 shard.stage_step(seg_of[k], optimizer, advance=fold, max_blocks=blocks, first_stage=k == 0,
                                  last_stage=k == nseg - 1, stamps=None if stamps is None else (s0, s1))
+                if k == nseg - 1:
+                    shard.gather_fresh()
             seg_shard = [(lambda st=None, k=k: _stage(k, st)) for k in range(nseg)]
 
         def shard_step(stamps=None):
@@ -258,6 +263,7 @@ def make_train_step(model: torch.nn.Module, space, optimizer, loss_fn: Callable,
                     from ..ops import kernels as K
                     K.advance_counter_(*fold)
             shard.all_gather_shadow(max_blocks=blocks, stamp=s1)
+            shard.gather_fresh()
             if post is not None:
                 post()
 
@@ -370,6 +376,7 @@ def _shard_ride(model, space, optimizer, shard, fwd_bwd, post, get_fold, blocks,
         st = None if stamps is None else (stamps.data_ptr(), stamps.data_ptr() + 8)
         shard.stage_step(2, optimizer, advance=get_fold(), max_blocks=blocks, first_stage=True, last_stage=True,
                          stamps=st)
+        shard.gather_fresh()
         if post is not None:
             post()
     return ride_fwd_bwd, shard_step, {"slices": len(riders), "state": state}

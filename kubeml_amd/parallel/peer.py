@@ -671,6 +671,27 @@ class PeerShard:
         self.dist.all_gather_object(flags, ok, group=self.group)
         return all(flags)
 
+    def set_fresh(self, ranges):
+        """Flat [lo, hi) ranges whose fp32 master every rank's step reads (BN / LN affine, biases:
+        nn ``master_of``).  The ZeRO-1 layout keeps a rank's master current only on its own chunks,
+        so :meth:`gather_fresh` re-reads these elements from their owners after each step."""
+        idx = [torch.arange(int(lo), int(hi), dtype=torch.int32) for lo, hi in ranges if hi > lo]
+        self._fresh = torch.cat(idx).to(self.device) if idx else None
+
+    def gather_fresh(self):
+        """Stream-ordered, capturable: the :meth:`set_fresh` elements owned elsewhere := their
+        owners' fp32 master (csrc/kernels/comm.hip k_zs_fresh).  Call after the step's last
+        all-gather."""
+        fresh = getattr(self, "_fresh", None)
+        if self.world == 1 or fresh is None or fresh.numel() == 0:
+            return
+        if self.region is None:
+            raise PeerCommError("sharded update used after close()")
+        segs = (ctypes.c_longlong * (3 * len(self.segments)))(*[int(v) for seg in self.segments for v in seg])
+        HIP.call("kml_zs_fresh", "p l p i i p i s", fresh.data_ptr(), int(fresh.numel()),
+                 ctypes.addressof(self._states), self.rank, self.world, ctypes.addressof(segs), len(self.segments),
+                 self._stream())
+
     def rider_self_test(self, riders, optimizer) -> bool:
         """Collective: every rider slice (:meth:`rider_slices`, in phase order) run once on its own
         launch on rank-dependent integer gradients with the master zeroed, lr = -1 and the first

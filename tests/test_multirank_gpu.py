@@ -55,6 +55,33 @@ def _model(dev, opt_kind):
     return m, sp, opt
 
 
+def _reference_updates(world, dev, opt_kind, steps):
+    """Master change after ``steps`` data-parallel steps in ONE process: every step sums every
+    rank's gradient (its own batch of that step, the current weights) in rank order and applies
+    the optimizer with grad scale 1/P — what the multi-rank step must reproduce step after step
+    (the ZeRO-1 plans included: a rank reads the fp32 master of BN / bias parameters it does
+    not own)."""
+    from kubeml_amd.nn import backward_loss, cross_entropy
+    m, sp, opt = _model(dev, opt_kind)
+    w0 = sp.master.clone()
+    data = [_batches(r, steps, dev) for r in range(world)]
+    for k in range(steps):
+        gsum = None
+        for r in range(world):
+            xs, ys = data[r]
+            sp.zero_grad()
+            loss = cross_entropy(m(xs[k]), ys[k])
+            backward_loss(loss)
+            sp.finish_grads()
+            g = sp.grad.clone()
+            gsum = g if gsum is None else gsum + g
+        sp.grad.copy_(gsum)
+        opt.set_grad_scale(1.0 / world)
+        opt.step()
+    torch.cuda.synchronize()
+    return sp.master - w0
+
+
 def _reference_update(world, dev, opt_kind):
     """One update from the initial model: every rank's gradient on the same kernels (eager),
     summed in rank order, optimizer with grad scale 1/P."""
@@ -128,6 +155,10 @@ def _rank_main(rank, world, port, q, cases):
             if rank == 0:
                 ref = _reference_update(world, dev, opt_kind).cpu()
                 res["rel"] = float((upd1 - ref).norm() / ref.norm())
+                if steps > 1:   # the whole trajectory, not only the first update
+                    refn = _reference_updates(world, dev, opt_kind, steps).cpu()
+                    upd = (sp.master - w0).cpu()
+                    res["rel_final"] = float((upd - refn).norm() / refn.norm())
             out[spec + "/" + opt_kind] = res
             if step.peer is not None:
                 step.peer.close()
@@ -186,10 +217,23 @@ def _check(world, res):
             assert 0 < rel < 1e-2, (key, rel)
         else:
             assert rel <= 1e-5, (key, rel)
+            if "rel_final" in rs[0]:
+                assert rs[0]["rel_final"] <= 1e-4, (key, rs[0]["rel_final"])
 
 
 def test_train_step_two_ranks_one_gpu():
     _check(2, _spawn(2, CASES))
+
+
+def test_shard_riders_match_the_shard_step_bit_for_bit():
+    """The riders apply the same recurrence in the same rank order as the end-of-backward shard
+    step, so after several momentum steps (the first-step flag cleared between them) the weights
+    are bit-identical.  Run back to back in fresh processes: plans that ran earlier in a process
+    may have settled other per-process kernel routes (tools/diag/ride_vs_shard.py compares step
+    by step)."""
+    res = _spawn(2, [("peer:shard:fp32:256", "sgdm", 3), ("peer:shardride:fp32:256", "sgdm", 3)])
+    for r in range(2):
+        assert res[r]["peer:shardride:fp32:256/sgdm"]["digests"] == res[r]["peer:shard:fp32:256/sgdm"]["digests"]
 
 
 def test_train_step_four_ranks_one_gpu():

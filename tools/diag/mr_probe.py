@@ -23,7 +23,7 @@ def main():
     for key in res[0]:
         rs = [res[r][key] for r in range(a.world)]
         same = all(r["digests"] == rs[0]["digests"] for r in rs)
-        print(key, "rel", rs[0].get("rel"), "same", same, "finite", all(r["finite"] for r in rs),
+        print(key, "rel", rs[0].get("rel"), "rel_final", rs[0].get("rel_final"), "same", same, "finite", all(r["finite"] for r in rs),
               "ride", [(r.get("ride_slices"), r.get("ride_taken")) for r in rs], flush=True)
 
 
