@@ -606,7 +606,7 @@ __host__ __device__ constexpr int bn_tslots(int C) { return 8 * bn_tstride(C >> 
 // never waits on more than one memory round trip.  Out-of-range chunks load a clamped
 // (valid) index and skip the store (no branch around a load: straight-line vmcnt).
 // ---------------------------------------------------------------------------------------
-template <int NT, int V>
+template <int NT, int V, bool PIPE>
 __global__ __launch_bounds__(NT) void k_bn_apply_v(
     const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
@@ -668,35 +668,63 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
   float sc[8], sf[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sc[k] = scale[k * TSTR + j8]; sf[k] = shift[k * TSTR + j8]; }
-  // grid-stride batches of V chunks (large tensors); T % (C/8) == 0 keeps the channels
-  for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
-    if (it > 0) {
+  // grid-stride batches of V chunks (large tensors); T % (C/8) == 0 keeps the channels.
+  // PIPE (the host's choice when a thread has more than one batch): each chunk's register is
+  // refilled with the next batch's chunk right after its store, so the next batch's loads are in
+  // flight while this batch is still being stored (ResNet-50's 56x56 BNs +6-9 %); single-batch
+  // launches (every ResNet-34 BN) keep the plain loop, whose code measured faster there
+  if constexpr (PIPE) {
+    for (int base = i0; base < n8; base += V * T) {
+      const int nb = base + V * T;
 #pragma unroll
-      for (int v = 0; v < V; ++v) xv[v] = reinterpret_cast<const uint4*>(x)[min(base + v * T, n8 - 1)];
-      if (res) {
+      for (int v = 0; v < V; ++v) {
+        float f[8], r[8];
+        unpack8(xv[v], f);
+        if (res) unpack8(rv[v], r);
 #pragma unroll
-        for (int v = 0; v < V; ++v) rv[v] = reinterpret_cast<const uint4*>(res)[min(base + v * T, n8 - 1)];
+        for (int k = 0; k < 8; ++k) {
+          float o = f[k] * sc[k] + sf[k];
+          if (res) o += r[k];
+          if (relu) o = fmaxf(o, 0.f);
+          f[k] = o;
+        }
+        const int i = base + v * T;
+        if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+        if (nb < n8) {
+          xv[v] = reinterpret_cast<const uint4*>(x)[min(nb + v * T, n8 - 1)];
+          if (res) rv[v] = reinterpret_cast<const uint4*>(res)[min(nb + v * T, n8 - 1)];
+        }
       }
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float f[8], r[8];
-      unpack8(xv[v], f);
-      if (res) unpack8(rv[v], r);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float o = f[k] * sc[k] + sf[k];
-        if (res) o += r[k];
-        if (relu) o = fmaxf(o, 0.f);
-        f[k] = o;
+  } else {
+    for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
+      if (it > 0) {
+  #pragma unroll
+        for (int v = 0; v < V; ++v) xv[v] = reinterpret_cast<const uint4*>(x)[min(base + v * T, n8 - 1)];
+        if (res) {
+  #pragma unroll
+          for (int v = 0; v < V; ++v) rv[v] = reinterpret_cast<const uint4*>(res)[min(base + v * T, n8 - 1)];
+        }
       }
-      const int i = base + v * T;
-      if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  #pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float f[8], r[8];
+        unpack8(xv[v], f);
+        if (res) unpack8(rv[v], r);
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float o = f[k] * sc[k] + sf[k];
+          if (res) o += r[k];
+          if (relu) o = fmaxf(o, 0.f);
+          f[k] = o;
+        }
+        const int i = base + v * T;
+        if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
+      }
     }
-  }
-}
+  }}
 
-template <int NT, int V>
+template <int NT, int V, bool PIPE>
 __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -764,39 +792,72 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
     a8[k] = tco[t]; b8[k] = tco[TS + t]; g8[k] = tco[2 * TS + t];
     m8[k] = tco[3 * TS + t]; r8[k] = tco[4 * TS + t];
   }
-  for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
-    if (it > 0) {
-#pragma unroll
+  if constexpr (PIPE) {   // as k_bn_apply_v
+    for (int base = i0; base < n8; base += V * T) {
+      const int nb = base + V * T;   // the next batch's chunk v is loaded right after chunk v is stored
+  #pragma unroll
       for (int v = 0; v < V; ++v) {
-        const int i = min(base + v * T, n8 - 1);
-        dv[v] = reinterpret_cast<const uint4*>(dy)[i];
-        xv[v] = reinterpret_cast<const uint4*>(x)[i];
-      }
-      if (y) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) yv[v] = reinterpret_cast<const uint4*>(y)[min(base + v * T, n8 - 1)];
+        float d[8], xf[8];
+        unpack8(dv[v], d);
+        unpack8(xv[v], xf);
+        if (y) {
+          float yf[8];
+          unpack8(yv[v], yf);
+  #pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+        }
+        const int i = base + v * T;
+        if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+        float o[8];
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xf[k] - m8[k]) * r8[k];
+          o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+        }
+        if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
+        if (nb < n8) {
+          const int inext = min(nb + v * T, n8 - 1);
+          dv[v] = reinterpret_cast<const uint4*>(dy)[inext];
+          xv[v] = reinterpret_cast<const uint4*>(x)[inext];
+          if (y) yv[v] = reinterpret_cast<const uint4*>(y)[inext];
+        }
       }
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float d[8], xf[8];
-      unpack8(dv[v], d);
-      unpack8(xv[v], xf);
-      if (y) {
-        float yf[8];
-        unpack8(yv[v], yf);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+  } else {
+    for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
+      if (it > 0) {
+  #pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const int i = min(base + v * T, n8 - 1);
+          dv[v] = reinterpret_cast<const uint4*>(dy)[i];
+          xv[v] = reinterpret_cast<const uint4*>(x)[i];
+        }
+        if (y) {
+  #pragma unroll
+          for (int v = 0; v < V; ++v) yv[v] = reinterpret_cast<const uint4*>(y)[min(base + v * T, n8 - 1)];
+        }
       }
-      const int i = base + v * T;
-      if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
-      float o[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float xh = (xf[k] - m8[k]) * r8[k];
-        o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+  #pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float d[8], xf[8];
+        unpack8(dv[v], d);
+        unpack8(xv[v], xf);
+        if (y) {
+          float yf[8];
+          unpack8(yv[v], yf);
+  #pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
+        }
+        const int i = base + v * T;
+        if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+        float o[8];
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xf[k] - m8[k]) * r8[k];
+          o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
+        }
+        if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
       }
-      if (i < n8) reinterpret_cast<uint4*>(dx)[i] = pack8(o);
     }
   }
 }
@@ -1150,9 +1211,12 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 5 * C + 5 * bn_tslots(C)) * sizeof(float);  // + transposed coefficients
     const KmlSgdRider rider = kml_rider_take();
+    const bool pipe = n8 > (long long)grid * TPB * V;   // more than one batch per thread
 #define KML_BWD_V(VV)                                                                                          \
-  hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, mean, \
-                     rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider)
+  do { if (pipe) hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, true>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, \
+                     mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider);                      \
+  else hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, false>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, mean, \
+                     rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider); } while (0)
     if (V == 1) KML_BWD_V(1);
     else if (V == 2) KML_BWD_V(2);
     else KML_BWD_V(4);
@@ -1202,9 +1266,12 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
     const int V = pick_v(n8, 8);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (2 * bn_tslots(C) + (stats_rows > 0 ? (2 * C + 4 * TPB) : 0)) * sizeof(float);
+    const bool pipe = n8 > (long long)grid * TPB * V;   // more than one batch per thread
 #define KML_AP_V(VV)                                                                                           \
-  hipLaunchKernelGGL((k_bn_apply_v<TPB, VV>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y,        \
-                     save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows)
+  do { if (pipe) hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, true>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, \
+                     res, y, save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows); \
+  else hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, false>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, \
+                     save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows); } while (0)
     if (V == 1) KML_AP_V(1);
     else if (V == 2) KML_AP_V(2);
     else if (V == 4) KML_AP_V(4);

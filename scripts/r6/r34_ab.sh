@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: ResNet-34 headline step, this tree vs _abbase, alternating x4
+set -o pipefail
+export TMPDIR=/tmp
+out=$GRAFT_REPO_ROOT/gpurun_out/r6/r34ab${1:-}
+mkdir -p $out
+for rep in 1 2 3 4; do
+  for t in new base; do
+    root=$GRAFT_REPO_ROOT; [ $t = base ] && root=$GRAFT_REPO_ROOT/_abbase
+    (cd $root && timeout -k 10 200 python -u bench.py --steps 200 --warmup 20 --no-epoch --e2e off > $out/r34_${t}_$rep.json 2>/dev/null) || exit 1
+    echo "r34 $t $rep $(tail -1 $out/r34_${t}_$rep.json | python -c "import json,sys;print(json.loads(sys.stdin.read())['ms_per_step'])")"
+  done
+done
