@@ -377,6 +377,68 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x4_t (&acc)[
   }
 }
 
+// 32x32x16 variant (k_gemm MF = 32): the A / B fragment of lane l is row (l & 31), k = 8 (l >> 5) .. +7
+// of a KC [rows][64] tile (same chunk swizzle as frag_kc); with B as the MFMA's first operand a lane's
+// accumulator registers 4g .. 4g+3 hold output row m = .. + (l & 31), columns n = .. + 8g + 4 (l >> 5) .. +3
+__device__ __forceinline__ bf16x8_t frag_kc32(const char* lds, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 31);
+  const int c = 2 * ks + (lane >> 5);
+  return *reinterpret_cast<const bf16x8_t*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
+}
+
+// the 4 consecutive output columns n .. n+3 of row m (OUT 0: bias, GELU, pre-activation copy; OUT 1)
+template <int OUT>
+__device__ __forceinline__ void gemm_store4(const GemmArgs& g, int m, int n, float (&v)[4]) {
+  if constexpr (OUT == 0) {
+    if (g.bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(g.bias + n);
+      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+    }
+    const long long off = (long long)m * g.ldc + n;
+    if (g.act == GEMM_ADD_C2) {
+      const uint2 ad = *reinterpret_cast<const uint2*>(g.c2 + off);
+      const uint2 q = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      v[0] = lo_bf(q.x) + lo_bf(ad.x); v[1] = hi_bf(q.x) + hi_bf(ad.x);
+      v[2] = lo_bf(q.y) + lo_bf(ad.y); v[3] = hi_bf(q.y) + hi_bf(ad.y);
+    } else if (g.c2) {
+      *reinterpret_cast<uint2*>(g.c2 + off) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    }
+    if (g.act == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+    }
+    *reinterpret_cast<uint2*>(static_cast<bf16_t*>(g.c) + off) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+  } else {
+    float4* p = reinterpret_cast<float4*>(static_cast<float*>(g.c) + (long long)m * g.ldc + n);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.beta != 0.f) {
+      o = *p;
+      o.x *= g.beta; o.y *= g.beta; o.z *= g.beta; o.w *= g.beta;
+    }
+    o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+    *p = o;
+  }
+}
+
+template <int OUT, int MR, int NR, int WM, int WN>
+__device__ __forceinline__ void gemm_epilogue32(const GemmArgs& g, f32x16_t (&acc)[MR][NR], int m0, int n0, int wm,
+                                                int wn, int lane) {
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int m = m0 + wm * WM + i * 32 + (lane & 31);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * WN + j * 32 + 8 * q + 4 * (lane >> 5);
+        if (n >= g.N) continue;
+        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        gemm_store4<OUT>(g, m, n, v);
+      }
+  }
+}
+
 // GEMM_STATS rows of a k_gemm tile (bf16 out): per-lane sums of the bf16-rounded outputs over the
 // lane's rows, a butterfly over the 16 lanes of a column group, then the two wave rows summed
 // through LDS (wave row 0 + wave row 1, fixed order).  Entered by every thread of the block.
@@ -740,12 +802,15 @@ __device__ __forceinline__ void gemm_out_rowpass(const GemmArgs& g, f32x4_t (&ac
 // so one tile's DMA stays in flight across the raw s_barrier (CDNA guide §5 "Pipelining
 // across barriers"; trailing steps re-issue the last tile into a stage nobody reads, so
 // the count never changes).
-template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S, int AG = 0>
+template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S, int AG = 0, int MF = 16>
 __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   static_assert(AG == 0 || (AG == 1 && A_KC && B_KC && OUT == 0) || (AG == 2 && A_KC && !B_KC && OUT == 0) ||
                     (AG == 3 && !A_KC && !B_KC && OUT == 3),
                 "implicit-GEMM gather: forward (AG 1) / input-gradient (AG 2) bf16 out, weight gradient (AG 3) slabs");
-  constexpr int WM = BM / 2, WN = BN / 4, MR = WM / 16, NR = WN / 16;
+  static_assert(MF == 16 || (MF == 32 && A_KC && B_KC && AG == 0 && OUT <= 1),
+                "the 32x32x16 form: K-contiguous operands, register epilogue (bf16 / fp32 out)");
+  constexpr int WM = BM / 2, WN = BN / 4, MR = WM / MF, NR = WN / MF;
+  using acc_t = typename std::conditional<MF == 32, f32x16_t, f32x4_t>::type;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NI = BM / 64 + BN / 64;   // DMA instructions per wave per stage
   static_assert(S * STAGE <= 160 * 1024, "LDS");
@@ -769,11 +834,11 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   if constexpr (AG >= 2) sb.init(g, n0, wave, lane);
   else sb.init(g.b, g.ldb, n0, g.N, wave, lane);
 
-  f32x4_t acc[MR][NR];
+  acc_t acc[MR][NR];
 #pragma unroll
   for (int i = 0; i < MR; ++i)
 #pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NR; ++j) acc[i][j] = acc_t{};
 
   auto issue = [&](int kt, int st) {
     char* dst = smem + st * STAGE;
@@ -785,20 +850,36 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   auto compute = [&](int st) {
     const char* sA = smem + st * STAGE;
     const char* sB = sA + A_BYTES;
+    if constexpr (MF == 32) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8_t af[MR], bfr[NR];
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8_t af[MR], bfr[NR];
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
-        bfr[j] = B_KC ? frag_kc(sB, wn * WN + j * 16, ks, lane) : frag_ks<BN>(sB, wn * WN + j * 16, ks, lane);
+        for (int j = 0; j < NR; ++j) bfr[j] = frag_kc32(sB, wn * WN + j * 32, ks, lane);
 #pragma unroll
-      for (int i = 0; i < MR; ++i)
-        af[i] = A_KC ? frag_kc(sA, wm * WM + i * 16, ks, lane) : frag_ks<BM>(sA, wm * WM + i * 16, ks, lane);
+        for (int i = 0; i < MR; ++i) af[i] = frag_kc32(sA, wm * WM + i * 32, ks, lane);
 #pragma unroll
-      for (int i = 0; i < MR; ++i)
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[MR], bfr[NR];
 #pragma unroll
         for (int j = 0; j < NR; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          bfr[j] = B_KC ? frag_kc(sB, wn * WN + j * 16, ks, lane) : frag_ks<BN>(sB, wn * WN + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+          af[i] = A_KC ? frag_kc(sA, wm * WM + i * 16, ks, lane) : frag_ks<BM>(sA, wm * WM + i * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
     }
   };
 
@@ -834,6 +915,10 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
     }
   }
 
+  if constexpr (MF == 32) {
+    gemm_epilogue32<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane);
+    return;
+  } else {
   if constexpr (OUT == 0) {
     if (g.act == GEMM_BNF) {
       if constexpr (BM == 128 && BN == 128 && S * STAGE >= BM * BN * 4) {
@@ -853,6 +938,7 @@ __global__ __launch_bounds__(NT) void k_gemm(GemmArgs g) {
   gemm_epilogue<OUT, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, tz);
   if constexpr (OUT == 0) {
     if (g.act == GEMM_STATS) gemm_stats_rows<BM, BN, MR, NR, WM, WN>(g, acc, m0, n0, wm, wn, lane, smem);
+  }
   }
 }
 
@@ -1324,7 +1410,7 @@ int launch8(GemmArgs g, int splits, hipStream_t s) {
 }
 
 template <int BM, int BN, bool A_KC, bool B_KC, int OUT, int S = (3 * (BM + BN) * BK * 2 <= 160 * 1024) ? 3 : 2,
-          int AG = 0>
+          int AG = 0, int MF = 16>
 int launch(GemmArgs g, int splits, hipStream_t s) {
   splits = splits < 1 ? 1 : splits;
   int chunk = (g.K + splits - 1) / splits;
@@ -1332,7 +1418,7 @@ int launch(GemmArgs g, int splits, hipStream_t s) {
   g.kchunk = chunk > 0 ? chunk : BK;
   const int z = g.K > 0 ? (g.K + g.kchunk - 1) / g.kchunk : 1;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, z);
-  hipLaunchKernelGGL((k_gemm<BM, BN, A_KC, B_KC, OUT, S, AG>), grid, dim3(NT), 0, s, g);
+  hipLaunchKernelGGL((k_gemm<BM, BN, A_KC, B_KC, OUT, S, AG, MF>), grid, dim3(NT), 0, s, g);
   KML_LAUNCH_CHECK();
 }
 
@@ -1359,6 +1445,12 @@ int by_tile(const GemmArgs& g, int tile, int splits, hipStream_t s) {
     case 5: return launch4<A_KC, B_KC, OUT>(g, splits, s);
     case 6: return launch8<A_KC, B_KC, OUT>(g, splits, s);
     case 7: return launch8<A_KC, B_KC, OUT, 192>(g, splits, s);
+    case 8:   // tiles 3 / 4 on v_mfma_f32_32x32x16_bf16 (forward layout, bf16 / fp32 out)
+      if constexpr (A_KC && B_KC && OUT <= 1) return launch<128, 128, A_KC, B_KC, OUT, 3, 0, 32>(g, splits, s);
+      break;
+    case 9:
+      if constexpr (A_KC && B_KC && OUT <= 1) return launch<128, 128, A_KC, B_KC, OUT, 2, 0, 32>(g, splits, s);
+      break;
   }
   return (int)hipErrorInvalidValue;
 }
@@ -1393,7 +1485,9 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
 //         4 = 128x128 with 2 stages (64 KB: two blocks per CU), 5 = 256x256 BK=32 4-slot ring,
 //         6 = 256x256 two-group phase schedule (k_gemm8), 7 = the same schedule on 256x192 tiles
 //         (BERT's N = 768 / 2304 / 3072 outputs split into 4 / 12 / 16 column tiles: with T = 16384
-//         tokens every launch is a whole number of waves over 256 CUs)
+//         tokens every launch is a whole number of waves over 256 CUs), 8 / 9 = tiles 3 / 4 with
+//         v_mfma_f32_32x32x16_bf16 fragments (layout 0, out 0 / 1; measured against 3 / 4 in
+//         profiles/r6/gemm/mfma_32x32.md)
 // Host contract (checked by ops/gemm.py): N % 4 == 0, ldc % 4 == 0, K-contiguous leading
 // dimensions % 8 == 0, 16-byte aligned pointers; a zero page of >= 16 bytes.  Tile 6 with
 // bf16 output also needs N % 8 == 0 and ldc % 8 == 0 (16-byte staged stores).

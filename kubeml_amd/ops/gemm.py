@@ -19,7 +19,9 @@ from .._native import HIP, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 TILES = {(256, 256): 0, (256, 128): 1, (128, 256): 2, (128, 128): 3, (128, 128, 2): 4, (256, 256, 4): 5,
-         (256, 256, 8): 6, (256, 192, 8): 7}  # (BM, BN[, stages])
+         (256, 256, 8): 6, (256, 192, 8): 7,
+         # tiles 3 / 4 on the 32x32x16 MFMA (layout 0 only): the measured alternative to 16x16x32
+         (128, 128, 3, "mf32"): 8, (128, 128, 2, "mf32"): 9}  # (BM, BN[, stages])
 _TUNE_FILE = os.environ.get("KUBEML_GEMM_TUNING_FILE") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _TUNED: dict = {}

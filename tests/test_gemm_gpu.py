@@ -18,7 +18,7 @@ def _rand(*s, scale=1.0):
 
 
 @pytest.mark.parametrize("tile", [(256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (256, 128), (128, 256),
-                                  (128, 128), (128, 128, 2)])
+                                  (128, 128), (128, 128, 2), (128, 128, 3, "mf32"), (128, 128, 2, "mf32")])
 @pytest.mark.parametrize("T,ip,op", [(512, 768, 2304), (200, 72, 136), (1216, 768, 1000)])
 def test_forward_bias_gelu(tile, T, ip, op):
     from kubeml_amd.ops import gemm as G
@@ -167,3 +167,17 @@ def test_linear_dgrad_addend_paths():
         else:   # fp32 split-K atomics: summation order differs run to run
             assert _rel(out, want) < 1e-2
 
+
+
+@pytest.mark.parametrize("tile", [(128, 128, 3, "mf32"), (128, 128, 2, "mf32")])
+@pytest.mark.parametrize("M,N,K", [(384, 256, 512), (200, 136, 72)])
+def test_mfma32_fp32_out_beta(tile, M, N, K):
+    """The 32x32x16 fragment form (tiles 8 / 9) with the fp32 beta epilogue: every accumulator
+    register lands on its (row, column) (a swapped row group or column half would show here)."""
+    from kubeml_amd.ops import gemm as G
+    torch.manual_seed(1)
+    a, b = _rand(M, K), _rand(N, K)
+    c0 = torch.randn(M, N, device=dev)
+    c = c0.clone()
+    G.gemm(a, K, b, K, c, N, M, N, K, 0, 1, beta=0.5, tile=tile, splits=1)
+    assert _rel(c, 0.5 * c0 + a.float() @ b.float().t()) < 1e-5

@@ -70,9 +70,11 @@ def main():
             ref = lambda: torch.addmm(C, A.t(), B, out_dtype=torch.float32)
         cands = []
         for tile in ((256, 256), (256, 256, 4), (256, 256, 8), (256, 192, 8), (256, 128), (128, 256), (128, 128),
-                     (128, 128, 2)):
+                     (128, 128, 2), (128, 128, 3, "mf32"), (128, 128, 2, "mf32")):
             tname = "x".join(str(v) for v in tile)
             if a.tiles != "all" and tname not in a.tiles.split(","):
+                continue
+            if tile[-1] == "mf32" and layout != 0:   # the 32x32x16 form: forward layout only
                 continue
             for s in ((1,) if layout != 2 else (1, 2, 4, 8, 16)):
                 if layout == 2 and s > 1 and K // s < 256:
@@ -92,6 +94,7 @@ def main():
             G.gemm(A, lda, B, ldb, C, N, M, N, K, layout, out if s == 1 else 2, beta=1.0 if layout == 2 else 0.0,
                    tile=tile, splits=s)
         nm = lambda t, s: (f"{t[0]}x{t[1]}" + (f"x{t[2]}st" if len(t) > 2 and t[2] != "slab" else "")
+                           + ("-mf32" if t[-1] == "mf32" else "")
                            + (f"/k{s}" if t[-1] == "slab" else f"/s{s}"))
         fns = [("torch", ref)] + [(nm(t, s), (lambda t=t, s=s: run(t, s))) for t, s in cands]
         for _, f in fns:
