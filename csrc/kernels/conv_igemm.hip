@@ -151,6 +151,18 @@ __device__ __forceinline__ Blk hw_blk() {
   return Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x};
 }
 
+// Forward pairs (kml_conv_fwd_pair): while g_fwd_rec is set, a forward launch of the register /
+// LDS-DMA / direct kernels records its body, arguments and grid instead of launching.
+struct FwdRec {
+  int body = -1;        // index in the paired-body list (fwd_body_id), -1: not pairable
+  ConvArgs a;
+  int gx = 0, gy = 0;
+  bool set = false;
+};
+FwdRec* g_fwd_rec = nullptr;
+template <class B>
+constexpr int fwd_body_id();
+
 // K-strided [BK][R] tiles of R = 32/64/128 columns use the XOR chunk swizzle of the glds
 // kernels (swz_ks, conflict-free reads and writes per tools/lds_banks.py); other widths keep
 // the +PADR row padding (2-3-way conflicts).
@@ -1227,6 +1239,13 @@ template <int MODE, int BM, int BN, int S>
 int launch_glds(const ConvArgs& a, hipStream_t s) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, a.splits);
   const bool tapu = (MODE != FWD) || (a.C % 64 == 0);
+  if constexpr (MODE == FWD) {
+    if (g_fwd_rec) {
+      *g_fwd_rec = FwdRec{tapu && a.splits == 1 ? fwd_body_id<GldsBody<FWD, BM, BN, S, true>>() : -1, a,
+                          (int)grid.x, (int)grid.y, true};
+      return 0;
+    }
+  }
   if (tapu) hipLaunchKernelGGL((k_conv_glds<MODE, BM, BN, S, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_conv_glds<MODE, BM, BN, S, false>), grid, dim3(256), 0, s, a);
   return (int)hipGetLastError();
@@ -1249,6 +1268,13 @@ int launch(const ConvArgs& a, hipStream_t s) {
   }
   // K-tile inside one tap: FWD needs Cin % BK == 0; DGRAD/WGRAD tap math is already per-tile/per-column
   const bool tapu = (MODE != FWD) || (a.C % BK == 0);
+  if constexpr (MODE == FWD) {
+    if (g_fwd_rec) {
+      *g_fwd_rec = FwdRec{tapu && a.splits == 1 ? fwd_body_id<IgemmBody<FWD, BM, BN, BK, true>>() : -1, a,
+                          (int)grid.x, (int)grid.y, true};
+      return 0;
+    }
+  }
   if (tapu) hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, true>), grid, dim3(256), 0, s, a, rider);
   else hipLaunchKernelGGL((k_conv_igemm<MODE, BM, BN, BK, false>), grid, dim3(256), 0, s, a, rider);
   return (int)hipGetLastError();
@@ -1384,6 +1410,13 @@ int launch_direct(const ConvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 16 * NR - 1) / (16 * NR), (a.M + 16 * MR - 1) / (16 * MR), 1);
   // ring depth: keep ~16 fragment loads per lane in flight
   constexpr int D = (MR + NR) <= 2 ? 8 : ((MR + NR) <= 4 ? 4 : 2);
+  if constexpr (MODE == FWD) {
+    if (g_fwd_rec) {
+      *g_fwd_rec = FwdRec{NW == 4 ? fwd_body_id<DirectBody<FWD, MR, NR, NW, D>>() : -1, a, (int)grid.x, (int)grid.y,
+                          true};
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((k_conv_direct<MODE, MR, NR, NW, D>), grid, dim3(64 * NW), 0, s, a);
   KML_LAUNCH_CHECK();
 }
@@ -2468,6 +2501,79 @@ int dispatch_pair(int which, const ConvArgs& ad, const ConvArgs& aw, hipStream_t
   return (int)hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------
+// Forward pairs: the two independent convolutions of a downsampling residual block (the strided
+// 3x3 main conv and the strided 1x1 projection, both reading the block input) in ONE launch —
+// the forward twin of k_conv_pair.  On ResNet-34/CIFAR each fills 128-256 of the 256 CUs and
+// costs a ~4-5 us dependent launch; pairing lets them share the chip.  The flat grid takes the
+// XCD-aware order of xcd_blk over both bodies' tiles.
+// ---------------------------------------------------------------------------------
+template <class B1, class B2>
+__global__ __launch_bounds__(256) void k_conv_fwd_pair(ConvArgs a1, ConvArgs a2, int g1x, int g1y, int g2x, int n1,
+                                                       int n2) {
+  static_assert(B1::THREADS == 256 && B2::THREADS == 256, "paired bodies run 256-thread blocks");
+  constexpr int SM = B1::SMEM > B2::SMEM ? B1::SMEM : B2::SMEM;
+  __shared__ __attribute__((aligned(1024))) char smem[SM];
+  const int nwg = n1 + n2, lin = (int)blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, x = lin & 7, k = lin >> 3;
+  int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  Blk b;
+  if (id < n1) {
+    b.gx = g1x;
+    b.x = id % g1x;
+    b.y = id / g1x;
+    b.z = 0;
+    (void)g1y;
+    B1::run(a1, b, smem);
+  } else {
+    id -= n1;
+    b.gx = g2x;
+    b.x = id % g2x;
+    b.y = id / g2x;
+    b.z = 0;
+    B2::run(a2, b, smem);
+  }
+}
+
+using FwGl6432 = GldsBody<FWD, 64, 32, 3, true>;
+using FwIg6432 = IgemmBody<FWD, 64, 32, 32, true>;
+using FwIg3232 = IgemmBody<FWD, 32, 32, 64, true>;
+using FwGl3232 = GldsBody<FWD, 32, 32, 3, true>;
+using FwDi3216 = DirectBody<FWD, 2, 1, 4, 4>;
+// ResNet-34/CIFAR's downsampling blocks: layer2 (3x3 on the LDS-DMA kernel + 1x1 register-staged),
+// layer3 (register-staged + LDS-DMA), layer4 (direct + register-staged)
+#define KML_FWD_PAIR_LIST(X) \
+  X(0, 1, FwGl6432, FwIg6432) \
+  X(2, 3, FwIg3232, FwGl3232) \
+  X(4, 2, FwDi3216, FwIg3232)
+
+template <class B>
+constexpr int fwd_body_id() {
+  if constexpr (std::is_same<B, FwGl6432>::value) return 0;
+  else if constexpr (std::is_same<B, FwIg6432>::value) return 1;
+  else if constexpr (std::is_same<B, FwIg3232>::value) return 2;
+  else if constexpr (std::is_same<B, FwGl3232>::value) return 3;
+  else if constexpr (std::is_same<B, FwDi3216>::value) return 4;
+  else return -1;
+}
+
+int launch_fwd_pair(const FwdRec& r1, const FwdRec& r2, hipStream_t s) {
+#define KML_FWD_PAIR_RUN(I1, I2, B1, B2)                                                                   \
+  if (r1.body == I1 && r2.body == I2) {                                                                     \
+    hipLaunchKernelGGL((k_conv_fwd_pair<B1, B2>), dim3((unsigned)(r1.gx * r1.gy + r2.gx * r2.gy)), dim3(256), 0, s, \
+                       r1.a, r2.a, r1.gx, r1.gy, r2.gx, r1.gx * r1.gy, r2.gx * r2.gy);                        \
+    KML_LAUNCH_CHECK();                                                                                     \
+  }                                                                                                         \
+  if (r1.body == I2 && r2.body == I1) {                                                                     \
+    hipLaunchKernelGGL((k_conv_fwd_pair<B1, B2>), dim3((unsigned)(r1.gx * r1.gy + r2.gx * r2.gy)), dim3(256), 0, s, \
+                       r2.a, r1.a, r2.gx, r2.gy, r1.gx, r2.gx * r2.gy, r1.gx * r1.gy);                        \
+    KML_LAUNCH_CHECK();                                                                                     \
+  }
+  KML_FWD_PAIR_LIST(KML_FWD_PAIR_RUN)
+#undef KML_FWD_PAIR_RUN
+  return -1;
+}
+
 // wT[c][t][k] = w[k][t][c] for up to 16 weights in one launch (kml_weight_transpose_multi).
 // One block per 64(k) x 64(c) tile of one tap: 16-byte loads along c into an LDS tile,
 // 16-byte stores along k out of it (k >= K zero-filled up to Kp).
@@ -2687,6 +2793,34 @@ KML_API int kml_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const floa
   if (a.splits > 1 && (!slab || !counters)) return (int)hipErrorInvalidValue;
   a.slab = slab; a.counters = counters;
   return dispatch<FWD>(a, bm, bn, bk, variant, s);
+}
+
+// Two independent forward convolutions in one launch (k_conv_fwd_pair).  q1 / q2: the 30
+// arguments of kml_conv_fwd (stream excluded) as 64-bit values, in its order.  Returns 0 when
+// launched as a pair, 1 when the two plans are not an instantiated pair (nothing launched: the
+// caller launches them with kml_conv_fwd), or an error code.
+KML_API int kml_conv_fwd_pair(const long long* q1, const long long* q2, hipStream_t s) {
+  FwdRec r[2];
+  const long long* q[2] = {q1, q2};
+  for (int i = 0; i < 2; ++i) {
+    const long long* v = q[i];
+    const int variant = (int)v[22];
+    if (variant != 0 && variant != 1 && variant != 2 && variant != 3) return 1;
+    g_fwd_rec = &r[i];
+    const int rc = kml_conv_fwd((const bf16_t*)v[0], (const bf16_t*)v[1], (bf16_t*)v[2], (const float*)v[3],
+                                (float*)v[4], (int)v[5], (int)v[6], (int)v[7], (int)v[8], (int)v[9], (int)v[10],
+                                (int)v[11], (int)v[12], (int)v[13], (int)v[14], (int)v[15], (int)v[16], (int)v[17],
+                                (int)v[18], (int)v[19], (int)v[20], (int)v[21], variant, (float*)v[23],
+                                (unsigned*)v[24], (float*)v[25], (unsigned*)v[26], (int)v[27], (int)v[28], (int)v[29],
+                                s);
+    g_fwd_rec = nullptr;
+    if (rc) return rc;
+    if (!r[i].set || r[i].body < 0) return 1;
+  }
+  const long long n = (long long)r[0].gx * r[0].gy + (long long)r[1].gx * r[1].gy;
+  if (n <= 0 || n > 0x7fffffffLL) return 1;
+  const int rc = launch_fwd_pair(r[0], r[1], s);
+  return rc < 0 ? 1 : rc;
 }
 
 // Halo forward (variant 4) of a conv whose INPUT is the raw output of another conv: that

@@ -251,27 +251,43 @@ class ConvBNUnit:
         return c, stats, G
 
     @staticmethod
+    def conv_stats(x, conv):
+        """The training conv of :meth:`forward`: (c, stats rows, G).  Per-wave partial statistics
+        from the conv epilogue (plain stores, every row written: no zeroing, no atomics); the BN
+        apply sums them in its prologue."""
+        from ..ops import kernels as K
+        w = shadow_of(conv.weight)
+        kh, kw = conv.kernel_size
+        bias = _conv_bias(conv)
+        K_out = w.shape[0]
+        wu = unrolled_for(conv, x) if bias is None else None   # the 1x1 form has no bias epilogue
+        G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, unroll=wu is not None)
+        stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
+        c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=bias, stats=stats, stats_part=True, wu=wu)
+        return c, stats, G
+
+    @staticmethod
+    def bn_train(c, stats, G, x, bn, relu: bool, res: Optional[torch.Tensor]):
+        """The training BN of :meth:`forward` over the conv output ``c`` of input ``x``."""
+        from ..ops import kernels as K
+        C = c.shape[-1]
+        mean = torch.empty(C, dtype=torch.float32, device=c.device)
+        rstd = torch.empty_like(mean)
+        y = K.bn_apply(c, stats, master_of(bn.weight), master_of(bn.bias), res=res, save_mean=mean, save_rstd=rstd,
+                       run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
+                       momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
+        return y, (x, c, y if relu else None, mean, rstd)
+
+    @staticmethod
     def forward(x, conv, bn, relu: bool, res: Optional[torch.Tensor], training: bool):
         from ..ops import kernels as K
+        if training:
+            c, stats, G = ConvBNUnit.conv_stats(x, conv)
+            return ConvBNUnit.bn_train(c, stats, G, x, bn, relu, res)
         w = shadow_of(conv.weight)
         kh, kw = conv.kernel_size
         gamma, beta = master_of(bn.weight), master_of(bn.bias)
         bias = _conv_bias(conv)
-        if training:
-            # per-wave partial statistics from the conv epilogue (plain stores, every row
-            # written: no zeroing, no atomics); bn_apply sums them in its prologue
-            K_out = w.shape[0]
-            wu = unrolled_for(conv, x) if bias is None else None   # the 1x1 form has no bias epilogue
-            G = K.conv_fwd_stats_rows(x.shape, K_out, kh, kw, conv.stride, conv.padding, unroll=wu is not None)
-            stats = torch.empty(G * 2 * K_out, dtype=torch.float32, device=x.device)
-            c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=bias, stats=stats, stats_part=True, wu=wu)
-            C = c.shape[-1]
-            mean = torch.empty(C, dtype=torch.float32, device=x.device)
-            rstd = torch.empty_like(mean)
-            y = K.bn_apply(c, stats, gamma, beta, res=res, save_mean=mean, save_rstd=rstd,
-                           run_mean=bn.running_mean, run_var=bn.running_var, eps=bn.eps,
-                           momentum=bn.momentum if bn.momentum is not None else 0.1, relu=relu, stats_rows=G)
-            return y, (x, c, y if relu else None, mean, rstd)
         c = K.conv_fwd(x, w, kh, kw, conv.stride, conv.padding, bias=bias)
         y = K.bn_apply(c, None, gamma, beta, res=res, run_mean=bn.running_mean, run_var=bn.running_var,
                        eps=bn.eps, relu=relu, training=False)
@@ -414,13 +430,28 @@ class BlockFn(Function):
         h = x
         short = None
         pending = None
+        pre = {}
+        if _FWD_PAIR and pend_in is None and len(plan) > 2 and plan[0][3] == "main" and plan[1][3] == "short" \
+                and x.is_cuda:
+            # a downsampling block: its first conv and the projection both read x — one launch
+            # (ops.kernels.conv_fwd_pair) when their plans pair; both BN applies follow
+            from ..ops import kernels as K
+            with K.conv_fwd_pair():
+                pre[0] = (ConvBNUnit.conv_rows(x, plan[0][0], group=_FOLD_GROUP) if fold == 0
+                          else ConvBNUnit.conv_stats(x, plan[0][0]))
+                pre[1] = ConvBNUnit.conv_stats(x, plan[1][0])
         for i, (conv, bn, relu, role) in enumerate(plan):
             if role == "short":
-                short, saved[i] = ConvBNUnit.forward(x, conv, bn, relu, None, training)
+                if i in pre:
+                    short, saved[i] = ConvBNUnit.bn_train(*pre[i], x, bn, relu, None)
+                else:
+                    short, saved[i] = ConvBNUnit.forward(x, conv, bn, relu, None, training)
             elif i == fold:
                 if pend_in is not None:
                     c, rows, G = ConvBNUnit.conv_rows_pending(pend_in, h, conv)
                     pend_in = None
+                elif i in pre:
+                    c, rows, G = pre[i]
                 else:
                     c, rows, G = ConvBNUnit.conv_rows(h, conv, group=_FOLD_GROUP)
                 pending = (i, h, c, rows, G, bn)
@@ -436,6 +467,8 @@ class BlockFn(Function):
             elif role == "last":
                 res = short if short is not None else x
                 h, saved[i] = ConvBNUnit.forward(h, conv, bn, relu, res, training)
+            elif i in pre:
+                h, saved[i] = ConvBNUnit.bn_train(*pre[i], h, bn, relu, None)
             else:
                 h, saved[i] = ConvBNUnit.forward(h, conv, bn, relu, None, training)
         ctx.block = block
@@ -510,6 +543,8 @@ class BlockFn(Function):
 
 
 _SHORT_LAST = True
+# downsampling blocks launch their first conv and the projection as one forward pair
+_FWD_PAIR = os.environ.get("KUBEML_FWD_PAIR", "1") != "0"
 
 
 def _short_last(short_saved, sc, conv1) -> bool:

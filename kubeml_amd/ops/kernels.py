@@ -14,6 +14,7 @@ Tensor conventions
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import math
 import os
@@ -395,16 +396,55 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
                      _p(rows), _p(zp), M, K, C, bk, _p(grp), _p(gcnt), tpg, _s())
         return out
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
-        HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
-                 KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg, int(_fold),
-                 int(_g22), _s())
+        _conv_fwd_launch(sig, (_p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
+                               KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg,
+                               int(_fold), int(_g22)))
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
-    HIP.call("kml_conv_fwd", sig, _p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
-             sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt), tpg,
-             int(_fold), int(_g22), _s())
+    _conv_fwd_launch(sig, (_p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
+                           sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt),
+                           tpg, int(_fold), int(_g22)))
     return out
+
+
+_FWD_PAIR = None   # list while a conv_fwd_pair() block records
+FWD_PAIRS_LAUNCHED = [0]   # k_conv_fwd_pair launches so far (tests check the pair path ran)
+
+
+def _conv_fwd_launch(sig, args):
+    if _FWD_PAIR is not None and len(_FWD_PAIR) < 2:
+        _FWD_PAIR.append((sig, args))
+        return
+    HIP.call("kml_conv_fwd", sig, *args, _s())
+
+
+@contextlib.contextmanager
+def conv_fwd_pair():
+    """Launch the (up to) two conv_fwd calls made inside this block as ONE kernel when their plans
+    form an instantiated forward pair (conv_igemm.hip k_conv_fwd_pair: the strided 3x3 and the
+    1x1 projection of a downsampling residual block, which both read the block input); otherwise
+    each launches on its own at the end of the block.  Only the register-staged / LDS-DMA / direct
+    plans record; any other route launches immediately, as always.  The convs must not depend on
+    each other."""
+    global _FWD_PAIR
+    prev, _FWD_PAIR = _FWD_PAIR, []
+    try:
+        yield
+    finally:
+        rec, _FWD_PAIR = _FWD_PAIR, prev
+        rc = 1
+        if len(rec) == 2:
+            import ctypes
+            q = [(ctypes.c_longlong * 30)(*[int(v) for v in a]) for _, a in rec]
+            rc = HIP.fn("kml_conv_fwd_pair", "p p s")(ctypes.addressof(q[0]), ctypes.addressof(q[1]), _s())
+        if rc == 1:
+            for sig, a in rec:
+                HIP.call("kml_conv_fwd", sig, *a, _s())
+        elif rc:
+            raise RuntimeError(f"kml_conv_fwd_pair failed: {rc}")
+        else:
+            FWD_PAIRS_LAUNCHED[0] += 1
 
 
 def conv_fwd_plan(C, M, K, Kd, cfg=None, geom=None):
