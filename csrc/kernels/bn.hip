@@ -21,6 +21,7 @@
 #include "kml_sgd.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -606,20 +607,47 @@ __host__ __device__ constexpr int bn_tslots(int C) { return 8 * bn_tstride(C >> 
 // never waits on more than one memory round trip.  Out-of-range chunks load a clamped
 // (valid) index and skip the store (no branch around a load: straight-line vmcnt).
 // ---------------------------------------------------------------------------------------
+struct BnApArgs {
+  const bf16_t* x;
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  const bf16_t* res;
+  bf16_t* y;
+  float* save_mean;
+  float* save_rstd;
+  float* run_mean;
+  float* run_var;
+  long long M;
+  int C;
+  float eps, momentum;
+  int relu, mode, stats_rows;
+};
+
+// one block (bid of nblk) of the apply; k_bn_apply_v runs it over its grid, k_bn_apply_pair over
+// a shared one
 template <int NT, int V, bool PIPE>
-__global__ __launch_bounds__(NT) void k_bn_apply_v(
-    const bf16_t* __restrict__ x, const float* __restrict__ stats, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
-    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ run_mean,
-    float* __restrict__ run_var, long long M, int C, float eps, float momentum, int relu, int mode,
-    int stats_rows) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];  // scale[TS], shift[TS], (sums[2C], scratch)
+__device__ __forceinline__ void bn_apply_body(const BnApArgs& p, int bid, int nblk, float* sh) {
+  const bf16_t* __restrict__ x = p.x;
+  const float* __restrict__ stats = p.stats;
+  const float* __restrict__ gamma = p.gamma;
+  const float* __restrict__ beta = p.beta;
+  const bf16_t* __restrict__ res = p.res;
+  bf16_t* __restrict__ y = p.y;
+  float* __restrict__ save_mean = p.save_mean;
+  float* __restrict__ save_rstd = p.save_rstd;
+  float* __restrict__ run_mean = p.run_mean;
+  float* __restrict__ run_var = p.run_var;
+  const long long M = p.M;
+  const int C = p.C, relu = p.relu, mode = p.mode, stats_rows = p.stats_rows;
+  const float eps = p.eps, momentum = p.momentum;
+  // sh: scale[TS], shift[TS], (sums[2C], scratch)
   const int TS = bn_tslots(C), TSTR = bn_tstride(C >> 3);
   float* scale = sh;
   float* shift = sh + TS;
   const int n8 = (int)(M * C / 8);
-  const int T = (int)gridDim.x * NT;
-  const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
+  const int T = nblk * NT;
+  const int i0 = bid * NT + (int)threadIdx.x;
   const bool parts = mode == 0 && stats_rows > 0;
   const bool early = parts && C / 2 <= NT;
   EarlyRows er;
@@ -654,7 +682,7 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
     const int tslot = (c & 7) * TSTR + (c >> 3);
     scale[tslot] = g * rstd;
     shift[tslot] = bb - mean * g * rstd;
-    if (mode == 0 && blockIdx.x == 0) {
+    if (mode == 0 && bid == 0) {
       if (save_mean) { save_mean[c] = mean; save_rstd[c] = rstd; }
       if (run_mean) {
         const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
@@ -699,19 +727,19 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
   } else {
     for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
       if (it > 0) {
-  #pragma unroll
+#pragma unroll
         for (int v = 0; v < V; ++v) xv[v] = reinterpret_cast<const uint4*>(x)[min(base + v * T, n8 - 1)];
         if (res) {
-  #pragma unroll
+#pragma unroll
           for (int v = 0; v < V; ++v) rv[v] = reinterpret_cast<const uint4*>(res)[min(base + v * T, n8 - 1)];
         }
       }
-  #pragma unroll
+#pragma unroll
       for (int v = 0; v < V; ++v) {
         float f[8], r[8];
         unpack8(xv[v], f);
         if (res) unpack8(rv[v], r);
-  #pragma unroll
+#pragma unroll
         for (int k = 0; k < 8; ++k) {
           float o = f[k] * sc[k] + sf[k];
           if (res) o += r[k];
@@ -722,7 +750,25 @@ __global__ __launch_bounds__(NT) void k_bn_apply_v(
         if (i < n8) reinterpret_cast<uint4*>(y)[i] = pack8(f);
       }
     }
-  }}
+  }
+}
+
+template <int NT, int V, bool PIPE>
+__global__ __launch_bounds__(NT) void k_bn_apply_v(BnApArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  bn_apply_body<NT, V, PIPE>(p, (int)blockIdx.x, (int)gridDim.x, sh);
+}
+
+// Two independent BN applies in one launch (kml_bn_apply_pair): blocks [0, n1) run the first
+// over a grid of n1, the rest the second over n2 — a downsampling block's main-branch BN and its
+// projection's BN, which follow one paired conv launch (k_conv_fwd_pair).
+template <int NT, int V1, int V2>
+__global__ __launch_bounds__(NT) void k_bn_apply_pair(BnApArgs p1, BnApArgs p2, int n1, int n2) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int b = (int)blockIdx.x;
+  if (b < n1) bn_apply_body<NT, V1, false>(p1, b, n1, sh);
+  else bn_apply_body<NT, V2, false>(p2, b - n1, n2, sh);
+}
 
 template <int NT, int V, bool PIPE>
 __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
@@ -795,7 +841,7 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   if constexpr (PIPE) {   // as k_bn_apply_v
     for (int base = i0; base < n8; base += V * T) {
       const int nb = base + V * T;   // the next batch's chunk v is loaded right after chunk v is stored
-  #pragma unroll
+#pragma unroll
       for (int v = 0; v < V; ++v) {
         float d[8], xf[8];
         unpack8(dv[v], d);
@@ -803,13 +849,13 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
         if (y) {
           float yf[8];
           unpack8(yv[v], yf);
-  #pragma unroll
+#pragma unroll
           for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
         }
         const int i = base + v * T;
         if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
         float o[8];
-  #pragma unroll
+#pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xh = (xf[k] - m8[k]) * r8[k];
           o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
@@ -826,18 +872,18 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   } else {
     for (int base = i0, it = 0; base < n8; base += V * T, ++it) {
       if (it > 0) {
-  #pragma unroll
+#pragma unroll
         for (int v = 0; v < V; ++v) {
           const int i = min(base + v * T, n8 - 1);
           dv[v] = reinterpret_cast<const uint4*>(dy)[i];
           xv[v] = reinterpret_cast<const uint4*>(x)[i];
         }
         if (y) {
-  #pragma unroll
+#pragma unroll
           for (int v = 0; v < V; ++v) yv[v] = reinterpret_cast<const uint4*>(y)[min(base + v * T, n8 - 1)];
         }
       }
-  #pragma unroll
+#pragma unroll
       for (int v = 0; v < V; ++v) {
         float d[8], xf[8];
         unpack8(dv[v], d);
@@ -845,13 +891,13 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
         if (y) {
           float yf[8];
           unpack8(yv[v], yf);
-  #pragma unroll
+#pragma unroll
           for (int k = 0; k < 8; ++k) d[k] = yf[k] > 0.f ? d[k] : 0.f;
         }
         const int i = base + v * T;
         if (dres && i < n8) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
         float o[8];
-  #pragma unroll
+#pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xh = (xf[k] - m8[k]) * r8[k];
           o[k] = a8[k] * (d[k] - b8[k] - xh * g8[k]);
@@ -1255,11 +1301,25 @@ KML_API int kml_bn_fold_rows(int G, int C) {
   return (long long)G * 2 * C * 4 <= FOLD_BYTES ? 0 : (G + FOLD_R - 1) / FOLD_R;
 }
 
+// kml_bn_apply_pair: while g_bn_rec is set, kml_bn_apply records its register-path launch
+struct BnRec {
+  BnApArgs p;
+  int V = 0, grid = 0;
+  size_t shm = 0;
+  bool ok = false;   // single-batch register path, no fold / wide-sum launch: pairable
+};
+static BnRec* g_bn_rec = nullptr;
+
 KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, const float* gamma, const float* beta,
                          const bf16_t* res, bf16_t* y, float* save_mean, float* save_rstd, float* run_mean,
                          float* run_var, long long M, int C, float eps, float momentum, int relu, int mode,
                          float* fold_ws, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (g_bn_rec) {   // recording: only the single-launch register path pairs
+    g_bn_rec->ok = false;
+    if (!reg_ok(M, C) || (mode == 0 && stats_rows > 0 && fold_ws && (long long)stats_rows * 2 * C * 4 > FOLD_BYTES))
+      return 0;
+  }
   if (mode == 0 && stats_rows > 0) stats = maybe_fold(stats, stats_rows, 2 * C, fold_ws, s);
   if (reg_ok(M, C)) {
     const long long n8 = M * C / 8;
@@ -1267,11 +1327,15 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (2 * bn_tslots(C) + (stats_rows > 0 ? (2 * C + 4 * TPB) : 0)) * sizeof(float);
     const bool pipe = n8 > (long long)grid * TPB * V;   // more than one batch per thread
+    const BnApArgs p{x, stats, gamma, beta, res, y, save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum,
+                     relu, mode, stats_rows};
+    if (g_bn_rec) {   // kml_bn_apply_pair: record, launch nothing
+      *g_bn_rec = BnRec{p, V, (int)grid, shm, !pipe && !(stats_rows > 0 && wide_sum(stats_rows, C))};
+      return 0;
+    }
 #define KML_AP_V(VV)                                                                                           \
-  do { if (pipe) hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, true>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, \
-                     res, y, save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows); \
-  else hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, false>), dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, \
-                     save_mean, save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows); } while (0)
+  do { if (pipe) hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, true>), dim3(grid), dim3(TPB), shm, s, p);           \
+  else hipLaunchKernelGGL((k_bn_apply_v<TPB, VV, false>), dim3(grid), dim3(TPB), shm, s, p); } while (0)
     if (V == 1) KML_AP_V(1);
     else if (V == 2) KML_AP_V(2);
     else if (V == 4) KML_AP_V(4);
@@ -1294,6 +1358,40 @@ KML_API int kml_bn_apply(const bf16_t* x, const float* stats, int stats_rows, co
   hipLaunchKernelGGL(k_bn_apply<TPB>, dim3(grid), dim3(TPB), shm, s, x, stats, gamma, beta, res, y, save_mean,
                      save_rstd, run_mean, run_var, M, C, eps, momentum, relu, mode, stats_rows);
   KML_LAUNCH_CHECK();
+}
+
+// Two independent training BN applies (kml_bn_apply's arguments, stream excluded, as 64-bit values
+// with the floats' bit patterns in the low words: q[11] M, q[13] eps, q[14] momentum) in one launch.
+// Returns 0 when launched as a pair, 1 when either is not a single-batch register-path apply
+// (nothing launched: the caller runs them with kml_bn_apply).
+KML_API int kml_bn_apply_pair(const long long* q1, const long long* q2, hipStream_t s) {
+  BnRec r[2];
+  const long long* q[2] = {q1, q2};
+  for (int i = 0; i < 2; ++i) {
+    const long long* v = q[i];
+    float eps, mom;
+    const unsigned e = (unsigned)v[13], m = (unsigned)v[14];
+    memcpy(&eps, &e, 4);
+    memcpy(&mom, &m, 4);
+    g_bn_rec = &r[i];
+    const int rc = kml_bn_apply((const bf16_t*)v[0], (const float*)v[1], (int)v[2], (const float*)v[3],
+                                (const float*)v[4], (const bf16_t*)v[5], (bf16_t*)v[6], (float*)v[7], (float*)v[8],
+                                (float*)v[9], (float*)v[10], v[11], (int)v[12], eps, mom, (int)v[15], (int)v[16],
+                                (float*)v[17], s);
+    g_bn_rec = nullptr;
+    if (rc) return rc;
+    if (!r[i].ok) return 1;
+  }
+  const size_t shm = r[0].shm > r[1].shm ? r[0].shm : r[1].shm;
+#define KML_BNP(A, B)                                                                                          \
+  if (r[0].V == A && r[1].V == B) {                                                                            \
+    hipLaunchKernelGGL((k_bn_apply_pair<TPB, A, B>), dim3((unsigned)(r[0].grid + r[1].grid)), dim3(TPB), shm, s, \
+                       r[0].p, r[1].p, r[0].grid, r[1].grid);                                                  \
+    KML_LAUNCH_CHECK();                                                                                        \
+  }
+  KML_BNP(1, 1) KML_BNP(1, 2) KML_BNP(2, 1) KML_BNP(2, 2)
+#undef KML_BNP
+  return 1;
 }
 
 // number of fp32 workspace floats kml_bn_bwd needs for the deterministic reduce

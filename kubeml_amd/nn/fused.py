@@ -431,6 +431,7 @@ class BlockFn(Function):
         short = None
         pending = None
         pre = {}
+        done = set()   # units of pre whose BN is already applied: (y, saved)
         if _FWD_PAIR and pend_in is None and len(plan) > 2 and plan[0][3] == "main" and plan[1][3] == "short" \
                 and x.is_cuda:
             # a downsampling block: its first conv and the projection both read x — one launch
@@ -440,9 +441,18 @@ class BlockFn(Function):
                 pre[0] = (ConvBNUnit.conv_rows(x, plan[0][0], group=_FOLD_GROUP) if fold == 0
                           else ConvBNUnit.conv_stats(x, plan[0][0]))
                 pre[1] = ConvBNUnit.conv_stats(x, plan[1][0])
+            if fold != 0:   # both BN applies in one launch as well (bn_apply_pair)
+                with K.bn_apply_pair():
+                    pre[0] = ConvBNUnit.bn_train(*pre[0], x, plan[0][1], plan[0][2], None)
+                    pre[1] = ConvBNUnit.bn_train(*pre[1], x, plan[1][1], plan[1][2], None)
+                done = {0, 1}
+            else:
+                done = set()
         for i, (conv, bn, relu, role) in enumerate(plan):
             if role == "short":
-                if i in pre:
+                if i in done:
+                    short, saved[i] = pre[i]
+                elif i in pre:
                     short, saved[i] = ConvBNUnit.bn_train(*pre[i], x, bn, relu, None)
                 else:
                     short, saved[i] = ConvBNUnit.forward(x, conv, bn, relu, None, training)
@@ -467,6 +477,8 @@ class BlockFn(Function):
             elif role == "last":
                 res = short if short is not None else x
                 h, saved[i] = ConvBNUnit.forward(h, conv, bn, relu, res, training)
+            elif i in done:
+                h, saved[i] = pre[i]
             elif i in pre:
                 h, saved[i] = ConvBNUnit.bn_train(*pre[i], h, bn, relu, None)
             else:

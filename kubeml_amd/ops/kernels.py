@@ -1206,11 +1206,48 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
         if res.shape != x.shape:
             raise ValueError("residual shape mismatch")
     ws = _fold_ws(stats_rows, C, x.device) if training and stats_rows > 0 else None
-    HIP.call("kml_bn_apply", "p p i p p p p p p p p l i f f i i p s",
-             _p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
-             _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu),
-             0 if training else 1, _p(ws), _s())
+    args = (_p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
+            _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu), 0 if training else 1, _p(ws))
+    if _BN_PAIR is not None and len(_BN_PAIR) < 2:
+        _BN_PAIR.append(args)
+        return y
+    HIP.call("kml_bn_apply", _BN_SIG, *args, _s())
     return y
+
+
+_BN_SIG = "p p i p p p p p p p p l i f f i i p s"
+_BN_PAIR = None   # list while a bn_apply_pair() block records
+BN_PAIRS_LAUNCHED = [0]
+
+
+@contextlib.contextmanager
+def bn_apply_pair():
+    """Launch the (up to) two bn_apply calls made inside this block as ONE kernel (bn.hip
+    k_bn_apply_pair) when both take the single-batch register path; otherwise each launches on its
+    own at the end of the block.  The applies must not depend on each other."""
+    global _BN_PAIR
+    prev, _BN_PAIR = _BN_PAIR, []
+    try:
+        yield
+    finally:
+        rec, _BN_PAIR = _BN_PAIR, prev
+        rc = 1
+        if len(rec) == 2:
+            import ctypes
+            import struct
+
+            def q(a):
+                v = [int(t) if not isinstance(t, float) else struct.unpack("<I", struct.pack("<f", t))[0] for t in a]
+                return (ctypes.c_longlong * 18)(*v)
+            qs = [q(a) for a in rec]
+            rc = HIP.fn("kml_bn_apply_pair", "p p s")(ctypes.addressof(qs[0]), ctypes.addressof(qs[1]), _s())
+        if rc == 1:
+            for a in rec:
+                HIP.call("kml_bn_apply", _BN_SIG, *a, _s())
+        elif rc:
+            raise RuntimeError(f"kml_bn_apply_pair failed: {rc}")
+        else:
+            BN_PAIRS_LAUNCHED[0] += 1
 
 
 # BN-backward dgamma/dbeta reduction: "fused" (default) = per-block partials, summed in

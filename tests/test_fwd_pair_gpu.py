@@ -67,3 +67,44 @@ def test_unpaired_plans_launch_separately():
     torch.cuda.synchronize()
     assert K_.FWD_PAIRS_LAUNCHED[0] == n0
     assert torch.equal(a, ref) and torch.equal(b, ref)
+
+
+def test_resnet34_paired_downsampling_blocks_match_unpaired():
+    """A ResNet-34 training forward + backward at batch 256 (the shapes the pairs are instantiated
+    for) with the downsampling blocks' conv pairs (layers 2-4) and BN-apply pairs (layers 3-4) against
+    the same step launched one kernel each: logits, loss, every gradient and the paired BNs'
+    running statistics bit-identical."""
+    from kubeml_amd.models.resnet import resnet34
+    from kubeml_amd.nn import cross_entropy, flatten_module
+    from kubeml_amd.nn import fused
+    from kubeml_amd.ops import kernels as K_
+    torch.manual_seed(0)
+    x = torch.randn(256, 32, 32, 8, device=dev).to(torch.bfloat16)
+    y = torch.randint(0, 1000, (256,), device=dev)
+    old = fused._FWD_PAIR
+    res, counts = [], []
+    try:
+        for on in (False, True):
+            fused._FWD_PAIR = on
+            c0 = (K_.FWD_PAIRS_LAUNCHED[0], K_.BN_PAIRS_LAUNCHED[0])
+            torch.manual_seed(3)
+            m = resnet34(1000).to(dev)
+            sp = flatten_module(m)
+            m.train()
+            sp.zero_grad()
+            out = m(x)
+            loss = cross_entropy(out, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            counts.append((K_.FWD_PAIRS_LAUNCHED[0] - c0[0], K_.BN_PAIRS_LAUNCHED[0] - c0[1]))
+            bns = [m.layer2[0].downsample[1], m.layer3[0].bn1, m.layer3[0].downsample[1], m.layer4[0].bn1,
+                   m.layer4[0].downsample[1]]
+            res.append((out.float(), float(loss), sp.grad.clone(),
+                        [torch.cat([b.running_mean, b.running_var]) for b in bns]))
+    finally:
+        fused._FWD_PAIR = old
+    assert counts == [(0, 0), (3, 2)], counts
+    (o0, l0, g0, r0), (o1, l1, g1, r1) = res
+    assert torch.equal(o1, o0) and l1 == l0
+    assert torch.equal(g1, g0)
+    assert all(torch.equal(a, b) for a, b in zip(r0, r1))
