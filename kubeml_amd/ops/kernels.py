@@ -398,13 +398,13 @@ def conv_fwd(x, w, KH, KW, stride, pad, bias=None, stats=None, relu=False, out=N
     if variant == DIRECT:  # bk carries the wave count of the direct kernel
         _conv_fwd_launch(sig, (_p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K,
                                KH, KW, sh, sw, ph, pw, int(relu), bm, bn, bk, 1, DIRECT, 0, 0, _p(grp), _p(gcnt), tpg,
-                               int(_fold), int(_g22)))
+                               int(_fold), int(_g22)), keep=(x, w, out, bias, rows, grp, gcnt))
         return out
     splits = effective_splits(Kd, bk, splits)
     slab, cnt = _splitk_ws(x.device, M, K, bm, bn, splits)
     _conv_fwd_launch(sig, (_p(x), _p(w), _p(out), _p(bias), _p(rows), int(stats_part), B, H, W, C, K, KH, KW,
                            sh, sw, ph, pw, int(relu), bm, bn, bk, splits, variant, _p(slab), _p(cnt), _p(grp), _p(gcnt),
-                           tpg, int(_fold), int(_g22)))
+                           tpg, int(_fold), int(_g22)), keep=(x, w, out, bias, rows, grp, gcnt, slab, cnt))
     return out
 
 
@@ -412,9 +412,12 @@ _FWD_PAIR = None   # list while a conv_fwd_pair() block records
 FWD_PAIRS_LAUNCHED = [0]   # k_conv_fwd_pair launches so far (tests check the pair path ran)
 
 
-def _conv_fwd_launch(sig, args):
+def _conv_fwd_launch(sig, args, keep=()):
+    """keep: every tensor the launch reads or writes.  A recorded launch runs later, so the record
+    holds them: a workspace the caller drops (the group-reduction scratch rows) must not go back to
+    the caching allocator — and to the other conv of the pair — before the kernel is launched."""
     if _FWD_PAIR is not None and len(_FWD_PAIR) < 2:
-        _FWD_PAIR.append((sig, args))
+        _FWD_PAIR.append((sig, args, keep))
         return
     HIP.call("kml_conv_fwd", sig, *args, _s())
 
@@ -436,10 +439,10 @@ def conv_fwd_pair():
         rc = 1
         if len(rec) == 2:
             import ctypes
-            q = [(ctypes.c_longlong * 30)(*[int(v) for v in a]) for _, a in rec]
+            q = [(ctypes.c_longlong * 30)(*[int(v) for v in a]) for _, a, _ in rec]
             rc = HIP.fn("kml_conv_fwd_pair", "p p s")(ctypes.addressof(q[0]), ctypes.addressof(q[1]), _s())
         if rc == 1:
-            for sig, a in rec:
+            for sig, a, _ in rec:
                 HIP.call("kml_conv_fwd", sig, *a, _s())
         elif rc:
             raise RuntimeError(f"kml_conv_fwd_pair failed: {rc}")
@@ -1208,8 +1211,8 @@ def bn_apply(x, stats, gamma, beta, y=None, res=None, save_mean=None, save_rstd=
     ws = _fold_ws(stats_rows, C, x.device) if training and stats_rows > 0 else None
     args = (_p(x), _p(stats), int(stats_rows), _p(gamma), _p(beta), _p(res), _p(y), _p(save_mean), _p(save_rstd),
             _p(run_mean), _p(run_var), M, C, float(eps), float(momentum), int(relu), 0 if training else 1, _p(ws))
-    if _BN_PAIR is not None and len(_BN_PAIR) < 2:
-        _BN_PAIR.append(args)
+    if _BN_PAIR is not None and len(_BN_PAIR) < 2:   # the record holds every operand until the launch
+        _BN_PAIR.append((args, (x, stats, gamma, beta, res, y, save_mean, save_rstd, run_mean, run_var, ws)))
         return y
     HIP.call("kml_bn_apply", _BN_SIG, *args, _s())
     return y
@@ -1239,10 +1242,10 @@ def bn_apply_pair():
             def q(a):
                 v = [int(t) if not isinstance(t, float) else struct.unpack("<I", struct.pack("<f", t))[0] for t in a]
                 return (ctypes.c_longlong * 18)(*v)
-            qs = [q(a) for a in rec]
+            qs = [q(a) for a, _ in rec]
             rc = HIP.fn("kml_bn_apply_pair", "p p s")(ctypes.addressof(qs[0]), ctypes.addressof(qs[1]), _s())
         if rc == 1:
-            for a in rec:
+            for a, _ in rec:
                 HIP.call("kml_bn_apply", _BN_SIG, *a, _s())
         elif rc:
             raise RuntimeError(f"kml_bn_apply_pair failed: {rc}")
