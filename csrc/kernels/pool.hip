@@ -63,44 +63,60 @@ __global__ void k_maxpool_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__
 // relu_out (optional): the pooled forward output of a fused BN -> ReLU -> max-pool; a window
 // whose maximum is not > 0 passes no gradient (its argmax sat at ReLU's zero), so dx is
 // already dz = d(BN output) and the BN backward needs no ReLU mask.
-// One grid row per input image row (b, ih): the output-row window [oh_lo, oh_hi] is computed once
-// per row and every index is 32-bit (the flat 64-bit div / mod chain per element cost more than the
-// memory traffic on ResNet-50's 112x112 stem pool: 164 us for 256 MB).
+// Every thread owns one 16-byte chunk (b, ih, iw, 8 channels) of dx; blocks of RPB whole input rows
+// (a row of R34's 16x16x64 stem map is 128 chunks: one row per block left half the threads idle on
+// 4096 blocks).  Per-row window bounds, 32-bit indices (the flat 64-bit div / mod chain per element
+// cost more than the memory traffic on ResNet-50's 112x112 stem pool: 164 us for 256 MB).
+// MW: at most MW windows per dimension cover an input element ((k + s - 1) / s; 2 for the 3x3/s2
+// and 2x2/s2 pools): the MW x MW candidate windows are unrolled and all their loads issued before
+// any is used (the data-dependent loop waited on each window's loads in turn)
+template <int MW>
 __global__ __launch_bounds__(256) void k_maxpool_bwd(const bf16_t* __restrict__ dy, const unsigned char* __restrict__ idx,
                                                      const bf16_t* __restrict__ relu_out, bf16_t* __restrict__ dx,
-                                                     PoolGeom g) {
+                                                     PoolGeom g, int rpb) {
   const int CH = g.C / 8;
   const int per_row = g.W * CH;
-  for (int row = blockIdx.y; row < g.B * g.H; row += gridDim.y) {
+  const int lr = (int)threadIdx.x / per_row;   // row within the block (rpb > 1: per_row <= 128)
+  const int ustart = rpb > 1 ? (int)threadIdx.x - lr * per_row : (int)threadIdx.x;
+  if (lr >= rpb) return;
+  for (int row = blockIdx.y * rpb + lr; row < g.B * g.H; row += gridDim.y * rpb) {
     const int b = row / g.H, ih = row - b * g.H;
     // outputs whose window contains ih: oh*s - p <= ih <= oh*s - p + k - 1
     const int oh_lo = max(0, (ih + g.p - g.k + g.s) / g.s), oh_hi = min(g.OH - 1, (ih + g.p) / g.s);
-    for (int u = blockIdx.x * 256 + threadIdx.x; u < per_row; u += gridDim.x * 256) {
+    for (int u = blockIdx.x * 256 + ustart; u < per_row; u += gridDim.x * 256) {
       const int iw = u / CH, ch = u - iw * CH;
       const int ow_lo = max(0, (iw + g.p - g.k + g.s) / g.s), ow_hi = min(g.OW - 1, (iw + g.p) / g.s);
+      uint2 pk[MW * MW];
+      uint4 dv[MW * MW], mv[MW * MW];
+      int tap[MW * MW];
+#pragma unroll
+      for (int a = 0; a < MW; ++a)
+#pragma unroll
+        for (int c = 0; c < MW; ++c) {
+          const int oh = oh_lo + a, ow = ow_lo + c, w = a * MW + c;
+          const int r = ih - (oh * g.s - g.p), q = iw - (ow * g.s - g.p);
+          const bool ok = oh <= oh_hi && ow <= ow_hi && r >= 0 && r < g.k && q >= 0 && q < g.k;
+          tap[w] = ok ? r * g.k + q : -1;
+          const long long o = ok ? ((long long)(b * g.OH + oh) * g.OW + ow) * CH + ch : 0;
+          pk[w] = reinterpret_cast<const uint2*>(idx)[o];
+          dv[w] = reinterpret_cast<const uint4*>(dy)[o];
+          if (relu_out) mv[w] = reinterpret_cast<const uint4*>(relu_out)[o];
+        }
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-        const int r = ih - (oh * g.s - g.p);
-        if (r < 0 || r >= g.k) continue;
-        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-          const int q = iw - (ow * g.s - g.p);
-          if (q < 0 || q >= g.k) continue;
-          const long long o = ((long long)(b * g.OH + oh) * g.OW + ow) * CH + ch;
-          const uint2 pk = reinterpret_cast<const uint2*>(idx)[o];
-          float d[8];
-          unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
-          if (relu_out) {
-            float m[8];
-            unpack8(reinterpret_cast<const uint4*>(relu_out)[o], m);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = m[i] > 0.f ? d[i] : 0.f;
-          }
-          const int tap = r * g.k + q;
+      for (int w = 0; w < MW * MW; ++w) {   // window order (oh, ow) ascending, as the loop summed
+        float d[8];
+        unpack8(dv[w], d);
+        if (relu_out) {
+          float m[8];
+          unpack8(mv[w], m);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const unsigned w = i < 4 ? pk.x : pk.y;
-            if ((int)((w >> (8 * (i & 3))) & 0xff) == tap) acc[i] += d[i];
-          }
+          for (int i = 0; i < 8; ++i) d[i] = m[i] > 0.f ? d[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned x = i < 4 ? pk[w].x : pk[w].y;
+          if (tap[w] >= 0 && (int)((x >> (8 * (i & 3))) & 0xff) == tap[w]) acc[i] += d[i];
         }
       }
       reinterpret_cast<uint4*>(dx)[(long long)row * per_row + u] = pack8(acc);
@@ -193,8 +209,14 @@ KML_API int kml_maxpool_bwd(const bf16_t* dy, const unsigned char* idx, const bf
   if (C % 8) return (int)hipErrorInvalidValue;
   PoolGeom g{B, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   const int per_row = W * (C / 8), rows = B * H;
-  const dim3 grid((per_row + 255) / 256, rows < 65535 ? rows : 65535);
-  hipLaunchKernelGGL(k_maxpool_bwd, grid, dim3(256), 0, st, dy, idx, relu_out, dx, g);
+  const int rpb = per_row <= 128 ? 256 / per_row : 1;   // whole rows per 256-thread block
+  const int gy = (rows + rpb - 1) / rpb;
+  const dim3 grid(rpb > 1 ? 1 : (per_row + 255) / 256, gy < 65535 ? gy : 65535);
+  const int mw = (k + s - 1) / s;
+  if (mw <= 1) hipLaunchKernelGGL(k_maxpool_bwd<1>, grid, dim3(256), 0, st, dy, idx, relu_out, dx, g, rpb);
+  else if (mw == 2) hipLaunchKernelGGL(k_maxpool_bwd<2>, grid, dim3(256), 0, st, dy, idx, relu_out, dx, g, rpb);
+  else if (mw == 3) hipLaunchKernelGGL(k_maxpool_bwd<3>, grid, dim3(256), 0, st, dy, idx, relu_out, dx, g, rpb);
+  else return (int)hipErrorInvalidValue;
   KML_LAUNCH_CHECK();
 }
 
