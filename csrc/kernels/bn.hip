@@ -770,18 +770,41 @@ __global__ __launch_bounds__(NT) void k_bn_apply_pair(BnApArgs p1, BnApArgs p2, 
   else bn_apply_body<NT, V2, false>(p2, b - n1, n2, sh);
 }
 
+struct BnbArgs {
+  const bf16_t* dy;
+  const bf16_t* y;
+  const bf16_t* x;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* part;
+  int G;
+  float* dgamma;
+  float* dbeta;
+  bf16_t* dx;
+  bf16_t* dres;
+  long long M;
+  int C, acc;
+};
+
+// one block (bid of nblk) of the backward apply; k_bn_bwd_apply_v runs it over its grid (after
+// its rider blocks split off), k_bn_bwd_apply_pair over a shared one
 template <int NT, int V, bool PIPE>
-__global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ gamma,
-    const float* __restrict__ part, int G, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long long M, int C, int acc, KmlSgdRider rider) {
-  // optimizer-update rider (kml_sgd.h): the last rider.blocks blocks of the grid
-  if ((int)blockIdx.x >= (int)gridDim.x - rider.blocks) {
-    kml_sgd_rider_run(rider, (int)blockIdx.x - ((int)gridDim.x - rider.blocks));
-    return;
-  }
-  extern __shared__ __attribute__((aligned(16))) float sh[];  // red4 scratch [4*NT], ka kb kc mu rs [C]
+__device__ __forceinline__ void bn_bwd_apply_body(const BnbArgs& p, int bid, int nblk, float* sh) {
+  const bf16_t* __restrict__ dy = p.dy;
+  const bf16_t* __restrict__ y = p.y;
+  const bf16_t* __restrict__ x = p.x;
+  const float* __restrict__ mean = p.mean;
+  const float* __restrict__ rstd = p.rstd;
+  const float* __restrict__ gamma = p.gamma;
+  const float* __restrict__ part = p.part;
+  float* __restrict__ dgamma = p.dgamma;
+  float* __restrict__ dbeta = p.dbeta;
+  bf16_t* __restrict__ dx = p.dx;
+  bf16_t* __restrict__ dres = p.dres;
+  const long long M = p.M;
+  const int G = p.G, C = p.C, acc = p.acc;
+  // sh: red4 scratch [4*NT], ka kb kc mu rs [C]
   float4* red4 = reinterpret_cast<float4*>(sh);
   float* ka = sh + 4 * NT;
   float* kb = ka + C;
@@ -790,8 +813,8 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   float* rs = ka + 4 * C;
   const float invM = 1.f / (float)M;
   const int n8 = (int)(M * C / 8);
-  const int T = ((int)gridDim.x - rider.blocks) * NT;
-  const int i0 = (int)blockIdx.x * NT + (int)threadIdx.x;
+  const int T = nblk * NT;
+  const int i0 = bid * NT + (int)threadIdx.x;
   const bool early = C / 2 <= NT;
   EarlyRows er;
   if (early) er.issue(part, G, 2 * C, NT);
@@ -817,7 +840,7 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
   const int TS = bn_tslots(C), TSTR = bn_tstride(C >> 3);
   for (int c = threadIdx.x; c < C; c += NT) {
     const float sb = kb[c], sg = kc[c];
-    if (blockIdx.x == 0) {  // one writer: store (overwrite) or add (accumulate)
+    if (bid == 0) {  // one writer: store (overwrite) or add (accumulate)
       dbeta[c] = acc ? dbeta[c] + sb : sb;
       dgamma[c] = acc ? dgamma[c] + sg : sg;
     }
@@ -906,6 +929,27 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(
       }
     }
   }
+}
+
+template <int NT, int V, bool PIPE>
+__global__ __launch_bounds__(NT) void k_bn_bwd_apply_v(BnbArgs p, KmlSgdRider rider) {
+  // optimizer-update rider (kml_sgd.h): the last rider.blocks blocks of the grid
+  if ((int)blockIdx.x >= (int)gridDim.x - rider.blocks) {
+    kml_sgd_rider_run(rider, (int)blockIdx.x - ((int)gridDim.x - rider.blocks));
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  bn_bwd_apply_body<NT, V, PIPE>(p, (int)blockIdx.x, (int)gridDim.x - rider.blocks, sh);
+}
+
+// Two independent BN backward applies in one launch (kml_bn_bwd_pair): a downsampling block's
+// projection BN and its first BN, both ready once the second conv's backward has run.
+template <int NT, int V1, int V2>
+__global__ __launch_bounds__(NT) void k_bn_bwd_apply_pair(BnbArgs p1, BnbArgs p2, int n1, int n2) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int b = (int)blockIdx.x;
+  if (b < n1) bn_bwd_apply_body<NT, V1, false>(p1, b, n1, sh);
+  else bn_bwd_apply_body<NT, V2, false>(p2, b - n1, n2, sh);
 }
 
 // Fold G partial rows [G][W] into ceil(G / R) rows (fixed order: deterministic), so the
@@ -1247,6 +1291,16 @@ static bool wide_sum(int G, int C) {
   return C <= 1024 && (G + slices - 1) / slices > 16;
 }
 
+// kml_bn_bwd_pair: while g_bnb_rec is set, the single-batch register-path backward apply (no rider
+// armed) records instead of launching; every other launch of the call runs as usual
+struct BnbRec {
+  BnbArgs p;
+  int V = 0, grid = 0;
+  size_t shm = 0;
+  bool set = false;
+};
+static BnbRec* g_bnb_rec = nullptr;
+
 static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean,
                                 const float* rstd, const float* gamma, const float* part, int G, float* dgamma,
                                 float* dbeta, bf16_t* dx, bf16_t* dres, long long M, int C, int acc,
@@ -1256,13 +1310,18 @@ static int launch_bwd_apply_fin(const bf16_t* dy, const bf16_t* y, const bf16_t*
     const int V = pick_v(n8, 4);
     const unsigned grid = v_grid(n8, V);
     const size_t shm = (4 * TPB + 5 * C + 5 * bn_tslots(C)) * sizeof(float);  // + transposed coefficients
-    const KmlSgdRider rider = kml_rider_take();
     const bool pipe = n8 > (long long)grid * TPB * V;   // more than one batch per thread
+    const BnbArgs p{dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc};
+    if (g_bnb_rec && g_kml_rider.blocks == 0 && !pipe) {   // kml_bn_bwd_pair: record, launch nothing
+      *g_bnb_rec = BnbRec{p, V, (int)grid, shm, true};
+      return 0;
+    }
+    const KmlSgdRider rider = kml_rider_take();
 #define KML_BWD_V(VV)                                                                                          \
-  do { if (pipe) hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, true>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, \
-                     mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider);                      \
-  else hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, false>), dim3(grid + rider.blocks), dim3(TPB), shm, s, dy, y, x, mean, \
-                     rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, acc, rider); } while (0)
+  do { if (pipe) hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, true>), dim3(grid + rider.blocks), dim3(TPB), shm, s, p, \
+                     rider);                                                                                    \
+  else hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, false>), dim3(grid + rider.blocks), dim3(TPB), shm, s, p, rider); \
+  } while (0)
     if (V == 1) KML_BWD_V(1);
     else if (V == 2) KML_BWD_V(2);
     else KML_BWD_V(4);
@@ -1452,6 +1511,60 @@ KML_API int kml_bn_bwd_apply_partial(const bf16_t* dy, const bf16_t* y, const bf
   if (C % 8 || C / 8 > TPB || G <= 0) return (int)hipErrorInvalidValue;
   part = maybe_fold(part, G, 2 * C, fold_ws, s);
   return launch_bwd_apply_fin(dy, y, x, mean, rstd, gamma, part, G, dgamma, dbeta, dx, dres, M, C, accumulate, s);
+}
+
+// Two independent training BN backwards with one apply launch.  q[0] selects the call: 0 =
+// kml_bn_bwd (q[1..15] its arguments, stream excluded, as 64-bit values), 1 =
+// kml_bn_bwd_apply_partial (q[1..16]).  Each call runs as usual (its reduction pass included)
+// except that a single-batch register-path apply is recorded; two recorded applies launch as one
+// k_bn_bwd_apply_pair, a lone one on its own.  Returns 0 or an error code.
+static int bnb_call(const long long* q, hipStream_t s) {
+  if (q[0] == 0)
+    return kml_bn_bwd((const bf16_t*)q[1], (const bf16_t*)q[2], (const bf16_t*)q[3], (const float*)q[4],
+                      (const float*)q[5], (const float*)q[6], (float*)q[7], (float*)q[8], (bf16_t*)q[9],
+                      (bf16_t*)q[10], (float*)q[11], (unsigned*)q[12], q[13], (int)q[14], (int)q[15], s);
+  if (q[0] == 1)
+    return kml_bn_bwd_apply_partial((const bf16_t*)q[1], (const bf16_t*)q[2], (const bf16_t*)q[3],
+                                    (const float*)q[4], (const float*)q[5], (const float*)q[6], (const float*)q[7],
+                                    (int)q[8], (float*)q[9], (float*)q[10], (bf16_t*)q[11], (bf16_t*)q[12], q[13],
+                                    (int)q[14], (float*)q[15], (int)q[16], s);
+  return (int)hipErrorInvalidValue;
+}
+
+static int bnb_launch_one(const BnbRec& r, hipStream_t s) {
+#define KML_BWD_ONE(VV) \
+  if (r.V == VV) hipLaunchKernelGGL((k_bn_bwd_apply_v<TPB, VV, false>), dim3(r.grid), dim3(TPB), r.shm, s, r.p, KmlSgdRider{});
+  KML_BWD_ONE(1) else KML_BWD_ONE(2) else KML_BWD_ONE(4) else return (int)hipErrorInvalidValue;
+#undef KML_BWD_ONE
+  KML_LAUNCH_CHECK();
+}
+
+KML_API int kml_bn_bwd_pair(const long long* q1, const long long* q2, hipStream_t s) {
+  BnbRec r[2];
+  const long long* q[2] = {q1, q2};
+  for (int i = 0; i < 2; ++i) {
+    g_bnb_rec = &r[i];
+    const int rc = bnb_call(q[i], s);
+    g_bnb_rec = nullptr;
+    if (rc) return rc;
+  }
+  if (r[0].set && r[1].set) {
+    const size_t shm = r[0].shm > r[1].shm ? r[0].shm : r[1].shm;
+#define KML_BNBP(A, B)                                                                                             \
+    if (r[0].V == A && r[1].V == B) {                                                                              \
+      hipLaunchKernelGGL((k_bn_bwd_apply_pair<TPB, A, B>), dim3((unsigned)(r[0].grid + r[1].grid)), dim3(TPB), shm, s, \
+                         r[0].p, r[1].p, r[0].grid, r[1].grid);                                                    \
+      KML_LAUNCH_CHECK();                                                                                          \
+    }
+    KML_BNBP(1, 1) KML_BNBP(1, 2) KML_BNBP(2, 1) KML_BNBP(2, 2)
+#undef KML_BNBP
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (!r[i].set) continue;
+    const int rc = bnb_launch_one(r[i], s);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 KML_API int kml_relu_fwd(const bf16_t* x, bf16_t* y, long long n, hipStream_t s) {

@@ -301,17 +301,31 @@ class ConvBNUnit:
         skips the reduction pass and never reads y.  ``consumer``: saved state
         (x, c, y, mean, rstd) of the BN that will consume dx — its partial rows are produced
         here, its mask applied to dx, and the partials returned."""
+        dc, dres, wu = ConvBNUnit.bn_backward(dy, saved, conv, bn, want_dres, partial)
+        dx, part_out = ConvBNUnit.conv_backward(dc, saved, conv, need_dx, wu, addend, consumer)
+        return dx, dres, part_out
+
+    @staticmethod
+    def bn_backward(dy, saved, conv, bn, want_dres: bool, partial=None):
+        """The BN half of :meth:`backward`: (dc, dres, the conv's unrolled-form marker)."""
         from ..ops import kernels as K
         x, c, y, mean, rstd = saved
-        kh, kw = conv.kernel_size
         dg, db, acc = grad_out_pair(bn.weight, bn.bias)
         wu = getattr(conv, "_kml_wu", None) if x.is_cuda else None   # set by this step's forward
-        dx, part_out = None, None
-        bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
         dres = torch.empty_like(dy) if want_dres else None
         dc = K.bn_bwd(dy, None if partial is not None else y, c, mean, rstd, master_of(bn.weight),
                       dg, db, dres=dres, partial=partial, accumulate=acc, rider=_take_rider(bn))
         object.__setattr__(conv, "_kml_wu", None)
+        return dc, dres, wu
+
+    @staticmethod
+    def conv_backward(dc, saved, conv, need_dx: bool, wu, addend=None, consumer=None):
+        """The conv half of :meth:`backward`: (dx, consumer partial rows)."""
+        from ..ops import kernels as K
+        x = saved[0]
+        kh, kw = conv.kernel_size
+        dx, part_out = None, None
+        bnf = None if consumer is None else (consumer[2], consumer[1], consumer[3], consumer[4])
         if need_dx:
             # dgrad + wgrad as one grouped launch (falls back to two for unpaired plans)
             w = shadow_of(conv.weight)
@@ -327,13 +341,13 @@ class ConvBNUnit:
                 conv.weight._kml_flat.defer_fold22(conv.weight, dw)
             object.__setattr__(conv, "_kml_wt", None)             # valid for one backward pass
             dx, part_out = r if bnf is not None else (r, None)
-            return dx, dres, part_out
+            return dx, part_out
         _wgrad(x, dc, conv, unroll=wu is not None, rider=_take_rider(conv))
         if need_dx:
             r = K.conv_dgrad(dc, shadow_of(conv.weight), x.shape, kh, kw, conv.stride, conv.padding,
                              addend=addend, bnf=bnf, wu=wu, bnf_mask=True)
             dx, part_out = r if bnf is not None else (r, None)
-        return dx, dres, part_out
+        return dx, part_out
 
 
 def _take_rider(conv):
@@ -518,6 +532,21 @@ class BlockFn(Function):
             is_first = k == 0
             addend = None
             swap = is_first and short and not is_last and _short_last(saved[short[0][0]], short[0][1][0], conv)
+            consumer = saved[main[k - 1][0]] if k > 0 else (prev_saved if need_x else None)
+            if not _BN_FUSE:
+                consumer = None
+            if is_first and not swap and short and not is_last and _BWD_PAIR and dout.is_cuda:
+                # the projection's BN backward and this unit's are independent: one apply launch
+                # (ops.kernels.bn_bwd_pair), then the projection's conv backward (its dgrad is this
+                # unit's dgrad addend), then this unit's
+                from ..ops import kernels as K
+                j, (sc, sb, _, _) = short[0]
+                with K.bn_bwd_pair():
+                    dc_s, _, wu_s = ConvBNUnit.bn_backward(dres, saved[j], sc, sb, False)
+                    dc, _, wu = ConvBNUnit.bn_backward(g, saved[i], conv, bn, False, partial)
+                addend, _ = ConvBNUnit.conv_backward(dc_s, saved[j], sc, need_x, wu_s)
+                g, partial = ConvBNUnit.conv_backward(dc, saved[i], conv, need_x, wu, addend, consumer)
+                continue
             if is_first and not swap:
                 # shortcut gradient joins here: identity -> dres, projection -> its dgrad
                 if short:
@@ -525,9 +554,6 @@ class BlockFn(Function):
                     addend, _, _ = ConvBNUnit.backward(dres, saved[j], sc, sb, False, need_x)
                 else:
                     addend = dres
-            consumer = saved[main[k - 1][0]] if k > 0 else (prev_saved if need_x else None)
-            if not _BN_FUSE:
-                consumer = None
             if swap:
                 # strided projection shortcut on a large map: the main conv's dgrad runs plain and the
                 # shortcut's dgrad takes it as its residual addend plus the consumer-BN epilogue —
@@ -555,8 +581,10 @@ class BlockFn(Function):
 
 
 _SHORT_LAST = True
-# downsampling blocks launch their first conv and the projection as one forward pair
+# downsampling blocks launch their first conv and the projection as one forward pair, and their
+# two BN backward applies as one launch (same switch)
 _FWD_PAIR = os.environ.get("KUBEML_FWD_PAIR", "1") != "0"
+_BWD_PAIR = _FWD_PAIR
 
 
 def _short_last(short_saved, sc, conv1) -> bool:

@@ -1270,12 +1270,17 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
     M = x.numel() // C
     if dx is None:
         dx = torch.empty_like(x)
+    record = _BNB_PAIR is not None and len(_BNB_PAIR) < 2 and rider is None
     if partial is not None:
         part, G = partial
+        fws = _fold_ws(G, C, dy.device)
+        args = (_p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
+                _p(dx), _p(dres), M, C, _p(fws), int(bool(accumulate)))
+        if record:
+            _BNB_PAIR.append(((1,) + args, (dy, y, x, mean, rstd, gamma, part, dgamma, dbeta, dx, dres, fws)))
+            return dx
         with _Riding(rider):
-            HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s",
-                     _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(part), int(G), _p(dgamma), _p(dbeta),
-                     _p(dx), _p(dres), M, C, _p(_fold_ws(G, C, dy.device)), int(bool(accumulate)), _s())
+            HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s", *args, _s())
         return dx
     ws = cnt = None
     if _BN_REDUCE in ("fused", "ticket"):
@@ -1283,11 +1288,43 @@ def bn_bwd(dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx=None, dres=None, parti
         ws = torch.empty(nws, dtype=F32, device=x.device)
         if _BN_REDUCE == "ticket":
             cnt = _COUNTERS.take(x.device, 1)
+    args = (_p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx), _p(dres), _p(ws),
+            _p(cnt), M, C, int(bool(accumulate)))
+    if record:   # the record holds every operand (the reduction workspace included) until the launch
+        _BNB_PAIR.append(((0,) + args, (dy, y, x, mean, rstd, gamma, dgamma, dbeta, dx, dres, ws, cnt)))
+        return dx
     with _Riding(rider):
-        HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s",
-                 _p(dy), _p(y), _p(x), _p(mean), _p(rstd), _p(gamma), _p(dgamma), _p(dbeta), _p(dx),
-                 _p(dres), _p(ws), _p(cnt), M, C, int(bool(accumulate)), _s())
+        HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s", *args, _s())
     return dx
+
+
+_BNB_PAIR = None   # list while a bn_bwd_pair() block records
+BNB_PAIRS = [0]    # bn_bwd_pair() blocks that recorded two calls (tests)
+
+
+@contextlib.contextmanager
+def bn_bwd_pair():
+    """Run the (up to) two bn_bwd calls made inside this block at its end with ONE apply launch
+    (bn.hip kml_bn_bwd_pair / k_bn_bwd_apply_pair) when both applies take the single-batch
+    register path; their reduction passes, if any, run first.  A call with a rider launches at
+    once, as always.  The two BN backwards must not depend on each other."""
+    global _BNB_PAIR
+    import ctypes
+    prev, _BNB_PAIR = _BNB_PAIR, []
+    try:
+        yield
+    finally:
+        rec, _BNB_PAIR = _BNB_PAIR, prev
+        if len(rec) == 2:
+            qs = [(ctypes.c_longlong * 17)(*[int(v) for v in a]) for a, _ in rec]
+            HIP.call("kml_bn_bwd_pair", "p p s", ctypes.addressof(qs[0]), ctypes.addressof(qs[1]), _s())
+            BNB_PAIRS[0] += 1
+        else:
+            for a, _ in rec:
+                if a[0] == 1:
+                    HIP.call("kml_bn_bwd_apply_partial", "p p p p p p p i p p p p l i p i s", *a[1:], _s())
+                else:
+                    HIP.call("kml_bn_bwd", "p p p p p p p p p p p p l i i s", *a[1:], _s())
 
 
 def relu_fwd(x):

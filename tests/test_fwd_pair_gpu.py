@@ -71,7 +71,8 @@ def test_unpaired_plans_launch_separately():
 
 def test_resnet34_paired_downsampling_blocks_match_unpaired():
     """A ResNet-34 training forward + backward at batch 256 (the shapes the pairs are instantiated
-    for) with the downsampling blocks' conv pairs (layers 2-4) and BN-apply pairs (layers 3-4) against
+    for) with the downsampling blocks' conv pairs (layers 2-4), BN-apply pairs (layers 3-4) and
+    BN-backward apply pairs (layers 2-4) against
     the same step launched one kernel each: logits, loss, every gradient and the paired BNs'
     running statistics bit-identical."""
     from kubeml_amd.models.resnet import resnet34
@@ -81,12 +82,12 @@ def test_resnet34_paired_downsampling_blocks_match_unpaired():
     torch.manual_seed(0)
     x = torch.randn(256, 32, 32, 8, device=dev).to(torch.bfloat16)
     y = torch.randint(0, 1000, (256,), device=dev)
-    old = fused._FWD_PAIR
+    old = fused._FWD_PAIR, fused._BWD_PAIR
     res, counts = [], []
     try:
         for on in (False, True):
-            fused._FWD_PAIR = on
-            c0 = (K_.FWD_PAIRS_LAUNCHED[0], K_.BN_PAIRS_LAUNCHED[0])
+            fused._FWD_PAIR = fused._BWD_PAIR = on
+            c0 = (K_.FWD_PAIRS_LAUNCHED[0], K_.BN_PAIRS_LAUNCHED[0], K_.BNB_PAIRS[0])
             torch.manual_seed(3)
             m = resnet34(1000).to(dev)
             sp = flatten_module(m)
@@ -96,14 +97,15 @@ def test_resnet34_paired_downsampling_blocks_match_unpaired():
             loss = cross_entropy(out, y)
             loss.backward()
             torch.cuda.synchronize()
-            counts.append((K_.FWD_PAIRS_LAUNCHED[0] - c0[0], K_.BN_PAIRS_LAUNCHED[0] - c0[1]))
+            counts.append((K_.FWD_PAIRS_LAUNCHED[0] - c0[0], K_.BN_PAIRS_LAUNCHED[0] - c0[1], K_.BNB_PAIRS[0] - c0[2]))
             bns = [m.layer2[0].downsample[1], m.layer3[0].bn1, m.layer3[0].downsample[1], m.layer4[0].bn1,
                    m.layer4[0].downsample[1]]
             res.append((out.float(), float(loss), sp.grad.clone(),
                         [torch.cat([b.running_mean, b.running_var]) for b in bns]))
     finally:
-        fused._FWD_PAIR = old
-    assert counts == [(0, 0), (3, 2)], counts
+        fused._FWD_PAIR, fused._BWD_PAIR = old
+    # backward: the projection BN and the first BN of each downsampling block share one apply launch
+    assert counts == [(0, 0, 0), (3, 2, 3)], counts
     (o0, l0, g0, r0), (o1, l1, g1, r1) = res
     assert torch.equal(o1, o0) and l1 == l0
     assert torch.equal(g1, g0)
