@@ -1235,6 +1235,16 @@ __global__ __launch_bounds__(NT) void k_bn_relu_maxpool3(
       const long long t = base + j * T;
       if (t >= total) continue;
       const int ch = (int)(t % CH);
+      // the chunk's 8 coefficients as two 16-byte reads each, once per output chunk (per-element
+      // 4-byte reads of scale[ch * 8 + i] were 2-way bank conflicts: 38 % in profiles/r6/final/r34_pmc.md)
+      float sc[8], sf[8];
+      {
+        const float4* s4 = reinterpret_cast<const float4*>(scale + ch * 8);
+        const float4* f4 = reinterpret_cast<const float4*>(shift + ch * 8);
+        const float4 a0 = s4[0], a1 = s4[1], b0 = f4[0], b1 = f4[1];
+        sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+        sf[0] = b0.x; sf[1] = b0.y; sf[2] = b0.z; sf[3] = b0.w; sf[4] = b1.x; sf[5] = b1.y; sf[6] = b1.z; sf[7] = b1.w;
+      }
       float best[8];
       int bi[8];
 #pragma unroll
@@ -1246,7 +1256,7 @@ __global__ __launch_bounds__(NT) void k_bn_relu_maxpool3(
         unpack8(v[j][tap], f);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float o = bf2f(f2bf(fmaxf(f[i] * scale[ch * 8 + i] + shift[ch * 8 + i], 0.f)));
+          const float o = bf2f(f2bf(fmaxf(f[i] * sc[i] + sf[i], 0.f)));
           if (o > best[i] || (o != o)) { best[i] = o; bi[i] = tap; }
         }
       }
