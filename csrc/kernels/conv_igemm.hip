@@ -1497,6 +1497,11 @@ struct HaloBody {
   static constexpr int SMEM_MAIN = SMEM_PATCH + (WLDS ? SMEM_W : 0) + SMEM_BN;
   static constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __device__ __forceinline__ static int swz(int pix) {
+    // 4x4 maps at pitch 8 (pixel = 8 y + x inside an image of 48 patch pixels): 2x + 8y spreads
+    // every read group over 16 distinct chunks (tools/lds_banks.py model: 1.33 -> 1.0 cycles per
+    // ds_read_b128; measured 14 % conflicts in profiles/r6/final/r34_pmc.md); pixel * 13 for
+    // the pitch-6 layouts
+    if constexpr (HW == 4 && PITCH == 8) return (2 * (pix & 7) + (pix & 8)) & SWZ;
     const int h = (HW == 8) ? (C == 64 ? pix : pix * 9) : pix * 13;
     return h & SWZ;
   }
