@@ -86,3 +86,29 @@ def test_implicit_gemm_operand_rows_conflict_free():
         for ks in range(bk // 32):
             addrs = [(lane & 15) * row + 64 * ks + 16 * (lane >> 4) for lane in range(64)]
             assert cycles(addrs, 16, G128) == 1, (bk, pad, ks)
+
+
+def test_halo_4x4_patch_reads_conflict_free():
+    """conv_igemm.hip HaloBody::swz on 4x4 maps at pitch 8 (ResNet-34 layer2's 3x3 convs, C = 128,
+    4 images per block): every A-fragment read of the main loop (ds_read_b128 lane groups, all taps,
+    K-steps and wave rows) hits 16 distinct 16-byte chunks."""
+    src = _src("conv_igemm.hip")
+    m = re.search(r"if constexpr \(HW == 4 && PITCH == 8\) return \(2 \* \(pix & 7\) \+ \(pix & 8\)\) & SWZ;", src)
+    assert m, "the 4x4 halo swizzle changed shape: update this test"
+    HW, C, IMG = 4, 128, 4
+    HP, CH, PITCH = HW + 2, C // 8, 8
+    IMGPIX, WM = HP * PITCH, IMG * HW * HW // 2
+    h = lambda p: (2 * (p & 7) + (p & 8)) & 15
+    for wm in range(2):
+        for i in range(WM // 16):
+            for ks in range(9 * C // 32):
+                tap = ks // (C // 32)
+                toff = (tap // 3) * PITCH + tap % 3
+                addrs = []
+                for lane in range(64):
+                    r = wm * WM + i * 16 + (lane & 15)
+                    im, p = divmod(r, HW * HW)
+                    pix = im * IMGPIX + (p // HW) * PITCH + (p % HW) + toff
+                    chunk = (ks % (C // 32)) * 4 + (lane >> 4)
+                    addrs.append((pix * CH + (chunk ^ h(pix))) * 16)
+                assert cycles(addrs, 16, G128) == 1, (wm, i, ks)
