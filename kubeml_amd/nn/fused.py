@@ -460,8 +460,6 @@ class BlockFn(Function):
                     pre[0] = ConvBNUnit.bn_train(*pre[0], x, plan[0][1], plan[0][2], None)
                     pre[1] = ConvBNUnit.bn_train(*pre[1], x, plan[1][1], plan[1][2], None)
                 done = {0, 1}
-            else:
-                done = set()
         for i, (conv, bn, relu, role) in enumerate(plan):
             if role == "short":
                 if i in done:
